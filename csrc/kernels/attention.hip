@@ -1,0 +1,374 @@
+// Paged attention on MFMA for gfx950: decode (split-K "flash-decoding", K5) and
+// varlen causal prefill with prefix / chunked-prefill support (K4).  SURVEY.md §2.9.
+//
+// Both kernels use v_mfma_f32_16x16x32_bf16 and need NO LDS transposes: the paged cache
+// layouts (rope_cache.hip) put every MFMA operand in lane-contiguous 8/16-byte runs.
+//
+// Fragment maps (16x16x32 bf16, cdna_hip_programming.md §3):
+//   A: lane l holds A[row = l&15][k = 8*(l>>4) + j]   j = 0..7
+//   B: lane l holds B[k = 8*(l>>4) + j][col = l&15]
+//   C: lane l reg i  = C[row = 4*(l>>4) + i][col = l&15]
+//
+// Scores are computed transposed, S^T = K * Q^T (keys on MFMA rows, queries on lanes), so
+// each lane owns one query column: the softmax row statistics stay lane-local up to a
+// 4-lane-group xor-shuffle.  The output is accumulated transposed too, O^T = V^T * P^T,
+// with the 32 keys of two pages assigned to the K slots in the permuted order
+//   k-slot (g, j) = page (j >> 2), key 4g + (j & 3)
+// which is exactly the order the S^T accumulators already sit in, so P feeds the second
+// MFMA from registers with no lane movement (the "accumulator as next operand" idiom).
+#include "common.h"
+
+#ifndef OME_NEG_INF
+#define OME_NEG_INF (-__builtin_inff())
+#endif
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 cat44(bf16x4 a, bf16x4 b) {
+  bf16x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+// ------------------------------------------------------------------------------------------
+// Decode: one workgroup = (partition, kv head, sequence); 4 waves split the partition's
+// 32-key tiles round-robin, each with its own online-softmax state, merged through LDS.
+// The G = Hq/Hkv query heads of the kv head share every K/V byte loaded (GQA-aware).
+// ------------------------------------------------------------------------------------------
+template <int D, int P>
+__global__ __launch_bounds__(256) void paged_decode_kernel(
+    const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ seq_lens, bf16* __restrict__ out, int64_t out_stride, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2, int window) {
+  static_assert(P == 16, "decode kernel assumes 16-token pages");
+  constexpr int NB = D / 16;  // 16-dim output blocks
+  constexpr int KS = D / 32;  // 32-dim k-steps for QK
+  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int seq_len = seq_lens[b];
+  const int p_start = part * part_size;
+  if (p_start >= seq_len) return;
+  const int p_end = min(seq_len, p_start + part_size);
+  const int G = Hq / Hkv;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = lane & 15, g = lane >> 4;
+  const int lo = window > 0 ? max(0, seq_len - window) : 0;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sm_m = smem;              // [4][16]
+  float* sm_l = smem + 64;         // [4][16]
+  float* sm_o = smem + 128;        // [4][16][D]
+
+  // Q^T fragments (B operand): head n, dims 32ks + 8g .. +7
+  bf16x8 qf[KS];
+  {
+    const bf16* qh = q + (int64_t)b * q_stride + (int64_t)(kvh * G + n) * D;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (n < G) qf[ks] = ld8(qh + 32 * ks + 8 * g);
+      else qf[ks] = bf16x8{};
+    }
+  }
+  float m_i = OME_NEG_INF, l_i = 0.f;
+  f32x4 o[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) o[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int* bt = block_tables + (int64_t)b * bt_stride;
+  const int64_t kpage = (int64_t)Hkv * P * D;  // elements per page (all heads)
+  for (int kb = p_start + wave * 32; kb < p_end; kb += 128) {
+    if (kb + 32 <= lo) continue;
+    const int pA = bt[kb / P];
+    const int pB = (kb + P < seq_len) ? bt[kb / P + 1] : pA;
+    const bf16* kA = k_cache + pA * kpage + (int64_t)kvh * P * D;
+    const bf16* kB = k_cache + pB * kpage + (int64_t)kvh * P * D;
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 a0 = ld8(kA + n * D + 32 * ks + 8 * g);
+      bf16x8 a1 = ld8(kB + n * D + 32 * ks + 8 * g);
+      s0 = mfma16(a0, qf[ks], s0);
+      s1 = mfma16(a1, qf[ks], s1);
+    }
+    float mt = OME_NEG_INF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k0 = kb + 4 * g + i, k1 = k0 + 16;
+      s0[i] = (k0 < p_end && k0 >= lo) ? s0[i] * scale_log2 : OME_NEG_INF;
+      s1[i] = (k1 < p_end && k1 >= lo) ? s1[i] * scale_log2 : OME_NEG_INF;
+      mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 16));
+    mt = fmaxf(mt, __shfl_xor(mt, 32));
+    const float m_new = fmaxf(m_i, mt);
+    const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
+    const float alpha = fast_exp2(m_i - m_use);
+    bf16x8 pb;
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p0 = fast_exp2(s0[i] - m_use), p1 = fast_exp2(s1[i] - m_use);
+      pb[i] = (bf16)p0;
+      pb[4 + i] = (bf16)p1;
+      rs += p0 + p1;
+    }
+    rs += __shfl_xor(rs, 16);
+    rs += __shfl_xor(rs, 32);
+    l_i = l_i * alpha + rs;
+    m_i = m_new;
+    const bf16* vA = v_cache + pA * kpage + (int64_t)kvh * D * P;
+    const bf16* vB = v_cache + pB * kpage + (int64_t)kvh * D * P;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int dim = 16 * nb + n;
+      bf16x8 a = cat44(ld4(vA + dim * P + 4 * g), ld4(vB + dim * P + 4 * g));
+      o[nb] = o[nb] * alpha;
+      o[nb] = mfma16(a, pb, o[nb]);
+    }
+  }
+  // ---- merge the 4 waves' states ----
+  if (g == 0) {
+    sm_m[wave * 16 + n] = m_i;
+    sm_l[wave * 16 + n] = l_i;
+  }
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm_o[(wave * 16 + n) * D + 16 * nb + 4 * g + i] = o[nb][i];
+  __syncthreads();
+  const int nparts = (seq_len + part_size - 1) / part_size;
+  for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+    const int h = idx / D, d = idx % D;
+    float M = OME_NEG_INF;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w * 16 + h]);
+    const float Mu = (M == OME_NEG_INF) ? 0.f : M;
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = fast_exp2(sm_m[w * 16 + h] - Mu);
+      L += sm_l[w * 16 + h] * f;
+      acc += sm_o[(w * 16 + h) * D + d] * f;
+    }
+    const int head = kvh * G + h;
+    const float res = L > 0.f ? acc / L : 0.f;
+    if (nparts == 1) {
+      out[(int64_t)b * out_stride + (int64_t)head * D + d] = (bf16)res;
+    } else {
+      const int64_t pidx = ((int64_t)b * Hq + head) * max_parts + part;
+      part_o[pidx * D + d] = res;
+      if (d == 0) {
+        part_ml[pidx * 2 + 0] = M;
+        part_ml[pidx * 2 + 1] = L;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const int* __restrict__ seq_lens,
+                                                                 const float* __restrict__ part_o,
+                                                                 const float* __restrict__ part_ml,
+                                                                 bf16* __restrict__ out, int64_t out_stride, int Hq,
+                                                                 int part_size, int max_parts) {
+  const int b = blockIdx.y, head = blockIdx.x, d = threadIdx.x;
+  const int seq_len = seq_lens[b];
+  const int nparts = (seq_len + part_size - 1) / part_size;
+  if (nparts <= 1) return;
+  const int64_t base = ((int64_t)b * Hq + head) * max_parts;
+  float M = OME_NEG_INF;
+  for (int p = 0; p < nparts; ++p) M = fmaxf(M, part_ml[(base + p) * 2]);
+  const float Mu = (M == OME_NEG_INF) ? 0.f : M;
+  float L = 0.f, acc = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    const float w = part_ml[(base + p) * 2 + 1] * fast_exp2(part_ml[(base + p) * 2] - Mu);
+    L += w;
+    acc += w * part_o[(base + p) * D + d];
+  }
+  out[(int64_t)b * out_stride + (int64_t)head * D + d] = (bf16)(L > 0.f ? acc / L : 0.f);
+}
+
+OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                             const int* block_tables, int bt_stride, const int* seq_lens, void* out,
+                             int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
+                             int part_size, int max_parts, float scale, int window, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (D != 128 || P != 16) return -2;
+  if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
+  if (part_size % 128 != 0 || max_parts <= 0) return -4;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
+  dim3 grid(max_parts, Hkv, B);
+  paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(
+      (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, seq_lens,
+      (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window);
+  OME_CHECK_LAUNCH();
+  if (max_parts > 1) {
+    paged_decode_reduce_kernel<128><<<dim3(Hq, B), 128, 0, stream>>>(seq_lens, (const float*)part_o,
+                                                                      (const float*)part_ml, (bf16*)out,
+                                                                      out_stride, Hq, part_size, max_parts);
+    OME_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Prefill: one workgroup = (work item, kv head).  A work item is 32 consecutive query rows of
+// one sequence.  Each wave takes one query head of the kv group (wave w: heads w, w+8, ...),
+// so the G waves of the workgroup stream the same K/V tiles (L1/L2 reuse across GQA heads).
+// Queries at local row r sit at absolute position (kv_len - q_len + r): this covers fresh
+// prompts (kv_len == q_len), chunked prefill and prefix-cache hits uniformly.
+// ------------------------------------------------------------------------------------------
+template <int D, int P>
+__global__ __launch_bounds__(512) void paged_prefill_kernel(
+    const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
+    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window) {
+  static_assert(P == 16, "prefill kernel assumes 16-token pages");
+  constexpr int NB = D / 16, KS = D / 32;
+  const int2 it = items[blockIdx.x];
+  const int s = it.x, r0 = it.y;
+  const int kvh = blockIdx.y;
+  const int q0 = cu_q[s];
+  const int q_len = cu_q[s + 1] - q0;
+  const int kv_len = kv_lens[s];
+  const int prefix = kv_len - q_len;
+  const int G = Hq / Hkv;
+  const int nwaves = blockDim.x >> 6;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = lane & 15, g = lane >> 4;
+  const int r_hi = min(r0 + 32, q_len);
+  const int kv_end = min(kv_len, prefix + r_hi);
+  int kv_lo = 0;
+  if (window > 0) kv_lo = max(0, prefix + r0 - window + 1) & ~31;
+  const int* bt = block_tables + (int64_t)s * bt_stride;
+  const int64_t kpage = (int64_t)Hkv * P * D;
+
+  for (int hl = wave; hl < G; hl += nwaves) {
+    const int head = kvh * G + hl;
+    bf16x8 qf[2][KS];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int r = r0 + 16 * rb + n;
+      const bf16* qr = q + (int64_t)(q0 + r) * q_stride + (int64_t)head * D;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) qf[rb][ks] = (r < q_len) ? ld8(qr + 32 * ks + 8 * g) : bf16x8{};
+    }
+    float m_i[2] = {OME_NEG_INF, OME_NEG_INF}, l_i[2] = {0.f, 0.f};
+    f32x4 o[2][NB];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) o[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kb = kv_lo; kb < kv_end; kb += 32) {
+      const int pA = bt[kb / P];
+      const int pB = (kb + P < kv_len) ? bt[kb / P + 1] : pA;
+      const bf16* kA = k_cache + pA * kpage + (int64_t)kvh * P * D;
+      const bf16* kB = k_cache + pB * kpage + (int64_t)kvh * P * D;
+      f32x4 sc[2][2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) sc[rb][0] = sc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 a0 = ld8(kA + n * D + 32 * ks + 8 * g);
+        bf16x8 a1 = ld8(kB + n * D + 32 * ks + 8 * g);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          sc[rb][0] = mfma16(a0, qf[rb][ks], sc[rb][0]);
+          sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
+        }
+      }
+      const bool need_mask = (kb + 32 > prefix + r0 + 1) || (kb + 32 > kv_len) || (window > 0);
+      bf16x8 pb[2];
+      float alpha[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int qpos = prefix + r0 + 16 * rb + n;
+        float mt = OME_NEG_INF;
+#pragma unroll
+        for (int X = 0; X < 2; ++X)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v = sc[rb][X][i] * scale_log2;
+            if (need_mask) {
+              const int key = kb + 16 * X + 4 * g + i;
+              const bool ok = key <= qpos && key < kv_len && (window <= 0 || key > qpos - window);
+              v = ok ? v : OME_NEG_INF;
+            }
+            sc[rb][X][i] = v;
+            mt = fmaxf(mt, v);
+          }
+        mt = fmaxf(mt, __shfl_xor(mt, 16));
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float m_new = fmaxf(m_i[rb], mt);
+        const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
+        alpha[rb] = fast_exp2(m_i[rb] - m_use);
+        float rs = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p0 = fast_exp2(sc[rb][0][i] - m_use), p1 = fast_exp2(sc[rb][1][i] - m_use);
+          pb[rb][i] = (bf16)p0;
+          pb[rb][4 + i] = (bf16)p1;
+          rs += p0 + p1;
+        }
+        rs += __shfl_xor(rs, 16);
+        rs += __shfl_xor(rs, 32);
+        l_i[rb] = l_i[rb] * alpha[rb] + rs;
+        m_i[rb] = m_new;
+      }
+      const bf16* vA = v_cache + pA * kpage + (int64_t)kvh * D * P;
+      const bf16* vB = v_cache + pB * kpage + (int64_t)kvh * D * P;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int dim = 16 * nb + n;
+        bf16x8 a = cat44(ld4(vA + dim * P + 4 * g), ld4(vB + dim * P + 4 * g));
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          o[rb][nb] = o[rb][nb] * alpha[rb];
+          o[rb][nb] = mfma16(a, pb[rb], o[rb][nb]);
+        }
+      }
+    }
+    // ---- epilogue: normalise, store O[row][dims 16nb+4g .. +3] as bf16x4 ----
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int r = r0 + 16 * rb + n;
+      if (r < q_len) {
+        const float inv = l_i[rb] > 0.f ? 1.f / l_i[rb] : 0.f;
+        bf16* orow = out + (int64_t)(q0 + r) * out_stride + (int64_t)head * D;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          bf16x4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = (bf16)(o[rb][nb][i] * inv);
+          *reinterpret_cast<bf16x4*>(orow + 16 * nb + 4 * g) = v;
+        }
+      }
+    }
+  }
+}
+
+OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                              const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
+                              const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
+                              int P, float scale, int window, hipStream_t stream) {
+  if (n_items <= 0) return 0;
+  if (D != 128 || P != 16) return -2;
+  if (Hq % Hkv != 0) return -3;
+  const int G = Hq / Hkv;
+  const int nw = G < 8 ? G : 8;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(n_items, Hkv);
+  paged_prefill_kernel<128, 16><<<grid, 64 * nw, 0, stream>>>(
+      (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
+      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window);
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,110 @@
+// Element-wise / gather kernels: SiLU-and-mul (K9), GELU-tanh-and-mul, vocab-parallel
+// embedding gather (K13), residual add, and embedding pooling + L2 normalisation (K14).
+// All memory-bound: 16-byte bf16x8 vectors per lane, grid-stride loops capped at
+// 256 CUs x 8 blocks (Guideline 11).
+#include "common.h"
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+template <int ACT>
+__global__ __launch_bounds__(256) void act_and_mul_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
+                                                          int64_t rows, int I) {
+  const int nv = I >> 3;
+  const int64_t total = rows * nv;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nv;
+    const int c = (int)(i % nv);
+    const bf16* xr = x + r * 2 * I;
+    bf16x8 g = ld8(xr + c * 8), u = ld8(xr + I + c * 8), o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gf = (float)g[j];
+      const float a = ACT == 0 ? silu(gf) : gelu_tanh(gf);
+      o[j] = (bf16)(a * (float)u[j]);
+    }
+    st8(out + r * I + c * 8, o);
+  }
+}
+
+static inline int grid_for(int64_t work, int nt) {
+  int64_t g = (work + nt - 1) / nt;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+OME_API int ome_act_and_mul(const void* x, void* out, int64_t rows, int I, int act, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (I % 8) return -2;
+  const int g = grid_for(rows * (I / 8), 256);
+  if (act == 0)
+    act_and_mul_kernel<0><<<g, 256, 0, stream>>>((const bf16*)x, (bf16*)out, rows, I);
+  else
+    act_and_mul_kernel<1><<<g, 256, 0, stream>>>((const bf16*)x, (bf16*)out, rows, I);
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// out[t] = table[ids[t] - vocab_start] if the id falls in this rank's shard, else 0.
+__global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ ids, const bf16* __restrict__ table,
+                                                        bf16* __restrict__ out, int T, int H, int vocab_start,
+                                                        int vocab_end) {
+  const int nv = H >> 3;
+  for (int t = blockIdx.x; t < T; t += gridDim.x) {
+    const int id = ids[t];
+    const bool own = id >= vocab_start && id < vocab_end;
+    const bf16* src = table + (int64_t)(own ? id - vocab_start : 0) * H;
+    for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+      bf16x8 v = {};
+      if (own) v = ld8(src + c * 8);
+      st8(out + (int64_t)t * H + c * 8, v);
+    }
+  }
+}
+
+OME_API int ome_embedding(const int* ids, const void* table, void* out, int T, int H, int vocab_start,
+                          int vocab_end, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 8) return -2;
+  const int g = T < 4096 ? T : 4096;
+  embedding_kernel<<<g, 256, 0, stream>>>(ids, (const bf16*)table, (bf16*)out, T, H, vocab_start, vocab_end);
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// Pooling for embedding models (--is-embedding): last-token or mean pooling over each sequence
+// followed by optional L2 normalisation. hidden [T, H] bf16, cu_lens [S+1] -> out [S, H] f32.
+__global__ __launch_bounds__(256) void pool_kernel(const bf16* __restrict__ hidden, const int* __restrict__ cu,
+                                                   float* __restrict__ out, int H, int mode, int normalize) {
+  __shared__ float red[4];
+  const int s = blockIdx.x;
+  const int b = cu[s], e = cu[s + 1];
+  float ss = 0.f;
+  for (int d = threadIdx.x; d < H; d += 256) {
+    float v = 0.f;
+    if (mode == 0) {
+      v = (float)hidden[(int64_t)(e - 1) * H + d];
+    } else {
+      for (int t = b; t < e; ++t) v += (float)hidden[(int64_t)t * H + d];
+      v /= (float)(e - b > 0 ? e - b : 1);
+    }
+    out[(int64_t)s * H + d] = v;
+    ss += v * v;
+  }
+  if (!normalize) return;
+  ss = block_sum<256>(ss, red);
+  const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+  for (int d = threadIdx.x; d < H; d += 256) out[(int64_t)s * H + d] *= inv;
+}
+
+OME_API int ome_pool(const void* hidden, const int* cu_lens, void* out, int S, int H, int mode, int normalize,
+                     hipStream_t stream) {
+  if (S <= 0) return 0;
+  pool_kernel<<<S, 256, 0, stream>>>((const bf16*)hidden, cu_lens, (float*)out, H, mode, normalize);
+  OME_CHECK_LAUNCH();
+  return 0;
+}

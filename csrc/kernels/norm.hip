@@ -1,0 +1,125 @@
+// RMSNorm and fused residual-add + RMSNorm (kernel K1 of SURVEY.md §2.9).
+//
+// One workgroup per token row; each lane holds its slice of the row in registers as
+// 16-byte bf16x8 vectors (vectorised per Guideline 13), so the row is read once and
+// written once: the op is purely HBM-bound.
+#include "common.h"
+
+template <int NT, int CHUNKS>
+__global__ __launch_bounds__(NT) void rmsnorm_kernel(const bf16* __restrict__ x, int64_t x_stride,
+                                                     const bf16* __restrict__ w, bf16* __restrict__ out,
+                                                     int64_t out_stride, int H, float eps) {
+  __shared__ float red[NT / 64];
+  const int row = blockIdx.x;
+  const bf16* xr = x + row * x_stride;
+  bf16* orow = out + row * out_stride;
+  const int nvec = H >> 3;
+  bf16x8 v[CHUNKS];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) {
+      v[c] = ld8(xr + i * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float f = (float)v[c][j];
+        ss += f * f;
+      }
+    }
+  }
+  ss = block_sum<NT>(ss, red);
+  const float rs = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) {
+      bf16x8 wv = ld8(w + i * 8), o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)v[c][j] * rs * (float)wv[j]);
+      st8(orow + i * 8, o);
+    }
+  }
+}
+
+// residual <- x + residual ; x <- rmsnorm(residual) * w      (in place, vLLM/SGLang semantics)
+template <int NT, int CHUNKS>
+__global__ __launch_bounds__(NT) void fused_add_rmsnorm_kernel(bf16* __restrict__ x, int64_t x_stride,
+                                                               bf16* __restrict__ res, int64_t res_stride,
+                                                               const bf16* __restrict__ w, int H,
+                                                               float eps) {
+  __shared__ float red[NT / 64];
+  const int row = blockIdx.x;
+  bf16* xr = x + row * x_stride;
+  bf16* rr = res + row * res_stride;
+  const int nvec = H >> 3;
+  bf16x8 v[CHUNKS];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) {
+      bf16x8 a = ld8(xr + i * 8), b = ld8(rr + i * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // round the sum to bf16 first: the residual stream is stored in bf16
+        bf16 s = (bf16)((float)a[j] + (float)b[j]);
+        v[c][j] = s;
+        float f = (float)s;
+        ss += f * f;
+      }
+      st8(rr + i * 8, v[c]);
+    }
+  }
+  ss = block_sum<NT>(ss, red);
+  const float rs = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) {
+      bf16x8 wv = ld8(w + i * 8), o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)v[c][j] * rs * (float)wv[j]);
+      st8(xr + i * 8, o);
+    }
+  }
+}
+
+#define DISPATCH_CHUNKS(H, NT, ...)                         \
+  do {                                                      \
+    const int _c = ((H) / 8 + (NT)-1) / (NT);               \
+    if (_c <= 1) { constexpr int CH = 1; __VA_ARGS__; }     \
+    else if (_c <= 2) { constexpr int CH = 2; __VA_ARGS__; } \
+    else if (_c <= 4) { constexpr int CH = 4; __VA_ARGS__; } \
+    else if (_c <= 8) { constexpr int CH = 8; __VA_ARGS__; } \
+    else return -1;                                         \
+  } while (0)
+
+OME_API int ome_rmsnorm(const void* x, int64_t x_stride, const void* w, void* out, int64_t out_stride,
+                        int rows, int H, float eps, hipStream_t stream) {
+  if (H % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -2;
+  // Small batches (decode) use 128-thread blocks to keep more lanes' loads in flight per CU.
+  if (rows < 512) {
+    DISPATCH_CHUNKS(H, 128, (rmsnorm_kernel<128, CH><<<rows, 128, 0, stream>>>(
+                                (const bf16*)x, x_stride, (const bf16*)w, (bf16*)out, out_stride, H, eps)));
+  } else {
+    DISPATCH_CHUNKS(H, 256, (rmsnorm_kernel<256, CH><<<rows, 256, 0, stream>>>(
+                                (const bf16*)x, x_stride, (const bf16*)w, (bf16*)out, out_stride, H, eps)));
+  }
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+OME_API int ome_fused_add_rmsnorm(void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w,
+                                  int rows, int H, float eps, hipStream_t stream) {
+  if (H % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -2;
+  if (rows < 512) {
+    DISPATCH_CHUNKS(H, 128, (fused_add_rmsnorm_kernel<128, CH><<<rows, 128, 0, stream>>>(
+                                (bf16*)x, x_stride, (bf16*)res, res_stride, (const bf16*)w, H, eps)));
+  } else {
+    DISPATCH_CHUNKS(H, 256, (fused_add_rmsnorm_kernel<256, CH><<<rows, 256, 0, stream>>>(
+                                (bf16*)x, x_stride, (bf16*)res, res_stride, (const bf16*)w, H, eps)));
+  }
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,154 @@
+// Fused "QKV split -> RoPE -> paged KV-cache write" (kernels K2 + K3 of SURVEY.md §2.9).
+//
+// Input is the fused QKV projection output [T, (Hq + 2*Hkv) * D].  Q is rotated into a
+// dense [T, Hq, D] buffer for the attention kernels; K is rotated and scattered into the
+// paged K cache; V is scattered *transposed* into the paged V cache.
+//
+// Paged cache layouts (chosen for the MFMA attention kernels, see attention_*.hip):
+//   K cache: [num_pages, Hkv, P, D]   — a page's keys are D-contiguous rows, so a lane can load
+//                                       the A operand of S^T = K Q^T straight from HBM (16 B).
+//   V cache: [num_pages, Hkv, D, P]   — transposed, so the A operand of O^T = V^T P^T is
+//                                       P-contiguous (keys) and loads straight from HBM too.
+// RoPE is the NeoX / HF "rotate_half" form; the cos/sin table [max_pos, rot_dim] (cos in the
+// first half, sin in the second) is precomputed on the host with the model's rope scaling
+// (llama3 / yarn / linear), so the kernel stays a pure streaming op (Appendix B, trig tables).
+#include "common.h"
+
+template <int D, int P>
+__global__ __launch_bounds__(256) void rope_qkv_cache_kernel(
+    const bf16* __restrict__ qkv, int64_t qkv_stride, const int* __restrict__ positions,
+    const float* __restrict__ cos_sin, int rot_dim, bf16* __restrict__ q_out, bf16* __restrict__ k_cache,
+    bf16* __restrict__ v_cache, const int* __restrict__ slots, int Hq, int Hkv, int apply_rope,
+    const bf16* __restrict__ q_norm_w, const bf16* __restrict__ k_norm_w, float qk_eps) {
+  const int t = blockIdx.x;
+  const bf16* row = qkv + (int64_t)t * qkv_stride;
+  const int pos = positions[t];
+  const int slot = slots[t];
+  const float* cs = cos_sin + (int64_t)pos * rot_dim;
+  const int half = rot_dim >> 1;
+  constexpr int DV = D / 8;  // 8-wide vectors per head row
+
+  // ---- Q and K: optional per-head RMSNorm (Qwen3 qk-norm), then rotate ----
+  // One wave handles one head row at a time: lane l < D/8 owns dims [8l, 8l+8).
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nheads = Hq + Hkv;
+  for (int h = wave; h < nheads; h += 4) {
+    const bool is_q = h < Hq;
+    const bf16* src = row + (int64_t)h * D;
+    bf16x8 x = {};
+    if (lane < DV) x = ld8(src + lane * 8);
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (float)x[j];
+    const bf16* nw = is_q ? q_norm_w : k_norm_w;
+    if (nw != nullptr) {
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
+      ss = wave_sum(ss);
+      const float rs = rsqrtf(ss / (float)D + qk_eps);
+      if (lane < DV) {
+        bf16x8 wv = ld8(nw + lane * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (float)(bf16)(f[j] * rs * (float)wv[j]);
+      }
+    }
+    if (apply_rope) {
+      // partner element for rotate_half lives half/8 lanes away (same wave)
+      const int d0 = lane * 8;
+      const int partner = (d0 < half) ? lane + (half >> 3) : lane - (half >> 3);
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = __shfl(f[j], partner < 64 ? partner : lane);
+      if (d0 < rot_dim) {
+        const int i0 = (d0 < half) ? d0 : d0 - half;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float c = cs[i0 + j], s = cs[half + i0 + j];
+          f[j] = (d0 < half) ? (f[j] * c - g[j] * s) : (f[j] * c + g[j] * s);
+        }
+      }
+    }
+    if (lane < DV) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)f[j];
+      if (is_q) {
+        st8(q_out + ((int64_t)t * Hq + h) * D + lane * 8, o);
+      } else if (slot >= 0) {
+        const int kh = h - Hq;
+        const int64_t page = slot / P, off = slot % P;
+        st8(k_cache + ((page * Hkv + kh) * P + off) * D + lane * 8, o);
+      }
+    }
+  }
+  // ---- V: transposed scatter into [page][kh][d][off] ----
+  if (slot >= 0) {
+    const int64_t page = slot / P, off = slot % P;
+    const bf16* vsrc = row + (int64_t)(Hq + Hkv) * D;
+    for (int i = threadIdx.x; i < Hkv * DV; i += blockDim.x) {
+      const int kh = i / DV, dv = i % DV;
+      bf16x8 x = ld8(vsrc + kh * D + dv * 8);
+      bf16* dst = v_cache + ((page * Hkv + kh) * D + dv * 8) * P + off;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[j * P] = x[j];
+    }
+  }
+}
+
+// Plain paged-cache write of already-projected K [T, Hkv, D] and V [T, Hkv, D] (used by the
+// PD-disaggregation receiver and by tests).
+template <int D, int P>
+__global__ void kv_cache_write_kernel(const bf16* __restrict__ k, const bf16* __restrict__ v,
+                                      int64_t kv_stride, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
+                                      const int* __restrict__ slots, int Hkv) {
+  const int t = blockIdx.x;
+  const int slot = slots[t];
+  if (slot < 0) return;
+  const int64_t page = slot / P, off = slot % P;
+  constexpr int DV = D / 8;
+  for (int i = threadIdx.x; i < Hkv * DV; i += blockDim.x) {
+    const int kh = i / DV, dv = i % DV;
+    bf16x8 kx = ld8(k + t * kv_stride + kh * D + dv * 8);
+    st8(k_cache + ((page * Hkv + kh) * P + off) * D + dv * 8, kx);
+    bf16x8 vx = ld8(v + t * kv_stride + kh * D + dv * 8);
+    bf16* dst = v_cache + ((page * Hkv + kh) * D + dv * 8) * P + off;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j * P] = vx[j];
+  }
+}
+
+OME_API int ome_rope_qkv_cache(const void* qkv, int64_t qkv_stride, const int* positions, const float* cos_sin,
+                               int rot_dim, void* q_out, void* k_cache, void* v_cache, const int* slots, int T,
+                               int Hq, int Hkv, int D, int P, int apply_rope, const void* q_norm_w,
+                               const void* k_norm_w, float qk_eps, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (D != 128 && D != 64) return -2;
+  if (rot_dim > D || rot_dim % 16 != 0) return -3;
+#define LAUNCH(DD, PP)                                                                                    \
+  rope_qkv_cache_kernel<DD, PP><<<T, 256, 0, stream>>>((const bf16*)qkv, qkv_stride, positions, cos_sin, \
+                                                      rot_dim, (bf16*)q_out, (bf16*)k_cache,             \
+                                                      (bf16*)v_cache, slots, Hq, Hkv, apply_rope,        \
+                                                      (const bf16*)q_norm_w, (const bf16*)k_norm_w, qk_eps)
+  if (D == 128 && P == 16) LAUNCH(128, 16);
+  else if (D == 64 && P == 16) LAUNCH(64, 16);
+  else return -4;
+#undef LAUNCH
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+OME_API int ome_kv_cache_write(const void* k, const void* v, int64_t kv_stride, void* k_cache, void* v_cache,
+                               const int* slots, int T, int Hkv, int D, int P, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (D == 128 && P == 16)
+    kv_cache_write_kernel<128, 16><<<T, 128, 0, stream>>>((const bf16*)k, (const bf16*)v, kv_stride,
+                                                          (bf16*)k_cache, (bf16*)v_cache, slots, Hkv);
+  else if (D == 64 && P == 16)
+    kv_cache_write_kernel<64, 16><<<T, 128, 0, stream>>>((const bf16*)k, (const bf16*)v, kv_stride,
+                                                         (bf16*)k_cache, (bf16*)v_cache, slots, Hkv);
+  else
+    return -4;
+  OME_CHECK_LAUNCH();
+  return 0;
+}

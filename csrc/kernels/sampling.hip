@@ -1,0 +1,149 @@
+// Token sampling over [B, V] logits (kernel K12): greedy, temperature, top-k, top-p, min-p.
+//
+// One 1024-thread workgroup per row.  The kept set {top-k} ∩ {top-p} ∩ {min-p} is found by
+// bisection on the logit threshold (exact counts / masses over the row each step, the row
+// stays L2-resident: 256 KB for a 128k vocab), and the token is then drawn with the
+// Gumbel-max trick over the kept set (argmax of l/T - log(-log u)), which samples exactly
+// from the renormalised softmax without a sort.  RNG: counter-based splitmix64 on
+// (seed, row, step, index) — reproducible per request seed, graph-capture safe.
+#include "common.h"
+
+#define NT 1024
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+template <typename T>
+__device__ __forceinline__ float ldf(const T* p, int64_t i) { return (float)p[i]; }
+
+struct ValIdx {
+  float v;
+  int i;
+};
+
+__device__ __forceinline__ ValIdx vi_max(ValIdx a, ValIdx b) {
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+
+__device__ ValIdx block_argmax(ValIdx x, float* sv, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ValIdx y{__shfl_xor(x.v, o), __shfl_xor(x.i, o)};
+    x = vi_max(x, y);
+  }
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) { sv[w] = x.v; si[w] = x.i; }
+  __syncthreads();
+  ValIdx r{sv[0], si[0]};
+  for (int k = 1; k < NT / 64; ++k) r = vi_max(r, ValIdx{sv[k], si[k]});
+  __syncthreads();
+  return r;
+}
+
+__device__ float block_sumf(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int k = 0; k < NT / 64; ++k) t += red[k];
+  __syncthreads();
+  return t;
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void sample_kernel(const T* __restrict__ logits, int64_t stride, int V,
+                                                    const float* __restrict__ temperature,
+                                                    const int* __restrict__ top_k, const float* __restrict__ top_p,
+                                                    const float* __restrict__ min_p,
+                                                    const uint64_t* __restrict__ seeds, uint64_t step,
+                                                    int* __restrict__ out_ids, float* __restrict__ out_logprob) {
+  __shared__ float sv[NT / 64];
+  __shared__ int si[NT / 64];
+  const int row = blockIdx.x;
+  const T* lr = logits + (int64_t)row * stride;
+  const float temp = temperature ? temperature[row] : 0.f;
+
+  // pass 1: max (and argmax for greedy)
+  ValIdx best{-__builtin_inff(), 0};
+  for (int i = threadIdx.x; i < V; i += NT) best = vi_max(best, ValIdx{ldf(lr, i), i});
+  best = block_argmax(best, sv, si);
+  const float mx = best.v;
+
+  // softmax denominator at temperature (used for top-p mass, min-p and logprobs)
+  const float invT = temp > 0.f ? 1.f / temp : 1.f;
+  float den = 0.f;
+  for (int i = threadIdx.x; i < V; i += NT) den += __expf((ldf(lr, i) - mx) * invT);
+  den = block_sumf(den, sv);
+
+  if (temp <= 0.f) {
+    if (threadIdx.x == 0) {
+      out_ids[row] = best.i;
+      if (out_logprob) out_logprob[row] = -__logf(den);
+    }
+    return;
+  }
+  const int k = top_k ? top_k[row] : -1;
+  const float pp = top_p ? top_p[row] : 1.f;
+  const float mp = min_p ? min_p[row] : 0.f;
+
+  // Threshold on scaled logit z = (l - mx) / T  (z <= 0).  Keep z >= thr.
+  float thr = -__builtin_inff();
+  if (mp > 0.f) thr = fmaxf(thr, __logf(mp));  // p_i / p_max >= min_p  <=>  z >= log(min_p)
+  const bool need_k = k > 0 && k < V;
+  const bool need_p = pp < 1.f;
+  // count(z >= t) and mass(z >= t) are monotone non-increasing in t, so each constraint's
+  // threshold is the LARGEST t that still keeps >= k tokens (top-k) / >= p of the mass
+  // (top-p).  The kept set is the intersection: the max of the two thresholds.
+  for (int which = 0; which < 2; ++which) {
+    if ((which == 0 && !need_k) || (which == 1 && !need_p)) continue;
+    float lo = -80.f, hi = 0.f;
+    for (int it = 0; it < 26; ++it) {
+      const float mid = 0.5f * (lo + hi);
+      float acc = 0.f;
+      for (int i = threadIdx.x; i < V; i += NT) {
+        const float z = (ldf(lr, i) - mx) * invT;
+        if (z >= mid) acc += which == 0 ? 1.f : __expf(z);
+      }
+      acc = block_sumf(acc, sv);
+      const bool big_enough = which == 0 ? (acc >= (float)k) : (acc / den >= pp);
+      if (big_enough) lo = mid; else hi = mid;
+    }
+    thr = fmaxf(thr, lo);
+  }
+  // Gumbel-max over the kept set
+  const uint64_t seed = seeds ? seeds[row] : 0x1234ull;
+  ValIdx pick{-__builtin_inff(), best.i};
+  for (int i = threadIdx.x; i < V; i += NT) {
+    const float z = (ldf(lr, i) - mx) * invT;
+    if (z >= thr) {
+      const uint64_t h = splitmix64(seed ^ splitmix64(step * 0x100000001B3ull + (uint64_t)i));
+      const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+      pick = vi_max(pick, ValIdx{z - __logf(-__logf(u)), i});
+    }
+  }
+  pick = block_argmax(pick, sv, si);
+  if (threadIdx.x == 0) {
+    out_ids[row] = pick.i;
+    if (out_logprob) out_logprob[row] = (ldf(lr, pick.i) - mx) * invT - __logf(den);
+  }
+}
+
+OME_API int ome_sample(const void* logits, int is_bf16, int64_t stride, int B, int V, const float* temperature,
+                       const int* top_k, const float* top_p, const float* min_p, const uint64_t* seeds,
+                       uint64_t step, int* out_ids, float* out_logprob, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (is_bf16)
+    sample_kernel<bf16><<<B, NT, 0, stream>>>((const bf16*)logits, stride, V, temperature, top_k, top_p, min_p,
+                                              seeds, step, out_ids, out_logprob);
+  else
+    sample_kernel<float><<<B, NT, 0, stream>>>((const float*)logits, stride, V, temperature, top_k, top_p, min_p,
+                                               seeds, step, out_ids, out_logprob);
+  OME_CHECK_LAUNCH();
+  return 0;
+}

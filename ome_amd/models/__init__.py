@@ -1,0 +1,54 @@
+"""Model registry for the first-party runtime.
+
+Architectures served (the HF ``architectures[0]`` names used by the reference's
+ClusterServingRuntime catalog, ``config/runtimes/**``): dense Llama-family decoders and MoE
+decoders.  ``load_format``: ``auto`` (safetensors if present, else random), ``safetensors``,
+``dummy`` (random-init weights of the architecture — the BASELINE benchmark rule).
+"""
+from __future__ import annotations
+
+from pathlib import Path
+
+import torch
+
+from ome_amd.models.config import ModelConfig
+
+DENSE_ARCHS = {
+    "LlamaForCausalLM", "MistralForCausalLM", "Qwen2ForCausalLM", "Qwen3ForCausalLM", "InternLM2ForCausalLM",
+    "LlamaModel", "MistralModel", "Qwen2Model", "Qwen3Model", "LlamaForSequenceClassification",
+    "Qwen2ForRewardModel", "Phi3ForCausalLM", "GraniteForCausalLM", "SmolLM3ForCausalLM",
+}
+MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM", "DeepseekV2ForCausalLM",
+             "DeepseekV3ForCausalLM", "PhiMoEForCausalLM"}
+
+
+def model_class(cfg: ModelConfig):
+    if cfg.is_moe:
+        from ome_amd.models.moe import MoEForCausalLM
+
+        return MoEForCausalLM
+    from ome_amd.models.llama import LlamaForCausalLM
+
+    return LlamaForCausalLM
+
+
+def supported(arch: str) -> bool:
+    return arch in DENSE_ARCHS or arch in MOE_ARCHS
+
+
+def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,
+                model_path: str | None = None, load_format: str = "auto", seed: int = 0):
+    cls = model_class(cfg)
+    m = cls(cfg, device=device, dtype=dtype, max_positions=max_positions)
+    fmt = load_format
+    if fmt == "auto":
+        fmt = "safetensors" if model_path and any(Path(model_path).glob("*.safetensors")) else "dummy"
+    if fmt == "dummy":
+        m.init_random(seed)
+    elif fmt == "safetensors":
+        from ome_amd.models.loader import iter_safetensors
+
+        m.load_hf_weights(iter_safetensors(model_path, device=device))
+    else:
+        raise ValueError(f"unknown load_format {load_format}")
+    return m

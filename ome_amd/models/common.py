@@ -1,0 +1,62 @@
+"""Shared runtime structures for model forward passes: attention metadata and the paged KV cache."""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+from ome_amd import ops
+
+
+@dataclass
+class AttnMeta:
+    """Per-step attention metadata (all int32, on the model device).
+
+    decode:  one query token per sequence, ``seq_lens`` includes the new token.
+    prefill: any mix of prompt chunks / single-token rows; sequence ``s`` owns query rows
+             ``cu_q[s]:cu_q[s+1]`` at absolute positions ``kv_lens[s]-q_len .. kv_lens[s]-1``.
+    """
+
+    mode: str
+    positions: torch.Tensor
+    slots: torch.Tensor
+    block_tables: torch.Tensor
+    seq_lens: torch.Tensor | None = None
+    cu_q: torch.Tensor | None = None
+    kv_lens: torch.Tensor | None = None
+    items: torch.Tensor | None = None
+    logits_idx: torch.Tensor | None = None
+    decode_ws: ops.DecodeWorkspace | None = None
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def is_decode(self) -> bool:
+        return self.mode == "decode"
+
+    @property
+    def num_tokens(self) -> int:
+        return self.positions.shape[0]
+
+
+class PagedKVCache:
+    """Per-layer paged K/V tensors: K ``[pages, Hkv, P, D]``, V ``[pages, Hkv, D, P]`` (bf16).
+
+    Zero-initialised so that masked (never-written) slots can never inject NaN/Inf into the
+    P*V product of the attention kernels.
+    """
+
+    def __init__(self, num_layers: int, num_pages: int, num_kv_heads: int, head_dim: int, page_size: int = 16,
+                 dtype=torch.bfloat16, device="cuda"):
+        self.num_layers, self.num_pages, self.page_size = num_layers, num_pages, page_size
+        self.num_kv_heads, self.head_dim, self.dtype = num_kv_heads, head_dim, dtype
+        self.k = [torch.zeros(num_pages, num_kv_heads, page_size, head_dim, dtype=dtype, device=device)
+                  for _ in range(num_layers)]
+        self.v = [torch.zeros(num_pages, num_kv_heads, head_dim, page_size, dtype=dtype, device=device)
+                  for _ in range(num_layers)]
+
+    @staticmethod
+    def bytes_per_page(num_layers: int, num_kv_heads: int, head_dim: int, page_size: int, dtype=torch.bfloat16) -> int:
+        return 2 * num_layers * num_kv_heads * head_dim * page_size * torch.tensor([], dtype=dtype).element_size()
+
+    def layer(self, i: int) -> tuple[torch.Tensor, torch.Tensor]:
+        return self.k[i], self.v[i]

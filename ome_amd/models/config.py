@@ -1,0 +1,247 @@
+"""Model architecture config for the first-party runtime (parsed from HF ``config.json``).
+
+Covers the dense decoder families of the reference runtime catalog (Llama 2/3/3.1/3.2,
+Mistral, Qwen2/2.5, Qwen3, and their embedding variants) and the MoE families
+(Mixtral, Qwen2/3-MoE, DeepSeek-V2/V3-style); see ``config/runtimes`` of the reference
+(``config/runtimes/srt/meta/llama-3-8b-instruct-rt.yaml``) for the architectures it serves.
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Any
+
+import torch
+
+
+@dataclass
+class ModelConfig:
+    architecture: str = "LlamaForCausalLM"
+    model_type: str = "llama"
+    hidden_size: int = 4096
+    num_layers: int = 32
+    num_heads: int = 32
+    num_kv_heads: int = 8
+    head_dim: int = 128
+    intermediate_size: int = 14336
+    vocab_size: int = 128256
+    rms_norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    rope_scaling: dict | None = None
+    partial_rotary_factor: float = 1.0
+    max_position_embeddings: int = 8192
+    tie_word_embeddings: bool = False
+    attention_bias: bool = False
+    qk_norm: bool = False
+    hidden_act: str = "silu"
+    sliding_window: int | None = None
+    torch_dtype: str = "bfloat16"
+    # MoE
+    num_experts: int = 0
+    num_experts_per_tok: int = 0
+    moe_intermediate_size: int = 0
+    num_shared_experts: int = 0
+    shared_expert_intermediate_size: int = 0
+    norm_topk_prob: bool = True
+    first_k_dense_replace: int = 0
+    moe_layer_freq: int = 1
+    routed_scaling_factor: float = 1.0
+    scoring_func: str = "softmax"
+    n_group: int = 1
+    topk_group: int = 1
+    # MLA (DeepSeek)
+    kv_lora_rank: int = 0
+    q_lora_rank: int = 0
+    qk_nope_head_dim: int = 0
+    qk_rope_head_dim: int = 0
+    v_head_dim: int = 0
+    quantization: str | None = None
+    is_embedding: bool = False
+    extra: dict = field(default_factory=dict)
+
+    @property
+    def is_moe(self) -> bool:
+        return self.num_experts > 0
+
+    @property
+    def is_mla(self) -> bool:
+        return self.kv_lora_rank > 0
+
+    @property
+    def rot_dim(self) -> int:
+        return int(self.head_dim * self.partial_rotary_factor)
+
+    def num_params(self) -> int:
+        H, L, V = self.hidden_size, self.num_layers, self.vocab_size
+        D = self.head_dim
+        attn = H * (self.num_heads * D) * 2 + H * (self.num_kv_heads * D) * 2
+        if self.is_moe:
+            mlp = self.num_experts * 3 * H * self.moe_intermediate_size + H * self.num_experts
+            mlp += self.num_shared_experts * 3 * H * (self.shared_expert_intermediate_size or self.moe_intermediate_size)
+        else:
+            mlp = 3 * H * self.intermediate_size
+        emb = V * H * (1 if self.tie_word_embeddings else 2)
+        return L * (attn + mlp + 2 * H) + emb + H
+
+    @classmethod
+    def from_hf(cls, cfg: dict[str, Any]) -> "ModelConfig":
+        text = cfg.get("text_config") or cfg
+        arch = (cfg.get("architectures") or ["LlamaForCausalLM"])[0]
+        H = text.get("hidden_size", 4096)
+        nh = text.get("num_attention_heads", 32)
+        hd = text.get("head_dim") or H // nh
+        mt = text.get("model_type", cfg.get("model_type", "llama"))
+        c = cls(
+            architecture=arch,
+            model_type=mt,
+            hidden_size=H,
+            num_layers=text.get("num_hidden_layers", 32),
+            num_heads=nh,
+            num_kv_heads=text.get("num_key_value_heads") or nh,
+            head_dim=hd,
+            intermediate_size=text.get("intermediate_size", 4 * H),
+            vocab_size=text.get("vocab_size", 32000),
+            rms_norm_eps=text.get("rms_norm_eps", 1e-6),
+            rope_theta=text.get("rope_theta", 10000.0),
+            rope_scaling=text.get("rope_scaling"),
+            partial_rotary_factor=text.get("partial_rotary_factor", 1.0),
+            max_position_embeddings=text.get("max_position_embeddings", 4096),
+            tie_word_embeddings=bool(cfg.get("tie_word_embeddings", text.get("tie_word_embeddings", False))),
+            attention_bias=bool(text.get("attention_bias", mt in ("qwen2", "qwen2_moe"))),
+            qk_norm=mt in ("qwen3", "qwen3_moe"),
+            hidden_act=text.get("hidden_act", text.get("hidden_activation", "silu")),
+            sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt == "mistral") else None,
+            torch_dtype=str(text.get("torch_dtype", cfg.get("torch_dtype", "bfloat16"))),
+        )
+        # MoE variants
+        ne = text.get("num_local_experts") or text.get("num_experts") or text.get("n_routed_experts") or 0
+        if ne:
+            c.num_experts = ne
+            c.num_experts_per_tok = text.get("num_experts_per_tok", 2)
+            c.moe_intermediate_size = text.get("moe_intermediate_size") or text.get("intermediate_size")
+            c.num_shared_experts = text.get("n_shared_experts") or (1 if text.get("shared_expert_intermediate_size") else 0)
+            c.shared_expert_intermediate_size = text.get("shared_expert_intermediate_size") or 0
+            c.norm_topk_prob = bool(text.get("norm_topk_prob", mt not in ("deepseek_v2",)))
+            c.first_k_dense_replace = text.get("first_k_dense_replace", 0)
+            c.moe_layer_freq = text.get("moe_layer_freq", 1) or 1
+            c.routed_scaling_factor = text.get("routed_scaling_factor", 1.0) or 1.0
+            c.scoring_func = text.get("scoring_func", "softmax")
+            c.n_group = text.get("n_group", 1) or 1
+            c.topk_group = text.get("topk_group", 1) or 1
+        if text.get("kv_lora_rank"):
+            c.kv_lora_rank = text["kv_lora_rank"]
+            c.q_lora_rank = text.get("q_lora_rank") or 0
+            c.qk_nope_head_dim = text.get("qk_nope_head_dim", 128)
+            c.qk_rope_head_dim = text.get("qk_rope_head_dim", 64)
+            c.v_head_dim = text.get("v_head_dim", 128)
+        q = cfg.get("quantization_config")
+        if q:
+            c.quantization = q.get("quant_method") or q.get("quant_type")
+        c.is_embedding = ("Embedding" in arch) or (arch.endswith("Model") and "ForCausalLM" not in arch)
+        c.extra = {k: v for k, v in cfg.items() if k not in ("text_config",)}
+        return c
+
+    @classmethod
+    def from_path(cls, path: str | Path) -> "ModelConfig":
+        p = Path(path)
+        if p.is_dir():
+            p = p / "config.json"
+        return cls.from_hf(json.loads(p.read_text()))
+
+    def shrink(self, num_layers: int | None = None, **kw) -> "ModelConfig":
+        import dataclasses
+
+        return dataclasses.replace(self, num_layers=num_layers or self.num_layers, **kw)
+
+
+# Canonical shapes (weights are random-init per BASELINE rules; these are the HF configs of
+# the named models, cf. reference testdata pkg/hfutil/modelconfig/testdata/llama3.json etc.).
+PRESETS: dict[str, dict] = {
+    "llama-3-8b": dict(architectures=["LlamaForCausalLM"], model_type="llama", hidden_size=4096,
+                       num_hidden_layers=32, num_attention_heads=32, num_key_value_heads=8,
+                       intermediate_size=14336, vocab_size=128256, rms_norm_eps=1e-5, rope_theta=500000.0,
+                       max_position_embeddings=8192, torch_dtype="bfloat16"),
+    "llama-3.1-8b": dict(architectures=["LlamaForCausalLM"], model_type="llama", hidden_size=4096,
+                         num_hidden_layers=32, num_attention_heads=32, num_key_value_heads=8,
+                         intermediate_size=14336, vocab_size=128256, rms_norm_eps=1e-5, rope_theta=500000.0,
+                         max_position_embeddings=131072,
+                         rope_scaling={"factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                       "original_max_position_embeddings": 8192, "rope_type": "llama3"}),
+    "llama-3-70b": dict(architectures=["LlamaForCausalLM"], model_type="llama", hidden_size=8192,
+                        num_hidden_layers=80, num_attention_heads=64, num_key_value_heads=8,
+                        intermediate_size=28672, vocab_size=128256, rms_norm_eps=1e-5, rope_theta=500000.0,
+                        max_position_embeddings=8192),
+    "qwen3-8b": dict(architectures=["Qwen3ForCausalLM"], model_type="qwen3", hidden_size=4096, num_hidden_layers=36,
+                     num_attention_heads=32, num_key_value_heads=8, head_dim=128, intermediate_size=12288,
+                     vocab_size=151936, rms_norm_eps=1e-6, rope_theta=1000000.0, max_position_embeddings=40960),
+    "mixtral-8x7b": dict(architectures=["MixtralForCausalLM"], model_type="mixtral", hidden_size=4096,
+                         num_hidden_layers=32, num_attention_heads=32, num_key_value_heads=8,
+                         intermediate_size=14336, num_local_experts=8, num_experts_per_tok=2, vocab_size=32000,
+                         rms_norm_eps=1e-5, rope_theta=1000000.0, max_position_embeddings=32768),
+    "tiny-llama": dict(architectures=["LlamaForCausalLM"], model_type="llama", hidden_size=256, num_hidden_layers=2,
+                       num_attention_heads=4, num_key_value_heads=2, head_dim=128, intermediate_size=512,
+                       vocab_size=1024, rms_norm_eps=1e-5, rope_theta=10000.0, max_position_embeddings=2048),
+    "tiny-moe": dict(architectures=["Qwen3MoeForCausalLM"], model_type="qwen3_moe", hidden_size=256,
+                     num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
+                     intermediate_size=512, moe_intermediate_size=128, num_experts=8, num_experts_per_tok=2,
+                     vocab_size=1024, rms_norm_eps=1e-6, rope_theta=10000.0, max_position_embeddings=2048),
+}
+
+
+def preset(name: str) -> ModelConfig:
+    return ModelConfig.from_hf(PRESETS[name])
+
+
+def rope_cos_sin(cfg: ModelConfig, max_pos: int, device=None) -> torch.Tensor:
+    """[max_pos, rot_dim] float32 table: cos in the first half, sin in the second.
+
+    Implements the HF rope_type variants used by the catalog: default, linear, dynamic (static
+    at max_pos), llama3 (Llama-3.1 wavelength-band scaling) and yarn (DeepSeek / Qwen).
+    """
+    rot = cfg.rot_dim
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, rot, 2, dtype=torch.float64) / rot))
+    sc = cfg.rope_scaling or {}
+    rtype = sc.get("rope_type", sc.get("type", "default"))
+    mscale = 1.0
+    pos = torch.arange(max_pos, dtype=torch.float64)
+    if rtype == "linear":
+        pos = pos / sc["factor"]
+    elif rtype == "llama3":
+        factor = sc["factor"]
+        lf, hf = sc.get("low_freq_factor", 1.0), sc.get("high_freq_factor", 4.0)
+        old = sc.get("original_max_position_embeddings", 8192)
+        low_wl, high_wl = old / lf, old / hf
+        wl = 2 * math.pi / inv
+        smooth = (old / wl - lf) / (hf - lf)
+        scaled = torch.where(wl > low_wl, inv / factor, inv)
+        mid = (wl <= low_wl) & (wl >= high_wl)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    elif rtype == "yarn":
+        factor = sc["factor"]
+        old = sc.get("original_max_position_embeddings", 4096)
+        bf, bs = sc.get("beta_fast", 32), sc.get("beta_slow", 1)
+
+        def corr(nrot):
+            return (rot * math.log(old / (nrot * 2 * math.pi))) / (2 * math.log(cfg.rope_theta))
+
+        lo, hi = max(math.floor(corr(bf)), 0), min(math.ceil(corr(bs)), rot - 1)
+        ramp = torch.clamp((torch.arange(rot // 2, dtype=torch.float64) - lo) / max(hi - lo, 1e-3), 0, 1)
+        extra = 1 - ramp
+        inv = inv / factor * (1 - extra) + inv * extra
+        ms, msa = sc.get("mscale", 1.0), sc.get("mscale_all_dim", 0.0)
+
+        def ym(s, m):
+            return 1.0 if s <= 1 else 0.1 * m * math.log(s) + 1.0
+
+        mscale = ym(factor, ms) / ym(factor, msa) if msa else ym(factor, ms)
+    elif rtype == "dynamic":
+        factor = sc["factor"]
+        old = cfg.max_position_embeddings
+        if max_pos > old:
+            base = cfg.rope_theta * ((factor * max_pos / old) - (factor - 1)) ** (rot / (rot - 2))
+            inv = 1.0 / (base ** (torch.arange(0, rot, 2, dtype=torch.float64) / rot))
+    freqs = torch.outer(pos, inv)
+    cs = torch.cat([freqs.cos() * mscale, freqs.sin() * mscale], dim=-1).float()
+    return cs.to(device) if device is not None else cs

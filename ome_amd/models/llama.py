@@ -1,0 +1,239 @@
+"""Dense decoder family (Llama 2/3/3.1/3.2, Mistral, Qwen2/2.5, Qwen3) on the ome_amd kernels.
+
+Per layer (SURVEY.md §3.6 hot loop):
+  fused_add_rmsnorm -> QKV GEMM (hipBLASLt) -> fused RoPE + paged KV write (HIP) ->
+  paged attention (HIP, MFMA) -> O GEMM -> TP all-reduce -> fused_add_rmsnorm ->
+  gate_up GEMM -> SiLU*mul (HIP) -> down GEMM -> TP all-reduce.
+Tensor parallelism is Megatron-style: QKV / gate_up column-parallel, O / down row-parallel,
+vocab-parallel embedding and LM head.  KV heads are replicated when tp > num_kv_heads.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ome_amd import ops
+from ome_amd.models.common import AttnMeta, PagedKVCache
+from ome_amd.models.config import ModelConfig, rope_cos_sin
+from ome_amd.parallel import state as pstate
+
+
+def _dtype(name: str) -> torch.dtype:
+    return {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32}.get(
+        str(name).replace("torch.", ""), torch.bfloat16)
+
+
+class TPShape:
+    """Local (per-rank) shapes of a dense decoder under tensor parallelism."""
+
+    def __init__(self, cfg: ModelConfig, tp: int, rank: int):
+        if cfg.num_heads % tp:
+            raise ValueError(f"num_heads {cfg.num_heads} not divisible by tp {tp}")
+        self.tp, self.rank = tp, rank
+        self.hq = cfg.num_heads // tp
+        if cfg.num_kv_heads >= tp:
+            if cfg.num_kv_heads % tp:
+                raise ValueError(f"num_kv_heads {cfg.num_kv_heads} not divisible by tp {tp}")
+            self.hkv = cfg.num_kv_heads // tp
+            self.kv_start = rank * self.hkv
+        else:  # replicate kv heads
+            self.hkv = 1
+            self.kv_start = rank * cfg.num_kv_heads // tp
+        inter = cfg.intermediate_size
+        self.inter = -(-inter // tp)
+        self.vocab = -(-cfg.vocab_size // tp)
+        self.vocab_start = rank * self.vocab
+        self.vocab_end = min(cfg.vocab_size, self.vocab_start + self.vocab)
+
+
+class LlamaForCausalLM:
+    """Weights live as plain tensors in per-layer lists (no nn.Module dispatch on the hot path)."""
+
+    def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
+        self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
+        st = pstate.get()
+        self.tp = TPShape(cfg, st.tp_size, st.tp_rank)
+        self.D = cfg.head_dim
+        self.eps = cfg.rms_norm_eps
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self.window = cfg.sliding_window or -1
+        self.act = 0 if cfg.hidden_act in ("silu", "swish") else 1
+        L = cfg.num_layers
+        self.layers = list(range(L))
+        self.w_qkv: list[torch.Tensor] = [None] * L
+        self.b_qkv: list[torch.Tensor | None] = [None] * L
+        self.w_o: list[torch.Tensor] = [None] * L
+        self.ln1: list[torch.Tensor] = [None] * L
+        self.ln2: list[torch.Tensor] = [None] * L
+        self.w_gu: list[torch.Tensor] = [None] * L
+        self.w_d: list[torch.Tensor] = [None] * L
+        self.qn: list[torch.Tensor | None] = [None] * L
+        self.kn: list[torch.Tensor | None] = [None] * L
+        self.embed: torch.Tensor | None = None
+        self.norm: torch.Tensor | None = None
+        self.lm_head: torch.Tensor | None = None
+        mp = max_positions or cfg.max_position_embeddings
+        self.cos_sin = rope_cos_sin(cfg, mp, device=self.device)
+
+    # ------------------------------------------------------------------ weights
+    def _alloc(self, *shape, std: float | None, gen: torch.Generator | None) -> torch.Tensor:
+        t = torch.empty(*shape, dtype=self.dtype, device=self.device)
+        if std is None:
+            t.fill_(1.0)
+        else:
+            t.normal_(0.0, std, generator=gen)
+        return t
+
+    def init_random(self, seed: int = 0, std: float = 0.02) -> "LlamaForCausalLM":
+        """Random-init weights of this architecture (BASELINE rule: synthetic weights)."""
+        cfg, tp, D = self.cfg, self.tp, self.D
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed + 7919 * pstate.get().rank)
+        H = cfg.hidden_size
+        qkv_rows = (tp.hq + 2 * tp.hkv) * D
+        for i in self.layers:
+            self.w_qkv[i] = self._alloc(qkv_rows, H, std=std, gen=gen)
+            if cfg.attention_bias:
+                self.b_qkv[i] = self._alloc(qkv_rows, std=std, gen=gen)
+            self.w_o[i] = self._alloc(H, tp.hq * D, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+            self.ln1[i] = self._alloc(H, std=None, gen=gen)
+            self.ln2[i] = self._alloc(H, std=None, gen=gen)
+            self.w_gu[i] = self._alloc(2 * tp.inter, H, std=std, gen=gen)
+            self.w_d[i] = self._alloc(H, tp.inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+            if cfg.qk_norm:
+                self.qn[i] = self._alloc(D, std=None, gen=gen)
+                self.kn[i] = self._alloc(D, std=None, gen=gen)
+        self.embed = self._alloc(tp.vocab, H, std=1.0, gen=gen)
+        self.norm = self._alloc(H, std=None, gen=gen)
+        self.lm_head = self.embed if cfg.tie_word_embeddings else self._alloc(tp.vocab, H, std=std, gen=gen)
+        return self
+
+    def load_hf_weights(self, weights) -> "LlamaForCausalLM":
+        """Load from an iterator of (hf_name, tensor) — shards / fuses for this TP rank."""
+        cfg, tp, D = self.cfg, self.tp, self.D
+        qkv_parts: dict[int, dict[str, torch.Tensor]] = {}
+        gu_parts: dict[int, dict[str, torch.Tensor]] = {}
+
+        def rows(t, start, n):
+            return t.narrow(0, start, n)
+
+        def put(t):
+            return t.to(device=self.device, dtype=self.dtype).contiguous()
+
+        for name, w in weights:
+            if name.startswith("model."):
+                name = name[len("model."):]
+            if name == "embed_tokens.weight":
+                self.embed = put(self._vocab_shard(w))
+                continue
+            if name == "norm.weight":
+                self.norm = put(w)
+                continue
+            if name == "lm_head.weight":
+                self.lm_head = put(self._vocab_shard(w))
+                continue
+            parts = name.split(".")
+            if parts[0] != "layers":
+                continue
+            i, rest = int(parts[1]), ".".join(parts[2:])
+            if i >= cfg.num_layers:
+                continue
+            if rest in ("self_attn.q_proj.weight", "self_attn.q_proj.bias"):
+                qkv_parts.setdefault(i, {})["q" + rest[-1]] = rows(w, tp.rank * tp.hq * D, tp.hq * D)
+            elif rest in ("self_attn.k_proj.weight", "self_attn.k_proj.bias"):
+                qkv_parts.setdefault(i, {})["k" + rest[-1]] = rows(w, tp.kv_start * D, tp.hkv * D)
+            elif rest in ("self_attn.v_proj.weight", "self_attn.v_proj.bias"):
+                qkv_parts.setdefault(i, {})["v" + rest[-1]] = rows(w, tp.kv_start * D, tp.hkv * D)
+            elif rest == "self_attn.o_proj.weight":
+                self.w_o[i] = put(w.narrow(1, tp.rank * tp.hq * D, tp.hq * D))
+            elif rest == "mlp.gate_proj.weight":
+                gu_parts.setdefault(i, {})["g"] = rows(w, tp.rank * tp.inter, min(tp.inter, w.shape[0] - tp.rank * tp.inter))
+            elif rest == "mlp.up_proj.weight":
+                gu_parts.setdefault(i, {})["u"] = rows(w, tp.rank * tp.inter, min(tp.inter, w.shape[0] - tp.rank * tp.inter))
+            elif rest == "mlp.down_proj.weight":
+                self.w_d[i] = put(w.narrow(1, tp.rank * tp.inter, min(tp.inter, w.shape[1] - tp.rank * tp.inter)))
+            elif rest == "input_layernorm.weight":
+                self.ln1[i] = put(w)
+            elif rest == "post_attention_layernorm.weight":
+                self.ln2[i] = put(w)
+            elif rest == "self_attn.q_norm.weight":
+                self.qn[i] = put(w)
+            elif rest == "self_attn.k_norm.weight":
+                self.kn[i] = put(w)
+        for i, p in qkv_parts.items():
+            self.w_qkv[i] = put(torch.cat([p["qt"], p["kt"], p["vt"]], 0))
+            if "qs" in p:
+                self.b_qkv[i] = put(torch.cat([p["qs"], p["ks"], p["vs"]], 0))
+        for i, p in gu_parts.items():
+            self.w_gu[i] = put(torch.cat([p["g"], p["u"]], 0))
+        if self.lm_head is None:
+            self.lm_head = self.embed
+        missing = [i for i in self.layers if self.w_qkv[i] is None or self.w_gu[i] is None]
+        if missing or self.embed is None:
+            raise ValueError(f"checkpoint incomplete: layers missing {missing[:4]}...")
+        return self
+
+    def _vocab_shard(self, w: torch.Tensor) -> torch.Tensor:
+        tp = self.tp
+        sh = w[tp.vocab_start:tp.vocab_end]
+        if sh.shape[0] < tp.vocab:
+            sh = torch.cat([sh, sh.new_zeros(tp.vocab - sh.shape[0], sh.shape[1])], 0)
+        return sh
+
+    def weight_bytes(self) -> int:
+        seen, n = set(), 0
+        for lst in (self.w_qkv, self.b_qkv, self.w_o, self.ln1, self.ln2, self.w_gu, self.w_d, self.qn, self.kn,
+                    [self.embed, self.norm, self.lm_head]):
+            for t in lst:
+                if t is not None and t.data_ptr() not in seen:
+                    seen.add(t.data_ptr())
+                    n += t.numel() * t.element_size()
+        return n
+
+    # ------------------------------------------------------------------ forward
+    def attention(self, q: torch.Tensor, k_cache, v_cache, meta: AttnMeta) -> torch.Tensor:
+        if meta.is_decode:
+            return ops.paged_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale,
+                                    meta.decode_ws, self.window)
+        return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
+                                 self.scale, self.window)
+
+    def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        gu = F.linear(x, self.w_gu[i])
+        a = ops.act_and_mul(gu, self.act)
+        return pstate.tp_all_reduce(F.linear(a, self.w_d[i]))
+
+    def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: PagedKVCache,
+                input_embeds: torch.Tensor | None = None) -> torch.Tensor:
+        """ids [T] int32 -> final normed hidden [T, H]."""
+        cfg, tp, D = self.cfg, self.tp, self.D
+        T = ids.shape[0]
+        if input_embeds is None:
+            h = ops.embedding(ids, self.embed, tp.vocab_start, tp.vocab_end)
+            h = pstate.tp_all_reduce(h)
+        else:
+            h = input_embeds
+        residual = h
+        x = ops.rmsnorm(h, self.ln1[0], self.eps)
+        for i in self.layers:
+            if i > 0:
+                ops.fused_add_rmsnorm(x, residual, self.ln1[i], self.eps)
+            qkv = F.linear(x, self.w_qkv[i], self.b_qkv[i])
+            q = torch.empty(T, tp.hq, D, dtype=self.dtype, device=x.device)
+            k_cache, v_cache = kv.layer(i)
+            ops.rope_qkv_cache(qkv, meta.positions, self.cos_sin, cfg.rot_dim, q, k_cache, v_cache, meta.slots,
+                               tp.hq, tp.hkv, D, True, self.qn[i], self.kn[i], self.eps)
+            attn = self.attention(q, k_cache, v_cache, meta)
+            o = pstate.tp_all_reduce(F.linear(attn.view(T, tp.hq * D), self.w_o[i]))
+            ops.fused_add_rmsnorm(o, residual, self.ln2[i], self.eps)
+            x = self.mlp(i, o)
+        ops.fused_add_rmsnorm(x, residual, self.norm, self.eps)
+        return x
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        logits = F.linear(hidden, self.lm_head)
+        if self.tp.tp > 1:
+            logits = pstate.tp_all_gather(logits, dim=-1)
+        return logits[:, : self.cfg.vocab_size]

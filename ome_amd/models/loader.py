@@ -1,0 +1,43 @@
+"""Checkpoint loading: SafeTensors shards -> (name, tensor) stream.
+
+Fast path (``ome_amd.io.native`` / ``csrc/omeio``): the C++ loader parses shard headers,
+``pread``s tensor byte ranges with a thread pool into pinned host buffers and issues
+``hipMemcpyAsync`` straight into HBM, double-buffered (SURVEY.md §7.1 "Native artifact
+I/O").  Fallback: ``safetensors.safe_open`` (no code execution; BASELINE loading rules).
+"""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+from typing import Iterator
+
+import torch
+
+
+def shard_files(model_path: str | Path) -> list[Path]:
+    p = Path(model_path)
+    idx = p / "model.safetensors.index.json"
+    if idx.exists():
+        wm = json.loads(idx.read_text())["weight_map"]
+        return sorted({p / f for f in wm.values()})
+    return sorted(p.glob("*.safetensors"))
+
+
+def iter_safetensors(model_path: str | Path, device="cpu") -> Iterator[tuple[str, torch.Tensor]]:
+    files = shard_files(model_path)
+    if not files:
+        raise FileNotFoundError(f"no safetensors shards under {model_path}")
+    try:
+        from ome_amd.io import native as nio
+
+        if nio.available() and torch.device(device).type == "cuda":
+            yield from nio.iter_tensors_to_device(files, device)
+            return
+    except ImportError:
+        pass
+    from safetensors import safe_open
+
+    for f in files:
+        with safe_open(str(f), framework="pt", device="cpu") as fh:
+            for name in fh.keys():
+                yield name, fh.get_tensor(name)

@@ -1,0 +1,181 @@
+"""Hot-path ops.  CUDA(HIP) tensors -> hand-written gfx950 kernels (``_native``); CPU tensors ->
+the fp32 reference implementations (``reference``).  No silent GPU fallback exists: if the
+native library is missing on a GPU the call raises.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._native import NativeError, available, call, ptr, stream_ptr  # noqa: F401
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _i32(t: torch.Tensor) -> torch.Tensor:
+    assert t.dtype == torch.int32 and t.is_contiguous(), "metadata tensors must be contiguous int32"
+    return t
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    if not _gpu(x):
+        r = ref.rmsnorm(x, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    H = x.shape[-1]
+    x2 = x.reshape(-1, H)
+    assert x2.stride(-1) == 1 and x.dtype == torch.bfloat16
+    out = torch.empty_like(x2) if out is None else out.reshape(-1, H)
+    call("ome_rmsnorm", x2.data_ptr(), x2.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), x2.shape[0], H,
+         float(eps), stream_ptr())
+    return out.view(x.shape)
+
+
+def fused_add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float) -> None:
+    """In place: res <- x + res; x <- rmsnorm(res) * w."""
+    if not _gpu(x):
+        return ref.fused_add_rmsnorm(x, res, w, eps)
+    H = x.shape[-1]
+    x2, r2 = x.view(-1, H), res.view(-1, H)
+    call("ome_fused_add_rmsnorm", x2.data_ptr(), x2.stride(0), r2.data_ptr(), r2.stride(0), w.data_ptr(),
+         x2.shape[0], H, float(eps), stream_ptr())
+
+
+def rope_qkv_cache(qkv, positions, cos_sin, rot_dim, q_out, k_cache, v_cache, slots, Hq, Hkv, D, apply_rope=True,
+                   q_norm_w=None, k_norm_w=None, qk_eps=1e-6) -> None:
+    P = k_cache.shape[2]
+    if not _gpu(qkv):
+        return ref.rope_qkv_cache(qkv, positions, cos_sin, rot_dim, q_out, k_cache, v_cache, slots, Hq, Hkv, D, P,
+                                  apply_rope, q_norm_w, k_norm_w, qk_eps)
+    call("ome_rope_qkv_cache", qkv.data_ptr(), qkv.stride(0), _i32(positions).data_ptr(), cos_sin.data_ptr(),
+         rot_dim, q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), _i32(slots).data_ptr(), qkv.shape[0], Hq,
+         Hkv, D, P, int(apply_rope), ptr(q_norm_w), ptr(k_norm_w), float(qk_eps), stream_ptr())
+
+
+def kv_cache_write(k, v, k_cache, v_cache, slots) -> None:
+    P = k_cache.shape[2]
+    if not _gpu(k):
+        return ref.kv_cache_write(k, v, k_cache, v_cache, slots, P)
+    T, Hkv, D = k.shape
+    assert k.stride() == v.stride()
+    call("ome_kv_cache_write", k.data_ptr(), v.data_ptr(), k.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+         _i32(slots).data_ptr(), T, Hkv, D, P, stream_ptr())
+
+
+def act_and_mul(x: torch.Tensor, act: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """act 0 = SiLU (SwiGLU), 1 = GELU-tanh (GeGLU).  x [.., 2I] -> [.., I]."""
+    if not _gpu(x):
+        return ref.act_and_mul(x, act)
+    I = x.shape[-1] // 2
+    rows = x.numel() // x.shape[-1]
+    out = torch.empty(*x.shape[:-1], I, dtype=x.dtype, device=x.device) if out is None else out
+    call("ome_act_and_mul", x.data_ptr(), out.data_ptr(), rows, I, act, stream_ptr())
+    return out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_start: int = 0, vocab_end: int | None = None,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    vocab_end = table.shape[0] + vocab_start if vocab_end is None else vocab_end
+    if not _gpu(ids):
+        return ref.embedding(ids, table, vocab_start, vocab_end)
+    T, H = ids.shape[0], table.shape[1]
+    out = torch.empty(T, H, dtype=table.dtype, device=table.device) if out is None else out
+    call("ome_embedding", _i32(ids).data_ptr(), table.data_ptr(), out.data_ptr(), T, H, vocab_start, vocab_end,
+         stream_ptr())
+    return out
+
+
+class DecodeWorkspace:
+    """Split-K partial buffers for paged decode, sized once (graph-capture safe)."""
+
+    def __init__(self, max_batch: int, Hq: int, D: int, max_context: int, part_size: int = 512, device="cuda"):
+        self.part_size = part_size
+        self.max_parts = max(1, -(-max_context // part_size))
+        self.part_o = torch.empty(max_batch * Hq * self.max_parts * D, dtype=torch.float32, device=device)
+        self.part_ml = torch.empty(max_batch * Hq * self.max_parts * 2, dtype=torch.float32, device=device)
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeWorkspace | None = None,
+                 window: int = -1, out=None) -> torch.Tensor:
+    """q [B, Hq, D] -> [B, Hq, D]."""
+    if not _gpu(q):
+        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    B, Hq, D = q.shape
+    Hkv, P = k_cache.shape[1], k_cache.shape[2]
+    if ws is None:
+        ws = DecodeWorkspace(B, Hq, D, block_tables.shape[1] * P, device=q.device)
+    out = torch.empty_like(q) if out is None else out
+    call("ome_paged_decode", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+         _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(seq_lens).data_ptr(), out.data_ptr(),
+         out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
+         float(scale), int(window), stream_ptr())
+    return out
+
+
+def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) -> list[tuple[int, int]]:
+    """(seq, row_start) work items, heaviest (longest key range) first."""
+    items = []
+    for s, (ql, kl) in enumerate(zip(q_lens, kv_lens)):
+        pre = kl - ql
+        for r in range(0, ql, tile):
+            items.append((pre + min(r + tile, ql), s, r))
+    items.sort(key=lambda x: -x[0])
+    return [(s, r) for _, s, r in items]
+
+
+def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale, window: int = -1,
+                  out=None) -> torch.Tensor:
+    """q [Tq, Hq, D]; items int32 [n, 2] from :func:`prefill_work_items`."""
+    if not _gpu(q):
+        r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    Tq, Hq, D = q.shape
+    Hkv, P = k_cache.shape[1], k_cache.shape[2]
+    out = torch.empty_like(q) if out is None else out
+    call("ome_paged_prefill", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+         _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
+         _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),
+         int(window), stream_ptr())
+    return out
+
+
+def sample(logits: torch.Tensor, temperature=None, top_k=None, top_p=None, min_p=None, seeds=None, step: int = 0,
+           out_ids=None, out_logprob=None):
+    """Returns (ids int32 [B], logprobs f32 [B])."""
+    if not _gpu(logits):
+        ids, lps = ref.sample(logits, temperature, top_k, top_p, min_p)
+        if out_ids is not None:
+            out_ids.copy_(ids)
+            ids = out_ids
+        if out_logprob is not None:
+            out_logprob.copy_(lps)
+            lps = out_logprob
+        return ids, lps
+    B, V = logits.shape
+    out_ids = torch.empty(B, dtype=torch.int32, device=logits.device) if out_ids is None else out_ids
+    out_logprob = torch.empty(B, dtype=torch.float32, device=logits.device) if out_logprob is None else out_logprob
+    call("ome_sample", logits.data_ptr(), int(logits.dtype == torch.bfloat16), logits.stride(0), B, V,
+         ptr(temperature), ptr(top_k), ptr(top_p), ptr(min_p), ptr(seeds), int(step) & (2**64 - 1),
+         out_ids.data_ptr(), out_logprob.data_ptr(), stream_ptr())
+    return out_ids, out_logprob
+
+
+def pool(hidden: torch.Tensor, cu_lens: torch.Tensor, mode: int = 0, normalize: bool = True) -> torch.Tensor:
+    if not _gpu(hidden):
+        return ref.pool(hidden, cu_lens, mode, normalize)
+    S, H = cu_lens.shape[0] - 1, hidden.shape[-1]
+    out = torch.empty(S, H, dtype=torch.float32, device=hidden.device)
+    call("ome_pool", hidden.data_ptr(), _i32(cu_lens).data_ptr(), out.data_ptr(), S, H, mode, int(normalize),
+         stream_ptr())
+    return out

@@ -1,0 +1,95 @@
+"""ctypes binding of the in-tree HIP kernel library (``ome_amd/_lib/libome_kernels.so``).
+
+Every launcher has the C signature ``int ome_xxx(..., hipStream_t)``; a non-zero return is a
+HIP error code (or a negative argument-check code) and is raised as :class:`NativeError`.
+
+Policy (the round contract): on a GPU the native path is mandatory — if the
+library is missing we raise, we never fall back to eager PyTorch silently.  CPU tensors use
+the reference implementations in :mod:`ome_amd.ops.reference` (that is how the engine and the
+scheduler are tested without a GPU).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+_LIB_DIR = Path(__file__).resolve().parent.parent / "_lib"
+_lock = threading.Lock()
+_libs: dict[str, C.CDLL] = {}
+
+vp, i32, i64, f32, u64 = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_uint64
+
+_SIGNATURES = {
+    "ome_kernels": {
+        "ome_rmsnorm": [vp, i64, vp, vp, i64, i32, i32, f32, vp],
+        "ome_fused_add_rmsnorm": [vp, i64, vp, i64, vp, i32, i32, f32, vp],
+        "ome_rope_qkv_cache": [vp, i64, vp, vp, i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, f32, vp],
+        "ome_kv_cache_write": [vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, vp],
+        "ome_act_and_mul": [vp, vp, i64, i32, i32, vp],
+        "ome_embedding": [vp, vp, vp, i32, i32, i32, i32, vp],
+        "ome_pool": [vp, vp, vp, i32, i32, i32, i32, vp],
+        "ome_paged_decode": [vp, i64, vp, vp, vp, i32, vp, vp, i64, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32,
+                             i32, vp],
+        "ome_paged_prefill": [vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, vp, i64, i32, i32, i32, i32, f32, i32, vp],
+        "ome_sample": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, u64, vp, vp, vp],
+    },
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib_path(name: str = "ome_kernels") -> Path:
+    return _LIB_DIR / f"lib{name}.so"
+
+
+def load(name: str = "ome_kernels") -> C.CDLL:
+    """Load (once) an in-tree native library; raise if it was not built."""
+    lib = _libs.get(name)
+    if lib is not None:
+        return lib
+    with _lock:
+        if name in _libs:
+            return _libs[name]
+        path = lib_path(name)
+        if not path.exists():
+            if os.environ.get("OME_AUTOBUILD", "1") == "1":
+                from ome_amd import build as _b
+
+                _b.build(verbose=False)
+            if not path.exists():
+                raise NativeError(f"{path} missing — run `python -m ome_amd.build` (hipcc, gfx950)")
+        lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+        for fn, argt in _SIGNATURES.get(name, {}).items():
+            f = getattr(lib, fn)
+            f.argtypes = argt
+            f.restype = C.c_int
+        _libs[name] = lib
+        return lib
+
+
+def available(name: str = "ome_kernels") -> bool:
+    try:
+        load(name)
+        return True
+    except (NativeError, OSError):
+        return False
+
+
+def call(fn: str, *args, lib: str = "ome_kernels") -> None:
+    rc = getattr(load(lib), fn)(*args)
+    if rc != 0:
+        raise NativeError(f"{fn} failed with code {rc}")
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,187 @@
+"""Plain-PyTorch fp32 reference implementations of every native op.
+
+They define the semantics the HIP kernels must reproduce (the GPU numerics tests compare the
+two), and they are the CPU execution path used by the CPU-only test-suite.  Cache layouts
+match the kernels exactly: K cache ``[pages, Hkv, P, D]``, V cache ``[pages, Hkv, D, P]``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    rs = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * rs * w.float()).to(x.dtype)
+
+
+def fused_add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: float) -> None:
+    s = (x.float() + res.float()).to(res.dtype)
+    res.copy_(s)
+    x.copy_(rmsnorm(s, w, eps))
+
+
+def apply_rope(x: torch.Tensor, cs: torch.Tensor, rot_dim: int) -> torch.Tensor:
+    """x [T, H, D] float, cs [T, rot_dim] (cos | sin)."""
+    half = rot_dim // 2
+    cos, sin = cs[:, None, :half], cs[:, None, half:rot_dim]
+    x1, x2 = x[..., :half], x[..., half:rot_dim]
+    out = x.clone()
+    out[..., :half] = x1 * cos - x2 * sin
+    out[..., half:rot_dim] = x2 * cos + x1 * sin
+    return out
+
+
+def rope_qkv_cache(qkv, positions, cos_sin, rot_dim, q_out, k_cache, v_cache, slots, Hq, Hkv, D, P, apply=True,
+                   q_norm_w=None, k_norm_w=None, qk_eps=1e-6) -> None:
+    T = qkv.shape[0]
+    if T == 0:
+        return
+    q = qkv[:, : Hq * D].float().view(T, Hq, D)
+    k = qkv[:, Hq * D:(Hq + Hkv) * D].float().view(T, Hkv, D)
+    v = qkv[:, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].view(T, Hkv, D)
+    if q_norm_w is not None:
+        q = rmsnorm(q.to(qkv.dtype), q_norm_w, qk_eps).float()
+    if k_norm_w is not None:
+        k = rmsnorm(k.to(qkv.dtype), k_norm_w, qk_eps).float()
+    if apply:
+        cs = cos_sin[positions.long()]
+        q = apply_rope(q, cs, rot_dim)
+        k = apply_rope(k, cs, rot_dim)
+    q_out.view(T, Hq, D).copy_(q.to(q_out.dtype))
+    kv_cache_write(k.to(k_cache.dtype), v, k_cache, v_cache, slots, P)
+
+
+def kv_cache_write(k, v, k_cache, v_cache, slots, P) -> None:
+    sl = slots.long()
+    ok = sl >= 0
+    if not bool(ok.any()):
+        return
+    sl, k, v = sl[ok], k[ok], v[ok]
+    page, off = sl // P, sl % P
+    k_cache[page, :, off, :] = k.to(k_cache.dtype)
+    v_cache[page, :, :, off] = v.to(v_cache.dtype)
+
+
+def act_and_mul(x: torch.Tensor, act: int = 0) -> torch.Tensor:
+    I = x.shape[-1] // 2
+    g, u = x[..., :I].float(), x[..., I:].float()
+    a = torch.nn.functional.silu(g) if act == 0 else torch.nn.functional.gelu(g, approximate="tanh")
+    return (a * u).to(x.dtype)
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_start: int = 0, vocab_end: int | None = None):
+    vocab_end = table.shape[0] + vocab_start if vocab_end is None else vocab_end
+    own = (ids >= vocab_start) & (ids < vocab_end)
+    local = torch.where(own, ids - vocab_start, torch.zeros_like(ids)).long()
+    out = table[local]
+    return out * own[:, None].to(out.dtype)
+
+
+def gather_kv(k_cache, v_cache, block_table, n: int, kvh: int, P: int):
+    """Contiguous K [n, D] and V [n, D] for one sequence / kv head."""
+    idx = torch.arange(n, device=k_cache.device)
+    pages = block_table[(idx // P).long()].long()
+    off = idx % P
+    k = k_cache[pages, kvh, off, :]
+    v = v_cache[pages, kvh, :, off]
+    return k.float(), v.float()
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1) -> torch.Tensor:
+    B, Hq, D = q.shape
+    Hkv, P = k_cache.shape[1], k_cache.shape[2]
+    G = Hq // Hkv
+    out = torch.zeros_like(q)
+    for b in range(B):
+        L = int(seq_lens[b])
+        if L <= 0:
+            continue
+        lo = max(0, L - window) if window > 0 else 0
+        for h in range(Hkv):
+            k, v = gather_kv(k_cache, v_cache, block_tables[b], L, h, P)
+            k, v = k[lo:], v[lo:]
+            qh = q[b, h * G:(h + 1) * G].float()
+            s = (qh @ k.T) * scale
+            out[b, h * G:(h + 1) * G] = (torch.softmax(s, -1) @ v).to(q.dtype)
+    return out
+
+
+def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window=-1) -> torch.Tensor:
+    Tq, Hq, D = q.shape
+    Hkv, P = k_cache.shape[1], k_cache.shape[2]
+    G = Hq // Hkv
+    out = torch.zeros_like(q)
+    S = len(kv_lens)
+    for s in range(S):
+        q0, q1 = int(cu_q[s]), int(cu_q[s + 1])
+        ql, L = q1 - q0, int(kv_lens[s])
+        if ql == 0:
+            continue
+        qpos = torch.arange(L - ql, L, device=q.device)[:, None]
+        kpos = torch.arange(L, device=q.device)[None, :]
+        mask = kpos <= qpos
+        if window > 0:
+            mask &= kpos > qpos - window
+        for h in range(Hkv):
+            k, v = gather_kv(k_cache, v_cache, block_tables[s], L, h, P)
+            qh = q[q0:q1, h * G:(h + 1) * G].float().transpose(0, 1)  # [G, ql, D]
+            sc = (qh @ k.T) * scale
+            sc = sc.masked_fill(~mask[None], float("-inf"))
+            o = torch.softmax(sc, -1) @ v
+            out[q0:q1, h * G:(h + 1) * G] = o.transpose(0, 1).to(q.dtype)
+    return out
+
+
+def sample(logits, temperature=None, top_k=None, top_p=None, min_p=None, generator=None):
+    """Returns (ids int32 [B], logprob f32 [B]).  Greedy where temperature <= 0."""
+    lf = logits.float()
+    B, V = lf.shape
+    ids = torch.empty(B, dtype=torch.int32, device=logits.device)
+    lps = torch.empty(B, dtype=torch.float32, device=logits.device)
+    for b in range(B):
+        t = float(temperature[b]) if temperature is not None else 0.0
+        row = lf[b]
+        if t <= 0:
+            i = int(torch.argmax(row))
+            ids[b] = i
+            lps[b] = torch.log_softmax(row, -1)[i]
+            continue
+        z = (row - row.max()) / t
+        logp = torch.log_softmax(z, -1)
+        keep = torch.ones(V, dtype=torch.bool, device=row.device)
+        k = int(top_k[b]) if top_k is not None else -1
+        if 0 < k < V:
+            kth = torch.topk(z, k).values[-1]
+            keep &= z >= kth
+        p = float(top_p[b]) if top_p is not None else 1.0
+        if p < 1.0:
+            sz, order = torch.sort(z, descending=True)
+            probs = torch.softmax(sz, -1)
+            cum = torch.cumsum(probs, -1)
+            n_keep = int((cum < p).sum()) + 1
+            thr = sz[min(n_keep, V) - 1]
+            keep &= z >= thr
+        mp = float(min_p[b]) if min_p is not None else 0.0
+        if mp > 0:
+            keep &= z >= math.log(mp)
+        probs = torch.softmax(z.masked_fill(~keep, float("-inf")), -1)
+        i = int(torch.multinomial(probs, 1, generator=generator))
+        ids[b] = i
+        lps[b] = logp[i]
+    return ids, lps
+
+
+def pool(hidden, cu_lens, mode: int = 0, normalize: bool = True) -> torch.Tensor:
+    S = len(cu_lens) - 1
+    outs = []
+    for s in range(S):
+        b, e = int(cu_lens[s]), int(cu_lens[s + 1])
+        h = hidden[e - 1].float() if mode == 0 else hidden[b:e].float().mean(0)
+        outs.append(h)
+    out = torch.stack(outs)
+    if normalize:
+        out = torch.nn.functional.normalize(out, dim=-1)
+    return out

@@ -1,0 +1,122 @@
+"""Process-group state for the runtime: one process per GPU, ``torch.distributed`` over RCCL.
+
+Parallel layout of an engine "group" of ``world = tp * pp`` ranks:
+  rank = pp_rank * tp + tp_rank.
+Rendezvous follows the reference's multi-pod contract (``--dist-init-addr
+$(LWS_LEADER_ADDRESS):5757 --nnodes $(LWS_GROUP_SIZE) --node-rank $(LWS_WORKER_INDEX)``,
+``config/runtimes/srt/deepseek-rdma-pd-rt.yaml:105-110``): a TCP store at the leader.
+On a single 8xMI355X node every pair of GPUs has a direct xGMI link, so the TP all-reduce
+goes through :mod:`ome_amd.parallel.comm` (one-shot P2P for small decode messages, RCCL
+otherwise).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ParallelState:
+    tp_size: int = 1
+    tp_rank: int = 0
+    pp_size: int = 1
+    pp_rank: int = 0
+    dp_size: int = 1
+    dp_rank: int = 0
+    ep_size: int = 1
+    ep_rank: int = 0
+    world_size: int = 1
+    rank: int = 0
+    tp_group: object | None = None
+    pp_group: object | None = None
+    ep_group: object | None = None
+    backend: str = "nccl"
+    comm: object | None = None  # ome_amd.parallel.comm.TPCommunicator
+
+    @property
+    def is_first_pp(self) -> bool:
+        return self.pp_rank == 0
+
+    @property
+    def is_last_pp(self) -> bool:
+        return self.pp_rank == self.pp_size - 1
+
+
+_STATE = ParallelState()
+
+
+def get() -> ParallelState:
+    return _STATE
+
+
+def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_init_addr: str | None = None,
+         rank: int | None = None, world_size: int | None = None, backend: str | None = None,
+         local_rank: int | None = None) -> ParallelState:
+    """Initialise torch.distributed (if world > 1) and build TP / PP / EP groups."""
+    global _STATE
+    world = world_size if world_size is not None else int(os.environ.get("WORLD_SIZE", tp_size * pp_size))
+    rk = rank if rank is not None else int(os.environ.get("RANK", 0))
+    if world != tp_size * pp_size:
+        raise ValueError(f"world_size {world} != tp {tp_size} * pp {pp_size}")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    st = ParallelState(tp_size=tp_size, pp_size=pp_size, world_size=world, rank=rk, backend=backend)
+    st.tp_rank, st.pp_rank = rk % tp_size, rk // tp_size
+    st.ep_size = ep_size or tp_size
+    st.ep_rank = st.tp_rank % st.ep_size
+    if world > 1:
+        if not dist.is_initialized():
+            init_method = f"tcp://{dist_init_addr}" if dist_init_addr else None
+            kw = {}
+            if backend == "nccl":
+                lr = local_rank if local_rank is not None else int(os.environ.get("LOCAL_RANK", rk % max(1, torch.cuda.device_count())))
+                torch.cuda.set_device(lr)
+                kw["device_id"] = torch.device("cuda", lr)
+            dist.init_process_group(backend=backend, init_method=init_method, rank=rk, world_size=world, **kw)
+        for p in range(pp_size):
+            ranks = list(range(p * tp_size, (p + 1) * tp_size))
+            g = dist.new_group(ranks) if tp_size > 1 else None
+            if p == st.pp_rank:
+                st.tp_group = g
+        for t in range(tp_size):
+            ranks = [p * tp_size + t for p in range(pp_size)]
+            g = dist.new_group(ranks) if pp_size > 1 else None
+            if t == st.tp_rank:
+                st.pp_group = g
+        st.ep_group = st.tp_group
+    _STATE = st
+    return st
+
+
+def set_state(st: ParallelState) -> None:
+    global _STATE
+    _STATE = st
+
+
+def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    st = _STATE
+    if st.tp_size == 1:
+        return x
+    if st.comm is not None and x.is_cuda:
+        return st.comm.all_reduce(x)
+    dist.all_reduce(x, group=st.tp_group)
+    return x
+
+
+def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
+    st = _STATE
+    if st.tp_size == 1:
+        return x
+    parts = [torch.empty_like(x) for _ in range(st.tp_size)]
+    dist.all_gather(parts, x.contiguous(), group=st.tp_group)
+    return torch.cat(parts, dim=dim)
+
+
+def destroy() -> None:
+    global _STATE
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    _STATE = ParallelState()

@@ -1,0 +1,238 @@
+"""The serving engine: scheduler + model runner + request lifecycle + metrics.
+
+Tensor parallelism follows the one-process-per-GPU model: every TP rank owns a scheduler
+replica; rank 0 (the one behind the HTTP server) broadcasts newly arrived requests/aborts
+each step over a CPU (gloo) group, so all ranks schedule identical batches, run the same
+forward (RCCL/xGMI collectives inside), and sample identical tokens from the all-gathered
+logits with the same counter-based seeds.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import time
+from dataclasses import asdict, dataclass, field
+
+import torch
+
+from ome_amd.models.config import ModelConfig, preset
+from ome_amd.runtime.metrics import EngineMetrics
+from ome_amd.runtime.request import ReqState, Request, SamplingParams
+from ome_amd.runtime.scheduler import Scheduler
+from ome_amd.runtime.tokenizer import get_tokenizer
+
+log = logging.getLogger("ome_amd.engine")
+
+
+@dataclass
+class EngineArgs:
+    model_path: str | None = None
+    model: str | None = None               # preset name when no model_path (random-init)
+    served_model_name: str | None = None
+    tp_size: int = 1
+    pp_size: int = 1
+    dp_size: int = 1
+    mem_fraction_static: float = 0.9
+    max_running_requests: int = 256
+    max_total_tokens: int | None = None
+    chunked_prefill_size: int = 8192
+    context_length: int | None = None
+    page_size: int = 16
+    cuda_graph: bool = True
+    cuda_graph_max_bs: int | None = None
+    load_format: str = "auto"
+    dtype: str = "bfloat16"
+    device: str = "cuda"
+    seed: int = 0
+    enable_mixed_chunk: bool = False
+    disable_radix_cache: bool = False
+    is_embedding: bool = False
+    kv_cache_dtype: str = "auto"
+    dist_init_addr: str | None = None
+    nnodes: int = 1
+    node_rank: int = 0
+    disaggregation_mode: str = "null"      # null | prefill | decode
+    num_layers_override: int | None = None
+    extra: dict = field(default_factory=dict)
+
+    def model_config(self) -> ModelConfig:
+        if self.model_path and os.path.exists(os.path.join(self.model_path, "config.json")):
+            cfg = ModelConfig.from_path(self.model_path)
+        else:
+            cfg = preset(self.model or "llama-3-8b")
+        if self.num_layers_override:
+            cfg = cfg.shrink(self.num_layers_override)
+        if self.is_embedding:
+            cfg.is_embedding = True
+        return cfg
+
+
+class Engine:
+    def __init__(self, args: EngineArgs):
+        from ome_amd.parallel import state as pstate
+        from ome_amd.runtime.model_runner import ModelRunner
+
+        self.args = args
+        self.cfg = args.model_config()
+        if args.tp_size > 1 or args.pp_size > 1:
+            pstate.init(args.tp_size, args.pp_size, dist_init_addr=args.dist_init_addr)
+        self.pstate = pstate.get()
+        device = args.device
+        if device == "cuda" and torch.cuda.is_available():
+            device = f"cuda:{torch.cuda.current_device()}"
+        elif device == "cuda":
+            device = "cpu"
+        self.max_context = min(args.context_length or self.cfg.max_position_embeddings,
+                               self.cfg.max_position_embeddings)
+        self.runner = ModelRunner(self.cfg, device=device, model_path=args.model_path, load_format=args.load_format,
+                                  page_size=args.page_size, mem_fraction_static=args.mem_fraction_static,
+                                  max_total_tokens=args.max_total_tokens, max_running=args.max_running_requests,
+                                  max_context=self.max_context, cuda_graph=args.cuda_graph,
+                                  cuda_graph_max_bs=args.cuda_graph_max_bs, seed=args.seed)
+        prefix = None
+        if not args.disable_radix_cache:
+            from ome_amd.runtime.prefix_cache import PrefixCache
+
+            prefix = PrefixCache(self.runner.pages, args.page_size)
+        self.scheduler = Scheduler(self.runner.pages, self.runner.slots, args.page_size, args.max_running_requests,
+                                   args.chunked_prefill_size, self.max_context, args.enable_mixed_chunk, prefix)
+        self.tokenizer = get_tokenizer(args.model_path, self.cfg.vocab_size)
+        eos = getattr(self.tokenizer, "eos_token_id", None)
+        self.eos_ids = {eos} if eos is not None else set()
+        self.metrics = EngineMetrics()
+        self.served_model_name = args.served_model_name or (args.model_path or args.model or "model")
+        self._lock = threading.Lock()
+        self._inbox: list[Request] = []
+        self._aborts: list[str] = []
+        self._wake = threading.Event()
+        self._stop = False
+        self.step_count = 0
+        self.kv_transfer = None  # PD disaggregation hook (ome_amd.runtime.disagg)
+
+    # ------------------------------------------------------------------ API
+    def make_request(self, prompt_ids: list[int], params: SamplingParams | None = None, **kw) -> Request:
+        params = params or SamplingParams()
+        params.validate()
+        if len(prompt_ids) == 0:
+            raise ValueError("empty prompt")
+        if len(prompt_ids) + 1 > self.max_context:
+            raise ValueError(f"prompt of {len(prompt_ids)} tokens exceeds context length {self.max_context}")
+        params.max_new_tokens = min(params.max_new_tokens, self.max_context - len(prompt_ids))
+        return Request(prompt_ids=list(prompt_ids), params=params, **kw)
+
+    def add_request(self, req: Request) -> Request:
+        with self._lock:
+            self._inbox.append(req)
+        self._wake.set()
+        return req
+
+    def abort(self, rid: str) -> None:
+        with self._lock:
+            self._aborts.append(rid)
+        self._wake.set()
+
+    def _drain_inbox(self) -> None:
+        with self._lock:
+            new, aborts = self._inbox, self._aborts
+            self._inbox, self._aborts = [], []
+        if self.pstate.tp_size > 1:
+            new, aborts = self._broadcast_control(new, aborts)
+        for r in new:
+            r.arrival_time = r.arrival_time or time.perf_counter()
+            self.scheduler.add(r)
+            self.metrics.on_arrival(r)
+        for rid in aborts:
+            r = self.scheduler.abort(rid)
+            if r is not None and r.on_token:
+                r.on_token(r, [], True)
+
+    def _broadcast_control(self, new, aborts):
+        import torch.distributed as dist
+
+        payload = [[(r.rid, r.prompt_ids, asdict(r.params)) for r in new], aborts]
+        obj = [payload if self.pstate.rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=self._cpu_group())
+        if self.pstate.rank == 0:
+            return new, aborts
+        reqs = [Request(prompt_ids=p, params=SamplingParams(**sp), rid=rid) for rid, p, sp in obj[0][0]]
+        return reqs, obj[0][1]
+
+    def _cpu_group(self):
+        import torch.distributed as dist
+
+        if not hasattr(self, "_gloo"):
+            self._gloo = dist.new_group(backend="gloo")
+        return self._gloo
+
+    def step(self) -> list[Request]:
+        """One scheduler iteration. Returns requests that finished in this step."""
+        self._drain_inbox()
+        batch = self.scheduler.schedule()
+        if batch is None:
+            return []
+        t0 = time.perf_counter()
+        if self.cfg.is_embedding:
+            embs = self.runner.embed(batch)
+            now = time.perf_counter()
+            done = []
+            for c, e in zip(batch.chunks, embs):
+                c.req.embedding = e
+                c.req.num_cached = c.start + c.length
+                if c.req.num_cached >= len(c.req.prompt_ids):
+                    c.req.first_token_time = now
+                    self.scheduler.finish(c.req, "stop")
+                    done.append(c.req)
+                    if c.req.on_token:
+                        c.req.on_token(c.req, [], True)
+            return done
+        ids, lps = self.runner.run(batch)
+        now = time.perf_counter()
+        done = self.scheduler.commit(batch, ids, lps, now, self.eos_ids)
+        self.step_count += 1
+        self.metrics.on_step(batch, now - t0, done, self.scheduler, self.runner.pages)
+        return done
+
+    def has_work(self) -> bool:
+        return self.scheduler.has_work() or bool(self._inbox)
+
+    def generate(self, prompts: list[list[int]], params: SamplingParams | list[SamplingParams] | None = None) -> list[Request]:
+        plist = params if isinstance(params, list) else [params] * len(prompts)
+        reqs = [self.add_request(self.make_request(p, SamplingParams(**asdict(sp)) if sp else None))
+                for p, sp in zip(prompts, plist)]
+        while any(not r.finished for r in reqs):
+            self.step()
+        return reqs
+
+    # ------------------------------------------------------------------ background loop
+    def run_forever(self) -> None:
+        while not self._stop:
+            if not self.has_work():
+                self._wake.wait(timeout=0.05)
+                self._wake.clear()
+                if self.pstate.tp_size == 1:
+                    continue
+            try:
+                self.step()
+            except Exception:  # noqa: BLE001 — surface and keep serving other requests
+                log.exception("engine step failed")
+                for r in list(self.scheduler.running):
+                    self.scheduler.finish(r, "abort:error")
+                    if r.on_token:
+                        r.on_token(r, [], True)
+
+    def start(self) -> threading.Thread:
+        t = threading.Thread(target=self.run_forever, name="ome-engine", daemon=True)
+        t.start()
+        return t
+
+    def shutdown(self) -> None:
+        self._stop = True
+        self._wake.set()
+
+    def health(self) -> dict:
+        return {"running": self.scheduler.num_running, "waiting": self.scheduler.num_waiting,
+                "kv_usage": self.runner.pages.usage(), "steps": self.step_count}
+
+
+__all__ = ["Engine", "EngineArgs", "Request", "ReqState", "SamplingParams"]

@@ -1,0 +1,300 @@
+"""ModelRunner: owns the model, the paged KV cache, and the decode HIP graphs.
+
+Step inputs are packed host-side into ONE pinned int32 buffer and sent with ONE
+``hipMemcpyAsync`` per step; decode steps replay a HIP graph captured per batch-size bucket
+(``--cuda-graph-max-bs``, reference runtimes use e.g. ``--cuda-graph-bs 128``), so the
+steady-state decode loop costs one H2D copy + one graph launch + one D2H copy of the
+sampled ids.  Prefill / mixed steps run eagerly (their GPU time dwarfs launch overhead).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import time
+
+import numpy as np
+import torch
+
+from ome_amd import ops
+from ome_amd.models import build_model
+from ome_amd.models.common import AttnMeta, PagedKVCache
+from ome_amd.models.config import ModelConfig
+from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
+from ome_amd.runtime.scheduler import StepBatch
+
+log = logging.getLogger("ome_amd.runtime")
+
+_MASK64 = (1 << 64) - 1
+
+
+def _mix(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _MASK64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _MASK64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _MASK64
+    return x ^ (x >> 31)
+
+
+def default_buckets(max_bs: int) -> list[int]:
+    b = [1, 2, 4, 8, 12, 16, 24, 32, 40, 48, 56, 64, 80, 96, 112, 128, 144, 160, 176, 192, 208, 224, 240, 256]
+    b += list(range(288, max_bs + 1, 32))
+    return [x for x in b if x <= max_bs] or [max_bs]
+
+
+class _DecodeBuffers:
+    FIELDS_I = ("ids", "pos", "slots", "seq_lens", "req_idx", "top_k")
+    FIELDS_F = ("temp", "top_p", "min_p")
+
+    def __init__(self, bmax: int, device):
+        self.bmax = bmax
+        n = (len(self.FIELDS_I) + len(self.FIELDS_F) + 2) * bmax
+        self.dev = torch.zeros(n, dtype=torch.int32, device=device)
+        self.host = torch.zeros(n, dtype=torch.int32, pin_memory=device.type == "cuda")
+        self.hnp = self.host.numpy()
+        self.hf = self.hnp.view(np.float32)
+        self.off = {}
+        o = 0
+        for f in self.FIELDS_I + self.FIELDS_F:
+            self.off[f] = o
+            o += bmax
+        self.off["seeds"] = o  # 2*bmax int32 words, 8-byte aligned (bmax even or o even)
+
+    def view(self, name: str, bs: int) -> torch.Tensor:
+        o = self.off[name]
+        if name in self.FIELDS_F:
+            return self.dev[o:o + bs].view(torch.float32)
+        if name == "seeds":
+            return self.dev[o:o + 2 * bs].view(torch.int64)
+        return self.dev[o:o + bs]
+
+
+class ModelRunner:
+    def __init__(self, cfg: ModelConfig, device: str | torch.device = "cuda", dtype=torch.bfloat16,
+                 model_path: str | None = None, load_format: str = "auto", page_size: int = 16,
+                 mem_fraction_static: float = 0.9, max_total_tokens: int | None = None, max_running: int = 256,
+                 max_context: int = 8192, cuda_graph: bool = True, cuda_graph_max_bs: int | None = None,
+                 seed: int = 0, kv_cache_dtype: str = "auto"):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.P = page_size
+        self.max_context = max_context
+        self.max_running = max_running
+        self.is_cuda = self.device.type == "cuda"
+        t0 = time.perf_counter()
+        self.model = build_model(cfg, self.device, dtype, max_positions=max_context + page_size,
+                                 model_path=model_path, load_format=load_format, seed=seed)
+        self.load_time = time.perf_counter() - t0
+        # ---- KV cache sizing (reference: --mem-frac 0.9, llama-3-8b-instruct-rt.yaml:59-60) ----
+        tp = self.model.tp
+        page_bytes = PagedKVCache.bytes_per_page(cfg.num_layers, tp.hkv, cfg.head_dim, page_size, dtype)
+        if self.is_cuda:
+            free, total = torch.cuda.mem_get_info(self.device)
+            used_by_others = total - free
+            budget = total * mem_fraction_static - used_by_others - 2 * (1 << 30)
+            num_pages = int(max(budget, 0) // page_bytes)
+        else:
+            num_pages = 4096
+        max_pages_per_seq = -(-max_context // page_size) + 1
+        want = max_running * max_pages_per_seq + 2
+        if max_total_tokens:
+            want = min(want, -(-max_total_tokens // page_size) + 2)
+        num_pages = max(min(num_pages, want), max_pages_per_seq + 2)
+        self.kv = PagedKVCache(cfg.num_layers, num_pages, tp.hkv, cfg.head_dim, page_size, dtype, self.device)
+        self.pages = PagePool(num_pages)
+        self.slots = ReqSlotPool(max_running + 1, max_pages_per_seq, self.device)
+        log.info("KV cache: %d pages x %d tokens (%.1f GiB), weights %.1f GiB", num_pages, page_size,
+                 num_pages * page_bytes / 2**30, self.model.weight_bytes() / 2**30)
+        # ---- decode graphs ----
+        self.bmax = max(2, cuda_graph_max_bs or max_running)
+        self.bmax += self.bmax % 2
+        self.buckets = default_buckets(self.bmax)
+        if self.buckets[-1] < self.bmax:
+            self.buckets.append(self.bmax)
+        self.dbuf = _DecodeBuffers(self.bmax, self.device)
+        self.out_ids = torch.zeros(self.bmax, dtype=torch.int32, device=self.device)
+        self.out_lp = torch.zeros(self.bmax, dtype=torch.float32, device=self.device)
+        self._ws_cache: dict[int, ops.DecodeWorkspace] = {}
+        self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_pool = None
+        self.use_graph = cuda_graph and self.is_cuda
+        if self.use_graph:
+            self.capture_graphs()
+
+    # ------------------------------------------------------------------ helpers
+    def decode_ws(self, bs: int) -> ops.DecodeWorkspace:
+        """Split-K partitioning chosen so a decode launch has >= ~1024 active workgroups."""
+        ws = self._ws_cache.get(bs)
+        if ws is None:
+            hkv = self.model.tp.hkv
+            parts = max(1, math.ceil(1024 / max(1, bs * hkv)))
+            part = max(256, -(-self.max_context // parts))
+            part = -(-part // 128) * 128
+            ws = ops.DecodeWorkspace(bs, self.model.tp.hq, self.cfg.head_dim, self.max_context + self.P, part,
+                                     self.device)
+            self._ws_cache[bs] = ws
+        return ws
+
+    def _decode_forward(self, bs: int) -> None:
+        d = self.dbuf
+        bt = self.slots.table.index_select(0, d.view("req_idx", bs))
+        meta = AttnMeta("decode", d.view("pos", bs), d.view("slots", bs), bt, seq_lens=d.view("seq_lens", bs),
+                        decode_ws=self.decode_ws(bs))
+        hidden = self.model.forward(d.view("ids", bs), meta, self.kv)
+        logits = self.model.compute_logits(hidden)
+        ops.sample(logits, d.view("temp", bs), d.view("top_k", bs), d.view("top_p", bs), d.view("min_p", bs),
+                   d.view("seeds", bs), 0, out_ids=self.out_ids[:bs], out_logprob=self.out_lp[:bs])
+
+    def capture_graphs(self) -> None:
+        t0 = time.perf_counter()
+        d = self.dbuf
+        d.hnp[:] = 0
+        d.hnp[d.off["slots"]:d.off["slots"] + d.bmax] = -1
+        d.dev.copy_(d.host)
+        torch.cuda.synchronize(self.device)
+        stream = torch.cuda.Stream(self.device)
+        stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(stream):
+            for bs in reversed(self.buckets):
+                self._decode_forward(bs)  # warm-up (allocations, hipBLASLt heuristics)
+        torch.cuda.current_stream(self.device).wait_stream(stream)
+        torch.cuda.synchronize(self.device)
+        for bs in reversed(self.buckets):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                self._decode_forward(bs)
+            if self.graph_pool is None:
+                self.graph_pool = g.pool()
+            self.graphs[bs] = g
+        torch.cuda.synchronize(self.device)
+        log.info("captured %d decode graphs in %.1fs", len(self.graphs), time.perf_counter() - t0)
+
+    @staticmethod
+    def _seed(req, pos: int) -> int:
+        base = req.params.seed if req.params.seed is not None else hash(req.rid) & _MASK64
+        return _mix((base * 1000003 + pos) & _MASK64)
+
+    # ------------------------------------------------------------------ steps
+    def run(self, batch: StepBatch) -> tuple[list[int], list[float]]:
+        self.slots.flush()
+        if batch.mode == "decode" and all(c.length == 1 for c in batch.chunks):
+            return self.run_decode(batch)
+        return self.run_prefill(batch)
+
+    def run_decode(self, batch: StepBatch):
+        B = len(batch.chunks)
+        bs = next((b for b in self.buckets if b >= B), None)
+        d = self.dbuf
+        if bs is None:  # larger than the biggest graph: eager in bucket-sized slices
+            return self.run_prefill(batch)
+        h, hf, off = d.hnp, d.hf, d.off
+        h[off["ids"]:off["ids"] + bs] = 0
+        h[off["slots"]:off["slots"] + bs] = -1
+        h[off["seq_lens"]:off["seq_lens"] + bs] = 0
+        h[off["req_idx"]:off["req_idx"] + bs] = self.slots.max_reqs - 1
+        h[off["pos"]:off["pos"] + bs] = 0
+        seeds = h[off["seeds"]:off["seeds"] + 2 * bs].view(np.uint64)
+        for i, c in enumerate(batch.chunks):
+            r = c.req
+            pos = c.start
+            h[off["ids"] + i] = r.all_ids[pos]
+            h[off["pos"] + i] = pos
+            h[off["slots"] + i] = r.pages[pos // self.P] * self.P + pos % self.P
+            h[off["seq_lens"] + i] = pos + 1
+            h[off["req_idx"] + i] = r.req_slot
+            p = r.params
+            h[off["top_k"] + i] = p.top_k
+            hf[off["temp"] + i] = p.temperature
+            hf[off["top_p"] + i] = p.top_p
+            hf[off["min_p"] + i] = p.min_p
+            seeds[i] = self._seed(r, pos)
+        for i in range(B, bs):
+            hf[off["temp"] + i] = 0.0
+            hf[off["top_p"] + i] = 1.0
+            h[off["top_k"] + i] = -1
+        d.dev.copy_(d.host, non_blocking=True)
+        if self.use_graph:
+            self.graphs[bs].replay()
+        else:
+            self._decode_forward(bs)
+        ids = self.out_ids[:B].to("cpu", non_blocking=False).tolist()
+        lps = self.out_lp[:B].to("cpu").tolist()
+        return ids, lps
+
+    def run_prefill(self, batch: StepBatch):
+        P = self.P
+        ids, pos, slots, q_lens, kv_lens, req_idx, sample_rows = [], [], [], [], [], [], []
+        for c in batch.chunks:
+            r = c.req
+            toks = r.all_ids[c.start:c.start + c.length]
+            ids.extend(toks)
+            pp = range(c.start, c.start + c.length)
+            pos.extend(pp)
+            pages = r.pages
+            slots.extend(pages[x // P] * P + x % P for x in pp)
+            q_lens.append(c.length)
+            kv_lens.append(c.start + c.length)
+            req_idx.append(r.req_slot)
+            sample_rows.append(len(ids) - 1)
+        items = ops.prefill_work_items(q_lens, kv_lens)
+        T, S, n_it = len(ids), len(q_lens), len(items)
+        cu = np.zeros(S + 1, dtype=np.int32)
+        cu[1:] = np.cumsum(q_lens)
+        packed = np.concatenate([np.asarray(ids, np.int32), np.asarray(pos, np.int32), np.asarray(slots, np.int32),
+                                 cu, np.asarray(kv_lens, np.int32), np.asarray(req_idx, np.int32),
+                                 np.asarray(sample_rows, np.int32),
+                                 np.asarray(items, np.int32).reshape(-1) if n_it else np.zeros(0, np.int32)])
+        host = torch.from_numpy(packed)
+        if self.is_cuda:
+            host = host.pin_memory()
+        dev = host.to(self.device, non_blocking=True)
+        o = 0
+
+        def take(n):
+            nonlocal o
+            t = dev[o:o + n]
+            o += n
+            return t
+
+        t_ids, t_pos, t_slots = take(T), take(T), take(T)
+        t_cu, t_kv, t_req, t_rows = take(S + 1), take(S), take(S), take(S)
+        t_items = take(2 * n_it).view(n_it, 2)
+        bt = self.slots.table.index_select(0, t_req)
+        meta = AttnMeta("prefill", t_pos, t_slots, bt, cu_q=t_cu, kv_lens=t_kv, items=t_items)
+        hidden = self.model.forward(t_ids, meta, self.kv)
+        logits = self.model.compute_logits(hidden.index_select(0, t_rows))
+        temp = torch.tensor([c.req.params.temperature for c in batch.chunks], dtype=torch.float32)
+        top_k = torch.tensor([c.req.params.top_k for c in batch.chunks], dtype=torch.int32)
+        top_p = torch.tensor([c.req.params.top_p for c in batch.chunks], dtype=torch.float32)
+        min_p = torch.tensor([c.req.params.min_p for c in batch.chunks], dtype=torch.float32)
+        if self.is_cuda:
+            sv = [self._seed(c.req, c.start + c.length) for c in batch.chunks]
+            seeds = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in sv], dtype=torch.int64)
+            temp, top_k, top_p, min_p, seeds = (x.to(self.device, non_blocking=True)
+                                                for x in (temp, top_k, top_p, min_p, seeds))
+            out_ids, out_lp = ops.sample(logits, temp, top_k, top_p, min_p, seeds, 0)
+        else:
+            out_ids, out_lp = ops.sample(logits, temp, top_k, top_p, min_p)
+        return out_ids.cpu().tolist(), out_lp.cpu().tolist()
+
+    def embed(self, batch: StepBatch) -> list[list[float]]:
+        """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts."""
+        P = self.P
+        ids, pos, slots, q_lens, req_idx = [], [], [], [], []
+        for c in batch.chunks:
+            r = c.req
+            ids.extend(r.prompt_ids)
+            pos.extend(range(len(r.prompt_ids)))
+            slots.extend(r.pages[x // P] * P + x % P for x in range(len(r.prompt_ids)))
+            q_lens.append(len(r.prompt_ids))
+            req_idx.append(r.req_slot)
+        cu = [0]
+        for q in q_lens:
+            cu.append(cu[-1] + q)
+        items = ops.prefill_work_items(q_lens, q_lens)
+        dv = self.device
+        t = lambda a: torch.tensor(a, dtype=torch.int32, device=dv)  # noqa: E731
+        bt = self.slots.table.index_select(0, t(req_idx))
+        meta = AttnMeta("prefill", t(pos), t(slots), bt, cu_q=t(cu), kv_lens=t(q_lens),
+                        items=t(items).view(-1, 2) if items else torch.zeros(0, 2, dtype=torch.int32, device=dv))
+        hidden = self.model.forward(t(ids), meta, self.kv)
+        return ops.pool(hidden, t(cu), 0, True).cpu().tolist()

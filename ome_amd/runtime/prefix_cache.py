@@ -1,0 +1,98 @@
+"""Page-granular prefix (radix) cache for the paged KV pool.
+
+Full pages of finished requests stay resident, keyed by a hash chain over their token
+content (h_i = H(h_{i-1}, tokens of page i)), so a new request whose prompt shares a prefix
+reuses those pages instead of recomputing them (SGLang radix cache, which the reference's
+runtimes keep enabled unless ``--disable-radix-cache``).  Pages matched by running requests
+are pinned (refcount); unpinned pages are evicted LRU-deepest-first when the allocator runs
+dry, and eviction of a page leaves its descendants unreachable so they are evicted next.
+"""
+from __future__ import annotations
+
+import itertools
+
+
+class PrefixCache:
+    def __init__(self, pool, page_size: int):
+        self.pool, self.P = pool, page_size
+        self.by_hash: dict[int, int] = {}          # chain hash -> page
+        self.meta: dict[int, list] = {}            # page -> [hash, refcount, last_use, depth]
+        self._clock = itertools.count()
+        self.hits = 0
+        self.queries = 0
+
+    def _chain(self, tokens: list[int]):
+        h = 0
+        for i in range(len(tokens) // self.P):
+            h = hash((h, tuple(tokens[i * self.P:(i + 1) * self.P])))
+            yield i, h
+
+    def match(self, tokens: list[int]) -> list[int]:
+        """Pin and return the cached pages covering the longest full-page prefix of ``tokens``."""
+        self.queries += 1
+        out = []
+        t = next(self._clock)
+        for _, h in self._chain(tokens):
+            p = self.by_hash.get(h)
+            if p is None:
+                break
+            m = self.meta[p]
+            m[1] += 1
+            m[2] = t
+            out.append(p)
+        if out:
+            self.hits += 1
+        return out
+
+    def insert(self, tokens: list[int], pages: list[int]) -> set[int]:
+        """Offer a finished request's pages; returns the pages now owned by the cache (the
+        caller frees the rest).  Unpins pages the request had matched."""
+        kept: set[int] = set()
+        t = next(self._clock)
+        for i, h in self._chain(tokens):
+            if i >= len(pages):
+                break
+            page = pages[i]
+            cur = self.by_hash.get(h)
+            if cur is None:
+                if page in self.meta:  # page cached under another hash: cannot happen, be safe
+                    continue
+                self.by_hash[h] = page
+                self.meta[page] = [h, 0, t, i]
+                kept.add(page)
+            elif cur == page:
+                m = self.meta[page]
+                m[1] = max(0, m[1] - 1)
+                m[2] = t
+                kept.add(page)
+        # pages the request matched beyond its own computed prefix are still pinned: release
+        for p in pages:
+            if p in self.meta and p not in kept:
+                self.meta[p][1] = max(0, self.meta[p][1] - 1)
+                kept.add(p)
+        return kept
+
+    def release(self, pages: list[int]) -> None:
+        for p in pages:
+            m = self.meta.get(p)
+            if m is not None:
+                m[1] = max(0, m[1] - 1)
+
+    def owns(self, page: int) -> bool:
+        return page in self.meta
+
+    def evict(self, n: int) -> int:
+        if n <= 0:
+            return 0
+        cand = sorted((m[2], -m[3], p) for p, m in self.meta.items() if m[1] == 0)
+        freed = []
+        for _, _, p in cand[:n]:
+            h = self.meta.pop(p)[0]
+            self.by_hash.pop(h, None)
+            freed.append(p)
+        self.pool.free(freed)
+        return len(freed)
+
+    @property
+    def num_pages(self) -> int:
+        return len(self.meta)

@@ -1,0 +1,96 @@
+"""Request / sampling-parameter objects of the first-party serving runtime."""
+from __future__ import annotations
+
+import enum
+import itertools
+import time
+from dataclasses import dataclass, field
+from typing import Callable
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 128
+    temperature: float = 0.0
+    top_p: float = 1.0
+    top_k: int = -1
+    min_p: float = 0.0
+    stop_token_ids: list[int] = field(default_factory=list)
+    stop: list[str] = field(default_factory=list)
+    ignore_eos: bool = False
+    seed: int | None = None
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
+    repetition_penalty: float = 1.0
+    logprobs: bool = False
+    n: int = 1
+
+    def validate(self) -> None:
+        if self.max_new_tokens < 0:
+            raise ValueError("max_new_tokens must be >= 0")
+        if self.temperature < 0:
+            raise ValueError("temperature must be >= 0")
+        if not 0 < self.top_p <= 1:
+            raise ValueError("top_p must be in (0, 1]")
+        if self.top_k == 0 or self.top_k < -1:
+            raise ValueError("top_k must be -1 or >= 1")
+        if not 0 <= self.min_p <= 1:
+            raise ValueError("min_p must be in [0, 1]")
+
+
+class ReqState(enum.Enum):
+    WAITING = "waiting"
+    RUNNING = "running"
+    FINISHED = "finished"
+
+
+_rid = itertools.count()
+
+
+@dataclass(eq=False)
+class Request:
+    prompt_ids: list[int]
+    params: SamplingParams = field(default_factory=SamplingParams)
+    rid: str = field(default_factory=lambda: f"req-{next(_rid)}")
+    output_ids: list[int] = field(default_factory=list)
+    output_logprobs: list[float] = field(default_factory=list)
+    state: ReqState = ReqState.WAITING
+    num_cached: int = 0            # tokens whose K/V is resident in the paged cache
+    num_prefix_hit: int = 0        # of those, how many came from the prefix cache
+    pages: list[int] = field(default_factory=list)
+    req_slot: int = -1             # row of the GPU page-table pool
+    finish_reason: str | None = None
+    arrival_time: float = field(default_factory=time.perf_counter)
+    first_token_time: float | None = None
+    finish_time: float | None = None
+    token_times: list[float] = field(default_factory=list)
+    on_token: Callable[["Request", list[int], bool], None] | None = None
+    # PD disaggregation: KV arrives from a prefill engine instead of being computed here
+    bootstrap: dict | None = None
+    embedding: list[float] | None = None
+    is_embedding: bool = False
+    preempted: int = 0
+    lora: str | None = None
+
+    @property
+    def all_ids(self) -> list[int]:
+        return self.prompt_ids + self.output_ids
+
+    @property
+    def seq_len(self) -> int:
+        return len(self.prompt_ids) + len(self.output_ids)
+
+    @property
+    def prefill_done(self) -> bool:
+        # decode-ready: every token except the last one has K/V in cache; the last token is the
+        # next decode input (a prompt whose final chunk left exactly one token is finished by a
+        # decode step, which is the same computation as a 1-token prefill chunk)
+        return self.num_cached >= self.seq_len - 1
+
+    @property
+    def ttft(self) -> float | None:
+        return None if self.first_token_time is None else self.first_token_time - self.arrival_time
+
+    @property
+    def finished(self) -> bool:
+        return self.state == ReqState.FINISHED

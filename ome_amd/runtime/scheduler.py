@@ -1,0 +1,244 @@
+"""Continuous-batching scheduler with chunked prefill and paged-KV admission control.
+
+Policy (SGLang-style, which is what the reference's runtime catalog configures through
+``--chunked-prefill-size`` / ``--max-running-requests`` / ``--mem-frac``):
+  * prefill-priority: when requests are waiting and KV pages are available, the step is a
+    prefill step packing up to ``chunked_prefill_size`` prompt tokens (a long prompt is split
+    into chunks across steps; partially-prefilled requests are continued first);
+  * otherwise a decode step over every decode-ready running request;
+  * if a decode step cannot get a page, the most recently admitted requests are preempted
+    (pages freed, recomputed later) — never a deadlock, never an OOM;
+  * optional mixed steps (``enable_mixed_chunk``): running decodes ride along a prefill step
+    as 1-token rows so prefills never stall decode (lower TPOT at some TTFT cost).
+"""
+from __future__ import annotations
+
+import collections
+from dataclasses import dataclass, field
+
+from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
+from ome_amd.runtime.request import ReqState, Request
+
+
+@dataclass
+class ScheduledChunk:
+    req: Request
+    start: int      # first token index computed this step
+    length: int     # tokens computed this step
+    sample: bool    # last row produces a new token
+
+
+@dataclass
+class StepBatch:
+    mode: str                                   # "prefill" | "decode"
+    chunks: list[ScheduledChunk] = field(default_factory=list)
+
+    @property
+    def reqs(self) -> list[Request]:
+        return [c.req for c in self.chunks]
+
+    @property
+    def num_tokens(self) -> int:
+        return sum(c.length for c in self.chunks)
+
+
+class Scheduler:
+    def __init__(self, pages: PagePool, slots: ReqSlotPool, page_size: int, max_running: int = 256,
+                 chunked_prefill_size: int = 8192, max_context: int = 8192, enable_mixed_chunk: bool = False,
+                 prefix_cache=None):
+        self.pages, self.slots, self.P = pages, slots, page_size
+        self.max_running = max_running
+        self.chunk = chunked_prefill_size
+        self.max_context = max_context
+        self.mixed = enable_mixed_chunk
+        self.prefix_cache = prefix_cache
+        self.waiting: collections.deque[Request] = collections.deque()
+        self.running: list[Request] = []
+        self.num_preemptions = 0
+
+    # ------------------------------------------------------------------ queue ops
+    def add(self, req: Request) -> None:
+        req.state = ReqState.WAITING
+        self.waiting.append(req)
+
+    def abort(self, rid: str) -> Request | None:
+        for q in (self.waiting, self.running):
+            for r in list(q):
+                if r.rid == rid:
+                    q.remove(r)
+                    self._release(r)
+                    r.state, r.finish_reason = ReqState.FINISHED, "abort"
+                    return r
+        return None
+
+    @property
+    def num_waiting(self) -> int:
+        return len(self.waiting)
+
+    @property
+    def num_running(self) -> int:
+        return len(self.running)
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    # ------------------------------------------------------------------ pages
+    def _pages_needed(self, req: Request, upto_tokens: int) -> int:
+        return max(0, -(-upto_tokens // self.P) - len(req.pages))
+
+    def _grow(self, req: Request, upto_tokens: int) -> bool:
+        need = self._pages_needed(req, upto_tokens)
+        if need == 0:
+            return True
+        got = self.pages.alloc(need)
+        if got is None and self.prefix_cache is not None:
+            self.prefix_cache.evict(need - self.pages.num_free)
+            got = self.pages.alloc(need)
+        if got is None:
+            return False
+        start = len(req.pages)
+        req.pages.extend(got)
+        self.slots.set_pages(req.req_slot, start, got)
+        return True
+
+    def _release(self, req: Request, cache_prefix: bool = False) -> None:
+        if req.pages:
+            if cache_prefix and self.prefix_cache is not None:
+                kept = self.prefix_cache.insert(req.all_ids[: req.num_cached], req.pages)
+                rest = [p for p in req.pages if p not in kept]
+                self.pages.free(rest)
+            else:
+                if self.prefix_cache is not None:
+                    self.prefix_cache.release(req.pages)
+                self.pages.free([p for p in req.pages if self.prefix_cache is None or not self.prefix_cache.owns(p)])
+            req.pages = []
+        if req.req_slot >= 0:
+            self.slots.free(req.req_slot)
+            req.req_slot = -1
+
+    def finish(self, req: Request, reason: str) -> None:
+        if req in self.running:
+            self.running.remove(req)
+        req.state, req.finish_reason = ReqState.FINISHED, reason
+        self._release(req, cache_prefix=True)
+
+    def _preempt_one(self, keep: Request | None = None) -> bool:
+        # newest admitted first (LIFO), never the request we are trying to serve
+        for r in reversed(self.running):
+            if r is keep:
+                continue
+            self.running.remove(r)
+            self._release(r)
+            r.num_cached = 0
+            r.num_prefix_hit = 0
+            r.state = ReqState.WAITING
+            r.preempted += 1
+            self.waiting.appendleft(r)
+            self.num_preemptions += 1
+            return True
+        return False
+
+    # ------------------------------------------------------------------ schedule
+    def schedule(self) -> StepBatch | None:
+        batch = self._schedule_prefill()
+        if batch is not None:
+            if self.mixed:
+                self._add_decodes(batch)
+            return batch
+        return self._schedule_decode()
+
+    def _schedule_prefill(self) -> StepBatch | None:
+        budget = self.chunk
+        chunks: list[ScheduledChunk] = []
+        # 1) continue partially prefilled running requests
+        for r in self.running:
+            if budget <= 0:
+                break
+            if r.num_cached < r.seq_len - 1:
+                n = min(r.seq_len - r.num_cached, budget)
+                if not self._grow(r, r.num_cached + n):
+                    break
+                chunks.append(ScheduledChunk(r, r.num_cached, n, r.num_cached + n == r.seq_len))
+                budget -= n
+        # 2) admit new requests
+        while self.waiting and budget > 0 and len(self.running) < self.max_running:
+            r = self.waiting[0]
+            if r.req_slot < 0:
+                slot = self.slots.alloc()
+                if slot is None:
+                    break
+                r.req_slot = slot
+            if self.prefix_cache is not None and r.num_cached == 0 and not r.pages:
+                hit_pages = self.prefix_cache.match(r.all_ids[: r.seq_len - 1])
+                if hit_pages:
+                    r.pages = list(hit_pages)
+                    self.slots.set_pages(r.req_slot, 0, hit_pages)
+                    r.num_cached = r.num_prefix_hit = len(hit_pages) * self.P
+            n = min(r.seq_len - r.num_cached, budget)
+            if not self._grow(r, r.num_cached + n):
+                if not self.running and not chunks:
+                    # cannot fit even alone: fail the request instead of spinning
+                    self.waiting.popleft()
+                    self._release(r)
+                    r.state, r.finish_reason = ReqState.FINISHED, "abort:kv_capacity"
+                    continue
+                break
+            self.waiting.popleft()
+            r.state = ReqState.RUNNING
+            self.running.append(r)
+            chunks.append(ScheduledChunk(r, r.num_cached, n, r.num_cached + n == r.seq_len))
+            budget -= n
+        return StepBatch("prefill", chunks) if chunks else None
+
+    def _add_decodes(self, batch: StepBatch) -> None:
+        inb = {id(c.req) for c in batch.chunks}
+        for r in self.running:
+            if id(r) in inb or not r.prefill_done:
+                continue
+            if self._grow(r, r.seq_len):
+                batch.chunks.append(ScheduledChunk(r, r.seq_len - 1, 1, True))
+
+    def _schedule_decode(self) -> StepBatch | None:
+        chunks = []
+        for r in list(self.running):
+            if r.state != ReqState.RUNNING or not r.prefill_done:
+                continue
+            while not self._grow(r, r.seq_len):
+                if not self._preempt_one(keep=r):
+                    break
+            if r.state != ReqState.RUNNING or len(r.pages) * self.P < r.seq_len:
+                continue
+            chunks.append(ScheduledChunk(r, r.seq_len - 1, 1, True))
+        return StepBatch("decode", chunks) if chunks else None
+
+    # ------------------------------------------------------------------ post-step
+    def commit(self, batch: StepBatch, next_ids: list[int], logprobs: list[float] | None, now: float,
+               eos_ids: set[int]) -> list[Request]:
+        """Apply a finished step; returns requests that finished in it."""
+        done = []
+        for i, c in enumerate(batch.chunks):
+            r = c.req
+            r.num_cached = c.start + c.length
+            if not c.sample or r.state != ReqState.RUNNING:
+                continue
+            tok = int(next_ids[i])
+            r.output_ids.append(tok)
+            if logprobs is not None:
+                r.output_logprobs.append(float(logprobs[i]))
+            r.token_times.append(now)
+            if r.first_token_time is None:
+                r.first_token_time = now
+            reason = None
+            p = r.params
+            if len(r.output_ids) >= p.max_new_tokens:
+                reason = "length"
+            elif not p.ignore_eos and (tok in eos_ids or tok in p.stop_token_ids):
+                reason = "stop"
+            elif r.seq_len >= self.max_context:
+                reason = "length"
+            if reason:
+                self.finish(r, reason)
+                done.append(r)
+            if r.on_token is not None:
+                r.on_token(r, [tok], reason is not None)
+        return done

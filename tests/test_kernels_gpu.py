@@ -1,0 +1,198 @@
+"""Numerics of every hand-written gfx950 kernel vs the plain-PyTorch fp32 reference of the same op."""
+import math
+import random
+
+import pytest
+import torch
+
+from ome_amd import ops
+from ome_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, atol=2e-2, rtol=2e-2):
+    a, b = a.float().cpu(), b.float().cpu()
+    err = (a - b).abs().max().item()
+    assert torch.allclose(a, b, atol=atol, rtol=rtol), f"max abs err {err}"
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+    random.seed(0)
+
+
+def test_native_library_loaded():
+    assert ops.available(), "libome_kernels.so must be built and loadable on the GPU box"
+
+
+@pytest.mark.parametrize("rows,H", [(1, 4096), (7, 4096), (600, 4096), (3, 8192), (5, 7168), (2, 256)])
+def test_rmsnorm(rows, H):
+    x = torch.randn(rows, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    _close(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x, w, 1e-5))
+
+
+@pytest.mark.parametrize("rows,H", [(1, 4096), (600, 4096), (5, 7168)])
+def test_fused_add_rmsnorm(rows, H):
+    x = torch.randn(rows, H, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(rows, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(H, device=DEV, dtype=torch.bfloat16)
+    x2, r2 = x.clone(), r.clone()
+    ops.fused_add_rmsnorm(x, r, w, 1e-5)
+    ref.fused_add_rmsnorm(x2, r2, w, 1e-5)
+    _close(r, r2, atol=1e-2)
+    _close(x, x2)
+
+
+def _cache(pages, Hkv, D, P=16):
+    k = torch.randn(pages, Hkv, P, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(pages, Hkv, D, P, device=DEV, dtype=torch.bfloat16)
+    return k, v
+
+
+@pytest.mark.parametrize("qk_norm", [False, True])
+@pytest.mark.parametrize("Hq,Hkv,rot", [(32, 8, 128), (8, 1, 128), (4, 2, 64)])
+def test_rope_qkv_cache(Hq, Hkv, rot, qk_norm):
+    from ome_amd.models.config import preset, rope_cos_sin
+
+    D, T, P = 128, 37, 16
+    cfg = preset("llama-3.1-8b")
+    cfg.head_dim, cfg.partial_rotary_factor = D, rot / D
+    cs = rope_cos_sin(cfg, 4096, device=DEV)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(40 * P, device=DEV)[:T].to(torch.int32)
+    slots[3] = -1
+    qn = torch.randn(D, device=DEV, dtype=torch.bfloat16) if qk_norm else None
+    kn = torch.randn(D, device=DEV, dtype=torch.bfloat16) if qk_norm else None
+    k1, v1 = _cache(40, Hkv, D)
+    k2, v2 = k1.clone(), v1.clone()
+    q1 = torch.empty(T, Hq, D, device=DEV, dtype=torch.bfloat16)
+    q2 = torch.empty_like(q1)
+    ops.rope_qkv_cache(qkv, pos, cs, rot, q1, k1, v1, slots, Hq, Hkv, D, True, qn, kn, 1e-6)
+    ref.rope_qkv_cache(qkv, pos, cs, rot, q2, k2, v2, slots, Hq, Hkv, D, P, True, qn, kn, 1e-6)
+    _close(q1, q2, atol=3e-2)
+    _close(k1, k2, atol=3e-2)
+    assert torch.equal(v1, v2)
+
+
+def test_act_and_mul():
+    x = torch.randn(33, 2 * 14336, device=DEV, dtype=torch.bfloat16)
+    _close(ops.act_and_mul(x, 0), ref.act_and_mul(x, 0))
+    _close(ops.act_and_mul(x, 1), ref.act_and_mul(x, 1))
+
+
+def test_embedding_vocab_parallel():
+    table = torch.randn(1000, 512, device=DEV, dtype=torch.bfloat16)
+    ids = torch.randint(0, 3000, (77,), device=DEV, dtype=torch.int32)
+    assert torch.equal(ops.embedding(ids, table, 1000, 2000), ref.embedding(ids, table, 1000, 2000))
+
+
+def _block_tables(seq_lens, P, num_pages):
+    perm = torch.randperm(num_pages - 1)[: sum(-(-L // P) for L in seq_lens) + 1] + 1
+    mx = max(-(-L // P) for L in seq_lens) + 1
+    bt = torch.zeros(len(seq_lens), mx, dtype=torch.int32)
+    o = 0
+    for i, L in enumerate(seq_lens):
+        n = -(-L // P)
+        bt[i, :n] = perm[o:o + n]
+        o += n
+    return bt.to(DEV)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16)])
+@pytest.mark.parametrize("seq_lens", [[1], [15, 16, 17, 33], [100, 1000, 3, 517], [5000, 7]])
+@pytest.mark.parametrize("part_size", [256, 8192])
+def test_paged_decode(Hq, Hkv, seq_lens, part_size):
+    D, P = 128, 16
+    npages = sum(-(-L // P) for L in seq_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    bt = _block_tables(seq_lens, P, npages)
+    sl = torch.tensor(seq_lens, dtype=torch.int32, device=DEV)
+    q = torch.randn(len(seq_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    ws = ops.DecodeWorkspace(len(seq_lens), Hq, D, 8192, part_size, DEV)
+    scale = 1 / math.sqrt(D)
+    out = ops.paged_decode(q, kc, vc, bt, sl, scale, ws)
+    _close(out, ref.paged_decode(q, kc, vc, bt, sl, scale), atol=2e-2)
+
+
+def test_paged_decode_window():
+    D, P, Hq, Hkv = 128, 16, 32, 8
+    seq_lens = [700, 40]
+    kc, vc = _cache(64, Hkv, D)
+    bt = _block_tables(seq_lens, P, 64)
+    sl = torch.tensor(seq_lens, dtype=torch.int32, device=DEV)
+    q = torch.randn(2, Hq, D, device=DEV, dtype=torch.bfloat16)
+    ws = ops.DecodeWorkspace(2, Hq, D, 1024, 256, DEV)
+    out = ops.paged_decode(q, kc, vc, bt, sl, 0.088, ws, window=128)
+    _close(out, ref.paged_decode(q, kc, vc, bt, sl, 0.088, window=128))
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 1)])
+@pytest.mark.parametrize("q_lens,kv_lens", [([5], [5]), ([37, 64, 1, 100], [37, 80, 300, 100]),
+                                            ([300], [1000]), ([1, 1, 1], [20, 33, 16])])
+def test_paged_prefill(Hq, Hkv, q_lens, kv_lens):
+    D, P = 128, 16
+    npages = sum(-(-L // P) for L in kv_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    bt = _block_tables(kv_lens, P, npages)
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    items = torch.tensor(ops.prefill_work_items(q_lens, kv_lens), dtype=torch.int32, device=DEV)
+    q = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    out = ops.paged_prefill(q, kc, vc, bt, cu, kl, items, 0.0884)
+    _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884), atol=2e-2)
+
+
+def test_paged_prefill_window():
+    D, P, Hq, Hkv = 128, 16, 32, 8
+    q_lens, kv_lens = [200, 50], [500, 50]
+    kc, vc = _cache(64, Hkv, D)
+    bt = _block_tables(kv_lens, P, 64)
+    cu = torch.tensor([0, 200, 250], dtype=torch.int32, device=DEV)
+    kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    items = torch.tensor(ops.prefill_work_items(q_lens, kv_lens), dtype=torch.int32, device=DEV)
+    q = torch.randn(250, Hq, D, device=DEV, dtype=torch.bfloat16)
+    out = ops.paged_prefill(q, kc, vc, bt, cu, kl, items, 0.0884, window=100)
+    _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884, window=100))
+
+
+def test_sample_greedy_and_filters():
+    B, V = 9, 128256
+    logits = torch.randn(B, V, device=DEV, dtype=torch.bfloat16) * 3
+    am = logits.float().argmax(-1)
+    ids, lp = ops.sample(logits)
+    assert torch.equal(ids.long().cpu(), am.cpu())
+    t = torch.ones(B, device=DEV)
+    k1 = torch.ones(B, dtype=torch.int32, device=DEV)
+    ids, _ = ops.sample(logits, t, k1, None, None, torch.arange(B, device=DEV, dtype=torch.int64))
+    assert torch.equal(ids.long().cpu(), am.cpu())  # top-k=1 == greedy
+    tp = torch.full((B,), 1e-6, device=DEV)
+    ids, _ = ops.sample(logits, t, None, tp, None, torch.arange(B, device=DEV, dtype=torch.int64))
+    assert torch.equal(ids.long().cpu(), am.cpu())  # tiny top-p == greedy
+    ref_lp = torch.log_softmax(logits.float(), -1).gather(1, am[:, None])[:, 0]
+    _, lp = ops.sample(logits)
+    _close(lp, ref_lp, atol=1e-2)
+
+
+def test_sample_distribution():
+    V = 16
+    logits = torch.log(torch.tensor([0.5, 0.25, 0.125, 0.125] + [1e-9] * (V - 4), device=DEV)).repeat(4096, 1)
+    t = torch.ones(4096, device=DEV)
+    seeds = torch.arange(4096, device=DEV, dtype=torch.int64) * 7919
+    ids, _ = ops.sample(logits.float(), t, None, None, None, seeds)
+    freq = torch.bincount(ids.long().cpu(), minlength=V).float() / 4096
+    assert abs(freq[0] - 0.5) < 0.05 and abs(freq[1] - 0.25) < 0.05
+    tk = torch.full((4096,), 2, dtype=torch.int32, device=DEV)
+    ids, _ = ops.sample(logits.float(), t, tk, None, None, seeds)
+    assert int(ids.max()) <= 1
+
+
+def test_pool():
+    h = torch.randn(50, 256, device=DEV, dtype=torch.bfloat16)
+    cu = torch.tensor([0, 10, 50], dtype=torch.int32, device=DEV)
+    _close(ops.pool(h, cu, 0, True), ref.pool(h, cu, 0, True), atol=1e-3)
+    _close(ops.pool(h, cu, 1, True), ref.pool(h, cu, 1, True), atol=1e-3)

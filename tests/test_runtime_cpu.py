@@ -1,0 +1,139 @@
+"""Runtime (scheduler / paged KV / prefix cache / engine) on CPU with the reference ops."""
+import random
+
+import pytest
+import torch
+
+from ome_amd.bench.scenarios import Scenario, validate
+from ome_amd.models.config import ModelConfig, preset, rope_cos_sin
+from ome_amd.ops import reference as ref
+from ome_amd.runtime.engine import Engine, EngineArgs
+from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
+from ome_amd.runtime.prefix_cache import PrefixCache
+from ome_amd.runtime.request import Request, SamplingParams
+from ome_amd.runtime.scheduler import Scheduler
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return Engine(EngineArgs(model="tiny-llama", device="cpu", max_running_requests=8, chunked_prefill_size=48,
+                             context_length=512))
+
+
+def test_engine_generates(eng):
+    reqs = eng.generate([[5, 6, 7], list(range(3, 90))], SamplingParams(max_new_tokens=5, ignore_eos=True))
+    assert [len(r.output_ids) for r in reqs] == [5, 5]
+    assert all(r.ttft is not None and r.ttft >= 0 for r in reqs)
+
+
+def test_chunked_prefill_equivalence():
+    """Chunk size must not change greedy outputs (same math, different batching)."""
+    prompts = [list(range(10, 10 + n)) for n in (30, 70, 5)]
+    outs = []
+    for chunk in (16, 512):
+        e = Engine(EngineArgs(model="tiny-llama", device="cpu", max_running_requests=8, chunked_prefill_size=chunk,
+                              context_length=512, disable_radix_cache=True))
+        outs.append([r.output_ids for r in e.generate(prompts, SamplingParams(max_new_tokens=6, ignore_eos=True))])
+    assert outs[0] == outs[1]
+
+
+def test_prefix_cache_hits_and_determinism(eng):
+    p = list(range(200, 260))
+    a = eng.generate([p], SamplingParams(max_new_tokens=4, ignore_eos=True))[0]
+    b = eng.generate([p], SamplingParams(max_new_tokens=4, ignore_eos=True))[0]
+    assert b.num_prefix_hit == 48 and a.output_ids == b.output_ids
+
+
+def test_decode_matches_full_recompute():
+    e = Engine(EngineArgs(model="tiny-llama", device="cpu", max_running_requests=4, context_length=256,
+                          disable_radix_cache=True))
+    r = e.generate([[9, 8, 7, 6]], SamplingParams(max_new_tokens=6, ignore_eos=True))[0]
+    r2 = e.generate([r.prompt_ids + r.output_ids[:-1]], SamplingParams(max_new_tokens=1, ignore_eos=True))[0]
+    assert r2.output_ids[0] == r.output_ids[-1]
+
+
+def test_preemption_under_kv_pressure():
+    pages, slots = PagePool(12), ReqSlotPool(9, 64)
+    s = Scheduler(pages, slots, 16, max_running=8, chunked_prefill_size=1000, max_context=1000)
+    reqs = [Request(prompt_ids=list(range(40)), params=SamplingParams(max_new_tokens=200)) for _ in range(3)]
+    for r in reqs:
+        s.add(r)
+    b = s.schedule()
+    assert b.mode == "prefill" and len(b.chunks) == 3  # 3 x 3 pages = 9 of 11
+    s.commit(b, [1, 1, 1], None, 0.0, set())
+    steps = 0
+    while s.num_running and steps < 100:
+        b = s.schedule()
+        if b is None:
+            break
+        s.commit(b, [1] * len(b.chunks), None, 0.0, set())
+        steps += 1
+    assert s.num_preemptions >= 1
+    assert pages.num_free + sum(len(r.pages) for r in s.running) == 11
+
+
+def test_stop_conditions():
+    pages, slots = PagePool(100), ReqSlotPool(9, 64)
+    s = Scheduler(pages, slots, 16, max_running=8, chunked_prefill_size=1000, max_context=1000)
+    r = Request(prompt_ids=[1, 2, 3], params=SamplingParams(max_new_tokens=10))
+    s.add(r)
+    b = s.schedule()
+    done = s.commit(b, [2], None, 0.0, eos_ids={2})
+    assert done == [r] and r.finish_reason == "stop" and pages.num_free == 99
+
+
+def test_prefix_cache_unit():
+    pool = PagePool(20)
+    pc = PrefixCache(pool, 4)
+    toks = list(range(12))
+    pages = pool.alloc(3)
+    kept = pc.insert(toks, pages)
+    assert kept == set(pages)
+    assert pc.match(toks[:11]) == pages[:2]
+    pc.release(pages[:2])
+    assert pc.evict(5) == 3 and pc.num_pages == 0
+
+
+def test_scenarios():
+    rng = random.Random(0)
+    for s in ["N(480,240)/(300,150)", "D(100,100)", "U(10,20)/(5,6)", "E(128)", "I(512,512)"]:
+        i, o = Scenario.parse(s).sample(rng)
+        assert i >= 1
+    assert validate("D(100,100)") and not validate("E(64)", "text-to-text")
+    assert not validate("D(100,100)junk")
+    with pytest.raises(ValueError):
+        Scenario.parse("X(1)")
+
+
+def test_rope_llama3_scaling_matches_hf_formula():
+    cfg = preset("llama-3.1-8b")
+    cs = rope_cos_sin(cfg, 16)
+    assert cs.shape == (16, 128)
+    assert torch.allclose(cs[0, :64], torch.ones(64))
+
+
+def test_model_config_from_reference_fixtures():
+    import json
+    import os
+
+    fx = "/root/reference/pkg/hfutil/modelconfig/testdata"
+    if not os.path.isdir(fx):
+        pytest.skip("reference fixtures not mounted")
+    c = ModelConfig.from_hf(json.load(open(f"{fx}/llama3.json")))
+    assert (c.hidden_size, c.num_layers, c.num_kv_heads) == (8192, 80, 8)
+    d = ModelConfig.from_hf(json.load(open(f"{fx}/deepseek_v3.json")))
+    assert d.is_moe and d.is_mla and d.num_experts == 256 and d.num_experts_per_tok == 8
+
+
+def test_reference_attention_consistency():
+    """paged_prefill with q_len==1 rows equals paged_decode."""
+    torch.manual_seed(0)
+    Hq, Hkv, D, P = 8, 2, 128, 16
+    kc = torch.randn(10, Hkv, P, D, dtype=torch.bfloat16)
+    vc = torch.randn(10, Hkv, D, P, dtype=torch.bfloat16)
+    bt = torch.tensor([[1, 2, 3], [4, 5, 6]], dtype=torch.int32)
+    sl = torch.tensor([40, 17], dtype=torch.int32)
+    q = torch.randn(2, Hq, D, dtype=torch.bfloat16)
+    a = ref.paged_decode(q, kc, vc, bt, sl, 0.1)
+    b = ref.paged_prefill(q, kc, vc, bt, torch.tensor([0, 1, 2]), sl, 0.1)
+    assert torch.allclose(a.float(), b.float(), atol=1e-2)
