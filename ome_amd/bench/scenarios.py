@@ -22,7 +22,7 @@ PATTERNS = {
     "D": re.compile(r"^D\((\d+),(\d+)\)$"),
     "U2": re.compile(r"^U\((\d+),(\d+)\)/\((\d+),(\d+)\)$"),
     "U1": re.compile(r"^U\((\d+),(\d+)\)$"),
-    "E": re.compile(r"^E\((\d+)\)$"),
+    "E": re.compile(r"^E\((\d+)(?:,(\d+))?\)$"),
     "I": re.compile(r"^I\((\d+),(\d+)(?:,(\d+))?\)$"),
 }
 
@@ -30,6 +30,7 @@ TASK_SCENARIOS = {
     "text-to-text": ("N", "D", "U2", "U1"),
     "text-to-embeddings": ("E",),
     "image-text-to-text": ("I",),
+    "image-to-text": ("I",),
     "image-to-embeddings": ("I",),
     "text-to-rerank": ("E",),
 }
@@ -38,6 +39,7 @@ DEFAULT_SCENARIOS = {
     "text-to-text": ["N(480,240)/(300,150)", "D(100,100)", "D(100,1000)", "D(2000,200)", "D(7800,200)"],
     "text-to-embeddings": ["E(64)", "E(128)", "E(256)", "E(512)", "E(1024)"],
     "image-text-to-text": ["I(512,512)", "I(1024,512)", "I(2048,2048)"],
+    "image-to-text": ["I(512,512)", "I(1024,512)", "I(2048,2048)"],
     "image-to-embeddings": ["I(512,512)", "I(1024,512)", "I(2048,2048)"],
     "text-to-rerank": ["E(64)", "E(128)"],
 }

@@ -11,6 +11,7 @@ from __future__ import annotations
 import logging
 import math
 import time
+import zlib
 
 import numpy as np
 import torch
@@ -170,7 +171,8 @@ class ModelRunner:
 
     @staticmethod
     def _seed(req, pos: int) -> int:
-        base = req.params.seed if req.params.seed is not None else hash(req.rid) & _MASK64
+        # stable across processes (TP ranks must draw identical tokens): no str hash()
+        base = req.params.seed if req.params.seed is not None else zlib.crc32(req.rid.encode())
         return _mix((base * 1000003 + pos) & _MASK64)
 
     # ------------------------------------------------------------------ steps

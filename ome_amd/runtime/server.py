@@ -1,0 +1,405 @@
+"""OpenAI-compatible HTTP server of the first-party runtime (the engine container of an ISVC).
+
+Endpoints (the contract the reference's runtime catalog and probes rely on,
+``config/runtimes/srt/meta/llama-3-8b-instruct-rt.yaml:76-102``): ``/v1/chat/completions``,
+``/v1/completions``, ``/v1/embeddings``, ``/v1/models``, ``/generate``, ``/health``,
+``/health_generate`` (a real 1-token generation), ``/metrics`` (SGLang + vLLM metric names),
+``/get_model_info``, ``/get_server_info``; plus the PD-disaggregation KV bootstrap routes.
+
+CLI flags follow SGLang's names so ServingRuntime YAML and the operator's TP/PP rewrite
+keep working: ``--model-path --served-model-name --tp-size --pp-size --dp-size --mem-frac
+--context-length --chunked-prefill-size --page-size --max-running-requests --port --host
+--enable-metrics --is-embedding --disable-radix-cache --disable-cuda-graph --cuda-graph-max-bs
+--dist-init-addr --nnodes --node-rank --disaggregation-mode ...``; unknown flags are logged and
+ignored.  Tensor parallelism: one process per GPU (rank 0 serves HTTP, other ranks run the
+engine loop in lockstep), torch.distributed over RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import sys
+import threading
+import time
+import uuid
+
+from fastapi import Request  # noqa: E402  (module level: FastAPI resolves string annotations here)
+
+log = logging.getLogger("ome_amd.server")
+
+
+def build_parser() -> argparse.ArgumentParser:
+    ap = argparse.ArgumentParser("ome_amd.runtime.server")
+    a = ap.add_argument
+    a("--model-path", "--model", dest="model_path", default=os.environ.get("MODEL_PATH"))
+    a("--model-preset", default=None, help="random-init architecture preset when model-path has no config")
+    a("--served-model-name", default=os.environ.get("SERVED_MODEL_NAME"))
+    a("--tp-size", "--tp", "--tensor-parallel-size", dest="tp_size", type=int, default=1)
+    a("--pp-size", "--pp", "--pipeline-parallel-size", dest="pp_size", type=int, default=1)
+    a("--dp-size", "--dp", "--data-parallel-size", dest="dp_size", type=int, default=1)
+    a("--mem-frac", "--mem-fraction-static", "--gpu-memory-utilization", dest="mem_frac", type=float, default=0.88)
+    a("--context-length", "--max-model-len", dest="context_length", type=int, default=None)
+    a("--chunked-prefill-size", type=int, default=8192)
+    a("--page-size", type=int, default=16)
+    a("--max-running-requests", "--max-num-seqs", dest="max_running_requests", type=int, default=256)
+    a("--max-total-tokens", type=int, default=None)
+    a("--host", default="0.0.0.0")
+    a("--port", type=int, default=8080)
+    a("--enable-metrics", action="store_true")
+    a("--is-embedding", action="store_true")
+    a("--disable-radix-cache", action="store_true")
+    a("--disable-cuda-graph", action="store_true")
+    a("--cuda-graph-max-bs", type=int, default=None)
+    a("--enable-mixed-chunk", action="store_true")
+    a("--load-format", default="auto")
+    a("--dtype", default="bfloat16")
+    a("--kv-cache-dtype", default="auto")
+    a("--random-seed", type=int, default=0)
+    a("--device", default="cuda")
+    a("--dist-init-addr", "--nccl-init", dest="dist_init_addr", default=None)
+    a("--nnodes", type=int, default=1)
+    a("--node-rank", type=int, default=0)
+    a("--disaggregation-mode", default="null", choices=["null", "prefill", "decode"])
+    a("--disaggregation-bootstrap-port", type=int, default=8998)
+    a("--log-requests", action="store_true")
+    a("--num-layers", type=int, default=None, help="debug: truncate the model")
+    return ap
+
+
+def engine_args_from(ns, rank_tp: int | None = None):
+    from ome_amd.runtime.engine import EngineArgs
+
+    mp = ns.model_path
+    preset = ns.model_preset
+    load_fmt = ns.load_format
+    if mp and mp.startswith("random://"):
+        preset, mp, load_fmt = mp[len("random://"):].split("?")[0], None, "dummy"
+    elif mp and not os.path.exists(os.path.join(mp, "config.json")) and preset is None:
+        # a model directory without a config (synthetic benchmark nodes): fall back to a preset
+        preset = os.environ.get("OME_MODEL_PRESET", "llama-3-8b")
+    return EngineArgs(model_path=mp, model=preset, served_model_name=ns.served_model_name, tp_size=ns.tp_size,
+                      pp_size=ns.pp_size, dp_size=ns.dp_size, mem_fraction_static=ns.mem_frac,
+                      max_running_requests=ns.max_running_requests, max_total_tokens=ns.max_total_tokens,
+                      chunked_prefill_size=ns.chunked_prefill_size, context_length=ns.context_length,
+                      page_size=ns.page_size, cuda_graph=not ns.disable_cuda_graph,
+                      cuda_graph_max_bs=ns.cuda_graph_max_bs, load_format=load_fmt, dtype=ns.dtype,
+                      device=ns.device, seed=ns.random_seed, enable_mixed_chunk=ns.enable_mixed_chunk,
+                      disable_radix_cache=ns.disable_radix_cache, is_embedding=ns.is_embedding,
+                      kv_cache_dtype=ns.kv_cache_dtype, dist_init_addr=ns.dist_init_addr, nnodes=ns.nnodes,
+                      node_rank=ns.node_rank, disaggregation_mode=ns.disaggregation_mode,
+                      num_layers_override=ns.num_layers)
+
+
+# ------------------------------------------------------------------ request plumbing
+class _Stream:
+    """Thread-safe bridge: engine thread -> asyncio queue of (new_token_ids, finished)."""
+
+    def __init__(self, loop):
+        self.loop = loop
+        self.q: asyncio.Queue = asyncio.Queue()
+
+    def __call__(self, req, toks, finished):
+        self.loop.call_soon_threadsafe(self.q.put_nowait, (list(toks), finished))
+
+
+def _sampling_from(body: dict, default_max: int):
+    from ome_amd.runtime.request import SamplingParams
+
+    stop = body.get("stop")
+    if isinstance(stop, str):
+        stop = [stop]
+    max_tokens = body.get("max_completion_tokens") or body.get("max_tokens") or body.get("max_new_tokens")
+    return SamplingParams(
+        max_new_tokens=int(max_tokens) if max_tokens is not None else default_max,
+        temperature=float(body.get("temperature", 1.0) if body.get("temperature") is not None else 1.0),
+        top_p=float(body.get("top_p") or 1.0), top_k=int(body.get("top_k") or -1),
+        min_p=float(body.get("min_p") or 0.0), stop=list(stop or []),
+        stop_token_ids=list(body.get("stop_token_ids") or []), ignore_eos=bool(body.get("ignore_eos", False)),
+        seed=body.get("seed"), presence_penalty=float(body.get("presence_penalty") or 0.0),
+        frequency_penalty=float(body.get("frequency_penalty") or 0.0),
+        repetition_penalty=float(body.get("repetition_penalty") or 1.0), logprobs=bool(body.get("logprobs")),
+        n=int(body.get("n") or 1))
+
+
+def create_app(engine, ns=None):
+    from fastapi import FastAPI
+    from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+
+    app = FastAPI(title="ome_amd runtime")
+    tok = engine.tokenizer
+    model_name = engine.served_model_name
+    created = int(time.time())
+    default_max = 128
+    app.state.engine = engine
+
+    def err(code: int, msg: str, typ: str = "invalid_request_error"):
+        return JSONResponse({"error": {"message": msg, "type": typ, "code": code}}, status_code=code)
+
+    async def run_request(prompt_ids, params):
+        loop = asyncio.get_running_loop()
+        stream = _Stream(loop)
+        req = engine.make_request(prompt_ids, params, on_token=stream)
+        engine.add_request(req)
+        return req, stream
+
+    @app.get("/health")
+    async def health():
+        return {"status": "ok", **engine.health()}
+
+    @app.get("/health_generate")
+    async def health_generate():
+        from ome_amd.runtime.request import SamplingParams
+
+        try:
+            req, stream = await run_request([tok.bos_token_id or 1, 3 + 72, 3 + 105], SamplingParams(max_new_tokens=1))
+            while True:
+                _, fin = await asyncio.wait_for(stream.q.get(), timeout=120)
+                if fin:
+                    break
+            if req.finish_reason and req.finish_reason.startswith("abort"):
+                return err(503, f"generation failed: {req.finish_reason}", "service_unavailable")
+            return {"status": "ok"}
+        except asyncio.TimeoutError:
+            return err(503, "health generation timed out", "service_unavailable")
+
+    @app.get("/v1/models")
+    async def models():
+        return {"object": "list", "data": [{"id": model_name, "object": "model", "created": created,
+                                            "owned_by": "ome_amd", "max_model_len": engine.max_context}]}
+
+    @app.get("/get_model_info")
+    async def model_info():
+        c = engine.cfg
+        return {"model_path": engine.args.model_path, "served_model_name": model_name,
+                "architecture": c.architecture, "is_generation": not c.is_embedding,
+                "num_layers": c.num_layers, "hidden_size": c.hidden_size, "vocab_size": c.vocab_size,
+                "context_length": engine.max_context}
+
+    @app.get("/get_server_info")
+    async def server_info():
+        a = engine.args
+        return {"tp_size": a.tp_size, "pp_size": a.pp_size, "page_size": a.page_size,
+                "max_running_requests": a.max_running_requests, "chunked_prefill_size": a.chunked_prefill_size,
+                "kv_pages": engine.runner.kv.num_pages, "cuda_graph_buckets": engine.runner.buckets,
+                "disaggregation_mode": a.disaggregation_mode, **engine.health()}
+
+    @app.get("/metrics")
+    async def metrics():
+        engine.metrics.model_name = model_name
+        return PlainTextResponse(engine.metrics.render(), media_type="text/plain; version=0.0.4")
+
+    def _encode(body: dict, chat: bool):
+        if chat:
+            msgs = body.get("messages")
+            if not isinstance(msgs, list) or not msgs:
+                raise ValueError("messages must be a non-empty list")
+            text = tok.apply_chat_template(msgs, add_generation_prompt=True)
+            return tok.encode(text)
+        p = body.get("prompt", body.get("text"))
+        if isinstance(p, list) and p and isinstance(p[0], int):
+            return list(p)
+        if isinstance(p, list):
+            p = p[0] if p else ""
+        if body.get("input_ids"):
+            return list(body["input_ids"])
+        if not isinstance(p, str):
+            raise ValueError("prompt must be a string or a list of token ids")
+        return tok.encode(p)
+
+    def _stop_hit(text: str, stops: list[str]) -> int | None:
+        idx = [text.find(s) for s in stops if s and s in text]
+        return min(idx) if idx else None
+
+    async def _complete(body: dict, chat: bool):
+        try:
+            ids = _encode(body, chat)
+            params = _sampling_from(body, default_max)
+            req, stream = await run_request(ids, params)
+        except ValueError as e:
+            return err(400, str(e))
+        rid = f"{'chatcmpl' if chat else 'cmpl'}-{uuid.uuid4().hex[:24]}"
+        obj = "chat.completion" if chat else "text_completion"
+        stops = params.stop
+
+        def usage():
+            return {"prompt_tokens": len(ids), "completion_tokens": len(req.output_ids),
+                    "total_tokens": len(ids) + len(req.output_ids)}
+
+        if body.get("stream"):
+            async def gen():
+                sent = ""
+                first = True
+                while True:
+                    toks, fin = await stream.q.get()
+                    text = tok.decode(req.output_ids)
+                    cut = _stop_hit(text, stops)
+                    if cut is not None:
+                        text, fin = text[:cut], True
+                        engine.abort(req.rid)
+                    delta = text[len(sent):]
+                    sent = text
+                    if chat:
+                        d = {"content": delta}
+                        if first:
+                            d["role"] = "assistant"
+                        choice = {"index": 0, "delta": d, "finish_reason": None}
+                        chunk_obj = "chat.completion.chunk"
+                    else:
+                        choice = {"index": 0, "text": delta, "finish_reason": None}
+                        chunk_obj = "text_completion"
+                    first = False
+                    if fin:
+                        choice["finish_reason"] = "stop" if cut is not None else _finish(req)
+                    out = {"id": rid, "object": chunk_obj, "created": int(time.time()), "model": model_name,
+                           "choices": [choice]}
+                    if fin and (body.get("stream_options") or {}).get("include_usage", True):
+                        out["usage"] = usage()
+                    yield f"data: {json.dumps(out)}\n\n"
+                    if fin:
+                        break
+                yield "data: [DONE]\n\n"
+
+            return StreamingResponse(gen(), media_type="text/event-stream")
+        while True:
+            _, fin = await stream.q.get()
+            if stops:
+                cut = _stop_hit(tok.decode(req.output_ids), stops)
+                if cut is not None:
+                    engine.abort(req.rid)
+                    break
+            if fin:
+                break
+        text = tok.decode(req.output_ids)
+        cut = _stop_hit(text, stops)
+        reason = _finish(req)
+        if cut is not None:
+            text, reason = text[:cut], "stop"
+        if chat:
+            choice = {"index": 0, "message": {"role": "assistant", "content": text}, "finish_reason": reason}
+        else:
+            choice = {"index": 0, "text": text, "finish_reason": reason, "logprobs": None}
+        if params.logprobs:
+            choice["logprobs"] = {"token_logprobs": req.output_logprobs, "tokens": req.output_ids}
+        return {"id": rid, "object": obj, "created": int(time.time()), "model": model_name, "choices": [choice],
+                "usage": usage()}
+
+    def _finish(req):
+        r = req.finish_reason or "stop"
+        return "length" if r == "length" else ("stop" if not r.startswith("abort") else "abort")
+
+    @app.post("/v1/chat/completions")
+    async def chat(request: Request):
+        return await _complete(await request.json(), True)
+
+    @app.post("/v1/completions")
+    async def completions(request: Request):
+        return await _complete(await request.json(), False)
+
+    @app.post("/generate")
+    async def generate(request: Request):
+        body = await request.json()
+        sp = body.get("sampling_params") or {}
+        merged = {**sp, "prompt": body.get("text"), "input_ids": body.get("input_ids"),
+                  "max_tokens": sp.get("max_new_tokens"), "stream": body.get("stream", False)}
+        res = await _complete(merged, False)
+        if isinstance(res, dict):
+            c = res["choices"][0]
+            return {"text": c["text"], "meta_info": {"finish_reason": c["finish_reason"], **res["usage"]}}
+        return res
+
+    @app.post("/v1/embeddings")
+    async def embeddings(request: Request):
+        body = await request.json()
+        inp = body.get("input")
+        items = inp if isinstance(inp, list) and (not inp or not isinstance(inp[0], int)) else [inp]
+        out, total = [], 0
+        from ome_amd.runtime.request import SamplingParams
+
+        for i, x in enumerate(items):
+            ids = list(x) if isinstance(x, list) else tok.encode(str(x))
+            total += len(ids)
+            req, stream = await run_request(ids, SamplingParams(max_new_tokens=0))
+            req.is_embedding = True
+            while True:
+                _, fin = await stream.q.get()
+                if fin:
+                    break
+            out.append({"object": "embedding", "index": i, "embedding": req.embedding or []})
+        return {"object": "list", "data": out, "model": model_name,
+                "usage": {"prompt_tokens": total, "total_tokens": total}}
+
+    if getattr(engine, "kv_transfer", None) is not None:
+        engine.kv_transfer.mount(app)
+    return app
+
+
+def _worker_main(rank: int, world: int, ns_dict: dict, addr: str, local_rank: int) -> None:
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(local_rank)})
+    ns = argparse.Namespace(**ns_dict)
+    ns.dist_init_addr = addr
+    from ome_amd.runtime.engine import Engine
+
+    eng = Engine(engine_args_from(ns))
+    eng.run_forever()
+
+
+def main(argv=None) -> int:
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    ap = build_parser()
+    ns, unknown = ap.parse_known_args(argv)
+    if unknown:
+        log.warning("ignoring unsupported flags: %s", " ".join(unknown))
+    world = ns.tp_size * ns.pp_size
+    per_node = max(1, world // max(1, ns.nnodes))
+    base_rank = ns.node_rank * per_node
+    procs = []
+    if world > 1:
+        import multiprocessing as mp
+
+        addr = ns.dist_init_addr or f"127.0.0.1:{29500 + (os.getpid() % 1000)}"
+        ns.dist_init_addr = addr
+        ctx = mp.get_context("spawn")
+        for i in range(1, per_node):
+            p = ctx.Process(target=_worker_main, args=(base_rank + i, world, vars(ns), addr, i), daemon=True)
+            p.start()
+            procs.append(p)
+        os.environ.update({"RANK": str(base_rank), "WORLD_SIZE": str(world), "LOCAL_RANK": "0"})
+    from ome_amd.runtime.engine import Engine
+
+    if world > 1 and base_rank != 0:
+        # worker pod of a multi-node group: serve probes only, run the engine loop in lockstep
+        eng = Engine(engine_args_from(ns))
+        threading.Thread(target=eng.run_forever, daemon=True).start()
+        from fastapi import FastAPI
+        import uvicorn
+
+        app = FastAPI()
+
+        @app.get("/health")
+        async def h():
+            return {"status": "ok", "rank": base_rank}
+
+        uvicorn.run(app, host=ns.host, port=ns.port, log_level="warning")
+        return 0
+    eng = Engine(engine_args_from(ns))
+    if ns.disaggregation_mode != "null":
+        from ome_amd.runtime.disagg import attach_kv_transfer
+
+        attach_kv_transfer(eng, ns.disaggregation_mode, ns.disaggregation_bootstrap_port)
+    eng.start()
+    app = create_app(eng, ns)
+    import uvicorn
+
+    log.info("serving %s on %s:%d (tp=%d)", eng.served_model_name, ns.host, ns.port, ns.tp_size)
+    uvicorn.run(app, host=ns.host, port=ns.port, log_level="warning")
+    eng.shutdown()
+    for p in procs:
+        p.terminate()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
