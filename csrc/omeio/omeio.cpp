@@ -1,0 +1,343 @@
+// Native artifact I/O — see omeio.h.
+#include "omeio.h"
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <hip/hip_runtime_api.h>
+#include <openssl/evp.h>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+struct Fd {
+  int fd = -1;
+  explicit Fd(int f) : fd(f) {}
+  ~Fd() {
+    if (fd >= 0) close(fd);
+  }
+};
+
+// pread the whole [off, off+len) range, retrying short reads.
+bool pread_full(int fd, void* dst, uint64_t len, uint64_t off) {
+  auto* p = static_cast<char*>(dst);
+  while (len) {
+    ssize_t r = pread(fd, p, std::min<uint64_t>(len, 1ull << 30), static_cast<off_t>(off));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    if (r == 0) return false;
+    p += r;
+    off += static_cast<uint64_t>(r);
+    len -= static_cast<uint64_t>(r);
+  }
+  return true;
+}
+
+bool pwrite_full(int fd, const void* src, uint64_t len, uint64_t off) {
+  auto* p = static_cast<const char*>(src);
+  while (len) {
+    ssize_t r = pwrite(fd, p, std::min<uint64_t>(len, 1ull << 30), static_cast<off_t>(off));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += r;
+    off += static_cast<uint64_t>(r);
+    len -= static_cast<uint64_t>(r);
+  }
+  return true;
+}
+
+struct Piece {
+  uint64_t file_off, len;
+  char* dst;
+};
+
+std::vector<Piece> split(int n, const uint64_t* offs, const uint64_t* sizes, void* const* dsts, uint64_t chunk) {
+  std::vector<Piece> out;
+  for (int i = 0; i < n; ++i) {
+    for (uint64_t o = 0; o < sizes[i]; o += chunk) {
+      out.push_back({offs[i] + o, std::min(chunk, sizes[i] - o), static_cast<char*>(dsts[i]) + o});
+    }
+  }
+  return out;
+}
+
+std::string hex(const unsigned char* d, unsigned n) {
+  static const char* k = "0123456789abcdef";
+  std::string s(2 * n, '0');
+  for (unsigned i = 0; i < n; ++i) {
+    s[2 * i] = k[d[i] >> 4];
+    s[2 * i + 1] = k[d[i] & 15];
+  }
+  return s;
+}
+
+}  // namespace
+
+OMEIO_API const char* omeio_last_error() { return g_err.c_str(); }
+
+OMEIO_API int omeio_st_header(const char* path, char* buf, size_t cap, uint64_t* header_len, uint64_t* data_offset) {
+  Fd f(open(path, O_RDONLY | O_CLOEXEC));
+  if (f.fd < 0) return fail(-ENOENT, std::string("open ") + path + ": " + strerror(errno));
+  struct stat st {};
+  fstat(f.fd, &st);
+  uint64_t n = 0;
+  if (!pread_full(f.fd, &n, 8, 0)) return fail(-EIO, "short read on safetensors length prefix");
+  // Header is JSON; bound it (reference caps at 10 MB, we allow 100 MB for huge sharded MoE
+  // headers) and against the file size so a corrupt prefix cannot trigger a giant allocation.
+  if (n == 0 || n > (100ull << 20) || 8 + n > static_cast<uint64_t>(st.st_size))
+    return fail(-EINVAL, "invalid safetensors header length " + std::to_string(n));
+  *header_len = n;
+  *data_offset = 8 + n;
+  if (cap < n + 1) return fail(-ENOSPC, "buffer too small");
+  if (!pread_full(f.fd, buf, n, 8)) return fail(-EIO, "short read on safetensors header");
+  buf[n] = 0;
+  if (buf[0] != '{') return fail(-EINVAL, "safetensors header is not a JSON object");
+  return 0;
+}
+
+OMEIO_API int omeio_read_ranges(const char* path, int n, const uint64_t* offs, const uint64_t* sizes,
+                                void* const* dst, int nthreads) {
+  Fd f(open(path, O_RDONLY | O_CLOEXEC));
+  if (f.fd < 0) return fail(-ENOENT, std::string("open ") + path + ": " + strerror(errno));
+  posix_fadvise(f.fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+  auto pieces = split(n, offs, sizes, dst, 64ull << 20);
+  nthreads = std::max(1, std::min<int>(nthreads, static_cast<int>(pieces.size())));
+  std::atomic<int> err{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    th.emplace_back([&, t] {
+      size_t lo = pieces.size() * t / nthreads, hi = pieces.size() * (t + 1) / nthreads;
+      for (size_t i = lo; i < hi && !err.load(); ++i)
+        if (!pread_full(f.fd, pieces[i].dst, pieces[i].len, pieces[i].file_off)) err = -EIO;
+    });
+  }
+  for (auto& x : th) x.join();
+  return err ? fail(err, std::string("read failed: ") + path) : 0;
+}
+
+OMEIO_API int omeio_load_ranges(const char* path, int n, const uint64_t* offs, const uint64_t* sizes,
+                                void* const* dst, void* stream, int nthreads, uint64_t chunk) {
+  Fd f(open(path, O_RDONLY | O_CLOEXEC));
+  if (f.fd < 0) return fail(-ENOENT, std::string("open ") + path + ": " + strerror(errno));
+  posix_fadvise(f.fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+  if (chunk == 0) chunk = 16ull << 20;
+  // Make sure the caller's pending work on the destination (e.g. allocation-side memsets) is done.
+  if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return fail(-EIO, "stream sync failed");
+  auto pieces = split(n, offs, sizes, dst, chunk);
+  if (pieces.empty()) return 0;
+  nthreads = std::max(1, std::min<int>(nthreads, static_cast<int>(pieces.size())));
+  std::atomic<int> err{0};
+  std::string msg;
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    th.emplace_back([&, t] {
+      hipStream_t s;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        err = -EIO;
+        return;
+      }
+      void* stage[2] = {nullptr, nullptr};
+      hipEvent_t ev[2];
+      bool used[2] = {false, false};
+      for (int b = 0; b < 2; ++b) {
+        if (hipHostMalloc(&stage[b], chunk, hipHostMallocDefault) != hipSuccess) err = -ENOMEM;
+        hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
+      }
+      size_t lo = pieces.size() * t / nthreads, hi = pieces.size() * (t + 1) / nthreads;
+      int b = 0;
+      for (size_t i = lo; i < hi && !err.load(); ++i, b ^= 1) {
+        if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) {
+          err = -EIO;
+          break;
+        }
+        if (!pread_full(f.fd, stage[b], pieces[i].len, pieces[i].file_off)) {
+          err = -EIO;
+          break;
+        }
+        if (hipMemcpyAsync(pieces[i].dst, stage[b], pieces[i].len, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipEventRecord(ev[b], s) != hipSuccess) {
+          err = -EIO;
+          break;
+        }
+        used[b] = true;
+      }
+      hipStreamSynchronize(s);
+      for (int k = 0; k < 2; ++k) {
+        if (stage[k]) hipHostFree(stage[k]);
+        hipEventDestroy(ev[k]);
+      }
+      hipStreamDestroy(s);
+    });
+  }
+  for (auto& x : th) x.join();
+  return err ? fail(err, std::string("device load failed: ") + path) : 0;
+}
+
+OMEIO_API int omeio_md5_file(const char* path, char* md5_hex) {
+  Fd f(open(path, O_RDONLY | O_CLOEXEC));
+  if (f.fd < 0) return fail(-ENOENT, std::string("open ") + path + ": " + strerror(errno));
+  posix_fadvise(f.fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+  EVP_DigestInit_ex(ctx, EVP_md5(), nullptr);
+  std::vector<char> buf(8 << 20);
+  ssize_t r;
+  while ((r = read(f.fd, buf.data(), buf.size())) > 0) EVP_DigestUpdate(ctx, buf.data(), static_cast<size_t>(r));
+  unsigned char d[EVP_MAX_MD_SIZE];
+  unsigned dl = 0;
+  EVP_DigestFinal_ex(ctx, d, &dl);
+  EVP_MD_CTX_free(ctx);
+  if (r < 0) return fail(-EIO, "read failed");
+  std::string h = hex(d, dl);
+  memcpy(md5_hex, h.c_str(), h.size() + 1);
+  return 0;
+}
+
+OMEIO_API int omeio_copy_file(const char* src, const char* dst, int nthreads, char* md5_hex) {
+  Fd in(open(src, O_RDONLY | O_CLOEXEC));
+  if (in.fd < 0) return fail(-ENOENT, std::string("open ") + src + ": " + strerror(errno));
+  struct stat st {};
+  fstat(in.fd, &st);
+  Fd out(open(dst, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644));
+  if (out.fd < 0) return fail(-EACCES, std::string("create ") + dst + ": " + strerror(errno));
+  const uint64_t size = static_cast<uint64_t>(st.st_size);
+  if (size && ftruncate(out.fd, static_cast<off_t>(size)) != 0) return fail(-EIO, "ftruncate failed");
+  const uint64_t chunk = 32ull << 20;
+  const uint64_t nchunks = (size + chunk - 1) / chunk;
+  nthreads = std::max(1, std::min<int>(nthreads, static_cast<int>(std::max<uint64_t>(1, nchunks))));
+  std::atomic<uint64_t> next{0};
+  std::atomic<int> err{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    th.emplace_back([&] {
+      std::vector<char> buf(chunk);
+      for (uint64_t c; (c = next.fetch_add(1)) < nchunks && !err.load();) {
+        uint64_t off = c * chunk, len = std::min(chunk, size - off);
+        if (!pread_full(in.fd, buf.data(), len, off) || !pwrite_full(out.fd, buf.data(), len, off)) err = -EIO;
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  if (err) return fail(err, std::string("copy failed: ") + src + " -> " + dst);
+  if (md5_hex) return omeio_md5_file(dst, md5_hex);
+  return 0;
+}
+
+OMEIO_API int omeio_aes_gcm_encrypt(const uint8_t* in, size_t in_len, const uint8_t* key, const uint8_t* nonce,
+                                    uint8_t* out, size_t* out_len) {
+  EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
+  int ok = EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) &&
+           EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 12, nullptr) &&
+           EVP_EncryptInit_ex(c, nullptr, nullptr, key, nonce);
+  memcpy(out, nonce, 12);
+  int l1 = 0, l2 = 0;
+  ok = ok && EVP_EncryptUpdate(c, out + 12, &l1, in, static_cast<int>(in_len)) &&
+       EVP_EncryptFinal_ex(c, out + 12 + l1, &l2) &&
+       EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, out + 12 + l1 + l2);
+  EVP_CIPHER_CTX_free(c);
+  if (!ok) return fail(-EINVAL, "AES-GCM encrypt failed");
+  *out_len = 12 + static_cast<size_t>(l1 + l2) + 16;
+  return 0;
+}
+
+OMEIO_API int omeio_aes_gcm_decrypt(const uint8_t* in, size_t in_len, const uint8_t* key, uint8_t* out,
+                                    size_t* out_len) {
+  if (in_len < 28) return fail(-EINVAL, "ciphertext too short");
+  EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
+  int l1 = 0, l2 = 0;
+  int ok = EVP_DecryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr) &&
+           EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 12, nullptr) &&
+           EVP_DecryptInit_ex(c, nullptr, nullptr, key, in) &&
+           EVP_DecryptUpdate(c, out, &l1, in + 12, static_cast<int>(in_len - 28)) &&
+           EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_TAG, 16, const_cast<uint8_t*>(in + in_len - 16));
+  ok = ok && EVP_DecryptFinal_ex(c, out + l1, &l2) > 0;
+  EVP_CIPHER_CTX_free(c);
+  if (!ok) return fail(-EBADMSG, "AES-GCM authentication failed");
+  *out_len = static_cast<size_t>(l1 + l2);
+  return 0;
+}
+
+namespace {
+int gcm_file(const char* src, const char* dst, const uint8_t* key, const uint8_t* nonce_or_null, bool enc) {
+  Fd in(open(src, O_RDONLY | O_CLOEXEC));
+  if (in.fd < 0) return fail(-ENOENT, std::string("open ") + src + ": " + strerror(errno));
+  struct stat st {};
+  fstat(in.fd, &st);
+  const uint64_t size = static_cast<uint64_t>(st.st_size);
+  uint8_t nonce[12], tag[16];
+  uint64_t body_off = 0, body_len = size;
+  if (enc) {
+    memcpy(nonce, nonce_or_null, 12);
+  } else {
+    if (size < 28) return fail(-EINVAL, "encrypted file too short");
+    if (!pread_full(in.fd, nonce, 12, 0) || !pread_full(in.fd, tag, 16, size - 16)) return fail(-EIO, "read failed");
+    body_off = 12;
+    body_len = size - 28;
+  }
+  std::string tmp = std::string(dst) + ".omeio-tmp";
+  Fd out(open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644));
+  if (out.fd < 0) return fail(-EACCES, "create " + tmp + ": " + strerror(errno));
+  EVP_CIPHER_CTX* c = EVP_CIPHER_CTX_new();
+  int ok = (enc ? EVP_EncryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr)
+                : EVP_DecryptInit_ex(c, EVP_aes_256_gcm(), nullptr, nullptr, nullptr)) &&
+           EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_IVLEN, 12, nullptr) &&
+           (enc ? EVP_EncryptInit_ex(c, nullptr, nullptr, key, nonce) : EVP_DecryptInit_ex(c, nullptr, nullptr, key, nonce));
+  uint64_t woff = 0;
+  if (ok && enc) ok = pwrite_full(out.fd, nonce, 12, 0), woff = 12;
+  const uint64_t chunk = 8ull << 20;
+  std::vector<uint8_t> ib(chunk), ob(chunk + 32);
+  for (uint64_t o = 0; ok && o < body_len; o += chunk) {
+    uint64_t len = std::min(chunk, body_len - o);
+    int ol = 0;
+    ok = pread_full(in.fd, ib.data(), len, body_off + o) &&
+         (enc ? EVP_EncryptUpdate(c, ob.data(), &ol, ib.data(), static_cast<int>(len))
+              : EVP_DecryptUpdate(c, ob.data(), &ol, ib.data(), static_cast<int>(len))) &&
+         pwrite_full(out.fd, ob.data(), static_cast<uint64_t>(ol), woff);
+    woff += static_cast<uint64_t>(ol);
+  }
+  int fl = 0;
+  if (ok) {
+    if (enc) {
+      ok = EVP_EncryptFinal_ex(c, ob.data(), &fl) && pwrite_full(out.fd, ob.data(), fl, woff) &&
+           EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_GET_TAG, 16, tag) && pwrite_full(out.fd, tag, 16, woff + fl);
+    } else {
+      ok = EVP_CIPHER_CTX_ctrl(c, EVP_CTRL_GCM_SET_TAG, 16, tag) && EVP_DecryptFinal_ex(c, ob.data(), &fl) > 0 &&
+           pwrite_full(out.fd, ob.data(), fl, woff);
+    }
+  }
+  EVP_CIPHER_CTX_free(c);
+  if (!ok) {
+    unlink(tmp.c_str());
+    return fail(-EBADMSG, enc ? "AES-GCM encryption failed" : "AES-GCM authentication failed (wrong key or corrupt file)");
+  }
+  if (rename(tmp.c_str(), dst) != 0) return fail(-EIO, std::string("rename failed: ") + strerror(errno));
+  return 0;
+}
+}  // namespace
+
+OMEIO_API int omeio_aes_gcm_encrypt_file(const char* src, const char* dst, const uint8_t* key, const uint8_t* nonce) {
+  return gcm_file(src, dst, key, nonce, true);
+}
+
+OMEIO_API int omeio_aes_gcm_decrypt_file(const char* src, const char* dst, const uint8_t* key) {
+  return gcm_file(src, dst, key, nullptr, false);
+}

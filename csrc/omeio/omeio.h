@@ -1,0 +1,49 @@
+// Native artifact I/O for the model agent and the engine's weight loader.
+//
+//  * safetensors header parsing (8-byte LE header length + JSON, bounded)          — agent + loader
+//  * parallel pread -> pinned staging -> hipMemcpyAsync into HBM (double-buffered) — loader
+//  * chunked parallel file copy with MD5 / byte verification                         — agent (gopher)
+//  * AES-256-GCM file decryption (OpenSSL EVP)                                        — ome-agent enigma
+//
+// C ABI (ctypes) so Python never needs a build of its own.  All functions return 0 on success
+// and a negative errno-style code otherwise; omeio_last_error() gives the message.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+#define OMEIO_API extern "C" __attribute__((visibility("default")))
+
+OMEIO_API const char* omeio_last_error();
+
+// Reads the JSON header of a .safetensors file into `buf` (capacity `cap`, NUL-terminated).
+// *header_len receives the JSON length, *data_offset the byte offset of the tensor data.
+OMEIO_API int omeio_st_header(const char* path, char* buf, size_t cap, uint64_t* header_len,
+                              uint64_t* data_offset);
+
+// Copies `n` byte ranges of one file into device memory.  Ranges are split over `nthreads`
+// reader threads, each owning two pinned staging buffers of `chunk` bytes so the pread of
+// chunk i+1 overlaps the DMA of chunk i.  `stream` is a hipStream_t (0 = null stream); the
+// call returns after all copies have completed.
+OMEIO_API int omeio_load_ranges(const char* path, int n, const uint64_t* file_offsets, const uint64_t* sizes,
+                                void* const* dst_device, void* stream, int nthreads, uint64_t chunk);
+
+// Same, into host memory (no GPU needed) — used by CPU loads and tests.
+OMEIO_API int omeio_read_ranges(const char* path, int n, const uint64_t* file_offsets, const uint64_t* sizes,
+                                void* const* dst_host, int nthreads);
+
+// Parallel chunked copy src -> dst (creates/truncates dst).  If md5_hex (33 bytes) is non-null
+// it receives the MD5 of the content.
+OMEIO_API int omeio_copy_file(const char* src, const char* dst, int nthreads, char* md5_hex);
+
+// MD5 of a file (hex, 33 bytes incl. NUL).
+OMEIO_API int omeio_md5_file(const char* path, char* md5_hex);
+
+// AES-256-GCM.  Layout of an encrypted file: 12-byte nonce | ciphertext | 16-byte tag.
+OMEIO_API int omeio_aes_gcm_encrypt_file(const char* src, const char* dst, const uint8_t* key32,
+                                         const uint8_t* nonce12);
+OMEIO_API int omeio_aes_gcm_decrypt_file(const char* src, const char* dst, const uint8_t* key32);
+// In-memory variants (the data-encryption key itself is wrapped this way).
+OMEIO_API int omeio_aes_gcm_decrypt(const uint8_t* in, size_t in_len, const uint8_t* key32, uint8_t* out,
+                                    size_t* out_len);
+OMEIO_API int omeio_aes_gcm_encrypt(const uint8_t* in, size_t in_len, const uint8_t* key32, const uint8_t* nonce12,
+                                    uint8_t* out, size_t* out_len);

@@ -92,7 +92,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = True) ->
     if io_src:
         built.append(_build_lib("omeio", io_src, sorted(iodir.glob("*.h")), hipcc,
                                 [f for f in HIP_FLAGS if not f.startswith("--offload")] + ["-pthread", "-D__HIP_PLATFORM_AMD__"],
-                                ["-pthread", "-L/opt/rocm/lib", "-lamdhip64"], force, jobs))
+                                ["-pthread", "-L/opt/rocm/lib", "-lamdhip64", "-lcrypto"], force, jobs))
     cdir = CSRC / "comm"
     comm_src = sorted(cdir.glob("*.hip"))
     if comm_src:

@@ -1,0 +1,167 @@
+"""ctypes bindings for ``ome_amd/_lib/libomeio.so`` (built from ``csrc/omeio`` by
+``python -m ome_amd.build``).
+
+On a GPU box the weight loader *requires* this library (no silent fallback — SURVEY §7.1);
+host-only utilities (header parse, copy, md5, AES-GCM) fall back to Python where noted.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_LIB_PATH = Path(__file__).resolve().parent.parent / "_lib" / "libomeio.so"
+_lib = None
+_err = None
+
+
+class OmeIOError(RuntimeError):
+    pass
+
+
+def load():
+    global _lib, _err
+    if _lib is not None or _err is not None:
+        if _lib is None:
+            raise OmeIOError(_err)
+        return _lib
+    if not _LIB_PATH.exists() and os.environ.get("OME_AUTOBUILD", "1") == "1":
+        try:
+            from ome_amd import build
+
+            build.build(verbose=False)
+        except Exception as e:  # noqa: BLE001
+            _err = f"libomeio build failed: {e}"
+            raise OmeIOError(_err) from e
+    try:
+        lib = ctypes.CDLL(str(_LIB_PATH))
+    except OSError as e:
+        _err = f"cannot load {_LIB_PATH}: {e}"
+        raise OmeIOError(_err) from e
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    vpp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "omeio_last_error": ([], ctypes.c_char_p),
+        "omeio_st_header": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, u64p, u64p], ctypes.c_int),
+        "omeio_load_ranges": ([ctypes.c_char_p, ctypes.c_int, u64p, u64p, vpp, ctypes.c_void_p, ctypes.c_int,
+                               ctypes.c_uint64], ctypes.c_int),
+        "omeio_read_ranges": ([ctypes.c_char_p, ctypes.c_int, u64p, u64p, vpp, ctypes.c_int], ctypes.c_int),
+        "omeio_copy_file": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p], ctypes.c_int),
+        "omeio_md5_file": ([ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+        "omeio_aes_gcm_encrypt_file": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+        "omeio_aes_gcm_decrypt_file": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
+        "omeio_aes_gcm_encrypt": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                   ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "omeio_aes_gcm_decrypt": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p,
+                                   ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes, fn.restype = args, res
+    _lib = lib
+    return lib
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except OmeIOError:
+        return False
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise OmeIOError(f"omeio error {rc}: {load().omeio_last_error().decode(errors='replace')}")
+
+
+def st_header(path: str | os.PathLike) -> tuple[bytes, int]:
+    lib = load()
+    cap = 1 << 20
+    while True:
+        buf = ctypes.create_string_buffer(cap)
+        hl, off = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = lib.omeio_st_header(str(path).encode(), buf, cap, ctypes.byref(hl), ctypes.byref(off))
+        if rc == -28 and hl.value + 1 > cap:  # ENOSPC: grow to the exact size
+            cap = hl.value + 1
+            continue
+        _check(rc)
+        return buf.raw[:hl.value], off.value
+
+
+def _arrays(offsets, sizes, ptrs):
+    n = len(offsets)
+    return (n, (ctypes.c_uint64 * n)(*offsets), (ctypes.c_uint64 * n)(*sizes), (ctypes.c_void_p * n)(*ptrs))
+
+
+def load_ranges(path, offsets, sizes, device_ptrs, stream: int = 0, threads: int = 8, chunk: int = 16 << 20) -> None:
+    n, o, s, p = _arrays(offsets, sizes, device_ptrs)
+    _check(load().omeio_load_ranges(str(path).encode(), n, o, s, p, ctypes.c_void_p(stream), threads, chunk))
+
+
+def read_ranges(path, offsets, sizes, host_ptrs, threads: int = 8) -> None:
+    n, o, s, p = _arrays(offsets, sizes, host_ptrs)
+    _check(load().omeio_read_ranges(str(path).encode(), n, o, s, p, threads))
+
+
+def copy_file(src, dst, threads: int = 8, md5: bool = False) -> str | None:
+    buf = ctypes.create_string_buffer(64) if md5 else None
+    _check(load().omeio_copy_file(str(src).encode(), str(dst).encode(), threads, buf))
+    return buf.value.decode() if md5 else None
+
+
+def md5_file(path) -> str:
+    buf = ctypes.create_string_buffer(64)
+    _check(load().omeio_md5_file(str(path).encode(), buf))
+    return buf.value.decode()
+
+
+def aes_gcm_encrypt_file(src, dst, key: bytes, nonce: bytes) -> None:
+    assert len(key) == 32 and len(nonce) == 12
+    _check(load().omeio_aes_gcm_encrypt_file(str(src).encode(), str(dst).encode(), key, nonce))
+
+
+def aes_gcm_decrypt_file(src, dst, key: bytes) -> None:
+    assert len(key) == 32
+    _check(load().omeio_aes_gcm_decrypt_file(str(src).encode(), str(dst).encode(), key))
+
+
+def aes_gcm_encrypt(data: bytes, key: bytes, nonce: bytes) -> bytes:
+    out = ctypes.create_string_buffer(len(data) + 28)
+    n = ctypes.c_size_t()
+    _check(load().omeio_aes_gcm_encrypt(data, len(data), key, nonce, out, ctypes.byref(n)))
+    return out.raw[:n.value]
+
+
+def aes_gcm_decrypt(blob: bytes, key: bytes) -> bytes:
+    out = ctypes.create_string_buffer(max(1, len(blob)))
+    n = ctypes.c_size_t()
+    _check(load().omeio_aes_gcm_decrypt(blob, len(blob), key, out, ctypes.byref(n)))
+    return out.raw[:n.value]
+
+
+def iter_tensors_to_device(files, device):
+    """Stream every tensor of ``files`` straight into HBM through the native loader."""
+    import torch
+
+    from ome_amd.io.safetensors import DTYPES, read_header
+
+    dev = torch.device(device)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for f in files:
+        hdr, data_off = read_header(f)
+        items = [(k, v) for k, v in hdr.items() if k != "__metadata__"]
+        tensors, offs, sizes, ptrs = [], [], [], []
+        for name, meta in items:
+            t = torch.empty(meta["shape"], dtype=DTYPES[meta["dtype"]], device=dev)
+            b, e = meta["data_offsets"]
+            if e - b != t.numel() * t.element_size():
+                raise OmeIOError(f"{f}:{name}: byte range {e - b} != shape/dtype size")
+            tensors.append((name, t))
+            if e > b:
+                offs.append(data_off + b)
+                sizes.append(e - b)
+                ptrs.append(t.data_ptr())
+        if offs:
+            load_ranges(f, offs, sizes, ptrs, stream=stream, threads=min(16, max(2, len(offs))))
+        yield from tensors

@@ -1,0 +1,498 @@
+"""Model agent — the per-node DaemonSet that materialises BaseModel / ClusterBaseModel artifacts
+on local disk and reports them to the control plane (``pkg/modelagent``).
+
+Pipeline (same contract as the reference, re-built around a thread pool + the object store):
+
+  Scout   (``scout.go``)   watches (Cluster)BaseModels, decides whether *this* node should hold the
+                           model (``storage.nodeSelector`` / required ``nodeAffinity``; PVC and
+                           vendor storage are skipped), and queues Download / DownloadOverride /
+                           Delete tasks; on start it reconciles deletions missed while down.
+  Gopher  (``gopher.go``)  worker pool: label node ``Updating``, fetch via the storage backend with
+                           retries + cancellation, verify, **ReuseIfExists** de-duplication (same
+                           content sha already on the node -> symlink, parent/children
+                           bookkeeping), parse ``config.json`` into ModelMetadata, label ``Ready`` /
+                           ``Failed``; Delete honours shared artifacts and the
+                           ``models.ome/reserve-model-artifact`` annotation.
+  NodeConfigMap (``configmap_reconciler.go``) one ConfigMap ``<ome-ns>/<node>`` labelled
+                           ``models.ome/basemodel-status=true`` with a ``ModelEntry`` JSON per model
+                           key; conflict-retried writes; periodic self-heal (recreate the CM /
+                           restore entries from the in-memory cache).
+  NodeLabeler (``node_label_reconciler.go``) node label ``models.ome.io/<hashed key>`` =
+                           Ready / Updating / Failed (removed on delete).
+
+Progress of long downloads is throttled (``progress_interval``, 30 s in the reference) and
+flushed into the entry's ``progress`` field.
+"""
+from __future__ import annotations
+
+import copy
+import json
+import logging
+import os
+import queue
+import shutil
+import threading
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+from ome_amd.api import constants as C
+from ome_amd.executor.kubelet import node_affinity_ok
+from ome_amd.modelagent import metrics as M
+from ome_amd.modelagent.modelconfig import load_model_config, model_metadata
+from ome_amd.storage import backends
+from ome_amd.storage.uri import StorageURIError, parse
+from ome_amd.store.store import AlreadyExists, Conflict, NotFound, Store, now_iso
+
+log = logging.getLogger("ome_amd.modelagent")
+
+STATUS_READY, STATUS_UPDATING, STATUS_FAILED, STATUS_DELETED = "Ready", "Updating", "Failed", "Deleted"
+DOWNLOAD, DOWNLOAD_OVERRIDE, DELETE = "Download", "DownloadOverride", "Delete"
+API = C.API_VERSION
+
+
+def model_key(obj: dict) -> str:
+    cluster = obj["kind"] == "ClusterBaseModel"
+    return C.model_configmap_key(obj["metadata"].get("namespace"), obj["metadata"]["name"], cluster)
+
+
+def dest_path(spec: dict, root: str) -> str:
+    """``storage.path`` or ``<root>/<sanitised source>`` (the reference concatenates the raw URI,
+    ``gopher.go:664-678``; we keep paths URI-free)."""
+    st = spec.get("storage") or {}
+    if st.get("path"):
+        return st["path"]
+    uri = st.get("storageUri") or ""
+    body = uri.split("://", 1)[-1].replace("@", "/").replace("?", "_").strip("/")
+    return os.path.join(root, body or "model")
+
+
+# ------------------------------------------------------------------ node ConfigMap
+class NodeConfigMap:
+    def __init__(self, store: Store, node: str, namespace: str = C.OME_NAMESPACE):
+        self.store, self.node, self.ns = store, node, namespace
+        self.cache: dict[str, dict] = {}
+        self.lock = threading.RLock()
+
+    def _ensure(self) -> dict:
+        cm = self.store.try_get("v1", "ConfigMap", self.node, self.ns)
+        if cm is None:
+            self._ensure_ns()
+            try:
+                cm = self.store.create({"apiVersion": "v1", "kind": "ConfigMap",
+                                        "metadata": {"name": self.node, "namespace": self.ns,
+                                                     "labels": {C.MODEL_STATUS_CM_LABEL: "true"}},
+                                        "data": {}})
+            except AlreadyExists:
+                cm = self.store.get("v1", "ConfigMap", self.node, self.ns)
+        return cm
+
+    def _ensure_ns(self) -> None:
+        if self.store.try_get("v1", "Namespace", self.ns) is None:
+            try:
+                self.store.create({"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": self.ns}})
+            except AlreadyExists:
+                pass
+
+    def _update(self, mutate, retries: int = 5) -> None:
+        for attempt in range(retries):
+            cm = self._ensure()
+            data = dict(cm.get("data") or {})
+            mutate(data)
+            if data == (cm.get("data") or {}):
+                return
+            cm["data"] = data
+            try:
+                self.store.update(cm)
+                return
+            except (Conflict, NotFound):
+                time.sleep(0.01 * (attempt + 1))
+        raise Conflict(f"ConfigMap {self.ns}/{self.node}: too many conflicts")
+
+    def set_entry(self, key: str, entry: dict) -> None:
+        with self.lock:
+            self.cache[key] = copy.deepcopy(entry)
+            blob = json.dumps(entry, sort_keys=True)
+            self._update(lambda d: d.__setitem__(key, blob))
+
+    def get_entry(self, key: str) -> dict | None:
+        cm = self.store.try_get("v1", "ConfigMap", self.node, self.ns)
+        raw = ((cm or {}).get("data") or {}).get(key)
+        return json.loads(raw) if raw else None
+
+    def delete_entry(self, key: str) -> None:
+        with self.lock:
+            self.cache.pop(key, None)
+            self._update(lambda d: d.pop(key, None))
+
+    def entries(self) -> dict[str, dict]:
+        cm = self.store.try_get("v1", "ConfigMap", self.node, self.ns)
+        return {k: json.loads(v) for k, v in ((cm or {}).get("data") or {}).items()}
+
+    def self_heal(self) -> int:
+        """Recreate the ConfigMap / restore cached entries someone removed (``configmap_reconciler.go:152-202``)."""
+        with self.lock:
+            have = self.entries()
+            missing = {k: v for k, v in self.cache.items() if k not in have or have[k] != v}
+            if missing:
+                self._update(lambda d: d.update({k: json.dumps(v, sort_keys=True) for k, v in missing.items()}))
+            return len(missing)
+
+
+# ------------------------------------------------------------------ node labels
+class NodeLabeler:
+    def __init__(self, store: Store, node: str):
+        self.store, self.node = store, node
+
+    def set(self, obj: dict, status: str | None, retries: int = 5) -> None:
+        cluster = obj["kind"] == "ClusterBaseModel"
+        label = C.model_label(obj["metadata"].get("namespace"), obj["metadata"]["name"], cluster)
+        for attempt in range(retries):
+            n = self.store.try_get("v1", "Node", self.node)
+            if n is None:
+                return
+            labels = n["metadata"].setdefault("labels", {})
+            if status is None:
+                if label not in labels:
+                    return
+                labels.pop(label)
+            else:
+                if labels.get(label) == status:
+                    return
+                labels[label] = status
+            try:
+                self.store.update(n)
+                return
+            except Conflict:
+                time.sleep(0.01 * (attempt + 1))
+
+
+# ------------------------------------------------------------------ tasks
+@dataclass
+class Task:
+    type: str
+    obj: dict
+    attempts: int = 0
+    cancel: threading.Event = field(default_factory=threading.Event)
+
+
+class Scout:
+    def __init__(self, agent: "ModelAgent"):
+        self.agent = agent
+        self.seen: dict[str, str] = {}  # model key -> spec hash
+
+    def node_labels(self) -> dict:
+        n = self.agent.store.try_get("v1", "Node", self.agent.node)
+        return (n or {}).get("metadata", {}).get("labels") or {}
+
+    def should_download(self, obj: dict) -> bool:
+        st = (obj.get("spec") or {}).get("storage") or {}
+        uri = st.get("storageUri")
+        if uri:
+            try:
+                if parse(uri).type in ("PVC", "VENDOR"):
+                    return False
+            except StorageURIError:
+                return True  # let the gopher report the bad URI as Failed
+        node = {"metadata": {"labels": self.node_labels()}}
+        spec = {"nodeSelector": st.get("nodeSelector") or {}, "affinity": {"nodeAffinity": st.get("nodeAffinity") or {}}}
+        return node_affinity_ok(spec, node)
+
+    @staticmethod
+    def spec_hash(obj: dict) -> str:
+        return json.dumps({"storage": (obj.get("spec") or {}).get("storage")}, sort_keys=True)
+
+    def on_event(self, ev) -> None:
+        obj = ev.obj
+        if obj.get("apiVersion", "").split("/")[0] != C.GROUP:
+            return
+        key = model_key(obj)
+        if ev.type == "DELETED" or obj["metadata"].get("deletionTimestamp"):
+            if key in self.seen or self.agent.cm.get_entry(key):
+                self.seen.pop(key, None)
+                self.agent.submit(Task(DELETE, obj))
+            return
+        if not self.should_download(obj):
+            if key in self.seen:  # no longer targeted at this node
+                self.seen.pop(key, None)
+                self.agent.submit(Task(DELETE, obj))
+            return
+        h = self.spec_hash(obj)
+        prev = self.seen.get(key)
+        if prev == h:
+            return
+        self.seen[key] = h
+        self.agent.submit(Task(DOWNLOAD if prev is None else DOWNLOAD_OVERRIDE, obj))
+
+    def resync(self) -> None:
+        """Startup pass: queue every targeted model; delete entries whose model is gone."""
+        live = set()
+        for kind, ns in (("ClusterBaseModel", None), ("BaseModel", None)):
+            for obj in self.agent.store.list(API, kind, ns):
+                live.add(model_key(obj))
+                from ome_amd.store.store import WatchEvent
+
+                self.on_event(WatchEvent("ADDED", obj))
+        for key, entry in self.agent.cm.entries().items():
+            if key not in live:
+                parsed = C.parse_model_configmap_key(key)
+                if parsed:
+                    ns, name, cluster = parsed
+                    stub = {"apiVersion": API, "kind": "ClusterBaseModel" if cluster else "BaseModel",
+                            "metadata": {"name": entry.get("name", name), **({} if cluster else {"namespace": ns})},
+                            "spec": {}}
+                    self.agent.submit(Task(DELETE, stub))
+
+
+class Gopher:
+    def __init__(self, agent: "ModelAgent"):
+        self.agent = agent
+        self.active: dict[str, Task] = {}
+        self.lock = threading.Lock()
+
+    # ---------------------------------------------------------------- entries
+    def _entry(self, obj: dict, status: str, config: dict | None = None, progress: dict | None = None) -> dict:
+        e = {"name": obj["metadata"]["name"], "status": status}
+        if config:
+            e["config"] = config
+        if progress:
+            e["progress"] = progress
+        return e
+
+    def _progress_fn(self, key: str, obj: dict):
+        last = [0.0]
+
+        def report(p: dict) -> None:
+            now = time.time()
+            if now - last[0] < self.agent.progress_interval and p.get("completedFiles") != p.get("totalFiles"):
+                return
+            last[0] = now
+            self.agent.cm.set_entry(key, self._entry(obj, STATUS_UPDATING, progress={**p, "lastUpdated": now_iso()}))
+
+        return report
+
+    # ---------------------------------------------------------------- processing
+    def process(self, task: Task) -> None:
+        key = model_key(task.obj)
+        if task.type == DELETE:
+            with self.lock:
+                t = self.active.get(key)
+                if t:
+                    t.cancel.set()
+            self._delete(task.obj, key)
+            return
+        with self.lock:
+            self.active[key] = task
+        try:
+            self._download(task, key)
+        finally:
+            with self.lock:
+                if self.active.get(key) is task:
+                    self.active.pop(key)
+
+    def _find_reusable(self, sha: str, key: str) -> tuple[str, str] | None:
+        if not sha:
+            return None
+        for k, e in self.agent.cm.entries().items():
+            if k == key or e.get("status") != STATUS_READY:
+                continue
+            art = (e.get("config") or {}).get("artifact") or {}
+            if art.get("sha") == sha and art.get("path") and not art.get("parentPath"):
+                return k, art["path"]
+        return None
+
+    def _download(self, task: Task, key: str) -> None:
+        obj, ag = task.obj, self.agent
+        spec = obj.get("spec") or {}
+        st = spec.get("storage") or {}
+        uri = st.get("storageUri") or ""
+        dest = dest_path(spec, ag.models_root)
+        policy = st.get("downloadPolicy") or "ReuseIfExists"
+        ag.labeler.set(obj, STATUS_UPDATING)
+        ag.cm.set_entry(key, self._entry(obj, STATUS_UPDATING))
+        t0 = time.time()
+        err = None
+        res = None
+        for attempt in range(ag.download_retry):
+            if task.cancel.is_set():
+                return
+            try:
+                if task.type == DOWNLOAD_OVERRIDE and policy == "AlwaysDownload" and os.path.isdir(dest) \
+                        and not os.path.islink(dest):
+                    shutil.rmtree(dest, ignore_errors=True)
+                res = backends.fetch(uri, dest, self._progress_fn(key, obj), token=self._hf_token(obj))
+                break
+            except (backends.FetchError, StorageURIError, OSError) as e:
+                err = e
+                M.DOWNLOAD_FAILURES.labels(model=obj["metadata"]["name"]).inc()
+                log.warning("download %s attempt %d failed: %s", key, attempt + 1, e)
+                time.sleep(min(2.0, ag.retry_backoff * (2 ** attempt)))
+        if res is None:
+            ag.labeler.set(obj, STATUS_FAILED)
+            ag.cm.set_entry(key, self._entry(obj, STATUS_FAILED, config={"error": str(err)[:500]}))
+            return
+        artifact = {"sha": res.sha, "path": res.path, "parentPath": {}, "childrenPaths": []}
+        reuse = self._find_reusable(res.sha, key) if policy == "ReuseIfExists" else None
+        if reuse and os.path.realpath(reuse[1]) != os.path.realpath(res.path):
+            parent_key, parent_path = reuse
+            # content already on the node: replace our copy with a symlink to the parent artifact
+            if os.path.isdir(res.path) and not os.path.islink(res.path):
+                shutil.rmtree(res.path, ignore_errors=True)
+            os.makedirs(os.path.dirname(res.path) or "/", exist_ok=True)
+            if not os.path.exists(res.path):
+                os.symlink(parent_path, res.path)
+            artifact["parentPath"] = {parent_key: parent_path}
+            pe = self.agent.cm.get_entry(parent_key) or {}
+            pa = (pe.get("config") or {}).setdefault("artifact", {})
+            pa.setdefault("childrenPaths", [])
+            if res.path not in pa["childrenPaths"]:
+                pa["childrenPaths"].append(res.path)
+                self.agent.cm.set_entry(parent_key, pe)
+        cfg: dict = {}
+        skip = (obj["metadata"].get("annotations") or {}).get(C.SKIP_CONFIG_PARSING, "").lower() == "true"
+        if not skip:
+            try:
+                cfg = model_metadata(load_model_config(res.path))
+            except (FileNotFoundError, ValueError, OSError) as e:
+                log.info("config parse skipped for %s: %s", key, e)
+        cfg["artifact"] = artifact
+        ag.cm.set_entry(key, self._entry(obj, STATUS_READY, config=cfg))
+        ag.labeler.set(obj, STATUS_READY)
+        M.DOWNLOADS.labels(model=obj["metadata"]["name"]).inc()
+        M.DOWNLOAD_SECONDS.observe(time.time() - t0)
+        if res.bytes:
+            M.DOWNLOAD_BYTES.inc(res.bytes)
+
+    def _hf_token(self, obj: dict) -> str | None:
+        st = (obj.get("spec") or {}).get("storage") or {}
+        key = st.get("key") or st.get("storageKey")
+        if not key:
+            return os.environ.get("HF_TOKEN")
+        ns = obj["metadata"].get("namespace") or C.OME_NAMESPACE
+        sec = self.agent.store.try_get("v1", "Secret", key, ns)
+        if not sec:
+            return None
+        from ome_amd.executor.kubelet import _secret_val
+
+        return _secret_val(sec, (st.get("parameters") or {}).get("secretKey", "token"))
+
+    def _delete(self, obj: dict, key: str) -> None:
+        ag = self.agent
+        entry = ag.cm.get_entry(key) or {}
+        art = (entry.get("config") or {}).get("artifact") or {}
+        path = art.get("path") or dest_path(obj.get("spec") or {}, ag.models_root)
+        reserve = (obj["metadata"].get("annotations") or {}).get(C.RESERVE_MODEL_ARTIFACT, "").lower() == "true"
+        st = ((obj.get("spec") or {}).get("storage") or {})
+        managed = bool(entry) and not (st.get("storageUri", "").startswith(("pvc://", "vendor://")))
+        children = [c for c in art.get("childrenPaths") or [] if os.path.lexists(c)]
+        if managed and not reserve and path and os.path.lexists(path):
+            if os.path.islink(path):
+                os.unlink(path)
+            elif children:
+                # other models symlink to this artifact: hand ownership to the first child
+                heir = children[0]
+                os.unlink(heir)
+                shutil.move(path, heir)
+                for c in children[1:]:
+                    os.unlink(c)
+                    os.symlink(heir, c)
+            elif os.path.realpath(path).startswith(os.path.realpath(ag.models_root)) or art.get("path"):
+                shutil.rmtree(path, ignore_errors=True)
+        for pk in (art.get("parentPath") or {}):
+            pe = ag.cm.get_entry(pk)
+            if pe:
+                pa = (pe.get("config") or {}).get("artifact") or {}
+                if path in (pa.get("childrenPaths") or []):
+                    pa["childrenPaths"].remove(path)
+                    ag.cm.set_entry(pk, pe)
+        ag.cm.delete_entry(key)
+        ag.labeler.set(obj, None)
+        M.DELETES.labels(model=obj["metadata"]["name"]).inc()
+
+
+class ModelAgent:
+    def __init__(self, store: Store, node: str, models_root: str = C.DEFAULT_MODEL_LOCAL_MOUNT_PATH,
+                 workers: int = 4, download_retry: int = 3, progress_interval: float = 30.0,
+                 heal_interval: float = 300.0, retry_backoff: float = 0.5):
+        self.store, self.node, self.models_root = store, node, models_root
+        self.cm = NodeConfigMap(store, node)
+        self.labeler = NodeLabeler(store, node)
+        self.scout = Scout(self)
+        self.gopher = Gopher(self)
+        self.tasks: queue.Queue[Task] = queue.Queue()
+        self.workers = workers
+        self.download_retry = download_retry
+        self.progress_interval = progress_interval
+        self.heal_interval = heal_interval
+        self.retry_backoff = retry_backoff
+        self._threads: list[threading.Thread] = []
+        self._stop = threading.Event()
+        self._watch = None
+        self.inflight = 0
+        self._inflight_lock = threading.Lock()
+
+    def submit(self, t: Task) -> None:
+        with self._inflight_lock:
+            self.inflight += 1
+        self.tasks.put(t)
+
+    def _worker(self) -> None:
+        while not self._stop.is_set():
+            try:
+                t = self.tasks.get(timeout=0.2)
+            except queue.Empty:
+                continue
+            try:
+                self.gopher.process(t)
+            except Exception:  # noqa: BLE001
+                log.exception("task %s for %s failed", t.type, t.obj["metadata"].get("name"))
+            finally:
+                with self._inflight_lock:
+                    self.inflight -= 1
+
+    def _healer(self) -> None:
+        while not self._stop.wait(self.heal_interval):
+            try:
+                self.cm.self_heal()
+            except Exception:  # noqa: BLE001
+                log.exception("configmap self-heal failed")
+
+    def start(self) -> None:
+        os.makedirs(self.models_root, exist_ok=True)
+        self._watch = self.store.watch(self.scout.on_event, ["BaseModel", "ClusterBaseModel"])
+        self.scout.resync()
+        for i in range(self.workers):
+            t = threading.Thread(target=self._worker, name=f"gopher-{i}", daemon=True)
+            t.start()
+            self._threads.append(t)
+        h = threading.Thread(target=self._healer, name="cm-heal", daemon=True)
+        h.start()
+        self._threads.append(h)
+
+    def drain(self, timeout: float = 60.0) -> bool:
+        """Wait until every queued task has been processed (tests / CLI one-shot mode)."""
+        end = time.time() + timeout
+        while time.time() < end:
+            with self._inflight_lock:
+                if self.inflight == 0:
+                    return True
+            time.sleep(0.02)
+        return False
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._watch:
+            self.store.unwatch(self._watch)
+        for t in self._threads:
+            t.join(timeout=2)
+
+    def healthz(self) -> tuple[bool, str]:
+        """``healthz.go:25-39``: models dir exists, is a directory and is writable."""
+        p = Path(self.models_root)
+        if not p.exists():
+            return False, f"models root {p} does not exist"
+        if not p.is_dir():
+            return False, f"models root {p} is not a directory"
+        if not os.access(p, os.W_OK):
+            return False, f"models root {p} is not writable"
+        return True, "ok"

@@ -76,7 +76,7 @@ def parse_model_size(s: str | None) -> float:
     if not s:
         return 0.0
     mult = 1.0
-    for suf, m in (("T", 1e12), ("B", 1e9), ("M", 1e6)):
+    for suf, m in (("T", 1e12), ("B", 1e9), ("M", 1e6), ("K", 1e3)):
         if s.endswith(suf):
             s, mult = s[:-1], m
             break
