@@ -10,8 +10,10 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 import zlib
+from pathlib import Path
 
 import numpy as np
 import torch
@@ -145,8 +147,45 @@ class ModelRunner:
         ops.sample(logits, d.view("temp", bs), d.view("top_k", bs), d.view("top_p", bs), d.view("min_p", bs),
                    d.view("seeds", bs), 0, out_ids=self.out_ids[:bs], out_logprob=self.out_lp[:bs])
 
+    # ------------------------------------------------------------------ GEMM tuning
+    TUNED_DIR = Path(__file__).resolve().parent.parent / "_tuned"
+
+    def _tuning_begin(self) -> bool:
+        """PyTorch TunableOp over the decode GEMM shapes: benchmarks every hipBLASLt / rocBLAS
+        solution for each (M=bucket, N, K) once and persists the winners in-tree
+        (``ome_amd/_tuned/tunableop_gfx950.csv``) so later starts skip tuning.  Tuning is only
+        ON during the eager pre-capture pass; prefill shapes use the tuned table when present and
+        the library heuristic otherwise (never tuned inside serving)."""
+        if os.environ.get("OME_TUNE_GEMM", "1") != "1" or not hasattr(torch.cuda, "tunable"):
+            return False
+        tun = torch.cuda.tunable
+        self.TUNED_DIR.mkdir(parents=True, exist_ok=True)
+        arch = torch.cuda.get_device_properties(self.device).gcnArchName.split(":")[0]
+        fname = str(self.TUNED_DIR / f"tunableop_{arch}.csv")
+        tun.set_filename(fname, insert_device_ordinal=False)
+        tun.enable(True)
+        tun.tuning_enable(True)
+        tun.set_max_tuning_duration(int(os.environ.get("OME_TUNE_MS", "40")))
+        tun.set_max_tuning_iterations(int(os.environ.get("OME_TUNE_ITERS", "30")))
+        if os.path.exists(fname):
+            tun.read_file(fname)
+        self._tune_file = fname
+        return True
+
+    def _tuning_end(self) -> None:
+        tun = torch.cuda.tunable
+        tun.tuning_enable(False)
+        # torch writes the table to the configured filename at process exit (newer releases
+        # also expose write_file for an explicit flush)
+        if hasattr(tun, "write_file"):
+            try:
+                tun.write_file(self._tune_file)
+            except Exception as e:  # noqa: BLE001 — read-only tree: keep the in-memory table
+                log.warning("could not persist tuned GEMM table: %s", e)
+
     def capture_graphs(self) -> None:
         t0 = time.perf_counter()
+        tuning = self._tuning_begin()
         d = self.dbuf
         d.hnp[:] = 0
         d.hnp[d.off["slots"]:d.off["slots"] + d.bmax] = -1
@@ -156,9 +195,12 @@ class ModelRunner:
         stream.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(stream):
             for bs in reversed(self.buckets):
-                self._decode_forward(bs)  # warm-up (allocations, hipBLASLt heuristics)
+                self._decode_forward(bs)  # warm-up (allocations, hipBLASLt heuristics / tuning)
         torch.cuda.current_stream(self.device).wait_stream(stream)
         torch.cuda.synchronize(self.device)
+        if tuning:
+            self._tuning_end()
+            log.info("GEMM tuning pass done in %.1fs", time.perf_counter() - t0)
         for bs in reversed(self.buckets):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.graph_pool):
