@@ -108,3 +108,22 @@ OME_API int ome_pool(const void* hidden, const int* cu_lens, void* out, int S, i
   OME_CHECK_LAUNCH();
   return 0;
 }
+
+// Overlapped scheduling: the next step is enqueued before the previous step's sampled ids
+// reach the host, so rows whose input token is still "pending" take it from the previous
+// step's device output: ids[i] = prev[src[i]] when src[i] >= 0 (one tiny kernel, no sync).
+__global__ void fill_pending_kernel(int* __restrict__ ids, const int* __restrict__ src, const int* __restrict__ prev,
+                                    int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int s = src[i];
+    if (s >= 0) ids[i] = prev[s];
+  }
+}
+
+OME_API int ome_fill_pending(int* ids, const int* src, const int* prev, int n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  fill_pending_kernel<<<(n + 255) / 256, 256, 0, stream>>>(ids, src, prev, n);
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -89,6 +89,19 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_start: int = 0, voca
     return out
 
 
+def fill_pending(ids: torch.Tensor, src: torch.Tensor, prev: torch.Tensor) -> None:
+    """ids[i] = prev[src[i]] where src[i] >= 0 (int32, in place) — overlapped scheduling."""
+    n = ids.shape[0]
+    if n == 0:
+        return
+    if not _gpu(ids):
+        m = src >= 0
+        ids[m] = prev[src[m].long()].to(ids.dtype)
+        return
+    assert ids.dtype == src.dtype == prev.dtype == torch.int32
+    call("ome_fill_pending", ids.data_ptr(), src.data_ptr(), prev.data_ptr(), n, stream_ptr())
+
+
 class DecodeWorkspace:
     """Split-K partial buffers for paged decode, sized once (graph-capture safe)."""
 
@@ -154,7 +167,7 @@ def sample(logits: torch.Tensor, temperature=None, top_k=None, top_p=None, min_p
            out_ids=None, out_logprob=None):
     """Returns (ids int32 [B], logprobs f32 [B])."""
     if not _gpu(logits):
-        ids, lps = ref.sample(logits, temperature, top_k, top_p, min_p)
+        ids, lps = ref.sample(logits, temperature, top_k, top_p, min_p, seeds=seeds)
         if out_ids is not None:
             out_ids.copy_(ids)
             ids = out_ids

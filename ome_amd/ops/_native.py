@@ -30,6 +30,7 @@ _SIGNATURES = {
         "ome_act_and_mul": [vp, vp, i64, i32, i32, vp],
         "ome_embedding": [vp, vp, vp, i32, i32, i32, i32, vp],
         "ome_pool": [vp, vp, vp, i32, i32, i32, i32, vp],
+        "ome_fill_pending": [vp, vp, vp, i32, vp],
         "ome_paged_decode": [vp, i64, vp, vp, vp, i32, vp, vp, i64, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32,
                              i32, vp],
         "ome_paged_prefill": [vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, vp, i64, i32, i32, i32, i32, f32, i32, vp],

@@ -135,8 +135,10 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, windo
     return out
 
 
-def sample(logits, temperature=None, top_k=None, top_p=None, min_p=None, generator=None):
-    """Returns (ids int32 [B], logprob f32 [B]).  Greedy where temperature <= 0."""
+def sample(logits, temperature=None, top_k=None, top_p=None, min_p=None, generator=None, seeds=None):
+    """Returns (ids int32 [B], logprob f32 [B]).  Greedy where temperature <= 0.  ``seeds``
+    (int64 [B]) makes each row's draw a pure function of its counter-based seed (the CPU
+    analogue of the kernel's per-row splitmix64 stream; the draws themselves differ)."""
     lf = logits.float()
     B, V = lf.shape
     ids = torch.empty(B, dtype=torch.int32, device=logits.device)
@@ -168,7 +170,11 @@ def sample(logits, temperature=None, top_k=None, top_p=None, min_p=None, generat
         if mp > 0:
             keep &= z >= math.log(mp)
         probs = torch.softmax(z.masked_fill(~keep, float("-inf")), -1)
-        i = int(torch.multinomial(probs, 1, generator=generator))
+        g = generator
+        if seeds is not None:
+            g = torch.Generator(device=row.device)
+            g.manual_seed(int(seeds[b]) & ((1 << 63) - 1))
+        i = int(torch.multinomial(probs, 1, generator=g))
         ids[b] = i
         lps[b] = logp[i]
     return ids, lps

@@ -53,6 +53,8 @@ class EngineArgs:
     nnodes: int = 1
     node_rank: int = 0
     disaggregation_mode: str = "null"      # null | prefill | decode
+    overlap_schedule: bool | None = None   # enqueue step k+1 before step k's tokens reach the host
+                                           # (None = on for GPU engines)
     num_layers_override: int | None = None
     extra: dict = field(default_factory=dict)
 
@@ -109,6 +111,10 @@ class Engine:
         self._stop = False
         self.step_count = 0
         self.kv_transfer = None  # PD disaggregation hook (ome_amd.runtime.disagg)
+        # overlapped scheduling: (batch, handle, launch time) of the step whose tokens are in flight
+        self._inflight = None
+        ov = self.runner.is_cuda if args.overlap_schedule is None else bool(args.overlap_schedule)
+        self.overlap = ov and not self.cfg.is_embedding
 
     # ------------------------------------------------------------------ API
     def make_request(self, prompt_ids: list[int], params: SamplingParams | None = None, **kw) -> Request:
@@ -166,35 +172,67 @@ class Engine:
         return self._gloo
 
     def step(self) -> list[Request]:
-        """One scheduler iteration. Returns requests that finished in this step."""
+        """One scheduler iteration: enqueue one step.  Returns requests that finished.
+
+        Overlapped mode (default on GPU): step k+1 is scheduled and enqueued *before* step k's
+        sampled tokens are copied back — its decode rows take their input ids from step k's
+        device output (``ModelRunner.launch(prev=...)``) — so host-side scheduling, input packing
+        and detokenisation hide behind the GPU.  Returned requests are those finished by step k.
+        """
         self._drain_inbox()
-        batch = self.scheduler.schedule()
-        if batch is None:
-            return []
-        t0 = time.perf_counter()
         if self.cfg.is_embedding:
-            embs = self.runner.embed(batch)
-            now = time.perf_counter()
-            done = []
-            for c, e in zip(batch.chunks, embs):
-                c.req.embedding = e
-                c.req.num_cached = c.start + c.length
-                if c.req.num_cached >= len(c.req.prompt_ids):
-                    c.req.first_token_time = now
-                    self.scheduler.finish(c.req, "stop")
-                    done.append(c.req)
-                    if c.req.on_token:
-                        c.req.on_token(c.req, [], True)
+            return self._embed_step()
+        prev = self._inflight
+        batch = self.scheduler.schedule()
+        launched = None
+        if batch is not None:
+            t0 = time.perf_counter()
+            handle = self.runner.launch(batch, prev[1] if prev else None)
+            self.scheduler.launch_commit(batch)
+            launched = (batch, handle, t0)
+        done: list[Request] = []
+        if not self.overlap:
+            if launched:
+                done = self._complete(*launched)
             return done
-        ids, lps = self.runner.run(batch)
+        if prev is not None:
+            done = self._complete(*prev)
+        self._inflight = launched
+        return done
+
+    def _complete(self, batch, handle, t0) -> list[Request]:
+        ids, lps = handle.result()
         now = time.perf_counter()
-        done = self.scheduler.commit(batch, ids, lps, now, self.eos_ids)
+        done = self.scheduler.final_commit(batch, ids, lps, now, self.eos_ids)
         self.step_count += 1
         self.metrics.on_step(batch, now - t0, done, self.scheduler, self.runner.pages)
         return done
 
+    def flush(self) -> list[Request]:
+        """Wait for the in-flight step (if any) and commit it."""
+        prev, self._inflight = self._inflight, None
+        return self._complete(*prev) if prev else []
+
+    def _embed_step(self) -> list[Request]:
+        batch = self.scheduler.schedule()
+        if batch is None:
+            return []
+        embs = self.runner.embed(batch)
+        now = time.perf_counter()
+        done = []
+        for c, e in zip(batch.chunks, embs):
+            c.req.embedding = e
+            c.req.num_cached = c.start + c.length
+            if c.req.num_cached >= len(c.req.prompt_ids):
+                c.req.first_token_time = now
+                self.scheduler.finish(c.req, "stop")
+                done.append(c.req)
+                if c.req.on_token:
+                    c.req.on_token(c.req, [], True)
+        return done
+
     def has_work(self) -> bool:
-        return self.scheduler.has_work() or bool(self._inbox)
+        return self.scheduler.has_work() or bool(self._inbox) or self._inflight is not None
 
     def generate(self, prompts: list[list[int]], params: SamplingParams | list[SamplingParams] | None = None) -> list[Request]:
         plist = params if isinstance(params, list) else [params] * len(prompts)

@@ -23,6 +23,7 @@ from ome_amd.models import build_model
 from ome_amd.models.common import AttnMeta, PagedKVCache
 from ome_amd.models.config import ModelConfig
 from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
+from ome_amd.runtime.request import PENDING
 from ome_amd.runtime.scheduler import StepBatch
 
 log = logging.getLogger("ome_amd.runtime")
@@ -44,7 +45,7 @@ def default_buckets(max_bs: int) -> list[int]:
 
 
 class _DecodeBuffers:
-    FIELDS_I = ("ids", "pos", "slots", "seq_lens", "req_idx", "top_k")
+    FIELDS_I = ("ids", "pos", "slots", "seq_lens", "req_idx", "top_k", "src")
     FIELDS_F = ("temp", "top_p", "min_p")
 
     def __init__(self, bmax: int, device):
@@ -68,6 +69,21 @@ class _DecodeBuffers:
         if name == "seeds":
             return self.dev[o:o + 2 * bs].view(torch.int64)
         return self.dev[o:o + bs]
+
+
+class StepHandle:
+    """An enqueued step: device outputs (for the next step's pending-token gather) plus the
+    pinned host copies that ``result()`` waits for."""
+
+    __slots__ = ("ids_dev", "n", "host_ids", "host_lp", "event")
+
+    def __init__(self, ids_dev, n, host_ids, host_lp, event):
+        self.ids_dev, self.n, self.host_ids, self.host_lp, self.event = ids_dev, n, host_ids, host_lp, event
+
+    def result(self) -> tuple[list[int], list[float]]:
+        if self.event is not None:
+            self.event.synchronize()
+        return self.host_ids[:self.n].tolist(), self.host_lp[:self.n].tolist()
 
 
 class ModelRunner:
@@ -116,6 +132,12 @@ class ModelRunner:
         self.dbuf = _DecodeBuffers(self.bmax, self.device)
         self.out_ids = torch.zeros(self.bmax, dtype=torch.int32, device=self.device)
         self.out_lp = torch.zeros(self.bmax, dtype=torch.float32, device=self.device)
+        # pinned landing zone for sampled ids / logprobs, double-buffered so step k+1 can be
+        # enqueued while the host still reads step k (overlapped scheduling)
+        nout = max(self.bmax, max_running + 8)
+        self._host_out = [(torch.zeros(nout, dtype=torch.int32, pin_memory=self.is_cuda),
+                           torch.zeros(nout, dtype=torch.float32, pin_memory=self.is_cuda)) for _ in range(2)]
+        self._ring = 0
         self._ws_cache: dict[int, ops.DecodeWorkspace] = {}
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
@@ -219,28 +241,60 @@ class ModelRunner:
 
     # ------------------------------------------------------------------ steps
     def run(self, batch: StepBatch) -> tuple[list[int], list[float]]:
+        """Synchronous step: enqueue + wait."""
+        return self.launch(batch).result()
+
+    def launch(self, batch: StepBatch, prev: "StepHandle | None" = None) -> "StepHandle":
+        """Enqueue one step.  Rows whose input token is PENDING (sampled by ``prev``, still in
+        flight) get it on the device from ``prev``'s output — no host round trip."""
         self.slots.flush()
         if batch.mode == "decode" and all(c.length == 1 for c in batch.chunks):
-            return self.run_decode(batch)
-        return self.run_prefill(batch)
+            bs = next((b for b in self.buckets if b >= len(batch.chunks)), None)
+            if bs is not None:
+                return self._launch_decode(batch, bs, prev)
+        return self._launch_eager(batch, prev)
 
-    def run_decode(self, batch: StepBatch):
+    def _finish_launch(self, ids_dev: torch.Tensor, lp_dev: torch.Tensor, n: int) -> "StepHandle":
+        hi, hl = self._host_out[self._ring]
+        self._ring ^= 1
+        if n:
+            hi[:n].copy_(ids_dev[:n], non_blocking=True)
+            hl[:n].copy_(lp_dev[:n], non_blocking=True)
+        ev = None
+        if self.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        return StepHandle(ids_dev, n, hi, hl, ev)
+
+    @staticmethod
+    def _src_row(r, pos: int, prev: "StepHandle | None") -> int:
+        """Row of ``prev``'s sampled output holding the token at ``pos`` if it is pending."""
+        if prev is None or not r.n_pending or pos != r.seq_len - 1 or r.all_ids[pos] != PENDING:
+            return -1
+        return r.pending_row
+
+    def _launch_decode(self, batch: StepBatch, bs: int, prev: "StepHandle | None") -> "StepHandle":
         B = len(batch.chunks)
-        bs = next((b for b in self.buckets if b >= B), None)
         d = self.dbuf
-        if bs is None:  # larger than the biggest graph: eager in bucket-sized slices
-            return self.run_prefill(batch)
         h, hf, off = d.hnp, d.hf, d.off
         h[off["ids"]:off["ids"] + bs] = 0
         h[off["slots"]:off["slots"] + bs] = -1
         h[off["seq_lens"]:off["seq_lens"] + bs] = 0
         h[off["req_idx"]:off["req_idx"] + bs] = self.slots.max_reqs - 1
         h[off["pos"]:off["pos"] + bs] = 0
+        h[off["src"]:off["src"] + bs] = -1
         seeds = h[off["seeds"]:off["seeds"] + 2 * bs].view(np.uint64)
+        any_pending = False
         for i, c in enumerate(batch.chunks):
             r = c.req
             pos = c.start
-            h[off["ids"] + i] = r.all_ids[pos]
+            tok = r.all_ids[pos]
+            src = self._src_row(r, pos, prev)
+            if src >= 0:
+                h[off["src"] + i] = src
+                any_pending = True
+                tok = 0
+            h[off["ids"] + i] = tok
             h[off["pos"] + i] = pos
             h[off["slots"] + i] = r.pages[pos // self.P] * self.P + pos % self.P
             h[off["seq_lens"] + i] = pos + 1
@@ -250,27 +304,36 @@ class ModelRunner:
             hf[off["temp"] + i] = p.temperature
             hf[off["top_p"] + i] = p.top_p
             hf[off["min_p"] + i] = p.min_p
-            seeds[i] = self._seed(r, pos)
+            seeds[i] = self._seed(r, pos + 1)  # keyed by the position of the token being drawn
         for i in range(B, bs):
             hf[off["temp"] + i] = 0.0
             hf[off["top_p"] + i] = 1.0
             h[off["top_k"] + i] = -1
         d.dev.copy_(d.host, non_blocking=True)
+        if any_pending:
+            ops.fill_pending(d.view("ids", bs), d.view("src", bs), prev.ids_dev)
         if self.use_graph:
             self.graphs[bs].replay()
         else:
             self._decode_forward(bs)
-        ids = self.out_ids[:B].to("cpu", non_blocking=False).tolist()
-        lps = self.out_lp[:B].to("cpu").tolist()
-        return ids, lps
+        return self._finish_launch(self.out_ids, self.out_lp, B)
 
-    def run_prefill(self, batch: StepBatch):
+    def _launch_eager(self, batch: StepBatch, prev: "StepHandle | None") -> "StepHandle":
         P = self.P
-        ids, pos, slots, q_lens, kv_lens, req_idx, sample_rows = [], [], [], [], [], [], []
+        ids, pos, slots, q_lens, kv_lens, req_idx, sample_rows, src = [], [], [], [], [], [], [], []
+        any_pending = False
         for c in batch.chunks:
             r = c.req
+            t0 = len(ids)
             toks = r.all_ids[c.start:c.start + c.length]
             ids.extend(toks)
+            src.extend([-1] * c.length)
+            last = c.start + c.length - 1
+            s_row = self._src_row(r, last, prev)
+            if s_row >= 0:
+                src[t0 + c.length - 1] = s_row
+                ids[t0 + c.length - 1] = 0
+                any_pending = True
             pp = range(c.start, c.start + c.length)
             pos.extend(pp)
             pages = r.pages
@@ -285,7 +348,7 @@ class ModelRunner:
         cu[1:] = np.cumsum(q_lens)
         packed = np.concatenate([np.asarray(ids, np.int32), np.asarray(pos, np.int32), np.asarray(slots, np.int32),
                                  cu, np.asarray(kv_lens, np.int32), np.asarray(req_idx, np.int32),
-                                 np.asarray(sample_rows, np.int32),
+                                 np.asarray(sample_rows, np.int32), np.asarray(src, np.int32),
                                  np.asarray(items, np.int32).reshape(-1) if n_it else np.zeros(0, np.int32)])
         host = torch.from_numpy(packed)
         if self.is_cuda:
@@ -301,7 +364,10 @@ class ModelRunner:
 
         t_ids, t_pos, t_slots = take(T), take(T), take(T)
         t_cu, t_kv, t_req, t_rows = take(S + 1), take(S), take(S), take(S)
+        t_src = take(T)
         t_items = take(2 * n_it).view(n_it, 2)
+        if any_pending:
+            ops.fill_pending(t_ids, t_src, prev.ids_dev)
         bt = self.slots.table.index_select(0, t_req)
         meta = AttnMeta("prefill", t_pos, t_slots, bt, cu_q=t_cu, kv_lens=t_kv, items=t_items)
         hidden = self.model.forward(t_ids, meta, self.kv)
@@ -310,15 +376,13 @@ class ModelRunner:
         top_k = torch.tensor([c.req.params.top_k for c in batch.chunks], dtype=torch.int32)
         top_p = torch.tensor([c.req.params.top_p for c in batch.chunks], dtype=torch.float32)
         min_p = torch.tensor([c.req.params.min_p for c in batch.chunks], dtype=torch.float32)
+        sv = [self._seed(c.req, c.start + c.length) for c in batch.chunks]
+        seeds = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in sv], dtype=torch.int64)
         if self.is_cuda:
-            sv = [self._seed(c.req, c.start + c.length) for c in batch.chunks]
-            seeds = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in sv], dtype=torch.int64)
             temp, top_k, top_p, min_p, seeds = (x.to(self.device, non_blocking=True)
                                                 for x in (temp, top_k, top_p, min_p, seeds))
-            out_ids, out_lp = ops.sample(logits, temp, top_k, top_p, min_p, seeds, 0)
-        else:
-            out_ids, out_lp = ops.sample(logits, temp, top_k, top_p, min_p)
-        return out_ids.cpu().tolist(), out_lp.cpu().tolist()
+        out_ids, out_lp = ops.sample(logits, temp, top_k, top_p, min_p, seeds, 0)
+        return self._finish_launch(out_ids.to(torch.int32), out_lp, S)
 
     def embed(self, batch: StepBatch) -> list[list[float]]:
         """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts."""

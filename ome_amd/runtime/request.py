@@ -46,6 +46,10 @@ class ReqState(enum.Enum):
 
 _rid = itertools.count()
 
+# Placeholder for a token that was sampled on the GPU by an in-flight step but has not reached
+# the host yet (overlapped scheduling); replaced in the step's final commit.
+PENDING = -1
+
 
 @dataclass(eq=False)
 class Request:
@@ -71,6 +75,8 @@ class Request:
     is_embedding: bool = False
     preempted: int = 0
     lora: str | None = None
+    n_pending: int = 0             # placeholders in output_ids awaiting their sampled token
+    pending_row: int = -1          # row of the newest pending token in its step's sampled output
 
     @property
     def all_ids(self) -> list[int]:

@@ -17,7 +17,7 @@ import collections
 from dataclasses import dataclass, field
 
 from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
-from ome_amd.runtime.request import ReqState, Request
+from ome_amd.runtime.request import PENDING, ReqState, Request
 
 
 @dataclass
@@ -26,6 +26,7 @@ class ScheduledChunk:
     start: int      # first token index computed this step
     length: int     # tokens computed this step
     sample: bool    # last row produces a new token
+    out_index: int = -1   # index in req.output_ids the sampled token lands at (set at launch)
 
 
 @dataclass
@@ -123,9 +124,10 @@ class Scheduler:
         self._release(req, cache_prefix=True)
 
     def _preempt_one(self, keep: Request | None = None) -> bool:
-        # newest admitted first (LIFO), never the request we are trying to serve
+        # newest admitted first (LIFO), never the request we are trying to serve, never one whose
+        # sampled token is still in flight (its recompute would need that token)
         for r in reversed(self.running):
-            if r is keep:
+            if r is keep or r.n_pending:
                 continue
             self.running.remove(r)
             self._release(r)
@@ -193,15 +195,19 @@ class Scheduler:
     def _add_decodes(self, batch: StepBatch) -> None:
         inb = {id(c.req) for c in batch.chunks}
         for r in self.running:
-            if id(r) in inb or not r.prefill_done:
+            if id(r) in inb or not r.prefill_done or self._exhausted(r):
                 continue
             if self._grow(r, r.seq_len):
                 batch.chunks.append(ScheduledChunk(r, r.seq_len - 1, 1, True))
 
+    def _exhausted(self, r: Request) -> bool:
+        """Every token this request may produce is already scheduled (incl. in-flight ones)."""
+        return len(r.output_ids) >= r.params.max_new_tokens or r.seq_len >= self.max_context
+
     def _schedule_decode(self) -> StepBatch | None:
         chunks = []
         for r in list(self.running):
-            if r.state != ReqState.RUNNING or not r.prefill_done:
+            if r.state != ReqState.RUNNING or not r.prefill_done or self._exhausted(r):
                 continue
             while not self._grow(r, r.seq_len):
                 if not self._preempt_one(keep=r):
@@ -212,17 +218,34 @@ class Scheduler:
         return StepBatch("decode", chunks) if chunks else None
 
     # ------------------------------------------------------------------ post-step
-    def commit(self, batch: StepBatch, next_ids: list[int], logprobs: list[float] | None, now: float,
-               eos_ids: set[int]) -> list[Request]:
-        """Apply a finished step; returns requests that finished in it."""
-        done = []
+    def launch_commit(self, batch: StepBatch) -> None:
+        """Phase 1, right after the step is enqueued on the GPU: advance the KV watermark and
+        reserve a PENDING output slot for every sampled row, so the next step can be scheduled
+        (and enqueued) before this step's tokens reach the host."""
         for i, c in enumerate(batch.chunks):
             r = c.req
             r.num_cached = c.start + c.length
-            if not c.sample or r.state != ReqState.RUNNING:
+            if c.sample and r.state == ReqState.RUNNING:
+                c.out_index = len(r.output_ids)
+                r.output_ids.append(PENDING)
+                r.n_pending += 1
+                r.pending_row = i
+
+    def final_commit(self, batch: StepBatch, next_ids: list[int], logprobs: list[float] | None, now: float,
+                     eos_ids: set[int]) -> list[Request]:
+        """Phase 2, once the step's sampled ids are on the host: fill the PENDING slots, stream
+        tokens, finish requests.  A request that finishes here may already sit in the next
+        in-flight step as a dead row; its trailing placeholders are dropped and its pages are
+        released — safe, because everything that could reuse them is enqueued later on the
+        same stream."""
+        done = []
+        for i, c in enumerate(batch.chunks):
+            r = c.req
+            if c.out_index < 0 or r.state != ReqState.RUNNING:
                 continue
+            r.n_pending -= 1
             tok = int(next_ids[i])
-            r.output_ids.append(tok)
+            r.output_ids[c.out_index] = tok
             if logprobs is not None:
                 r.output_logprobs.append(float(logprobs[i]))
             r.token_times.append(now)
@@ -230,15 +253,26 @@ class Scheduler:
                 r.first_token_time = now
             reason = None
             p = r.params
-            if len(r.output_ids) >= p.max_new_tokens:
+            n_out = c.out_index + 1
+            if n_out >= p.max_new_tokens:
                 reason = "length"
             elif not p.ignore_eos and (tok in eos_ids or tok in p.stop_token_ids):
                 reason = "stop"
-            elif r.seq_len >= self.max_context:
+            elif len(r.prompt_ids) + n_out >= self.max_context:
                 reason = "length"
             if reason:
+                if len(r.output_ids) > n_out:  # speculative rows already launched past the end
+                    del r.output_ids[n_out:]
+                    r.n_pending = 0
+                    r.num_cached = min(r.num_cached, r.seq_len)
                 self.finish(r, reason)
                 done.append(r)
             if r.on_token is not None:
                 r.on_token(r, [tok], reason is not None)
         return done
+
+    def commit(self, batch: StepBatch, next_ids: list[int], logprobs: list[float] | None, now: float,
+               eos_ids: set[int]) -> list[Request]:
+        """Synchronous (non-overlapped) commit: both phases at once."""
+        self.launch_commit(batch)
+        return self.final_commit(batch, next_ids, logprobs, now, eos_ids)

@@ -52,6 +52,7 @@ def build_parser() -> argparse.ArgumentParser:
     a("--is-embedding", action="store_true")
     a("--disable-radix-cache", action="store_true")
     a("--disable-cuda-graph", action="store_true")
+    a("--disable-overlap-schedule", action="store_true")
     a("--cuda-graph-max-bs", type=int, default=None)
     a("--enable-mixed-chunk", action="store_true")
     a("--load-format", default="auto")
@@ -90,7 +91,8 @@ def engine_args_from(ns, rank_tp: int | None = None):
                       disable_radix_cache=ns.disable_radix_cache, is_embedding=ns.is_embedding,
                       kv_cache_dtype=ns.kv_cache_dtype, dist_init_addr=ns.dist_init_addr, nnodes=ns.nnodes,
                       node_rank=ns.node_rank, disaggregation_mode=ns.disaggregation_mode,
-                      num_layers_override=ns.num_layers)
+                      num_layers_override=ns.num_layers,
+                      overlap_schedule=False if ns.disable_overlap_schedule else None)
 
 
 # ------------------------------------------------------------------ request plumbing
