@@ -18,6 +18,8 @@
 // MFMA from registers with no lane movement (the "accumulator as next operand" idiom).
 #include "common.h"
 
+#include <cstdlib>
+
 #ifndef OME_NEG_INF
 #define OME_NEG_INF (-__builtin_inff())
 #endif
@@ -193,6 +195,190 @@ __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const int* __res
   out[(int64_t)b * out_stride + (int64_t)head * D + d] = (bf16)(L > 0.f ? acc / L : 0.f);
 }
 
+// ------------------------------------------------------------------------------------------
+// Decode v2 (default): same math and layouts as v1, re-scheduled for HBM streaming.
+//  * a tile's K AND V fragments are issued together (one memory round trip per 32-key tile,
+//    not two), and the next tile of the wave is issued before the current one is consumed
+//    (2-deep register ring, counted vmcnt by the compiler): ~32 KB in flight per wave;
+//  * the LDS merge stores only the G live query heads (8.5 KB for G=4 instead of 33 KB), so
+//    occupancy is set by VGPRs, not LDS.
+// ------------------------------------------------------------------------------------------
+template <int D>
+struct KVTile {
+  bf16x8 ka[D / 32], kb[D / 32];
+  bf16x4 va[D / 16], vb[D / 16];
+};
+
+template <int D, int P>
+__device__ __forceinline__ void kv_tile_load(KVTile<D>& t, const bf16* __restrict__ k_cache,
+                                             const bf16* __restrict__ v_cache, const int* __restrict__ bt, int kb,
+                                             int seq_len, int64_t kpage, int kvh, int n, int g) {
+  const int pA = bt[kb / P];
+  const int pB = (kb + P < seq_len) ? bt[kb / P + 1] : pA;
+  const bf16* kA = k_cache + pA * kpage + (int64_t)kvh * P * D;
+  const bf16* kB = k_cache + pB * kpage + (int64_t)kvh * P * D;
+  const bf16* vA = v_cache + pA * kpage + (int64_t)kvh * D * P;
+  const bf16* vB = v_cache + pB * kpage + (int64_t)kvh * D * P;
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    t.ka[ks] = ld8(kA + n * D + 32 * ks + 8 * g);
+    t.kb[ks] = ld8(kB + n * D + 32 * ks + 8 * g);
+  }
+#pragma unroll
+  for (int nb = 0; nb < D / 16; ++nb) {
+    const int dim = 16 * nb + n;
+    t.va[nb] = ld4(vA + dim * P + 4 * g);
+    t.vb[nb] = ld4(vB + dim * P + 4 * g);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void kv_tile_compute(const KVTile<D>& t, const bf16x8 (&qf)[D / 32], f32x4 (&o)[D / 16],
+                                                float& m_i, float& l_i, int kb, int p_end, int lo, float scale_log2,
+                                                int g) {
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    s0 = mfma16(t.ka[ks], qf[ks], s0);
+    s1 = mfma16(t.kb[ks], qf[ks], s1);
+  }
+  float mt = OME_NEG_INF;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k0 = kb + 4 * g + i, k1 = k0 + 16;
+    s0[i] = (k0 < p_end && k0 >= lo) ? s0[i] * scale_log2 : OME_NEG_INF;
+    s1[i] = (k1 < p_end && k1 >= lo) ? s1[i] * scale_log2 : OME_NEG_INF;
+    mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
+  }
+  mt = fmaxf(mt, __shfl_xor(mt, 16));
+  mt = fmaxf(mt, __shfl_xor(mt, 32));
+  const float m_new = fmaxf(m_i, mt);
+  const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
+  const float alpha = fast_exp2(m_i - m_use);
+  bf16x8 pb;
+  float rs = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float p0 = fast_exp2(s0[i] - m_use), p1 = fast_exp2(s1[i] - m_use);
+    pb[i] = (bf16)p0;
+    pb[4 + i] = (bf16)p1;
+    rs += p0 + p1;
+  }
+  rs += __shfl_xor(rs, 16);
+  rs += __shfl_xor(rs, 32);
+  l_i = l_i * alpha + rs;
+  m_i = m_new;
+#pragma unroll
+  for (int nb = 0; nb < D / 16; ++nb) {
+    o[nb] = o[nb] * alpha;
+    o[nb] = mfma16(cat44(t.va[nb], t.vb[nb]), pb, o[nb]);
+  }
+}
+
+template <int D, int P, bool PF>
+__global__ __launch_bounds__(256) void paged_decode_v2_kernel(
+    const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ seq_lens, bf16* __restrict__ out, int64_t out_stride, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2, int window) {
+  static_assert(P == 16, "decode kernel assumes 16-token pages");
+  constexpr int NB = D / 16, KS = D / 32;
+  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int seq_len = seq_lens[b];
+  const int p_start = part * part_size;
+  if (p_start >= seq_len) return;
+  const int p_end = min(seq_len, p_start + part_size);
+  const int G = Hq / Hkv;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n = lane & 15, g = lane >> 4;
+  const int lo = window > 0 ? max(0, seq_len - window) : 0;
+
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sm_m = smem;              // [4][G]
+  float* sm_l = smem + 4 * G;      // [4][G]
+  float* sm_o = smem + 8 * G;      // [4][G][D]
+
+  bf16x8 qf[KS];
+  {
+    const bf16* qh = q + (int64_t)b * q_stride + (int64_t)(kvh * G + n) * D;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = (n < G) ? ld8(qh + 32 * ks + 8 * g) : bf16x8{};
+  }
+  float m_i = OME_NEG_INF, l_i = 0.f;
+  f32x4 o[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) o[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int* bt = block_tables + (int64_t)b * bt_stride;
+  const int64_t kpage = (int64_t)Hkv * P * D;
+  int kb = p_start + wave * 32;
+  if (lo > 0) {  // sliding window: skip whole tiles before the window
+    while (kb + 32 <= lo && kb < p_end) kb += 128;
+  }
+  if (!PF) {
+    for (; kb < p_end; kb += 128) {
+      KVTile<D> t;
+      kv_tile_load<D, P>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
+      kv_tile_compute<D>(t, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
+    }
+  } else if (kb < p_end) {
+    KVTile<D> t0, t1;
+    kv_tile_load<D, P>(t0, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
+    for (;;) {
+      const int kn = kb + 128;
+      const bool more = kn < p_end;
+      if (more) kv_tile_load<D, P>(t1, k_cache, v_cache, bt, kn, seq_len, kpage, kvh, n, g);
+      kv_tile_compute<D>(t0, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
+      if (!more) break;
+      const int kn2 = kn + 128;
+      const bool more2 = kn2 < p_end;
+      if (more2) kv_tile_load<D, P>(t0, k_cache, v_cache, bt, kn2, seq_len, kpage, kvh, n, g);
+      kv_tile_compute<D>(t1, qf, o, m_i, l_i, kn, p_end, lo, scale_log2, g);
+      if (!more2) break;
+      kb = kn2;
+    }
+  }
+  // ---- merge the 4 waves' states (only the G live heads) ----
+  if (g == 0 && n < G) {
+    sm_m[wave * G + n] = m_i;
+    sm_l[wave * G + n] = l_i;
+  }
+  if (n < G) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sm_o[(wave * G + n) * D + 16 * nb + 4 * g + i] = o[nb][i];
+  }
+  __syncthreads();
+  const int nparts = (seq_len + part_size - 1) / part_size;
+  for (int idx = threadIdx.x; idx < G * D; idx += 256) {
+    const int h = idx / D, d = idx % D;
+    float M = OME_NEG_INF;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, sm_m[w * G + h]);
+    const float Mu = (M == OME_NEG_INF) ? 0.f : M;
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float f = fast_exp2(sm_m[w * G + h] - Mu);
+      L += sm_l[w * G + h] * f;
+      acc += sm_o[(w * G + h) * D + d] * f;
+    }
+    const int head = kvh * G + h;
+    const float res = L > 0.f ? acc / L : 0.f;
+    if (nparts == 1) {
+      out[(int64_t)b * out_stride + (int64_t)head * D + d] = (bf16)res;
+    } else {
+      const int64_t pidx = ((int64_t)b * Hq + head) * max_parts + part;
+      part_o[pidx * D + d] = res;
+      if (d == 0) {
+        part_ml[pidx * 2 + 0] = M;
+        part_ml[pidx * 2 + 1] = L;
+      }
+    }
+  }
+}
+
 OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                              const int* block_tables, int bt_stride, const int* seq_lens, void* out,
                              int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
@@ -202,11 +388,22 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
   if (part_size % 128 != 0 || max_parts <= 0) return -4;
   const float scale_log2 = scale * 1.4426950408889634f;
-  const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
   dim3 grid(max_parts, Hkv, B);
-  paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(
-      (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, seq_lens,
-      (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window);
+  const char* ve = getenv("OME_DECODE_ATTN");  // A/B switch for benchmarking (default v2)
+  const int variant = ve ? atoi(ve) : 2;
+  if (variant == 1) {
+    const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
+    paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(
+        (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, seq_lens,
+        (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window);
+  } else {
+    const int G = Hq / Hkv;
+    const size_t smem = (8 * G + 4 * G * D) * sizeof(float);
+    auto kern = variant == 3 ? paged_decode_v2_kernel<128, 16, false> : paged_decode_v2_kernel<128, 16, true>;
+    kern<<<grid, 256, smem, stream>>>(
+        (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, seq_lens,
+        (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window);
+  }
   OME_CHECK_LAUNCH();
   if (max_parts > 1) {
     paged_decode_reduce_kernel<128><<<dim3(Hq, B), 128, 0, stream>>>(seq_lens, (const float*)part_o,

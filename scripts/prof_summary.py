@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace run (CSV) into markdown: top kernels, per-category
+time per engine step (one sample kernel launch == one step), and GEMM shapes by grid."""
+import collections
+import csv
+import sys
+from pathlib import Path
+
+CATS = [("gemm", ("Cijk_", "Custom_Cijk", "gemm", "Gemm")), ("attn_decode", ("paged_decode",)),
+        ("attn_prefill", ("paged_prefill",)), ("rope_kv", ("rope_qkv", "kv_cache_write")),
+        ("norm", ("rmsnorm",)), ("act", ("act_and_mul",)), ("sample", ("sample_kernel",)),
+        ("embed", ("embedding_kernel",)), ("copy", ("copyBuffer", "fill_pending", "Fill", "index")),
+        ("comm", ("rccl", "nccl", "allreduce", "AllReduce"))]
+
+
+def cat_of(name: str) -> str:
+    for c, keys in CATS:
+        if any(k in name for k in keys):
+            return c
+    return "other"
+
+
+def short(name: str, n: int = 90) -> str:
+    return name if len(name) <= n else name[:n] + "…"
+
+
+def main(d: str, last_steps: int = 0) -> None:
+    d = Path(d)
+    trace = next(d.rglob("*kernel_trace.csv"))
+    rows = list(csv.DictReader(open(trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    if last_steps:  # keep only the window covering the last N engine steps (the timed region)
+        marks = [i for i, r in enumerate(rows) if "sample_kernel" in r["Kernel_Name"]]
+        if len(marks) > last_steps:
+            rows = rows[marks[-last_steps - 1] + 1:]
+    tot = collections.Counter()
+    cnt = collections.Counter()
+    cat = collections.Counter()
+    grids = collections.Counter()
+    gcnt = collections.Counter()
+    steps = 0
+    t_first, t_last = None, None
+    for r in rows:
+        name = r["Kernel_Name"]
+        dt = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        t_first = s if t_first is None else min(t_first, s)
+        t_last = e if t_last is None else max(t_last, e)
+        tot[name] += dt
+        cnt[name] += 1
+        c = cat_of(name)
+        cat[c] += dt
+        if c == "gemm":
+            key = f"{short(name, 60)} grid=({r['Grid_Size_X']},{r['Grid_Size_Y']},{r['Grid_Size_Z']})"
+            grids[key] += dt
+            gcnt[key] += 1
+        if "sample_kernel" in name:
+            steps += 1
+    busy = sum(tot.values())
+    print(f"# Kernel summary: {trace.parent.name}\n")
+    print(f"kernels: {len(rows)}, busy {busy / 1e6:.1f} ms over {(t_last - t_first) / 1e6:.1f} ms wall "
+          f"({100 * busy / max(1, t_last - t_first):.0f}% GPU busy), engine steps (sample launches): {steps}\n")
+    print("## By category (per step = total / steps)\n\n| category | total ms | % | per step us |\n|---|---:|---:|---:|")
+    for c, v in cat.most_common():
+        print(f"| {c} | {v / 1e6:.2f} | {100 * v / busy:.1f} | {v / 1e3 / max(1, steps):.1f} |")
+    print("\n## Top kernels\n\n| total ms | % | calls | avg us | kernel |\n|---:|---:|---:|---:|---|")
+    for n, v in tot.most_common(25):
+        print(f"| {v / 1e6:.2f} | {100 * v / busy:.1f} | {cnt[n]} | {v / cnt[n] / 1e3:.1f} | `{short(n)}` |")
+    print("\n## GEMMs by kernel+grid\n\n| total ms | calls | avg us | kernel / grid |\n|---:|---:|---:|---|")
+    for n, v in grids.most_common(20):
+        print(f"| {v / 1e6:.2f} | {gcnt[n]} | {v / gcnt[n] / 1e3:.1f} | `{n}` |")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 0)
