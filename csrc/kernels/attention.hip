@@ -280,10 +280,13 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ seq_lens, bf16* __restrict__ out, int64_t out_stride, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2, int window) {
+    float* __restrict__ part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2, int window,
+    const int* __restrict__ order) {
   static_assert(P == 16, "decode kernel assumes 16-token pages");
   constexpr int NB = D / 16, KS = D / 32;
-  const int part = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  // blockIdx.z walks sequences longest-first when the host provides ``order`` (the dispatcher
+  // hands out workgroups in grid order, so the long tail starts first instead of last)
+  const int part = blockIdx.x, kvh = blockIdx.y, b = order ? order[blockIdx.z] : blockIdx.z;
   const int seq_len = seq_lens[b];
   const int p_start = part * part_size;
   if (p_start >= seq_len) return;
@@ -382,7 +385,8 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
 OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                              const int* block_tables, int bt_stride, const int* seq_lens, void* out,
                              int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
-                             int part_size, int max_parts, float scale, int window, hipStream_t stream) {
+                             int part_size, int max_parts, float scale, int window, const int* order,
+                             hipStream_t stream) {
   if (B <= 0) return 0;
   if (D != 128 || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
@@ -390,7 +394,7 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(max_parts, Hkv, B);
   const char* ve = getenv("OME_DECODE_ATTN");  // A/B switch for benchmarking (default v2)
-  const int variant = ve ? atoi(ve) : 2;
+  const int variant = ve ? atoi(ve) : 3;
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
     paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(
@@ -399,10 +403,11 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   } else {
     const int G = Hq / Hkv;
     const size_t smem = (8 * G + 4 * G * D) * sizeof(float);
-    auto kern = variant == 3 ? paged_decode_v2_kernel<128, 16, false> : paged_decode_v2_kernel<128, 16, true>;
+    auto kern = variant == 2 ? paged_decode_v2_kernel<128, 16, true> : paged_decode_v2_kernel<128, 16, false>;
     kern<<<grid, 256, smem, stream>>>(
         (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, seq_lens,
-        (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window);
+        (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window,
+        order);
   }
   OME_CHECK_LAUNCH();
   if (max_parts > 1) {

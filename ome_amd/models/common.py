@@ -27,6 +27,7 @@ class AttnMeta:
     items: torch.Tensor | None = None
     logits_idx: torch.Tensor | None = None
     decode_ws: ops.DecodeWorkspace | None = None
+    order: torch.Tensor | None = None      # decode: sequences longest-first (workgroup dispatch order)
     extra: dict = field(default_factory=dict)
 
     @property

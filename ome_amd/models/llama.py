@@ -196,7 +196,7 @@ class LlamaForCausalLM:
     def attention(self, q: torch.Tensor, k_cache, v_cache, meta: AttnMeta) -> torch.Tensor:
         if meta.is_decode:
             return ops.paged_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale,
-                                    meta.decode_ws, self.window)
+                                    meta.decode_ws, self.window, order=meta.order)
         return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
                                  self.scale, self.window)
 

@@ -113,8 +113,9 @@ class DecodeWorkspace:
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeWorkspace | None = None,
-                 window: int = -1, out=None) -> torch.Tensor:
-    """q [B, Hq, D] -> [B, Hq, D]."""
+                 window: int = -1, out=None, order: torch.Tensor | None = None) -> torch.Tensor:
+    """q [B, Hq, D] -> [B, Hq, D].  ``order`` (int32 [B], optional): sequence visit order for the
+    workgroup dispatcher (longest first balances the tail)."""
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window)
         if out is not None:
@@ -129,7 +130,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeW
     call("ome_paged_decode", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(seq_lens).data_ptr(), out.data_ptr(),
          out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
-         float(scale), int(window), stream_ptr())
+         float(scale), int(window), _i32(order).data_ptr() if order is not None else None, stream_ptr())
     return out
 
 

@@ -32,7 +32,7 @@ _SIGNATURES = {
         "ome_pool": [vp, vp, vp, i32, i32, i32, i32, vp],
         "ome_fill_pending": [vp, vp, vp, i32, vp],
         "ome_paged_decode": [vp, i64, vp, vp, vp, i32, vp, vp, i64, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32,
-                             i32, vp],
+                             i32, vp, vp],
         "ome_paged_prefill": [vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, vp, i64, i32, i32, i32, i32, f32, i32, vp],
         "ome_sample": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, u64, vp, vp, vp],
     },

@@ -45,7 +45,7 @@ def default_buckets(max_bs: int) -> list[int]:
 
 
 class _DecodeBuffers:
-    FIELDS_I = ("ids", "pos", "slots", "seq_lens", "req_idx", "top_k", "src")
+    FIELDS_I = ("ids", "pos", "slots", "seq_lens", "req_idx", "top_k", "src", "order")
     FIELDS_F = ("temp", "top_p", "min_p")
 
     def __init__(self, bmax: int, device):
@@ -163,7 +163,7 @@ class ModelRunner:
         d = self.dbuf
         bt = self.slots.table.index_select(0, d.view("req_idx", bs))
         meta = AttnMeta("decode", d.view("pos", bs), d.view("slots", bs), bt, seq_lens=d.view("seq_lens", bs),
-                        decode_ws=self.decode_ws(bs))
+                        decode_ws=self.decode_ws(bs), order=d.view("order", bs))
         hidden = self.model.forward(d.view("ids", bs), meta, self.kv)
         logits = self.model.compute_logits(hidden)
         ops.sample(logits, d.view("temp", bs), d.view("top_k", bs), d.view("top_p", bs), d.view("min_p", bs),
@@ -309,6 +309,8 @@ class ModelRunner:
             hf[off["temp"] + i] = 0.0
             hf[off["top_p"] + i] = 1.0
             h[off["top_k"] + i] = -1
+        # attention visits sequences longest-first (padding rows, seq_len 0, last)
+        h[off["order"]:off["order"] + bs] = np.argsort(-h[off["seq_lens"]:off["seq_lens"] + bs], kind="stable")
         d.dev.copy_(d.host, non_blocking=True)
         if any_pending:
             ops.fill_pending(d.view("ids", bs), d.view("src", bs), prev.ids_dev)

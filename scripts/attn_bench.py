@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--variants", default="1,2,3")
     ap.add_argument("--parts", default="4096,1024,512,256")
     ap.add_argument("--ctx", type=int, default=0, help="fixed context (0 = bench distribution)")
+    ap.add_argument("--pool-pages", type=int, default=0, help="scatter pages over a pool this large (TLB test)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     rng = random.Random(0)
@@ -32,11 +33,10 @@ def main():
             o = max(1, int(rng.gauss(300, 150)))
             lens.append(i + rng.randrange(0, o))
     maxpg = max(-(-L // P) for L in lens) + 1
-    npages = sum(-(-L // P) for L in lens) + 8
+    npages = max(sum(-(-L // P) for L in lens) + 8, a.pool_pages)
     kc = torch.randn(npages, Hkv, P, D, device=dev, dtype=torch.bfloat16)
     vc = torch.randn(npages, Hkv, D, P, device=dev, dtype=torch.bfloat16)
-    perm = list(range(1, npages))
-    rng.shuffle(perm)
+    perm = rng.sample(range(1, npages), sum(-(-L // P) for L in lens))
     bt = torch.zeros(B, maxpg, dtype=torch.int32)
     o = 0
     for b, L in enumerate(lens):

@@ -106,7 +106,9 @@ def _block_tables(seq_lens, P, num_pages):
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16)])
 @pytest.mark.parametrize("seq_lens", [[1], [15, 16, 17, 33], [100, 1000, 3, 517], [5000, 7]])
 @pytest.mark.parametrize("part_size", [256, 8192])
-def test_paged_decode(Hq, Hkv, seq_lens, part_size):
+@pytest.mark.parametrize("variant", ["1", "2", "3"])
+def test_paged_decode(Hq, Hkv, seq_lens, part_size, variant, monkeypatch):
+    monkeypatch.setenv("OME_DECODE_ATTN", variant)
     D, P = 128, 16
     npages = sum(-(-L // P) for L in seq_lens) + 8
     kc, vc = _cache(npages, Hkv, D)
@@ -116,10 +118,16 @@ def test_paged_decode(Hq, Hkv, seq_lens, part_size):
     ws = ops.DecodeWorkspace(len(seq_lens), Hq, D, 8192, part_size, DEV)
     scale = 1 / math.sqrt(D)
     out = ops.paged_decode(q, kc, vc, bt, sl, scale, ws)
-    _close(out, ref.paged_decode(q, kc, vc, bt, sl, scale), atol=2e-2)
+    expect = ref.paged_decode(q, kc, vc, bt, sl, scale)
+    _close(out, expect, atol=2e-2)
+    if variant != "1":  # longest-first visit order must not change the result
+        order = torch.argsort(sl, descending=True).to(torch.int32)
+        _close(ops.paged_decode(q, kc, vc, bt, sl, scale, ws, order=order), expect, atol=2e-2)
 
 
-def test_paged_decode_window():
+@pytest.mark.parametrize("variant", ["1", "2", "3"])
+def test_paged_decode_window(variant, monkeypatch):
+    monkeypatch.setenv("OME_DECODE_ATTN", variant)
     D, P, Hq, Hkv = 128, 16, 32, 8
     seq_lens = [700, 40]
     kc, vc = _cache(64, Hkv, D)
