@@ -15,6 +15,10 @@ class AttnMeta:
     decode:  one query token per sequence, ``seq_lens`` includes the new token.
     prefill: any mix of prompt chunks / single-token rows; sequence ``s`` owns query rows
              ``cu_q[s]:cu_q[s+1]`` at absolute positions ``kv_lens[s]-q_len .. kv_lens[s]-1``.
+    mixed:   rows ``[0, num_prefill)`` are prefill chunks (``cu_q``/``kv_lens``/``items``/
+             ``block_tables``), rows ``[num_prefill, T)`` are single-token decode rows run by the
+             GQA-sharing decode kernel (``seq_lens``/``dec_block_tables``/``order``/``decode_ws``)
+             — so decodes riding along a prefill step cost decode-kernel KV traffic, not G x it.
     """
 
     mode: str
@@ -28,6 +32,8 @@ class AttnMeta:
     logits_idx: torch.Tensor | None = None
     decode_ws: ops.DecodeWorkspace | None = None
     order: torch.Tensor | None = None      # decode: sequences longest-first (workgroup dispatch order)
+    num_prefill: int = 0                   # mixed: rows before this index are prefill rows
+    dec_block_tables: torch.Tensor | None = None
     extra: dict = field(default_factory=dict)
 
     @property

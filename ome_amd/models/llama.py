@@ -197,6 +197,14 @@ class LlamaForCausalLM:
         if meta.is_decode:
             return ops.paged_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale,
                                     meta.decode_ws, self.window, order=meta.order)
+        if meta.mode == "mixed":
+            n = meta.num_prefill
+            out = torch.empty_like(q)
+            ops.paged_prefill(q[:n], k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
+                              self.scale, self.window, out=out[:n])
+            ops.paged_decode(q[n:], k_cache, v_cache, meta.dec_block_tables, meta.seq_lens, self.scale,
+                             meta.decode_ws, self.window, out=out[n:], order=meta.order)
+            return out
         return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
                                  self.scale, self.window)
 

@@ -321,17 +321,24 @@ class ModelRunner:
         return self._finish_launch(self.out_ids, self.out_lp, B)
 
     def _launch_eager(self, batch: StepBatch, prev: "StepHandle | None") -> "StepHandle":
+        """Eager step for prefill / mixed batches.  Token rows are laid out prefill chunks first,
+        then single-token rows (decodes riding along, or 1-token prompt tails), which attention
+        routes to the decode kernel; sampled rows keep ``batch.chunks`` order."""
         P = self.P
-        ids, pos, slots, q_lens, kv_lens, req_idx, sample_rows, src = [], [], [], [], [], [], [], []
+        chunks = batch.chunks
+        pre = [i for i, c in enumerate(chunks) if c.length > 1]
+        dec = [i for i, c in enumerate(chunks) if c.length == 1]
+        ids, pos, slots, q_lens, kv_lens, req_idx, src = [], [], [], [], [], [], []
+        dec_lens, dec_req = [], []
+        last_row = [0] * len(chunks)
         any_pending = False
-        for c in batch.chunks:
+        for i in pre + dec:
+            c = chunks[i]
             r = c.req
             t0 = len(ids)
-            toks = r.all_ids[c.start:c.start + c.length]
-            ids.extend(toks)
+            ids.extend(r.all_ids[c.start:c.start + c.length])
             src.extend([-1] * c.length)
-            last = c.start + c.length - 1
-            s_row = self._src_row(r, last, prev)
+            s_row = self._src_row(r, c.start + c.length - 1, prev)
             if s_row >= 0:
                 src[t0 + c.length - 1] = s_row
                 ids[t0 + c.length - 1] = 0
@@ -340,17 +347,24 @@ class ModelRunner:
             pos.extend(pp)
             pages = r.pages
             slots.extend(pages[x // P] * P + x % P for x in pp)
-            q_lens.append(c.length)
-            kv_lens.append(c.start + c.length)
-            req_idx.append(r.req_slot)
-            sample_rows.append(len(ids) - 1)
-        items = ops.prefill_work_items(q_lens, kv_lens)
-        T, S, n_it = len(ids), len(q_lens), len(items)
+            if c.length > 1:
+                q_lens.append(c.length)
+                kv_lens.append(c.start + c.length)
+                req_idx.append(r.req_slot)
+            else:
+                dec_lens.append(c.start + 1)
+                dec_req.append(r.req_slot)
+            last_row[i] = len(ids) - 1
+        items = ops.prefill_work_items(q_lens, kv_lens) if q_lens else []
+        T, S, n_it, nd = len(ids), len(q_lens), len(items), len(dec_lens)
         cu = np.zeros(S + 1, dtype=np.int32)
         cu[1:] = np.cumsum(q_lens)
+        dec_order = np.argsort(-np.asarray(dec_lens, np.int64), kind="stable").astype(np.int32) if nd else \
+            np.zeros(0, np.int32)
         packed = np.concatenate([np.asarray(ids, np.int32), np.asarray(pos, np.int32), np.asarray(slots, np.int32),
                                  cu, np.asarray(kv_lens, np.int32), np.asarray(req_idx, np.int32),
-                                 np.asarray(sample_rows, np.int32), np.asarray(src, np.int32),
+                                 np.asarray(last_row, np.int32), np.asarray(src, np.int32),
+                                 np.asarray(dec_lens, np.int32), np.asarray(dec_req, np.int32), dec_order,
                                  np.asarray(items, np.int32).reshape(-1) if n_it else np.zeros(0, np.int32)])
         host = torch.from_numpy(packed)
         if self.is_cuda:
@@ -365,26 +379,40 @@ class ModelRunner:
             return t
 
         t_ids, t_pos, t_slots = take(T), take(T), take(T)
-        t_cu, t_kv, t_req, t_rows = take(S + 1), take(S), take(S), take(S)
+        t_cu, t_kv, t_req, t_rows = take(S + 1), take(S), take(S), take(len(chunks))
         t_src = take(T)
+        t_dlen, t_dreq, t_dord = take(nd), take(nd), take(nd)
         t_items = take(2 * n_it).view(n_it, 2)
         if any_pending:
             ops.fill_pending(t_ids, t_src, prev.ids_dev)
-        bt = self.slots.table.index_select(0, t_req)
-        meta = AttnMeta("prefill", t_pos, t_slots, bt, cu_q=t_cu, kv_lens=t_kv, items=t_items)
+        ws = None
+        if nd:
+            bucket = next((b for b in self.buckets if b >= nd), None)
+            ws = self.decode_ws(bucket) if bucket is not None else ops.DecodeWorkspace(
+                nd, self.model.tp.hq, self.cfg.head_dim, self.max_context + self.P, 512, self.device)
+        if S and nd:
+            meta = AttnMeta("mixed", t_pos, t_slots, self.slots.table.index_select(0, t_req), seq_lens=t_dlen,
+                            cu_q=t_cu, kv_lens=t_kv, items=t_items, decode_ws=ws, order=t_dord,
+                            num_prefill=int(cu[-1]), dec_block_tables=self.slots.table.index_select(0, t_dreq))
+        elif S:
+            meta = AttnMeta("prefill", t_pos, t_slots, self.slots.table.index_select(0, t_req), cu_q=t_cu,
+                            kv_lens=t_kv, items=t_items)
+        else:
+            meta = AttnMeta("decode", t_pos, t_slots, self.slots.table.index_select(0, t_dreq), seq_lens=t_dlen,
+                            decode_ws=ws, order=t_dord)
         hidden = self.model.forward(t_ids, meta, self.kv)
         logits = self.model.compute_logits(hidden.index_select(0, t_rows))
-        temp = torch.tensor([c.req.params.temperature for c in batch.chunks], dtype=torch.float32)
-        top_k = torch.tensor([c.req.params.top_k for c in batch.chunks], dtype=torch.int32)
-        top_p = torch.tensor([c.req.params.top_p for c in batch.chunks], dtype=torch.float32)
-        min_p = torch.tensor([c.req.params.min_p for c in batch.chunks], dtype=torch.float32)
-        sv = [self._seed(c.req, c.start + c.length) for c in batch.chunks]
+        temp = torch.tensor([c.req.params.temperature for c in chunks], dtype=torch.float32)
+        top_k = torch.tensor([c.req.params.top_k for c in chunks], dtype=torch.int32)
+        top_p = torch.tensor([c.req.params.top_p for c in chunks], dtype=torch.float32)
+        min_p = torch.tensor([c.req.params.min_p for c in chunks], dtype=torch.float32)
+        sv = [self._seed(c.req, c.start + c.length) for c in chunks]
         seeds = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in sv], dtype=torch.int64)
         if self.is_cuda:
             temp, top_k, top_p, min_p, seeds = (x.to(self.device, non_blocking=True)
                                                 for x in (temp, top_k, top_p, min_p, seeds))
         out_ids, out_lp = ops.sample(logits, temp, top_k, top_p, min_p, seeds, 0)
-        return self._finish_launch(out_ids.to(torch.int32), out_lp, S)
+        return self._finish_launch(out_ids.to(torch.int32), out_lp, len(chunks))
 
     def embed(self, batch: StepBatch) -> list[list[float]]:
         """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts."""
