@@ -13,21 +13,20 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 template <int ACT>
 __global__ __launch_bounds__(256) void act_and_mul_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
                                                           int64_t rows, int I) {
+  // grid (column blocks, rows): no per-element 64-bit division, every lane one 16-B vector
   const int nv = I >> 3;
-  const int64_t total = rows * nv;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / nv;
-    const int c = (int)(i % nv);
-    const bf16* xr = x + r * 2 * I;
-    bf16x8 g = ld8(xr + c * 8), u = ld8(xr + I + c * 8), o;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = blockIdx.y;
+  if (c >= nv) return;
+  const bf16* xr = x + r * 2 * I;
+  bf16x8 g = ld8(xr + c * 8), u = ld8(xr + I + c * 8), o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gf = (float)g[j];
-      const float a = ACT == 0 ? silu(gf) : gelu_tanh(gf);
-      o[j] = (bf16)(a * (float)u[j]);
-    }
-    st8(out + r * I + c * 8, o);
+  for (int j = 0; j < 8; ++j) {
+    const float gf = (float)g[j];
+    const float a = ACT == 0 ? silu(gf) : gelu_tanh(gf);
+    o[j] = (bf16)(a * (float)u[j]);
   }
+  st8(out + r * I + c * 8, o);
 }
 
 static inline int grid_for(int64_t work, int nt) {
@@ -40,11 +39,16 @@ static inline int grid_for(int64_t work, int nt) {
 OME_API int ome_act_and_mul(const void* x, void* out, int64_t rows, int I, int act, hipStream_t stream) {
   if (rows <= 0) return 0;
   if (I % 8) return -2;
-  const int g = grid_for(rows * (I / 8), 256);
-  if (act == 0)
-    act_and_mul_kernel<0><<<g, 256, 0, stream>>>((const bf16*)x, (bf16*)out, rows, I);
-  else
-    act_and_mul_kernel<1><<<g, 256, 0, stream>>>((const bf16*)x, (bf16*)out, rows, I);
+  for (int64_t r0 = 0; r0 < rows; r0 += 65535) {  // grid.y limit
+    const int64_t n = rows - r0 < 65535 ? rows - r0 : 65535;
+    const dim3 g((I / 8 + 255) / 256, (unsigned)n);
+    const bf16* xp = (const bf16*)x + r0 * 2 * I;
+    bf16* op = (bf16*)out + r0 * I;
+    if (act == 0)
+      act_and_mul_kernel<0><<<g, 256, 0, stream>>>(xp, op, n, I);
+    else
+      act_and_mul_kernel<1><<<g, 256, 0, stream>>>(xp, op, n, I);
+  }
   OME_CHECK_LAUNCH();
   return 0;
 }

@@ -28,15 +28,21 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(const bf16* __restrict__ x,
       }
     }
   }
+  bf16x8 wv[CHUNKS];  // issue the weight loads before the reduction's barrier
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) wv[c] = ld8(w + i * 8);
+  }
   ss = block_sum<NT>(ss, red);
   const float rs = rsqrtf(ss / (float)H + eps);
 #pragma unroll
   for (int c = 0; c < CHUNKS; ++c) {
     const int i = threadIdx.x + c * NT;
     if (i < nvec) {
-      bf16x8 wv = ld8(w + i * 8), o;
+      bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)v[c][j] * rs * (float)wv[j]);
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)v[c][j] * rs * (float)wv[c][j]);
       st8(orow + i * 8, o);
     }
   }
@@ -71,15 +77,21 @@ __global__ __launch_bounds__(NT) void fused_add_rmsnorm_kernel(bf16* __restrict_
       st8(rr + i * 8, v[c]);
     }
   }
+  bf16x8 wv[CHUNKS];  // issue the weight loads before the reduction's barrier
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) wv[c] = ld8(w + i * 8);
+  }
   ss = block_sum<NT>(ss, red);
   const float rs = rsqrtf(ss / (float)H + eps);
 #pragma unroll
   for (int c = 0; c < CHUNKS; ++c) {
     const int i = threadIdx.x + c * NT;
     if (i < nvec) {
-      bf16x8 wv = ld8(w + i * 8), o;
+      bf16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)v[c][j] * rs * (float)wv[j]);
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)v[c][j] * rs * (float)wv[c][j]);
       st8(xr + i * 8, o);
     }
   }

@@ -29,56 +29,62 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_kernel(
   constexpr int DV = D / 8;  // 8-wide vectors per head row
 
   // ---- Q and K: optional per-head RMSNorm (Qwen3 qk-norm), then rotate ----
-  // One wave handles one head row at a time: lane l < D/8 owns dims [8l, 8l+8).
+  // A head row is LPH = D/8 lanes (8 dims each); a wave processes 64/LPH head rows at once
+  // (4 for D=128), so the 40 Q+K rows of a Llama-3 token take 3 wave-iterations, not 10, and
+  // every lane of the wave is busy.  All reductions / partner shuffles stay inside a row group.
+  constexpr int LPH = D / 8, HPW = 64 / LPH;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sub = lane / LPH, l = lane % LPH, gbase = sub * LPH;
   const int nheads = Hq + Hkv;
-  for (int h = wave; h < nheads; h += 4) {
+  for (int h0 = wave * HPW; h0 < nheads; h0 += 4 * HPW) {
+    const int h = h0 + sub;
+    const bool valid = h < nheads;
     const bool is_q = h < Hq;
-    const bf16* src = row + (int64_t)h * D;
     bf16x8 x = {};
-    if (lane < DV) x = ld8(src + lane * 8);
+    if (valid) x = ld8(row + (int64_t)h * D + l * 8);
     float f[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = (float)x[j];
     const bf16* nw = is_q ? q_norm_w : k_norm_w;
-    if (nw != nullptr) {
+    if (nw != nullptr) {  // wave-uniform: q_norm_w and k_norm_w are both set or both null
       float ss = 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += f[j] * f[j];
-      ss = wave_sum(ss);
+#pragma unroll
+      for (int m = 1; m < LPH; m <<= 1) ss += __shfl_xor(ss, m);
       const float rs = rsqrtf(ss / (float)D + qk_eps);
-      if (lane < DV) {
-        bf16x8 wv = ld8(nw + lane * 8);
+      if (valid) {
+        bf16x8 wv = ld8(nw + l * 8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = (float)(bf16)(f[j] * rs * (float)wv[j]);
       }
     }
     if (apply_rope) {
-      // partner element for rotate_half lives half/8 lanes away (same wave)
-      const int d0 = lane * 8;
-      const int partner = (d0 < half) ? lane + (half >> 3) : lane - (half >> 3);
+      const int d0 = l * 8;
+      const int hl = half >> 3;  // lanes between a dim and its rotate_half partner
+      const int partner = gbase + ((d0 < half) ? l + hl : l - hl);
       float g[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = __shfl(f[j], partner < 64 ? partner : lane);
+      for (int j = 0; j < 8; ++j) g[j] = __shfl(f[j], (partner >= gbase && partner < gbase + LPH) ? partner : lane);
       if (d0 < rot_dim) {
         const int i0 = (d0 < half) ? d0 : d0 - half;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float c = cs[i0 + j], s = cs[half + i0 + j];
-          f[j] = (d0 < half) ? (f[j] * c - g[j] * s) : (f[j] * c + g[j] * s);
+          const float c = cs[i0 + j], sn = cs[half + i0 + j];
+          f[j] = (d0 < half) ? (f[j] * c - g[j] * sn) : (f[j] * c + g[j] * sn);
         }
       }
     }
-    if (lane < DV) {
+    if (valid) {
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (bf16)f[j];
       if (is_q) {
-        st8(q_out + ((int64_t)t * Hq + h) * D + lane * 8, o);
+        st8(q_out + ((int64_t)t * Hq + h) * D + l * 8, o);
       } else if (slot >= 0) {
         const int kh = h - Hq;
         const int64_t page = slot / P, off = slot % P;
-        st8(k_cache + ((page * Hkv + kh) * P + off) * D + lane * 8, o);
+        st8(k_cache + ((page * Hkv + kh) * P + off) * D + l * 8, o);
       }
     }
   }

@@ -45,7 +45,7 @@ class EngineArgs:
     dtype: str = "bfloat16"
     device: str = "cuda"
     seed: int = 0
-    enable_mixed_chunk: bool = False
+    enable_mixed_chunk: bool = True        # decodes ride along prefill steps (one weight pass)
     disable_radix_cache: bool = False
     is_embedding: bool = False
     kv_cache_dtype: str = "auto"

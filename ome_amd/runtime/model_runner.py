@@ -152,7 +152,8 @@ class ModelRunner:
         if ws is None:
             hkv = self.model.tp.hkv
             parts = max(1, math.ceil(1024 / max(1, bs * hkv)))
-            part = max(256, -(-self.max_context // parts))
+            span = self.max_context + self.P  # seq_lens never exceed this: one part covers it all
+            part = max(256, -(-span // parts))
             part = -(-part // 128) * 128
             ws = ops.DecodeWorkspace(bs, self.model.tp.hq, self.cfg.head_dim, self.max_context + self.P, part,
                                      self.device)

@@ -54,7 +54,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--disable-cuda-graph", action="store_true")
     a("--disable-overlap-schedule", action="store_true")
     a("--cuda-graph-max-bs", type=int, default=None)
-    a("--enable-mixed-chunk", action="store_true")
+    a("--enable-mixed-chunk", action="store_true", default=True)
+    a("--disable-mixed-chunk", dest="enable_mixed_chunk", action="store_false")
     a("--load-format", default="auto")
     a("--dtype", default="bfloat16")
     a("--kv-cache-dtype", default="auto")
