@@ -314,13 +314,29 @@ def inject_metrics_aggregation(pod: dict, cm: dict) -> None:
         ann.setdefault(C.PROMETHEUS_PORT, ann.get(C.CONTAINER_PROMETHEUS_PORT, str(C.DEFAULT_HTTP_PORT)))
         ann.setdefault(C.PROMETHEUS_PATH, ann.get(C.CONTAINER_PROMETHEUS_PATH, C.DEFAULT_PROMETHEUS_PATH))
     if str(enable).lower() == "true":
+        port = ann.get(C.CONTAINER_PROMETHEUS_PORT, str(C.DEFAULT_HTTP_PORT))
+        path = ann.get(C.CONTAINER_PROMETHEUS_PATH, C.DEFAULT_PROMETHEUS_PATH)
         for c in pod["spec"].get("containers") or []:
             if c.get("name") == C.MAIN_CONTAINER:
                 env = c.setdefault("env", [])
-                env.append({"name": "CONTAINER_PROMETHEUS_METRICS_PORT",
-                            "value": ann.get(C.CONTAINER_PROMETHEUS_PORT, str(C.DEFAULT_HTTP_PORT))})
-                env.append({"name": "CONTAINER_PROMETHEUS_METRICS_PATH",
-                            "value": ann.get(C.CONTAINER_PROMETHEUS_PATH, C.DEFAULT_PROMETHEUS_PATH)})
+                env.append({"name": "CONTAINER_PROMETHEUS_METRICS_PORT", "value": port})
+                env.append({"name": "CONTAINER_PROMETHEUS_METRICS_PATH", "value": path})
+        # no Knative queue-proxy to host the merge in raw / multi-node modes: add the aggregator
+        # sidecar (ome_amd.metrics_aggregator) and point Prometheus at it
+        names = {c.get("name") for c in pod["spec"].get("containers") or []}
+        if "queue-proxy" not in names and "metrics-aggregator" not in names:
+            agg = str(cfg.get("aggregatePort", 9088))
+            pod["spec"].setdefault("containers", []).append({
+                "name": "metrics-aggregator", "image": cfg.get("image", "ome-amd/metrics-aggregator:latest"),
+                "command": ["python", "-m", "ome_amd.metrics_aggregator"],
+                "env": [{"name": "AGGREGATE_PROMETHEUS_METRICS_PORT", "value": agg},
+                        {"name": "CONTAINER_PROMETHEUS_METRICS_PORT", "value": port},
+                        {"name": "CONTAINER_PROMETHEUS_METRICS_PATH", "value": path},
+                        {"name": "QUEUE_PROXY_METRICS_PORT", "value": ""}],
+                "ports": [{"containerPort": int(agg), "name": "agg-metrics"}],
+                "resources": {"requests": {"cpu": "50m", "memory": "64Mi"}, "limits": {"cpu": "200m", "memory": "256Mi"}}})
+            if str(scrape).lower() == "true":
+                ann[C.PROMETHEUS_PORT] = agg
 
 
 def inject_model_init(pod: dict, cm: dict) -> None:

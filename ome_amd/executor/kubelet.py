@@ -224,6 +224,7 @@ class Kubelet:
         self.gpu_owner: dict[int, tuple] = {}
         self.probe_scale = probe_scale
         self.restart_backoff = restart_backoff
+        self.api_url: str | None = None  # manager REST API handed to pods (router discovery, agents)
         self._lock = threading.RLock()
         self.proxies = ServiceProxies(store, self, os.path.join(self.state_dir, "dns.json"))
         self.register_node()
@@ -383,6 +384,9 @@ class Kubelet:
             return s
 
         env = {k: fix(v) for k, v in env.items()}
+        for k, v in env.items():  # *_PORT env values naming a container port follow the remap
+            if k.endswith("_PORT") and v.isdigit() and int(v) in ports:
+                env[k] = str(ports[int(v)])
         cmd = list(c.get("command") or [])
         args = list(c.get("args") or [])
         if not cmd:
@@ -395,9 +399,14 @@ class Kubelet:
             argv = ["/bin/bash", argv[1], translate_command(argv[2])] + argv[3:]
         else:
             argv = shlex.split(translate_command(shlex.join(argv)))
-        for i, a in enumerate(argv[:-1]):  # exec-form "--port", "8080" pairs
-            if a == "--port" and argv[i + 1].isdigit() and int(argv[i + 1]) in ports:
-                argv[i + 1] = str(ports[int(argv[i + 1])])
+        for i, a in enumerate(argv[:-1]):  # exec-form "--port", "8080" / "--addr", ":8080" pairs
+            nxt = argv[i + 1]
+            if a == "--port" and nxt.isdigit() and int(nxt) in ports:
+                argv[i + 1] = str(ports[int(nxt)])
+            elif a in ("--addr", "--listen", "--metrics-addr") and nxt.rpartition(":")[2].isdigit():
+                hp, _, pt = nxt.rpartition(":")
+                if int(pt) in ports:
+                    argv[i + 1] = f"{hp}:{ports[int(pt)]}"
         if ports and not any("--port" in a for a in argv) and "ome_amd.runtime.server" in " ".join(argv):
             argv += ["--port", str(next(iter(ports.values())))]
         return ContainerRun(c["name"], argv, env, workdir, os.path.join(workdir, f"{c['name']}.log"), c)
@@ -423,6 +432,7 @@ class Kubelet:
         base.update({"HOSTNAME": pod["spec"].get("hostname") or name, "POD_NAME": name, "POD_NAMESPACE": ns,
                      "PYTHONPATH": REPO_ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
                      "OME_LOCAL_DNS": self.proxies.dns_path, "OME_POD_PORTS": json.dumps(ports),
+                     "OME_API_SERVER": self.api_url or "",
                      "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
         if ids:
             base["HIP_VISIBLE_DEVICES"] = ",".join(map(str, ids))

@@ -22,6 +22,7 @@ import threading
 import time
 
 import yaml
+from fastapi import Request  # module level: FastAPI resolves the string annotations against it
 
 from ome_amd.admission import webhooks
 from ome_amd.api import constants as C
@@ -139,6 +140,29 @@ class Cluster:
                 self.executor.kubelet.sync()
         self.manager.run_until_idle(fast_forward=6.0)
 
+    def serve_api(self, host: str = "127.0.0.1", port: int = 0) -> str:
+        """Run the REST API in a background thread; pods get it as ``$OME_API_SERVER``."""
+        import socket
+
+        import uvicorn
+
+        if port == 0:
+            with socket.socket() as s:
+                s.bind((host, 0))
+                port = s.getsockname()[1]
+        server = uvicorn.Server(uvicorn.Config(create_api(self), host=host, port=port, log_level="warning"))
+        t = threading.Thread(target=server.run, name="ome-api", daemon=True)
+        t.start()
+        for _ in range(100):
+            if server.started:
+                break
+            time.sleep(0.05)
+        self._api_server = server
+        self.api_url = f"http://{host}:{port}"
+        if self.executor:
+            self.executor.kubelet.api_url = self.api_url
+        return self.api_url
+
     def wait_for(self, pred, timeout: float = 60.0, interval: float = 0.2, drive: bool = False) -> bool:
         end = time.time() + timeout
         while time.time() < end:
@@ -150,6 +174,8 @@ class Cluster:
         return False
 
     def shutdown(self) -> None:
+        if getattr(self, "_api_server", None) is not None:
+            self._api_server.should_exit = True
         if self._started:
             self.manager.stop()
         if self.agent:
@@ -160,7 +186,7 @@ class Cluster:
 
 # ------------------------------------------------------------------ REST API
 def create_api(cluster: Cluster):
-    from fastapi import Body, FastAPI, HTTPException, Request
+    from fastapi import FastAPI, HTTPException
     from fastapi.responses import JSONResponse, PlainTextResponse
 
     from ome_amd.store import store as S
@@ -266,9 +292,9 @@ def create_api(cluster: Cluster):
         return await handle(request, group, version, None, plural, name, sub)
 
     @app.post("/apply")
-    async def apply(body: str = Body(..., media_type="text/plain")):
+    async def apply(request: Request):
         try:
-            return {"items": cluster.apply(body)}
+            return {"items": cluster.apply((await request.body()).decode())}
         except Exception as e:  # noqa: BLE001
             return err(e)
 
