@@ -401,7 +401,7 @@ class Kubelet:
             argv = shlex.split(translate_command(shlex.join(argv)))
         for i, a in enumerate(argv[:-1]):  # exec-form "--port", "8080" / "--addr", ":8080" pairs
             nxt = argv[i + 1]
-            if a == "--port" and nxt.isdigit() and int(nxt) in ports:
+            if (a == "--port" or a.endswith("-port")) and nxt.isdigit() and int(nxt) in ports:
                 argv[i + 1] = str(ports[int(nxt)])
             elif a in ("--addr", "--listen", "--metrics-addr") and nxt.rpartition(":")[2].isdigit():
                 hp, _, pt = nxt.rpartition(":")

@@ -1,0 +1,225 @@
+"""Prefill/decode disaggregation: KV-cache hand-off between a prefill engine and a decode engine
+(the reference runs SGLang ``--disaggregation-mode prefill|decode`` behind its PD router;
+``config/runtimes/srt/*-pd-rt.yaml``).
+
+Flow (one request, room id R chosen by the router — :mod:`ome_amd.router`):
+
+  router --(R, decode addr)--> prefill engine: runs the prompt, samples the first token, then
+        pushes {header, K/V pages of the prompt, first token} to the decode engine's receiver;
+  router --(R)--> decode engine: holds the request until the KV for R arrives, installs the pages
+        into its own paged cache (page ids differ: copied page-by-page) and continues decoding
+        from the first token — which it also streams to the client.
+
+Transport: a length-prefixed TCP stream per hand-off (``--disaggregation-bootstrap-port`` + TP
+rank, one stream per TP rank since each rank owns its head shard).  The payload is the raw
+page images in the cache's own MFMA layouts (K ``[pages, Hkv, P, D]``, V ``[pages, Hkv, D, P]``)
+so neither side reformats; on the decode side the bytes land in one pinned buffer and are
+uploaded with a single H2D copy, then scattered with ``index_copy_`` per layer.  Arrival order
+does not matter: KV that arrives before its request waits in the inbox, and vice versa.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import socket
+import struct
+import threading
+import time
+
+import numpy as np
+import torch
+
+log = logging.getLogger("ome_amd.disagg")
+
+MAGIC = b"OMEKV1\0\0"
+
+
+def _recv_exact(sock: socket.socket, n: int) -> bytes:
+    buf = bytearray(n)
+    view = memoryview(buf)
+    got = 0
+    while got < n:
+        k = sock.recv_into(view[got:], min(n - got, 1 << 24))
+        if k == 0:
+            raise ConnectionError("peer closed during KV transfer")
+        got += k
+    return bytes(buf)
+
+
+class KVTransfer:
+    def __init__(self, engine, mode: str, port: int, host: str = "0.0.0.0"):
+        assert mode in ("prefill", "decode")
+        self.engine, self.mode = engine, mode
+        self.rank = engine.pstate.rank if engine.pstate.tp_size > 1 else 0
+        self.port = port
+        self.lock = threading.Lock()
+        self.inbox: dict[int, tuple[dict, bytes]] = {}   # room -> (header, payload) (decode side)
+        self.waiting: dict[int, object] = {}              # room -> Request awaiting its KV (decode)
+        self.sent = 0
+        self.received = 0
+        self._sock = None
+        if mode == "decode":
+            self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            self._sock.bind((host, port + self.rank))
+            self._sock.listen(64)
+            self.port = self._sock.getsockname()[1] - self.rank
+            threading.Thread(target=self._accept_loop, name="kv-recv", daemon=True).start()
+        else:
+            engine.scheduler.on_finish = self._on_prefill_finish
+
+    # ------------------------------------------------------------------ decode side
+    def _accept_loop(self) -> None:
+        while True:
+            try:
+                conn, _ = self._sock.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._recv_one, args=(conn,), daemon=True).start()
+
+    def _recv_one(self, conn: socket.socket) -> None:
+        try:
+            with conn:
+                if _recv_exact(conn, 8) != MAGIC:
+                    raise ConnectionError("bad KV transfer magic")
+                (hl,) = struct.unpack("<I", _recv_exact(conn, 4))
+                header = json.loads(_recv_exact(conn, hl))
+                payload = _recv_exact(conn, int(header["nbytes"]))
+                conn.sendall(b"OK")
+            with self.lock:
+                self.inbox[int(header["room"])] = (header, payload)
+            self.received += 1
+            self.engine._wake.set()
+        except Exception as e:  # noqa: BLE001
+            log.warning("KV receive failed: %s", e)
+
+    def hold(self, req) -> None:
+        """Decode engine: park a request until its KV arrives (called from the engine thread)."""
+        self.waiting[int(req.bootstrap["room"])] = req
+
+    def poll(self) -> int:
+        """Decode engine, start of every step: install every request whose KV has arrived."""
+        if not self.waiting:
+            return 0
+        with self.lock:
+            ready = [r for r in self.waiting if r in self.inbox]
+        n = 0
+        for room in ready:
+            req = self.waiting[room]
+            with self.lock:
+                header, payload = self.inbox[room]
+            if not self._install(req, header, payload):
+                break  # out of KV pages: retry next step (decodes finishing free pages)
+            with self.lock:
+                self.inbox.pop(room, None)
+            self.waiting.pop(room)
+            n += 1
+        return n
+
+    def _install(self, req, header: dict, payload: bytes) -> bool:
+        from ome_amd.runtime.request import ReqState
+
+        eng = self.engine
+        sch, runner = eng.scheduler, eng.runner
+        kv, P = runner.kv, runner.P
+        L = int(header["n_tokens"])
+        if list(header["shape_k"][1:]) != list(kv.k[0].shape[1:]) or int(header["layers"]) != kv.num_layers:
+            req.state, req.finish_reason = ReqState.FINISHED, "abort:kv_layout_mismatch"
+            if req.on_token:
+                req.on_token(req, [], True)
+            return True
+        if req.req_slot < 0:
+            slot = sch.slots.alloc()
+            if slot is None:
+                return False
+            req.req_slot = slot
+        n_pages = -(-L // P)
+        pages = sch.pages.alloc(n_pages)
+        if pages is None:
+            return False
+        req.pages = list(pages)
+        sch.slots.set_pages(req.req_slot, 0, pages)
+        sch.slots.flush()
+        src = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
+        if runner.is_cuda:
+            src = src.pin_memory().to(runner.device, non_blocking=True)
+        idx = torch.tensor(pages, dtype=torch.long, device=runner.device)
+        kbytes = int(np.prod(header["shape_k"])) * kv.k[0].element_size()
+        vbytes = int(np.prod(header["shape_v"])) * kv.v[0].element_size()
+        o = 0
+        for i in range(kv.num_layers):
+            kk = src[o:o + kbytes].view(kv.dtype).view(header["shape_k"])
+            o += kbytes
+            vv = src[o:o + vbytes].view(kv.dtype).view(header["shape_v"])
+            o += vbytes
+            kv.k[i].index_copy_(0, idx, kk)
+            kv.v[i].index_copy_(0, idx, vv)
+        now = time.perf_counter()
+        req.output_ids.append(int(header["first_token"]))
+        req.output_logprobs.append(float(header.get("first_logprob", 0.0)))
+        req.token_times.append(now)
+        req.first_token_time = now
+        req.num_cached = L
+        req.state = ReqState.RUNNING
+        sch.running.append(req)
+        eng.metrics.on_arrival(req)
+        if req.on_token is not None:
+            finished = req.params.max_new_tokens <= 1
+            req.on_token(req, [req.output_ids[-1]], finished)
+            if finished:
+                sch.finish(req, "length")
+        return True
+
+    # ------------------------------------------------------------------ prefill side
+    def _on_prefill_finish(self, req) -> None:
+        """Scheduler hook (before the pages are released): snapshot the prompt's KV pages and
+        push them to the decode engine in the background."""
+        b = req.bootstrap or {}
+        if b.get("disagg_role") != "prefill" or not req.output_ids or req.finish_reason and \
+                req.finish_reason.startswith("abort"):
+            return
+        runner = self.engine.runner
+        kv, P = runner.kv, runner.P
+        L = len(req.prompt_ids)
+        pages = req.pages[: -(-L // P)]
+        idx = torch.tensor(pages, dtype=torch.long, device=runner.device)
+        parts = []
+        for i in range(kv.num_layers):
+            parts.append(kv.k[i].index_select(0, idx).reshape(-1).view(torch.uint8))
+            parts.append(kv.v[i].index_select(0, idx).reshape(-1).view(torch.uint8))
+        blob = torch.cat(parts).cpu().numpy().tobytes()
+        header = {"room": int(b["bootstrap_room"]), "n_tokens": L, "first_token": int(req.output_ids[0]),
+                  "first_logprob": float(req.output_logprobs[0]) if req.output_logprobs else 0.0,
+                  "layers": kv.num_layers, "shape_k": [len(pages), *kv.k[0].shape[1:]],
+                  "shape_v": [len(pages), *kv.v[0].shape[1:]], "dtype": str(kv.dtype), "nbytes": len(blob)}
+        host, port = b.get("bootstrap_host") or "127.0.0.1", int(b["bootstrap_port"]) + self.rank
+        threading.Thread(target=self._send, args=(host, port, header, blob), daemon=True).start()
+
+    def _send(self, host: str, port: int, header: dict, blob: bytes, retries: int = 20) -> None:
+        from ome_amd.executor.dns import resolve_host_port
+
+        host, port = resolve_host_port(host, port)
+        h = json.dumps(header).encode()
+        for attempt in range(retries):
+            try:
+                with socket.create_connection((host, port), timeout=30) as s:
+                    s.sendall(MAGIC + struct.pack("<I", len(h)) + h)
+                    s.sendall(blob)
+                    if _recv_exact(s, 2) != b"OK":
+                        raise ConnectionError("no ack")
+                self.sent += 1
+                return
+            except OSError as e:
+                log.warning("KV push to %s:%d failed (%s), retry %d", host, port, e, attempt + 1)
+                time.sleep(min(2.0, 0.1 * 2 ** attempt))
+        log.error("KV push for room %s dropped", header["room"])
+
+    def close(self) -> None:
+        if self._sock is not None:
+            self._sock.close()
+
+
+def attach_kv_transfer(engine, mode: str, port: int) -> KVTransfer:
+    kt = KVTransfer(engine, mode, port)
+    engine.kv_transfer = kt
+    return kt

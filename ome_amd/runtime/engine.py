@@ -144,11 +144,20 @@ class Engine:
             self._inbox, self._aborts = [], []
         if self.pstate.tp_size > 1:
             new, aborts = self._broadcast_control(new, aborts)
+        kt = self.kv_transfer
         for r in new:
             r.arrival_time = r.arrival_time or time.perf_counter()
+            if kt is not None and kt.mode == "decode" and (r.bootstrap or {}).get("disagg_role") == "decode":
+                kt.hold(r)  # its KV comes from a prefill engine (ome_amd.runtime.disagg)
+                continue
             self.scheduler.add(r)
             self.metrics.on_arrival(r)
         for rid in aborts:
+            if kt is not None:
+                for room, w in list(kt.waiting.items()):
+                    if w.rid == rid:
+                        kt.waiting.pop(room)
+                        w.state, w.finish_reason = ReqState.FINISHED, "abort"
             r = self.scheduler.abort(rid)
             if r is not None and r.on_token:
                 r.on_token(r, [], True)
@@ -180,6 +189,8 @@ class Engine:
         and detokenisation hide behind the GPU.  Returned requests are those finished by step k.
         """
         self._drain_inbox()
+        if self.kv_transfer is not None and self.kv_transfer.mode == "decode":
+            self.kv_transfer.poll()
         if self.cfg.is_embedding:
             return self._embed_step()
         prev = self._inflight
@@ -232,7 +243,8 @@ class Engine:
         return done
 
     def has_work(self) -> bool:
-        return self.scheduler.has_work() or bool(self._inbox) or self._inflight is not None
+        return (self.scheduler.has_work() or bool(self._inbox) or self._inflight is not None
+                or bool(self.kv_transfer is not None and self.kv_transfer.waiting))
 
     def generate(self, prompts: list[list[int]], params: SamplingParams | list[SamplingParams] | None = None) -> list[Request]:
         plist = params if isinstance(params, list) else [params] * len(prompts)

@@ -56,6 +56,7 @@ class Scheduler:
         self.waiting: collections.deque[Request] = collections.deque()
         self.running: list[Request] = []
         self.num_preemptions = 0
+        self.on_finish = None  # hook(req) before a finished request's pages are released (PD prefill)
 
     # ------------------------------------------------------------------ queue ops
     def add(self, req: Request) -> None:
@@ -121,6 +122,8 @@ class Scheduler:
         if req in self.running:
             self.running.remove(req)
         req.state, req.finish_reason = ReqState.FINISHED, reason
+        if self.on_finish is not None and req.bootstrap:
+            self.on_finish(req)
         self._release(req, cache_prefix=True)
 
     def _preempt_one(self, keep: Request | None = None) -> bool:

@@ -141,12 +141,20 @@ def create_app(engine, ns=None):
     def err(code: int, msg: str, typ: str = "invalid_request_error"):
         return JSONResponse({"error": {"message": msg, "type": typ, "code": code}}, status_code=code)
 
-    async def run_request(prompt_ids, params):
+    async def run_request(prompt_ids, params, bootstrap=None):
         loop = asyncio.get_running_loop()
         stream = _Stream(loop)
-        req = engine.make_request(prompt_ids, params, on_token=stream)
+        if bootstrap and bootstrap.get("disagg_role") == "prefill":
+            params.max_new_tokens = 1  # the prefill engine only produces the first token + KV
+        req = engine.make_request(prompt_ids, params, on_token=stream, bootstrap=bootstrap)
         engine.add_request(req)
         return req, stream
+
+    def _bootstrap_of(body: dict):
+        if body.get("bootstrap_room") is None:
+            return None
+        return {k: body.get(k) for k in ("bootstrap_room", "bootstrap_host", "bootstrap_port", "disagg_role",
+                                         "bootstrap_prefill")} | {"room": int(body["bootstrap_room"])}
 
     @app.get("/health")
     async def health():
@@ -187,7 +195,8 @@ def create_app(engine, ns=None):
         return {"tp_size": a.tp_size, "pp_size": a.pp_size, "page_size": a.page_size,
                 "max_running_requests": a.max_running_requests, "chunked_prefill_size": a.chunked_prefill_size,
                 "kv_pages": engine.runner.kv.num_pages, "cuda_graph_buckets": engine.runner.buckets,
-                "disaggregation_mode": a.disaggregation_mode, **engine.health()}
+                "disaggregation_mode": a.disaggregation_mode,
+                "disaggregation_bootstrap_port": getattr(engine.kv_transfer, "port", None), **engine.health()}
 
     @app.get("/metrics")
     async def metrics():
@@ -220,7 +229,7 @@ def create_app(engine, ns=None):
         try:
             ids = _encode(body, chat)
             params = _sampling_from(body, default_max)
-            req, stream = await run_request(ids, params)
+            req, stream = await run_request(ids, params, _bootstrap_of(body))
         except ValueError as e:
             return err(400, str(e))
         rid = f"{'chatcmpl' if chat else 'cmpl'}-{uuid.uuid4().hex[:24]}"
