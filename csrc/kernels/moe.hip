@@ -1,0 +1,289 @@
+// Mixture-of-Experts kernels (SURVEY.md §2.9 K10 routing + K11 grouped GEMM) for gfx950.
+//
+//   ome_moe_route   : gate logits [T, E] -> softmax (or sigmoid) -> top-k ids / weights,
+//                     optional renormalisation; one wave per token, E <= 512, k <= 16.
+//   ome_moe_align   : counting sort of the T*k assignments by expert -> expert_offsets [E+1],
+//                     sorted_ids [T*k] (flat assignment index t*k+j) and its inverse, all on the
+//                     device (graph-capturable: no host sync on the per-expert counts).
+//   ome_moe_gemm    : grouped GEMM  out[p, :] = A[row(p), :] @ W[e(p)]^T  over the sorted
+//                     assignments p; A rows are gathered through sorted_ids / k (gate_up) or
+//                     read in sorted order (down).  64x64 MFMA tiles, tiles of an expert never
+//                     straddle experts; each workgroup finds its (expert, m-tile) by scanning
+//                     the offsets, so the grid is a static upper bound.
+//   ome_moe_combine : out[t] = sum_j w[t, j] * Y[inv[t*k + j]]   (fp32 accumulate)
+#include "common.h"
+
+#ifndef OME_NEG_INF
+#define OME_NEG_INF (-__builtin_inff())
+#endif
+
+// ------------------------------------------------------------------------------------------
+// routing
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void moe_route_kernel(const T* __restrict__ logits, int64_t stride, int n_tok,
+                                                        int E, int k, int renorm, int scoring,
+                                                        float* __restrict__ topk_w, int* __restrict__ topk_ids) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + wave;
+  if (t >= n_tok) return;
+  constexpr int MAXV = 8;  // E <= 512
+  float v[MAXV];
+  const T* row = logits + (int64_t)t * stride;
+  float mx = OME_NEG_INF;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int e = lane + 64 * i;
+    v[i] = e < E ? (float)row[e] : OME_NEG_INF;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int e = lane + 64 * i;
+    float p;
+    if (scoring == 0) p = e < E ? __expf(v[i] - mx) : 0.f;        // softmax numerator
+    else p = e < E ? 1.f / (1.f + __expf(-v[i])) : -1.f;           // sigmoid score
+    v[i] = p;
+    sum += (e < E && scoring == 0) ? p : 0.f;
+  }
+  if (scoring == 0) {
+    sum = wave_sum(sum);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) v[i] *= inv;
+  }
+  float picked_sum = 0.f;
+  for (int j = 0; j < k; ++j) {
+    // argmax over the wave (ties -> lowest expert id)
+    float best = -2.f;
+    int bi = 1 << 30;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int e = lane + 64 * i;
+      if (e < E && (v[i] > best || (v[i] == best && e < bi))) {
+        best = v[i];
+        bi = e;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o);
+      const int oi = __shfl_xor(bi, o);
+      if (ob > best || (ob == best && oi < bi)) {
+        best = ob;
+        bi = oi;
+      }
+    }
+    if (lane == 0) {
+      topk_w[(int64_t)t * k + j] = best;
+      topk_ids[(int64_t)t * k + j] = bi;
+    }
+    picked_sum += best;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)  // remove the winner (static register indexing)
+      if (lane + 64 * i == bi) v[i] = -3.f;
+  }
+  if (renorm && lane == 0) {
+    const float inv = 1.f / picked_sum;
+    for (int j = 0; j < k; ++j) topk_w[(int64_t)t * k + j] *= inv;
+  }
+}
+
+OME_API int ome_moe_route(const void* logits, int is_bf16, int64_t stride, int n_tok, int E, int k, int renorm,
+                          int scoring, float* topk_w, int* topk_ids, hipStream_t stream) {
+  if (n_tok <= 0) return 0;
+  if (E > 512 || k > E || k <= 0) return -2;
+  const int g = (n_tok + 3) / 4;
+  if (is_bf16)
+    moe_route_kernel<bf16><<<g, 256, 0, stream>>>((const bf16*)logits, stride, n_tok, E, k, renorm, scoring, topk_w,
+                                                  topk_ids);
+  else
+    moe_route_kernel<float><<<g, 256, 0, stream>>>((const float*)logits, stride, n_tok, E, k, renorm, scoring,
+                                                   topk_w, topk_ids);
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// alignment (counting sort by expert), single workgroup
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__ topk_ids, int n, int E,
+                                                         int* __restrict__ offsets, int* __restrict__ sorted_ids,
+                                                         int* __restrict__ inv) {
+  extern __shared__ int sh[];  // [E] counts then [E] cursors
+  int* cnt = sh;
+  int* cur = sh + E;
+  for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[topk_ids[i]], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int e = 0; e < E; ++e) {
+      offsets[e] = acc;
+      cur[e] = acc;
+      acc += cnt[e];
+    }
+    offsets[E] = acc;
+  }
+  __syncthreads();
+  // stable within an expert is not required (the combine uses the inverse map)
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int p = atomicAdd(&cur[topk_ids[i]], 1);
+    sorted_ids[p] = i;
+    inv[i] = p;
+  }
+}
+
+OME_API int ome_moe_align(const int* topk_ids, int n, int E, int* offsets, int* sorted_ids, int* inv,
+                          hipStream_t stream) {
+  if (n <= 0) {
+    return hipMemsetAsync(offsets, 0, (E + 1) * sizeof(int), stream);
+  }
+  moe_align_kernel<<<1, 1024, 2 * E * sizeof(int), stream>>>(topk_ids, n, E, offsets, sorted_ids, inv);
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// grouped GEMM: 64x64 output tile per 256-thread workgroup, BK = 32, MFMA 16x16x32 bf16.
+// Waves as 2(M) x 2(N), each 32x32 = 2x2 MFMA tiles.  LDS rows padded to 40 bf16 (80 B) so
+// the 16 rows a ds_read_b128 group touches start on distinct bank quads.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+constexpr int GBM = 64, GBN = 64, GBK = 32, GLD = GBK + 8;
+
+__global__ __launch_bounds__(256) void moe_gemm_kernel(const bf16* __restrict__ A, int64_t lda,
+                                                       const int* __restrict__ sorted_ids, int gather_div,
+                                                       const bf16* __restrict__ W, const int* __restrict__ offsets,
+                                                       int E, int N, int K, bf16* __restrict__ out, int64_t ldo) {
+  __shared__ __attribute__((aligned(16))) bf16 sA[GBM * GLD];
+  __shared__ __attribute__((aligned(16))) bf16 sB[GBN * GLD];
+  __shared__ int s_tile[3];
+  // ---- find (expert, m0) of this workgroup's tile ----
+  if (threadIdx.x == 0) {
+    int t = blockIdx.y, e = 0, found = 0;
+    for (; e < E; ++e) {
+      const int c = offsets[e + 1] - offsets[e];
+      const int nt = (c + GBM - 1) / GBM;
+      if (t < nt) {
+        found = 1;
+        break;
+      }
+      t -= nt;
+    }
+    s_tile[0] = found ? e : -1;
+    s_tile[1] = found ? offsets[e] + t * GBM : 0;
+    s_tile[2] = found ? offsets[e + 1] : 0;
+  }
+  __syncthreads();
+  const int e = s_tile[0];
+  if (e < 0) return;
+  const int m0 = s_tile[1], m_end = s_tile[2];
+  const int n0 = blockIdx.x * GBN;
+  const bf16* We = W + (int64_t)e * N * K;
+
+  const int tid = threadIdx.x;
+  // global->LDS staging: each thread moves one 16-B chunk of A and one of B per k-step
+  const int lr = tid >> 2, lc = (tid & 3) * 8;  // row 0..63, k offset 0/8/16/24
+  const int arow = m0 + lr;
+  int64_t a_off = -1;
+  if (arow < m_end) {
+    const int src = gather_div > 0 ? sorted_ids[arow] / gather_div : arow;
+    a_off = (int64_t)src * lda;
+  }
+  const int brow = n0 + lr;
+  const bf16* bptr = brow < N ? We + (int64_t)brow * K : nullptr;
+
+  const int wave = tid >> 6, lane = tid & 63;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 ra = {}, rb = {};
+  if (a_off >= 0) ra = ld8(A + a_off + lc);
+  if (bptr) rb = ld8(bptr + lc);
+  for (int k0 = 0; k0 < K; k0 += GBK) {
+    __syncthreads();
+    *reinterpret_cast<bf16x8*>(&sA[lr * GLD + lc]) = ra;
+    *reinterpret_cast<bf16x8*>(&sB[lr * GLD + lc]) = rb;
+    __syncthreads();
+    if (k0 + GBK < K) {  // prefetch the next k-step while this one computes
+      if (a_off >= 0) ra = ld8(A + a_off + k0 + GBK + lc);
+      if (bptr) rb = ld8(bptr + k0 + GBK + lc);
+    }
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const bf16x8*>(&sA[(wm + 16 * i + fr) * GLD + fk]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(&sB[(wn + 16 * j + fr) * GLD + fk]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+  }
+  // ---- epilogue: C lane map row = 4*(l>>4)+r, col = l&15 ----
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+        const int col = n0 + wn + 16 * j + (lane & 15);
+        if (row < m_end && col < N) out[(int64_t)row * ldo + col] = (bf16)acc[i][j][r];
+      }
+}
+
+OME_API int ome_moe_gemm(const void* A, int64_t lda, const int* sorted_ids, int gather_div, const void* W,
+                         const int* offsets, int E, int N, int K, int max_m_tiles, void* out, int64_t ldo,
+                         hipStream_t stream) {
+  if (max_m_tiles <= 0) return 0;
+  if (K % GBK != 0 || lda % 8 != 0) return -2;
+  if (max_m_tiles > 65535) return -3;
+  dim3 grid((N + GBN - 1) / GBN, max_m_tiles);
+  moe_gemm_kernel<<<grid, 256, 0, stream>>>((const bf16*)A, lda, sorted_ids, gather_div, (const bf16*)W, offsets,
+                                            E, N, K, (bf16*)out, ldo);
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// combine
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict__ Y, const float* __restrict__ w,
+                                                          const int* __restrict__ inv, int k, int H,
+                                                          bf16* __restrict__ out, float scale) {
+  const int t = blockIdx.x;
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const float wj = w[(int64_t)t * k + j];
+      const bf16x8 y = ld8(Y + (int64_t)inv[(int64_t)t * k + j] * H + c * 8);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wj * (float)y[q];
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = (bf16)(acc[q] * scale);
+    st8(out + (int64_t)t * H + c * 8, o);
+  }
+}
+
+OME_API int ome_moe_combine(const void* Y, const float* w, const int* inv, int n_tok, int k, int H, void* out,
+                            float scale, hipStream_t stream) {
+  if (n_tok <= 0) return 0;
+  if (H % 8) return -2;
+  moe_combine_kernel<<<n_tok, 256, 0, stream>>>((const bf16*)Y, w, inv, k, H, (bf16*)out, scale);
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,147 @@
+"""Sparse MoE decoders (Mixtral, Qwen2-MoE, Qwen3-MoE, PhiMoE) on the ome_amd kernels.
+
+Attention is the dense-family path (``llama.py``); the MLP becomes:
+  router GEMM (hipBLASLt) -> ``ome_moe_route`` (softmax top-k, renorm) ->
+  ``ome_moe_align`` (device counting sort) -> grouped MFMA GEMM gate_up (A rows gathered) ->
+  SiLU*mul -> grouped MFMA GEMM down -> ``ome_moe_combine`` (+ shared expert, Qwen2-MoE) ->
+  TP all-reduce.
+Experts are tensor-parallel over the intermediate dimension (every rank holds a 1/tp slice of
+every expert), so the collective pattern matches the dense family; expert parallelism with
+all-to-all dispatch is the alternative for very large expert counts.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from ome_amd import ops
+from ome_amd.models.llama import LlamaForCausalLM
+from ome_amd.parallel import state as pstate
+
+
+class MoEForCausalLM(LlamaForCausalLM):
+    def __init__(self, cfg, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
+        super().__init__(cfg, device, dtype, max_positions)
+        tp = self.tp
+        self.E = cfg.num_experts
+        self.k = cfg.num_experts_per_tok
+        self.renorm = cfg.norm_topk_prob
+        self.moe_inter = -(-cfg.moe_intermediate_size // tp.tp)
+        self.shared_inter = -(-(cfg.shared_expert_intermediate_size or 0) // tp.tp)
+        L = cfg.num_layers
+        self.w_router: list[torch.Tensor] = [None] * L
+        self.w13: list[torch.Tensor] = [None] * L     # [E, 2*I_local, H]
+        self.w2: list[torch.Tensor] = [None] * L      # [E, H, I_local]
+        self.w_sgu: list[torch.Tensor | None] = [None] * L   # shared expert gate_up
+        self.w_sd: list[torch.Tensor | None] = [None] * L    # shared expert down
+        self.w_sgate: list[torch.Tensor | None] = [None] * L  # shared expert sigmoid gate [1, H]
+        step = max(1, cfg.moe_layer_freq)
+        self.moe_layers = {i for i in range(L) if i >= cfg.first_k_dense_replace and (i + 1) % step == 0} \
+            if step > 1 else {i for i in range(L) if i >= cfg.first_k_dense_replace}
+
+    def init_random(self, seed: int = 0, std: float = 0.02) -> "MoEForCausalLM":
+        super().init_random(seed, std)
+        cfg = self.cfg
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed + 104729 + 7919 * pstate.get().rank)
+        H, I = cfg.hidden_size, self.moe_inter
+        for i in self.layers:
+            if i not in self.moe_layers:
+                continue
+            self.w_gu[i] = self.w_d[i] = None  # dense MLP replaced by experts
+            self.w_router[i] = self._alloc(self.E, H, std=std, gen=gen)
+            self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen)
+            self.w2[i] = self._alloc(self.E, H, I, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+            if self.shared_inter:
+                self.w_sgu[i] = self._alloc(2 * self.shared_inter, H, std=std, gen=gen)
+                self.w_sd[i] = self._alloc(H, self.shared_inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+                self.w_sgate[i] = self._alloc(1, H, std=std, gen=gen)
+        return self
+
+    def load_hf_weights(self, weights) -> "MoEForCausalLM":
+        tp = self.tp
+        I, SI = self.moe_inter, self.shared_inter
+        experts: dict[int, dict[int, dict[str, torch.Tensor]]] = {}
+        shared: dict[int, dict[str, torch.Tensor]] = {}
+        rest_iter = []
+
+        def put(t):
+            return t.to(device=self.device, dtype=self.dtype).contiguous()
+
+        def rows(t, n):
+            return t.narrow(0, tp.rank * n, min(n, t.shape[0] - tp.rank * n))
+
+        def cols(t, n):
+            return t.narrow(1, tp.rank * n, min(n, t.shape[1] - tp.rank * n))
+
+        for name, w in weights:
+            n = name[len("model."):] if name.startswith("model.") else name
+            parts = n.split(".")
+            if parts[0] == "layers" and len(parts) > 3 and parts[2] in ("block_sparse_moe", "mlp") and \
+                    int(parts[1]) in self.moe_layers:
+                i = int(parts[1])
+                sub = ".".join(parts[3:])
+                if sub == "gate.weight":
+                    self.w_router[i] = put(w)
+                elif sub.startswith("experts."):
+                    e = int(parts[4])
+                    kind = parts[5]  # w1/w2/w3 (Mixtral) or gate_proj/up_proj/down_proj
+                    experts.setdefault(i, {}).setdefault(e, {})[kind] = w
+                elif sub.startswith("shared_expert."):
+                    shared.setdefault(i, {})[parts[4]] = w
+                elif sub == "shared_expert_gate.weight":
+                    self.w_sgate[i] = put(w)
+                continue
+            rest_iter.append((name, w))
+        # dense / attention / embeddings through the base loader (it tolerates missing MLPs below)
+        self._load_base(rest_iter)
+        for i, ex in experts.items():
+            gs, ds = [], []
+            for e in range(self.E):
+                d = ex[e]
+                g = d.get("w1", d.get("gate_proj"))
+                u = d.get("w3", d.get("up_proj"))
+                dn = d.get("w2", d.get("down_proj"))
+                if g is None or u is None or dn is None:
+                    raise ValueError(f"layer {i} expert {e}: missing weights")
+                gs.append(torch.cat([rows(g, I), rows(u, I)], 0))
+                ds.append(cols(dn, I))
+            self.w13[i] = put(torch.stack(gs))
+            self.w2[i] = put(torch.stack(ds))
+            self.w_gu[i] = self.w_d[i] = None
+        for i, d in shared.items():
+            self.w_sgu[i] = put(torch.cat([rows(d["gate_proj"], SI), rows(d["up_proj"], SI)], 0))
+            self.w_sd[i] = put(cols(d["down_proj"], SI))
+        return self
+
+    def _load_base(self, weights) -> None:
+        # the base loader validates dense MLP weights; present them as satisfied for MoE layers
+        saved = [self.w_gu[i] for i in self.layers]
+        placeholder = torch.empty(0, device=self.device)
+        for i in self.moe_layers:
+            self.w_gu[i] = placeholder
+        super().load_hf_weights(iter(weights))
+        for i in self.moe_layers:
+            if self.w_gu[i] is placeholder:
+                self.w_gu[i] = saved[i]
+
+    def weight_bytes(self) -> int:
+        n = super().weight_bytes()
+        for lst in (self.w_router, self.w13, self.w2, self.w_sgu, self.w_sd, self.w_sgate):
+            n += sum(t.numel() * t.element_size() for t in lst if t is not None)
+        return n
+
+    def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        if i not in self.moe_layers:
+            return super().mlp(i, x)
+        logits = F.linear(x, self.w_router[i])
+        tw, tid = ops.moe_route(logits, self.k, self.renorm)
+        out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act)
+        if self.w_sgu[i] is not None:
+            sh = F.linear(ops.act_and_mul(F.linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
+            if self.w_sgate[i] is not None:
+                sh = sh * torch.sigmoid(F.linear(x, self.w_sgate[i]))
+            out = out + sh
+        return pstate.tp_all_reduce(out)

@@ -102,6 +102,56 @@ def fill_pending(ids: torch.Tensor, src: torch.Tensor, prev: torch.Tensor) -> No
     call("ome_fill_pending", ids.data_ptr(), src.data_ptr(), prev.data_ptr(), n, stream_ptr())
 
 
+def moe_route(logits: torch.Tensor, k: int, renorm: bool = True, scoring: str = "softmax",
+              out_w: torch.Tensor | None = None, out_ids: torch.Tensor | None = None):
+    """Router: logits [T, E] -> (weights f32 [T, k], expert ids int32 [T, k])."""
+    if not _gpu(logits):
+        w, ids = ref.moe_route(logits, k, renorm, scoring)
+        if out_w is not None:
+            out_w.copy_(w)
+            out_ids.copy_(ids)
+            return out_w, out_ids
+        return w, ids
+    T, E = logits.shape
+    out_w = torch.empty(T, k, dtype=torch.float32, device=logits.device) if out_w is None else out_w
+    out_ids = torch.empty(T, k, dtype=torch.int32, device=logits.device) if out_ids is None else out_ids
+    call("ome_moe_route", logits.data_ptr(), int(logits.dtype == torch.bfloat16), logits.stride(0), T, E, k,
+         int(renorm), 0 if scoring == "softmax" else 1, out_w.data_ptr(), out_ids.data_ptr(), stream_ptr())
+    return out_w, out_ids
+
+
+def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
+              act: int = 0, scale: float = 1.0) -> torch.Tensor:
+    """Sparse MoE MLP on MFMA: align (counting sort by expert, on device) -> grouped GEMM gate_up
+    with gathered A rows -> SiLU*mul -> grouped GEMM down -> weighted combine.  Shapes are
+    static given T (graph-capturable); per-expert counts never leave the GPU."""
+    if not _gpu(x):
+        return ref.fused_moe(x, topk_w, topk_ids, w13, w2, act, scale)
+    T, H = x.shape
+    E, I2, _ = w13.shape
+    I = I2 // 2
+    k = topk_ids.shape[1]
+    n = T * k
+    dev = x.device
+    offsets = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    sorted_ids = torch.empty(n, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    call("ome_moe_align", topk_ids.data_ptr(), n, E, offsets.data_ptr(), sorted_ids.data_ptr(), inv.data_ptr(),
+         stream_ptr())
+    max_tiles = -(-n // 64) + E
+    gu = torch.empty(n, I2, dtype=x.dtype, device=dev)
+    call("ome_moe_gemm", x.data_ptr(), x.stride(0), sorted_ids.data_ptr(), k, w13.data_ptr(), offsets.data_ptr(),
+         E, I2, H, max_tiles, gu.data_ptr(), gu.stride(0), stream_ptr())
+    h = act_and_mul(gu, act)
+    y = torch.empty(n, H, dtype=x.dtype, device=dev)
+    call("ome_moe_gemm", h.data_ptr(), h.stride(0), None, 0, w2.data_ptr(), offsets.data_ptr(), E, H, I,
+         max_tiles, y.data_ptr(), y.stride(0), stream_ptr())
+    out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    call("ome_moe_combine", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), float(scale),
+         stream_ptr())
+    return out
+
+
 class DecodeWorkspace:
     """Split-K partial buffers for paged decode, sized once (graph-capture safe)."""
 

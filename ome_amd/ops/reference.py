@@ -191,3 +191,27 @@ def pool(hidden, cu_lens, mode: int = 0, normalize: bool = True) -> torch.Tensor
     if normalize:
         out = torch.nn.functional.normalize(out, dim=-1)
     return out
+
+
+# ------------------------------------------------------------------ MoE
+def moe_route(logits, k: int, renorm: bool, scoring: str = "softmax"):
+    lf = logits.float()
+    p = torch.softmax(lf, -1) if scoring == "softmax" else torch.sigmoid(lf)
+    w, ids = torch.topk(p, k, dim=-1)  # ties: torch.topk order is implementation-defined
+    if renorm:
+        w = w / w.sum(-1, keepdim=True)
+    return w.float(), ids.to(torch.int32)
+
+
+def fused_moe(x, topk_w, topk_ids, w13, w2, act: int = 0, scale: float = 1.0):
+    """x [T, H]; w13 [E, 2I, H] (gate rows then up rows); w2 [E, H, I]."""
+    T, H = x.shape
+    out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
+    xf = x.float()
+    for e in torch.unique(topk_ids).tolist():
+        tok, slot = (topk_ids == e).nonzero(as_tuple=True)
+        gu = xf[tok] @ w13[e].float().t()
+        h = act_and_mul(gu.to(x.dtype), act).float()
+        y = (h.to(x.dtype).float() @ w2[e].float().t()).to(x.dtype).float()
+        out.index_add_(0, tok, y * topk_w[tok, slot].float()[:, None])
+    return (out * scale).to(x.dtype)
