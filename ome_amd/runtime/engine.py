@@ -87,7 +87,10 @@ class Engine:
             device = "cpu"
         self.max_context = min(args.context_length or self.cfg.max_position_embeddings,
                                self.cfg.max_position_embeddings)
-        self.runner = ModelRunner(self.cfg, device=device, model_path=args.model_path, load_format=args.load_format,
+        dtype = {"bfloat16": torch.bfloat16, "float16": torch.float16, "float32": torch.float32,
+                 "auto": torch.bfloat16}.get(str(args.dtype), torch.bfloat16)
+        self.runner = ModelRunner(self.cfg, device=device, dtype=dtype, model_path=args.model_path,
+                                  load_format=args.load_format,
                                   page_size=args.page_size, mem_fraction_static=args.mem_fraction_static,
                                   max_total_tokens=args.max_total_tokens, max_running=args.max_running_requests,
                                   max_context=self.max_context, cuda_graph=args.cuda_graph,
@@ -109,6 +112,7 @@ class Engine:
         self._aborts: list[str] = []
         self._wake = threading.Event()
         self._stop = False
+        self._stop_pending = False
         self.step_count = 0
         self.kv_transfer = None  # PD disaggregation hook (ome_amd.runtime.disagg)
         # overlapped scheduling: (batch, handle, launch time) of the step whose tokens are in flight
@@ -162,16 +166,28 @@ class Engine:
             if r is not None and r.on_token:
                 r.on_token(r, [], True)
 
-    def _broadcast_control(self, new, aborts):
+    def _broadcast_control(self, new, aborts, stop: bool = False):
+        """Rank 0 -> all TP ranks, once per step: new requests, aborts, and the group stop flag
+        (followers leave ``run_forever`` when the leader shuts down)."""
         import torch.distributed as dist
 
-        payload = [[(r.rid, r.prompt_ids, asdict(r.params)) for r in new], aborts]
+        payload = [[(r.rid, r.prompt_ids, asdict(r.params), r.bootstrap) for r in new], aborts,
+                   stop or self._stop_pending]
         obj = [payload if self.pstate.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=self._cpu_group())
+        if obj[0][2]:
+            self._stop = True
         if self.pstate.rank == 0:
             return new, aborts
-        reqs = [Request(prompt_ids=p, params=SamplingParams(**sp), rid=rid) for rid, p, sp in obj[0][0]]
+        reqs = [Request(prompt_ids=p, params=SamplingParams(**sp), rid=rid, bootstrap=b)
+                for rid, p, sp, b in obj[0][0]]
         return reqs, obj[0][1]
+
+    def stop_group(self) -> None:
+        """Leader: tell every follower rank to exit its step loop (one final control broadcast)."""
+        if self.pstate.tp_size > 1 and self.pstate.rank == 0:
+            self._broadcast_control([], [], stop=True)
+        self._stop = True
 
     def _cpu_group(self):
         import torch.distributed as dist
@@ -277,7 +293,10 @@ class Engine:
         return t
 
     def shutdown(self) -> None:
-        self._stop = True
+        if self.pstate.tp_size > 1 and self.pstate.rank == 0:
+            self._stop_pending = True  # the loop broadcasts it on its next step, then exits
+        else:
+            self._stop = True
         self._wake.set()
 
     def health(self) -> dict:
