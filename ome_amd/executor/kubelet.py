@@ -385,7 +385,7 @@ class Kubelet:
 
         env = {k: fix(v) for k, v in env.items()}
         for k, v in env.items():  # *_PORT env values naming a container port follow the remap
-            if k.endswith("_PORT") and v.isdigit() and int(v) in ports:
+            if (k == "PORT" or k.endswith("_PORT")) and v.isdigit() and int(v) in ports:
                 env[k] = str(ports[int(v)])
         cmd = list(c.get("command") or [])
         args = list(c.get("args") or [])

@@ -185,13 +185,17 @@ class ModelRunner:
         self.TUNED_DIR.mkdir(parents=True, exist_ok=True)
         arch = torch.cuda.get_device_properties(self.device).gcnArchName.split(":")[0]
         fname = str(self.TUNED_DIR / f"tunableop_{arch}.csv")
-        tun.set_filename(fname, insert_device_ordinal=False)
         tun.enable(True)
         tun.tuning_enable(True)
         tun.set_max_tuning_duration(int(os.environ.get("OME_TUNE_MS", "40")))
         tun.set_max_tuning_iterations(int(os.environ.get("OME_TUNE_ITERS", "30")))
         if os.path.exists(fname):
             tun.read_file(fname)
+        # one writer for the in-tree table: other ranks of a multi-GPU job keep their results in
+        # a private file (torch writes the table at process exit)
+        if int(os.environ.get("LOCAL_RANK", "0")) != 0:
+            fname = os.path.join("/tmp", f"tunableop_{arch}_rank{os.environ.get('LOCAL_RANK')}_{os.getpid()}.csv")
+        tun.set_filename(fname, insert_device_ordinal=False)
         self._tune_file = fname
         return True
 
