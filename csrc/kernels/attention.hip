@@ -557,6 +557,190 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Prefill v2 (G == 4): the workgroup's 4 waves share each 32-key K/V tile through LDS instead
+// of each wave streaming it from L1/L2 (v1 was load-path bound: 4 waves x 16 KB per tile).
+// Wave w takes head (w % G) of the kv group and row block (w / G): an item is 32*(4/G) query
+// rows.  Tiles are double-buffered: the next tile's global loads are in flight while the
+// current one is consumed from LDS.  LDS images (conflict-free for ds_read_b128):
+//   K: [32 keys][128 dims + 8 pad]         (row = 272 B: 16 rows start on distinct bank quads)
+//   V: [128 dims][32 keys + 8 pad], keys stored in the MFMA k-slot order of the S^T
+//      accumulators (slot 8g+j: j<4 -> page A key 4g+j, j>=4 -> page B key 4g+j-4), so a
+//      lane's A fragment of O^T = V^T P^T is one 16-B read.
+// ------------------------------------------------------------------------------------------
+constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
+
+__global__ __launch_bounds__(256) void paged_prefill_v2_kernel(
+    const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
+    const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
+    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window) {
+  constexpr int D = 128, P = 16, NB = D / 16, KS = D / 32;
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][32 * PF_KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][D * PF_VLD];
+  const int2 it = items[blockIdx.x];
+  const int s = it.x, r0_item = it.y;
+  const int kvh = blockIdx.y;
+  const int q0 = cu_q[s];
+  const int q_len = cu_q[s + 1] - q0;
+  const int kv_len = kv_lens[s];
+  const int prefix = kv_len - q_len;
+  const int G = Hq / Hkv;
+  const int rows_per_item = 32 * (4 / G);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n = lane & 15, g = lane >> 4;
+  const int hl = wave % G, rblk = wave / G;
+  const int head = kvh * G + hl;
+  const int r0 = r0_item + 32 * rblk;
+  const int item_hi = min(r0_item + rows_per_item, q_len);
+  const int kv_end = min(kv_len, prefix + item_hi);
+  int kv_lo = 0;
+  if (window > 0) kv_lo = max(0, prefix + r0_item - window + 1) & ~31;
+  const int* bt = block_tables + (int64_t)s * bt_stride;
+  const int64_t kpage = (int64_t)Hkv * P * D;
+
+  // ---- per-wave query fragments (rows r0 .. r0+31 of `head`) ----
+  bf16x8 qf[2][KS];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int r = r0 + 16 * rb + n;
+    const bf16* qr = q + (int64_t)(q0 + r) * q_stride + (int64_t)head * D;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[rb][ks] = (r < q_len) ? ld8(qr + 32 * ks + 8 * g) : bf16x8{};
+  }
+  float m_i[2] = {OME_NEG_INF, OME_NEG_INF}, l_i[2] = {0.f, 0.f};
+  f32x4 o[2][NB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) o[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- cooperative tile staging: 2 x 16 B of K and 2 x 16 B of V per thread ----
+  bf16x8 rk[2], rv[2];
+  auto load_tile = [&](int kb) {
+    const int pA = bt[kb / P];
+    const int pB = (kb + P < kv_len) ? bt[kb / P + 1] : pA;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int key = c >> 4, dc = c & 15;
+      const bf16* kp = k_cache + (key < 16 ? pA : pB) * kpage + (int64_t)kvh * P * D;
+      rk[i] = ld8(kp + (key & 15) * D + dc * 8);
+      const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
+      const bf16* vp = v_cache + (page ? pB : pA) * kpage + (int64_t)kvh * D * P;
+      rv[i] = ld8(vp + dim * P + half * 8);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      const int key = c >> 4, dc = c & 15;
+      *reinterpret_cast<bf16x8*>(&sK[buf][key * PF_KLD + dc * 8]) = rk[i];
+      const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
+      bf16* vrow = &sV[buf][dim * PF_VLD];
+      bf16x4 lo4 = {rv[i][0], rv[i][1], rv[i][2], rv[i][3]};
+      bf16x4 hi4 = {rv[i][4], rv[i][5], rv[i][6], rv[i][7]};
+      *reinterpret_cast<bf16x4*>(vrow + (2 * half) * 8 + page * 4) = lo4;      // keys 8h..8h+3
+      *reinterpret_cast<bf16x4*>(vrow + (2 * half + 1) * 8 + page * 4) = hi4;  // keys 8h+4..8h+7
+    }
+  };
+
+  int kb = kv_lo;
+  if (kb < kv_end) {
+    load_tile(kb);
+    store_tile(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  const bool active = r0 < q_len;  // a wave whose rows are all past q_len still stages tiles
+  for (; kb < kv_end; kb += 32) {
+    const bool more = kb + 32 < kv_end;
+    if (more) load_tile(kb + 32);
+    if (active) {
+      f32x4 sc[2][2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) sc[rb][0] = sc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[buf][n * PF_KLD + 32 * ks + 8 * g]);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[buf][(16 + n) * PF_KLD + 32 * ks + 8 * g]);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          sc[rb][0] = mfma16(a0, qf[rb][ks], sc[rb][0]);
+          sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
+        }
+      }
+      const bool need_mask = (kb + 32 > prefix + r0 + 1) || (kb + 32 > kv_len) || (window > 0);
+      bf16x8 pb[2];
+      float alpha[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int qpos = prefix + r0 + 16 * rb + n;
+        float mt = OME_NEG_INF;
+#pragma unroll
+        for (int X = 0; X < 2; ++X)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v = sc[rb][X][i] * scale_log2;
+            if (need_mask) {
+              const int key = kb + 16 * X + 4 * g + i;
+              const bool ok = key <= qpos && key < kv_len && (window <= 0 || key > qpos - window);
+              v = ok ? v : OME_NEG_INF;
+            }
+            sc[rb][X][i] = v;
+            mt = fmaxf(mt, v);
+          }
+        mt = fmaxf(mt, __shfl_xor(mt, 16));
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float m_new = fmaxf(m_i[rb], mt);
+        const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
+        alpha[rb] = fast_exp2(m_i[rb] - m_use);
+        float rs = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p0 = fast_exp2(sc[rb][0][i] - m_use), p1 = fast_exp2(sc[rb][1][i] - m_use);
+          pb[rb][i] = (bf16)p0;
+          pb[rb][4 + i] = (bf16)p1;
+          rs += p0 + p1;
+        }
+        rs += __shfl_xor(rs, 16);
+        rs += __shfl_xor(rs, 32);
+        l_i[rb] = l_i[rb] * alpha[rb] + rs;
+        m_i[rb] = m_new;
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sV[buf][(16 * nb + n) * PF_VLD + 8 * g]);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          o[rb][nb] = o[rb][nb] * alpha[rb];
+          o[rb][nb] = mfma16(a, pb[rb], o[rb][nb]);
+        }
+      }
+    }
+    if (more) store_tile(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (!active) return;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int r = r0 + 16 * rb + n;
+    if (r < q_len) {
+      const float inv = l_i[rb] > 0.f ? 1.f / l_i[rb] : 0.f;
+      bf16* orow = out + (int64_t)(q0 + r) * out_stride + (int64_t)head * D;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = (bf16)(o[rb][nb][i] * inv);
+        *reinterpret_cast<bf16x4*>(orow + 16 * nb + 4 * g) = v;
+      }
+    }
+  }
+}
+
 OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                               const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
                               const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
@@ -565,12 +749,20 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
   if (D != 128 || P != 16) return -2;
   if (Hq % Hkv != 0) return -3;
   const int G = Hq / Hkv;
-  const int nw = G < 8 ? G : 8;
   const float scale_log2 = scale * 1.4426950408889634f;
   dim3 grid(n_items, Hkv);
-  paged_prefill_kernel<128, 16><<<grid, 64 * nw, 0, stream>>>(
-      (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window);
+  const char* ve = getenv("OME_PREFILL_ATTN");
+  const int variant = ve ? atoi(ve) : 2;
+  if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
+    paged_prefill_v2_kernel<<<grid, 256, 0, stream>>>(
+        (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, cu_q,
+        kv_lens, (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window);
+  } else {
+    const int nw = G < 8 ? G : 8;
+    paged_prefill_kernel<128, 16><<<grid, 64 * nw, 0, stream>>>(
+        (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, cu_q,
+        kv_lens, (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window);
+  }
   OME_CHECK_LAUNCH();
   return 0;
 }

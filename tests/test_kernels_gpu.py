@@ -139,10 +139,12 @@ def test_paged_decode_window(variant, monkeypatch):
     _close(out, ref.paged_decode(q, kc, vc, bt, sl, 0.088, window=128))
 
 
-@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 1)])
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 1), (16, 4)])
 @pytest.mark.parametrize("q_lens,kv_lens", [([5], [5]), ([37, 64, 1, 100], [37, 80, 300, 100]),
-                                            ([300], [1000]), ([1, 1, 1], [20, 33, 16])])
-def test_paged_prefill(Hq, Hkv, q_lens, kv_lens):
+                                            ([300], [1000]), ([1, 1, 1], [20, 33, 16]), ([1000], [1000])])
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_paged_prefill(Hq, Hkv, q_lens, kv_lens, variant, monkeypatch):
+    monkeypatch.setenv("OME_PREFILL_ATTN", variant)
     D, P = 128, 16
     npages = sum(-(-L // P) for L in kv_lens) + 8
     kc, vc = _cache(npages, Hkv, D)
