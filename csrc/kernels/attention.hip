@@ -570,14 +570,15 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
 // ------------------------------------------------------------------------------------------
 constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
 
-__global__ __launch_bounds__(256) void paged_prefill_v2_kernel(
+template <int SUB>
+__global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
     const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
     bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window) {
   constexpr int D = 128, P = 16, NB = D / 16, KS = D / 32;
-  __shared__ __attribute__((aligned(16))) bf16 sK[2][32 * PF_KLD];
-  __shared__ __attribute__((aligned(16))) bf16 sV[2][D * PF_VLD];
+  __shared__ __attribute__((aligned(16))) bf16 sK[2][SUB][32 * PF_KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sV[2][SUB][D * PF_VLD];
   const int2 it = items[blockIdx.x];
   const int s = it.x, r0_item = it.y;
   const int kvh = blockIdx.y;
@@ -615,35 +616,43 @@ __global__ __launch_bounds__(256) void paged_prefill_v2_kernel(
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) o[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- cooperative tile staging: 2 x 16 B of K and 2 x 16 B of V per thread ----
-  bf16x8 rk[2], rv[2];
-  auto load_tile = [&](int kb) {
-    const int pA = bt[kb / P];
-    const int pB = (kb + P < kv_len) ? bt[kb / P + 1] : pA;
+  // ---- cooperative tile staging: per 32-key subtile, 2 x 16 B of K and 2 x 16 B of V per thread;
+  // a pipeline stage is SUB subtiles (32*SUB keys), so SUB x more bytes are in flight per wait ----
+  bf16x8 rk[SUB][2], rv[SUB][2];
+  auto load_tile = [&](int kb0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i;
-      const int key = c >> 4, dc = c & 15;
-      const bf16* kp = k_cache + (key < 16 ? pA : pB) * kpage + (int64_t)kvh * P * D;
-      rk[i] = ld8(kp + (key & 15) * D + dc * 8);
-      const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
-      const bf16* vp = v_cache + (page ? pB : pA) * kpage + (int64_t)kvh * D * P;
-      rv[i] = ld8(vp + dim * P + half * 8);
+    for (int u = 0; u < SUB; ++u) {
+      const int kb = kb0 + 32 * u;
+      const int pi = kb / P;
+      const int pA = (kb < kv_len) ? bt[pi] : bt[0];  // out-of-range subtiles: any valid page (masked)
+      const int pB = (kb + P < kv_len) ? bt[pi + 1] : pA;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = tid + 256 * i;
+        const int key = c >> 4, dc = c & 15;
+        const bf16* kp = k_cache + (key < 16 ? pA : pB) * kpage + (int64_t)kvh * P * D;
+        rk[u][i] = ld8(kp + (key & 15) * D + dc * 8);
+        const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
+        const bf16* vp = v_cache + (page ? pB : pA) * kpage + (int64_t)kvh * D * P;
+        rv[u][i] = ld8(vp + dim * P + half * 8);
+      }
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i;
-      const int key = c >> 4, dc = c & 15;
-      *reinterpret_cast<bf16x8*>(&sK[buf][key * PF_KLD + dc * 8]) = rk[i];
-      const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
-      bf16* vrow = &sV[buf][dim * PF_VLD];
-      bf16x4 lo4 = {rv[i][0], rv[i][1], rv[i][2], rv[i][3]};
-      bf16x4 hi4 = {rv[i][4], rv[i][5], rv[i][6], rv[i][7]};
-      *reinterpret_cast<bf16x4*>(vrow + (2 * half) * 8 + page * 4) = lo4;      // keys 8h..8h+3
-      *reinterpret_cast<bf16x4*>(vrow + (2 * half + 1) * 8 + page * 4) = hi4;  // keys 8h+4..8h+7
-    }
+    for (int u = 0; u < SUB; ++u)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = tid + 256 * i;
+        const int key = c >> 4, dc = c & 15;
+        *reinterpret_cast<bf16x8*>(&sK[buf][u][key * PF_KLD + dc * 8]) = rk[u][i];
+        const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
+        bf16* vrow = &sV[buf][u][dim * PF_VLD];
+        bf16x4 lo4 = {rv[u][i][0], rv[u][i][1], rv[u][i][2], rv[u][i][3]};
+        bf16x4 hi4 = {rv[u][i][4], rv[u][i][5], rv[u][i][6], rv[u][i][7]};
+        *reinterpret_cast<bf16x4*>(vrow + (2 * half) * 8 + page * 4) = lo4;      // keys 8h..8h+3
+        *reinterpret_cast<bf16x4*>(vrow + (2 * half + 1) * 8 + page * 4) = hi4;  // keys 8h+4..8h+7
+      }
   };
 
   int kb = kv_lo;
@@ -654,24 +663,27 @@ __global__ __launch_bounds__(256) void paged_prefill_v2_kernel(
   __syncthreads();
   int buf = 0;
   const bool active = r0 < q_len;  // a wave whose rows are all past q_len still stages tiles
-  for (; kb < kv_end; kb += 32) {
-    const bool more = kb + 32 < kv_end;
-    if (more) load_tile(kb + 32);
-    if (active) {
+  for (; kb < kv_end; kb += 32 * SUB) {
+    const bool more = kb + 32 * SUB < kv_end;
+    if (more) load_tile(kb + 32 * SUB);
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) {
+    const int kbu = kb + 32 * u;
+    if (active && kbu < kv_end) {
       f32x4 sc[2][2];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) sc[rb][0] = sc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[buf][n * PF_KLD + 32 * ks + 8 * g]);
-        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[buf][(16 + n) * PF_KLD + 32 * ks + 8 * g]);
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[buf][u][n * PF_KLD + 32 * ks + 8 * g]);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[buf][u][(16 + n) * PF_KLD + 32 * ks + 8 * g]);
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           sc[rb][0] = mfma16(a0, qf[rb][ks], sc[rb][0]);
           sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
         }
       }
-      const bool need_mask = (kb + 32 > prefix + r0 + 1) || (kb + 32 > kv_len) || (window > 0);
+      const bool need_mask = (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0);
       bf16x8 pb[2];
       float alpha[2];
 #pragma unroll
@@ -684,7 +696,7 @@ __global__ __launch_bounds__(256) void paged_prefill_v2_kernel(
           for (int i = 0; i < 4; ++i) {
             float v = sc[rb][X][i] * scale_log2;
             if (need_mask) {
-              const int key = kb + 16 * X + 4 * g + i;
+              const int key = kbu + 16 * X + 4 * g + i;
               const bool ok = key <= qpos && key < kv_len && (window <= 0 || key > qpos - window);
               v = ok ? v : OME_NEG_INF;
             }
@@ -711,13 +723,14 @@ __global__ __launch_bounds__(256) void paged_prefill_v2_kernel(
       }
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sV[buf][(16 * nb + n) * PF_VLD + 8 * g]);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sV[buf][u][(16 * nb + n) * PF_VLD + 8 * g]);
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           o[rb][nb] = o[rb][nb] * alpha[rb];
           o[rb][nb] = mfma16(a, pb[rb], o[rb][nb]);
         }
       }
+    }
     }
     if (more) store_tile(buf ^ 1);
     __syncthreads();
@@ -754,7 +767,7 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
   const char* ve = getenv("OME_PREFILL_ATTN");
   const int variant = ve ? atoi(ve) : 2;
   if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
-    paged_prefill_v2_kernel<<<grid, 256, 0, stream>>>(
+    paged_prefill_v2_kernel<2><<<grid, 256, 0, stream>>>(
         (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, cu_q,
         kv_lens, (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window);
   } else {
