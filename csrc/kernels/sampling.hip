@@ -147,3 +147,71 @@ OME_API int ome_sample(const void* logits, int is_bf16, int64_t stride, int B, i
   OME_CHECK_LAUNCH();
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------
+// Repetition / frequency / presence penalties (K12, vLLM / OpenAI semantics):
+//   counts[slot, v] low 24 bits = occurrences of v in the OUTPUT so far, bit 24 = v occurs in
+//   the prompt or output ("seen", for the repetition penalty).
+//   logit' = seen ? (logit > 0 ? logit / rep : logit * rep) : logit
+//   logit' -= freq * out_count + pres * (out_count > 0)
+// Rows whose three penalties are neutral return immediately, so the kernels stay in the decode
+// graph at ~zero cost when no request uses penalties.
+// ------------------------------------------------------------------------------------------
+constexpr int kSeenBit = 1 << 24;
+
+template <typename T>
+__global__ __launch_bounds__(256) void apply_penalties_kernel(T* __restrict__ logits, int64_t stride, int V,
+                                                              const int* __restrict__ counts, int64_t cstride,
+                                                              const int* __restrict__ slot,
+                                                              const float* __restrict__ rep,
+                                                              const float* __restrict__ freq,
+                                                              const float* __restrict__ pres) {
+  const int row = blockIdx.y;
+  const float rp = rep[row], fp = freq[row], pp = pres[row];
+  if (rp == 1.f && fp == 0.f && pp == 0.f) return;
+  const int* cr = counts + (int64_t)slot[row] * cstride;
+  T* lr = logits + (int64_t)row * stride;
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) {
+    const int c = cr[v];
+    if (c == 0) continue;
+    float x = (float)lr[v];
+    if ((c & kSeenBit) && rp != 1.f) x = x > 0.f ? x / rp : x * rp;
+    const int oc = c & (kSeenBit - 1);
+    x -= fp * (float)oc + (oc > 0 ? pp : 0.f);
+    lr[v] = (T)x;
+  }
+}
+
+OME_API int ome_apply_penalties(void* logits, int is_bf16, int64_t stride, int B, int V, const int* counts,
+                                int64_t cstride, const int* slot, const float* rep, const float* freq,
+                                const float* pres, hipStream_t stream) {
+  if (B <= 0) return 0;
+  dim3 grid(16, B);
+  if (is_bf16)
+    apply_penalties_kernel<bf16><<<grid, 256, 0, stream>>>((bf16*)logits, stride, V, counts, cstride, slot, rep,
+                                                           freq, pres);
+  else
+    apply_penalties_kernel<float><<<grid, 256, 0, stream>>>((float*)logits, stride, V, counts, cstride, slot, rep,
+                                                            freq, pres);
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// After sampling: count the new token for rows that use penalties.
+__global__ void update_counts_kernel(int* __restrict__ counts, int64_t cstride, const int* __restrict__ slot,
+                                     const int* __restrict__ ids, const float* __restrict__ rep,
+                                     const float* __restrict__ freq, const float* __restrict__ pres, int B) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  if (rep[i] == 1.f && freq[i] == 0.f && pres[i] == 0.f) return;
+  int* c = counts + (int64_t)slot[i] * cstride + ids[i];
+  *c = ((*c) + 1) | kSeenBit;  // one writer per (slot, token): a request occupies one row per step
+}
+
+OME_API int ome_update_counts(int* counts, int64_t cstride, const int* slot, const int* ids, const float* rep,
+                              const float* freq, const float* pres, int B, hipStream_t stream) {
+  if (B <= 0) return 0;
+  update_counts_kernel<<<(B + 255) / 256, 256, 0, stream>>>(counts, cstride, slot, ids, rep, freq, pres, B);
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -102,6 +102,23 @@ def fill_pending(ids: torch.Tensor, src: torch.Tensor, prev: torch.Tensor) -> No
     call("ome_fill_pending", ids.data_ptr(), src.data_ptr(), prev.data_ptr(), n, stream_ptr())
 
 
+def apply_penalties(logits, counts, slot, rep, freq, pres) -> None:
+    """Repetition / frequency / presence penalties on logits [B, V] in place (neutral rows skip)."""
+    if not _gpu(logits):
+        return ref.apply_penalties(logits, counts, slot, rep, freq, pres)
+    B, V = logits.shape
+    call("ome_apply_penalties", logits.data_ptr(), int(logits.dtype == torch.bfloat16), logits.stride(0), B, V,
+         counts.data_ptr(), counts.stride(0), _i32(slot).data_ptr(), rep.data_ptr(), freq.data_ptr(), pres.data_ptr(),
+         stream_ptr())
+
+
+def update_counts(counts, slot, ids, rep, freq, pres) -> None:
+    if not _gpu(counts):
+        return ref.update_counts(counts, slot, ids, rep, freq, pres)
+    call("ome_update_counts", counts.data_ptr(), counts.stride(0), _i32(slot).data_ptr(), _i32(ids).data_ptr(),
+         rep.data_ptr(), freq.data_ptr(), pres.data_ptr(), ids.shape[0], stream_ptr())
+
+
 def moe_route(logits: torch.Tensor, k: int, renorm: bool = True, scoring: str = "softmax",
               out_w: torch.Tensor | None = None, out_ids: torch.Tensor | None = None):
     """Router: logits [T, E] -> (weights f32 [T, k], expert ids int32 [T, k])."""

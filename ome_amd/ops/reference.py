@@ -215,3 +215,34 @@ def fused_moe(x, topk_w, topk_ids, w13, w2, act: int = 0, scale: float = 1.0):
         y = (h.to(x.dtype).float() @ w2[e].float().t()).to(x.dtype).float()
         out.index_add_(0, tok, y * topk_w[tok, slot].float()[:, None])
     return (out * scale).to(x.dtype)
+
+
+SEEN_BIT = 1 << 24
+
+
+def apply_penalties(logits, counts, slot, rep, freq, pres):
+    """In place; see csrc/kernels/sampling.hip."""
+    for b in range(logits.shape[0]):
+        rp, fp, pp = float(rep[b]), float(freq[b]), float(pres[b])
+        if rp == 1.0 and fp == 0.0 and pp == 0.0:
+            continue
+        c = counts[int(slot[b])]
+        nz = (c != 0).nonzero(as_tuple=True)[0]
+        if nz.numel() == 0:
+            continue
+        x = logits[b, nz].float()
+        cc = c[nz]
+        seen = (cc & SEEN_BIT) != 0
+        if rp != 1.0:
+            x = torch.where(seen, torch.where(x > 0, x / rp, x * rp), x)
+        oc = (cc & (SEEN_BIT - 1)).float()
+        x = x - fp * oc - pp * (oc > 0).float()
+        logits[b, nz] = x.to(logits.dtype)
+
+
+def update_counts(counts, slot, ids, rep, freq, pres):
+    for b in range(ids.shape[0]):
+        if float(rep[b]) == 1.0 and float(freq[b]) == 0.0 and float(pres[b]) == 0.0:
+            continue
+        s, t = int(slot[b]), int(ids[b])
+        counts[s, t] = (counts[s, t] + 1) | SEEN_BIT

@@ -46,7 +46,7 @@ def default_buckets(max_bs: int) -> list[int]:
 
 class _DecodeBuffers:
     FIELDS_I = ("ids", "pos", "slots", "seq_lens", "req_idx", "top_k", "src", "order")
-    FIELDS_F = ("temp", "top_p", "min_p")
+    FIELDS_F = ("temp", "top_p", "min_p", "rep", "freq", "pres")
 
     def __init__(self, bmax: int, device):
         self.bmax = bmax
@@ -139,6 +139,8 @@ class ModelRunner:
                            torch.zeros(nout, dtype=torch.float32, pin_memory=self.is_cuda)) for _ in range(2)]
         self._ring = 0
         self._ws_cache: dict[int, ops.DecodeWorkspace] = {}
+        # penalty bookkeeping: per request slot, output-token counts | prompt/output "seen" bit
+        self.counts = torch.zeros(max_running + 1, cfg.vocab_size, dtype=torch.int32, device=self.device)
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         self.use_graph = cuda_graph and self.is_cuda
@@ -167,8 +169,11 @@ class ModelRunner:
                         decode_ws=self.decode_ws(bs), order=d.view("order", bs))
         hidden = self.model.forward(d.view("ids", bs), meta, self.kv)
         logits = self.model.compute_logits(hidden)
+        pen = (d.view("rep", bs), d.view("freq", bs), d.view("pres", bs))
+        ops.apply_penalties(logits, self.counts, d.view("req_idx", bs), *pen)
         ops.sample(logits, d.view("temp", bs), d.view("top_k", bs), d.view("top_p", bs), d.view("min_p", bs),
                    d.view("seeds", bs), 0, out_ids=self.out_ids[:bs], out_logprob=self.out_lp[:bs])
+        ops.update_counts(self.counts, d.view("req_idx", bs), self.out_ids[:bs], *pen)
 
     # ------------------------------------------------------------------ GEMM tuning
     TUNED_DIR = Path(__file__).resolve().parent.parent / "_tuned"
@@ -271,6 +276,26 @@ class ModelRunner:
             ev.record()
         return StepHandle(ids_dev, n, hi, hl, ev)
 
+    def _init_penalty_rows(self, chunks) -> None:
+        """First time a penalised request runs in its slot: zero the slot's count row, mark the
+        prompt (and any already-generated tokens, e.g. after a preemption) as seen."""
+        for c in chunks:
+            r = c.req
+            if r.pen_init or not r.params.has_penalties or r.req_slot < 0:
+                continue
+            row = self.counts[r.req_slot]
+            row.zero_()
+            seen = [t for t in r.prompt_ids]
+            outs = [t for t in r.output_ids if t != PENDING]
+            if seen:
+                row[torch.tensor(seen, dtype=torch.long, device=self.device)] = ops.reference.SEEN_BIT
+            if outs:
+                oc = np.bincount(np.asarray(outs), minlength=self.cfg.vocab_size)
+                nz = np.nonzero(oc)[0]
+                idx = torch.from_numpy(nz).to(self.device)
+                row[idx] = torch.from_numpy(oc[nz].astype(np.int32)).to(self.device) | ops.reference.SEEN_BIT
+            r.pen_init = True
+
     @staticmethod
     def _src_row(r, pos: int, prev: "StepHandle | None") -> int:
         """Row of ``prev``'s sampled output holding the token at ``pos`` if it is pending."""
@@ -309,13 +334,20 @@ class ModelRunner:
             hf[off["temp"] + i] = p.temperature
             hf[off["top_p"] + i] = p.top_p
             hf[off["min_p"] + i] = p.min_p
+            hf[off["rep"] + i] = p.repetition_penalty
+            hf[off["freq"] + i] = p.frequency_penalty
+            hf[off["pres"] + i] = p.presence_penalty
             seeds[i] = self._seed(r, pos + 1)  # keyed by the position of the token being drawn
         for i in range(B, bs):
             hf[off["temp"] + i] = 0.0
             hf[off["top_p"] + i] = 1.0
             h[off["top_k"] + i] = -1
+            hf[off["rep"] + i] = 1.0
+            hf[off["freq"] + i] = 0.0
+            hf[off["pres"] + i] = 0.0
         # attention visits sequences longest-first (padding rows, seq_len 0, last)
         h[off["order"]:off["order"] + bs] = np.argsort(-h[off["seq_lens"]:off["seq_lens"] + bs], kind="stable")
+        self._init_penalty_rows(batch.chunks)
         d.dev.copy_(d.host, non_blocking=True)
         if any_pending:
             ops.fill_pending(d.view("ids", bs), d.view("src", bs), prev.ids_dev)
@@ -405,8 +437,25 @@ class ModelRunner:
         else:
             meta = AttnMeta("decode", t_pos, t_slots, self.slots.table.index_select(0, t_dreq), seq_lens=t_dlen,
                             decode_ws=ws, order=t_dord)
+        self._init_penalty_rows(chunks)
         hidden = self.model.forward(t_ids, meta, self.kv)
         logits = self.model.compute_logits(hidden.index_select(0, t_rows))
+        pen = None
+        if any(c.req.params.has_penalties for c in chunks):
+            pen = [torch.tensor([getattr(c.req.params, f) for c in chunks], dtype=torch.float32)
+                   for f in ("repetition_penalty", "frequency_penalty", "presence_penalty")]
+            pslot = torch.tensor([c.req.req_slot for c in chunks], dtype=torch.int32)
+            if self.is_cuda:
+                pen = [x.to(self.device, non_blocking=True) for x in pen]
+                pslot = pslot.to(self.device, non_blocking=True)
+            # only rows that sample a token this step are penalised/counted
+            sample_mask = torch.tensor([c.sample for c in chunks], dtype=torch.bool)
+            if not bool(sample_mask.all()):
+                keep = sample_mask.to(pen[0].device)
+                pen[0] = torch.where(keep, pen[0], torch.ones_like(pen[0]))
+                pen[1] = torch.where(keep, pen[1], torch.zeros_like(pen[1]))
+                pen[2] = torch.where(keep, pen[2], torch.zeros_like(pen[2]))
+            ops.apply_penalties(logits, self.counts, pslot, *pen)
         temp = torch.tensor([c.req.params.temperature for c in chunks], dtype=torch.float32)
         top_k = torch.tensor([c.req.params.top_k for c in chunks], dtype=torch.int32)
         top_p = torch.tensor([c.req.params.top_p for c in chunks], dtype=torch.float32)
@@ -417,7 +466,10 @@ class ModelRunner:
             temp, top_k, top_p, min_p, seeds = (x.to(self.device, non_blocking=True)
                                                 for x in (temp, top_k, top_p, min_p, seeds))
         out_ids, out_lp = ops.sample(logits, temp, top_k, top_p, min_p, seeds, 0)
-        return self._finish_launch(out_ids.to(torch.int32), out_lp, len(chunks))
+        out_ids = out_ids.to(torch.int32)
+        if pen is not None:
+            ops.update_counts(self.counts, pslot, out_ids, *pen)
+        return self._finish_launch(out_ids, out_lp, len(chunks))
 
     def embed(self, batch: StepBatch) -> list[list[float]]:
         """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts."""

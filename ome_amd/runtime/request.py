@@ -25,6 +25,10 @@ class SamplingParams:
     logprobs: bool = False
     n: int = 1
 
+    @property
+    def has_penalties(self) -> bool:
+        return self.repetition_penalty != 1.0 or self.frequency_penalty != 0.0 or self.presence_penalty != 0.0
+
     def validate(self) -> None:
         if self.max_new_tokens < 0:
             raise ValueError("max_new_tokens must be >= 0")
@@ -76,6 +80,7 @@ class Request:
     preempted: int = 0
     lora: str | None = None
     n_pending: int = 0             # placeholders in output_ids awaiting their sampled token
+    pen_init: bool = False         # penalty count row initialised for the current req_slot
     pending_row: int = -1          # row of the newest pending token in its step's sampled output
 
     @property

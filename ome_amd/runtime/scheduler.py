@@ -117,6 +117,7 @@ class Scheduler:
         if req.req_slot >= 0:
             self.slots.free(req.req_slot)
             req.req_slot = -1
+        req.pen_init = False
 
     def finish(self, req: Request, reason: str) -> None:
         if req in self.running:

@@ -208,3 +208,29 @@ def test_pool():
     cu = torch.tensor([0, 10, 50], dtype=torch.int32, device=DEV)
     _close(ops.pool(h, cu, 0, True), ref.pool(h, cu, 0, True), atol=1e-3)
     _close(ops.pool(h, cu, 1, True), ref.pool(h, cu, 1, True), atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_penalties(dtype):
+    B, V, S = 6, 128256, 9
+    logits = (torch.randn(B, V, device=DEV) * 3).to(dtype)
+    counts = torch.zeros(S, V, dtype=torch.int32, device=DEV)
+    g = torch.Generator().manual_seed(0)
+    for s in range(S):
+        idx = torch.randint(0, V, (300,), generator=g)
+        counts[s, idx[:200].to(DEV)] = ref.SEEN_BIT
+        counts[s, idx[200:].to(DEV)] = ref.SEEN_BIT | torch.randint(1, 5, (100,), generator=g, dtype=torch.int32).to(DEV)
+    slot = torch.tensor([3, 0, 8, 1, 5, 2], dtype=torch.int32, device=DEV)
+    rep = torch.tensor([1.0, 1.3, 2.0, 1.0, 1.1, 1.0], device=DEV)
+    freq = torch.tensor([0.0, 0.5, 0.0, 1.0, 0.2, 0.0], device=DEV)
+    pres = torch.tensor([0.0, 0.25, 0.0, 0.0, 1.5, 0.0], device=DEV)
+    want = logits.clone().cpu()
+    ref.apply_penalties(want, counts.cpu(), slot.cpu(), rep.cpu(), freq.cpu(), pres.cpu())
+    got = logits.clone()
+    ops.apply_penalties(got, counts, slot, rep, freq, pres)
+    _close(got, want, atol=1e-2 if dtype == torch.bfloat16 else 1e-5, rtol=1e-2)
+    ids = torch.randint(0, V, (B,), dtype=torch.int32, device=DEV)
+    cw = counts.cpu().clone()
+    ref.update_counts(cw, slot.cpu(), ids.cpu(), rep.cpu(), freq.cpu(), pres.cpu())
+    ops.update_counts(counts, slot, ids, rep, freq, pres)
+    assert torch.equal(counts.cpu(), cw)
