@@ -17,6 +17,7 @@ import torch.nn.functional as F
 from ome_amd import ops
 from ome_amd.models.common import AttnMeta, PagedKVCache
 from ome_amd.models.config import ModelConfig, rope_cos_sin
+from ome_amd.models.quant import Fp8Weight, dequant_fp8_stream, fp8_block_size, linear, quantize_weight
 from ome_amd.parallel import state as pstate
 
 
@@ -76,6 +77,8 @@ class LlamaForCausalLM:
         self.lm_head: torch.Tensor | None = None
         mp = max_positions or cfg.max_position_embeddings
         self.cos_sin = rope_cos_sin(cfg, mp, device=self.device)
+        self.fp8 = (cfg.quantization or "").lower() in ("fp8", "fbgemm_fp8")
+        self.fp8_block = fp8_block_size(cfg) if self.fp8 else 0
 
     # ------------------------------------------------------------------ weights
     def _alloc(self, *shape, std: float | None, gen: torch.Generator | None) -> torch.Tensor:
@@ -108,7 +111,30 @@ class LlamaForCausalLM:
         self.embed = self._alloc(tp.vocab, H, std=1.0, gen=gen)
         self.norm = self._alloc(H, std=None, gen=gen)
         self.lm_head = self.embed if cfg.tie_word_embeddings else self._alloc(tp.vocab, H, std=std, gen=gen)
+        self._post_load()
         return self
+
+    def _quantizable(self, w) -> bool:
+        return isinstance(w, torch.Tensor) and w.dim() == 2 and w.numel() > 0 and w.shape[0] % 64 == 0 and \
+            w.shape[1] % 128 == 0
+
+    def _post_load(self) -> None:
+        """``quantization: fp8``: the QKV / O / gate-up / down projections become W8A8 (the
+        embedding, LM head and norms stay bf16, as in the reference runtimes)."""
+        if not self.fp8:
+            return
+        kept = 0
+        for lst in (self.w_qkv, self.w_o, self.w_gu, self.w_d):
+            for i in self.layers:
+                if self._quantizable(lst[i]):
+                    lst[i] = quantize_weight(lst[i], self.fp8_block)
+                elif isinstance(lst[i], torch.Tensor) and lst[i].numel():
+                    kept += 1
+        if kept:
+            import logging
+
+            logging.getLogger("ome_amd.models").warning("fp8: %d projections keep bf16 (shape not 64x128-tileable)",
+                                                        kept)
 
     def load_hf_weights(self, weights) -> "LlamaForCausalLM":
         """Load from an iterator of (hf_name, tensor) — shards / fuses for this TP rank."""
@@ -122,6 +148,8 @@ class LlamaForCausalLM:
         def put(t):
             return t.to(device=self.device, dtype=self.dtype).contiguous()
 
+        if self.fp8:
+            weights = dequant_fp8_stream(weights, self.fp8_block, self.dtype)
         for name, w in weights:
             if name.startswith("model."):
                 name = name[len("model."):]
@@ -173,6 +201,7 @@ class LlamaForCausalLM:
         missing = [i for i in self.layers if self.w_qkv[i] is None or self.w_gu[i] is None]
         if missing or self.embed is None:
             raise ValueError(f"checkpoint incomplete: layers missing {missing[:4]}...")
+        self._post_load()
         return self
 
     def _vocab_shard(self, w: torch.Tensor) -> torch.Tensor:
@@ -187,7 +216,9 @@ class LlamaForCausalLM:
         for lst in (self.w_qkv, self.b_qkv, self.w_o, self.ln1, self.ln2, self.w_gu, self.w_d, self.qn, self.kn,
                     [self.embed, self.norm, self.lm_head]):
             for t in lst:
-                if t is not None and t.data_ptr() not in seen:
+                if isinstance(t, Fp8Weight):
+                    n += t.nbytes()
+                elif t is not None and t.data_ptr() not in seen:
                     seen.add(t.data_ptr())
                     n += t.numel() * t.element_size()
         return n
@@ -209,9 +240,9 @@ class LlamaForCausalLM:
                                  self.scale, self.window)
 
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
-        gu = F.linear(x, self.w_gu[i])
+        gu = linear(x, self.w_gu[i])
         a = ops.act_and_mul(gu, self.act)
-        return pstate.tp_all_reduce(F.linear(a, self.w_d[i]))
+        return pstate.tp_all_reduce(linear(a, self.w_d[i]))
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: PagedKVCache,
                 input_embeds: torch.Tensor | None = None) -> torch.Tensor:
@@ -228,13 +259,13 @@ class LlamaForCausalLM:
         for i in self.layers:
             if i > 0:
                 ops.fused_add_rmsnorm(x, residual, self.ln1[i], self.eps)
-            qkv = F.linear(x, self.w_qkv[i], self.b_qkv[i])
+            qkv = linear(x, self.w_qkv[i], self.b_qkv[i])
             q = torch.empty(T, tp.hq, D, dtype=self.dtype, device=x.device)
             k_cache, v_cache = kv.layer(i)
             ops.rope_qkv_cache(qkv, meta.positions, self.cos_sin, cfg.rot_dim, q, k_cache, v_cache, meta.slots,
                                tp.hq, tp.hkv, D, True, self.qn[i], self.kn[i], self.eps)
             attn = self.attention(q, k_cache, v_cache, meta)
-            o = pstate.tp_all_reduce(F.linear(attn.view(T, tp.hq * D), self.w_o[i]))
+            o = pstate.tp_all_reduce(linear(attn.view(T, tp.hq * D), self.w_o[i]))
             ops.fused_add_rmsnorm(o, residual, self.ln2[i], self.eps)
             x = self.mlp(i, o)
         ops.fused_add_rmsnorm(x, residual, self.norm, self.eps)

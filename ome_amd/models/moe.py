@@ -66,6 +66,10 @@ class MoEForCausalLM(LlamaForCausalLM):
         experts: dict[int, dict[int, dict[str, torch.Tensor]]] = {}
         shared: dict[int, dict[str, torch.Tensor]] = {}
         rest_iter = []
+        if self.fp8:
+            from ome_amd.models.quant import dequant_fp8_stream
+
+            weights = dequant_fp8_stream(weights, self.fp8_block, self.dtype)
 
         def put(t):
             return t.to(device=self.device, dtype=self.dtype).contiguous()

@@ -1,0 +1,120 @@
+"""FP8 (OCP e4m3fn) weight-quantised linear layers.
+
+The reference's runtimes serve ``quantization: fp8`` checkpoints two ways, and both are covered:
+
+* **per-channel** (``--quantization fp8`` online quantisation of a bf16 checkpoint, and the
+  per-tensor / per-channel ``weight_scale`` FP8 checkpoints such as Llama-3.1-*-FP8): weight
+  scale per output row, activation scale per token;
+* **block-scaled** (DeepSeek-V3 / Kimi-K2 style ``weight_scale_inv`` with
+  ``weight_block_size: [128, 128]``): weight scale per 128x128 block, activation scale per
+  1x128 group.
+
+Activations are always quantised dynamically by ``ome_fp8_quant`` (static ``input_scale`` of a
+checkpoint is ignored: dynamic scales are at least as accurate and cost one fused pass).  The
+GEMM is ``ome_fp8_gemm`` (csrc/kernels/fp8.hip).  FP8 checkpoints are streamed through
+:func:`dequant_fp8_stream` so every model loader keeps seeing bf16 tensors, then
+:func:`quantize_weight` re-quantises the fused (QKV / gate-up) shards: with the checkpoint's own
+block structure and ``amax/448`` scales that round-trip is exact.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from ome_amd import ops
+from ome_amd.ops import reference as ref
+
+
+@dataclass
+class Fp8Weight:
+    q: torch.Tensor        # [N, K] float8_e4m3fn
+    scale: torch.Tensor    # [N] (block 0) or [ceil(N/128), K/128] (block 128), float32
+    block: int = 0
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    def nbytes(self) -> int:
+        return self.q.numel() + self.scale.numel() * 4
+
+    def dequant(self, dtype=torch.bfloat16) -> torch.Tensor:
+        return ref.fp8_dequant_weight(self.q, self.scale, self.block).to(dtype)
+
+
+def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
+    """bf16/fp32 [N, K] -> Fp8Weight (amax/448 scales per row, or per 128x128 block)."""
+    N, K = w.shape
+    wf = w.float()
+    if block:
+        nb, kb = -(-N // block), K // block
+        pad = nb * block - N
+        wp = F.pad(wf, (0, 0, 0, pad)) if pad else wf
+        blocks = wp.reshape(nb, block, kb, block)
+        amax = blocks.abs().amax(dim=(1, 3))
+        s = torch.where(amax > 0, amax / ref.FP8_MAX, torch.ones_like(amax))
+        q = (blocks / s[:, None, :, None]).clamp(-ref.FP8_MAX, ref.FP8_MAX).to(torch.float8_e4m3fn)
+        q = q.reshape(nb * block, K)[:N].contiguous()
+        return Fp8Weight(q, s.contiguous(), block)
+    amax = wf.abs().amax(-1)
+    s = torch.where(amax > 0, amax / ref.FP8_MAX, torch.ones_like(amax))
+    q = (wf / s[:, None]).clamp(-ref.FP8_MAX, ref.FP8_MAX).to(torch.float8_e4m3fn).contiguous()
+    return Fp8Weight(q, s.contiguous(), 0)
+
+
+def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """Dispatch: plain tensor -> hipBLASLt GEMM; Fp8Weight -> W8A8 MFMA path."""
+    if isinstance(w, Fp8Weight):
+        return ops.fp8_linear(x, w.q, w.scale, w.block, bias)
+    return F.linear(x, w, bias)
+
+
+def fp8_block_size(cfg) -> int:
+    qc = (cfg.extra or {}).get("quantization_config") or {}
+    wbs = qc.get("weight_block_size")
+    if wbs:
+        if list(wbs) != [128, 128]:
+            raise ValueError(f"unsupported fp8 weight_block_size {wbs} (128x128 only)")
+        return 128
+    return 0
+
+
+def dequant_fp8_stream(weights, block: int, dtype=torch.bfloat16):
+    """Pass (name, tensor) through, turning FP8 checkpoint weights + their ``weight_scale`` /
+    ``weight_scale_inv`` companions into dequantised tensors (order-independent)."""
+    pending_w: dict[str, torch.Tensor] = {}
+    pending_s: dict[str, tuple[torch.Tensor, bool]] = {}
+
+    def emit(base: str, q: torch.Tensor, s: torch.Tensor, blockwise: bool):
+        s = s.float().to(q.device)
+        if s.numel() == 1:
+            w = q.float() * s.reshape(())
+        elif blockwise:  # ``weight_scale_inv``: one scale per block x block tile
+            w = ref.fp8_dequant_weight(q, s.reshape(-(-q.shape[0] // (block or 128)), -1), block or 128)
+        else:            # ``weight_scale``: per output channel
+            w = q.float() * s.reshape(-1, 1)
+        return base + ".weight", w.to(dtype)
+
+    for name, t in weights:
+        if name.endswith(".input_scale") or name.endswith(".activation_scale"):
+            continue
+        if name.endswith(".weight_scale") or name.endswith(".weight_scale_inv"):
+            base = name.rsplit(".", 1)[0]
+            blockwise = name.endswith("_inv")
+            if base in pending_w:
+                yield emit(base, pending_w.pop(base), t, blockwise)
+            else:
+                pending_s[base] = (t, blockwise)
+            continue
+        if name.endswith(".weight") and t.dtype in (torch.float8_e4m3fn, torch.float8_e5m2):
+            base = name[: -len(".weight")]
+            if base in pending_s:
+                yield emit(base, t, *pending_s.pop(base))
+            else:
+                pending_w[base] = t
+            continue
+        yield name, t
+    if pending_w:
+        raise ValueError(f"fp8 weights without scales: {sorted(pending_w)[:4]}")

@@ -119,6 +119,49 @@ def update_counts(counts, slot, ids, rep, freq, pres) -> None:
          rep.data_ptr(), freq.data_ptr(), pres.data_ptr(), ids.shape[0], stream_ptr())
 
 
+def fp8_quant(x: torch.Tensor, group: int = 0):
+    """Dynamic activation quantisation to OCP e4m3: x [M, K] bf16 -> (q [M, K], scale f32 [M, KB]).
+    ``group`` 0 = one scale per row, 128 = one per 128-wide K group (block-scaled checkpoints)."""
+    if not _gpu(x):
+        return ref.fp8_quant(x, group)
+    M, K = x.shape
+    assert x.dtype == torch.bfloat16 and x.stride(1) == 1
+    q = torch.empty(M, K, dtype=torch.float8_e4m3fn, device=x.device)
+    s = torch.empty(M, K // group if group else 1, dtype=torch.float32, device=x.device)
+    call("ome_fp8_quant", x.data_ptr(), x.stride(0), M, K, q.data_ptr(), s.data_ptr(), group, stream_ptr())
+    return q, s
+
+
+def fp8_gemm(qa, sa, qw, sw, block: int = 0, bias=None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[M, N] bf16 = dequant(qa) . dequant(qw)^T (+ bias); qw [N, K] e4m3 with per-channel (block=0,
+    sw [N]) or 128x128 block scales (block=128, sw [N/128, K/128])."""
+    if not _gpu(qa):
+        r = ref.fp8_gemm(qa, sa, qw, sw, block, bias)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    M, K = qa.shape
+    N = qw.shape[0]
+    assert qw.shape[1] == K and qa.is_contiguous() and qw.is_contiguous()
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=qa.device)
+    call("ome_fp8_gemm", qa.data_ptr(), qa.stride(0), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), M, N, K, block,
+         out.data_ptr(), out.stride(0), ptr(bias), stream_ptr())
+    return out
+
+
+def fp8_linear(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0, bias=None) -> torch.Tensor:
+    """W8A8 linear: dynamic per-token (or per-1x128-group) activation quant + FP8 MFMA GEMM."""
+    shape = x.shape
+    x2 = x.reshape(-1, shape[-1])
+    qa, sa = fp8_quant(x2, block)
+    y = fp8_gemm(qa, sa, qw, sw, block, bias)
+    if y.dtype != x.dtype:  # CPU reference models may run in fp32
+        y = y.to(x.dtype)
+    return y.reshape(*shape[:-1], qw.shape[0])
+
+
 def moe_route(logits: torch.Tensor, k: int, renorm: bool = True, scoring: str = "softmax",
               out_w: torch.Tensor | None = None, out_ids: torch.Tensor | None = None):
     """Router: logits [T, E] -> (weights f32 [T, k], expert ids int32 [T, k])."""

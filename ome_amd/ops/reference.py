@@ -246,3 +246,35 @@ def update_counts(counts, slot, ids, rep, freq, pres):
             continue
         s, t = int(slot[b]), int(ids[b])
         counts[s, t] = (counts[s, t] + 1) | SEEN_BIT
+
+
+# ------------------------------------------------------------------ FP8 (OCP e4m3fn) W8A8
+FP8_MAX = 448.0
+
+
+def fp8_quant(x: torch.Tensor, group: int = 0):
+    """x [M, K] -> (q float8_e4m3fn [M, K], scale f32 [M, K/group or 1])."""
+    M, K = x.shape
+    g = K if group == 0 else group
+    xg = x.float().reshape(M, K // g, g)
+    amax = xg.abs().amax(-1)
+    s = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    q = (xg * (1.0 / s)[..., None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).reshape(M, K)
+    return q, s
+
+
+def fp8_dequant_weight(q: torch.Tensor, scale: torch.Tensor, block: int) -> torch.Tensor:
+    w = q.float()
+    if block:
+        s = scale.float().repeat_interleave(block, 0)[: w.shape[0]].repeat_interleave(block, 1)[:, : w.shape[1]]
+        return w * s
+    return w * scale.float().reshape(-1, 1)
+
+
+def fp8_gemm(qa, sa, qw, sw, block: int, bias=None, out_dtype=torch.bfloat16):
+    a = qa.float()
+    a = a * (sa.float().repeat_interleave(block, 1) if block else sa.float().reshape(-1, 1))
+    out = a @ fp8_dequant_weight(qw, sw, block).t()
+    if bias is not None:
+        out = out + bias.float()
+    return out.to(out_dtype)

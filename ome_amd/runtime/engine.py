@@ -49,6 +49,7 @@ class EngineArgs:
     disable_radix_cache: bool = False
     is_embedding: bool = False
     kv_cache_dtype: str = "auto"
+    quantization: str | None = None        # "fp8": W8A8 projections (online quant of bf16 weights)
     dist_init_addr: str | None = None
     nnodes: int = 1
     node_rank: int = 0
@@ -67,6 +68,8 @@ class EngineArgs:
             cfg = cfg.shrink(self.num_layers_override)
         if self.is_embedding:
             cfg.is_embedding = True
+        if self.quantization:
+            cfg.quantization = self.quantization
         return cfg
 
 

@@ -59,6 +59,7 @@ def build_parser() -> argparse.ArgumentParser:
     a("--load-format", default="auto")
     a("--dtype", default="bfloat16")
     a("--kv-cache-dtype", default="auto")
+    a("--quantization", default=None, help="fp8: W8A8 projections (per-channel online, or the checkpoint's blocks)")
     a("--random-seed", type=int, default=0)
     a("--device", default="cuda")
     a("--dist-init-addr", "--nccl-init", dest="dist_init_addr", default=None)
@@ -90,7 +91,8 @@ def engine_args_from(ns, rank_tp: int | None = None):
                       cuda_graph_max_bs=ns.cuda_graph_max_bs, load_format=load_fmt, dtype=ns.dtype,
                       device=ns.device, seed=ns.random_seed, enable_mixed_chunk=ns.enable_mixed_chunk,
                       disable_radix_cache=ns.disable_radix_cache, is_embedding=ns.is_embedding,
-                      kv_cache_dtype=ns.kv_cache_dtype, dist_init_addr=ns.dist_init_addr, nnodes=ns.nnodes,
+                      kv_cache_dtype=ns.kv_cache_dtype, quantization=ns.quantization,
+                      dist_init_addr=ns.dist_init_addr, nnodes=ns.nnodes,
                       node_rank=ns.node_rank, disaggregation_mode=ns.disaggregation_mode,
                       num_layers_override=ns.num_layers,
                       overlap_schedule=False if ns.disable_overlap_schedule else None)
