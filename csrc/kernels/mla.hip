@@ -1,0 +1,225 @@
+// Multi-head latent attention (DeepSeek-V2/V3, Kimi-K2) in the absorbed
+// form, for gfx950.
+//
+// Every layer caches one 576-wide latent row per token: [c_kv (512, kv_a_layernorm'd) | k_pe
+// (64, roped)], paged as cache[pages, 16, 576] bf16.  With W_UK folded into the query
+// (q_lat = [q_nope . W_UK | q_pe], 576 wide) and W_UV applied after the attention, MLA is
+// multi-QUERY attention over that latent: scores use all 576 dims, values are the first 512.
+// The same kernel serves decode, prefill and chunked prefill: a work item is one query token
+// x 16 heads (every head of a token shares the causal limit) x one split-K partition.
+//
+// Workgroup = 4 waves: all four compute S^T for the same 16 heads x 32 keys (the K tile is
+// staged once in LDS and read by all), and each wave owns 128 of the 512 value dims.
+//   S^T = K . Q^T     v_mfma_f32_16x16x32_bf16, A = K rows from LDS (ds_read_b128),
+//                     B = Q held in registers (18 k-steps of 32 dims)
+//   O^T += V^T . P^T  A = V^T from the SAME LDS image via ds_read_b64_tr_b16 (hardware
+//                     transpose, cdna_hip_programming.md T10), B = P^T straight from the S^T
+//                     accumulators in the permuted k-slot order of attention.hip
+// LDS rows are 1152 B (72 x 16-B chunks); chunk x of key row r lives at x ^ (r & 7), which
+// spreads both the row reads and the transposed reads over the banks.
+#include "common.h"
+
+#ifndef OME_NEG_INF
+#define OME_NEG_INF (-__builtin_inff())
+#endif
+
+namespace {
+
+constexpr int DK = 576, DV = 512, CH = DK / 8;  // 72 chunks of 8 bf16 per key row
+constexpr int KT = 32;                          // keys per iteration (two 16-token pages)
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * CH + (chunk ^ (row & 7)); }
+
+__device__ __forceinline__ bf16x4 tr_read(const bf16* lds_base, int byte_off) {
+  const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (s16x4 __attribute__((address_space(3)))*)((__attribute__((address_space(3))) char*)(
+          (__attribute__((address_space(3))) bf16*)lds_base) + byte_off));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void mla_attn_kernel(
+    const bf16* __restrict__ q, int64_t q_stride_t, const bf16* __restrict__ cache,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_row,
+    const int* __restrict__ kv_lens, int H, float scale_log2, int parts, bf16* __restrict__ out,
+    int64_t out_stride_t, float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+  __shared__ __attribute__((aligned(16))) bf16 sK[KT * DK];
+  const int t = blockIdx.x, h0 = blockIdx.y * 16, part = blockIdx.z;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int col = lane & 15, g = lane >> 4;
+  const int L = kv_lens[t];
+  const int n_pages = (L + 15) >> 4;
+  const int pairs = (n_pages + 1) >> 1;
+  const int per_part = (pairs + parts - 1) / parts;
+  const int pair_begin = part * per_part, pair_end = min(pairs, pair_begin + per_part);
+  const int* bt = block_tables + (int64_t)tok_row[t] * bt_stride;
+  const int64_t ws_row = ((int64_t)t * H + h0 + col) * parts + part;
+
+  // ---- Q^T operand: lane (col, g) holds Q[h0+col][32 s + 8 g + j] ----
+  bf16x8 qf[DK / 32];
+  const bf16* qp = q + (int64_t)t * q_stride_t + (int64_t)(h0 + col) * DK + 8 * g;
+#pragma unroll
+  for (int s = 0; s < DK / 32; ++s) qf[s] = ld8(qp + 32 * s);
+
+  f32x4 o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = OME_NEG_INF, lsum = 0.f;
+
+  // staging: 32 keys x 72 chunks = 2304 chunks, 9 per thread; chunk c -> (key c/72, x c%72)
+  bf16x8 stage[9];
+  auto load_pair = [&](int pr) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int c = tid + 256 * i;
+      const int key = c / CH, x = c - key * CH;
+      const int pg = 2 * pr + (key >> 4);
+      const int page = bt[pg < n_pages ? pg : 0];
+      stage[i] = ld8(cache + ((int64_t)page * 16 + (key & 15)) * DK + 8 * x);
+    }
+  };
+  if (pair_begin < pair_end) load_pair(pair_begin);
+
+  for (int pr = pair_begin; pr < pair_end; ++pr) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int c = tid + 256 * i;
+      const int key = c / CH, x = c - key * CH;
+      *reinterpret_cast<bf16x8*>(&sK[swz(key, x) * 8]) = stage[i];
+    }
+    __syncthreads();
+    if (pr + 1 < pair_end) load_pair(pr + 1);
+
+    // ---- S^T [32 keys x 16 heads] ----
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < DK / 32; ++s) {
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[swz(col, 4 * s + g) * 8]);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[swz(16 + col, 4 * s + g) * 8]);
+      s0 = mfma16x32(a0, qf[s], s0);
+      s1 = mfma16x32(a1, qf[s], s1);
+    }
+    // ---- mask + online softmax (column = head, lane-local up to the 4 lane groups) ----
+    const int kbase = pr * KT;
+    float mx = OME_NEG_INF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s0[i] = (kbase + 4 * g + i < L) ? s0[i] * scale_log2 : OME_NEG_INF;
+      s1[i] = (kbase + 16 + 4 * g + i < L) ? s1[i] * scale_log2 : OME_NEG_INF;
+      mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = (m_new == OME_NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - m_new);
+    bf16x8 pb;
+    float ps = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p0 = (m_new == OME_NEG_INF) ? 0.f : __builtin_amdgcn_exp2f(s0[i] - m_new);
+      const float p1 = (m_new == OME_NEG_INF) ? 0.f : __builtin_amdgcn_exp2f(s1[i] - m_new);
+      ps += p0 + p1;
+      pb[i] = (bf16)p0;
+      pb[4 + i] = (bf16)p1;
+    }
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    lsum = lsum * alpha + ps;
+    m = m_new;
+    // ---- O^T [this wave's 128 dims x 16 heads] += V^T . P^T ----
+    // tr-read block: rows = keys 4g + q (+16 for page B), cols = 16 dims; lane 4q+p of the
+    // group addresses row q, columns 4p..4p+3.
+    const int qrow = (lane & 15) >> 2, pcol = lane & 3;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const int d0 = wave * 128 + 16 * nb + 4 * pcol;  // first of this lane's 4 dims
+      const int ra = 4 * g + qrow, rb = 16 + 4 * g + qrow;
+      const int oa = swz(ra, d0 >> 3) * 16 + (d0 & 7) * 2;
+      const int ob = swz(rb, d0 >> 3) * 16 + (d0 & 7) * 2;
+      const bf16x4 va = tr_read(sK, oa), vb = tr_read(sK, ob);
+      bf16x8 a;
+      a[0] = va[0]; a[1] = va[1]; a[2] = va[2]; a[3] = va[3];
+      a[4] = vb[0]; a[5] = vb[1]; a[6] = vb[2]; a[7] = vb[3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[nb][i] *= alpha;
+      o[nb] = mfma16x32(a, pb, o[nb]);
+    }
+  }
+
+  // ---- epilogue: O^T lane map dim = 16 nb + 4 g + i, head = col ----
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  if (parts == 1) {
+    bf16* op = out + (int64_t)t * out_stride_t + (int64_t)(h0 + col) * DV + wave * 128 + 4 * g;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (bf16)(o[nb][i] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * nb) = v;
+    }
+  } else {
+    float* wp = ws_o + ws_row * DV + wave * 128 + 4 * g;
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb)
+      *reinterpret_cast<f32x4*>(wp + 16 * nb) = f32x4{o[nb][0] * inv, o[nb][1] * inv, o[nb][2] * inv,
+                                                       o[nb][3] * inv};
+    if (wave == 0 && g == 0) {
+      ws_ml[2 * ws_row] = m;
+      ws_ml[2 * ws_row + 1] = lsum;
+    }
+  }
+}
+
+// merge split-K partitions: one workgroup per (token, head), 128 threads x 4 dims
+__global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict__ ws_o,
+                                                         const float* __restrict__ ws_ml, int H, int parts,
+                                                         bf16* __restrict__ out, int64_t out_stride_t) {
+  const int t = blockIdx.x, h = blockIdx.y;
+  const int64_t row0 = ((int64_t)t * H + h) * parts;
+  float M = OME_NEG_INF;
+  for (int p = 0; p < parts; ++p)
+    if (ws_ml[2 * (row0 + p) + 1] > 0.f) M = fmaxf(M, ws_ml[2 * (row0 + p)]);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float den = 0.f;
+  for (int p = 0; p < parts; ++p) {
+    const float l = ws_ml[2 * (row0 + p) + 1];
+    if (!(l > 0.f)) continue;
+    const float w = l * __builtin_amdgcn_exp2f(ws_ml[2 * (row0 + p)] - M);
+    const f32x4 v = *reinterpret_cast<const f32x4*>(ws_o + (row0 + p) * DV + 4 * threadIdx.x);
+    acc += w * v;
+    den += w;
+  }
+  const float inv = den > 0.f ? 1.f / den : 0.f;
+  bf16x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = (bf16)(acc[i] * inv);
+  *reinterpret_cast<bf16x4*>(out + (int64_t)t * out_stride_t + (int64_t)h * DV + 4 * threadIdx.x) = r;
+}
+
+// q [T, H, 576] (token stride q_stride_t), cache [pages, 16, 576], out [T, H, 512].
+// tok_row[t] = block-table row of token t; kv_lens[t] = keys visible to token t (causal).
+// parts > 1 needs ws_o [T*H*parts*512] f32 and ws_ml [T*H*parts*2] f32.
+OME_API int ome_mla_attn(const void* q, int64_t q_stride_t, const void* cache, const int* block_tables,
+                         int bt_stride, const int* tok_row, const int* kv_lens, int T, int H, float scale,
+                         int parts, void* out, int64_t out_stride_t, float* ws_o, float* ws_ml, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (H % 16 || parts < 1 || (parts > 1 && (!ws_o || !ws_ml))) return -2;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(T, H / 16, parts);
+  mla_attn_kernel<<<grid, 256, 0, stream>>>((const bf16*)q, q_stride_t, (const bf16*)cache, block_tables, bt_stride,
+                                            tok_row, kv_lens, H, scale_log2, parts, (bf16*)out, out_stride_t, ws_o,
+                                            ws_ml);
+  OME_CHECK_LAUNCH();
+  if (parts > 1) {
+    mla_reduce_kernel<<<dim3(T, H), 128, 0, stream>>>(ws_o, ws_ml, H, parts, (bf16*)out, out_stride_t);
+    OME_CHECK_LAUNCH();
+  }
+  return 0;
+}

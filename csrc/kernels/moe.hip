@@ -20,15 +20,23 @@
 // ------------------------------------------------------------------------------------------
 // routing
 // ------------------------------------------------------------------------------------------
+// group_mode: 0 = plain top-k; 1 = DeepSeek-V2 "group_limited_greedy" (group score = max);
+// 2 = DeepSeek-V3 "noaux_tc" (group score = sum of the group's top-2 biased scores).  Experts are
+// chosen on score + bias (``e_score_correction_bias``) restricted to the best ``topk_group``
+// groups (other experts score 0, as in the HF reference); weights are the unbiased scores.
 template <typename T>
 __global__ __launch_bounds__(256) void moe_route_kernel(const T* __restrict__ logits, int64_t stride, int n_tok,
                                                         int E, int k, int renorm, int scoring,
-                                                        float* __restrict__ topk_w, int* __restrict__ topk_ids) {
+                                                        const float* __restrict__ bias, int n_group, int topk_group,
+                                                        int group_mode, float* __restrict__ topk_w,
+                                                        int* __restrict__ topk_ids) {
+  __shared__ float s_key[4][512];
+  __shared__ int s_gsel[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = blockIdx.x * 4 + wave;
   if (t >= n_tok) return;
   constexpr int MAXV = 8;  // E <= 512
-  float v[MAXV];
+  float v[MAXV], key[MAXV];
   const T* row = logits + (int64_t)t * stride;
   float mx = OME_NEG_INF;
 #pragma unroll
@@ -54,54 +62,112 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const T* __restrict__ lo
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) v[i] *= inv;
   }
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int e = lane + 64 * i;
+    key[i] = e < E ? v[i] + (bias ? bias[e] : 0.f) : -3.f;
+  }
+  if (group_mode && n_group > 1) {
+    const int gs = E / n_group;
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i)
+      if (lane + 64 * i < E) s_key[wave][lane + 64 * i] = key[i];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    float gscore = OME_NEG_INF;
+    if (lane < n_group) {
+      float b1 = OME_NEG_INF, b2 = OME_NEG_INF;
+      for (int j = 0; j < gs; ++j) {
+        const float x = s_key[wave][lane * gs + j];
+        if (x > b1) {
+          b2 = b1;
+          b1 = x;
+        } else if (x > b2) {
+          b2 = x;
+        }
+      }
+      gscore = group_mode == 1 ? b1 : b1 + (gs > 1 ? b2 : 0.f);
+    }
+    int chosen = 0;  // bit set on the lanes whose group is selected
+    for (int j = 0; j < topk_group; ++j) {
+      float best = gscore;
+      int bi = lane < n_group ? lane : 1 << 30;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ob > best || (ob == best && oi < bi)) {
+          best = ob;
+          bi = oi;
+        }
+      }
+      if (lane == bi) {
+        chosen = 1;
+        gscore = OME_NEG_INF;
+      }
+    }
+    s_gsel[wave][lane] = chosen;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int i = 0; i < MAXV; ++i) {
+      const int e = lane + 64 * i;
+      if (e < E && !s_gsel[wave][e / gs]) key[i] = 0.f;
+    }
+  }
   float picked_sum = 0.f;
   for (int j = 0; j < k; ++j) {
-    // argmax over the wave (ties -> lowest expert id)
-    float best = -2.f;
+    // argmax over the wave on the selection key (ties -> lowest expert id)
+    float best = -4.f, bw = 0.f;
     int bi = 1 << 30;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i) {
       const int e = lane + 64 * i;
-      if (e < E && (v[i] > best || (v[i] == best && e < bi))) {
-        best = v[i];
+      if (e < E && (key[i] > best || (key[i] == best && e < bi))) {
+        best = key[i];
+        bw = v[i];
         bi = e;
       }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const float ob = __shfl_xor(best, o);
+      const float ow = __shfl_xor(bw, o);
       const int oi = __shfl_xor(bi, o);
       if (ob > best || (ob == best && oi < bi)) {
         best = ob;
+        bw = ow;
         bi = oi;
       }
     }
     if (lane == 0) {
-      topk_w[(int64_t)t * k + j] = best;
+      topk_w[(int64_t)t * k + j] = bw;
       topk_ids[(int64_t)t * k + j] = bi;
     }
-    picked_sum += best;
+    picked_sum += bw;
 #pragma unroll
     for (int i = 0; i < MAXV; ++i)  // remove the winner (static register indexing)
-      if (lane + 64 * i == bi) v[i] = -3.f;
+      if (lane + 64 * i == bi) key[i] = -5.f;
   }
   if (renorm && lane == 0) {
-    const float inv = 1.f / picked_sum;
+    const float inv = 1.f / (picked_sum + 1e-20f);
     for (int j = 0; j < k; ++j) topk_w[(int64_t)t * k + j] *= inv;
   }
 }
 
 OME_API int ome_moe_route(const void* logits, int is_bf16, int64_t stride, int n_tok, int E, int k, int renorm,
-                          int scoring, float* topk_w, int* topk_ids, hipStream_t stream) {
+                          int scoring, const float* bias, int n_group, int topk_group, int group_mode,
+                          float* topk_w, int* topk_ids, hipStream_t stream) {
   if (n_tok <= 0) return 0;
   if (E > 512 || k > E || k <= 0) return -2;
+  if (group_mode && n_group > 1 && (E % n_group || n_group > 64 || topk_group > n_group)) return -2;
   const int g = (n_tok + 3) / 4;
   if (is_bf16)
-    moe_route_kernel<bf16><<<g, 256, 0, stream>>>((const bf16*)logits, stride, n_tok, E, k, renorm, scoring, topk_w,
-                                                  topk_ids);
+    moe_route_kernel<bf16><<<g, 256, 0, stream>>>((const bf16*)logits, stride, n_tok, E, k, renorm, scoring, bias,
+                                                  n_group, topk_group, group_mode, topk_w, topk_ids);
   else
-    moe_route_kernel<float><<<g, 256, 0, stream>>>((const float*)logits, stride, n_tok, E, k, renorm, scoring,
-                                                   topk_w, topk_ids);
+    moe_route_kernel<float><<<g, 256, 0, stream>>>((const float*)logits, stride, n_tok, E, k, renorm, scoring, bias,
+                                                   n_group, topk_group, group_mode, topk_w, topk_ids);
   OME_CHECK_LAUNCH();
   return 0;
 }

@@ -23,6 +23,10 @@ MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM",
 
 
 def model_class(cfg: ModelConfig):
+    if cfg.is_mla:
+        from ome_amd.models.deepseek import DeepseekForCausalLM
+
+        return DeepseekForCausalLM
     if cfg.is_moe:
         from ome_amd.models.moe import MoEForCausalLM
 

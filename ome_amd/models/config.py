@@ -187,6 +187,41 @@ PRESETS: dict[str, dict] = {
                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                      intermediate_size=512, moe_intermediate_size=128, num_experts=8, num_experts_per_tok=2,
                      vocab_size=1024, rms_norm_eps=1e-6, rope_theta=10000.0, max_position_embeddings=2048),
+    "deepseek-v3": dict(architectures=["DeepseekV3ForCausalLM"], model_type="deepseek_v3", hidden_size=7168,
+                        num_hidden_layers=61, num_attention_heads=128, num_key_value_heads=128,
+                        intermediate_size=18432, moe_intermediate_size=2048, n_routed_experts=256,
+                        n_shared_experts=1, num_experts_per_tok=8, first_k_dense_replace=3, moe_layer_freq=1,
+                        n_group=8, topk_group=4, topk_method="noaux_tc", scoring_func="sigmoid", norm_topk_prob=True,
+                        routed_scaling_factor=2.5, kv_lora_rank=512, q_lora_rank=1536, qk_nope_head_dim=128,
+                        qk_rope_head_dim=64, v_head_dim=128, vocab_size=129280, rms_norm_eps=1e-6, rope_theta=10000.0,
+                        max_position_embeddings=163840,
+                        rope_scaling={"type": "yarn", "factor": 40, "original_max_position_embeddings": 4096,
+                                      "beta_fast": 32, "beta_slow": 1, "mscale": 1.0, "mscale_all_dim": 1.0}),
+    "deepseek-v2-lite": dict(architectures=["DeepseekV2ForCausalLM"], model_type="deepseek_v2", hidden_size=2048,
+                             num_hidden_layers=27, num_attention_heads=16, num_key_value_heads=16,
+                             intermediate_size=10944, moe_intermediate_size=1408, n_routed_experts=64,
+                             n_shared_experts=2, num_experts_per_tok=6, first_k_dense_replace=1, n_group=1,
+                             topk_group=1, topk_method="greedy", scoring_func="softmax", norm_topk_prob=False,
+                             routed_scaling_factor=1.0, kv_lora_rank=512, q_lora_rank=None, qk_nope_head_dim=128,
+                             qk_rope_head_dim=64, v_head_dim=128, vocab_size=102400, rms_norm_eps=1e-6,
+                             rope_theta=10000.0, max_position_embeddings=163840),
+    "tiny-deepseek": dict(architectures=["DeepseekV3ForCausalLM"], model_type="deepseek_v3", hidden_size=256,
+                          num_hidden_layers=3, num_attention_heads=16, num_key_value_heads=16, intermediate_size=512,
+                          moe_intermediate_size=64, n_routed_experts=16, n_shared_experts=1, num_experts_per_tok=4,
+                          first_k_dense_replace=1, n_group=4, topk_group=2, topk_method="noaux_tc",
+                          scoring_func="sigmoid", norm_topk_prob=True, routed_scaling_factor=2.5, kv_lora_rank=512,
+                          q_lora_rank=128, qk_nope_head_dim=32, qk_rope_head_dim=64, v_head_dim=32, vocab_size=1024,
+                          rms_norm_eps=1e-6, rope_theta=10000.0, max_position_embeddings=2048,
+                          rope_scaling={"type": "yarn", "factor": 4, "original_max_position_embeddings": 512,
+                                        "beta_fast": 32, "beta_slow": 1, "mscale": 1.0, "mscale_all_dim": 1.0}),
+    "tiny-deepseek-v2": dict(architectures=["DeepseekV2ForCausalLM"], model_type="deepseek_v2", hidden_size=256,
+                             num_hidden_layers=2, num_attention_heads=16, num_key_value_heads=16,
+                             intermediate_size=512, moe_intermediate_size=64, n_routed_experts=16, n_shared_experts=2,
+                             num_experts_per_tok=4, first_k_dense_replace=1, n_group=4, topk_group=2,
+                             topk_method="group_limited_greedy", scoring_func="softmax", norm_topk_prob=False,
+                             routed_scaling_factor=16.0, kv_lora_rank=512, q_lora_rank=None, qk_nope_head_dim=32,
+                             qk_rope_head_dim=64, v_head_dim=32, vocab_size=1024, rms_norm_eps=1e-6,
+                             rope_theta=10000.0, max_position_embeddings=2048),
 }
 
 

@@ -163,10 +163,12 @@ def fp8_linear(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int =
 
 
 def moe_route(logits: torch.Tensor, k: int, renorm: bool = True, scoring: str = "softmax",
-              out_w: torch.Tensor | None = None, out_ids: torch.Tensor | None = None):
-    """Router: logits [T, E] -> (weights f32 [T, k], expert ids int32 [T, k])."""
+              out_w: torch.Tensor | None = None, out_ids: torch.Tensor | None = None, bias: torch.Tensor | None = None,
+              n_group: int = 1, topk_group: int = 1, group_mode: int = 0):
+    """Router: logits [T, E] -> (weights f32 [T, k], expert ids int32 [T, k]).  ``group_mode`` 1/2 =
+    DeepSeek-V2 group_limited_greedy / DeepSeek-V3 noaux_tc (with ``bias``)."""
     if not _gpu(logits):
-        w, ids = ref.moe_route(logits, k, renorm, scoring)
+        w, ids = ref.moe_route(logits, k, renorm, scoring, bias, n_group, topk_group, group_mode)
         if out_w is not None:
             out_w.copy_(w)
             out_ids.copy_(ids)
@@ -175,8 +177,11 @@ def moe_route(logits: torch.Tensor, k: int, renorm: bool = True, scoring: str = 
     T, E = logits.shape
     out_w = torch.empty(T, k, dtype=torch.float32, device=logits.device) if out_w is None else out_w
     out_ids = torch.empty(T, k, dtype=torch.int32, device=logits.device) if out_ids is None else out_ids
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous()
     call("ome_moe_route", logits.data_ptr(), int(logits.dtype == torch.bfloat16), logits.stride(0), T, E, k,
-         int(renorm), 0 if scoring == "softmax" else 1, out_w.data_ptr(), out_ids.data_ptr(), stream_ptr())
+         int(renorm), 0 if scoring == "softmax" else 1, ptr(bias), n_group, topk_group, group_mode,
+         out_w.data_ptr(), out_ids.data_ptr(), stream_ptr())
     return out_w, out_ids
 
 
@@ -241,6 +246,49 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeW
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(seq_lens).data_ptr(), out.data_ptr(),
          out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
          float(scale), int(window), _i32(order).data_ptr() if order is not None else None, stream_ptr())
+    return out
+
+
+class MLAWorkspace:
+    """Split-K partials for :func:`mla_attn`: partitions are only used while (tokens x head
+    groups) is below ~1024 workgroups, so the buffers are bounded by 1024*16 rows."""
+
+    TARGET_WGS = 1024
+    MAX_PARTS = 16
+
+    def __init__(self, device="cuda"):
+        rows = self.TARGET_WGS * 16
+        self.ws_o = torch.empty(rows * 512, dtype=torch.float32, device=device)
+        self.ws_ml = torch.empty(rows * 2, dtype=torch.float32, device=device)
+
+    @classmethod
+    def parts(cls, T: int, H: int) -> int:
+        wgs = T * (H // 16)
+        return 1 if wgs >= cls.TARGET_WGS else max(1, min(cls.MAX_PARTS, cls.TARGET_WGS // max(wgs, 1)))
+
+
+def mla_attn(q, cache, block_tables, tok_row, kv_lens, scale: float, ws: MLAWorkspace | None = None,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    """Absorbed multi-head latent attention (DeepSeek MLA) over the paged latent cache:
+    q [T, H, 576] (latent-projected nope part | roped pe part), cache [pages, 16, 576]
+    -> out [T, H, 512].  Token t sees keys [0, kv_lens[t]) of block-table row tok_row[t]."""
+    if not _gpu(q):
+        r = ref.mla_attn(q, cache, block_tables, tok_row, kv_lens, scale)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    T, H, DK = q.shape
+    assert DK == 576 and H % 16 == 0 and q.stride(2) == 1 and q.stride(1) == DK and cache.shape[-1] == 576
+    if out is None:
+        out = torch.empty(T, H, 512, dtype=q.dtype, device=q.device)
+    parts = MLAWorkspace.parts(T, H)
+    if parts > 1 and ws is None:
+        ws = MLAWorkspace(q.device)
+    call("ome_mla_attn", q.data_ptr(), q.stride(0), cache.data_ptr(), _i32(block_tables).data_ptr(),
+         block_tables.stride(0), _i32(tok_row).data_ptr(), _i32(kv_lens).data_ptr(), T, H, float(scale), parts,
+         out.data_ptr(), out.stride(0), ws.ws_o.data_ptr() if parts > 1 else None,
+         ws.ws_ml.data_ptr() if parts > 1 else None, stream_ptr())
     return out
 
 

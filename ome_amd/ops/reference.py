@@ -194,12 +194,24 @@ def pool(hidden, cu_lens, mode: int = 0, normalize: bool = True) -> torch.Tensor
 
 
 # ------------------------------------------------------------------ MoE
-def moe_route(logits, k: int, renorm: bool, scoring: str = "softmax"):
+def moe_route(logits, k: int, renorm: bool, scoring: str = "softmax", bias=None, n_group: int = 1,
+              topk_group: int = 1, group_mode: int = 0):
+    """HF semantics (Mixtral/Qwen softmax top-k; DeepSeek-V2 group_limited_greedy = mode 1,
+    DeepSeek-V3 noaux_tc = mode 2 with e_score_correction_bias)."""
     lf = logits.float()
     p = torch.softmax(lf, -1) if scoring == "softmax" else torch.sigmoid(lf)
-    w, ids = torch.topk(p, k, dim=-1)  # ties: torch.topk order is implementation-defined
+    key = p + bias.float() if bias is not None else p.clone()
+    if group_mode and n_group > 1:
+        T, E = key.shape
+        grp = key.view(T, n_group, E // n_group)
+        gs = grp.max(-1).values if group_mode == 1 else grp.topk(min(2, E // n_group), -1).values.sum(-1)
+        gidx = gs.topk(topk_group, -1).indices
+        gmask = torch.zeros_like(gs, dtype=torch.bool).scatter_(1, gidx, True)
+        key = key.masked_fill(~gmask.repeat_interleave(E // n_group, 1), 0.0)
+    _, ids = torch.topk(key, k, dim=-1)  # ties: torch.topk order is implementation-defined
+    w = p.gather(1, ids)
     if renorm:
-        w = w / w.sum(-1, keepdim=True)
+        w = w / (w.sum(-1, keepdim=True) + 1e-20)
     return w.float(), ids.to(torch.int32)
 
 
@@ -278,3 +290,19 @@ def fp8_gemm(qa, sa, qw, sw, block: int, bias=None, out_dtype=torch.bfloat16):
     if bias is not None:
         out = out + bias.float()
     return out.to(out_dtype)
+
+
+def mla_attn(q, cache, block_tables, tok_row, kv_lens, scale):
+    """Absorbed MLA: q [T, H, 576], cache [pages, 16, 576] -> out [T, H, 512] (values = the first
+    512 latent dims)."""
+    T, H, DK = q.shape
+    P = cache.shape[-2]
+    out = torch.empty(T, H, 512, dtype=q.dtype, device=q.device)
+    flat = cache.reshape(-1, P, DK)
+    for t in range(T):
+        L = int(kv_lens[t])
+        pages = block_tables[int(tok_row[t])][: -(-L // P)].long()
+        kv = flat[pages].reshape(-1, DK)[:L].float()
+        s = (q[t].float() @ kv.t()) * scale
+        out[t] = (torch.softmax(s, -1) @ kv[:, :512]).to(q.dtype)
+    return out

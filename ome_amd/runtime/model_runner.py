@@ -105,7 +105,8 @@ class ModelRunner:
         self.load_time = time.perf_counter() - t0
         # ---- KV cache sizing (reference: --mem-frac 0.9, llama-3-8b-instruct-rt.yaml:59-60) ----
         tp = self.model.tp
-        page_bytes = PagedKVCache.bytes_per_page(cfg.num_layers, tp.hkv, cfg.head_dim, page_size, dtype)
+        kv_heads, k_dim, v_dim = getattr(self.model, "kv_layout", (tp.hkv, cfg.head_dim, cfg.head_dim))
+        page_bytes = PagedKVCache.bytes_per_page(cfg.num_layers, kv_heads, k_dim, page_size, dtype, v_dim)
         if self.is_cuda:
             free, total = torch.cuda.mem_get_info(self.device)
             used_by_others = total - free
@@ -118,7 +119,7 @@ class ModelRunner:
         if max_total_tokens:
             want = min(want, -(-max_total_tokens // page_size) + 2)
         num_pages = max(min(num_pages, want), max_pages_per_seq + 2)
-        self.kv = PagedKVCache(cfg.num_layers, num_pages, tp.hkv, cfg.head_dim, page_size, dtype, self.device)
+        self.kv = PagedKVCache(cfg.num_layers, num_pages, kv_heads, k_dim, page_size, dtype, self.device, v_dim)
         self.pages = PagePool(num_pages)
         self.slots = ReqSlotPool(max_running + 1, max_pages_per_seq, self.device)
         log.info("KV cache: %d pages x %d tokens (%.1f GiB), weights %.1f GiB", num_pages, page_size,
@@ -148,8 +149,10 @@ class ModelRunner:
             self.capture_graphs()
 
     # ------------------------------------------------------------------ helpers
-    def decode_ws(self, bs: int) -> ops.DecodeWorkspace:
+    def decode_ws(self, bs: int) -> ops.DecodeWorkspace | None:
         """Split-K partitioning chosen so a decode launch has >= ~1024 active workgroups."""
+        if getattr(self.model, "kv_layout", None) is not None:
+            return None  # MLA models carry their own workspace
         ws = self._ws_cache.get(bs)
         if ws is None:
             hkv = self.model.tp.hkv
@@ -425,8 +428,7 @@ class ModelRunner:
         ws = None
         if nd:
             bucket = next((b for b in self.buckets if b >= nd), None)
-            ws = self.decode_ws(bucket) if bucket is not None else ops.DecodeWorkspace(
-                nd, self.model.tp.hq, self.cfg.head_dim, self.max_context + self.P, 512, self.device)
+            ws = self.decode_ws(bucket if bucket is not None else nd)
         if S and nd:
             meta = AttnMeta("mixed", t_pos, t_slots, self.slots.table.index_select(0, t_req), seq_lens=t_dlen,
                             cu_q=t_cu, kv_lens=t_kv, items=t_items, decode_ws=ws, order=t_dord,
