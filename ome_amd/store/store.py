@@ -90,7 +90,17 @@ def parse_selector(sel: str | dict | None) -> list[tuple[str, str, list[str]]]:
         for e in sel.get("matchExpressions", []) or []:
             out.append((e["key"], e["operator"], [str(x) for x in e.get("values", []) or []]))
         return out
-    for part in [p.strip() for p in sel.split(",") if p.strip()]:
+    parts, depth, cur = [], 0, ""
+    for ch in sel:  # split on commas outside "(...)" value lists
+        depth += ch == "("
+        depth -= ch == ")"
+        if ch == "," and depth == 0:
+            parts.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    parts.append(cur)
+    for part in [p.strip() for p in parts if p.strip()]:
         if "!=" in part:
             k, v = part.split("!=", 1)
             out.append((k.strip(), "!=", [v.strip()]))

@@ -11,8 +11,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _setup(lens, pages_per_row=80, num_pages=700, seed=0):
+def _setup(lens, seed=0):
     g = torch.Generator().manual_seed(seed)
+    pages_per_row = -(-max(lens) // 16) + 1
+    num_pages = len(lens) * pages_per_row + 1
     cache = (torch.randn(num_pages, 16, 576, generator=g) * 0.5).to(torch.bfloat16)
     rows = len(lens)
     perm = torch.randperm(num_pages - 1, generator=g)[: rows * pages_per_row] + 1
