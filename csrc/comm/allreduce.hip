@@ -1,0 +1,262 @@
+// Custom tensor-parallel all-reduce over xGMI peer mappings.
+//
+// An 8x MI355X node is a full mesh: every GPU has a direct xGMI link to every other one, so a
+// small all-reduce is fastest as ONE kernel in which each GPU reads all peers' inputs directly
+// (no ring, no RCCL proxy), and a large one as reduce-scatter + all-gather over the same
+// mappings, which moves (N-1)/N of the bytes per link instead of the ring's 2(N-1)/N hops.
+//
+// Memory per rank (shared with the peers through hipIpc handles):
+//   signal  (hipDeviceMallocUncached): start/end flags [kMaxBlocks][kMaxRanks] + per-block epoch
+//           counters — uncached so spinning never reads a stale line;
+//   data    (coarse-grained): the rank's staged input (one-shot) or reduced chunk (two-shot).
+// Synchronisation is per workgroup: block b of every rank bumps its epoch (kept in device memory,
+// so captured HIP graphs replay correctly), stores it into flag[b][rank] of every peer with a
+// system-scope release, and waits (system-scope acquire, bounded spin) until all peers' flags
+// reached the epoch.  A bounded spin that expires records an error word instead of hanging the
+// GPU.  Accumulation is in fp32.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#define OME_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kMaxBlocks = 128;
+constexpr int kThreads = 512;
+constexpr uint64_t kSpinLimit = 1ull << 26;
+
+struct Signal {
+  uint32_t start[kMaxBlocks][kMaxRanks];
+  uint32_t end[kMaxBlocks][kMaxRanks];
+  uint32_t epoch[kMaxBlocks];
+  uint32_t error;
+};
+
+struct Peers {
+  Signal* sig[kMaxRanks];
+  char* data[kMaxRanks];
+};
+
+typedef __bf16 bf16;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void st_release(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ uint32_t ld_acquire(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// all ranks' block b meet here; `which` 0 = start flags, 1 = end flags
+__device__ __forceinline__ void block_barrier(const Peers& P, int rank, int world, uint32_t epoch, int which) {
+  __syncthreads();
+  if (threadIdx.x < world) {
+    __threadfence_system();
+    Signal* peer = P.sig[threadIdx.x];
+    st_release(which ? &peer->end[blockIdx.x][rank] : &peer->start[blockIdx.x][rank], epoch);
+    Signal* self = P.sig[rank];
+    uint32_t* f = which ? &self->end[blockIdx.x][threadIdx.x] : &self->start[blockIdx.x][threadIdx.x];
+    uint64_t spins = 0;
+    while (ld_acquire(f) < epoch) {
+      if (++spins > kSpinLimit) {
+        atomicOr(&self->error, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // make the peers' released data visible to plain loads
+}
+
+__device__ __forceinline__ void add8(float* acc, u32x4 v) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t w = v[i];
+    acc[2 * i] += __uint_as_float(w << 16);
+    acc[2 * i + 1] += __uint_as_float(w & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ u32x4 pack8(const float* a) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const bf16 lo = (bf16)a[2 * i], hi = (bf16)a[2 * i + 1];
+    r[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+  }
+  return r;
+}
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void ar_one_shot(Peers P, int rank, int64_t n_vec, u32x4* __restrict__ out) {
+  __shared__ uint32_t s_epoch;
+  Signal* self = P.sig[rank];
+  if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  block_barrier(P, rank, W, epoch, 0);
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n_vec; i += (int64_t)gridDim.x * kThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    u32x4 v[W];
+#pragma unroll
+    for (int r = 0; r < W; ++r) v[r] = reinterpret_cast<const u32x4*>(P.data[(rank + r) % W])[i];
+#pragma unroll
+    for (int r = 0; r < W; ++r) add8(acc, v[r]);
+    out[i] = pack8(acc);
+  }
+  block_barrier(P, rank, W, epoch, 1);  // nobody may restage its buffer while a peer still reads it
+  if (threadIdx.x == 0) self->epoch[blockIdx.x] = epoch;
+}
+
+// reduce-scatter into the own buffer's chunk, then all-gather the peers' reduced chunks
+template <int W>
+__global__ __launch_bounds__(kThreads) void ar_two_shot(Peers P, int rank, int64_t n_vec, u32x4* __restrict__ out) {
+  __shared__ uint32_t s_epoch;
+  Signal* self = P.sig[rank];
+  if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  const int64_t chunk = (n_vec + W - 1) / W;
+  block_barrier(P, rank, W, epoch, 0);
+  const int64_t c0 = rank * chunk, c1 = c0 + chunk < n_vec ? c0 + chunk : n_vec;
+  u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]);
+  for (int64_t i = c0 + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < c1; i += (int64_t)gridDim.x * kThreads) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    u32x4 v[W];
+#pragma unroll
+    for (int r = 0; r < W; ++r) v[r] = reinterpret_cast<const u32x4*>(P.data[(rank + r) % W])[i];
+#pragma unroll
+    for (int r = 0; r < W; ++r) add8(acc, v[r]);
+    const u32x4 s = pack8(acc);
+    out[i] = s;
+    mine[n_vec + i] = s;  // peers gather it from the second half of our buffer
+  }
+  block_barrier(P, rank, W, epoch, 1);
+  for (int r = 1; r < W; ++r) {
+    const int src = (rank + r) % W;
+    const int64_t s0 = src * chunk, s1 = s0 + chunk < n_vec ? s0 + chunk : n_vec;
+    const u32x4* theirs = reinterpret_cast<const u32x4*>(P.data[src]) + n_vec;
+    for (int64_t i = s0 + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < s1; i += (int64_t)gridDim.x * kThreads)
+      out[i] = theirs[i];
+  }
+  // no closing meeting is needed: a peer can only restage (first half) after its own kernel
+  // ended, i.e. after the barrier above that every reader of its input passed, and it writes its
+  // next reduced chunk (second half) only after the next call's start barrier, which this
+  // block reaches after it finished gathering.
+  if (threadIdx.x == 0) self->epoch[blockIdx.x] = epoch;
+}
+
+struct Ctx {
+  int rank, world;
+  size_t data_bytes;
+  Signal* sig;
+  char* data;
+  Peers peers;
+  bool opened[kMaxRanks];
+};
+
+}  // namespace
+
+// allocate this rank's signal + data buffers; returns the two IPC handles (64 bytes each)
+OME_API int ome_comm_create(int rank, int world, size_t data_bytes, void** ctx_out, void* sig_handle,
+                            void* data_handle) {
+  if (world < 2 || world > kMaxRanks || rank < 0 || rank >= world) return -2;
+  Ctx* c = new Ctx();
+  memset(c, 0, sizeof(Ctx));
+  c->rank = rank;
+  c->world = world;
+  c->data_bytes = data_bytes;
+  hipError_t e = hipExtMallocWithFlags((void**)&c->sig, sizeof(Signal), hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(c->sig, 0, sizeof(Signal));
+  if (e != hipSuccess) return (int)e;
+  e = hipMalloc((void**)&c->data, 2 * data_bytes);  // input half + reduced-chunk half (two-shot)
+  if (e != hipSuccess) return (int)e;
+  e = hipIpcGetMemHandle((hipIpcMemHandle_t*)sig_handle, c->sig);
+  if (e != hipSuccess) return (int)e;
+  e = hipIpcGetMemHandle((hipIpcMemHandle_t*)data_handle, c->data);
+  if (e != hipSuccess) return (int)e;
+  c->peers.sig[rank] = c->sig;
+  c->peers.data[rank] = c->data;
+  *ctx_out = c;
+  return 0;
+}
+
+OME_API int ome_comm_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// map every peer's buffers (handles: world x handle_size bytes each, own entries ignored)
+OME_API int ome_comm_open(void* ctx, const void* sig_handles, const void* data_handles) {
+  Ctx* c = (Ctx*)ctx;
+  const size_t hs = sizeof(hipIpcMemHandle_t);
+  for (int r = 0; r < c->world; ++r) {
+    if (r == c->rank) continue;
+    hipIpcMemHandle_t hsig, hdat;
+    memcpy(&hsig, (const char*)sig_handles + r * hs, hs);
+    memcpy(&hdat, (const char*)data_handles + r * hs, hs);
+    void* p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, hsig, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return (int)e;
+    c->peers.sig[r] = (Signal*)p;
+    e = hipIpcOpenMemHandle(&p, hdat, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) return (int)e;
+    c->peers.data[r] = (char*)p;
+    c->opened[r] = true;
+  }
+  return 0;
+}
+
+// in-place-safe bf16 sum: out = sum over ranks of `in` (n elements, n % 8 == 0)
+OME_API int ome_comm_all_reduce(void* ctx, const void* in, void* out, int64_t n, int two_shot, int blocks,
+                                hipStream_t stream) {
+  Ctx* c = (Ctx*)ctx;
+  if (n % 8) return -2;
+  const size_t bytes = (size_t)n * 2;
+  if (bytes > c->data_bytes) return -3;
+  if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
+  hipError_t e = hipMemcpyAsync(c->data, in, bytes, hipMemcpyDeviceToDevice, stream);
+  if (e != hipSuccess) return (int)e;
+  const int64_t n_vec = n / 8;
+  dim3 grid(blocks), block(kThreads);
+#define OME_AR_CASE(W)                                                                               \
+  case W:                                                                                            \
+    if (two_shot)                                                                                    \
+      ar_two_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, (u32x4*)out);             \
+    else                                                                                             \
+      ar_one_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, (u32x4*)out);             \
+    break;
+  switch (c->world) {
+    OME_AR_CASE(2)
+    OME_AR_CASE(4)
+    OME_AR_CASE(8)
+    default:
+      return -2;
+  }
+#undef OME_AR_CASE
+  e = hipGetLastError();
+  return (int)e;
+}
+
+OME_API int ome_comm_error(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  uint32_t err = 0;
+  if (hipMemcpy(&err, &c->sig->error, sizeof(err), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (int)err;
+}
+
+OME_API void ome_comm_destroy(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c) return;
+  for (int r = 0; r < c->world; ++r) {
+    if (c->opened[r]) {
+      (void)hipIpcCloseMemHandle(c->peers.sig[r]);
+      (void)hipIpcCloseMemHandle(c->peers.data[r]);
+    }
+  }
+  (void)hipFree(c->sig);
+  (void)hipFree(c->data);
+  delete c;
+}

@@ -45,6 +45,14 @@ _SIGNATURES = {
         "ome_fp8_gemm": [vp, i64, vp, vp, vp, i32, i32, i32, i32, vp, i64, vp, vp],
         "ome_sample": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, u64, vp, vp, vp],
     },
+    "ome_comm": {
+        "ome_comm_create": [i32, i32, C.c_size_t, C.POINTER(vp), vp, vp],
+        "ome_comm_handle_size": [],
+        "ome_comm_open": [vp, vp, vp],
+        "ome_comm_all_reduce": [vp, vp, vp, i64, i32, i32, vp],
+        "ome_comm_error": [vp],
+        "ome_comm_destroy": [vp],
+    },
 }
 
 
