@@ -76,17 +76,24 @@ def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_in
                 torch.cuda.set_device(lr)
                 kw["device_id"] = torch.device("cuda", lr)
             dist.init_process_group(backend=backend, init_method=init_method, rank=rk, world_size=world, **kw)
+        tp_cpu = None
         for p in range(pp_size):
             ranks = list(range(p * tp_size, (p + 1) * tp_size))
             g = dist.new_group(ranks) if tp_size > 1 else None
+            gc = dist.new_group(ranks, backend="gloo") if tp_size > 1 else None
             if p == st.pp_rank:
-                st.tp_group = g
+                st.tp_group, tp_cpu = g, gc
         for t in range(tp_size):
             ranks = [p * tp_size + t for p in range(pp_size)]
             g = dist.new_group(ranks) if pp_size > 1 else None
             if t == st.tp_rank:
                 st.pp_group = g
         st.ep_group = st.tp_group
+        single_node = int(os.environ.get("LOCAL_WORLD_SIZE", world)) >= world
+        if backend == "nccl" and tp_size in (2, 4, 8) and single_node and os.environ.get("OME_CUSTOM_AR", "1") != "0":
+            from ome_amd.parallel.comm import TPCommunicator
+
+            st.comm = TPCommunicator(st.tp_group, cpu_group=tp_cpu)
     _STATE = st
     return st
 
