@@ -53,16 +53,19 @@ class PagedKVCache:
     """
 
     def __init__(self, num_layers: int, num_pages: int, num_kv_heads: int, head_dim: int, page_size: int = 16,
-                 dtype=torch.bfloat16, device="cuda", v_dim: int | None = None):
+                 dtype=torch.bfloat16, device="cuda", v_dim: int | None = None, layers: list[int] | None = None):
         """``v_dim`` = 0: key-only cache (MLA keeps one latent row per token, the values are a
-        slice of it); ``None``: same width as the keys."""
+        slice of it); ``None``: same width as the keys.  ``layers``: the global layer ids held
+        here (a pipeline stage's slice); other entries of ``k`` / ``v`` are None."""
         self.num_layers, self.num_pages, self.page_size = num_layers, num_pages, page_size
         self.num_kv_heads, self.head_dim, self.dtype = num_kv_heads, head_dim, dtype
         self.v_dim = head_dim if v_dim is None else v_dim
+        self.local_layers = list(range(num_layers)) if layers is None else list(layers)
+        own = set(self.local_layers)
         self.k = [torch.zeros(num_pages, num_kv_heads, page_size, head_dim, dtype=dtype, device=device)
-                  for _ in range(num_layers)]
+                  if i in own else None for i in range(num_layers)]
         self.v = [torch.zeros(num_pages, num_kv_heads, self.v_dim, page_size, dtype=dtype, device=device)
-                  for _ in range(num_layers)]
+                  if i in own else None for i in range(num_layers)]
 
     @staticmethod
     def bytes_per_page(num_layers: int, num_kv_heads: int, head_dim: int, page_size: int, dtype=torch.bfloat16,

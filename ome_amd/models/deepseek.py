@@ -78,7 +78,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
             self.routed_scale = 1.0  # V2 applies the factor only to unnormalised weights
         L = cfg.num_layers
         step = max(1, cfg.moe_layer_freq)
-        self.moe_layers = {i for i in range(L) if cfg.num_experts and i >= cfg.first_k_dense_replace and
+        self.moe_layers = {i for i in self.layers if cfg.num_experts and i >= cfg.first_k_dense_replace and
                            i % step == 0}
         self.w_qa: list = [None] * L      # [q_lora + 576, H] fused q_a / kv_a (or [576, H] if no q_lora)
         self.qa_ln: list = [None] * L
@@ -191,7 +191,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 self.lm_head = put(self._vocab_shard(w))
                 continue
             p = n.split(".")
-            if p[0] != "layers" or int(p[1]) >= cfg.num_layers:
+            if p[0] != "layers" or int(p[1]) not in self._layer_set:
                 continue
             i, rest = int(p[1]), ".".join(p[2:])
             d = parts.setdefault(i, {})
@@ -340,18 +340,11 @@ class DeepseekForCausalLM(LlamaForCausalLM):
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: PagedKVCache,
                 input_embeds: torch.Tensor | None = None) -> torch.Tensor:
-        tp = self.tp
-        if input_embeds is None:
-            h = pstate.tp_all_reduce(ops.embedding(ids, self.embed, tp.vocab_start, tp.vocab_end))
-        else:
-            h = input_embeds
-        residual = h
-        x = ops.rmsnorm(h, self.ln1[0], self.eps)
+        x, residual = self._stage_input(ids, input_embeds)
         for i in self.layers:
             if i > 0:
                 ops.fused_add_rmsnorm(x, residual, self.ln1[i], self.eps)
             o = self.attention_block(i, x, meta, kv)
             ops.fused_add_rmsnorm(o, residual, self.ln2[i], self.eps)
             x = self.mlp(i, o)
-        ops.fused_add_rmsnorm(x, residual, self.norm, self.eps)
-        return x
+        return self._stage_output(x, residual)

@@ -62,7 +62,10 @@ class LlamaForCausalLM:
         self.window = cfg.sliding_window or -1
         self.act = 0 if cfg.hidden_act in ("silu", "swish") else 1
         L = cfg.num_layers
-        self.layers = list(range(L))
+        # pipeline parallelism: this stage owns a contiguous slice of the decoder layers; the
+        # per-layer lists stay indexed by the global layer id (other stages' entries are None)
+        self.layers = pstate.stage_layers(L, st.pp_size, st.pp_rank)
+        self._layer_set = set(self.layers)
         self.w_qkv: list[torch.Tensor] = [None] * L
         self.b_qkv: list[torch.Tensor | None] = [None] * L
         self.w_o: list[torch.Tensor] = [None] * L
@@ -166,7 +169,7 @@ class LlamaForCausalLM:
             if parts[0] != "layers":
                 continue
             i, rest = int(parts[1]), ".".join(parts[2:])
-            if i >= cfg.num_layers:
+            if i not in self._layer_set:
                 continue
             if rest in ("self_attn.q_proj.weight", "self_attn.q_proj.bias"):
                 qkv_parts.setdefault(i, {})["q" + rest[-1]] = rows(w, tp.rank * tp.hq * D, tp.hq * D)
@@ -249,13 +252,7 @@ class LlamaForCausalLM:
         """ids [T] int32 -> final normed hidden [T, H]."""
         cfg, tp, D = self.cfg, self.tp, self.D
         T = ids.shape[0]
-        if input_embeds is None:
-            h = ops.embedding(ids, self.embed, tp.vocab_start, tp.vocab_end)
-            h = pstate.tp_all_reduce(h)
-        else:
-            h = input_embeds
-        residual = h
-        x = ops.rmsnorm(h, self.ln1[0], self.eps)
+        x, residual = self._stage_input(ids, input_embeds)
         for i in self.layers:
             if i > 0:
                 ops.fused_add_rmsnorm(x, residual, self.ln1[i], self.eps)
@@ -268,6 +265,29 @@ class LlamaForCausalLM:
             o = pstate.tp_all_reduce(linear(attn.view(T, tp.hq * D), self.w_o[i]))
             ops.fused_add_rmsnorm(o, residual, self.ln2[i], self.eps)
             x = self.mlp(i, o)
+        return self._stage_output(x, residual)
+
+    def _stage_input(self, ids: torch.Tensor, input_embeds: torch.Tensor | None):
+        """(x, residual) entering this stage's first layer: embedding + first RMSNorm on the
+        first pipeline stage, received from the previous stage otherwise."""
+        st = pstate.get()
+        T, H = ids.shape[0], self.cfg.hidden_size
+        if st.pp_size > 1 and not st.is_first_pp:
+            x, residual = pstate.pp_recv(((T, H), self.dtype, ids.device), ((T, H), self.dtype, ids.device))
+            return x, residual
+        if input_embeds is None:
+            h = pstate.tp_all_reduce(ops.embedding(ids, self.embed, self.tp.vocab_start, self.tp.vocab_end))
+        else:
+            h = input_embeds
+        return ops.rmsnorm(h, self.ln1[0], self.eps), h
+
+    def _stage_output(self, x: torch.Tensor, residual: torch.Tensor) -> torch.Tensor | None:
+        """Last stage: final norm -> hidden states.  Earlier stages: ship (x, residual) on and
+        return None (the sampled tokens come back via :func:`pstate.pp_broadcast_from_last`)."""
+        st = pstate.get()
+        if st.pp_size > 1 and not st.is_last_pp:
+            pstate.pp_send(x, residual)
+            return None
         ops.fused_add_rmsnorm(x, residual, self.norm, self.eps)
         return x
 

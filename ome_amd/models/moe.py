@@ -38,8 +38,8 @@ class MoEForCausalLM(LlamaForCausalLM):
         self.w_sd: list[torch.Tensor | None] = [None] * L    # shared expert down
         self.w_sgate: list[torch.Tensor | None] = [None] * L  # shared expert sigmoid gate [1, H]
         step = max(1, cfg.moe_layer_freq)
-        self.moe_layers = {i for i in range(L) if i >= cfg.first_k_dense_replace and (i + 1) % step == 0} \
-            if step > 1 else {i for i in range(L) if i >= cfg.first_k_dense_replace}
+        self.moe_layers = {i for i in self.layers if i >= cfg.first_k_dense_replace and (i + 1) % step == 0} \
+            if step > 1 else {i for i in self.layers if i >= cfg.first_k_dense_replace}
 
     def init_random(self, seed: int = 0, std: float = 0.02) -> "MoEForCausalLM":
         super().init_random(seed, std)

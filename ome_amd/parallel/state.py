@@ -122,6 +122,43 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     return torch.cat(parts, dim=dim)
 
 
+def stage_layers(num_layers: int, pp_size: int, pp_rank: int) -> list[int]:
+    """Contiguous, balanced split of the decoder layers over pipeline stages."""
+    return list(range(pp_rank * num_layers // pp_size, (pp_rank + 1) * num_layers // pp_size))
+
+
+def _pp_peer(stage: int) -> int:
+    st = _STATE
+    return stage * st.tp_size + st.tp_rank
+
+
+def pp_send(*tensors: torch.Tensor) -> None:
+    """Activations to the next pipeline stage (same TP rank): RCCL p2p on GPU, gloo on CPU."""
+    st = _STATE
+    dst = _pp_peer(st.pp_rank + 1)
+    for t in tensors:
+        dist.send(t.contiguous(), dst=dst)
+
+
+def pp_recv(*like: tuple[tuple, torch.dtype, torch.device]) -> list[torch.Tensor]:
+    st = _STATE
+    src = _pp_peer(st.pp_rank - 1)
+    out = []
+    for shape, dtype, device in like:
+        t = torch.empty(shape, dtype=dtype, device=device)
+        dist.recv(t, src=src)
+        out.append(t)
+    return out
+
+
+def pp_broadcast_from_last(t: torch.Tensor) -> torch.Tensor:
+    """The last stage samples; every stage needs the tokens (identical scheduler state)."""
+    st = _STATE
+    if st.pp_size > 1:
+        dist.broadcast(t, src=_pp_peer(st.pp_size - 1), group=st.pp_group)
+    return t
+
+
 def destroy() -> None:
     global _STATE
     if dist.is_initialized():

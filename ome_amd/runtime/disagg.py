@@ -123,7 +123,8 @@ class KVTransfer:
         sch, runner = eng.scheduler, eng.runner
         kv, P = runner.kv, runner.P
         L = int(header["n_tokens"])
-        if list(header["shape_k"][1:]) != list(kv.k[0].shape[1:]) or int(header["layers"]) != kv.num_layers:
+        k0 = kv.k[kv.local_layers[0]]
+        if list(header["shape_k"][1:]) != list(k0.shape[1:]) or int(header["layers"]) != len(kv.local_layers):
             req.state, req.finish_reason = ReqState.FINISHED, "abort:kv_layout_mismatch"
             if req.on_token:
                 req.on_token(req, [], True)
@@ -144,10 +145,10 @@ class KVTransfer:
         if runner.is_cuda:
             src = src.pin_memory().to(runner.device, non_blocking=True)
         idx = torch.tensor(pages, dtype=torch.long, device=runner.device)
-        kbytes = int(np.prod(header["shape_k"])) * kv.k[0].element_size()
-        vbytes = int(np.prod(header["shape_v"])) * kv.v[0].element_size()
+        kbytes = int(np.prod(header["shape_k"])) * k0.element_size()
+        vbytes = int(np.prod(header["shape_v"])) * k0.element_size()
         o = 0
-        for i in range(kv.num_layers):
+        for i in kv.local_layers:
             kk = src[o:o + kbytes].view(kv.dtype).view(header["shape_k"])
             o += kbytes
             vv = src[o:o + vbytes].view(kv.dtype).view(header["shape_v"])
@@ -184,14 +185,14 @@ class KVTransfer:
         pages = req.pages[: -(-L // P)]
         idx = torch.tensor(pages, dtype=torch.long, device=runner.device)
         parts = []
-        for i in range(kv.num_layers):
+        for i in kv.local_layers:
             parts.append(kv.k[i].index_select(0, idx).reshape(-1).view(torch.uint8))
             parts.append(kv.v[i].index_select(0, idx).reshape(-1).view(torch.uint8))
         blob = torch.cat(parts).cpu().numpy().tobytes()
         header = {"room": int(b["bootstrap_room"]), "n_tokens": L, "first_token": int(req.output_ids[0]),
                   "first_logprob": float(req.output_logprobs[0]) if req.output_logprobs else 0.0,
-                  "layers": kv.num_layers, "shape_k": [len(pages), *kv.k[0].shape[1:]],
-                  "shape_v": [len(pages), *kv.v[0].shape[1:]], "dtype": str(kv.dtype), "nbytes": len(blob)}
+                  "layers": len(kv.local_layers), "shape_k": [len(pages), *kv.k[kv.local_layers[0]].shape[1:]],
+                  "shape_v": [len(pages), *kv.v[kv.local_layers[0]].shape[1:]], "dtype": str(kv.dtype), "nbytes": len(blob)}
         host, port = b.get("bootstrap_host") or "127.0.0.1", int(b["bootstrap_port"]) + self.rank
         threading.Thread(target=self._send, args=(host, port, header, blob), daemon=True).start()
 

@@ -121,7 +121,7 @@ class Engine:
         # overlapped scheduling: (batch, handle, launch time) of the step whose tokens are in flight
         self._inflight = None
         ov = self.runner.is_cuda if args.overlap_schedule is None else bool(args.overlap_schedule)
-        self.overlap = ov and not self.cfg.is_embedding
+        self.overlap = ov and not self.cfg.is_embedding and self.pstate.pp_size == 1
 
     # ------------------------------------------------------------------ API
     def make_request(self, prompt_ids: list[int], params: SamplingParams | None = None, **kw) -> Request:
@@ -149,7 +149,7 @@ class Engine:
         with self._lock:
             new, aborts = self._inbox, self._aborts
             self._inbox, self._aborts = [], []
-        if self.pstate.tp_size > 1:
+        if self.pstate.world_size > 1:
             new, aborts = self._broadcast_control(new, aborts)
         kt = self.kv_transfer
         for r in new:
@@ -188,7 +188,7 @@ class Engine:
 
     def stop_group(self) -> None:
         """Leader: tell every follower rank to exit its step loop (one final control broadcast)."""
-        if self.pstate.tp_size > 1 and self.pstate.rank == 0:
+        if self.pstate.world_size > 1 and self.pstate.rank == 0:
             self._broadcast_control([], [], stop=True)
         self._stop = True
 
@@ -279,7 +279,7 @@ class Engine:
             if not self.has_work():
                 self._wake.wait(timeout=0.05)
                 self._wake.clear()
-                if self.pstate.tp_size == 1:
+                if self.pstate.world_size == 1:
                     continue
             try:
                 self.step()
@@ -296,7 +296,7 @@ class Engine:
         return t
 
     def shutdown(self) -> None:
-        if self.pstate.tp_size > 1 and self.pstate.rank == 0:
+        if self.pstate.world_size > 1 and self.pstate.rank == 0:
             self._stop_pending = True  # the loop broadcasts it on its next step, then exits
         else:
             self._stop = True

@@ -22,6 +22,7 @@ from ome_amd import ops
 from ome_amd.models import build_model
 from ome_amd.models.common import AttnMeta, PagedKVCache
 from ome_amd.models.config import ModelConfig
+from ome_amd.parallel import state as pstate
 from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
 from ome_amd.runtime.request import PENDING
 from ome_amd.runtime.scheduler import StepBatch
@@ -106,7 +107,8 @@ class ModelRunner:
         # ---- KV cache sizing (reference: --mem-frac 0.9, llama-3-8b-instruct-rt.yaml:59-60) ----
         tp = self.model.tp
         kv_heads, k_dim, v_dim = getattr(self.model, "kv_layout", (tp.hkv, cfg.head_dim, cfg.head_dim))
-        page_bytes = PagedKVCache.bytes_per_page(cfg.num_layers, kv_heads, k_dim, page_size, dtype, v_dim)
+        n_local = len(self.model.layers)
+        page_bytes = PagedKVCache.bytes_per_page(n_local, kv_heads, k_dim, page_size, dtype, v_dim)
         if self.is_cuda:
             free, total = torch.cuda.mem_get_info(self.device)
             used_by_others = total - free
@@ -119,7 +121,9 @@ class ModelRunner:
         if max_total_tokens:
             want = min(want, -(-max_total_tokens // page_size) + 2)
         num_pages = max(min(num_pages, want), max_pages_per_seq + 2)
-        self.kv = PagedKVCache(cfg.num_layers, num_pages, kv_heads, k_dim, page_size, dtype, self.device, v_dim)
+        self.kv = PagedKVCache(cfg.num_layers, num_pages, kv_heads, k_dim, page_size, dtype, self.device, v_dim,
+                               layers=self.model.layers)
+        self.pp = pstate.get().pp_size > 1
         self.pages = PagePool(num_pages)
         self.slots = ReqSlotPool(max_running + 1, max_pages_per_seq, self.device)
         log.info("KV cache: %d pages x %d tokens (%.1f GiB), weights %.1f GiB", num_pages, page_size,
@@ -144,7 +148,8 @@ class ModelRunner:
         self.counts = torch.zeros(max_running + 1, cfg.vocab_size, dtype=torch.int32, device=self.device)
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
-        self.use_graph = cuda_graph and self.is_cuda
+        # pipeline stages run eagerly: the stage hand-off is a blocking p2p exchange
+        self.use_graph = cuda_graph and self.is_cuda and not self.pp
         if self.use_graph:
             self.capture_graphs()
 
@@ -261,7 +266,7 @@ class ModelRunner:
         """Enqueue one step.  Rows whose input token is PENDING (sampled by ``prev``, still in
         flight) get it on the device from ``prev``'s output — no host round trip."""
         self.slots.flush()
-        if batch.mode == "decode" and all(c.length == 1 for c in batch.chunks):
+        if batch.mode == "decode" and not self.pp and all(c.length == 1 for c in batch.chunks):
             bs = next((b for b in self.buckets if b >= len(batch.chunks)), None)
             if bs is not None:
                 return self._launch_decode(batch, bs, prev)
@@ -441,6 +446,12 @@ class ModelRunner:
                             decode_ws=ws, order=t_dord)
         self._init_penalty_rows(chunks)
         hidden = self.model.forward(t_ids, meta, self.kv)
+        if hidden is None:  # an earlier pipeline stage: tokens arrive from the last stage
+            out_ids = torch.empty(len(chunks), dtype=torch.int32, device=self.device)
+            out_lp = torch.empty(len(chunks), dtype=torch.float32, device=self.device)
+            pstate.pp_broadcast_from_last(out_ids)
+            pstate.pp_broadcast_from_last(out_lp)
+            return self._finish_launch(out_ids, out_lp, len(chunks))
         logits = self.model.compute_logits(hidden.index_select(0, t_rows))
         pen = None
         if any(c.req.params.has_penalties for c in chunks):
@@ -471,6 +482,9 @@ class ModelRunner:
         out_ids = out_ids.to(torch.int32)
         if pen is not None:
             ops.update_counts(self.counts, pslot, out_ids, *pen)
+        if self.pp:
+            pstate.pp_broadcast_from_last(out_ids)
+            pstate.pp_broadcast_from_last(out_lp.float().contiguous())
         return self._finish_launch(out_ids, out_lp, len(chunks))
 
     def embed(self, batch: StepBatch) -> list[list[float]]:
