@@ -65,8 +65,13 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         mp = max_positions or cfg.max_position_embeddings
         self.cos_sin = rope_cos_sin(rc, mp, device=self.device)
         self.interleaved_rope = bool((cfg.extra or {}).get("rope_interleave", True))
-        # MoE
+        # MoE (expert parallelism under DP attention: this rank owns experts [e0, e0 + E_local))
         self.E, self.k = cfg.num_experts, cfg.num_experts_per_tok
+        self.ep = st.ep_size
+        if self.E and self.E % self.ep:
+            raise ValueError(f"{self.E} experts do not split over ep={self.ep}")
+        self.E_local = self.E // self.ep if self.E else 0
+        self.e0 = st.ep_rank * self.E_local
         self.moe_inter = -(-cfg.moe_intermediate_size // st.tp_size) if cfg.num_experts else 0
         self.shared_inter = -(-(cfg.num_shared_experts * cfg.moe_intermediate_size) // st.tp_size) \
             if cfg.num_shared_experts else 0
@@ -100,7 +105,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
     def init_random(self, seed: int = 0, std: float = 0.02) -> "DeepseekForCausalLM":
         cfg = self.cfg
         gen = torch.Generator(device=self.device)
-        gen.manual_seed(seed + 7919 * pstate.get().rank)
+        gen.manual_seed(seed + 7919 * pstate.get().tp_rank)
         H, Hl = cfg.hidden_size, self.Hl
         out_std = std / math.sqrt(2 * cfg.num_layers)
         st = pstate.get()
@@ -121,8 +126,9 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 self.w_router[i] = self._alloc(self.E, H, std=std, gen=gen)
                 if self.group_mode == 2:
                     self.b_router[i] = torch.zeros(self.E, dtype=torch.float32, device=self.device)
-                self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen)
-                self.w2[i] = self._alloc(self.E, H, I, std=out_std, gen=gen)
+                sl = slice(self.e0, self.e0 + self.E_local)
+                self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen)[sl].contiguous()
+                self.w2[i] = self._alloc(self.E, H, I, std=out_std, gen=gen)[sl].contiguous()
                 if self.shared_inter:
                     self.w_sgu[i] = self._alloc(2 * self.shared_inter, H, std=std, gen=gen)
                     self.w_sd[i] = self._alloc(H, self.shared_inter, std=out_std, gen=gen)
@@ -236,7 +242,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 self.w_sd[i] = put(cols(d["mlp.shared_experts.down_proj.weight"], SI))
         for i, ex in experts.items():
             gs, ds = [], []
-            for e in range(self.E):
+            for e in range(self.e0, self.e0 + self.E_local):
                 de = ex[e]
                 gs.append(torch.cat([rows(de["gate_proj"], I), rows(de["up_proj"], I)], 0))
                 ds.append(cols(de["down_proj"], I))
@@ -333,7 +339,12 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         tw, tid = ops.moe_route(logits, self.k, cfg.norm_topk_prob and self.k > 1, cfg.scoring_func,
                                 bias=self.b_router[i], n_group=cfg.n_group, topk_group=cfg.topk_group,
                                 group_mode=self.group_mode)
-        out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale)
+        if self.ep > 1:
+            from ome_amd.parallel.ep import moe_ep_forward
+
+            out = moe_ep_forward(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale, self.E)
+        else:
+            out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale)
         if self.w_sgu[i] is not None:
             out = out + linear(ops.act_and_mul(linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
         return pstate.tp_all_reduce(out)

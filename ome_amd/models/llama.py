@@ -96,7 +96,7 @@ class LlamaForCausalLM:
         """Random-init weights of this architecture (BASELINE rule: synthetic weights)."""
         cfg, tp, D = self.cfg, self.tp, self.D
         gen = torch.Generator(device=self.device)
-        gen.manual_seed(seed + 7919 * pstate.get().rank)
+        gen.manual_seed(seed + 7919 * pstate.get().tp_rank)
         H = cfg.hidden_size
         qkv_rows = (tp.hq + 2 * tp.hkv) * D
         for i in self.layers:

@@ -25,7 +25,14 @@ class MoEForCausalLM(LlamaForCausalLM):
     def __init__(self, cfg, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
         super().__init__(cfg, device, dtype, max_positions)
         tp = self.tp
+        st = pstate.get()
         self.E = cfg.num_experts
+        # expert parallelism (DP attention): this rank owns experts [e0, e0 + E_local)
+        self.ep = st.ep_size
+        if self.E % self.ep:
+            raise ValueError(f"{self.E} experts do not split over ep={self.ep}")
+        self.E_local = self.E // self.ep
+        self.e0 = st.ep_rank * self.E_local
         self.k = cfg.num_experts_per_tok
         self.renorm = cfg.norm_topk_prob
         self.moe_inter = -(-cfg.moe_intermediate_size // tp.tp)
@@ -45,15 +52,16 @@ class MoEForCausalLM(LlamaForCausalLM):
         super().init_random(seed, std)
         cfg = self.cfg
         gen = torch.Generator(device=self.device)
-        gen.manual_seed(seed + 104729 + 7919 * pstate.get().rank)
+        gen.manual_seed(seed + 104729 + 7919 * pstate.get().tp_rank)
         H, I = cfg.hidden_size, self.moe_inter
         for i in self.layers:
             if i not in self.moe_layers:
                 continue
             self.w_gu[i] = self.w_d[i] = None  # dense MLP replaced by experts
             self.w_router[i] = self._alloc(self.E, H, std=std, gen=gen)
-            self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen)
-            self.w2[i] = self._alloc(self.E, H, I, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+            self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen)[self.e0:self.e0 + self.E_local].contiguous()
+            self.w2[i] = self._alloc(self.E, H, I, std=std / math.sqrt(2 * cfg.num_layers),
+                                     gen=gen)[self.e0:self.e0 + self.E_local].contiguous()
             if self.shared_inter:
                 self.w_sgu[i] = self._alloc(2 * self.shared_inter, H, std=std, gen=gen)
                 self.w_sd[i] = self._alloc(H, self.shared_inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
@@ -103,7 +111,7 @@ class MoEForCausalLM(LlamaForCausalLM):
         self._load_base(rest_iter)
         for i, ex in experts.items():
             gs, ds = [], []
-            for e in range(self.E):
+            for e in range(self.e0, self.e0 + self.E_local):
                 d = ex[e]
                 g = d.get("w1", d.get("gate_proj"))
                 u = d.get("w3", d.get("up_proj"))
@@ -142,7 +150,12 @@ class MoEForCausalLM(LlamaForCausalLM):
             return super().mlp(i, x)
         logits = F.linear(x, self.w_router[i])
         tw, tid = ops.moe_route(logits, self.k, self.renorm)
-        out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act)
+        if self.ep > 1:
+            from ome_amd.parallel.ep import moe_ep_forward
+
+            out = moe_ep_forward(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E)
+        else:
+            out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act)
         if self.w_sgu[i] is not None:
             sh = F.linear(ops.act_and_mul(F.linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
             if self.w_sgate[i] is not None:

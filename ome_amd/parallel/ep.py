@@ -1,0 +1,88 @@
+"""Expert-parallel MoE with all-to-all token dispatch / combine (SURVEY.md §2.9 K17, §2.8 C4;
+the reference's runtimes use DeepEP ``--moe-a2a-backend deepep`` for this).
+
+Under DP attention every rank holds different tokens and 1/EP of the experts.  Per MoE layer:
+
+  route locally -> sort the T*k (token, expert) assignments by owning rank ->
+  all-to-all-v #1: counts, then the token rows and their local expert ids ->
+  owner runs its experts as a k=1 grouped MoE (``ome_moe_*`` kernels) ->
+  all-to-all-v #2: expert outputs travel back in the same order ->
+  combine in the original (token, slot) order with the routing weights (fp32).
+
+On one MI355X node the all-to-alls are RCCL over the xGMI mesh (every pair of GPUs has a direct
+link, so an all-to-all is N-1 independent point-to-point transfers); on CPU they run on gloo.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from ome_amd import ops
+from ome_amd.parallel import state as pstate
+
+
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: list[int], in_splits: list[int], group) -> None:
+    if inp.is_cuda or dist.get_backend(group) != "gloo":
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+        return
+    # gloo has no all_to_all: N-1 pairwise exchanges (CPU tests only)
+    st = pstate.get()
+    ws, me = dist.get_world_size(group), dist.get_rank(group)
+    ioff = [0]
+    for s in in_splits:
+        ioff.append(ioff[-1] + s)
+    ooff = [0]
+    for s in out_splits:
+        ooff.append(ooff[-1] + s)
+    out[ooff[me]:ooff[me + 1]].copy_(inp[ioff[me]:ioff[me + 1]])
+    for step in range(1, ws):
+        dst, src = (me + step) % ws, (me - step) % ws
+        reqs = []
+        if in_splits[dst]:
+            reqs.append(dist.isend(inp[ioff[dst]:ioff[dst + 1]].contiguous(), dst, group=group))
+        buf = None
+        if out_splits[src]:
+            buf = torch.empty_like(out[ooff[src]:ooff[src + 1]])
+            reqs.append(dist.irecv(buf, src, group=group))
+        for r in reqs:
+            r.wait()
+        if buf is not None:
+            out[ooff[src]:ooff[src + 1]].copy_(buf)
+    del st
+
+
+def moe_ep_forward(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13_local: torch.Tensor,
+                   w2_local: torch.Tensor, act: int, scale: float, num_experts: int) -> torch.Tensor:
+    """x [T, H] (this rank's tokens), routing [T, k] over the global experts; w13/w2 hold this
+    rank's ``E / ep`` experts.  Returns the routed-expert output [T, H] (no shared expert)."""
+    st = pstate.get()
+    group, ep, me = st.ep_group, st.ep_size, st.ep_rank
+    T, H = x.shape
+    k = topk_ids.shape[1]
+    e_local = num_experts // ep
+    flat_ids = topk_ids.reshape(-1).long()
+    owner = flat_ids // e_local
+    order = torch.argsort(owner, stable=True)
+    send_counts = torch.bincount(owner, minlength=ep)
+    recv_counts = torch.empty_like(send_counts)
+    _a2a(recv_counts, send_counts, [1] * ep, [1] * ep, group)
+    sc, rc = send_counts.tolist(), recv_counts.tolist()
+    tok = order // k
+    send_x = x.index_select(0, tok)
+    send_e = (flat_ids.index_select(0, order) - owner.index_select(0, order) * e_local).to(torch.int32)
+    R = sum(rc)
+    recv_x = x.new_empty(R, H)
+    recv_e = torch.empty(R, dtype=torch.int32, device=x.device)
+    _a2a(recv_x, send_x, rc, sc, group)
+    _a2a(recv_e, send_e, rc, sc, group)
+    if R:
+        ones = torch.ones(R, 1, dtype=torch.float32, device=x.device)
+        y = ops.fused_moe(recv_x, ones, recv_e.view(R, 1), w13_local, w2_local, act, 1.0)
+    else:
+        y = x.new_empty(0, H)
+    back = x.new_empty(T * k, H)
+    _a2a(back, y, sc, rc, group)
+    unsorted = torch.empty_like(back)
+    unsorted.index_copy_(0, order, back)
+    out = (unsorted.view(T, k, H).float() * topk_w.float().view(T, k, 1)).sum(1) * scale
+    return out.to(x.dtype)

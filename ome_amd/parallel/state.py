@@ -54,19 +54,29 @@ def get() -> ParallelState:
 
 def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_init_addr: str | None = None,
          rank: int | None = None, world_size: int | None = None, backend: str | None = None,
-         local_rank: int | None = None) -> ParallelState:
-    """Initialise torch.distributed (if world > 1) and build TP / PP / EP groups."""
+         local_rank: int | None = None, dp_size: int = 1) -> ParallelState:
+    """Initialise torch.distributed (if world > 1) and build TP / PP / EP groups.
+
+    ``dp_size > 1`` is DP attention (SGLang ``--tp N --dp N --enable-dp-attention``): every rank
+    runs attention and dense layers for its OWN requests with full weights (attention TP = 1),
+    while MoE experts are partitioned over all N ranks (EP = N) and tokens travel to their
+    experts by all-to-all (:mod:`ome_amd.parallel.ep`)."""
     global _STATE
-    world = world_size if world_size is not None else int(os.environ.get("WORLD_SIZE", tp_size * pp_size))
+    if dp_size > 1:
+        if tp_size not in (1, dp_size) or pp_size != 1:
+            raise ValueError("DP attention needs tp_size == dp_size and pp_size == 1")
+        tp_size = 1
+    world = world_size if world_size is not None else int(os.environ.get("WORLD_SIZE", tp_size * pp_size * dp_size))
     rk = rank if rank is not None else int(os.environ.get("RANK", 0))
-    if world != tp_size * pp_size:
-        raise ValueError(f"world_size {world} != tp {tp_size} * pp {pp_size}")
+    if world != tp_size * pp_size * dp_size:
+        raise ValueError(f"world_size {world} != tp {tp_size} * pp {pp_size} * dp {dp_size}")
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     st = ParallelState(tp_size=tp_size, pp_size=pp_size, world_size=world, rank=rk, backend=backend)
-    st.tp_rank, st.pp_rank = rk % tp_size, rk // tp_size
-    st.ep_size = ep_size or tp_size
-    st.ep_rank = st.tp_rank % st.ep_size
+    st.dp_size, st.dp_rank = dp_size, (rk if dp_size > 1 else 0)
+    st.tp_rank, st.pp_rank = rk % tp_size, (rk // tp_size) % pp_size
+    st.ep_size = dp_size if dp_size > 1 else 1
+    st.ep_rank = st.dp_rank
     if world > 1:
         if not dist.is_initialized():
             init_method = f"tcp://{dist_init_addr}" if dist_init_addr else None
@@ -88,7 +98,7 @@ def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_in
             g = dist.new_group(ranks) if pp_size > 1 else None
             if t == st.tp_rank:
                 st.pp_group = g
-        st.ep_group = st.tp_group
+        st.ep_group = dist.group.WORLD if dp_size > 1 else None
         single_node = int(os.environ.get("LOCAL_WORLD_SIZE", world)) >= world
         if backend == "nccl" and tp_size in (2, 4, 8) and single_node and os.environ.get("OME_CUSTOM_AR", "1") != "0":
             from ome_amd.parallel.comm import TPCommunicator

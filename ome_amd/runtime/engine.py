@@ -54,6 +54,7 @@ class EngineArgs:
     nnodes: int = 1
     node_rank: int = 0
     disaggregation_mode: str = "null"      # null | prefill | decode
+    enable_dp_attention: bool = False      # --dp N --enable-dp-attention: per-rank batches + EP MoE
     overlap_schedule: bool | None = None   # enqueue step k+1 before step k's tokens reach the host
                                            # (None = on for GPU engines)
     num_layers_override: int | None = None
@@ -80,9 +81,13 @@ class Engine:
 
         self.args = args
         self.cfg = args.model_config()
-        if args.tp_size > 1 or args.pp_size > 1:
-            pstate.init(args.tp_size, args.pp_size, dist_init_addr=args.dist_init_addr)
+        dp = args.dp_size if args.enable_dp_attention else 1
+        if args.tp_size > 1 or args.pp_size > 1 or dp > 1:
+            pstate.init(args.tp_size, args.pp_size, dist_init_addr=args.dist_init_addr, dp_size=dp)
         self.pstate = pstate.get()
+        self.dp = self.pstate.dp_size > 1
+        self._remote: dict[str, Request] = {}   # DP attention, rank 0: requests served by other ranks
+        self._dp_next = 0
         device = args.device
         if device == "cuda" and torch.cuda.is_available():
             device = f"cuda:{torch.cuda.current_device()}"
@@ -96,7 +101,7 @@ class Engine:
                                   load_format=args.load_format,
                                   page_size=args.page_size, mem_fraction_static=args.mem_fraction_static,
                                   max_total_tokens=args.max_total_tokens, max_running=args.max_running_requests,
-                                  max_context=self.max_context, cuda_graph=args.cuda_graph,
+                                  max_context=self.max_context, cuda_graph=args.cuda_graph and not self.dp,
                                   cuda_graph_max_bs=args.cuda_graph_max_bs, seed=args.seed)
         prefix = None
         if not args.disable_radix_cache:
@@ -121,7 +126,7 @@ class Engine:
         # overlapped scheduling: (batch, handle, launch time) of the step whose tokens are in flight
         self._inflight = None
         ov = self.runner.is_cuda if args.overlap_schedule is None else bool(args.overlap_schedule)
-        self.overlap = ov and not self.cfg.is_embedding and self.pstate.pp_size == 1
+        self.overlap = ov and not self.cfg.is_embedding and self.pstate.pp_size == 1 and not self.dp
 
     # ------------------------------------------------------------------ API
     def make_request(self, prompt_ids: list[int], params: SamplingParams | None = None, **kw) -> Request:
@@ -153,6 +158,11 @@ class Engine:
             new, aborts = self._broadcast_control(new, aborts)
         kt = self.kv_transfer
         for r in new:
+            if self.dp and getattr(r, "dp_rank", 0) != self.pstate.rank:
+                if self.pstate.rank == 0:
+                    self._remote[r.rid] = r  # proxy: tokens arrive from the owning rank
+                    self.metrics.on_arrival(r)
+                continue
             r.arrival_time = r.arrival_time or time.perf_counter()
             if kt is not None and kt.mode == "decode" and (r.bootstrap or {}).get("disagg_role") == "decode":
                 kt.hold(r)  # its KV comes from a prefill engine (ome_amd.runtime.disagg)
@@ -166,6 +176,9 @@ class Engine:
                         kt.waiting.pop(room)
                         w.state, w.finish_reason = ReqState.FINISHED, "abort"
             r = self.scheduler.abort(rid)
+            if r is None and rid in self._remote:  # DP proxy: the owning rank aborts its copy
+                r = self._remote.pop(rid)
+                r.state, r.finish_reason = ReqState.FINISHED, "abort"
             if r is not None and r.on_token:
                 r.on_token(r, [], True)
 
@@ -174,17 +187,34 @@ class Engine:
         (followers leave ``run_forever`` when the leader shuts down)."""
         import torch.distributed as dist
 
-        payload = [[(r.rid, r.prompt_ids, asdict(r.params), r.bootstrap) for r in new], aborts,
-                   stop or self._stop_pending]
+        if self.dp and self.pstate.rank == 0:
+            for r in new:  # DP attention: least-loaded rank owns the request
+                r.dp_rank = self._dp_assign()
+        payload = [[(r.rid, r.prompt_ids, asdict(r.params), r.bootstrap, getattr(r, "dp_rank", 0)) for r in new],
+                   aborts, stop or self._stop_pending]
         obj = [payload if self.pstate.rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=self._cpu_group())
         if obj[0][2]:
             self._stop = True
         if self.pstate.rank == 0:
             return new, aborts
-        reqs = [Request(prompt_ids=p, params=SamplingParams(**sp), rid=rid, bootstrap=b)
-                for rid, p, sp, b in obj[0][0]]
+        reqs = []
+        for rid, p, sp, b, dr in obj[0][0]:
+            r = Request(prompt_ids=p, params=SamplingParams(**sp), rid=rid, bootstrap=b)
+            r.dp_rank = dr
+            reqs.append(r)
         return reqs, obj[0][1]
+
+    def _dp_assign(self) -> int:
+        """Rank 0: the DP rank with the fewest outstanding requests (round-robin on ties)."""
+        n = self.pstate.dp_size
+        load = [0] * n
+        load[0] = len(self.scheduler.running) + len(self.scheduler.waiting)
+        for r in self._remote.values():
+            load[r.dp_rank] += 1
+        best = min(range(n), key=lambda i: (load[i], (i - self._dp_next) % n))
+        self._dp_next = (best + 1) % n
+        return best
 
     def stop_group(self) -> None:
         """Leader: tell every follower rank to exit its step loop (one final control broadcast)."""
@@ -212,6 +242,8 @@ class Engine:
             self.kv_transfer.poll()
         if self.cfg.is_embedding:
             return self._embed_step()
+        if self.dp:
+            return self._dp_step()
         prev = self._inflight
         batch = self.scheduler.schedule()
         launched = None
@@ -238,6 +270,56 @@ class Engine:
         self.metrics.on_step(batch, now - t0, done, self.scheduler, self.runner.pages)
         return done
 
+    def _dp_step(self) -> list[Request]:
+        """DP attention: every rank schedules its own requests, all ranks run the forward in
+        lockstep (a rank without work runs one dummy token so the MoE all-to-alls are complete),
+        and the followers report their new tokens to rank 0, which owns the HTTP streams."""
+        import torch.distributed as dist
+
+        batch = self.scheduler.schedule()
+        mine = torch.tensor([0 if batch is None else sum(c.length for c in batch.chunks)], dtype=torch.int64)
+        allw = [torch.zeros(1, dtype=torch.int64) for _ in range(self.pstate.world_size)]
+        dist.all_gather(allw, mine, group=self._cpu_group())
+        if not any(int(w) for w in allw):
+            return []
+        done: list[Request] = []
+        touched = []
+        if batch is not None:
+            t0 = time.perf_counter()
+            handle = self.runner.launch(batch)
+            self.scheduler.launch_commit(batch)
+            done = self._complete(batch, handle, t0)
+            touched = list({id(c.req): c.req for c in batch.chunks}.values())
+        else:
+            self.runner.idle_forward()
+        updates = []
+        for r in touched:
+            k = getattr(r, "_reported", 0)
+            updates.append((r.rid, r.output_ids[k:], r.output_logprobs[k:], r.state == ReqState.FINISHED,
+                            r.finish_reason))
+            r._reported = len(r.output_ids)
+        gathered = [None] * self.pstate.world_size if self.pstate.rank == 0 else None
+        dist.gather_object(updates, gathered, dst=0, group=self._cpu_group())
+        if self.pstate.rank == 0:
+            now = time.perf_counter()
+            for rank_updates in gathered[1:]:
+                for rid, toks, lps, fin, reason in rank_updates:
+                    p = self._remote.get(rid)
+                    if p is None:
+                        continue
+                    if toks and p.first_token_time is None:
+                        p.first_token_time = now
+                    p.output_ids.extend(toks)
+                    p.output_logprobs.extend(lps)
+                    p.token_times.extend([now] * len(toks))
+                    if fin:
+                        p.state, p.finish_reason = ReqState.FINISHED, reason
+                        self._remote.pop(rid, None)
+                        done.append(p)
+                    if p.on_token is not None and (toks or fin):
+                        p.on_token(p, list(toks), fin)
+        return done
+
     def flush(self) -> list[Request]:
         """Wait for the in-flight step (if any) and commit it."""
         prev, self._inflight = self._inflight, None
@@ -262,7 +344,7 @@ class Engine:
         return done
 
     def has_work(self) -> bool:
-        return (self.scheduler.has_work() or bool(self._inbox) or self._inflight is not None
+        return (self.scheduler.has_work() or bool(self._inbox) or self._inflight is not None or bool(self._remote)
                 or bool(self.kv_transfer is not None and self.kv_transfer.waiting))
 
     def generate(self, prompts: list[list[int]], params: SamplingParams | list[SamplingParams] | None = None) -> list[Request]:

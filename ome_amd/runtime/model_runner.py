@@ -487,6 +487,17 @@ class ModelRunner:
             pstate.pp_broadcast_from_last(out_lp.float().contiguous())
         return self._finish_launch(out_ids, out_lp, len(chunks))
 
+    def idle_forward(self) -> None:
+        """DP attention: this rank has nothing scheduled but its peers do -- run one dummy token
+        (scratch page 0) through the model so every MoE all-to-all has all participants."""
+        dv = self.device
+        z = torch.zeros(1, dtype=torch.int32, device=dv)
+        meta = AttnMeta("prefill", z, z.clone(), torch.zeros(1, 1, dtype=torch.int32, device=dv),
+                        cu_q=torch.tensor([0, 1], dtype=torch.int32, device=dv),
+                        kv_lens=torch.ones(1, dtype=torch.int32, device=dv),
+                        items=torch.zeros(1, 2, dtype=torch.int32, device=dv))
+        self.model.forward(z, meta, self.kv)
+
     def embed(self, batch: StepBatch) -> list[list[float]]:
         """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts."""
         P = self.P

@@ -81,6 +81,7 @@ class Request:
     lora: str | None = None
     n_pending: int = 0             # placeholders in output_ids awaiting their sampled token
     pen_init: bool = False         # penalty count row initialised for the current req_slot
+    dp_rank: int = 0               # DP attention: the rank whose scheduler owns the request
     pending_row: int = -1          # row of the newest pending token in its step's sampled output
 
     @property

@@ -59,6 +59,9 @@ def build_parser() -> argparse.ArgumentParser:
     a("--load-format", default="auto")
     a("--dtype", default="bfloat16")
     a("--kv-cache-dtype", default="auto")
+    a("--enable-dp-attention", action="store_true",
+      help="--dp N with --tp N: attention/dense layers data-parallel per rank, MoE experts expert-parallel")
+    a("--moe-a2a-backend", default="rccl", help="expert-parallel dispatch backend (rccl all-to-all over xGMI)")
     a("--quantization", default=None, help="fp8: W8A8 projections (per-channel online, or the checkpoint's blocks)")
     a("--random-seed", type=int, default=0)
     a("--device", default="cuda")
@@ -92,6 +95,7 @@ def engine_args_from(ns, rank_tp: int | None = None):
                       device=ns.device, seed=ns.random_seed, enable_mixed_chunk=ns.enable_mixed_chunk,
                       disable_radix_cache=ns.disable_radix_cache, is_embedding=ns.is_embedding,
                       kv_cache_dtype=ns.kv_cache_dtype, quantization=ns.quantization,
+                      enable_dp_attention=ns.enable_dp_attention,
                       dist_init_addr=ns.dist_init_addr, nnodes=ns.nnodes,
                       node_rank=ns.node_rank, disaggregation_mode=ns.disaggregation_mode,
                       num_layers_override=ns.num_layers,
@@ -366,7 +370,7 @@ def main(argv=None) -> int:
     ns, unknown = ap.parse_known_args(argv)
     if unknown:
         log.warning("ignoring unsupported flags: %s", " ".join(unknown))
-    world = ns.tp_size * ns.pp_size
+    world = (ns.dp_size if ns.enable_dp_attention and ns.tp_size == 1 else ns.tp_size) * ns.pp_size
     per_node = max(1, world // max(1, ns.nnodes))
     base_rank = ns.node_rank * per_node
     procs = []

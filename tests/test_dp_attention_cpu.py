@@ -1,0 +1,75 @@
+"""DP attention + expert parallelism on CPU (gloo): 2 ranks, each scheduling its own requests
+with full attention / dense weights and half of the experts, MoE tokens exchanged by
+all-to-all (``ome_amd.parallel.ep``), tokens relayed to rank 0 -- must generate what a single
+rank generates from the same HF checkpoint (Qwen3-MoE and DeepSeek-V3 layouts)."""
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from ome_amd.io.safetensors import save_file
+from ome_amd.models import build_model
+from ome_amd.models.config import PRESETS, ModelConfig
+from tests.test_deepseek_cpu import _hf_weights
+from tests.test_moe_cpu import _export_hf
+
+PROMPTS = [[3 + (i * 37 + j) % 1000 for j in range(5 + 7 * i)] for i in range(5)]
+
+
+def _worker(rank, world, port, path, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from ome_amd.runtime.engine import Engine, EngineArgs
+    from ome_amd.runtime.request import SamplingParams
+
+    eng = Engine(EngineArgs(model_path=path, tp_size=world, dp_size=world, enable_dp_attention=True, device="cpu",
+                            max_running_requests=8, context_length=256, dtype="float32"))
+    m = eng.runner.model
+    assert m.E_local == m.E // world and m.e0 == rank * m.E_local
+    if rank == 0:
+        reqs = eng.generate(PROMPTS, SamplingParams(max_new_tokens=8, ignore_eos=True))
+        owners = {r.dp_rank for r in reqs}
+        eng.stop_group()
+        q.put(([r.output_ids for r in reqs], owners))
+    else:
+        eng.run_forever()
+
+
+def _checkpoint(tmp_path, kind):
+    if kind == "qwen3-moe":
+        hf = dict(PRESETS["tiny-moe"])
+        m = build_model(ModelConfig.from_hf(hf), "cpu", torch.float32, load_format="dummy", seed=5)
+        _export_hf(m, tmp_path, "qwen3")
+    else:
+        hf = dict(PRESETS["tiny-deepseek"])
+        w = _hf_weights(ModelConfig.from_hf(hf), seed=2)
+        save_file({k: v.contiguous() for k, v in w.items()}, tmp_path / "model.safetensors")
+    (tmp_path / "config.json").write_text(json.dumps(hf))
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("kind", ["qwen3-moe", "deepseek-v3"])
+def test_dp_attention_ep_matches_single(tmp_path, kind):
+    _checkpoint(tmp_path, kind)
+    from ome_amd.runtime.engine import Engine, EngineArgs
+    from ome_amd.runtime.request import SamplingParams
+
+    single = Engine(EngineArgs(model_path=str(tmp_path), device="cpu", max_running_requests=8, context_length=256,
+                               dtype="float32"))
+    want = [r.output_ids for r in single.generate(PROMPTS, SamplingParams(max_new_tokens=8, ignore_eos=True))]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got, owners = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert owners == {0, 1}  # both ranks served requests
+    assert got == want
