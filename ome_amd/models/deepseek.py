@@ -98,6 +98,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         self.w_sgu: list = [None] * L
         self.w_sd: list = [None] * L
         self.kv_layout = (1, KV_LATENT + ROPE_DIM, 0)
+        self.tune_gemms = False  # TunableOp pre-capture tuning is validated on the dense family only
         self._ws = None
         self._arange = None
 
@@ -318,7 +319,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         flat = cache.view(-1, KV_LATENT + ROPE_DIM)
         # padding rows carry slot -1: park them in the scratch page 0
         flat.index_copy_(0, meta.slots.long().clamp_min(0), torch.cat([c, k_pe], -1))
-        q_nope = q[..., : self.nope].transpose(0, 1)                      # [Hl, T, nope]
+        q_nope = q[..., : self.nope].transpose(0, 1).contiguous()         # [Hl, T, nope]
         q_lat = torch.bmm(q_nope, self.w_uk[i])                           # [Hl, T, 512]
         q_full = torch.cat([q_lat.transpose(0, 1), q_pe], -1).contiguous()  # [T, Hl, 576]
         o_lat = torch.empty(T, Hl, KV_LATENT, dtype=x.dtype, device=x.device)
@@ -327,7 +328,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         cache3 = cache.view(cache.shape[0], -1, KV_LATENT + ROPE_DIM)
         for s, e, bt, rows, lens in self._token_rows(meta, T):
             ops.mla_attn(q_full[s:e], cache3, bt, rows, lens, self.scale, self._ws, out=o_lat[s:e])
-        o = torch.bmm(o_lat.transpose(0, 1), self.w_uv[i])                # [Hl, T, vd]
+        o = torch.bmm(o_lat.transpose(0, 1).contiguous(), self.w_uv[i])   # [Hl, T, vd]
         o = o.transpose(0, 1).reshape(T, Hl * self.vd)
         return pstate.tp_all_reduce(linear(o, self.w_o[i]))
 

@@ -33,6 +33,7 @@ class MoEForCausalLM(LlamaForCausalLM):
             raise ValueError(f"{self.E} experts do not split over ep={self.ep}")
         self.E_local = self.E // self.ep
         self.e0 = st.ep_rank * self.E_local
+        self.tune_gemms = False  # TunableOp pre-capture tuning is validated on the dense family only
         self.k = cfg.num_experts_per_tok
         self.renorm = cfg.norm_topk_prob
         self.moe_inter = -(-cfg.moe_intermediate_size // tp.tp)

@@ -194,6 +194,8 @@ class ModelRunner:
         the library heuristic otherwise (never tuned inside serving)."""
         if os.environ.get("OME_TUNE_GEMM", "1") != "1" or not hasattr(torch.cuda, "tunable"):
             return False
+        if not getattr(self.model, "tune_gemms", True):
+            return False
         tun = torch.cuda.tunable
         self.TUNED_DIR.mkdir(parents=True, exist_ok=True)
         arch = torch.cuda.get_device_properties(self.device).gcnArchName.split(":")[0]
@@ -229,6 +231,9 @@ class ModelRunner:
         d = self.dbuf
         d.hnp[:] = 0
         d.hnp[d.off["slots"]:d.off["slots"] + d.bmax] = -1
+        for name, v in (("rep", 1.0), ("top_p", 1.0)):   # neutral sampling params for the warm-up rows
+            d.hf[d.off[name]:d.off[name] + d.bmax] = v
+        d.hnp[d.off["top_k"]:d.off["top_k"] + d.bmax] = -1
         d.dev.copy_(d.host)
         torch.cuda.synchronize(self.device)
         stream = torch.cuda.Stream(self.device)
