@@ -16,6 +16,11 @@
 //   k-slot (g, j) = page (j >> 2), key 4g + (j & 3)
 // which is exactly the order the S^T accumulators already sit in, so P feeds the second
 // MFMA from registers with no lane movement (the "accumulator as next operand" idiom).
+//
+// KV-cache formats (K15): every kernel except decode v1 is templated on the cache element
+// format F (common.h KVFmt).  fp8 caches are read at half the bytes and converted to bf16 in
+// registers just before the MFMA; the host folds k_scale into the softmax scale and the
+// kernels multiply the normalised output by v_scale.
 #include "common.h"
 
 #include <cstdlib>
@@ -35,6 +40,35 @@ __device__ __forceinline__ bf16x8 cat44(bf16x4 a, bf16x4 b) {
   r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
   r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
   return r;
+}
+
+// raw cache fragments (8 consecutive elements / 4 consecutive elements) and their bf16 views
+template <int F> struct KVRaw {
+  typedef uint2 K8;
+  typedef uint32_t V4;
+};
+template <> struct KVRaw<KV_BF16> {
+  typedef bf16x8 K8;
+  typedef bf16x4 V4;
+};
+
+template <int F>
+__device__ __forceinline__ bf16x8 k8_bf16(const typename KVRaw<F>::K8& x) {
+  if constexpr (F == KV_BF16) return x;
+  else return fp8x8_to_bf16<F>(x);
+}
+template <int F>
+__device__ __forceinline__ bf16x4 v4_bf16(const typename KVRaw<F>::V4& x) {
+  if constexpr (F == KV_BF16) return x;
+  else return fp8x4_to_bf16<F>(x);
+}
+template <int F>
+__device__ __forceinline__ typename KVRaw<F>::K8 k8_load(const typename KVStore<F>::T* p) {
+  return *reinterpret_cast<const typename KVRaw<F>::K8*>(p);
+}
+template <int F>
+__device__ __forceinline__ typename KVRaw<F>::V4 v4_load(const typename KVStore<F>::T* p) {
+  return *reinterpret_cast<const typename KVRaw<F>::V4*>(p);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -201,46 +235,48 @@ __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const int* __res
 //    not two), and the next tile of the wave is issued before the current one is consumed
 //    (2-deep register ring, counted vmcnt by the compiler): ~32 KB in flight per wave;
 //  * the LDS merge stores only the G live query heads (8.5 KB for G=4 instead of 33 KB), so
-//    occupancy is set by VGPRs, not LDS.
+//    occupancy is set by VGPRs, not LDS;
+//  * fp8 caches keep the raw bytes in the tile (half the VGPRs) and convert at consume time.
 // ------------------------------------------------------------------------------------------
-template <int D>
+template <int D, int F>
 struct KVTile {
-  bf16x8 ka[D / 32], kb[D / 32];
-  bf16x4 va[D / 16], vb[D / 16];
+  typename KVRaw<F>::K8 ka[D / 32], kb[D / 32];
+  typename KVRaw<F>::V4 va[D / 16], vb[D / 16];
 };
 
-template <int D, int P>
-__device__ __forceinline__ void kv_tile_load(KVTile<D>& t, const bf16* __restrict__ k_cache,
-                                             const bf16* __restrict__ v_cache, const int* __restrict__ bt, int kb,
-                                             int seq_len, int64_t kpage, int kvh, int n, int g) {
+template <int D, int P, int F>
+__device__ __forceinline__ void kv_tile_load(KVTile<D, F>& t, const typename KVStore<F>::T* __restrict__ k_cache,
+                                             const typename KVStore<F>::T* __restrict__ v_cache,
+                                             const int* __restrict__ bt, int kb, int seq_len, int64_t kpage, int kvh,
+                                             int n, int g) {
   const int pA = bt[kb / P];
   const int pB = (kb + P < seq_len) ? bt[kb / P + 1] : pA;
-  const bf16* kA = k_cache + pA * kpage + (int64_t)kvh * P * D;
-  const bf16* kB = k_cache + pB * kpage + (int64_t)kvh * P * D;
-  const bf16* vA = v_cache + pA * kpage + (int64_t)kvh * D * P;
-  const bf16* vB = v_cache + pB * kpage + (int64_t)kvh * D * P;
+  const typename KVStore<F>::T* kA = k_cache + pA * kpage + (int64_t)kvh * P * D;
+  const typename KVStore<F>::T* kB = k_cache + pB * kpage + (int64_t)kvh * P * D;
+  const typename KVStore<F>::T* vA = v_cache + pA * kpage + (int64_t)kvh * D * P;
+  const typename KVStore<F>::T* vB = v_cache + pB * kpage + (int64_t)kvh * D * P;
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
-    t.ka[ks] = ld8(kA + n * D + 32 * ks + 8 * g);
-    t.kb[ks] = ld8(kB + n * D + 32 * ks + 8 * g);
+    t.ka[ks] = k8_load<F>(kA + n * D + 32 * ks + 8 * g);
+    t.kb[ks] = k8_load<F>(kB + n * D + 32 * ks + 8 * g);
   }
 #pragma unroll
   for (int nb = 0; nb < D / 16; ++nb) {
     const int dim = 16 * nb + n;
-    t.va[nb] = ld4(vA + dim * P + 4 * g);
-    t.vb[nb] = ld4(vB + dim * P + 4 * g);
+    t.va[nb] = v4_load<F>(vA + dim * P + 4 * g);
+    t.vb[nb] = v4_load<F>(vB + dim * P + 4 * g);
   }
 }
 
-template <int D>
-__device__ __forceinline__ void kv_tile_compute(const KVTile<D>& t, const bf16x8 (&qf)[D / 32], f32x4 (&o)[D / 16],
-                                                float& m_i, float& l_i, int kb, int p_end, int lo, float scale_log2,
-                                                int g) {
+template <int D, int F>
+__device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf16x8 (&qf)[D / 32],
+                                                f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
+                                                int lo, float scale_log2, int g) {
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
-    s0 = mfma16(t.ka[ks], qf[ks], s0);
-    s1 = mfma16(t.kb[ks], qf[ks], s1);
+    s0 = mfma16(k8_bf16<F>(t.ka[ks]), qf[ks], s0);
+    s1 = mfma16(k8_bf16<F>(t.kb[ks]), qf[ks], s1);
   }
   float mt = OME_NEG_INF;
 #pragma unroll
@@ -271,17 +307,17 @@ __device__ __forceinline__ void kv_tile_compute(const KVTile<D>& t, const bf16x8
 #pragma unroll
   for (int nb = 0; nb < D / 16; ++nb) {
     o[nb] = o[nb] * alpha;
-    o[nb] = mfma16(cat44(t.va[nb], t.vb[nb]), pb, o[nb]);
+    o[nb] = mfma16(cat44(v4_bf16<F>(t.va[nb]), v4_bf16<F>(t.vb[nb])), pb, o[nb]);
   }
 }
 
-template <int D, int P, bool PF>
+template <int D, int P, bool PF, int F>
 __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
-    const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
-    const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
+    const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ seq_lens, bf16* __restrict__ out, int64_t out_stride, float* __restrict__ part_o,
     float* __restrict__ part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2, int window,
-    const int* __restrict__ order) {
+    const int* __restrict__ order, float v_scale) {
   static_assert(P == 16, "decode kernel assumes 16-token pages");
   constexpr int NB = D / 16, KS = D / 32;
   // blockIdx.z walks sequences longest-first when the host provides ``order`` (the dispatcher
@@ -320,23 +356,23 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
   }
   if (!PF) {
     for (; kb < p_end; kb += 128) {
-      KVTile<D> t;
-      kv_tile_load<D, P>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D>(t, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
+      KVTile<D, F> t;
+      kv_tile_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
+      kv_tile_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
     }
   } else if (kb < p_end) {
-    KVTile<D> t0, t1;
-    kv_tile_load<D, P>(t0, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
+    KVTile<D, F> t0, t1;
+    kv_tile_load<D, P, F>(t0, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
     for (;;) {
       const int kn = kb + 128;
       const bool more = kn < p_end;
-      if (more) kv_tile_load<D, P>(t1, k_cache, v_cache, bt, kn, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D>(t0, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
+      if (more) kv_tile_load<D, P, F>(t1, k_cache, v_cache, bt, kn, seq_len, kpage, kvh, n, g);
+      kv_tile_compute<D, F>(t0, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
       if (!more) break;
       const int kn2 = kn + 128;
       const bool more2 = kn2 < p_end;
-      if (more2) kv_tile_load<D, P>(t0, k_cache, v_cache, bt, kn2, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D>(t1, qf, o, m_i, l_i, kn, p_end, lo, scale_log2, g);
+      if (more2) kv_tile_load<D, P, F>(t0, k_cache, v_cache, bt, kn2, seq_len, kpage, kvh, n, g);
+      kv_tile_compute<D, F>(t1, qf, o, m_i, l_i, kn, p_end, lo, scale_log2, g);
       if (!more2) break;
       kb = kn2;
     }
@@ -368,7 +404,7 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
       acc += sm_o[(w * G + h) * D + d] * f;
     }
     const int head = kvh * G + h;
-    const float res = L > 0.f ? acc / L : 0.f;
+    const float res = L > 0.f ? acc / L * v_scale : 0.f;
     if (nparts == 1) {
       out[(int64_t)b * out_stride + (int64_t)head * D + d] = (bf16)res;
     } else {
@@ -382,19 +418,35 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
   }
 }
 
+template <int F>
+static void launch_decode_v2(int variant, dim3 grid, size_t smem, hipStream_t stream, const void* q,
+                             int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
+                             int bt_stride, const int* seq_lens, void* out, int64_t out_stride, void* part_o,
+                             void* part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2,
+                             int window, const int* order, float v_scale) {
+  auto kern = variant == 2 ? paged_decode_v2_kernel<128, 16, true, F> : paged_decode_v2_kernel<128, 16, false, F>;
+  kern<<<grid, 256, smem, stream>>>((const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache,
+                                    (const typename KVStore<F>::T*)v_cache, block_tables, bt_stride, seq_lens,
+                                    (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size,
+                                    max_parts, scale_log2, window, order, v_scale);
+}
+
+// kv_fmt: KVFmt of the cache; k_scale / v_scale: per-layer dequantisation scales (1 for bf16)
 OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                              const int* block_tables, int bt_stride, const int* seq_lens, void* out,
                              int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
-                             int part_size, int max_parts, float scale, int window, const int* order,
-                             hipStream_t stream) {
+                             int part_size, int max_parts, float scale, int window, const int* order, int kv_fmt,
+                             float k_scale, float v_scale, hipStream_t stream) {
   if (B <= 0) return 0;
   if (D != 128 || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
   if (part_size % 128 != 0 || max_parts <= 0) return -4;
-  const float scale_log2 = scale * 1.4426950408889634f;
+  if (kv_fmt < 0 || kv_fmt > 2) return -5;
+  const float scale_log2 = scale * k_scale * 1.4426950408889634f;
   dim3 grid(max_parts, Hkv, B);
-  const char* ve = getenv("OME_DECODE_ATTN");  // A/B switch for benchmarking (default v2)
-  const int variant = ve ? atoi(ve) : 3;
+  const char* ve = getenv("OME_DECODE_ATTN");  // A/B switch for benchmarking (default v3 = v2 without ring)
+  int variant = ve ? atoi(ve) : 3;
+  if (variant == 1 && kv_fmt != KV_BF16) variant = 3;  // v1 reads bf16 caches only
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
     paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(
@@ -403,11 +455,13 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   } else {
     const int G = Hq / Hkv;
     const size_t smem = (8 * G + 4 * G * D) * sizeof(float);
-    auto kern = variant == 2 ? paged_decode_v2_kernel<128, 16, true> : paged_decode_v2_kernel<128, 16, false>;
-    kern<<<grid, 256, smem, stream>>>(
-        (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, seq_lens,
-        (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window,
-        order);
+#define ARGS                                                                                                     \
+  variant, grid, smem, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, out, out_stride, \
+      part_o, part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window, order, v_scale
+    if (kv_fmt == KV_BF16) launch_decode_v2<KV_BF16>(ARGS);
+    else if (kv_fmt == KV_E4M3) launch_decode_v2<KV_E4M3>(ARGS);
+    else launch_decode_v2<KV_E5M2>(ARGS);
+#undef ARGS
   }
   OME_CHECK_LAUNCH();
   if (max_parts > 1) {
@@ -426,12 +480,12 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
 // Queries at local row r sit at absolute position (kv_len - q_len + r): this covers fresh
 // prompts (kv_len == q_len), chunked prefill and prefix-cache hits uniformly.
 // ------------------------------------------------------------------------------------------
-template <int D, int P>
+template <int D, int P, int F>
 __global__ __launch_bounds__(512) void paged_prefill_kernel(
-    const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
-    const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
+    const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
-    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window) {
+    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window, float v_scale) {
   static_assert(P == 16, "prefill kernel assumes 16-token pages");
   constexpr int NB = D / 16, KS = D / 32;
   const int2 it = items[blockIdx.x];
@@ -472,15 +526,15 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
     for (int kb = kv_lo; kb < kv_end; kb += 32) {
       const int pA = bt[kb / P];
       const int pB = (kb + P < kv_len) ? bt[kb / P + 1] : pA;
-      const bf16* kA = k_cache + pA * kpage + (int64_t)kvh * P * D;
-      const bf16* kB = k_cache + pB * kpage + (int64_t)kvh * P * D;
+      const typename KVStore<F>::T* kA = k_cache + pA * kpage + (int64_t)kvh * P * D;
+      const typename KVStore<F>::T* kB = k_cache + pB * kpage + (int64_t)kvh * P * D;
       f32x4 sc[2][2];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) sc[rb][0] = sc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 a0 = ld8(kA + n * D + 32 * ks + 8 * g);
-        bf16x8 a1 = ld8(kB + n * D + 32 * ks + 8 * g);
+        bf16x8 a0 = kv_ld8<F>(kA + n * D + 32 * ks + 8 * g);
+        bf16x8 a1 = kv_ld8<F>(kB + n * D + 32 * ks + 8 * g);
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           sc[rb][0] = mfma16(a0, qf[rb][ks], sc[rb][0]);
@@ -525,12 +579,12 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
         l_i[rb] = l_i[rb] * alpha[rb] + rs;
         m_i[rb] = m_new;
       }
-      const bf16* vA = v_cache + pA * kpage + (int64_t)kvh * D * P;
-      const bf16* vB = v_cache + pB * kpage + (int64_t)kvh * D * P;
+      const typename KVStore<F>::T* vA = v_cache + pA * kpage + (int64_t)kvh * D * P;
+      const typename KVStore<F>::T* vB = v_cache + pB * kpage + (int64_t)kvh * D * P;
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         const int dim = 16 * nb + n;
-        bf16x8 a = cat44(ld4(vA + dim * P + 4 * g), ld4(vB + dim * P + 4 * g));
+        bf16x8 a = cat44(kv_ld4<F>(vA + dim * P + 4 * g), kv_ld4<F>(vB + dim * P + 4 * g));
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           o[rb][nb] = o[rb][nb] * alpha[rb];
@@ -543,7 +597,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
     for (int rb = 0; rb < 2; ++rb) {
       const int r = r0 + 16 * rb + n;
       if (r < q_len) {
-        const float inv = l_i[rb] > 0.f ? 1.f / l_i[rb] : 0.f;
+        const float inv = l_i[rb] > 0.f ? v_scale / l_i[rb] : 0.f;
         bf16* orow = out + (int64_t)(q0 + r) * out_stride + (int64_t)head * D;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
@@ -567,16 +621,19 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
 //   V: [128 dims][32 keys + 8 pad], keys stored in the MFMA k-slot order of the S^T
 //      accumulators (slot 8g+j: j<4 -> page A key 4g+j, j>=4 -> page B key 4g+j-4), so a
 //      lane's A fragment of O^T = V^T P^T is one 16-B read.
+// fp8 caches are staged raw in registers (8 B per chunk) and converted to bf16 on the LDS
+// write, so the LDS images and the MFMA loop are identical for every cache format.
 // ------------------------------------------------------------------------------------------
 constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
 
-template <int SUB>
+template <int SUB, int F>
 __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
-    const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k_cache,
-    const bf16* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
+    const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
-    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window) {
+    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window, float v_scale) {
   constexpr int D = 128, P = 16, NB = D / 16, KS = D / 32;
+  typedef typename KVRaw<F>::K8 Raw8;  // 8 consecutive cache elements
   __shared__ __attribute__((aligned(16))) bf16 sK[2][SUB][32 * PF_KLD];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][SUB][D * PF_VLD];
   const int2 it = items[blockIdx.x];
@@ -616,9 +673,9 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) o[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- cooperative tile staging: per 32-key subtile, 2 x 16 B of K and 2 x 16 B of V per thread;
-  // a pipeline stage is SUB subtiles (32*SUB keys), so SUB x more bytes are in flight per wait ----
-  bf16x8 rk[SUB][2], rv[SUB][2];
+  // ---- cooperative tile staging: per 32-key subtile, 2 x 8 elements of K and 2 x 8 of V per
+  // thread; a pipeline stage is SUB subtiles (32*SUB keys), so SUB x more bytes are in flight ----
+  Raw8 rk[SUB][2], rv[SUB][2];
   auto load_tile = [&](int kb0) {
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
@@ -630,11 +687,11 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
       for (int i = 0; i < 2; ++i) {
         const int c = tid + 256 * i;
         const int key = c >> 4, dc = c & 15;
-        const bf16* kp = k_cache + (key < 16 ? pA : pB) * kpage + (int64_t)kvh * P * D;
-        rk[u][i] = ld8(kp + (key & 15) * D + dc * 8);
+        const typename KVStore<F>::T* kp = k_cache + (key < 16 ? pA : pB) * kpage + (int64_t)kvh * P * D;
+        rk[u][i] = k8_load<F>(kp + (key & 15) * D + dc * 8);
         const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
-        const bf16* vp = v_cache + (page ? pB : pA) * kpage + (int64_t)kvh * D * P;
-        rv[u][i] = ld8(vp + dim * P + half * 8);
+        const typename KVStore<F>::T* vp = v_cache + (page ? pB : pA) * kpage + (int64_t)kvh * D * P;
+        rv[u][i] = k8_load<F>(vp + dim * P + half * 8);
       }
     }
   };
@@ -645,11 +702,12 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
       for (int i = 0; i < 2; ++i) {
         const int c = tid + 256 * i;
         const int key = c >> 4, dc = c & 15;
-        *reinterpret_cast<bf16x8*>(&sK[buf][u][key * PF_KLD + dc * 8]) = rk[u][i];
+        *reinterpret_cast<bf16x8*>(&sK[buf][u][key * PF_KLD + dc * 8]) = k8_bf16<F>(rk[u][i]);
         const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
         bf16* vrow = &sV[buf][u][dim * PF_VLD];
-        bf16x4 lo4 = {rv[u][i][0], rv[u][i][1], rv[u][i][2], rv[u][i][3]};
-        bf16x4 hi4 = {rv[u][i][4], rv[u][i][5], rv[u][i][6], rv[u][i][7]};
+        const bf16x8 vv = k8_bf16<F>(rv[u][i]);
+        bf16x4 lo4 = {vv[0], vv[1], vv[2], vv[3]};
+        bf16x4 hi4 = {vv[4], vv[5], vv[6], vv[7]};
         *reinterpret_cast<bf16x4*>(vrow + (2 * half) * 8 + page * 4) = lo4;      // keys 8h..8h+3
         *reinterpret_cast<bf16x4*>(vrow + (2 * half + 1) * 8 + page * 4) = hi4;  // keys 8h+4..8h+7
       }
@@ -741,7 +799,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   for (int rb = 0; rb < 2; ++rb) {
     const int r = r0 + 16 * rb + n;
     if (r < q_len) {
-      const float inv = l_i[rb] > 0.f ? 1.f / l_i[rb] : 0.f;
+      const float inv = l_i[rb] > 0.f ? v_scale / l_i[rb] : 0.f;
       bf16* orow = out + (int64_t)(q0 + r) * out_stride + (int64_t)head * D;
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
@@ -754,28 +812,45 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   }
 }
 
+template <int F>
+static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, const void* q, int64_t q_stride,
+                           const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
+                           const int* cu_q, const int* kv_lens, const int* items, void* out, int64_t out_stride,
+                           int Hq, int Hkv, float scale_log2, int window, float v_scale) {
+  typedef typename KVStore<F>::T T;
+  if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
+    paged_prefill_v2_kernel<2, F><<<grid, 256, 0, stream>>>(
+        (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
+        (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window, v_scale);
+  } else {
+    const int nw = G < 8 ? G : 8;
+    paged_prefill_kernel<128, 16, F><<<grid, 64 * nw, 0, stream>>>(
+        (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
+        (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window, v_scale);
+  }
+}
+
 OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                               const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
                               const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
-                              int P, float scale, int window, hipStream_t stream) {
+                              int P, float scale, int window, int kv_fmt, float k_scale, float v_scale,
+                              hipStream_t stream) {
   if (n_items <= 0) return 0;
   if (D != 128 || P != 16) return -2;
   if (Hq % Hkv != 0) return -3;
+  if (kv_fmt < 0 || kv_fmt > 2) return -5;
   const int G = Hq / Hkv;
-  const float scale_log2 = scale * 1.4426950408889634f;
+  const float scale_log2 = scale * k_scale * 1.4426950408889634f;
   dim3 grid(n_items, Hkv);
   const char* ve = getenv("OME_PREFILL_ATTN");
   const int variant = ve ? atoi(ve) : 2;
-  if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
-    paged_prefill_v2_kernel<2><<<grid, 256, 0, stream>>>(
-        (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, cu_q,
-        kv_lens, (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window);
-  } else {
-    const int nw = G < 8 ? G : 8;
-    paged_prefill_kernel<128, 16><<<grid, 64 * nw, 0, stream>>>(
-        (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, cu_q,
-        kv_lens, (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window);
-  }
+#define ARGS                                                                                                   \
+  variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, out, \
+      out_stride, Hq, Hkv, scale_log2, window, v_scale
+  if (kv_fmt == KV_BF16) launch_prefill<KV_BF16>(ARGS);
+  else if (kv_fmt == KV_E4M3) launch_prefill<KV_E4M3>(ARGS);
+  else launch_prefill<KV_E5M2>(ARGS);
+#undef ARGS
   OME_CHECK_LAUNCH();
   return 0;
 }

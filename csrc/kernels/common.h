@@ -61,6 +61,83 @@ __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<
 __device__ __forceinline__ void st8(bf16* p, bf16x8 v) { *reinterpret_cast<bf16x8*>(p) = v; }
 __device__ __forceinline__ bf16x4 ld4(const bf16* p) { return *reinterpret_cast<const bf16x4*>(p); }
 
+// ------------------------------------------------------------------------------------------
+// Paged KV-cache element formats (K15, `--kv-cache-dtype`).  The attention kernels are
+// templated on the format; fp8 entries are converted to bf16 in registers right before the
+// MFMA (the hardware converters v_cvt_pk_f32_fp8 / _bf8 on gfx950 use the OCP encodings), and
+// the per-layer scalar scales are folded into the softmax scale (K) and the output
+// normalisation (V), so the inner loops never multiply by a scale.
+// ------------------------------------------------------------------------------------------
+enum KVFmt { KV_BF16 = 0, KV_E4M3 = 1, KV_E5M2 = 2 };
+
+template <int F> struct KVStore { typedef uint8_t T; };
+template <> struct KVStore<KV_BF16> { typedef bf16 T; };
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int F>
+__device__ __forceinline__ bf16x4 fp8x4_to_bf16(uint32_t v) {
+  f32x2 lo, hi;
+  if constexpr (F == KV_E4M3) {
+    lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)v, false);
+    hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)v, true);
+  } else {
+    lo = __builtin_amdgcn_cvt_pk_f32_bf8((int)v, false);
+    hi = __builtin_amdgcn_cvt_pk_f32_bf8((int)v, true);
+  }
+  return bf16x4{(bf16)lo.x, (bf16)lo.y, (bf16)hi.x, (bf16)hi.y};
+}
+
+template <int F>
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16(uint2 v) {
+  const bf16x4 a = fp8x4_to_bf16<F>(v.x), b = fp8x4_to_bf16<F>(v.y);
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+
+// 8 / 4 consecutive cache elements -> bf16
+template <int F>
+__device__ __forceinline__ bf16x8 kv_ld8(const typename KVStore<F>::T* p) {
+  if constexpr (F == KV_BF16) return ld8(p);
+  else return fp8x8_to_bf16<F>(*reinterpret_cast<const uint2*>(p));
+}
+template <int F>
+__device__ __forceinline__ bf16x4 kv_ld4(const typename KVStore<F>::T* p) {
+  if constexpr (F == KV_BF16) return ld4(p);
+  else return fp8x4_to_bf16<F>(*reinterpret_cast<const uint32_t*>(p));
+}
+
+// float pair -> saturated fp8 pair written into the low / high 16 bits of `old`
+template <int F, bool HI>
+__device__ __forceinline__ int fp8_pack2(float a, float b, int old) {
+  constexpr float M = F == KV_E4M3 ? 448.f : 57344.f;
+  a = fminf(fmaxf(a, -M), M);
+  b = fminf(fmaxf(b, -M), M);
+  if constexpr (F == KV_E4M3) return __builtin_amdgcn_cvt_pk_fp8_f32(a, b, old, HI);
+  else return __builtin_amdgcn_cvt_pk_bf8_f32(a, b, old, HI);
+}
+
+// store 8 floats (already multiplied by the inverse scale) as cache elements
+template <int F>
+__device__ __forceinline__ void kv_st8(typename KVStore<F>::T* p, const float (&f)[8]) {
+  if constexpr (F == KV_BF16) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)f[j];
+    st8(p, o);
+  } else {
+    uint2 o;
+    o.x = (uint32_t)fp8_pack2<F, true>(f[2], f[3], fp8_pack2<F, false>(f[0], f[1], 0));
+    o.y = (uint32_t)fp8_pack2<F, true>(f[6], f[7], fp8_pack2<F, false>(f[4], f[5], 0));
+    *reinterpret_cast<uint2*>(p) = o;
+  }
+}
+
+template <int F>
+__device__ __forceinline__ void kv_st1(typename KVStore<F>::T* p, float f) {
+  if constexpr (F == KV_BF16) *p = (bf16)f;
+  else *p = (uint8_t)(fp8_pack2<F, false>(f, 0.f, 0) & 0xff);
+}
+
 // XCD-aware remap of a linear workgroup id (bijective for any nwg; T1 of the guide).
 // Blocks b and b+8 share an XCD under round-robin dispatch, so give each XCD group a
 // contiguous chunk of the logical id space.

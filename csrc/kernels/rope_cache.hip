@@ -9,17 +9,20 @@
 //                                       the A operand of S^T = K Q^T straight from HBM (16 B).
 //   V cache: [num_pages, Hkv, D, P]   — transposed, so the A operand of O^T = V^T P^T is
 //                                       P-contiguous (keys) and loads straight from HBM too.
+// The cache element type is a template parameter (KVFmt in common.h): bf16, or OCP fp8
+// e4m3 / e5m2 (`--kv-cache-dtype fp8*`, K15) stored as fp8(x / scale) with saturation.
 // RoPE is the NeoX / HF "rotate_half" form; the cos/sin table [max_pos, rot_dim] (cos in the
 // first half, sin in the second) is precomputed on the host with the model's rope scaling
 // (llama3 / yarn / linear), so the kernel stays a pure streaming op (Appendix B, trig tables).
 #include "common.h"
 
-template <int D, int P>
+template <int D, int P, int F>
 __global__ __launch_bounds__(256) void rope_qkv_cache_kernel(
     const bf16* __restrict__ qkv, int64_t qkv_stride, const int* __restrict__ positions,
-    const float* __restrict__ cos_sin, int rot_dim, bf16* __restrict__ q_out, bf16* __restrict__ k_cache,
-    bf16* __restrict__ v_cache, const int* __restrict__ slots, int Hq, int Hkv, int apply_rope,
-    const bf16* __restrict__ q_norm_w, const bf16* __restrict__ k_norm_w, float qk_eps) {
+    const float* __restrict__ cos_sin, int rot_dim, bf16* __restrict__ q_out,
+    typename KVStore<F>::T* __restrict__ k_cache, typename KVStore<F>::T* __restrict__ v_cache,
+    const int* __restrict__ slots, int Hq, int Hkv, int apply_rope, const bf16* __restrict__ q_norm_w,
+    const bf16* __restrict__ k_norm_w, float qk_eps, float k_inv_scale, float v_inv_scale) {
   const int t = blockIdx.x;
   const bf16* row = qkv + (int64_t)t * qkv_stride;
   const int pos = positions[t];
@@ -76,15 +79,20 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_kernel(
       }
     }
     if (valid) {
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (bf16)f[j];
       if (is_q) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)f[j];
         st8(q_out + ((int64_t)t * Hq + h) * D + l * 8, o);
       } else if (slot >= 0) {
         const int kh = h - Hq;
         const int64_t page = slot / P, off = slot % P;
-        st8(k_cache + ((page * Hkv + kh) * P + off) * D + l * 8, o);
+        if constexpr (F != KV_BF16) {
+          // quantise the bf16-rounded key (the value a bf16 cache would have held)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = (float)(bf16)f[j] * k_inv_scale;
+        }
+        kv_st8<F>(k_cache + ((page * Hkv + kh) * P + off) * D + l * 8, f);
       }
     }
   }
@@ -95,66 +103,92 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_kernel(
     for (int i = threadIdx.x; i < Hkv * DV; i += blockDim.x) {
       const int kh = i / DV, dv = i % DV;
       bf16x8 x = ld8(vsrc + kh * D + dv * 8);
-      bf16* dst = v_cache + ((page * Hkv + kh) * D + dv * 8) * P + off;
+      typename KVStore<F>::T* dst = v_cache + ((page * Hkv + kh) * D + dv * 8) * P + off;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dst[j * P] = x[j];
+      for (int j = 0; j < 8; ++j) kv_st1<F>(dst + j * P, F == KV_BF16 ? (float)x[j] : (float)x[j] * v_inv_scale);
     }
   }
 }
 
 // Plain paged-cache write of already-projected K [T, Hkv, D] and V [T, Hkv, D] (used by the
 // PD-disaggregation receiver and by tests).
-template <int D, int P>
-__global__ void kv_cache_write_kernel(const bf16* __restrict__ k, const bf16* __restrict__ v,
-                                      int64_t kv_stride, bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
-                                      const int* __restrict__ slots, int Hkv) {
+template <int D, int P, int F>
+__global__ void kv_cache_write_kernel(const bf16* __restrict__ k, const bf16* __restrict__ v, int64_t kv_stride,
+                                      typename KVStore<F>::T* __restrict__ k_cache,
+                                      typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ slots,
+                                      int Hkv, float k_inv_scale, float v_inv_scale) {
   const int t = blockIdx.x;
   const int slot = slots[t];
   if (slot < 0) return;
   const int64_t page = slot / P, off = slot % P;
   constexpr int DV = D / 8;
+  constexpr bool q8 = F != KV_BF16;
   for (int i = threadIdx.x; i < Hkv * DV; i += blockDim.x) {
     const int kh = i / DV, dv = i % DV;
     bf16x8 kx = ld8(k + t * kv_stride + kh * D + dv * 8);
-    st8(k_cache + ((page * Hkv + kh) * P + off) * D + dv * 8, kx);
-    bf16x8 vx = ld8(v + t * kv_stride + kh * D + dv * 8);
-    bf16* dst = v_cache + ((page * Hkv + kh) * D + dv * 8) * P + off;
+    float f[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dst[j * P] = vx[j];
+    for (int j = 0; j < 8; ++j) f[j] = q8 ? (float)kx[j] * k_inv_scale : (float)kx[j];
+    kv_st8<F>(k_cache + ((page * Hkv + kh) * P + off) * D + dv * 8, f);
+    bf16x8 vx = ld8(v + t * kv_stride + kh * D + dv * 8);
+    typename KVStore<F>::T* dst = v_cache + ((page * Hkv + kh) * D + dv * 8) * P + off;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kv_st1<F>(dst + j * P, q8 ? (float)vx[j] * v_inv_scale : (float)vx[j]);
   }
 }
 
+// kv_fmt: KVFmt of the cache tensors; k_scale / v_scale: dequantisation scales (fp8 only)
 OME_API int ome_rope_qkv_cache(const void* qkv, int64_t qkv_stride, const int* positions, const float* cos_sin,
                                int rot_dim, void* q_out, void* k_cache, void* v_cache, const int* slots, int T,
                                int Hq, int Hkv, int D, int P, int apply_rope, const void* q_norm_w,
-                               const void* k_norm_w, float qk_eps, hipStream_t stream) {
+                               const void* k_norm_w, float qk_eps, int kv_fmt, float k_scale, float v_scale,
+                               hipStream_t stream) {
   if (T <= 0) return 0;
   if (D != 128 && D != 64) return -2;
   if (rot_dim > D || rot_dim % 16 != 0) return -3;
-#define LAUNCH(DD, PP)                                                                                    \
-  rope_qkv_cache_kernel<DD, PP><<<T, 256, 0, stream>>>((const bf16*)qkv, qkv_stride, positions, cos_sin, \
-                                                      rot_dim, (bf16*)q_out, (bf16*)k_cache,             \
-                                                      (bf16*)v_cache, slots, Hq, Hkv, apply_rope,        \
-                                                      (const bf16*)q_norm_w, (const bf16*)k_norm_w, qk_eps)
-  if (D == 128 && P == 16) LAUNCH(128, 16);
-  else if (D == 64 && P == 16) LAUNCH(64, 16);
-  else return -4;
+  if (P != 16) return -4;
+  if (kv_fmt < 0 || kv_fmt > 2) return -5;
+  const float ki = 1.f / k_scale, vi = 1.f / v_scale;
+#define LAUNCH(DD, FF)                                                                                          \
+  rope_qkv_cache_kernel<DD, 16, FF><<<T, 256, 0, stream>>>(                                                    \
+      (const bf16*)qkv, qkv_stride, positions, cos_sin, rot_dim, (bf16*)q_out, (KVStore<FF>::T*)k_cache,       \
+      (KVStore<FF>::T*)v_cache, slots, Hq, Hkv, apply_rope, (const bf16*)q_norm_w, (const bf16*)k_norm_w,      \
+      qk_eps, ki, vi)
+  if (D == 128) {
+    if (kv_fmt == KV_BF16) LAUNCH(128, KV_BF16);
+    else if (kv_fmt == KV_E4M3) LAUNCH(128, KV_E4M3);
+    else LAUNCH(128, KV_E5M2);
+  } else {
+    if (kv_fmt == KV_BF16) LAUNCH(64, KV_BF16);
+    else if (kv_fmt == KV_E4M3) LAUNCH(64, KV_E4M3);
+    else LAUNCH(64, KV_E5M2);
+  }
 #undef LAUNCH
   OME_CHECK_LAUNCH();
   return 0;
 }
 
 OME_API int ome_kv_cache_write(const void* k, const void* v, int64_t kv_stride, void* k_cache, void* v_cache,
-                               const int* slots, int T, int Hkv, int D, int P, hipStream_t stream) {
+                               const int* slots, int T, int Hkv, int D, int P, int kv_fmt, float k_scale,
+                               float v_scale, hipStream_t stream) {
   if (T <= 0) return 0;
-  if (D == 128 && P == 16)
-    kv_cache_write_kernel<128, 16><<<T, 128, 0, stream>>>((const bf16*)k, (const bf16*)v, kv_stride,
-                                                          (bf16*)k_cache, (bf16*)v_cache, slots, Hkv);
-  else if (D == 64 && P == 16)
-    kv_cache_write_kernel<64, 16><<<T, 128, 0, stream>>>((const bf16*)k, (const bf16*)v, kv_stride,
-                                                         (bf16*)k_cache, (bf16*)v_cache, slots, Hkv);
-  else
-    return -4;
+  if ((D != 128 && D != 64) || P != 16) return -4;
+  if (kv_fmt < 0 || kv_fmt > 2) return -5;
+  const float ki = 1.f / k_scale, vi = 1.f / v_scale;
+#define LAUNCH(DD, FF)                                                                                    \
+  kv_cache_write_kernel<DD, 16, FF><<<T, 128, 0, stream>>>((const bf16*)k, (const bf16*)v, kv_stride,   \
+                                                           (KVStore<FF>::T*)k_cache,                     \
+                                                           (KVStore<FF>::T*)v_cache, slots, Hkv, ki, vi)
+  if (D == 128) {
+    if (kv_fmt == KV_BF16) LAUNCH(128, KV_BF16);
+    else if (kv_fmt == KV_E4M3) LAUNCH(128, KV_E4M3);
+    else LAUNCH(128, KV_E5M2);
+  } else {
+    if (kv_fmt == KV_BF16) LAUNCH(64, KV_BF16);
+    else if (kv_fmt == KV_E4M3) LAUNCH(64, KV_E4M3);
+    else LAUNCH(64, KV_E5M2);
+  }
+#undef LAUNCH
   OME_CHECK_LAUNCH();
   return 0;
 }

@@ -45,9 +45,24 @@ class AttnMeta:
         return self.positions.shape[0]
 
 
-class PagedKVCache:
-    """Per-layer paged K/V tensors: K ``[pages, Hkv, P, D]``, V ``[pages, Hkv, D, P]`` (bf16).
+#: ``--kv-cache-dtype`` values (SGLang / vLLM spelling) -> cache element dtype (None = model dtype)
+KV_CACHE_DTYPES = {"auto": None, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
+                   "fp8": torch.float8_e4m3fn, "fp8_e4m3": torch.float8_e4m3fn, "fp8_e5m2": torch.float8_e5m2}
 
+
+def kv_cache_dtype(name: str | None, model_dtype=torch.bfloat16):
+    key = (name or "auto").lower()
+    if key not in KV_CACHE_DTYPES:
+        raise ValueError(f"unsupported --kv-cache-dtype {name!r} (choose from {sorted(KV_CACHE_DTYPES)})")
+    return KV_CACHE_DTYPES[key] or model_dtype
+
+
+class PagedKVCache:
+    """Per-layer paged K/V tensors: K ``[pages, Hkv, P, D]``, V ``[pages, Hkv, D, P]``.
+
+    Elements are the model dtype (bf16), or OCP fp8 e4m3 / e5m2 (``--kv-cache-dtype fp8*``, K15)
+    holding ``x / scale`` with one dequantisation scale per layer for K and for V
+    (``k_scale`` / ``v_scale``, 1.0 unless the checkpoint provides them).
     Zero-initialised so that masked (never-written) slots can never inject NaN/Inf into the
     P*V product of the attention kernels.
     """
@@ -66,6 +81,21 @@ class PagedKVCache:
                   if i in own else None for i in range(num_layers)]
         self.v = [torch.zeros(num_pages, num_kv_heads, self.v_dim, page_size, dtype=dtype, device=device)
                   if i in own else None for i in range(num_layers)]
+        self.k_scale = [1.0] * num_layers
+        self.v_scale = [1.0] * num_layers
+
+    @property
+    def is_fp8(self) -> bool:
+        return self.dtype in (torch.float8_e4m3fn, torch.float8_e5m2)
+
+    def scales(self, i: int) -> tuple[float, float]:
+        return self.k_scale[i], self.v_scale[i]
+
+    def set_scales(self, scales: dict[int, tuple[float, float]]) -> None:
+        """Per-layer (k_scale, v_scale) from a checkpoint (``*.k_scale`` / ``*.v_scale``)."""
+        for i, (ks, vs) in scales.items():
+            if 0 <= i < self.num_layers:
+                self.k_scale[i], self.v_scale[i] = float(ks), float(vs)
 
     @staticmethod
     def bytes_per_page(num_layers: int, num_kv_heads: int, head_dim: int, page_size: int, dtype=torch.bfloat16,

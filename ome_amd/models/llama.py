@@ -66,6 +66,7 @@ class LlamaForCausalLM:
         # per-layer lists stay indexed by the global layer id (other stages' entries are None)
         self.layers = pstate.stage_layers(L, st.pp_size, st.pp_rank)
         self._layer_set = set(self.layers)
+        self.kv_scales: dict[int, tuple[float, float]] = {}  # checkpoint fp8 KV scales per layer
         self.w_qkv: list[torch.Tensor] = [None] * L
         self.b_qkv: list[torch.Tensor | None] = [None] * L
         self.w_o: list[torch.Tensor] = [None] * L
@@ -193,6 +194,12 @@ class LlamaForCausalLM:
                 self.qn[i] = put(w)
             elif rest == "self_attn.k_norm.weight":
                 self.kn[i] = put(w)
+            elif rest.endswith((".k_scale", ".v_scale")) and rest.startswith("self_attn."):
+                # fp8 KV-cache scales (``self_attn.k_scale`` / ``self_attn.attn.k_scale`` /
+                # ``self_attn.k_proj.k_scale`` spellings), consumed by --kv-cache-dtype fp8
+                ks, vs = self.kv_scales.get(i, (1.0, 1.0))
+                val = float(w.float().max())
+                self.kv_scales[i] = (val, vs) if rest.endswith(".k_scale") else (ks, val)
         for i, p in qkv_parts.items():
             self.w_qkv[i] = put(torch.cat([p["qt"], p["kt"], p["vt"]], 0))
             if "qs" in p:
@@ -227,20 +234,22 @@ class LlamaForCausalLM:
         return n
 
     # ------------------------------------------------------------------ forward
-    def attention(self, q: torch.Tensor, k_cache, v_cache, meta: AttnMeta) -> torch.Tensor:
+    def attention(self, q: torch.Tensor, k_cache, v_cache, meta: AttnMeta, ks: float = 1.0,
+                  vs: float = 1.0) -> torch.Tensor:
+        """``ks`` / ``vs``: the layer's fp8 KV dequantisation scales (1 for a bf16 cache)."""
         if meta.is_decode:
             return ops.paged_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale,
-                                    meta.decode_ws, self.window, order=meta.order)
+                                    meta.decode_ws, self.window, order=meta.order, k_scale=ks, v_scale=vs)
         if meta.mode == "mixed":
             n = meta.num_prefill
             out = torch.empty_like(q)
             ops.paged_prefill(q[:n], k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
-                              self.scale, self.window, out=out[:n])
+                              self.scale, self.window, out=out[:n], k_scale=ks, v_scale=vs)
             ops.paged_decode(q[n:], k_cache, v_cache, meta.dec_block_tables, meta.seq_lens, self.scale,
-                             meta.decode_ws, self.window, out=out[n:], order=meta.order)
+                             meta.decode_ws, self.window, out=out[n:], order=meta.order, k_scale=ks, v_scale=vs)
             return out
         return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
-                                 self.scale, self.window)
+                                 self.scale, self.window, k_scale=ks, v_scale=vs)
 
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
         gu = linear(x, self.w_gu[i])
@@ -259,9 +268,10 @@ class LlamaForCausalLM:
             qkv = linear(x, self.w_qkv[i], self.b_qkv[i])
             q = torch.empty(T, tp.hq, D, dtype=self.dtype, device=x.device)
             k_cache, v_cache = kv.layer(i)
+            ks, vs = kv.scales(i)
             ops.rope_qkv_cache(qkv, meta.positions, self.cos_sin, cfg.rot_dim, q, k_cache, v_cache, meta.slots,
-                               tp.hq, tp.hkv, D, True, self.qn[i], self.kn[i], self.eps)
-            attn = self.attention(q, k_cache, v_cache, meta)
+                               tp.hq, tp.hkv, D, True, self.qn[i], self.kn[i], self.eps, ks, vs)
+            attn = self.attention(q, k_cache, v_cache, meta, ks, vs)
             o = pstate.tp_all_reduce(linear(attn.view(T, tp.hq * D), self.w_o[i]))
             ops.fused_add_rmsnorm(o, residual, self.ln2[i], self.eps)
             x = self.mlp(i, o)

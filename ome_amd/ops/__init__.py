@@ -45,25 +45,38 @@ def fused_add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: 
          x2.shape[0], H, float(eps), stream_ptr())
 
 
+#: paged KV-cache element formats understood by the kernels (csrc/kernels/common.h KVFmt)
+KV_FORMATS = {torch.bfloat16: 0, torch.float8_e4m3fn: 1, torch.float8_e5m2: 2}
+
+
+def kv_format(cache: torch.Tensor) -> int:
+    f = KV_FORMATS.get(cache.dtype)
+    if f is None:
+        raise TypeError(f"unsupported KV-cache dtype {cache.dtype} (bf16 / float8_e4m3fn / float8_e5m2)")
+    return f
+
+
 def rope_qkv_cache(qkv, positions, cos_sin, rot_dim, q_out, k_cache, v_cache, slots, Hq, Hkv, D, apply_rope=True,
-                   q_norm_w=None, k_norm_w=None, qk_eps=1e-6) -> None:
+                   q_norm_w=None, k_norm_w=None, qk_eps=1e-6, k_scale: float = 1.0, v_scale: float = 1.0) -> None:
+    """``k_scale`` / ``v_scale``: dequantisation scales of an fp8 cache (entries hold x / scale)."""
     P = k_cache.shape[2]
     if not _gpu(qkv):
         return ref.rope_qkv_cache(qkv, positions, cos_sin, rot_dim, q_out, k_cache, v_cache, slots, Hq, Hkv, D, P,
-                                  apply_rope, q_norm_w, k_norm_w, qk_eps)
+                                  apply_rope, q_norm_w, k_norm_w, qk_eps, k_scale, v_scale)
     call("ome_rope_qkv_cache", qkv.data_ptr(), qkv.stride(0), _i32(positions).data_ptr(), cos_sin.data_ptr(),
          rot_dim, q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(), _i32(slots).data_ptr(), qkv.shape[0], Hq,
-         Hkv, D, P, int(apply_rope), ptr(q_norm_w), ptr(k_norm_w), float(qk_eps), stream_ptr())
+         Hkv, D, P, int(apply_rope), ptr(q_norm_w), ptr(k_norm_w), float(qk_eps), kv_format(k_cache),
+         float(k_scale), float(v_scale), stream_ptr())
 
 
-def kv_cache_write(k, v, k_cache, v_cache, slots) -> None:
+def kv_cache_write(k, v, k_cache, v_cache, slots, k_scale: float = 1.0, v_scale: float = 1.0) -> None:
     P = k_cache.shape[2]
     if not _gpu(k):
-        return ref.kv_cache_write(k, v, k_cache, v_cache, slots, P)
+        return ref.kv_cache_write(k, v, k_cache, v_cache, slots, P, k_scale, v_scale)
     T, Hkv, D = k.shape
     assert k.stride() == v.stride()
     call("ome_kv_cache_write", k.data_ptr(), v.data_ptr(), k.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
-         _i32(slots).data_ptr(), T, Hkv, D, P, stream_ptr())
+         _i32(slots).data_ptr(), T, Hkv, D, P, kv_format(k_cache), float(k_scale), float(v_scale), stream_ptr())
 
 
 def act_and_mul(x: torch.Tensor, act: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -228,11 +241,13 @@ class DecodeWorkspace:
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeWorkspace | None = None,
-                 window: int = -1, out=None, order: torch.Tensor | None = None) -> torch.Tensor:
+                 window: int = -1, out=None, order: torch.Tensor | None = None, k_scale: float = 1.0,
+                 v_scale: float = 1.0) -> torch.Tensor:
     """q [B, Hq, D] -> [B, Hq, D].  ``order`` (int32 [B], optional): sequence visit order for the
-    workgroup dispatcher (longest first balances the tail)."""
+    workgroup dispatcher (longest first balances the tail).  The cache may be bf16 or fp8
+    (``k_scale`` / ``v_scale`` dequantise it)."""
     if not _gpu(q):
-        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window)
+        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window, k_scale, v_scale)
         if out is not None:
             out.copy_(r)
             return out
@@ -245,7 +260,8 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeW
     call("ome_paged_decode", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(seq_lens).data_ptr(), out.data_ptr(),
          out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
-         float(scale), int(window), _i32(order).data_ptr() if order is not None else None, stream_ptr())
+         float(scale), int(window), _i32(order).data_ptr() if order is not None else None, kv_format(k_cache),
+         float(k_scale), float(v_scale), stream_ptr())
     return out
 
 
@@ -304,10 +320,10 @@ def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) ->
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale, window: int = -1,
-                  out=None) -> torch.Tensor:
+                  out=None, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
     """q [Tq, Hq, D]; items int32 [n, 2] from :func:`prefill_work_items`."""
     if not _gpu(q):
-        r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window)
+        r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window, k_scale, v_scale)
         if out is not None:
             out.copy_(r)
             return out
@@ -318,7 +334,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     call("ome_paged_prefill", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
          _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),
-         int(window), stream_ptr())
+         int(window), kv_format(k_cache), float(k_scale), float(v_scale), stream_ptr())
     return out
 
 

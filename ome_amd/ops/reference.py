@@ -34,8 +34,20 @@ def apply_rope(x: torch.Tensor, cs: torch.Tensor, rot_dim: int) -> torch.Tensor:
     return out
 
 
+#: finite range of the fp8 KV-cache formats (values are saturated, never NaN)
+FP8_RANGE = {torch.float8_e4m3fn: 448.0, torch.float8_e5m2: 57344.0}
+
+
+def to_cache(x: torch.Tensor, dtype, scale: float = 1.0) -> torch.Tensor:
+    """Cache entry for ``x``: bf16 as-is, fp8 = saturate(bf16(x) / scale) (round to nearest even)."""
+    if dtype not in FP8_RANGE:
+        return x.to(dtype)
+    m = FP8_RANGE[dtype]
+    return (x.to(torch.bfloat16).float() / scale).clamp(-m, m).to(dtype)
+
+
 def rope_qkv_cache(qkv, positions, cos_sin, rot_dim, q_out, k_cache, v_cache, slots, Hq, Hkv, D, P, apply=True,
-                   q_norm_w=None, k_norm_w=None, qk_eps=1e-6) -> None:
+                   q_norm_w=None, k_norm_w=None, qk_eps=1e-6, k_scale=1.0, v_scale=1.0) -> None:
     T = qkv.shape[0]
     if T == 0:
         return
@@ -51,18 +63,19 @@ def rope_qkv_cache(qkv, positions, cos_sin, rot_dim, q_out, k_cache, v_cache, sl
         q = apply_rope(q, cs, rot_dim)
         k = apply_rope(k, cs, rot_dim)
     q_out.view(T, Hq, D).copy_(q.to(q_out.dtype))
-    kv_cache_write(k.to(k_cache.dtype), v, k_cache, v_cache, slots, P)
+    kdt = k_cache.dtype if k_cache.dtype not in FP8_RANGE else torch.bfloat16
+    kv_cache_write(k.to(kdt), v, k_cache, v_cache, slots, P, k_scale, v_scale)
 
 
-def kv_cache_write(k, v, k_cache, v_cache, slots, P) -> None:
+def kv_cache_write(k, v, k_cache, v_cache, slots, P, k_scale=1.0, v_scale=1.0) -> None:
     sl = slots.long()
     ok = sl >= 0
     if not bool(ok.any()):
         return
     sl, k, v = sl[ok], k[ok], v[ok]
     page, off = sl // P, sl % P
-    k_cache[page, :, off, :] = k.to(k_cache.dtype)
-    v_cache[page, :, :, off] = v.to(v_cache.dtype)
+    k_cache[page, :, off, :] = to_cache(k, k_cache.dtype, k_scale)
+    v_cache[page, :, :, off] = to_cache(v, v_cache.dtype, v_scale)
 
 
 def act_and_mul(x: torch.Tensor, act: int = 0) -> torch.Tensor:
@@ -80,17 +93,18 @@ def embedding(ids: torch.Tensor, table: torch.Tensor, vocab_start: int = 0, voca
     return out * own[:, None].to(out.dtype)
 
 
-def gather_kv(k_cache, v_cache, block_table, n: int, kvh: int, P: int):
-    """Contiguous K [n, D] and V [n, D] for one sequence / kv head."""
+def gather_kv(k_cache, v_cache, block_table, n: int, kvh: int, P: int, k_scale=1.0, v_scale=1.0):
+    """Contiguous (dequantised) K [n, D] and V [n, D] for one sequence / kv head."""
     idx = torch.arange(n, device=k_cache.device)
     pages = block_table[(idx // P).long()].long()
     off = idx % P
     k = k_cache[pages, kvh, off, :]
     v = v_cache[pages, kvh, :, off]
-    return k.float(), v.float()
+    return k.float() * k_scale, v.float() * v_scale
 
 
-def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1) -> torch.Tensor:
+def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, k_scale=1.0,
+                 v_scale=1.0) -> torch.Tensor:
     B, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -101,7 +115,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1) 
             continue
         lo = max(0, L - window) if window > 0 else 0
         for h in range(Hkv):
-            k, v = gather_kv(k_cache, v_cache, block_tables[b], L, h, P)
+            k, v = gather_kv(k_cache, v_cache, block_tables[b], L, h, P, k_scale, v_scale)
             k, v = k[lo:], v[lo:]
             qh = q[b, h * G:(h + 1) * G].float()
             s = (qh @ k.T) * scale
@@ -109,7 +123,8 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1) 
     return out
 
 
-def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window=-1) -> torch.Tensor:
+def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window=-1, k_scale=1.0,
+                  v_scale=1.0) -> torch.Tensor:
     Tq, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -126,7 +141,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, windo
         if window > 0:
             mask &= kpos > qpos - window
         for h in range(Hkv):
-            k, v = gather_kv(k_cache, v_cache, block_tables[s], L, h, P)
+            k, v = gather_kv(k_cache, v_cache, block_tables[s], L, h, P, k_scale, v_scale)
             qh = q[q0:q1, h * G:(h + 1) * G].float().transpose(0, 1)  # [G, ql, D]
             sc = (qh @ k.T) * scale
             sc = sc.masked_fill(~mask[None], float("-inf"))

@@ -124,7 +124,8 @@ class KVTransfer:
         kv, P = runner.kv, runner.P
         L = int(header["n_tokens"])
         k0 = kv.k[kv.local_layers[0]]
-        if list(header["shape_k"][1:]) != list(k0.shape[1:]) or int(header["layers"]) != len(kv.local_layers):
+        if list(header["shape_k"][1:]) != list(k0.shape[1:]) or int(header["layers"]) != len(kv.local_layers) \
+                or header.get("dtype", str(kv.dtype)) != str(kv.dtype):
             req.state, req.finish_reason = ReqState.FINISHED, "abort:kv_layout_mismatch"
             if req.on_token:
                 req.on_token(req, [], True)

@@ -102,7 +102,8 @@ class Engine:
                                   page_size=args.page_size, mem_fraction_static=args.mem_fraction_static,
                                   max_total_tokens=args.max_total_tokens, max_running=args.max_running_requests,
                                   max_context=self.max_context, cuda_graph=args.cuda_graph and not self.dp,
-                                  cuda_graph_max_bs=args.cuda_graph_max_bs, seed=args.seed)
+                                  cuda_graph_max_bs=args.cuda_graph_max_bs, seed=args.seed,
+                                  kv_cache_dtype_name=args.kv_cache_dtype)
         prefix = None
         if not args.disable_radix_cache:
             from ome_amd.runtime.prefix_cache import PrefixCache

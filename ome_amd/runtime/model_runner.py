@@ -20,7 +20,7 @@ import torch
 
 from ome_amd import ops
 from ome_amd.models import build_model
-from ome_amd.models.common import AttnMeta, PagedKVCache
+from ome_amd.models.common import AttnMeta, PagedKVCache, kv_cache_dtype
 from ome_amd.models.config import ModelConfig
 from ome_amd.parallel import state as pstate
 from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
@@ -92,7 +92,7 @@ class ModelRunner:
                  model_path: str | None = None, load_format: str = "auto", page_size: int = 16,
                  mem_fraction_static: float = 0.9, max_total_tokens: int | None = None, max_running: int = 256,
                  max_context: int = 8192, cuda_graph: bool = True, cuda_graph_max_bs: int | None = None,
-                 seed: int = 0, kv_cache_dtype: str = "auto"):
+                 seed: int = 0, kv_cache_dtype_name: str = "auto"):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -108,7 +108,14 @@ class ModelRunner:
         tp = self.model.tp
         kv_heads, k_dim, v_dim = getattr(self.model, "kv_layout", (tp.hkv, cfg.head_dim, cfg.head_dim))
         n_local = len(self.model.layers)
-        page_bytes = PagedKVCache.bytes_per_page(n_local, kv_heads, k_dim, page_size, dtype, v_dim)
+        kv_dtype = kv_cache_dtype(kv_cache_dtype_name, dtype)
+        if kv_dtype != dtype and getattr(self.model, "kv_layout", None) is not None:
+            # MLA's latent cache (mla.hip) keeps the model dtype
+            log.warning("--kv-cache-dtype %s is not supported by the MLA latent cache; using %s",
+                        kv_cache_dtype_name, dtype)
+            kv_dtype = dtype
+        self.kv_dtype = kv_dtype
+        page_bytes = PagedKVCache.bytes_per_page(n_local, kv_heads, k_dim, page_size, kv_dtype, v_dim)
         if self.is_cuda:
             free, total = torch.cuda.mem_get_info(self.device)
             used_by_others = total - free
@@ -121,8 +128,10 @@ class ModelRunner:
         if max_total_tokens:
             want = min(want, -(-max_total_tokens // page_size) + 2)
         num_pages = max(min(num_pages, want), max_pages_per_seq + 2)
-        self.kv = PagedKVCache(cfg.num_layers, num_pages, kv_heads, k_dim, page_size, dtype, self.device, v_dim,
+        self.kv = PagedKVCache(cfg.num_layers, num_pages, kv_heads, k_dim, page_size, kv_dtype, self.device, v_dim,
                                layers=self.model.layers)
+        if self.kv.is_fp8:
+            self.kv.set_scales(getattr(self.model, "kv_scales", None) or {})
         self.pp = pstate.get().pp_size > 1
         self.pages = PagePool(num_pages)
         self.slots = ReqSlotPool(max_running + 1, max_pages_per_seq, self.device)
