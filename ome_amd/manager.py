@@ -291,6 +291,11 @@ def create_api(cluster: Cluster):
     async def g_sub(request: Request, group: str, version: str, plural: str, name: str, sub: str):
         return await handle(request, group, version, None, plural, name, sub)
 
+    # web console (H8): dashboard at /console/, its REST API at /console/api/v1
+    from ome_amd.console import mount as mount_console
+
+    mount_console(app, st, models_root=getattr(cluster.agent, "models_root", None))
+
     @app.post("/apply")
     async def apply(request: Request):
         try:
