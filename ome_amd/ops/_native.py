@@ -55,6 +55,11 @@ _SIGNATURES = {
         "ome_comm_all_reduce": [vp, vp, vp, i64, i32, i32, vp],
         "ome_comm_error": [vp],
         "ome_comm_destroy": [vp],
+        "ome_kvlink_export": [vp, vp, C.POINTER(i64)],
+        "ome_kvlink_handle_size": [],
+        "ome_kvlink_open": [vp, C.POINTER(vp)],
+        "ome_kvlink_close": [vp],
+        "ome_kvlink_copy": [vp, vp, vp, vp, i32, i32, i64, i64, vp],
     },
 }
 

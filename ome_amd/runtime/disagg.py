@@ -16,10 +16,17 @@ page images in the cache's own MFMA layouts (K ``[pages, Hkv, P, D]``, V ``[page
 so neither side reformats; on the decode side the bytes land in one pinned buffer and are
 uploaded with a single H2D copy, then scattered with ``index_copy_`` per layer.  Arrival order
 does not matter: KV that arrives before its request waits in the inbox, and vice versa.
+
+Same-node fast path (``OMEKV2``, :mod:`ome_amd.runtime.kvlink`): when both engines sit on one
+MI355X node the prefill engine asks the receiver for landing slots, maps the decode engine's
+exported landing pool once (hipIpc), writes the pages over xGMI from its own GPU, then sends a
+small DONE record; the decode engine copies landing slots into its cache pages on device.  No
+host bounce; the TCP blob path stays as the fallback for other nodes / CPU engines.
 """
 from __future__ import annotations
 
 import json
+import os
 import logging
 import socket
 import struct
@@ -32,6 +39,17 @@ import torch
 log = logging.getLogger("ome_amd.disagg")
 
 MAGIC = b"OMEKV1\0\0"
+MAGIC2 = b"OMEKV2\0\0"   # same-node IPC handshake: RESERVE -> (slots, handles) -> DONE
+
+
+def _send_msg(sock: socket.socket, obj: dict) -> None:
+    b = json.dumps(obj).encode()
+    sock.sendall(struct.pack("<I", len(b)) + b)
+
+
+def _recv_msg(sock: socket.socket) -> dict:
+    (n,) = struct.unpack("<I", _recv_exact(sock, 4))
+    return json.loads(_recv_exact(sock, n))
 
 
 def _recv_exact(sock: socket.socket, n: int) -> bytes:
@@ -58,6 +76,22 @@ class KVTransfer:
         self.sent = 0
         self.received = 0
         self._sock = None
+        self.host = socket.gethostname()
+        self.landing = None        # decode side: kvlink.LandingPool (same-node IPC fast path)
+        self.peers: dict = {}      # prefill side: (host, port) -> kvlink.PeerMapping
+        self.ipc_sent = 0
+        self.ipc_received = 0
+        runner = engine.runner
+        use_ipc = os.environ.get("OME_PD_IPC", "1") == "1"
+        if mode == "decode" and use_ipc:
+            from ome_amd.runtime import kvlink
+
+            if kvlink.available(runner.device):
+                try:
+                    toks = int(os.environ.get("OME_PD_LANDING_TOKENS", str(min(65536, 4 * engine.max_context))))
+                    self.landing = kvlink.LandingPool(runner.kv, max(1, toks // runner.P))
+                except Exception as e:  # noqa: BLE001 — no IPC export: TCP path only
+                    log.warning("PD landing pool unavailable (%s); using the TCP path", e)
         if mode == "decode":
             self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
@@ -80,7 +114,10 @@ class KVTransfer:
     def _recv_one(self, conn: socket.socket) -> None:
         try:
             with conn:
-                if _recv_exact(conn, 8) != MAGIC:
+                magic = _recv_exact(conn, 8)
+                if magic == MAGIC2:
+                    return self._recv_ipc(conn)
+                if magic != MAGIC:
                     raise ConnectionError("bad KV transfer magic")
                 (hl,) = struct.unpack("<I", _recv_exact(conn, 4))
                 header = json.loads(_recv_exact(conn, hl))
@@ -92,6 +129,35 @@ class KVTransfer:
             self.engine._wake.set()
         except Exception as e:  # noqa: BLE001
             log.warning("KV receive failed: %s", e)
+
+    def _recv_ipc(self, conn: socket.socket) -> None:
+        """Same-node handshake: RESERVE {room, n_pages, host, dtype} -> {ok, slots, pool} ->
+        the prefill GPU writes the pages -> DONE {header}."""
+        req = _recv_msg(conn)
+        lp = self.landing
+        if lp is None or req.get("host") != self.host or req.get("dtype") != str(lp.kv.dtype):
+            _send_msg(conn, {"ok": False, "ipc": False})
+            return
+        slots = lp.reserve(int(req["n_pages"]))
+        if slots is None:
+            _send_msg(conn, {"ok": False, "ipc": True, "retry": True})
+            return
+        _send_msg(conn, {"ok": True, "slots": slots,
+                         "pool": lp.describe() if req.get("session") != lp.session else {"session": lp.session}})
+        try:
+            done = _recv_msg(conn)
+            if not done.get("ok"):
+                raise ConnectionError(done.get("error", "sender aborted"))
+            conn.sendall(b"OK")
+        except Exception:
+            lp.release(slots)
+            raise
+        header = done["header"]
+        with self.lock:
+            self.inbox[int(header["room"])] = (header, ("ipc", slots))
+        self.received += 1
+        self.ipc_received += 1
+        self.engine._wake.set()
 
     def hold(self, req) -> None:
         """Decode engine: park a request until its KV arrives (called from the engine thread)."""
@@ -142,6 +208,12 @@ class KVTransfer:
         req.pages = list(pages)
         sch.slots.set_pages(req.req_slot, 0, pages)
         sch.slots.flush()
+        if isinstance(payload, tuple) and payload[0] == "ipc":
+            self.landing.install(payload[1][:n_pages], pages)
+            if runner.is_cuda:
+                torch.cuda.current_stream(runner.device).synchronize()
+            self.landing.release(payload[1])
+            return self._activate(req, header)
         src = torch.frombuffer(bytearray(payload), dtype=torch.uint8)
         if runner.is_cuda:
             src = src.pin_memory().to(runner.device, non_blocking=True)
@@ -156,6 +228,14 @@ class KVTransfer:
             o += vbytes
             kv.k[i].index_copy_(0, idx, kk)
             kv.v[i].index_copy_(0, idx, vv)
+        return self._activate(req, header)
+
+    def _activate(self, req, header: dict) -> bool:
+        from ome_amd.runtime.request import ReqState
+
+        eng = self.engine
+        sch = eng.scheduler
+        L = int(header["n_tokens"])
         now = time.perf_counter()
         req.output_ids.append(int(header["first_token"]))
         req.output_logprobs.append(float(header.get("first_logprob", 0.0)))
@@ -175,7 +255,9 @@ class KVTransfer:
     # ------------------------------------------------------------------ prefill side
     def _on_prefill_finish(self, req) -> None:
         """Scheduler hook (before the pages are released): snapshot the prompt's KV pages and
-        push them to the decode engine in the background."""
+        push them to the decode engine in the background.  On a GPU the snapshot is an on-device
+        copy (the pages are free for reuse right after this hook); the same-node IPC path then
+        writes it into the decode GPU over xGMI, the TCP path ships it through the host."""
         b = req.bootstrap or {}
         if b.get("disagg_role") != "prefill" or not req.output_ids or req.finish_reason and \
                 req.finish_reason.startswith("abort"):
@@ -185,17 +267,82 @@ class KVTransfer:
         L = len(req.prompt_ids)
         pages = req.pages[: -(-L // P)]
         idx = torch.tensor(pages, dtype=torch.long, device=runner.device)
-        parts = []
-        for i in kv.local_layers:
-            parts.append(kv.k[i].index_select(0, idx).reshape(-1).view(torch.uint8))
-            parts.append(kv.v[i].index_select(0, idx).reshape(-1).view(torch.uint8))
-        blob = torch.cat(parts).cpu().numpy().tobytes()
+        ks = [kv.k[i].index_select(0, idx) for i in kv.local_layers]
+        vs = [kv.v[i].index_select(0, idx) for i in kv.local_layers]
+        event = None
+        if runner.is_cuda:
+            event = torch.cuda.Event()
+            event.record(torch.cuda.current_stream(runner.device))
         header = {"room": int(b["bootstrap_room"]), "n_tokens": L, "first_token": int(req.output_ids[0]),
                   "first_logprob": float(req.output_logprobs[0]) if req.output_logprobs else 0.0,
                   "layers": len(kv.local_layers), "shape_k": [len(pages), *kv.k[kv.local_layers[0]].shape[1:]],
-                  "shape_v": [len(pages), *kv.v[kv.local_layers[0]].shape[1:]], "dtype": str(kv.dtype), "nbytes": len(blob)}
+                  "shape_v": [len(pages), *kv.v[kv.local_layers[0]].shape[1:]], "dtype": str(kv.dtype)}
         host, port = b.get("bootstrap_host") or "127.0.0.1", int(b["bootstrap_port"]) + self.rank
-        threading.Thread(target=self._send, args=(host, port, header, blob), daemon=True).start()
+        threading.Thread(target=self._push, args=(host, port, header, ks, vs, event), daemon=True).start()
+
+    def _push(self, host: str, port: int, header: dict, ks: list, vs: list, event) -> None:
+        runner = self.engine.runner
+        if event is not None:
+            event.synchronize()
+        if runner.is_cuda and os.environ.get("OME_PD_IPC", "1") == "1":
+            try:
+                if self._send_ipc(host, port, header, ks, vs):
+                    return
+            except Exception as e:  # noqa: BLE001 — any IPC trouble: fall back to the TCP blob
+                log.warning("KV IPC push to %s:%d failed (%s); falling back to TCP", host, port, e)
+        parts = []
+        for k, v in zip(ks, vs):
+            parts.append(k.reshape(-1).view(torch.uint8))
+            parts.append(v.reshape(-1).view(torch.uint8))
+        blob = torch.cat(parts).cpu().numpy().tobytes()
+        self._send(host, port, {**header, "nbytes": len(blob)}, blob)
+
+    def _send_ipc(self, host: str, port: int, header: dict, ks: list, vs: list, retries: int = 200) -> bool:
+        """RESERVE -> write pages over xGMI -> DONE.  False = receiver has no IPC path for us."""
+        from ome_amd.executor.dns import resolve_host_port
+        from ome_amd.runtime import kvlink
+
+        rhost, rport = resolve_host_port(host, port)
+        runner = self.engine.runner
+        n = int(header["shape_k"][0])
+        key = (rhost, rport)
+        for attempt in range(retries):
+            peer = self.peers.get(key)
+            with socket.create_connection((rhost, rport), timeout=30) as s:
+                s.sendall(MAGIC2)
+                _send_msg(s, {"room": header["room"], "n_pages": n, "host": self.host, "dtype": header["dtype"],
+                              "session": peer.session if peer else None})
+                rep = _recv_msg(s)
+                if not rep.get("ok"):
+                    if not rep.get("ipc", True):
+                        return False
+                    time.sleep(min(0.05, 0.001 * 2 ** min(attempt, 6)))  # landing pool full: wait
+                    continue
+                pool = rep["pool"]
+                if peer is None or peer.session != pool["session"]:
+                    if peer is not None:
+                        peer.close()
+                    peer = kvlink.PeerMapping(pool, runner.device)
+                    self.peers[key] = peer
+                try:
+                    stream = self._ipc_stream()
+                    peer.write(ks, vs, rep["slots"], stream)
+                except Exception as e:
+                    _send_msg(s, {"ok": False, "error": str(e)})
+                    raise
+                _send_msg(s, {"ok": True, "header": header})
+                if _recv_exact(s, 2) != b"OK":
+                    raise ConnectionError("no ack")
+            self.sent += 1
+            self.ipc_sent += 1
+            return True
+        raise TimeoutError("decode landing pool stayed full")
+
+    def _ipc_stream(self):
+        st = getattr(self, "_stream", None)
+        if st is None:
+            st = self._stream = torch.cuda.Stream(self.engine.runner.device)
+        return st
 
     def _send(self, host: str, port: int, header: dict, blob: bytes, retries: int = 20) -> None:
         from ome_amd.executor.dns import resolve_host_port
