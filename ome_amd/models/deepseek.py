@@ -85,6 +85,9 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         step = max(1, cfg.moe_layer_freq)
         self.moe_layers = {i for i in self.layers if cfg.num_experts and i >= cfg.first_k_dense_replace and
                            i % step == 0}
+        from ome_amd.parallel import eplb
+
+        eplb.attach(self)  # expert slots per rank (+ redundant replicas) under expert parallelism
         self.w_qa: list = [None] * L      # [q_lora + 576, H] fused q_a / kv_a (or [576, H] if no q_lora)
         self.qa_ln: list = [None] * L
         self.w_qb: list = [None] * L      # [Hl * qk_dim, q_lora] (or [Hl * qk_dim, H] = q_proj)
@@ -127,9 +130,9 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 self.w_router[i] = self._alloc(self.E, H, std=std, gen=gen)
                 if self.group_mode == 2:
                     self.b_router[i] = torch.zeros(self.E, dtype=torch.float32, device=self.device)
-                sl = slice(self.e0, self.e0 + self.E_local)
-                self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen)[sl].contiguous()
-                self.w2[i] = self._alloc(self.E, H, I, std=out_std, gen=gen)[sl].contiguous()
+                idx = torch.tensor(self.local_experts(i), dtype=torch.long, device=self.device)
+                self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen).index_select(0, idx).contiguous()
+                self.w2[i] = self._alloc(self.E, H, I, std=out_std, gen=gen).index_select(0, idx).contiguous()
                 if self.shared_inter:
                     self.w_sgu[i] = self._alloc(2 * self.shared_inter, H, std=std, gen=gen)
                     self.w_sd[i] = self._alloc(H, self.shared_inter, std=out_std, gen=gen)
@@ -243,7 +246,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 self.w_sd[i] = put(cols(d["mlp.shared_experts.down_proj.weight"], SI))
         for i, ex in experts.items():
             gs, ds = [], []
-            for e in range(self.e0, self.e0 + self.E_local):
+            for e in self.local_experts(i):
                 de = ex[e]
                 gs.append(torch.cat([rows(de["gate_proj"], I), rows(de["up_proj"], I)], 0))
                 ds.append(cols(de["down_proj"], I))
@@ -257,6 +260,11 @@ class DeepseekForCausalLM(LlamaForCausalLM):
             raise ValueError(f"checkpoint incomplete: layers missing {missing[:4]}")
         self._post_load()
         return self
+
+    def local_experts(self, i: int) -> list[int]:
+        from ome_amd.parallel import eplb
+
+        return eplb.local_experts(self, i)
 
     def weight_bytes(self) -> int:
         from ome_amd.models.quant import Fp8Weight
@@ -343,7 +351,11 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         if self.ep > 1:
             from ome_amd.parallel.ep import moe_ep_forward
 
-            out = moe_ep_forward(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale, self.E)
+            tables = None
+            if self.eplb is not None:
+                self.eplb.record(i, tid)
+                tables = self.eplb.tables[i]
+            out = moe_ep_forward(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale, self.E, tables)
         else:
             out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale)
         if self.w_sgu[i] is not None:

@@ -48,6 +48,9 @@ class MoEForCausalLM(LlamaForCausalLM):
         step = max(1, cfg.moe_layer_freq)
         self.moe_layers = {i for i in self.layers if i >= cfg.first_k_dense_replace and (i + 1) % step == 0} \
             if step > 1 else {i for i in self.layers if i >= cfg.first_k_dense_replace}
+        from ome_amd.parallel import eplb
+
+        eplb.attach(self)  # expert slots per rank (+ redundant replicas) under expert parallelism
 
     def init_random(self, seed: int = 0, std: float = 0.02) -> "MoEForCausalLM":
         super().init_random(seed, std)
@@ -60,9 +63,10 @@ class MoEForCausalLM(LlamaForCausalLM):
                 continue
             self.w_gu[i] = self.w_d[i] = None  # dense MLP replaced by experts
             self.w_router[i] = self._alloc(self.E, H, std=std, gen=gen)
-            self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen)[self.e0:self.e0 + self.E_local].contiguous()
+            idx = torch.tensor(self.local_experts(i), dtype=torch.long, device=self.device)
+            self.w13[i] = self._alloc(self.E, 2 * I, H, std=std, gen=gen).index_select(0, idx).contiguous()
             self.w2[i] = self._alloc(self.E, H, I, std=std / math.sqrt(2 * cfg.num_layers),
-                                     gen=gen)[self.e0:self.e0 + self.E_local].contiguous()
+                                     gen=gen).index_select(0, idx).contiguous()
             if self.shared_inter:
                 self.w_sgu[i] = self._alloc(2 * self.shared_inter, H, std=std, gen=gen)
                 self.w_sd[i] = self._alloc(H, self.shared_inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
@@ -112,7 +116,7 @@ class MoEForCausalLM(LlamaForCausalLM):
         self._load_base(rest_iter)
         for i, ex in experts.items():
             gs, ds = [], []
-            for e in range(self.e0, self.e0 + self.E_local):
+            for e in self.local_experts(i):
                 d = ex[e]
                 g = d.get("w1", d.get("gate_proj"))
                 u = d.get("w3", d.get("up_proj"))
@@ -140,6 +144,11 @@ class MoEForCausalLM(LlamaForCausalLM):
             if self.w_gu[i] is placeholder:
                 self.w_gu[i] = saved[i]
 
+    def local_experts(self, i: int) -> list[int]:
+        from ome_amd.parallel import eplb
+
+        return eplb.local_experts(self, i)
+
     def weight_bytes(self) -> int:
         n = super().weight_bytes()
         for lst in (self.w_router, self.w13, self.w2, self.w_sgu, self.w_sd, self.w_sgate):
@@ -154,7 +163,11 @@ class MoEForCausalLM(LlamaForCausalLM):
         if self.ep > 1:
             from ome_amd.parallel.ep import moe_ep_forward
 
-            out = moe_ep_forward(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E)
+            tables = None
+            if self.eplb is not None:
+                self.eplb.record(i, tid)
+                tables = self.eplb.tables[i]
+            out = moe_ep_forward(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E, tables)
         else:
             out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act)
         if self.w_sgu[i] is not None:

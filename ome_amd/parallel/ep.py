@@ -52,16 +52,27 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: list[int], in_splits:
 
 
 def moe_ep_forward(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13_local: torch.Tensor,
-                   w2_local: torch.Tensor, act: int, scale: float, num_experts: int) -> torch.Tensor:
-    """x [T, H] (this rank's tokens), routing [T, k] over the global experts; w13/w2 hold this
-    rank's ``E / ep`` experts.  Returns the routed-expert output [T, H] (no shared expert)."""
+                   w2_local: torch.Tensor, act: int, scale: float, num_experts: int,
+                   tables: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+    """x [T, H] (this rank's tokens), routing [T, k] over the global (logical) experts; w13/w2
+    hold this rank's expert slots.  Without ``tables`` rank r owns experts [r*E/ep, (r+1)*E/ep);
+    with EPLB tables (``ome_amd.parallel.eplb``: rep_rank / rep_slot [E, Rmax], n_rep [E]) each
+    (token, k-slot) assignment goes to replica ``(t*k + j) mod n_rep[e]`` of its expert, which
+    spreads a replicated hot expert's rows evenly over its copies.  Returns [T, H]."""
     st = pstate.get()
     group, ep, me = st.ep_group, st.ep_size, st.ep_rank
     T, H = x.shape
     k = topk_ids.shape[1]
-    e_local = num_experts // ep
     flat_ids = topk_ids.reshape(-1).long()
-    owner = flat_ids // e_local
+    if tables is None:
+        e_local = num_experts // ep
+        owner = flat_ids // e_local
+        local_slot = flat_ids - owner * e_local
+    else:
+        rep_rank, rep_slot, n_rep = tables
+        j = torch.arange(flat_ids.shape[0], device=flat_ids.device) % n_rep.index_select(0, flat_ids)
+        owner = rep_rank[flat_ids, j]
+        local_slot = rep_slot[flat_ids, j]
     order = torch.argsort(owner, stable=True)
     send_counts = torch.bincount(owner, minlength=ep)
     recv_counts = torch.empty_like(send_counts)
@@ -69,7 +80,7 @@ def moe_ep_forward(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor
     sc, rc = send_counts.tolist(), recv_counts.tolist()
     tok = order // k
     send_x = x.index_select(0, tok)
-    send_e = (flat_ids.index_select(0, order) - owner.index_select(0, order) * e_local).to(torch.int32)
+    send_e = local_slot.index_select(0, order).to(torch.int32)
     R = sum(rc)
     recv_x = x.new_empty(R, H)
     recv_e = torch.empty(R, dtype=torch.int32, device=x.device)

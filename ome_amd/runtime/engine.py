@@ -55,6 +55,8 @@ class EngineArgs:
     node_rank: int = 0
     disaggregation_mode: str = "null"      # null | prefill | decode
     enable_dp_attention: bool = False      # --dp N --enable-dp-attention: per-rank batches + EP MoE
+    ep_num_redundant_experts: int = 0      # EPLB: extra expert slots (replicas of hot experts) over the EP ranks
+    eplb_rebalance_steps: int = 0          # EPLB: re-place experts from recorded loads every N lockstep steps
     overlap_schedule: bool | None = None   # enqueue step k+1 before step k's tokens reach the host
                                            # (None = on for GPU engines)
     num_layers_override: int | None = None
@@ -71,6 +73,8 @@ class EngineArgs:
             cfg.is_embedding = True
         if self.quantization:
             cfg.quantization = self.quantization
+        if self.ep_num_redundant_experts:
+            cfg.extra = {**(cfg.extra or {}), "ep_num_redundant_experts": int(self.ep_num_redundant_experts)}
         return cfg
 
 
@@ -319,6 +323,14 @@ class Engine:
                         done.append(p)
                     if p.on_token is not None and (toks or fin):
                         p.on_token(p, list(toks), fin)
+        self._dp_steps = getattr(self, "_dp_steps", 0) + 1
+        n = self.args.eplb_rebalance_steps
+        if n and self._dp_steps % n == 0:  # every rank reaches this point in the same lockstep step
+            from ome_amd.parallel.eplb import rebalance_model
+
+            imb = rebalance_model(self.runner.model)
+            if imb:
+                log.info("EPLB round: max/mean expert load per rank %.3f", max(imb.values()))
         return done
 
     def flush(self) -> list[Request]:
