@@ -14,6 +14,8 @@ Policy (SGLang-style, which is what the reference's runtime catalog configures t
 from __future__ import annotations
 
 import collections
+import time
+import os
 from dataclasses import dataclass, field
 
 from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
@@ -57,6 +59,12 @@ class Scheduler:
         self.running: list[Request] = []
         self.num_preemptions = 0
         self.on_finish = None  # hook(req) before a finished request's pages are released (PD prefill)
+        # prefill batching (throughput knob, off by default): while decodes are running, hold new
+        # requests until their prompts add up to ``prefill_batch_tokens`` or the oldest has waited
+        # ``prefill_max_wait_s`` -- fewer, larger prefill chunks run their GEMMs at higher MFMA
+        # efficiency, at the cost of queueing delay (TTFT)
+        self.prefill_batch_tokens = int(os.environ.get("OME_PREFILL_BATCH_TOKENS", "0"))
+        self.prefill_max_wait_s = float(os.environ.get("OME_PREFILL_MAX_WAIT_MS", "50")) / 1000.0
 
     # ------------------------------------------------------------------ queue ops
     def add(self, req: Request) -> None:
@@ -167,6 +175,11 @@ class Scheduler:
                 chunks.append(ScheduledChunk(r, r.num_cached, n, r.num_cached + n == r.seq_len))
                 budget -= n
         # 2) admit new requests
+        if self.prefill_batch_tokens and not chunks and self.running and self.waiting:
+            pending = sum(r.seq_len - r.num_cached for r in self.waiting)
+            if pending < min(self.prefill_batch_tokens, budget) and \
+                    time.perf_counter() - self.waiting[0].arrival_time < self.prefill_max_wait_s:
+                return None
         while self.waiting and budget > 0 and len(self.running) < self.max_running:
             r = self.waiting[0]
             if r.req_slot < 0:
