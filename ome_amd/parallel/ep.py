@@ -97,3 +97,88 @@ def moe_ep_forward(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor
     unsorted.index_copy_(0, order, back)
     out = (unsorted.view(T, k, H).float() * topk_w.float().view(T, k, 1)).sum(1) * scale
     return out.to(x.dtype)
+
+
+def _a2a_async(out, inp, out_splits, in_splits, group):
+    """Issue an all-to-all-v; returns a waitable (RCCL: runs on the communicator's stream, so
+    the compute stream keeps going until ``wait()``).  gloo (CPU tests) completes inline."""
+    if inp.is_cuda or dist.get_backend(group) != "gloo":
+        return dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=True)
+    _a2a(out, inp, out_splits, in_splits, group)
+    return None
+
+
+def moe_ep_forward_tbo(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13_local: torch.Tensor,
+                       w2_local: torch.Tensor, act: int, scale: float, num_experts: int,
+                       tables: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+    """Two-batch overlap of the expert-parallel MoE block (SGLang ``--enable-two-batch-overlap``,
+    reference deepseek-rdma-pd-rt.yaml:89): the token rows are split into two micro-batches;
+    their dispatches are issued back to back, then micro-batch A's experts run while B's
+    dispatch is still on the wire, and B's experts run while A's combine is on the wire:
+
+        comm stream   | dispatch A | dispatch B | combine A | combine B |
+        compute       |            | experts A  | experts B |   sum     |
+
+    Every rank always runs exactly two micro-batches (an empty half still takes part in the
+    collectives), so the collective sequence is identical across ranks.  Math is identical to
+    :func:`moe_ep_forward` (each row's experts and weights are unchanged; the combine is in
+    fp32 in (token, slot) order)."""
+    st = pstate.get()
+    group, ep = st.ep_group, st.ep_size
+    T, H = x.shape
+    k = topk_ids.shape[1]
+    flat_ids = topk_ids.reshape(-1).long()
+    if tables is None:
+        e_local = num_experts // ep
+        owner = flat_ids // e_local
+        local_slot = flat_ids - owner * e_local
+    else:
+        rep_rank, rep_slot, n_rep = tables
+        j = torch.arange(flat_ids.shape[0], device=flat_ids.device) % n_rep.index_select(0, flat_ids)
+        owner = rep_rank[flat_ids, j]
+        local_slot = rep_slot[flat_ids, j]
+    half = (T + 1) // 2
+    bounds = [(0, half * k), (half * k, T * k)]  # assignment ranges of micro-batches A and B
+    mbs = []
+    counts = []
+    for a0, a1 in bounds:
+        own = owner[a0:a1]
+        order = torch.argsort(own, stable=True) + a0
+        counts.append(torch.bincount(own, minlength=ep))
+        mbs.append({"order": order})
+    send_counts = torch.stack(counts, 1).reshape(-1)  # [ep, 2]: one exchange for both halves
+    recv_counts = torch.empty_like(send_counts)
+    _a2a(recv_counts, send_counts, [2] * ep, [2] * ep, group)
+    sc, rc = send_counts.view(ep, 2).tolist(), recv_counts.view(ep, 2).tolist()
+    for m, mb in enumerate(mbs):
+        mb["sc"] = [r[m] for r in sc]
+        mb["rc"] = [r[m] for r in rc]
+        order = mb["order"]
+        send_x = x.index_select(0, order // k)
+        send_e = local_slot.index_select(0, order).to(torch.int32)
+        R = sum(mb["rc"])
+        mb["rx"] = x.new_empty(R, H)
+        mb["re"] = torch.empty(R, dtype=torch.int32, device=x.device)
+        mb["keep"] = (send_x, send_e)  # alive until the transfer completes
+        mb["h"] = [_a2a_async(mb["rx"], send_x, mb["rc"], mb["sc"], group),
+                   _a2a_async(mb["re"], send_e, mb["rc"], mb["sc"], group)]
+    for mb in mbs:
+        for h in mb["h"]:
+            if h is not None:
+                h.wait()
+        R = mb["rx"].shape[0]
+        if R:
+            ones = torch.ones(R, 1, dtype=torch.float32, device=x.device)
+            y = ops.fused_moe(mb["rx"], ones, mb["re"].view(R, 1), w13_local, w2_local, act, 1.0)
+        else:
+            y = x.new_empty(0, H)
+        mb["y"] = y
+        mb["back"] = x.new_empty(sum(mb["sc"]), H)
+        mb["hc"] = _a2a_async(mb["back"], y, mb["sc"], mb["rc"], group)
+    unsorted = x.new_empty(T * k, H)
+    for mb in mbs:
+        if mb["hc"] is not None:
+            mb["hc"].wait()
+        unsorted.index_copy_(0, mb["order"], mb["back"])
+    out = (unsorted.view(T, k, H).float() * topk_w.float().view(T, k, 1)).sum(1) * scale
+    return out.to(x.dtype)

@@ -35,6 +35,7 @@ class ParallelState:
     ep_group: object | None = None
     backend: str = "nccl"
     comm: object | None = None  # ome_amd.parallel.comm.TPCommunicator
+    tbo: bool = False           # two-batch overlap of the EP MoE all-to-alls (parallel/ep.py)
 
     @property
     def is_first_pp(self) -> bool:

@@ -57,6 +57,7 @@ class EngineArgs:
     enable_dp_attention: bool = False      # --dp N --enable-dp-attention: per-rank batches + EP MoE
     ep_num_redundant_experts: int = 0      # EPLB: extra expert slots (replicas of hot experts) over the EP ranks
     eplb_rebalance_steps: int = 0          # EPLB: re-place experts from recorded loads every N lockstep steps
+    enable_two_batch_overlap: bool = False # EP MoE: two micro-batches, all-to-alls overlapped with experts
     overlap_schedule: bool | None = None   # enqueue step k+1 before step k's tokens reach the host
                                            # (None = on for GPU engines)
     num_layers_override: int | None = None
@@ -89,6 +90,7 @@ class Engine:
         if args.tp_size > 1 or args.pp_size > 1 or dp > 1:
             pstate.init(args.tp_size, args.pp_size, dist_init_addr=args.dist_init_addr, dp_size=dp)
         self.pstate = pstate.get()
+        self.pstate.tbo = bool(args.enable_two_batch_overlap and self.pstate.ep_size > 1)
         self.dp = self.pstate.dp_size > 1
         self._remote: dict[str, Request] = {}   # DP attention, rank 0: requests served by other ranks
         self._dp_next = 0

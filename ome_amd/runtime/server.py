@@ -62,6 +62,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--enable-dp-attention", action="store_true",
       help="--dp N with --tp N: attention/dense layers data-parallel per rank, MoE experts expert-parallel")
     a("--moe-a2a-backend", default="rccl", help="expert-parallel dispatch backend (rccl all-to-all over xGMI)")
+    a("--enable-two-batch-overlap", action="store_true",
+      help="EP MoE: split tokens into two micro-batches, overlap their all-to-alls with expert compute")
     a("--enable-eplb", action="store_true", help="expert-parallel load balancing (re-place experts from loads)")
     a("--ep-num-redundant-experts", type=int, default=0, help="EPLB: replicas of hot experts across EP ranks")
     a("--eplb-rebalance-num-iterations", type=int, default=1000, help="EPLB: lockstep steps between rebalances")
@@ -102,6 +104,7 @@ def engine_args_from(ns, rank_tp: int | None = None):
                       kv_cache_dtype=ns.kv_cache_dtype, quantization=ns.quantization,
                       enable_dp_attention=ns.enable_dp_attention,
                       ep_num_redundant_experts=ns.ep_num_redundant_experts,
+                      enable_two_batch_overlap=ns.enable_two_batch_overlap,
                       eplb_rebalance_steps=ns.eplb_rebalance_num_iterations if ns.enable_eplb else 0,
                       dist_init_addr=ns.dist_init_addr, nnodes=ns.nnodes,
                       node_rank=ns.node_rank, disaggregation_mode=ns.disaggregation_mode,

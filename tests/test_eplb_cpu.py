@@ -76,14 +76,15 @@ def test_migrate_moves_rows(monkeypatch):
         assert [int(x) for x in got[:, 0]] == new.phys_to_log[r]
 
 
-def _worker(rank, world, port, path, q):
+def _worker(rank, world, port, path, q, tbo=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     from ome_amd.runtime.engine import Engine, EngineArgs
     from ome_amd.runtime.request import SamplingParams
 
     eng = Engine(EngineArgs(model_path=path, tp_size=world, dp_size=world, enable_dp_attention=True, device="cpu",
                             max_running_requests=8, context_length=256, dtype="float32",
-                            ep_num_redundant_experts=2, eplb_rebalance_steps=3))
+                            ep_num_redundant_experts=2, eplb_rebalance_steps=3, enable_two_batch_overlap=tbo))
+    assert eng.pstate.tbo == tbo
     m = eng.runner.model
     assert m.eplb is not None and m.E_local == (m.E + 2) // world
     if rank == 0:
@@ -95,8 +96,10 @@ def _worker(rank, world, port, path, q):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("kind", ["qwen3-moe", "deepseek-v3"])
-def test_eplb_engine_matches_single(tmp_path, kind):
+@pytest.mark.parametrize("kind,tbo", [("qwen3-moe", False), ("deepseek-v3", False), ("qwen3-moe", True),
+                                      ("deepseek-v3", True)])
+def test_eplb_engine_matches_single(tmp_path, kind, tbo):
+    """(with ``tbo``: two-batch overlap of the EP all-to-alls on top of EPLB)"""
     _checkpoint(tmp_path, kind)
     from ome_amd.runtime.engine import Engine, EngineArgs
     from ome_amd.runtime.request import SamplingParams
@@ -109,7 +112,7 @@ def test_eplb_engine_matches_single(tmp_path, kind):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q, tbo)) for r in range(2)]
     for p in ps:
         p.start()
     got, rounds = q.get(timeout=300)
