@@ -66,6 +66,34 @@ def main(d: str, last_steps: int = 0) -> None:
     print("\n## Top kernels\n\n| total ms | % | calls | avg us | kernel |\n|---:|---:|---:|---:|---|")
     for n, v in tot.most_common(25):
         print(f"| {v / 1e6:.2f} | {100 * v / busy:.1f} | {cnt[n]} | {v / cnt[n] / 1e3:.1f} | `{short(n)}` |")
+    # ---- per step type: a step ends at its sample kernel; "mixed" if it ran prefill attention
+    kinds = {"decode": collections.Counter(), "mixed": collections.Counter()}
+    nk = {"decode": 0, "mixed": 0}
+    span = {"decode": 0, "mixed": 0}
+    cur = collections.Counter()
+    has_pf = False
+    s0 = None
+    for r in rows:
+        name = r["Kernel_Name"]
+        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        s0 = st if s0 is None else s0
+        cur[cat_of(name)] += en - st
+        has_pf |= "paged_prefill" in name
+        if "sample_kernel" in name:
+            k = "mixed" if has_pf else "decode"
+            kinds[k].update(cur)
+            nk[k] += 1
+            span[k] += en - s0
+            cur, has_pf, s0 = collections.Counter(), False, None
+    print("\n## Per step type (us per step; span = first kernel start to sample end)\n")
+    print("| category | decode-only | mixed (prefill + decodes) |\n|---|---:|---:|")
+    for c in sorted(set(kinds["decode"]) | set(kinds["mixed"]), key=lambda c: -(kinds["decode"][c] + kinds["mixed"][c])):
+        print(f"| {c} | {kinds['decode'][c] / 1e3 / max(1, nk['decode']):.0f} | "
+              f"{kinds['mixed'][c] / 1e3 / max(1, nk['mixed']):.0f} |")
+    print(f"| **busy total** | {sum(kinds['decode'].values()) / 1e3 / max(1, nk['decode']):.0f} | "
+          f"{sum(kinds['mixed'].values()) / 1e3 / max(1, nk['mixed']):.0f} |")
+    print(f"| **span** | {span['decode'] / 1e3 / max(1, nk['decode']):.0f} | {span['mixed'] / 1e3 / max(1, nk['mixed']):.0f} |")
+    print(f"| steps | {nk['decode']} | {nk['mixed']} |")
     print("\n## GEMMs by kernel+grid\n\n| total ms | calls | avg us | kernel / grid |\n|---:|---:|---:|---|")
     for n, v in grids.most_common(20):
         print(f"| {v / 1e6:.2f} | {gcnt[n]} | {v / gcnt[n] / 1e3:.1f} | `{n}` |")
