@@ -311,7 +311,81 @@ __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf1
   }
 }
 
-template <int D, int P, bool PF, int F>
+// ---- key-permuted tile (decode v4): MFMA row n of S^T tile s0 holds key 8*((n>>2)&1) + (n&3) of page
+// (n>>3), tile s1 the key 4 later.  The S^T accumulators of lane group g then hold keys
+// 8*(g&1) .. +7 of page g>>1, so the V^T operand of a lane is 8 CONSECUTIVE keys of one page:
+// one 16-B load per 16 dims (bf16) instead of two 8-B loads from two pages.
+template <int D, int F>
+struct KVTileP {
+  typename KVRaw<F>::K8 ka[D / 32], kb[D / 32];
+  typename KVRaw<F>::K8 v[D / 16];
+};
+
+template <int D, int P, int F>
+__device__ __forceinline__ void kv_tilep_load(KVTileP<D, F>& t, const typename KVStore<F>::T* __restrict__ k_cache,
+                                              const typename KVStore<F>::T* __restrict__ v_cache,
+                                              const int* __restrict__ bt, int kb, int seq_len, int64_t kpage, int kvh,
+                                              int n, int g) {
+  const int pA = bt[kb / P];
+  const int pB = (kb + P < seq_len) ? bt[kb / P + 1] : pA;
+  const int prow = (n >> 3) ? pB : pA, krow = 8 * ((n >> 2) & 1) + (n & 3);
+  const typename KVStore<F>::T* k0 = k_cache + prow * kpage + (int64_t)kvh * P * D + krow * D;
+  const typename KVStore<F>::T* k1 = k0 + 4 * D;
+  const typename KVStore<F>::T* vp = v_cache + ((g >> 1) ? pB : pA) * kpage + (int64_t)kvh * D * P + 8 * (g & 1);
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    t.ka[ks] = k8_load<F>(k0 + 32 * ks + 8 * g);
+    t.kb[ks] = k8_load<F>(k1 + 32 * ks + 8 * g);
+  }
+#pragma unroll
+  for (int nb = 0; nb < D / 16; ++nb) t.v[nb] = k8_load<F>(vp + (16 * nb + n) * P);
+}
+
+template <int D, int F>
+__device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const bf16x8 (&qf)[D / 32],
+                                                 f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
+                                                 int lo, float scale_log2, int g) {
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < D / 32; ++ks) {
+    s0 = mfma16(k8_bf16<F>(t.ka[ks]), qf[ks], s0);
+    s1 = mfma16(k8_bf16<F>(t.kb[ks]), qf[ks], s1);
+  }
+  const int base = kb + 16 * (g >> 1) + 8 * (g & 1);
+  float mt = OME_NEG_INF;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k0 = base + i, k1 = k0 + 4;
+    s0[i] = (k0 < p_end && k0 >= lo) ? s0[i] * scale_log2 : OME_NEG_INF;
+    s1[i] = (k1 < p_end && k1 >= lo) ? s1[i] * scale_log2 : OME_NEG_INF;
+    mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
+  }
+  mt = fmaxf(mt, __shfl_xor(mt, 16));
+  mt = fmaxf(mt, __shfl_xor(mt, 32));
+  const float m_new = fmaxf(m_i, mt);
+  const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
+  const float alpha = fast_exp2(m_i - m_use);
+  bf16x8 pb;
+  float rs = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float p0 = fast_exp2(s0[i] - m_use), p1 = fast_exp2(s1[i] - m_use);
+    pb[i] = (bf16)p0;
+    pb[4 + i] = (bf16)p1;
+    rs += p0 + p1;
+  }
+  rs += __shfl_xor(rs, 16);
+  rs += __shfl_xor(rs, 32);
+  l_i = l_i * alpha + rs;
+  m_i = m_new;
+#pragma unroll
+  for (int nb = 0; nb < D / 16; ++nb) {
+    o[nb] = o[nb] * alpha;
+    o[nb] = mfma16(k8_bf16<F>(t.v[nb]), pb, o[nb]);
+  }
+}
+
+template <int D, int P, int MODE, int F>
 __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -354,7 +428,13 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
   if (lo > 0) {  // sliding window: skip whole tiles before the window
     while (kb + 32 <= lo && kb < p_end) kb += 128;
   }
-  if (!PF) {
+  if (MODE == 2) {
+    for (; kb < p_end; kb += 128) {
+      KVTileP<D, F> t;
+      kv_tilep_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
+      kv_tilep_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
+    }
+  } else if (MODE == 0) {
     for (; kb < p_end; kb += 128) {
       KVTile<D, F> t;
       kv_tile_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
@@ -424,7 +504,9 @@ static void launch_decode_v2(int variant, dim3 grid, size_t smem, hipStream_t st
                              int bt_stride, const int* seq_lens, void* out, int64_t out_stride, void* part_o,
                              void* part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2,
                              int window, const int* order, float v_scale) {
-  auto kern = variant == 2 ? paged_decode_v2_kernel<128, 16, true, F> : paged_decode_v2_kernel<128, 16, false, F>;
+  auto kern = variant == 2   ? paged_decode_v2_kernel<128, 16, 1, F>
+              : variant == 4 ? paged_decode_v2_kernel<128, 16, 2, F>
+                             : paged_decode_v2_kernel<128, 16, 0, F>;
   kern<<<grid, 256, smem, stream>>>((const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache,
                                     (const typename KVStore<F>::T*)v_cache, block_tables, bt_stride, seq_lens,
                                     (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size,
@@ -444,8 +526,10 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
   const float scale_log2 = scale * k_scale * 1.4426950408889634f;
   dim3 grid(max_parts, Hkv, B);
-  const char* ve = getenv("OME_DECODE_ATTN");  // A/B switch for benchmarking (default v3 = v2 without ring)
-  int variant = ve ? atoi(ve) : 3;
+  // A/B switch for benchmarking: 1 = v1, 2 = v2 (register ring), 3 = v2 without ring, 4 = v3 with
+  // key-permuted tiles (16-B V loads; default: 5.38 vs 5.24 TB/s on the bench's context mix)
+  const char* ve = getenv("OME_DECODE_ATTN");
+  int variant = ve ? atoi(ve) : 4;
   if (variant == 1 && kv_fmt != KV_BF16) variant = 3;  // v1 reads bf16 caches only
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);

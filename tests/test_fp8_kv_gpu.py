@@ -84,7 +84,7 @@ def test_kv_cache_write_fp8(dt):
 @pytest.mark.parametrize("dt", FP8)
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8)])
 @pytest.mark.parametrize("seq_lens", [[1], [15, 16, 17, 33], [100, 1000, 3, 517]])
-@pytest.mark.parametrize("variant", ["2", "3"])
+@pytest.mark.parametrize("variant", ["2", "3", "4"])
 def test_paged_decode_fp8(dt, Hq, Hkv, seq_lens, variant, monkeypatch):
     monkeypatch.setenv("OME_DECODE_ATTN", variant)
     D, P = 128, 16

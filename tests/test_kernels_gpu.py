@@ -106,7 +106,7 @@ def _block_tables(seq_lens, P, num_pages):
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1), (64, 8), (16, 16)])
 @pytest.mark.parametrize("seq_lens", [[1], [15, 16, 17, 33], [100, 1000, 3, 517], [5000, 7]])
 @pytest.mark.parametrize("part_size", [256, 8192])
-@pytest.mark.parametrize("variant", ["1", "2", "3"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
 def test_paged_decode(Hq, Hkv, seq_lens, part_size, variant, monkeypatch):
     monkeypatch.setenv("OME_DECODE_ATTN", variant)
     D, P = 128, 16
@@ -125,7 +125,7 @@ def test_paged_decode(Hq, Hkv, seq_lens, part_size, variant, monkeypatch):
         _close(ops.paged_decode(q, kc, vc, bt, sl, scale, ws, order=order), expect, atol=2e-2)
 
 
-@pytest.mark.parametrize("variant", ["1", "2", "3"])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
 def test_paged_decode_window(variant, monkeypatch):
     monkeypatch.setenv("OME_DECODE_ATTN", variant)
     D, P, Hq, Hkv = 128, 16, 32, 8
