@@ -31,6 +31,30 @@
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// raw score -> log2-domain logit: s * scale * log2(e), or with logit soft-capping (Gemma-2:
+// cap * tanh(s * scale / cap)) cap * log2(e) * tanh(s * scale / cap)
+struct Scaler {
+  float mul;      // scale * log2(e) (cap_inv == 0)
+  float cap_inv;  // scale / cap, 0 = no soft-capping
+  float cap_l2;   // cap * log2(e)
+  __device__ __forceinline__ float operator()(float s) const {
+    if (cap_inv > 0.f) {
+      const float e = fast_exp2(2.8853900817779268f * s * cap_inv);  // exp(2x)
+      return cap_l2 * (1.f - 2.f / (e + 1.f));                        // tanh(x), saturating at +-1
+    }
+    return s * mul;
+  }
+};
+
+static inline Scaler make_scaler(float scale, float softcap) {
+  const float l2e = 1.4426950408889634f;
+  Scaler r;
+  r.mul = scale * l2e;
+  r.cap_inv = softcap > 0.f ? scale / softcap : 0.f;
+  r.cap_l2 = softcap > 0.f ? softcap * l2e : 0.f;
+  return r;
+}
+
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -271,7 +295,7 @@ __device__ __forceinline__ void kv_tile_load(KVTile<D, F>& t, const typename KVS
 template <int D, int F>
 __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf16x8 (&qf)[D / 32],
                                                 f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
-                                                int lo, float scale_log2, int g) {
+                                                int lo, Scaler scl, int g) {
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
@@ -282,8 +306,8 @@ __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf1
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k0 = kb + 4 * g + i, k1 = k0 + 16;
-    s0[i] = (k0 < p_end && k0 >= lo) ? s0[i] * scale_log2 : OME_NEG_INF;
-    s1[i] = (k1 < p_end && k1 >= lo) ? s1[i] * scale_log2 : OME_NEG_INF;
+    s0[i] = (k0 < p_end && k0 >= lo) ? scl(s0[i]) : OME_NEG_INF;
+    s1[i] = (k1 < p_end && k1 >= lo) ? scl(s1[i]) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
   mt = fmaxf(mt, __shfl_xor(mt, 16));
@@ -344,7 +368,7 @@ __device__ __forceinline__ void kv_tilep_load(KVTileP<D, F>& t, const typename K
 template <int D, int F>
 __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const bf16x8 (&qf)[D / 32],
                                                  f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
-                                                 int lo, float scale_log2, int g) {
+                                                 int lo, Scaler scl, int g) {
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
@@ -356,8 +380,8 @@ __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const b
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k0 = base + i, k1 = k0 + 4;
-    s0[i] = (k0 < p_end && k0 >= lo) ? s0[i] * scale_log2 : OME_NEG_INF;
-    s1[i] = (k1 < p_end && k1 >= lo) ? s1[i] * scale_log2 : OME_NEG_INF;
+    s0[i] = (k0 < p_end && k0 >= lo) ? scl(s0[i]) : OME_NEG_INF;
+    s1[i] = (k1 < p_end && k1 >= lo) ? scl(s1[i]) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
   mt = fmaxf(mt, __shfl_xor(mt, 16));
@@ -390,7 +414,7 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ seq_lens, bf16* __restrict__ out, int64_t out_stride, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2, int window,
+    float* __restrict__ part_ml, int Hq, int Hkv, int part_size, int max_parts, Scaler scl, int window,
     const int* __restrict__ order, float v_scale) {
   static_assert(P == 16, "decode kernel assumes 16-token pages");
   constexpr int NB = D / 16, KS = D / 32;
@@ -432,13 +456,13 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     for (; kb < p_end; kb += 128) {
       KVTileP<D, F> t;
       kv_tilep_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tilep_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
+      kv_tilep_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g);
     }
   } else if (MODE == 0) {
     for (; kb < p_end; kb += 128) {
       KVTile<D, F> t;
       kv_tile_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
+      kv_tile_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g);
     }
   } else if (kb < p_end) {
     KVTile<D, F> t0, t1;
@@ -447,12 +471,12 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
       const int kn = kb + 128;
       const bool more = kn < p_end;
       if (more) kv_tile_load<D, P, F>(t1, k_cache, v_cache, bt, kn, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t0, qf, o, m_i, l_i, kb, p_end, lo, scale_log2, g);
+      kv_tile_compute<D, F>(t0, qf, o, m_i, l_i, kb, p_end, lo, scl, g);
       if (!more) break;
       const int kn2 = kn + 128;
       const bool more2 = kn2 < p_end;
       if (more2) kv_tile_load<D, P, F>(t0, k_cache, v_cache, bt, kn2, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t1, qf, o, m_i, l_i, kn, p_end, lo, scale_log2, g);
+      kv_tile_compute<D, F>(t1, qf, o, m_i, l_i, kn, p_end, lo, scl, g);
       if (!more2) break;
       kb = kn2;
     }
@@ -498,63 +522,86 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
   }
 }
 
-template <int F>
+template <int D, int F>
 static void launch_decode_v2(int variant, dim3 grid, size_t smem, hipStream_t stream, const void* q,
                              int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                              int bt_stride, const int* seq_lens, void* out, int64_t out_stride, void* part_o,
-                             void* part_ml, int Hq, int Hkv, int part_size, int max_parts, float scale_log2,
+                             void* part_ml, int Hq, int Hkv, int part_size, int max_parts, Scaler scl,
                              int window, const int* order, float v_scale) {
-  auto kern = variant == 2   ? paged_decode_v2_kernel<128, 16, 1, F>
-              : variant == 4 ? paged_decode_v2_kernel<128, 16, 2, F>
-                             : paged_decode_v2_kernel<128, 16, 0, F>;
+  auto kern = variant == 2   ? paged_decode_v2_kernel<D, 16, 1, F>
+              : variant == 4 ? paged_decode_v2_kernel<D, 16, 2, F>
+                             : paged_decode_v2_kernel<D, 16, 0, F>;
   kern<<<grid, 256, smem, stream>>>((const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache,
                                     (const typename KVStore<F>::T*)v_cache, block_tables, bt_stride, seq_lens,
                                     (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size,
-                                    max_parts, scale_log2, window, order, v_scale);
+                                    max_parts, scl, window, order, v_scale);
 }
 
-// kv_fmt: KVFmt of the cache; k_scale / v_scale: per-layer dequantisation scales (1 for bf16)
+// kv_fmt: KVFmt of the cache; k_scale / v_scale: per-layer dequantisation scales (1 for bf16);
+// softcap: attention-logit soft-capping (Gemma-2), 0 = off.  Head dims 64 / 128 / 256.
+template <int D>
+static int decode_dispatch(int variant, int kv_fmt, dim3 grid, int B, hipStream_t stream, const void* q,
+                           int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
+                           int bt_stride, const int* seq_lens, void* out, int64_t out_stride, void* part_o,
+                           void* part_ml, int Hq, int Hkv, int part_size, int max_parts, Scaler scl, int window,
+                           const int* order, float v_scale) {
+  const int G = Hq / Hkv;
+  const size_t smem = (8 * G + 4 * G * D) * sizeof(float);
+#define ARGS                                                                                                     \
+  variant, grid, smem, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, out, out_stride, \
+      part_o, part_ml, Hq, Hkv, part_size, max_parts, scl, window, order, v_scale
+  if (kv_fmt == KV_BF16) launch_decode_v2<D, KV_BF16>(ARGS);
+  else if (kv_fmt == KV_E4M3) launch_decode_v2<D, KV_E4M3>(ARGS);
+  else launch_decode_v2<D, KV_E5M2>(ARGS);
+#undef ARGS
+  OME_CHECK_LAUNCH();
+  if (max_parts > 1) {
+    paged_decode_reduce_kernel<D><<<dim3(Hq, B), D, 0, stream>>>(seq_lens, (const float*)part_o,
+                                                                  (const float*)part_ml, (bf16*)out, out_stride, Hq,
+                                                                  part_size, max_parts);
+    OME_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
 OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                              const int* block_tables, int bt_stride, const int* seq_lens, void* out,
                              int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
                              int part_size, int max_parts, float scale, int window, const int* order, int kv_fmt,
-                             float k_scale, float v_scale, hipStream_t stream) {
+                             float k_scale, float v_scale, float softcap, hipStream_t stream) {
   if (B <= 0) return 0;
-  if (D != 128 || P != 16) return -2;
+  if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
   if (part_size % 128 != 0 || max_parts <= 0) return -4;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
-  const float scale_log2 = scale * k_scale * 1.4426950408889634f;
+  const Scaler scl = make_scaler(scale * k_scale, softcap);
   dim3 grid(max_parts, Hkv, B);
   // A/B switch for benchmarking: 1 = v1, 2 = v2 (register ring), 3 = v2 without ring, 4 = v3 with
   // key-permuted tiles (16-B V loads; default: 5.38 vs 5.24 TB/s on the bench's context mix)
   const char* ve = getenv("OME_DECODE_ATTN");
   int variant = ve ? atoi(ve) : 4;
-  if (variant == 1 && kv_fmt != KV_BF16) variant = 3;  // v1 reads bf16 caches only
+  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f)) variant = 4;  // v1: bf16, D=128 only
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
     paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(
         (const bf16*)q, q_stride, (const bf16*)k_cache, (const bf16*)v_cache, block_tables, bt_stride, seq_lens,
-        (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window);
-  } else {
-    const int G = Hq / Hkv;
-    const size_t smem = (8 * G + 4 * G * D) * sizeof(float);
-#define ARGS                                                                                                     \
-  variant, grid, smem, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, out, out_stride, \
-      part_o, part_ml, Hq, Hkv, part_size, max_parts, scale_log2, window, order, v_scale
-    if (kv_fmt == KV_BF16) launch_decode_v2<KV_BF16>(ARGS);
-    else if (kv_fmt == KV_E4M3) launch_decode_v2<KV_E4M3>(ARGS);
-    else launch_decode_v2<KV_E5M2>(ARGS);
-#undef ARGS
-  }
-  OME_CHECK_LAUNCH();
-  if (max_parts > 1) {
-    paged_decode_reduce_kernel<128><<<dim3(Hq, B), 128, 0, stream>>>(seq_lens, (const float*)part_o,
-                                                                      (const float*)part_ml, (bf16*)out,
-                                                                      out_stride, Hq, part_size, max_parts);
+        (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size, max_parts, scl.mul, window);
     OME_CHECK_LAUNCH();
+    if (max_parts > 1) {
+      paged_decode_reduce_kernel<128><<<dim3(Hq, B), 128, 0, stream>>>(seq_lens, (const float*)part_o,
+                                                                        (const float*)part_ml, (bf16*)out,
+                                                                        out_stride, Hq, part_size, max_parts);
+      OME_CHECK_LAUNCH();
+    }
+    return 0;
   }
-  return 0;
+#define ARGS                                                                                                      \
+  variant, kv_fmt, grid, B, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, out,         \
+      out_stride, part_o, part_ml, Hq, Hkv, part_size, max_parts, scl, window, order, v_scale
+  if (D == 64) return decode_dispatch<64>(ARGS);
+  if (D == 256) return decode_dispatch<256>(ARGS);
+  return decode_dispatch<128>(ARGS);
+#undef ARGS
 }
 
 // ------------------------------------------------------------------------------------------
@@ -569,7 +616,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
-    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window, float v_scale) {
+    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale) {
   static_assert(P == 16, "prefill kernel assumes 16-token pages");
   constexpr int NB = D / 16, KS = D / 32;
   const int2 it = items[blockIdx.x];
@@ -636,7 +683,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
         for (int X = 0; X < 2; ++X)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float v = sc[rb][X][i] * scale_log2;
+            float v = scl(sc[rb][X][i]);
             if (need_mask) {
               const int key = kb + 16 * X + 4 * g + i;
               const bool ok = key <= qpos && key < kv_len && (window <= 0 || key > qpos - window);
@@ -715,7 +762,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
-    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, float scale_log2, int window, float v_scale) {
+    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale) {
   constexpr int D = 128, P = 16, NB = D / 16, KS = D / 32;
   typedef typename KVRaw<F>::K8 Raw8;  // 8 consecutive cache elements
   __shared__ __attribute__((aligned(16))) bf16 sK[2][SUB][32 * PF_KLD];
@@ -836,7 +883,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
         for (int X = 0; X < 2; ++X)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float v = sc[rb][X][i] * scale_log2;
+            float v = scl(sc[rb][X][i]);
             if (need_mask) {
               const int key = kbu + 16 * X + 4 * g + i;
               const bool ok = key <= qpos && key < kv_len && (window <= 0 || key > qpos - window);
@@ -896,44 +943,60 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   }
 }
 
-template <int F>
+template <int D, int F>
 static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, const void* q, int64_t q_stride,
                            const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                            const int* cu_q, const int* kv_lens, const int* items, void* out, int64_t out_stride,
-                           int Hq, int Hkv, float scale_log2, int window, float v_scale) {
+                           int Hq, int Hkv, Scaler scl, int window, float v_scale) {
   typedef typename KVStore<F>::T T;
-  if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
-    paged_prefill_v2_kernel<2, F><<<grid, 256, 0, stream>>>(
-        (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-        (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window, v_scale);
-  } else {
-    const int nw = G < 8 ? G : 8;
-    paged_prefill_kernel<128, 16, F><<<grid, 64 * nw, 0, stream>>>(
-        (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-        (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scale_log2, window, v_scale);
+  if constexpr (D == 128) {
+    if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
+      paged_prefill_v2_kernel<2, F><<<grid, 256, 0, stream>>>(
+          (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
+          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale);
+      return;
+    }
   }
+  const int nw = G < 8 ? G : 8;
+  paged_prefill_kernel<D, 16, F><<<grid, 64 * nw, 0, stream>>>(
+      (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
+      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale);
+}
+
+template <int D>
+static void prefill_dispatch(int kv_fmt, int variant, int G, dim3 grid, hipStream_t stream, const void* q,
+                             int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
+                             int bt_stride, const int* cu_q, const int* kv_lens, const int* items, void* out,
+                             int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale) {
+#define ARGS                                                                                                   \
+  variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, out, \
+      out_stride, Hq, Hkv, scl, window, v_scale
+  if (kv_fmt == KV_BF16) launch_prefill<D, KV_BF16>(ARGS);
+  else if (kv_fmt == KV_E4M3) launch_prefill<D, KV_E4M3>(ARGS);
+  else launch_prefill<D, KV_E5M2>(ARGS);
+#undef ARGS
 }
 
 OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
                               const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
                               const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
                               int P, float scale, int window, int kv_fmt, float k_scale, float v_scale,
-                              hipStream_t stream) {
+                              float softcap, hipStream_t stream) {
   if (n_items <= 0) return 0;
-  if (D != 128 || P != 16) return -2;
+  if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0) return -3;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
   const int G = Hq / Hkv;
-  const float scale_log2 = scale * k_scale * 1.4426950408889634f;
+  const Scaler scl = make_scaler(scale * k_scale, softcap);
   dim3 grid(n_items, Hkv);
   const char* ve = getenv("OME_PREFILL_ATTN");
   const int variant = ve ? atoi(ve) : 2;
-#define ARGS                                                                                                   \
-  variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, out, \
-      out_stride, Hq, Hkv, scale_log2, window, v_scale
-  if (kv_fmt == KV_BF16) launch_prefill<KV_BF16>(ARGS);
-  else if (kv_fmt == KV_E4M3) launch_prefill<KV_E4M3>(ARGS);
-  else launch_prefill<KV_E5M2>(ARGS);
+#define ARGS                                                                                                     \
+  kv_fmt, variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, \
+      out, out_stride, Hq, Hkv, scl, window, v_scale
+  if (D == 64) prefill_dispatch<64>(ARGS);
+  else if (D == 256) prefill_dispatch<256>(ARGS);
+  else prefill_dispatch<128>(ARGS);
 #undef ARGS
   OME_CHECK_LAUNCH();
   return 0;

@@ -144,7 +144,7 @@ OME_API int ome_rope_qkv_cache(const void* qkv, int64_t qkv_stride, const int* p
                                const void* k_norm_w, float qk_eps, int kv_fmt, float k_scale, float v_scale,
                                hipStream_t stream) {
   if (T <= 0) return 0;
-  if (D != 128 && D != 64) return -2;
+  if (D != 128 && D != 64 && D != 256) return -2;
   if (rot_dim > D || rot_dim % 16 != 0) return -3;
   if (P != 16) return -4;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
@@ -158,6 +158,10 @@ OME_API int ome_rope_qkv_cache(const void* qkv, int64_t qkv_stride, const int* p
     if (kv_fmt == KV_BF16) LAUNCH(128, KV_BF16);
     else if (kv_fmt == KV_E4M3) LAUNCH(128, KV_E4M3);
     else LAUNCH(128, KV_E5M2);
+  } else if (D == 256) {
+    if (kv_fmt == KV_BF16) LAUNCH(256, KV_BF16);
+    else if (kv_fmt == KV_E4M3) LAUNCH(256, KV_E4M3);
+    else LAUNCH(256, KV_E5M2);
   } else {
     if (kv_fmt == KV_BF16) LAUNCH(64, KV_BF16);
     else if (kv_fmt == KV_E4M3) LAUNCH(64, KV_E4M3);
@@ -172,7 +176,7 @@ OME_API int ome_kv_cache_write(const void* k, const void* v, int64_t kv_stride, 
                                const int* slots, int T, int Hkv, int D, int P, int kv_fmt, float k_scale,
                                float v_scale, hipStream_t stream) {
   if (T <= 0) return 0;
-  if ((D != 128 && D != 64) || P != 16) return -4;
+  if ((D != 128 && D != 64 && D != 256) || P != 16) return -4;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
   const float ki = 1.f / k_scale, vi = 1.f / v_scale;
 #define LAUNCH(DD, FF)                                                                                    \
@@ -183,6 +187,10 @@ OME_API int ome_kv_cache_write(const void* k, const void* v, int64_t kv_stride, 
     if (kv_fmt == KV_BF16) LAUNCH(128, KV_BF16);
     else if (kv_fmt == KV_E4M3) LAUNCH(128, KV_E4M3);
     else LAUNCH(128, KV_E5M2);
+  } else if (D == 256) {
+    if (kv_fmt == KV_BF16) LAUNCH(256, KV_BF16);
+    else if (kv_fmt == KV_E4M3) LAUNCH(256, KV_E4M3);
+    else LAUNCH(256, KV_E5M2);
   } else {
     if (kv_fmt == KV_BF16) LAUNCH(64, KV_BF16);
     else if (kv_fmt == KV_E4M3) LAUNCH(64, KV_E4M3);

@@ -242,12 +242,12 @@ class DecodeWorkspace:
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeWorkspace | None = None,
                  window: int = -1, out=None, order: torch.Tensor | None = None, k_scale: float = 1.0,
-                 v_scale: float = 1.0) -> torch.Tensor:
+                 v_scale: float = 1.0, softcap: float = 0.0) -> torch.Tensor:
     """q [B, Hq, D] -> [B, Hq, D].  ``order`` (int32 [B], optional): sequence visit order for the
     workgroup dispatcher (longest first balances the tail).  The cache may be bf16 or fp8
     (``k_scale`` / ``v_scale`` dequantise it)."""
     if not _gpu(q):
-        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window, k_scale, v_scale)
+        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window, k_scale, v_scale, softcap)
         if out is not None:
             out.copy_(r)
             return out
@@ -261,7 +261,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeW
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(seq_lens).data_ptr(), out.data_ptr(),
          out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
          float(scale), int(window), _i32(order).data_ptr() if order is not None else None, kv_format(k_cache),
-         float(k_scale), float(v_scale), stream_ptr())
+         float(k_scale), float(v_scale), float(softcap), stream_ptr())
     return out
 
 
@@ -320,10 +320,12 @@ def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) ->
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale, window: int = -1,
-                  out=None, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
-    """q [Tq, Hq, D]; items int32 [n, 2] from :func:`prefill_work_items`."""
+                  out=None, k_scale: float = 1.0, v_scale: float = 1.0, softcap: float = 0.0) -> torch.Tensor:
+    """q [Tq, Hq, D]; items int32 [n, 2] from :func:`prefill_work_items`.  ``softcap`` > 0:
+    attention-logit soft-capping ``cap * tanh(score / cap)`` (Gemma-2)."""
     if not _gpu(q):
-        r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window, k_scale, v_scale)
+        r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window, k_scale, v_scale,
+                              softcap)
         if out is not None:
             out.copy_(r)
             return out
@@ -334,7 +336,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     call("ome_paged_prefill", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
          _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),
-         int(window), kv_format(k_cache), float(k_scale), float(v_scale), stream_ptr())
+         int(window), kv_format(k_cache), float(k_scale), float(v_scale), float(softcap), stream_ptr())
     return out
 
 

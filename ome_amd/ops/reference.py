@@ -103,8 +103,12 @@ def gather_kv(k_cache, v_cache, block_table, n: int, kvh: int, P: int, k_scale=1
     return k.float() * k_scale, v.float() * v_scale
 
 
+def _cap(s: torch.Tensor, softcap: float) -> torch.Tensor:
+    return softcap * torch.tanh(s / softcap) if softcap and softcap > 0 else s
+
+
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, k_scale=1.0,
-                 v_scale=1.0) -> torch.Tensor:
+                 v_scale=1.0, softcap=0.0) -> torch.Tensor:
     B, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -118,13 +122,13 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, 
             k, v = gather_kv(k_cache, v_cache, block_tables[b], L, h, P, k_scale, v_scale)
             k, v = k[lo:], v[lo:]
             qh = q[b, h * G:(h + 1) * G].float()
-            s = (qh @ k.T) * scale
+            s = _cap((qh @ k.T) * scale, softcap)
             out[b, h * G:(h + 1) * G] = (torch.softmax(s, -1) @ v).to(q.dtype)
     return out
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window=-1, k_scale=1.0,
-                  v_scale=1.0) -> torch.Tensor:
+                  v_scale=1.0, softcap=0.0) -> torch.Tensor:
     Tq, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -143,7 +147,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, windo
         for h in range(Hkv):
             k, v = gather_kv(k_cache, v_cache, block_tables[s], L, h, P, k_scale, v_scale)
             qh = q[q0:q1, h * G:(h + 1) * G].float().transpose(0, 1)  # [G, ql, D]
-            sc = (qh @ k.T) * scale
+            sc = _cap((qh @ k.T) * scale, softcap)
             sc = sc.masked_fill(~mask[None], float("-inf"))
             o = torch.softmax(sc, -1) @ v
             out[q0:q1, h * G:(h + 1) * G] = o.transpose(0, 1).to(q.dtype)

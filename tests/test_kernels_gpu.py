@@ -234,3 +234,64 @@ def test_penalties(dtype):
     ref.update_counts(cw, slot.cpu(), ids.cpu(), rep.cpu(), freq.cpu(), pres.cpu())
     ops.update_counts(counts, slot, ids, rep, freq, pres)
     assert torch.equal(counts.cpu(), cw)
+
+
+@pytest.mark.parametrize("D", [64, 256])
+@pytest.mark.parametrize("softcap", [0.0, 50.0])
+@pytest.mark.parametrize("variant", ["3", "4"])
+def test_paged_decode_head_dims_softcap(D, softcap, variant, monkeypatch):
+    """Head dims 64 (GPT-OSS class) / 256 (Gemma-2/3) and Gemma-2 attention-logit soft-capping."""
+    monkeypatch.setenv("OME_DECODE_ATTN", variant)
+    Hq, Hkv, P = 8, 4, 16
+    seq_lens = [1, 37, 300, 1000]
+    npages = sum(-(-L // P) for L in seq_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    kc, vc = kc * 3, vc
+    bt = _block_tables(seq_lens, P, npages)
+    sl = torch.tensor(seq_lens, dtype=torch.int32, device=DEV)
+    q = torch.randn(len(seq_lens), Hq, D, device=DEV, dtype=torch.bfloat16) * 3
+    ws = ops.DecodeWorkspace(len(seq_lens), Hq, D, 2048, 256, DEV)
+    scale = D ** -0.5
+    out = ops.paged_decode(q, kc, vc, bt, sl, scale, ws, softcap=softcap)
+    _close(out, ref.paged_decode(q, kc, vc, bt, sl, scale, -1, 1.0, 1.0, softcap), atol=3e-2)
+    out_w = ops.paged_decode(q, kc, vc, bt, sl, scale, ws, window=100, softcap=softcap)
+    _close(out_w, ref.paged_decode(q, kc, vc, bt, sl, scale, 100, 1.0, 1.0, softcap), atol=3e-2)
+
+
+@pytest.mark.parametrize("D", [64, 128, 256])
+@pytest.mark.parametrize("softcap", [0.0, 30.0])
+def test_paged_prefill_head_dims_softcap(D, softcap):
+    Hq, Hkv, P = 8, 2, 16
+    q_lens, kv_lens = [37, 64, 1, 100], [37, 80, 300, 100]
+    npages = sum(-(-L // P) for L in kv_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    kc = kc * 3
+    bt = _block_tables(kv_lens, P, npages)
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    items = torch.tensor(ops.prefill_work_items(q_lens, kv_lens), dtype=torch.int32, device=DEV)
+    q = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16) * 3
+    out = ops.paged_prefill(q, kc, vc, bt, cu, kl, items, D ** -0.5, window=64, softcap=softcap)
+    _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, D ** -0.5, 64, 1.0, 1.0, softcap), atol=3e-2)
+
+
+@pytest.mark.parametrize("D", [64, 256])
+def test_rope_qkv_cache_head_dims(D):
+    from ome_amd.models.config import preset, rope_cos_sin
+
+    Hq, Hkv, T, P = 8, 4, 19, 16
+    cfg = preset("llama-3.1-8b")
+    cfg.head_dim, cfg.partial_rotary_factor = D, 1.0
+    cs = rope_cos_sin(cfg, 4096, device=DEV)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(20 * P, device=DEV)[:T].to(torch.int32)
+    k1, v1 = _cache(20, Hkv, D)
+    k2, v2 = k1.clone(), v1.clone()
+    q1 = torch.empty(T, Hq, D, device=DEV, dtype=torch.bfloat16)
+    q2 = torch.empty_like(q1)
+    ops.rope_qkv_cache(qkv, pos, cs, D, q1, k1, v1, slots, Hq, Hkv, D)
+    ref.rope_qkv_cache(qkv, pos, cs, D, q2, k2, v2, slots, Hq, Hkv, D, P)
+    _close(q1, q2, atol=3e-2)
+    _close(k1, k2, atol=3e-2)
+    assert torch.equal(v1, v2)
