@@ -18,11 +18,16 @@ DENSE_ARCHS = {
     "LlamaModel", "MistralModel", "Qwen2Model", "Qwen3Model", "LlamaForSequenceClassification",
     "Qwen2ForRewardModel", "Phi3ForCausalLM", "GraniteForCausalLM", "SmolLM3ForCausalLM",
 }
+GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
 MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM", "DeepseekV2ForCausalLM",
              "DeepseekV3ForCausalLM", "PhiMoEForCausalLM"}
 
 
 def model_class(cfg: ModelConfig):
+    if cfg.architecture in GEMMA_ARCHS or cfg.model_type in ("gemma", "gemma2", "gemma3", "gemma3_text"):
+        from ome_amd.models.gemma import GemmaForCausalLM
+
+        return GemmaForCausalLM
     if cfg.is_mla:
         from ome_amd.models.deepseek import DeepseekForCausalLM
 
@@ -37,7 +42,7 @@ def model_class(cfg: ModelConfig):
 
 
 def supported(arch: str) -> bool:
-    return arch in DENSE_ARCHS or arch in MOE_ARCHS
+    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,

@@ -93,6 +93,13 @@ class ModelConfig:
         nh = text.get("num_attention_heads", 32)
         hd = text.get("head_dim") or H // nh
         mt = text.get("model_type", cfg.get("model_type", "llama"))
+        rope_theta, rope_scaling = text.get("rope_theta", 10000.0), text.get("rope_scaling")
+        rp = text.get("rope_parameters")  # transformers >= 5: {rope_type, rope_theta, ...} or per layer type
+        if isinstance(rp, dict) and rp:
+            glob = rp.get("full_attention", rp) if ("full_attention" in rp or "sliding_attention" in rp) else rp
+            rope_theta = glob.get("rope_theta", rope_theta)
+            if glob.get("rope_type", "default") != "default":
+                rope_scaling = dict(glob)
         c = cls(
             architecture=arch,
             model_type=mt,
@@ -104,13 +111,13 @@ class ModelConfig:
             intermediate_size=text.get("intermediate_size", 4 * H),
             vocab_size=text.get("vocab_size", 32000),
             rms_norm_eps=text.get("rms_norm_eps", 1e-6),
-            rope_theta=text.get("rope_theta", 10000.0),
-            rope_scaling=text.get("rope_scaling"),
+            rope_theta=rope_theta,
+            rope_scaling=rope_scaling,
             partial_rotary_factor=text.get("partial_rotary_factor", 1.0),
             max_position_embeddings=text.get("max_position_embeddings", 4096),
             tie_word_embeddings=bool(cfg.get("tie_word_embeddings", text.get("tie_word_embeddings", False))),
             attention_bias=bool(text.get("attention_bias", mt in ("qwen2", "qwen2_moe"))),
-            qk_norm=mt in ("qwen3", "qwen3_moe"),
+            qk_norm=mt in ("qwen3", "qwen3_moe", "gemma3", "gemma3_text"),
             hidden_act=text.get("hidden_act", text.get("hidden_activation", "silu")),
             sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt == "mistral") else None,
             torch_dtype=str(text.get("torch_dtype", cfg.get("torch_dtype", "bfloat16"))),
@@ -183,6 +190,17 @@ PRESETS: dict[str, dict] = {
     "tiny-llama": dict(architectures=["LlamaForCausalLM"], model_type="llama", hidden_size=256, num_hidden_layers=2,
                        num_attention_heads=4, num_key_value_heads=2, head_dim=128, intermediate_size=512,
                        vocab_size=1024, rms_norm_eps=1e-5, rope_theta=10000.0, max_position_embeddings=2048),
+    "gemma-2-9b": dict(architectures=["Gemma2ForCausalLM"], model_type="gemma2", hidden_size=3584,
+                       num_hidden_layers=42, num_attention_heads=16, num_key_value_heads=8, head_dim=256,
+                       intermediate_size=14336, vocab_size=256000, rms_norm_eps=1e-6, rope_theta=10000.0,
+                       max_position_embeddings=8192, sliding_window=4096, query_pre_attn_scalar=256,
+                       attn_logit_softcapping=50.0, final_logit_softcapping=30.0, hidden_activation="gelu_pytorch_tanh",
+                       tie_word_embeddings=True),
+    "tiny-gemma2": dict(architectures=["Gemma2ForCausalLM"], model_type="gemma2", hidden_size=256, num_hidden_layers=2,
+                        num_attention_heads=4, num_key_value_heads=2, head_dim=256, intermediate_size=512,
+                        vocab_size=1024, rms_norm_eps=1e-6, rope_theta=10000.0, max_position_embeddings=2048,
+                        sliding_window=64, query_pre_attn_scalar=256, attn_logit_softcapping=50.0,
+                        final_logit_softcapping=30.0, hidden_activation="gelu_pytorch_tanh", tie_word_embeddings=True),
     "tiny-moe": dict(architectures=["Qwen3MoeForCausalLM"], model_type="qwen3_moe", hidden_size=256,
                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                      intermediate_size=512, moe_intermediate_size=128, num_experts=8, num_experts_per_tok=2,

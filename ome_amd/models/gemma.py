@@ -21,10 +21,7 @@ kernels:
 """
 from __future__ import annotations
 
-import math
-
 import torch
-import torch.nn.functional as F
 
 from ome_amd import ops
 from ome_amd.models.common import AttnMeta, PagedKVCache
@@ -69,8 +66,10 @@ class GemmaForCausalLM(LlamaForCausalLM):
         self.post_ff: list[torch.Tensor | None] = [None] * L
         mp = max_positions or cfg.max_position_embeddings
         self.cos_sin_local = self.cos_sin
-        if self.gen == 3 and hf.get("rope_local_base_freq"):
-            lc = ModelConfig(**{**cfg.__dict__, "rope_theta": float(hf["rope_local_base_freq"]), "rope_scaling": None})
+        rp = hf.get("rope_parameters") or {}
+        local_theta = (rp.get("sliding_attention") or {}).get("rope_theta") or hf.get("rope_local_base_freq")
+        if self.gen == 3 and local_theta:
+            lc = ModelConfig(**{**cfg.__dict__, "rope_theta": float(local_theta), "rope_scaling": None})
             self.cos_sin_local = rope_cos_sin(lc, mp, device=self.device)
         self.normalizer = torch.tensor(cfg.hidden_size ** 0.5, dtype=dtype).item()
 
