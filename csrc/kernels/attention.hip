@@ -235,7 +235,8 @@ __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const int* __res
                                                                  const float* __restrict__ part_o,
                                                                  const float* __restrict__ part_ml,
                                                                  bf16* __restrict__ out, int64_t out_stride, int Hq,
-                                                                 int part_size, int max_parts) {
+                                                                 int part_size, int max_parts,
+                                                                 const float* __restrict__ sinks = nullptr) {
   const int b = blockIdx.y, head = blockIdx.x, d = threadIdx.x;
   const int seq_len = seq_lens[b];
   const int nparts = (seq_len + part_size - 1) / part_size;
@@ -250,6 +251,7 @@ __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const int* __res
     L += w;
     acc += w * part_o[(base + p) * D + d];
   }
+  if (sinks != nullptr) L += fast_exp2(sinks[head] * 1.4426950408889634f - Mu);
   out[(int64_t)b * out_stride + (int64_t)head * D + d] = (bf16)(L > 0.f ? acc / L : 0.f);
 }
 
@@ -415,7 +417,7 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ seq_lens, bf16* __restrict__ out, int64_t out_stride, float* __restrict__ part_o,
     float* __restrict__ part_ml, int Hq, int Hkv, int part_size, int max_parts, Scaler scl, int window,
-    const int* __restrict__ order, float v_scale) {
+    const int* __restrict__ order, float v_scale, const float* __restrict__ sinks) {
   static_assert(P == 16, "decode kernel assumes 16-token pages");
   constexpr int NB = D / 16, KS = D / 32;
   // blockIdx.z walks sequences longest-first when the host provides ``order`` (the dispatcher
@@ -508,6 +510,8 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
       acc += sm_o[(w * G + h) * D + d] * f;
     }
     const int head = kvh * G + h;
+    // attention sink (GPT-OSS): an extra softmax column with logit sinks[head] and no value
+    if (sinks != nullptr && nparts == 1) L += fast_exp2(sinks[head] * 1.4426950408889634f - Mu);
     const float res = L > 0.f ? acc / L * v_scale : 0.f;
     if (nparts == 1) {
       out[(int64_t)b * out_stride + (int64_t)head * D + d] = (bf16)res;
@@ -527,14 +531,14 @@ static void launch_decode_v2(int variant, dim3 grid, size_t smem, hipStream_t st
                              int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                              int bt_stride, const int* seq_lens, void* out, int64_t out_stride, void* part_o,
                              void* part_ml, int Hq, int Hkv, int part_size, int max_parts, Scaler scl,
-                             int window, const int* order, float v_scale) {
+                             int window, const int* order, float v_scale, const float* sinks) {
   auto kern = variant == 2   ? paged_decode_v2_kernel<D, 16, 1, F>
               : variant == 4 ? paged_decode_v2_kernel<D, 16, 2, F>
                              : paged_decode_v2_kernel<D, 16, 0, F>;
   kern<<<grid, 256, smem, stream>>>((const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache,
                                     (const typename KVStore<F>::T*)v_cache, block_tables, bt_stride, seq_lens,
                                     (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size,
-                                    max_parts, scl, window, order, v_scale);
+                                    max_parts, scl, window, order, v_scale, sinks);
 }
 
 // kv_fmt: KVFmt of the cache; k_scale / v_scale: per-layer dequantisation scales (1 for bf16);
@@ -544,12 +548,12 @@ static int decode_dispatch(int variant, int kv_fmt, dim3 grid, int B, hipStream_
                            int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                            int bt_stride, const int* seq_lens, void* out, int64_t out_stride, void* part_o,
                            void* part_ml, int Hq, int Hkv, int part_size, int max_parts, Scaler scl, int window,
-                           const int* order, float v_scale) {
+                           const int* order, float v_scale, const float* sinks) {
   const int G = Hq / Hkv;
   const size_t smem = (8 * G + 4 * G * D) * sizeof(float);
 #define ARGS                                                                                                     \
   variant, grid, smem, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, out, out_stride, \
-      part_o, part_ml, Hq, Hkv, part_size, max_parts, scl, window, order, v_scale
+      part_o, part_ml, Hq, Hkv, part_size, max_parts, scl, window, order, v_scale, sinks
   if (kv_fmt == KV_BF16) launch_decode_v2<D, KV_BF16>(ARGS);
   else if (kv_fmt == KV_E4M3) launch_decode_v2<D, KV_E4M3>(ARGS);
   else launch_decode_v2<D, KV_E5M2>(ARGS);
@@ -558,7 +562,7 @@ static int decode_dispatch(int variant, int kv_fmt, dim3 grid, int B, hipStream_
   if (max_parts > 1) {
     paged_decode_reduce_kernel<D><<<dim3(Hq, B), D, 0, stream>>>(seq_lens, (const float*)part_o,
                                                                   (const float*)part_ml, (bf16*)out, out_stride, Hq,
-                                                                  part_size, max_parts);
+                                                                  part_size, max_parts, sinks);
     OME_CHECK_LAUNCH();
   }
   return 0;
@@ -568,7 +572,7 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
                              const int* block_tables, int bt_stride, const int* seq_lens, void* out,
                              int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
                              int part_size, int max_parts, float scale, int window, const int* order, int kv_fmt,
-                             float k_scale, float v_scale, float softcap, hipStream_t stream) {
+                             float k_scale, float v_scale, float softcap, const float* sinks, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
@@ -580,7 +584,7 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   // key-permuted tiles (16-B V loads; default: 5.38 vs 5.24 TB/s on the bench's context mix)
   const char* ve = getenv("OME_DECODE_ATTN");
   int variant = ve ? atoi(ve) : 4;
-  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f)) variant = 4;  // v1: bf16, D=128 only
+  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks)) variant = 4;  // v1: plain bf16 D=128
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
     paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(
@@ -597,7 +601,7 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   }
 #define ARGS                                                                                                      \
   variant, kv_fmt, grid, B, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, seq_lens, out,         \
-      out_stride, part_o, part_ml, Hq, Hkv, part_size, max_parts, scl, window, order, v_scale
+      out_stride, part_o, part_ml, Hq, Hkv, part_size, max_parts, scl, window, order, v_scale, sinks
   if (D == 64) return decode_dispatch<64>(ARGS);
   if (D == 256) return decode_dispatch<256>(ARGS);
   return decode_dispatch<128>(ARGS);
@@ -616,7 +620,8 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
-    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale) {
+    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale,
+    const float* __restrict__ sinks) {
   static_assert(P == 16, "prefill kernel assumes 16-token pages");
   constexpr int NB = D / 16, KS = D / 32;
   const int2 it = items[blockIdx.x];
@@ -728,7 +733,8 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
     for (int rb = 0; rb < 2; ++rb) {
       const int r = r0 + 16 * rb + n;
       if (r < q_len) {
-        const float inv = l_i[rb] > 0.f ? v_scale / l_i[rb] : 0.f;
+        const float lt = sinks ? l_i[rb] + fast_exp2(sinks[head] * 1.4426950408889634f - m_i[rb]) : l_i[rb];
+        const float inv = lt > 0.f ? v_scale / lt : 0.f;
         bf16* orow = out + (int64_t)(q0 + r) * out_stride + (int64_t)head * D;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
@@ -762,7 +768,8 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
-    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale) {
+    bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale,
+    const float* __restrict__ sinks) {
   constexpr int D = 128, P = 16, NB = D / 16, KS = D / 32;
   typedef typename KVRaw<F>::K8 Raw8;  // 8 consecutive cache elements
   __shared__ __attribute__((aligned(16))) bf16 sK[2][SUB][32 * PF_KLD];
@@ -930,7 +937,8 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   for (int rb = 0; rb < 2; ++rb) {
     const int r = r0 + 16 * rb + n;
     if (r < q_len) {
-      const float inv = l_i[rb] > 0.f ? v_scale / l_i[rb] : 0.f;
+      const float lt = sinks ? l_i[rb] + fast_exp2(sinks[head] * 1.4426950408889634f - m_i[rb]) : l_i[rb];
+      const float inv = lt > 0.f ? v_scale / lt : 0.f;
       bf16* orow = out + (int64_t)(q0 + r) * out_stride + (int64_t)head * D;
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
@@ -947,30 +955,31 @@ template <int D, int F>
 static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, const void* q, int64_t q_stride,
                            const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                            const int* cu_q, const int* kv_lens, const int* items, void* out, int64_t out_stride,
-                           int Hq, int Hkv, Scaler scl, int window, float v_scale) {
+                           int Hq, int Hkv, Scaler scl, int window, float v_scale, const float* sinks) {
   typedef typename KVStore<F>::T T;
   if constexpr (D == 128) {
     if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
       paged_prefill_v2_kernel<2, F><<<grid, 256, 0, stream>>>(
           (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale);
+          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks);
       return;
     }
   }
   const int nw = G < 8 ? G : 8;
   paged_prefill_kernel<D, 16, F><<<grid, 64 * nw, 0, stream>>>(
       (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale);
+      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks);
 }
 
 template <int D>
 static void prefill_dispatch(int kv_fmt, int variant, int G, dim3 grid, hipStream_t stream, const void* q,
                              int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                              int bt_stride, const int* cu_q, const int* kv_lens, const int* items, void* out,
-                             int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale) {
+                             int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale,
+                             const float* sinks) {
 #define ARGS                                                                                                   \
   variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, out, \
-      out_stride, Hq, Hkv, scl, window, v_scale
+      out_stride, Hq, Hkv, scl, window, v_scale, sinks
   if (kv_fmt == KV_BF16) launch_prefill<D, KV_BF16>(ARGS);
   else if (kv_fmt == KV_E4M3) launch_prefill<D, KV_E4M3>(ARGS);
   else launch_prefill<D, KV_E5M2>(ARGS);
@@ -981,7 +990,7 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
                               const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
                               const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
                               int P, float scale, int window, int kv_fmt, float k_scale, float v_scale,
-                              float softcap, hipStream_t stream) {
+                              float softcap, const float* sinks, hipStream_t stream) {
   if (n_items <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0) return -3;
@@ -993,7 +1002,7 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
   const int variant = ve ? atoi(ve) : 2;
 #define ARGS                                                                                                     \
   kv_fmt, variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, \
-      out, out_stride, Hq, Hkv, scl, window, v_scale
+      out, out_stride, Hq, Hkv, scl, window, v_scale, sinks
   if (D == 64) prefill_dispatch<64>(ARGS);
   else if (D == 256) prefill_dispatch<256>(ARGS);
   else prefill_dispatch<128>(ARGS);

@@ -23,8 +23,15 @@ __global__ __launch_bounds__(256) void act_and_mul_kernel(const bf16* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float gf = (float)g[j];
-    const float a = ACT == 0 ? silu(gf) : gelu_tanh(gf);
-    o[j] = (bf16)(a * (float)u[j]);
+    if constexpr (ACT == 2) {
+      // GPT-OSS clamped SwiGLU: (clamp(u, -7, 7) + 1) * g' * sigmoid(1.702 g'), g' = min(g, 7)
+      const float g2 = fminf(gf, 7.f);
+      const float u2 = fminf(fmaxf((float)u[j], -7.f), 7.f);
+      o[j] = (bf16)((u2 + 1.f) * g2 / (1.f + __expf(-1.702f * g2)));
+    } else {
+      const float a = ACT == 0 ? silu(gf) : gelu_tanh(gf);
+      o[j] = (bf16)(a * (float)u[j]);
+    }
   }
   st8(out + r * I + c * 8, o);
 }
@@ -46,8 +53,10 @@ OME_API int ome_act_and_mul(const void* x, void* out, int64_t rows, int I, int a
     bf16* op = (bf16*)out + r0 * I;
     if (act == 0)
       act_and_mul_kernel<0><<<g, 256, 0, stream>>>(xp, op, n, I);
-    else
+    else if (act == 1)
       act_and_mul_kernel<1><<<g, 256, 0, stream>>>(xp, op, n, I);
+    else
+      act_and_mul_kernel<2><<<g, 256, 0, stream>>>(xp, op, n, I);
   }
   OME_CHECK_LAUNCH();
   return 0;

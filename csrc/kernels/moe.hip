@@ -227,7 +227,8 @@ constexpr int GBM = 64, GBN = 64, GBK = 32, GLD = GBK + 8;
 __global__ __launch_bounds__(256) void moe_gemm_kernel(const bf16* __restrict__ A, int64_t lda,
                                                        const int* __restrict__ sorted_ids, int gather_div,
                                                        const bf16* __restrict__ W, const int* __restrict__ offsets,
-                                                       int E, int N, int K, bf16* __restrict__ out, int64_t ldo) {
+                                                       int E, int N, int K, bf16* __restrict__ out, int64_t ldo,
+                                                       const bf16* __restrict__ bias) {
   __shared__ __attribute__((aligned(16))) bf16 sA[GBM * GLD];
   __shared__ __attribute__((aligned(16))) bf16 sB[GBN * GLD];
   __shared__ int s_tile[3];
@@ -306,19 +307,23 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(const bf16* __restrict__ 
       for (int r = 0; r < 4; ++r) {
         const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
         const int col = n0 + wn + 16 * j + (lane & 15);
-        if (row < m_end && col < N) out[(int64_t)row * ldo + col] = (bf16)acc[i][j][r];
+        if (row < m_end && col < N) {
+          const float b = bias != nullptr ? (float)bias[(int64_t)e * N + col] : 0.f;  // per-expert bias (GPT-OSS)
+          out[(int64_t)row * ldo + col] = (bf16)(acc[i][j][r] + b);
+        }
       }
 }
 
+// bias: optional per-expert bias [E, N] added in the epilogue
 OME_API int ome_moe_gemm(const void* A, int64_t lda, const int* sorted_ids, int gather_div, const void* W,
                          const int* offsets, int E, int N, int K, int max_m_tiles, void* out, int64_t ldo,
-                         hipStream_t stream) {
+                         const void* bias, hipStream_t stream) {
   if (max_m_tiles <= 0) return 0;
   if (K % GBK != 0 || lda % 8 != 0) return -2;
   if (max_m_tiles > 65535) return -3;
   dim3 grid((N + GBN - 1) / GBN, max_m_tiles);
   moe_gemm_kernel<<<grid, 256, 0, stream>>>((const bf16*)A, lda, sorted_ids, gather_div, (const bf16*)W, offsets,
-                                            E, N, K, (bf16*)out, ldo);
+                                            E, N, K, (bf16*)out, ldo, (const bf16*)bias);
   OME_CHECK_LAUNCH();
   return 0;
 }

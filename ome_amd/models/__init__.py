@@ -24,6 +24,10 @@ MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM",
 
 
 def model_class(cfg: ModelConfig):
+    if cfg.architecture == "GptOssForCausalLM" or cfg.model_type == "gpt_oss":
+        from ome_amd.models.gpt_oss import GptOssForCausalLM
+
+        return GptOssForCausalLM
     if cfg.architecture in GEMMA_ARCHS or cfg.model_type in ("gemma", "gemma2", "gemma3", "gemma3_text"):
         from ome_amd.models.gemma import GemmaForCausalLM
 
@@ -42,7 +46,7 @@ def model_class(cfg: ModelConfig):
 
 
 def supported(arch: str) -> bool:
-    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS
+    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch == "GptOssForCausalLM"
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,

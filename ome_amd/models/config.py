@@ -201,6 +201,20 @@ PRESETS: dict[str, dict] = {
                         vocab_size=1024, rms_norm_eps=1e-6, rope_theta=10000.0, max_position_embeddings=2048,
                         sliding_window=64, query_pre_attn_scalar=256, attn_logit_softcapping=50.0,
                         final_logit_softcapping=30.0, hidden_activation="gelu_pytorch_tanh", tie_word_embeddings=True),
+    "gpt-oss-20b": dict(architectures=["GptOssForCausalLM"], model_type="gpt_oss", hidden_size=2880,
+                        num_hidden_layers=24, num_attention_heads=64, num_key_value_heads=8, head_dim=64,
+                        intermediate_size=2880, num_local_experts=32, num_experts_per_tok=4, vocab_size=201088,
+                        rms_norm_eps=1e-5, sliding_window=128, attention_bias=True, max_position_embeddings=131072,
+                        rope_parameters={"rope_type": "yarn", "factor": 32.0, "beta_fast": 32.0, "beta_slow": 1.0,
+                                         "truncate": False, "original_max_position_embeddings": 4096,
+                                         "rope_theta": 150000.0}),
+    "tiny-gpt-oss": dict(architectures=["GptOssForCausalLM"], model_type="gpt_oss", hidden_size=256,
+                         num_hidden_layers=2, num_attention_heads=8, num_key_value_heads=2, head_dim=64,
+                         intermediate_size=256, num_local_experts=8, num_experts_per_tok=2, vocab_size=1024,
+                         rms_norm_eps=1e-5, sliding_window=32, attention_bias=True, max_position_embeddings=2048,
+                         rope_parameters={"rope_type": "yarn", "factor": 8.0, "beta_fast": 32.0, "beta_slow": 1.0,
+                                          "truncate": False, "original_max_position_embeddings": 256,
+                                          "rope_theta": 150000.0}),
     "tiny-moe": dict(architectures=["Qwen3MoeForCausalLM"], model_type="qwen3_moe", hidden_size=256,
                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                      intermediate_size=512, moe_intermediate_size=128, num_experts=8, num_experts_per_tok=2,
@@ -279,7 +293,10 @@ def rope_cos_sin(cfg: ModelConfig, max_pos: int, device=None) -> torch.Tensor:
         def corr(nrot):
             return (rot * math.log(old / (nrot * 2 * math.pi))) / (2 * math.log(cfg.rope_theta))
 
-        lo, hi = max(math.floor(corr(bf)), 0), min(math.ceil(corr(bs)), rot - 1)
+        if sc.get("truncate", True):
+            lo, hi = max(math.floor(corr(bf)), 0), min(math.ceil(corr(bs)), rot - 1)
+        else:  # GPT-OSS: unrounded correction range
+            lo, hi = max(corr(bf), 0), min(corr(bs), rot - 1)
         ramp = torch.clamp((torch.arange(rot // 2, dtype=torch.float64) - lo) / max(hi - lo, 1e-3), 0, 1)
         extra = 1 - ramp
         inv = inv / factor * (1 - extra) + inv * extra

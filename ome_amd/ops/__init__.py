@@ -199,12 +199,13 @@ def moe_route(logits: torch.Tensor, k: int, renorm: bool = True, scoring: str = 
 
 
 def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
-              act: int = 0, scale: float = 1.0) -> torch.Tensor:
+              act: int = 0, scale: float = 1.0, b13: torch.Tensor | None = None,
+              b2: torch.Tensor | None = None) -> torch.Tensor:
     """Sparse MoE MLP on MFMA: align (counting sort by expert, on device) -> grouped GEMM gate_up
     with gathered A rows -> SiLU*mul -> grouped GEMM down -> weighted combine.  Shapes are
     static given T (graph-capturable); per-expert counts never leave the GPU."""
     if not _gpu(x):
-        return ref.fused_moe(x, topk_w, topk_ids, w13, w2, act, scale)
+        return ref.fused_moe(x, topk_w, topk_ids, w13, w2, act, scale, b13, b2)
     T, H = x.shape
     E, I2, _ = w13.shape
     I = I2 // 2
@@ -219,11 +220,11 @@ def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13
     max_tiles = -(-n // 64) + E
     gu = torch.empty(n, I2, dtype=x.dtype, device=dev)
     call("ome_moe_gemm", x.data_ptr(), x.stride(0), sorted_ids.data_ptr(), k, w13.data_ptr(), offsets.data_ptr(),
-         E, I2, H, max_tiles, gu.data_ptr(), gu.stride(0), stream_ptr())
+         E, I2, H, max_tiles, gu.data_ptr(), gu.stride(0), ptr(b13), stream_ptr())
     h = act_and_mul(gu, act)
     y = torch.empty(n, H, dtype=x.dtype, device=dev)
     call("ome_moe_gemm", h.data_ptr(), h.stride(0), None, 0, w2.data_ptr(), offsets.data_ptr(), E, H, I,
-         max_tiles, y.data_ptr(), y.stride(0), stream_ptr())
+         max_tiles, y.data_ptr(), y.stride(0), ptr(b2), stream_ptr())
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     call("ome_moe_combine", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), float(scale),
          stream_ptr())
@@ -242,12 +243,13 @@ class DecodeWorkspace:
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeWorkspace | None = None,
                  window: int = -1, out=None, order: torch.Tensor | None = None, k_scale: float = 1.0,
-                 v_scale: float = 1.0, softcap: float = 0.0) -> torch.Tensor:
+                 v_scale: float = 1.0, softcap: float = 0.0, sinks: torch.Tensor | None = None) -> torch.Tensor:
     """q [B, Hq, D] -> [B, Hq, D].  ``order`` (int32 [B], optional): sequence visit order for the
     workgroup dispatcher (longest first balances the tail).  The cache may be bf16 or fp8
     (``k_scale`` / ``v_scale`` dequantise it)."""
     if not _gpu(q):
-        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window, k_scale, v_scale, softcap)
+        r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window, k_scale, v_scale, softcap,
+                             sinks)
         if out is not None:
             out.copy_(r)
             return out
@@ -261,8 +263,16 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeW
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(seq_lens).data_ptr(), out.data_ptr(),
          out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
          float(scale), int(window), _i32(order).data_ptr() if order is not None else None, kv_format(k_cache),
-         float(k_scale), float(v_scale), float(softcap), stream_ptr())
+         float(k_scale), float(v_scale), float(softcap), _sinks(sinks), stream_ptr())
     return out
+
+
+def _sinks(s: torch.Tensor | None):
+    """Attention-sink logits (GPT-OSS): fp32 [Hq] on the device, or None."""
+    if s is None:
+        return None
+    assert s.dtype == torch.float32 and s.is_contiguous()
+    return s.data_ptr()
 
 
 class MLAWorkspace:
@@ -320,12 +330,13 @@ def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) ->
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale, window: int = -1,
-                  out=None, k_scale: float = 1.0, v_scale: float = 1.0, softcap: float = 0.0) -> torch.Tensor:
+                  out=None, k_scale: float = 1.0, v_scale: float = 1.0, softcap: float = 0.0,
+                  sinks: torch.Tensor | None = None) -> torch.Tensor:
     """q [Tq, Hq, D]; items int32 [n, 2] from :func:`prefill_work_items`.  ``softcap`` > 0:
     attention-logit soft-capping ``cap * tanh(score / cap)`` (Gemma-2)."""
     if not _gpu(q):
         r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window, k_scale, v_scale,
-                              softcap)
+                              softcap, sinks)
         if out is not None:
             out.copy_(r)
             return out
@@ -336,7 +347,8 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     call("ome_paged_prefill", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
          _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),
-         int(window), kv_format(k_cache), float(k_scale), float(v_scale), float(softcap), stream_ptr())
+         int(window), kv_format(k_cache), float(k_scale), float(v_scale), float(softcap), _sinks(sinks),
+         stream_ptr())
     return out
 
 

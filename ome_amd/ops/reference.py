@@ -81,6 +81,10 @@ def kv_cache_write(k, v, k_cache, v_cache, slots, P, k_scale=1.0, v_scale=1.0) -
 def act_and_mul(x: torch.Tensor, act: int = 0) -> torch.Tensor:
     I = x.shape[-1] // 2
     g, u = x[..., :I].float(), x[..., I:].float()
+    if act == 2:  # GPT-OSS clamped SwiGLU
+        g = g.clamp(max=7.0)
+        u = u.clamp(-7.0, 7.0)
+        return ((u + 1) * g * torch.sigmoid(1.702 * g)).to(x.dtype)
     a = torch.nn.functional.silu(g) if act == 0 else torch.nn.functional.gelu(g, approximate="tanh")
     return (a * u).to(x.dtype)
 
@@ -107,8 +111,17 @@ def _cap(s: torch.Tensor, softcap: float) -> torch.Tensor:
     return softcap * torch.tanh(s / softcap) if softcap and softcap > 0 else s
 
 
+def _softmax_sink(s: torch.Tensor, sink) -> torch.Tensor:
+    """softmax over [scores, sink] with the sink column dropped (GPT-OSS attention sinks)."""
+    if sink is None:
+        return torch.softmax(s, -1)
+    col = sink.float().reshape(*([1] * (s.dim() - 1)), 1).expand(*s.shape[:-1], 1) if sink.dim() == 0 else sink
+    full = torch.cat([s, col], -1)
+    return torch.softmax(full, -1)[..., :-1]
+
+
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, k_scale=1.0,
-                 v_scale=1.0, softcap=0.0) -> torch.Tensor:
+                 v_scale=1.0, softcap=0.0, sinks=None) -> torch.Tensor:
     B, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -123,12 +136,13 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, 
             k, v = k[lo:], v[lo:]
             qh = q[b, h * G:(h + 1) * G].float()
             s = _cap((qh @ k.T) * scale, softcap)
-            out[b, h * G:(h + 1) * G] = (torch.softmax(s, -1) @ v).to(q.dtype)
+            sk = None if sinks is None else sinks[h * G:(h + 1) * G].float().view(G, 1)
+            out[b, h * G:(h + 1) * G] = (_softmax_sink(s, sk) @ v).to(q.dtype)
     return out
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window=-1, k_scale=1.0,
-                  v_scale=1.0, softcap=0.0) -> torch.Tensor:
+                  v_scale=1.0, softcap=0.0, sinks=None) -> torch.Tensor:
     Tq, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -149,7 +163,8 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, windo
             qh = q[q0:q1, h * G:(h + 1) * G].float().transpose(0, 1)  # [G, ql, D]
             sc = _cap((qh @ k.T) * scale, softcap)
             sc = sc.masked_fill(~mask[None], float("-inf"))
-            o = torch.softmax(sc, -1) @ v
+            sk = None if sinks is None else sinks[h * G:(h + 1) * G].float().view(G, 1, 1).expand(G, sc.shape[1], 1)
+            o = _softmax_sink(sc, sk) @ v
             out[q0:q1, h * G:(h + 1) * G] = o.transpose(0, 1).to(q.dtype)
     return out
 
@@ -234,16 +249,22 @@ def moe_route(logits, k: int, renorm: bool, scoring: str = "softmax", bias=None,
     return w.float(), ids.to(torch.int32)
 
 
-def fused_moe(x, topk_w, topk_ids, w13, w2, act: int = 0, scale: float = 1.0):
-    """x [T, H]; w13 [E, 2I, H] (gate rows then up rows); w2 [E, H, I]."""
+def fused_moe(x, topk_w, topk_ids, w13, w2, act: int = 0, scale: float = 1.0, b13=None, b2=None):
+    """x [T, H]; w13 [E, 2I, H] (gate rows then up rows); w2 [E, H, I]; optional per-expert
+    biases b13 [E, 2I], b2 [E, H] (GPT-OSS)."""
     T, H = x.shape
     out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
     xf = x.float()
     for e in torch.unique(topk_ids).tolist():
         tok, slot = (topk_ids == e).nonzero(as_tuple=True)
         gu = xf[tok] @ w13[e].float().t()
+        if b13 is not None:
+            gu = gu + b13[e].float()
         h = act_and_mul(gu.to(x.dtype), act).float()
-        y = (h.to(x.dtype).float() @ w2[e].float().t()).to(x.dtype).float()
+        y = h.to(x.dtype).float() @ w2[e].float().t()
+        if b2 is not None:
+            y = y + b2[e].float()
+        y = y.to(x.dtype).float()
         out.index_add_(0, tok, y * topk_w[tok, slot].float()[:, None])
     return (out * scale).to(x.dtype)
 

@@ -295,3 +295,42 @@ def test_rope_qkv_cache_head_dims(D):
     _close(q1, q2, atol=3e-2)
     _close(k1, k2, atol=3e-2)
     assert torch.equal(v1, v2)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("parts", [4096, 256])
+def test_paged_attention_sinks(D, parts):
+    """GPT-OSS attention sinks in decode (incl. split-K reduce) and prefill."""
+    Hq, Hkv, P = 16, 2, 16
+    seq_lens = [1, 37, 300, 1000]
+    npages = sum(-(-L // P) for L in seq_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    bt = _block_tables(seq_lens, P, npages)
+    sl = torch.tensor(seq_lens, dtype=torch.int32, device=DEV)
+    sinks = torch.randn(Hq, device=DEV, dtype=torch.float32) * 2
+    q = torch.randn(len(seq_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    ws = ops.DecodeWorkspace(len(seq_lens), Hq, D, 2048, parts, DEV)
+    out = ops.paged_decode(q, kc, vc, bt, sl, D ** -0.5, ws, window=128, sinks=sinks)
+    _close(out, ref.paged_decode(q, kc, vc, bt, sl, D ** -0.5, 128, 1.0, 1.0, 0.0, sinks), atol=2e-2)
+    q_lens = [37, 64, 1, 100]
+    kv_lens = [37, 80, 300, 100]
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    items = torch.tensor(ops.prefill_work_items(q_lens, kv_lens), dtype=torch.int32, device=DEV)
+    bt2 = _block_tables(kv_lens, P, npages)
+    qp = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    outp = ops.paged_prefill(qp, kc, vc, bt2, cu, kl, items, D ** -0.5, sinks=sinks)
+    _close(outp, ref.paged_prefill(qp, kc, vc, bt2, cu, kl, D ** -0.5, -1, 1.0, 1.0, 0.0, sinks), atol=2e-2)
+
+
+def test_fused_moe_bias_and_gptoss_act():
+    T, H, I, E, k = 37, 256, 128, 8, 4
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    w13 = torch.randn(E, 2 * I, H, device=DEV, dtype=torch.bfloat16) * 0.1
+    w2 = torch.randn(E, H, I, device=DEV, dtype=torch.bfloat16) * 0.1
+    b13 = torch.randn(E, 2 * I, device=DEV, dtype=torch.bfloat16)
+    b2 = torch.randn(E, H, device=DEV, dtype=torch.bfloat16)
+    logits = torch.randn(T, E, device=DEV, dtype=torch.bfloat16)
+    tw, tid = ops.moe_route(logits, k, True)
+    out = ops.fused_moe(x, tw, tid, w13, w2, 2, 1.0, b13, b2)
+    _close(out, ref.fused_moe(x, tw, tid, w13, w2, 2, 1.0, b13, b2), atol=5e-2, rtol=5e-2)
