@@ -36,6 +36,21 @@ __global__ __launch_bounds__(256) void act_and_mul_kernel(const bf16* __restrict
   st8(out + r * I + c * 8, o);
 }
 
+// Non-gated activation (Starcoder2 / GPT-NeoX MLPs), in place on a contiguous bf16 tensor:
+// ACT 1 = GELU-tanh, 3 = GELU (erf), 0 = SiLU
+template <int ACT>
+__global__ __launch_bounds__(256) void act_kernel(bf16* __restrict__ x, int64_t nvec) {
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
+    bf16x8 a = ld8(x + v * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = (float)a[j];
+      a[j] = (bf16)(ACT == 0 ? silu(f) : ACT == 1 ? gelu_tanh(f) : 0.5f * f * (1.f + erff(f * 0.7071067811865476f)));
+    }
+    st8(x + v * 8, a);
+  }
+}
+
 static inline int grid_for(int64_t work, int nt) {
   int64_t g = (work + nt - 1) / nt;
   if (g > 2048) g = 2048;
@@ -58,6 +73,18 @@ OME_API int ome_act_and_mul(const void* x, void* out, int64_t rows, int I, int a
     else
       act_and_mul_kernel<2><<<g, 256, 0, stream>>>(xp, op, n, I);
   }
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+OME_API int ome_act(void* x, int64_t n, int act, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (n % 8) return -2;
+  const int64_t nv = n / 8;
+  const int g = grid_for(nv, 256);
+  if (act == 0) act_kernel<0><<<g, 256, 0, stream>>>((bf16*)x, nv);
+  else if (act == 1) act_kernel<1><<<g, 256, 0, stream>>>((bf16*)x, nv);
+  else act_kernel<3><<<g, 256, 0, stream>>>((bf16*)x, nv);
   OME_CHECK_LAUNCH();
   return 0;
 }

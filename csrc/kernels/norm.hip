@@ -97,6 +97,65 @@ __global__ __launch_bounds__(NT) void fused_add_rmsnorm_kernel(bf16* __restrict_
   }
 }
 
+// LayerNorm with bias (Starcoder2, GPT-NeoX): out = (x - mean) * rstd * w + b; with ``res`` set the
+// residual add is fused in front (res <- x + res, normalise res, write x), like fused_add_rmsnorm.
+template <int NT, int CHUNKS, bool ADD>
+__global__ __launch_bounds__(NT) void layernorm_kernel(bf16* __restrict__ x, int64_t x_stride,
+                                                       bf16* __restrict__ res, int64_t res_stride,
+                                                       const bf16* __restrict__ w, const bf16* __restrict__ b,
+                                                       bf16* __restrict__ out, int64_t out_stride, int H, float eps) {
+  __shared__ float red[NT / 64];
+  const int row = blockIdx.x;
+  bf16* xr = x + row * x_stride;
+  const int nvec = H >> 3;
+  bf16x8 v[CHUNKS];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) {
+      v[c] = ld8(xr + i * 8);
+      if constexpr (ADD) {
+        bf16* rr = res + row * res_stride;
+        const bf16x8 r = ld8(rr + i * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (bf16)((float)v[c][j] + (float)r[j]);
+        st8(rr + i * 8, v[c]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (float)v[c][j];
+    }
+  }
+  const float mean = block_sum<NT>(s, red) / (float)H;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (float)v[c][j] - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(block_sum<NT>(ss, red) / (float)H + eps);
+  bf16* orow = ADD ? xr : out + row * out_stride;
+#pragma unroll
+  for (int c = 0; c < CHUNKS; ++c) {
+    const int i = threadIdx.x + c * NT;
+    if (i < nvec) {
+      const bf16x8 wv = ld8(w + i * 8);
+      bf16x8 bv = {};
+      if (b != nullptr) bv = ld8(b + i * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)(((float)v[c][j] - mean) * rstd * (float)wv[j] + (float)bv[j]);
+      st8(orow + i * 8, o);
+    }
+  }
+}
+
 #define DISPATCH_CHUNKS(H, NT, ...)                         \
   do {                                                      \
     const int _c = ((H) / 8 + (NT)-1) / (NT);               \
@@ -131,6 +190,23 @@ OME_API int ome_fused_add_rmsnorm(void* x, int64_t x_stride, void* res, int64_t 
   } else {
     DISPATCH_CHUNKS(H, 256, (fused_add_rmsnorm_kernel<256, CH><<<rows, 256, 0, stream>>>(
                                 (bf16*)x, x_stride, (bf16*)res, res_stride, (const bf16*)w, H, eps)));
+  }
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// res == nullptr: out = LN(x); else res <- x + res, x <- LN(res) (out unused)
+OME_API int ome_layernorm(void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w, const void* b,
+                          void* out, int64_t out_stride, int rows, int H, float eps, hipStream_t stream) {
+  if (H % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -2;
+  if (res != nullptr) {
+    DISPATCH_CHUNKS(H, 256, (layernorm_kernel<256, CH, true><<<rows, 256, 0, stream>>>(
+                                (bf16*)x, x_stride, (bf16*)res, res_stride, (const bf16*)w, (const bf16*)b,
+                                nullptr, 0, H, eps)));
+  } else {
+    DISPATCH_CHUNKS(H, 256, (layernorm_kernel<256, CH, false><<<rows, 256, 0, stream>>>(
+                                (bf16*)x, x_stride, nullptr, 0, (const bf16*)w, (const bf16*)b, (bf16*)out,
+                                out_stride, H, eps)));
   }
   OME_CHECK_LAUNCH();
   return 0;

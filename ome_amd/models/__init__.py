@@ -19,6 +19,7 @@ DENSE_ARCHS = {
     "Qwen2ForRewardModel", "Phi3ForCausalLM", "GraniteForCausalLM", "SmolLM3ForCausalLM",
 }
 GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
+LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM"}
 MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM", "DeepseekV2ForCausalLM",
              "DeepseekV3ForCausalLM", "PhiMoEForCausalLM"}
 
@@ -32,6 +33,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.gemma import GemmaForCausalLM
 
         return GemmaForCausalLM
+    if cfg.architecture in LAYERNORM_ARCHS or cfg.model_type in ("starcoder2", "gpt_neox"):
+        from ome_amd.models.layernorm_lm import LayerNormForCausalLM
+
+        return LayerNormForCausalLM
     if cfg.is_mla:
         from ome_amd.models.deepseek import DeepseekForCausalLM
 
@@ -46,7 +51,8 @@ def model_class(cfg: ModelConfig):
 
 
 def supported(arch: str) -> bool:
-    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch == "GptOssForCausalLM"
+    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or \
+        arch == "GptOssForCausalLM"
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,

@@ -93,11 +93,14 @@ class ModelConfig:
         nh = text.get("num_attention_heads", 32)
         hd = text.get("head_dim") or H // nh
         mt = text.get("model_type", cfg.get("model_type", "llama"))
-        rope_theta, rope_scaling = text.get("rope_theta", 10000.0), text.get("rope_scaling")
+        rope_theta = text.get("rope_theta", text.get("rotary_emb_base", 10000.0))
+        rope_scaling = text.get("rope_scaling")
+        prf = text.get("partial_rotary_factor") or text.get("rotary_pct") or 1.0
         rp = text.get("rope_parameters")  # transformers >= 5: {rope_type, rope_theta, ...} or per layer type
         if isinstance(rp, dict) and rp:
             glob = rp.get("full_attention", rp) if ("full_attention" in rp or "sliding_attention" in rp) else rp
             rope_theta = glob.get("rope_theta", rope_theta)
+            prf = glob.get("partial_rotary_factor") or prf
             if glob.get("rope_type", "default") != "default":
                 rope_scaling = dict(glob)
         c = cls(
@@ -110,16 +113,16 @@ class ModelConfig:
             head_dim=hd,
             intermediate_size=text.get("intermediate_size", 4 * H),
             vocab_size=text.get("vocab_size", 32000),
-            rms_norm_eps=text.get("rms_norm_eps", 1e-6),
+            rms_norm_eps=text.get("rms_norm_eps") or text.get("layer_norm_eps") or text.get("norm_epsilon") or 1e-6,
             rope_theta=rope_theta,
             rope_scaling=rope_scaling,
-            partial_rotary_factor=text.get("partial_rotary_factor", 1.0),
+            partial_rotary_factor=float(prf),
             max_position_embeddings=text.get("max_position_embeddings", 4096),
             tie_word_embeddings=bool(cfg.get("tie_word_embeddings", text.get("tie_word_embeddings", False))),
-            attention_bias=bool(text.get("attention_bias", mt in ("qwen2", "qwen2_moe"))),
+            attention_bias=bool(text.get("attention_bias", text.get("use_bias", mt in ("qwen2", "qwen2_moe")))),
             qk_norm=mt in ("qwen3", "qwen3_moe", "gemma3", "gemma3_text"),
             hidden_act=text.get("hidden_act", text.get("hidden_activation", "silu")),
-            sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt == "mistral") else None,
+            sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt in ("mistral", "starcoder2")) else None,
             torch_dtype=str(text.get("torch_dtype", cfg.get("torch_dtype", "bfloat16"))),
         )
         # MoE variants
@@ -215,6 +218,24 @@ PRESETS: dict[str, dict] = {
                          rope_parameters={"rope_type": "yarn", "factor": 8.0, "beta_fast": 32.0, "beta_slow": 1.0,
                                           "truncate": False, "original_max_position_embeddings": 256,
                                           "rope_theta": 150000.0}),
+    "starcoder2-7b": dict(architectures=["Starcoder2ForCausalLM"], model_type="starcoder2", hidden_size=4608,
+                          num_hidden_layers=32, num_attention_heads=36, num_key_value_heads=4,
+                          intermediate_size=18432, vocab_size=49152, norm_epsilon=1e-5, rope_theta=1000000.0,
+                          sliding_window=4096, max_position_embeddings=16384, use_bias=True,
+                          hidden_act="gelu_pytorch_tanh", tie_word_embeddings=False),
+    "tiny-starcoder2": dict(architectures=["Starcoder2ForCausalLM"], model_type="starcoder2", hidden_size=256,
+                            num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2,
+                            intermediate_size=512, vocab_size=1024, norm_epsilon=1e-5, rope_theta=10000.0,
+                            sliding_window=64, max_position_embeddings=2048, use_bias=True,
+                            hidden_act="gelu_pytorch_tanh", tie_word_embeddings=True),
+    "pythia-1.4b": dict(architectures=["GPTNeoXForCausalLM"], model_type="gpt_neox", hidden_size=2048,
+                        num_hidden_layers=24, num_attention_heads=16, intermediate_size=8192, vocab_size=50304,
+                        layer_norm_eps=1e-5, rotary_pct=0.25, rotary_emb_base=10000, use_parallel_residual=True,
+                        hidden_act="gelu", max_position_embeddings=2048, attention_bias=True),
+    "tiny-neox": dict(architectures=["GPTNeoXForCausalLM"], model_type="gpt_neox", hidden_size=256,
+                      num_hidden_layers=2, num_attention_heads=4, intermediate_size=1024, vocab_size=1024,
+                      layer_norm_eps=1e-5, rotary_pct=0.25, rotary_emb_base=10000, use_parallel_residual=True,
+                      hidden_act="gelu", max_position_embeddings=2048, attention_bias=True),
     "tiny-moe": dict(architectures=["Qwen3MoeForCausalLM"], model_type="qwen3_moe", hidden_size=256,
                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                      intermediate_size=512, moe_intermediate_size=128, num_experts=8, num_experts_per_tok=2,

@@ -148,9 +148,8 @@ class GemmaForCausalLM(LlamaForCausalLM):
         cfg, tp, D = self.cfg, self.tp, self.D
         T = ids.shape[0]
         x, residual = self._stage_input(ids, input_embeds)
-        first = self.layers[0]
         for i in self.layers:
-            if i > first:
+            if i > 0:
                 ops.fused_add_rmsnorm(x, residual, self.ln1[i], self.eps)
             qkv = linear(x, self.w_qkv[i], self.b_qkv[i])
             q = torch.empty(T, tp.hq, D, dtype=self.dtype, device=x.device)

@@ -45,6 +45,39 @@ def fused_add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: 
          x2.shape[0], H, float(eps), stream_ptr())
 
 
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, eps: float) -> torch.Tensor:
+    """LayerNorm with optional bias (Starcoder2 / GPT-NeoX)."""
+    if not _gpu(x):
+        return ref.layernorm(x, w, b, eps)
+    H = x.shape[-1]
+    x2 = x.reshape(-1, H)
+    assert x2.stride(-1) == 1 and x.dtype == torch.bfloat16
+    out = torch.empty_like(x2)
+    call("ome_layernorm", x2.data_ptr(), x2.stride(0), None, 0, w.data_ptr(), ptr(b), out.data_ptr(), out.stride(0),
+         x2.shape[0], H, float(eps), stream_ptr())
+    return out.view(x.shape)
+
+
+def fused_add_layernorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None,
+                        eps: float) -> None:
+    """In place: res <- x + res; x <- layernorm(res) * w + b."""
+    if not _gpu(x):
+        return ref.fused_add_layernorm(x, res, w, b, eps)
+    H = x.shape[-1]
+    x2, r2 = x.view(-1, H), res.view(-1, H)
+    call("ome_layernorm", x2.data_ptr(), x2.stride(0), r2.data_ptr(), r2.stride(0), w.data_ptr(), ptr(b), None, 0,
+         x2.shape[0], H, float(eps), stream_ptr())
+
+
+def act(x: torch.Tensor, kind: int) -> torch.Tensor:
+    """In place non-gated activation: 0 SiLU, 1 GELU-tanh, 3 GELU (erf)."""
+    if not _gpu(x):
+        return ref.act(x, kind)
+    assert x.is_contiguous() and x.dtype == torch.bfloat16
+    call("ome_act", x.data_ptr(), x.numel(), int(kind), stream_ptr())
+    return x
+
+
 #: paged KV-cache element formats understood by the kernels (csrc/kernels/common.h KVFmt)
 KV_FORMATS = {torch.bfloat16: 0, torch.float8_e4m3fn: 1, torch.float8_e5m2: 2}
 

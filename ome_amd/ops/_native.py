@@ -30,6 +30,8 @@ _SIGNATURES = {
                                i32, f32, f32, vp],
         "ome_kv_cache_write": [vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, f32, f32, vp],
         "ome_act_and_mul": [vp, vp, i64, i32, i32, vp],
+        "ome_act": [vp, i64, i32, vp],
+        "ome_layernorm": [vp, i64, vp, i64, vp, vp, vp, i64, i32, i32, f32, vp],
         "ome_embedding": [vp, vp, vp, i32, i32, i32, i32, vp],
         "ome_pool": [vp, vp, vp, i32, i32, i32, i32, vp],
         "ome_fill_pending": [vp, vp, vp, i32, vp],

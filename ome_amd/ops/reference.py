@@ -23,6 +23,29 @@ def fused_add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: 
     x.copy_(rmsnorm(s, w, eps))
 
 
+def layernorm(x: torch.Tensor, w: torch.Tensor, b, eps: float) -> torch.Tensor:
+    return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), w.float(), None if b is None else b.float(),
+                                          eps).to(x.dtype)
+
+
+def fused_add_layernorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b, eps: float) -> None:
+    s = (x.float() + res.float()).to(res.dtype)
+    res.copy_(s)
+    x.copy_(layernorm(s, w, b, eps))
+
+
+def act(x: torch.Tensor, kind: int) -> torch.Tensor:
+    f = x.float()
+    if kind == 0:
+        y = torch.nn.functional.silu(f)
+    elif kind == 1:
+        y = torch.nn.functional.gelu(f, approximate="tanh")
+    else:
+        y = torch.nn.functional.gelu(f)
+    x.copy_(y.to(x.dtype))
+    return x
+
+
 def apply_rope(x: torch.Tensor, cs: torch.Tensor, rot_dim: int) -> torch.Tensor:
     """x [T, H, D] float, cs [T, rot_dim] (cos | sin)."""
     half = rot_dim // 2
