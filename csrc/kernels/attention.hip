@@ -31,6 +31,13 @@
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// First key a query at position ``qpos`` may see.  ``window`` > 0: sliding window of that many keys
+// (Mistral / Gemma / GPT-OSS); ``window`` < -1: chunked attention with chunks of -window tokens
+// (Llama-4 RoPE layers: keys in the query's own chunk only); otherwise full causal.
+__device__ __forceinline__ int attn_lo(int qpos, int window) {
+  return window > 0 ? max(0, qpos - window + 1) : (window < -1 ? qpos - qpos % (-window) : 0);
+}
+
 // raw score -> log2-domain logit: s * scale * log2(e), or with logit soft-capping (Gemma-2:
 // cap * tanh(s * scale / cap)) cap * log2(e) * tanh(s * scale / cap)
 struct Scaler {
@@ -117,7 +124,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   const int G = Hq / Hkv;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n = lane & 15, g = lane >> 4;
-  const int lo = window > 0 ? max(0, seq_len - window) : 0;
+  const int lo = attn_lo(seq_len - 1, window);
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sm_m = smem;              // [4][16]
@@ -430,7 +437,7 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
   const int G = Hq / Hkv;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n = lane & 15, g = lane >> 4;
-  const int lo = window > 0 ? max(0, seq_len - window) : 0;
+  const int lo = attn_lo(seq_len - 1, window);
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sm_m = smem;              // [4][G]
@@ -638,7 +645,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
   const int r_hi = min(r0 + 32, q_len);
   const int kv_end = min(kv_len, prefix + r_hi);
   int kv_lo = 0;
-  if (window > 0) kv_lo = max(0, prefix + r0 - window + 1) & ~31;
+  kv_lo = attn_lo(prefix + r0, window) & ~31;
   const int* bt = block_tables + (int64_t)s * bt_stride;
   const int64_t kpage = (int64_t)Hkv * P * D;
 
@@ -677,7 +684,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
           sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
         }
       }
-      const bool need_mask = (kb + 32 > prefix + r0 + 1) || (kb + 32 > kv_len) || (window > 0);
+      const bool need_mask = (kb + 32 > prefix + r0 + 1) || (kb + 32 > kv_len) || (window > 0 || window < -1);
       bf16x8 pb[2];
       float alpha[2];
 #pragma unroll
@@ -691,7 +698,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
             float v = scl(sc[rb][X][i]);
             if (need_mask) {
               const int key = kb + 16 * X + 4 * g + i;
-              const bool ok = key <= qpos && key < kv_len && (window <= 0 || key > qpos - window);
+              const bool ok = key <= qpos && key < kv_len && key >= attn_lo(qpos, window);
               v = ok ? v : OME_NEG_INF;
             }
             sc[rb][X][i] = v;
@@ -791,7 +798,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   const int item_hi = min(r0_item + rows_per_item, q_len);
   const int kv_end = min(kv_len, prefix + item_hi);
   int kv_lo = 0;
-  if (window > 0) kv_lo = max(0, prefix + r0_item - window + 1) & ~31;
+  kv_lo = attn_lo(prefix + r0_item, window) & ~31;
   const int* bt = block_tables + (int64_t)s * bt_stride;
   const int64_t kpage = (int64_t)Hkv * P * D;
 
@@ -879,7 +886,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
           sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
         }
       }
-      const bool need_mask = (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0);
+      const bool need_mask = (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0 || window < -1);
       bf16x8 pb[2];
       float alpha[2];
 #pragma unroll
@@ -893,7 +900,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
             float v = scl(sc[rb][X][i]);
             if (need_mask) {
               const int key = kbu + 16 * X + 4 * g + i;
-              const bool ok = key <= qpos && key < kv_len && (window <= 0 || key > qpos - window);
+              const bool ok = key <= qpos && key < kv_len && key >= attn_lo(qpos, window);
               v = ok ? v : OME_NEG_INF;
             }
             sc[rb][X][i] = v;

@@ -20,6 +20,7 @@ DENSE_ARCHS = {
 }
 GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
 LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM"}
+LLAMA4_ARCHS = {"Llama4ForCausalLM", "Llama4ForConditionalGeneration"}
 MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM", "DeepseekV2ForCausalLM",
              "DeepseekV3ForCausalLM", "PhiMoEForCausalLM"}
 
@@ -33,6 +34,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.gemma import GemmaForCausalLM
 
         return GemmaForCausalLM
+    if cfg.architecture in LLAMA4_ARCHS or cfg.model_type in ("llama4", "llama4_text"):
+        from ome_amd.models.llama4 import Llama4ForCausalLM
+
+        return Llama4ForCausalLM
     if cfg.architecture in LAYERNORM_ARCHS or cfg.model_type in ("starcoder2", "gpt_neox"):
         from ome_amd.models.layernorm_lm import LayerNormForCausalLM
 
@@ -51,7 +56,7 @@ def model_class(cfg: ModelConfig):
 
 
 def supported(arch: str) -> bool:
-    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or \
+    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or \
         arch == "GptOssForCausalLM"
 
 

@@ -151,6 +151,8 @@ class ModelConfig:
             c.quantization = q.get("quant_method") or q.get("quant_type")
         c.is_embedding = ("Embedding" in arch) or (arch.endswith("Model") and "ForCausalLM" not in arch)
         c.extra = {k: v for k, v in cfg.items() if k not in ("text_config",)}
+        if text is not cfg:  # multimodal wrappers: the language model's keys win
+            c.extra.update({k: v for k, v in text.items() if k != "quantization_config"})
         return c
 
     @classmethod
@@ -236,6 +238,27 @@ PRESETS: dict[str, dict] = {
                       num_hidden_layers=2, num_attention_heads=4, intermediate_size=1024, vocab_size=1024,
                       layer_norm_eps=1e-5, rotary_pct=0.25, rotary_emb_base=10000, use_parallel_residual=True,
                       hidden_act="gelu", max_position_embeddings=2048, attention_bias=True),
+    "llama-4-scout-17b-16e": dict(architectures=["Llama4ForConditionalGeneration"], model_type="llama4",
+                                  text_config=dict(model_type="llama4_text", hidden_size=5120, num_hidden_layers=48,
+                                                   num_attention_heads=40, num_key_value_heads=8, head_dim=128,
+                                                   intermediate_size=8192, intermediate_size_mlp=16384,
+                                                   num_local_experts=16, num_experts_per_tok=1, vocab_size=202048,
+                                                   rms_norm_eps=1e-5, max_position_embeddings=10485760,
+                                                   attention_chunk_size=8192, interleave_moe_layer_step=1,
+                                                   use_qk_norm=True, no_rope_layer_interval=4, floor_scale=8192,
+                                                   attn_scale=0.1, attn_temperature_tuning=True,
+                                                   rope_theta=500000.0,
+                                                   rope_scaling={"rope_type": "llama3", "factor": 16.0,
+                                                                 "low_freq_factor": 1.0, "high_freq_factor": 1.0,
+                                                                 "original_max_position_embeddings": 8192})),
+    "tiny-llama4": dict(architectures=["Llama4ForCausalLM"], model_type="llama4_text", hidden_size=256,
+                        num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
+                        intermediate_size=256, intermediate_size_mlp=512, num_local_experts=8, num_experts_per_tok=1,
+                        vocab_size=1024, rms_norm_eps=1e-5, max_position_embeddings=4096, attention_chunk_size=64,
+                        interleave_moe_layer_step=2, use_qk_norm=True, no_rope_layer_interval=4, floor_scale=32,
+                        attn_scale=0.1, rope_theta=500000.0,
+                        rope_scaling={"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                      "high_freq_factor": 4.0, "original_max_position_embeddings": 256}),
     "tiny-moe": dict(architectures=["Qwen3MoeForCausalLM"], model_type="qwen3_moe", hidden_size=256,
                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                      intermediate_size=512, moe_intermediate_size=128, num_experts=8, num_experts_per_tok=2,

@@ -143,6 +143,16 @@ def _softmax_sink(s: torch.Tensor, sink) -> torch.Tensor:
     return torch.softmax(full, -1)[..., :-1]
 
 
+def attn_lo(qpos, window: int):
+    """First visible key for query position(s) ``qpos`` (see attention.hip ``attn_lo``): sliding
+    window (``window`` > 0), chunked attention with chunks of ``-window`` (``window`` < -1), else 0."""
+    if window > 0:
+        return (qpos - window + 1).clamp(min=0)
+    if window < -1:
+        return qpos - qpos % (-window)
+    return qpos * 0
+
+
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, k_scale=1.0,
                  v_scale=1.0, softcap=0.0, sinks=None) -> torch.Tensor:
     B, Hq, D = q.shape
@@ -153,7 +163,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, 
         L = int(seq_lens[b])
         if L <= 0:
             continue
-        lo = max(0, L - window) if window > 0 else 0
+        lo = int(attn_lo(torch.tensor(L - 1), window))
         for h in range(Hkv):
             k, v = gather_kv(k_cache, v_cache, block_tables[b], L, h, P, k_scale, v_scale)
             k, v = k[lo:], v[lo:]
@@ -179,8 +189,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, windo
         qpos = torch.arange(L - ql, L, device=q.device)[:, None]
         kpos = torch.arange(L, device=q.device)[None, :]
         mask = kpos <= qpos
-        if window > 0:
-            mask &= kpos > qpos - window
+        mask &= kpos >= attn_lo(qpos, window)
         for h in range(Hkv):
             k, v = gather_kv(k_cache, v_cache, block_tables[s], L, h, P, k_scale, v_scale)
             qh = q[q0:q1, h * G:(h + 1) * G].float().transpose(0, 1)  # [G, ql, D]

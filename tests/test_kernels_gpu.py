@@ -125,8 +125,9 @@ def test_paged_decode(Hq, Hkv, seq_lens, part_size, variant, monkeypatch):
         _close(ops.paged_decode(q, kc, vc, bt, sl, scale, ws, order=order), expect, atol=2e-2)
 
 
+@pytest.mark.parametrize("window", [128, -256, -64])  # sliding; chunked (Llama 4) as window < -1
 @pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
-def test_paged_decode_window(variant, monkeypatch):
+def test_paged_decode_window(variant, window, monkeypatch):
     monkeypatch.setenv("OME_DECODE_ATTN", variant)
     D, P, Hq, Hkv = 128, 16, 32, 8
     seq_lens = [700, 40]
@@ -135,8 +136,8 @@ def test_paged_decode_window(variant, monkeypatch):
     sl = torch.tensor(seq_lens, dtype=torch.int32, device=DEV)
     q = torch.randn(2, Hq, D, device=DEV, dtype=torch.bfloat16)
     ws = ops.DecodeWorkspace(2, Hq, D, 1024, 256, DEV)
-    out = ops.paged_decode(q, kc, vc, bt, sl, 0.088, ws, window=128)
-    _close(out, ref.paged_decode(q, kc, vc, bt, sl, 0.088, window=128))
+    out = ops.paged_decode(q, kc, vc, bt, sl, 0.088, ws, window=window)
+    _close(out, ref.paged_decode(q, kc, vc, bt, sl, 0.088, window=window))
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 1), (16, 4)])
@@ -157,7 +158,10 @@ def test_paged_prefill(Hq, Hkv, q_lens, kv_lens, variant, monkeypatch):
     _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884), atol=2e-2)
 
 
-def test_paged_prefill_window():
+@pytest.mark.parametrize("window", [100, -128, -48])
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_paged_prefill_window(window, variant, monkeypatch):
+    monkeypatch.setenv("OME_PREFILL_ATTN", variant)
     D, P, Hq, Hkv = 128, 16, 32, 8
     q_lens, kv_lens = [200, 50], [500, 50]
     kc, vc = _cache(64, Hkv, D)
@@ -166,8 +170,8 @@ def test_paged_prefill_window():
     kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
     items = torch.tensor(ops.prefill_work_items(q_lens, kv_lens), dtype=torch.int32, device=DEV)
     q = torch.randn(250, Hq, D, device=DEV, dtype=torch.bfloat16)
-    out = ops.paged_prefill(q, kc, vc, bt, cu, kl, items, 0.0884, window=100)
-    _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884, window=100))
+    out = ops.paged_prefill(q, kc, vc, bt, cu, kl, items, 0.0884, window=window)
+    _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884, window=window))
 
 
 def test_sample_greedy_and_filters():
