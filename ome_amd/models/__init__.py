@@ -21,6 +21,7 @@ DENSE_ARCHS = {
 GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
 LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM"}
 LLAMA4_ARCHS = {"Llama4ForCausalLM", "Llama4ForConditionalGeneration"}
+QWEN2_VL_ARCHS = {"Qwen2VLForConditionalGeneration"}
 MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM", "DeepseekV2ForCausalLM",
              "DeepseekV3ForCausalLM", "PhiMoEForCausalLM"}
 
@@ -34,6 +35,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.gemma import GemmaForCausalLM
 
         return GemmaForCausalLM
+    if cfg.architecture in QWEN2_VL_ARCHS or cfg.model_type == "qwen2_vl":
+        from ome_amd.models.qwen2_vl import Qwen2VLForConditionalGeneration
+
+        return Qwen2VLForConditionalGeneration
     if cfg.architecture in LLAMA4_ARCHS or cfg.model_type in ("llama4", "llama4_text"):
         from ome_amd.models.llama4 import Llama4ForCausalLM
 
@@ -56,7 +61,7 @@ def model_class(cfg: ModelConfig):
 
 
 def supported(arch: str) -> bool:
-    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or \
+    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or \
         arch == "GptOssForCausalLM"
 
 

@@ -119,7 +119,7 @@ class ModelConfig:
             partial_rotary_factor=float(prf),
             max_position_embeddings=text.get("max_position_embeddings", 4096),
             tie_word_embeddings=bool(cfg.get("tie_word_embeddings", text.get("tie_word_embeddings", False))),
-            attention_bias=bool(text.get("attention_bias", text.get("use_bias", mt in ("qwen2", "qwen2_moe")))),
+            attention_bias=bool(text.get("attention_bias", text.get("use_bias", mt in ("qwen2", "qwen2_moe", "qwen2_vl", "qwen2_vl_text")))),
             qk_norm=mt in ("qwen3", "qwen3_moe", "gemma3", "gemma3_text"),
             hidden_act=text.get("hidden_act", text.get("hidden_activation", "silu")),
             sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt in ("mistral", "starcoder2")) else None,
@@ -251,6 +251,22 @@ PRESETS: dict[str, dict] = {
                                                    rope_scaling={"rope_type": "llama3", "factor": 16.0,
                                                                  "low_freq_factor": 1.0, "high_freq_factor": 1.0,
                                                                  "original_max_position_embeddings": 8192})),
+    "qwen2-vl-7b": dict(architectures=["Qwen2VLForConditionalGeneration"], model_type="qwen2_vl", hidden_size=3584,
+                        num_hidden_layers=28, num_attention_heads=28, num_key_value_heads=4, intermediate_size=18944,
+                        vocab_size=152064, rms_norm_eps=1e-6, rope_theta=1000000.0, max_position_embeddings=32768,
+                        rope_scaling={"type": "mrope", "mrope_section": [16, 24, 24]}, image_token_id=151655,
+                        video_token_id=151656, vision_start_token_id=151652, vision_end_token_id=151653,
+                        vision_config=dict(depth=32, embed_dim=1280, hidden_size=3584, num_heads=16, mlp_ratio=4,
+                                           patch_size=14, spatial_merge_size=2, temporal_patch_size=2,
+                                           in_channels=3, hidden_act="quick_gelu")),
+    "tiny-qwen2-vl": dict(architectures=["Qwen2VLForConditionalGeneration"], model_type="qwen2_vl", hidden_size=256,
+                          num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, intermediate_size=512,
+                          vocab_size=1024, rms_norm_eps=1e-6, rope_theta=1000000.0, max_position_embeddings=4096,
+                          rope_scaling={"type": "mrope", "mrope_section": [8, 12, 12]}, image_token_id=1000,
+                          video_token_id=1003, vision_start_token_id=1001, vision_end_token_id=1002,
+                          vision_config=dict(depth=2, embed_dim=128, hidden_size=256, num_heads=4, mlp_ratio=2,
+                                             patch_size=14, spatial_merge_size=2, temporal_patch_size=2,
+                                             in_channels=3, hidden_act="quick_gelu")),
     "tiny-llama4": dict(architectures=["Llama4ForCausalLM"], model_type="llama4_text", hidden_size=256,
                         num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                         intermediate_size=256, intermediate_size_mlp=512, num_local_experts=8, num_experts_per_tok=1,

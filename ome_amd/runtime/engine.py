@@ -146,6 +146,34 @@ class Engine:
         params.max_new_tokens = min(params.max_new_tokens, self.max_context - len(prompt_ids))
         return Request(prompt_ids=list(prompt_ids), params=params, **kw)
 
+    def make_mm_request(self, prompt_ids: list[int], images: list, params: SamplingParams | None = None,
+                        **kw) -> Request:
+        """A prompt with one image placeholder token per image (the model's ``image_token_id``) and
+        the images (data URL / path / bytes / PIL, or a preprocessed ``(pixel_values, (t, h, w))``).
+        Placeholders are expanded to one token per merged vision patch (content-hash ids, so the
+        prefix cache only matches identical images) and the M-RoPE positions are precomputed."""
+        import torch
+
+        from ome_amd.multimodal import MMInput, expand_image_tokens, mrope_positions
+        from ome_amd.multimodal.inputs import preprocess_image
+
+        m = self.runner.model
+        if not getattr(m, "is_multimodal", False):
+            raise ValueError(f"{self.cfg.architecture} does not accept image inputs")
+        pvs, grids = [], []
+        for im in images:
+            if isinstance(im, tuple):
+                pv, g = im
+            else:
+                pv, g = preprocess_image(im, patch=m.visual.patch, merge=m.merge, temporal=m.visual.temporal)
+            pvs.append(torch.as_tensor(pv, dtype=torch.float32))
+            grids.append(tuple(int(v) for v in g))
+        ids, spans = expand_image_tokens(list(prompt_ids), m.image_token_id, grids, m.merge, pvs,
+                                         self.cfg.vocab_size)
+        pos, delta = mrope_positions(len(ids), spans, grids, m.merge)
+        mm = MMInput(torch.cat(pvs, 0), grids, spans, pos, delta)
+        return self.make_request(ids, params, mm=mm, **kw)
+
     def add_request(self, req: Request) -> Request:
         with self._lock:
             self._inbox.append(req)

@@ -347,7 +347,7 @@ class ModelRunner:
                 any_pending = True
                 tok = 0
             h[off["ids"] + i] = tok
-            h[off["pos"] + i] = pos
+            h[off["pos"] + i] = pos + (r.mm.rope_delta if r.mm is not None else 0)  # M-RoPE text offset
             h[off["slots"] + i] = r.pages[pos // self.P] * self.P + pos % self.P
             h[off["seq_lens"] + i] = pos + 1
             h[off["req_idx"] + i] = r.req_slot
@@ -459,7 +459,10 @@ class ModelRunner:
             meta = AttnMeta("decode", t_pos, t_slots, self.slots.table.index_select(0, t_dreq), seq_lens=t_dlen,
                             decode_ws=ws, order=t_dord)
         self._init_penalty_rows(chunks)
-        hidden = self.model.forward(t_ids, meta, self.kv)
+        embeds = None
+        if getattr(self.model, "is_multimodal", False) and any(chunks[i].req.mm is not None for i in pre + dec):
+            embeds = self._mm_prepare(chunks, pre + dec, T, t_ids, meta)
+        hidden = self.model.forward(t_ids, meta, self.kv, embeds)
         if hidden is None:  # an earlier pipeline stage: tokens arrive from the last stage
             out_ids = torch.empty(len(chunks), dtype=torch.int32, device=self.device)
             out_lp = torch.empty(len(chunks), dtype=torch.float32, device=self.device)
@@ -500,6 +503,46 @@ class ModelRunner:
             pstate.pp_broadcast_from_last(out_ids)
             pstate.pp_broadcast_from_last(out_lp.float().contiguous())
         return self._finish_launch(out_ids, out_lp, len(chunks))
+
+    def _mm_prepare(self, chunks, order, T: int, t_ids: torch.Tensor, meta: AttnMeta):
+        """Multimodal rows of an eager step: per-row 3D M-RoPE positions -> a row-indexed cos/sin
+        table (``meta.extra['rope']``), and the input embeddings with every image-placeholder row
+        replaced by its vision feature (vision tower run once per request, at the first chunk
+        that reaches one of its images; freed once the prompt is fully cached)."""
+        m = self.model
+        p3 = np.empty((3, T), dtype=np.int64)
+        rows, feats, row = [], [], 0
+        for i in order:
+            c = chunks[i]
+            r, L = c.req, c.length
+            xs = np.arange(c.start, c.start + L)
+            mm = r.mm
+            if mm is None:
+                p3[:, row:row + L] = xs
+            else:
+                plen = len(r.prompt_ids)
+                blk = np.empty((3, L), dtype=np.int64)
+                inside = xs < plen
+                blk[:, inside] = mm.mrope_pos[:, xs[inside]]
+                blk[:, ~inside] = xs[~inside] + mm.rope_delta
+                p3[:, row:row + L] = blk
+                off = 0
+                for s, n in mm.spans:
+                    lo, hi = max(s, c.start), min(s + n, c.start + L)
+                    if lo < hi:
+                        if mm.features is None:
+                            mm.features = m.encode_images(mm.pixel_values, mm.grid_thw)
+                        rows.extend(range(row + lo - c.start, row + hi - c.start))
+                        feats.append(mm.features[off + lo - s: off + hi - s])
+                    off += n
+                if c.start + L >= plen:
+                    mm.features = None  # prompt fully scheduled: image features no longer needed
+            row += L
+        dv = self.device
+        meta.extra["rope"] = (torch.arange(T, dtype=torch.int32, device=dv), m.mrope_table(torch.from_numpy(p3)))
+        r_dev = torch.tensor(rows, dtype=torch.long, device=dv)
+        f = torch.cat(feats, 0) if feats else torch.zeros(0, m.cfg.hidden_size, dtype=m.dtype, device=dv)
+        return m.embed_with_images(t_ids, r_dev, f)
 
     def idle_forward(self) -> None:
         """DP attention: this rank has nothing scheduled but its peers do -- run one dummy token

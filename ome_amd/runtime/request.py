@@ -5,7 +5,7 @@ import enum
 import itertools
 import time
 from dataclasses import dataclass, field
-from typing import Callable
+from typing import Any, Callable
 
 
 @dataclass
@@ -83,6 +83,7 @@ class Request:
     pen_init: bool = False         # penalty count row initialised for the current req_slot
     dp_rank: int = 0               # DP attention: the rank whose scheduler owns the request
     pending_row: int = -1          # row of the newest pending token in its step's sampled output
+    mm: Any = None                 # multimodal inputs (ome_amd.multimodal.MMInput): images, spans, M-RoPE
 
     @property
     def all_ids(self) -> list[int]:

@@ -31,6 +31,9 @@ from fastapi import Request  # noqa: E402  (module level: FastAPI resolves strin
 log = logging.getLogger("ome_amd.server")
 
 
+_IMG_SENTINEL = "\x00<ome-image>\x00"  # stands in for an image content part while the chat template renders
+
+
 def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser("ome_amd.runtime.server")
     a = ap.add_argument
@@ -157,12 +160,15 @@ def create_app(engine, ns=None):
     def err(code: int, msg: str, typ: str = "invalid_request_error"):
         return JSONResponse({"error": {"message": msg, "type": typ, "code": code}}, status_code=code)
 
-    async def run_request(prompt_ids, params, bootstrap=None):
+    async def run_request(prompt_ids, params, bootstrap=None, images=None):
         loop = asyncio.get_running_loop()
         stream = _Stream(loop)
         if bootstrap and bootstrap.get("disagg_role") == "prefill":
             params.max_new_tokens = 1  # the prefill engine only produces the first token + KV
-        req = engine.make_request(prompt_ids, params, on_token=stream, bootstrap=bootstrap)
+        if images:
+            req = engine.make_mm_request(prompt_ids, images, params, on_token=stream, bootstrap=bootstrap)
+        else:
+            req = engine.make_request(prompt_ids, params, on_token=stream, bootstrap=bootstrap)
         engine.add_request(req)
         return req, stream
 
@@ -219,23 +225,58 @@ def create_app(engine, ns=None):
         engine.metrics.model_name = model_name
         return PlainTextResponse(engine.metrics.render(), media_type="text/plain; version=0.0.4")
 
+    def _chat_images(msgs: list) -> tuple[list, list]:
+        """OpenAI ``image_url`` / ``image`` content parts -> (messages with a sentinel text part in
+        their place, image sources in order)."""
+        images, out = [], []
+        for m in msgs:
+            content = m.get("content") if isinstance(m, dict) else None
+            if not isinstance(content, list):
+                out.append(m)
+                continue
+            parts = []
+            for c in content:
+                if isinstance(c, dict) and c.get("type") in ("image_url", "image"):
+                    src = c.get("image_url", c.get("image"))
+                    images.append(src.get("url") if isinstance(src, dict) else src)
+                    parts.append({"type": "text", "text": _IMG_SENTINEL})
+                else:
+                    parts.append(c)
+            out.append({**m, "content": parts})
+        return out, images
+
     def _encode(body: dict, chat: bool):
+        """-> (prompt ids, images); image prompts carry one ``image_token_id`` per image, wrapped
+        in the model's vision start / end tokens."""
         if chat:
             msgs = body.get("messages")
             if not isinstance(msgs, list) or not msgs:
                 raise ValueError("messages must be a non-empty list")
+            msgs, images = _chat_images(msgs)
             text = tok.apply_chat_template(msgs, add_generation_prompt=True)
-            return tok.encode(text)
+            if not images:
+                return tok.encode(text), []
+            m = engine.runner.model
+            if not getattr(m, "is_multimodal", False):
+                raise ValueError(f"model {model_name} does not accept image inputs")
+            segs = text.split(_IMG_SENTINEL)
+            ids = []
+            for k, seg in enumerate(segs):
+                ids.extend(tok.encode(seg) if seg else [])
+                if k + 1 < len(segs):
+                    ids.extend([m.vision_start_id, m.image_token_id, m.vision_end_id])
+            return ids, images
         p = body.get("prompt", body.get("text"))
+        images = list(body.get("image_data") or [])  # SGLang /generate spelling
         if isinstance(p, list) and p and isinstance(p[0], int):
-            return list(p)
+            return list(p), images
         if isinstance(p, list):
             p = p[0] if p else ""
         if body.get("input_ids"):
-            return list(body["input_ids"])
+            return list(body["input_ids"]), images
         if not isinstance(p, str):
             raise ValueError("prompt must be a string or a list of token ids")
-        return tok.encode(p)
+        return tok.encode(p), images
 
     def _stop_hit(text: str, stops: list[str]) -> int | None:
         idx = [text.find(s) for s in stops if s and s in text]
@@ -243,10 +284,11 @@ def create_app(engine, ns=None):
 
     async def _complete(body: dict, chat: bool):
         try:
-            ids = _encode(body, chat)
+            ids, images = _encode(body, chat)
             params = _sampling_from(body, default_max)
-            req, stream = await run_request(ids, params, _bootstrap_of(body))
-        except ValueError as e:
+            req, stream = await run_request(ids, params, _bootstrap_of(body), images)
+            ids = req.prompt_ids  # image placeholders expanded
+        except (ValueError, OSError) as e:  # OSError: undecodable image data
             return err(400, str(e))
         rid = f"{'chatcmpl' if chat else 'cmpl'}-{uuid.uuid4().hex[:24]}"
         obj = "chat.completion" if chat else "text_completion"
@@ -331,6 +373,7 @@ def create_app(engine, ns=None):
         body = await request.json()
         sp = body.get("sampling_params") or {}
         merged = {**sp, "prompt": body.get("text"), "input_ids": body.get("input_ids"),
+                  "image_data": body.get("image_data"),
                   "max_tokens": sp.get("max_new_tokens"), "stream": body.get("stream", False)}
         res = await _complete(merged, False)
         if isinstance(res, dict):

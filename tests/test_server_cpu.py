@@ -62,3 +62,34 @@ def test_sglang_style_flags_parse():
     assert ns.tp_size == 4 and ns.mem_frac == 0.9 and "--trust-remote-code" in unknown
     ea = engine_args_from(ns)
     assert ea.tp_size == 4 and ea.model == "llama-3-8b"  # no config.json -> random-init preset
+
+
+def test_chat_with_image_data_url():
+    """OpenAI ``image_url`` content (data URL) on a vision-language model: the image is decoded,
+    expanded into one placeholder per merged patch and served; usage counts the expanded prompt."""
+    import base64
+    import io
+
+    import numpy as np
+    from PIL import Image
+
+    buf = io.BytesIO()
+    Image.fromarray(np.random.default_rng(0).integers(0, 255, (60, 90, 3), dtype=np.uint8)).save(buf, "PNG")
+    url = "data:image/png;base64," + base64.b64encode(buf.getvalue()).decode()
+    eng = Engine(EngineArgs(model="tiny-qwen2-vl", device="cpu", max_running_requests=4, context_length=512,
+                            served_model_name="vl"))
+    eng.start()
+    with TestClient(create_app(eng)) as c:
+        msg = [{"role": "user", "content": [{"type": "text", "text": "what is this?"},
+                                            {"type": "image_url", "image_url": {"url": url}}]}]
+        r = c.post("/v1/chat/completions", json={"model": "vl", "messages": msg, "max_tokens": 4})
+        assert r.status_code == 200, r.text
+        body = r.json()
+        assert body["usage"]["completion_tokens"] == 4
+        assert body["usage"]["prompt_tokens"] > 6  # 56x84 resize -> 4x6 patches -> 6 image tokens + text
+        bad = [{"role": "user", "content": [{"type": "image_url", "image_url": {"url": "data:image/png;base64,AAAA"}}]}]
+        assert c.post("/v1/chat/completions", json={"model": "vl", "messages": bad}).status_code == 400
+    eng.shutdown()
+    eng2 = Engine(EngineArgs(model="tiny-llama", device="cpu", max_running_requests=4, context_length=256))
+    with TestClient(create_app(eng2)) as c:
+        assert c.post("/v1/chat/completions", json={"messages": msg}).status_code == 400
