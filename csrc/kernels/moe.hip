@@ -13,6 +13,8 @@
 //   ome_moe_combine : out[t] = sum_j w[t, j] * Y[inv[t*k + j]]   (fp32 accumulate)
 #include "common.h"
 
+#include <cstdlib>
+
 #ifndef OME_NEG_INF
 #define OME_NEG_INF (-__builtin_inff())
 #endif
@@ -314,16 +316,166 @@ __global__ __launch_bounds__(256) void moe_gemm_kernel(const bf16* __restrict__ 
       }
 }
 
-// bias: optional per-expert bias [E, N] added in the epilogue
+// ------------------------------------------------------------------------------------------
+// grouped GEMM v2: the same 64x64 tile / 2x2-wave layout, but a BK = 64 or 128 k-step staged
+// through DOUBLE-buffered LDS: the next step's global loads are issued before this step's MFMAs
+// and written to the other buffer after them, so one barrier per k-step (v1: two per 32) and
+// BK/32 x 16 B of W + A in flight per thread.  Decode-time MoE GEMMs are weight-streaming
+// (tens of rows per expert), so this is a bandwidth kernel: the win is bytes in flight.
+// ------------------------------------------------------------------------------------------
+template <int BM, int BN, int BK>
+__global__ __launch_bounds__(256) void moe_gemm_v2_kernel(const bf16* __restrict__ A, int64_t lda,
+                                                          const int* __restrict__ sorted_ids, int gather_div,
+                                                          const bf16* __restrict__ W, const int* __restrict__ offsets,
+                                                          int E, int N, int K, bf16* __restrict__ out, int64_t ldo,
+                                                          const bf16* __restrict__ bias) {
+  constexpr int LD = BK + 8, CPR = BK / 8;           // padded LDS row, 16-B chunks per row
+  constexpr int CA = BM * CPR / 256, CB = BN * CPR / 256;  // chunks per thread per operand
+  constexpr int MI = BM / 32, NJ = BN / 32;          // 16x16 MFMA tiles per wave (waves 2 x 2)
+  static_assert(CA >= 1 && CB >= 1 && 2 * (BM + BN) * LD * 2 <= 65536, "tile");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (BM + BN) * LD];
+  __shared__ int s_tile[3];
+  bf16* sA = smem;                  // [2][BM * LD]
+  bf16* sB = smem + 2 * BM * LD;    // [2][BN * LD]
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // ---- (expert, m0) of this tile: wave 0 prefix-sums the per-expert tile counts 64 at a time ----
+  if (tid == 0) s_tile[0] = -1;
+  __syncthreads();
+  if (wave == 0) {
+    int base = 0;
+    const int y = blockIdx.y;
+    for (int e0 = 0; e0 < E; e0 += 64) {
+      const int e = e0 + lane;
+      const int nt = e < E ? (offsets[e + 1] - offsets[e] + BM - 1) / BM : 0;
+      int incl = nt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      const int t = y - base;
+      if (t >= incl - nt && t < incl) {
+        s_tile[0] = e;
+        s_tile[1] = offsets[e] + (t - (incl - nt)) * BM;
+        s_tile[2] = offsets[e + 1];
+      }
+      base += __shfl(incl, 63);
+      if (y < base) break;
+    }
+  }
+  __syncthreads();
+  const int e = s_tile[0];
+  if (e < 0) return;
+  const int m0 = s_tile[1], m_end = s_tile[2];
+  const int n0 = blockIdx.x * BN;
+  const bf16* We = W + (int64_t)e * N * K;
+  const int lc = (tid % CPR) * 8;
+  int64_t a_off[CA];
+  const bf16* bptr[CB];
+#pragma unroll
+  for (int j = 0; j < CA; ++j) {
+    const int arow = m0 + (tid + 256 * j) / CPR;
+    a_off[j] = -1;
+    if (arow < m_end) a_off[j] = (int64_t)(gather_div > 0 ? sorted_ids[arow] / gather_div : arow) * lda;
+  }
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    const int r = n0 + (tid + 256 * j) / CPR;
+    bptr[j] = r < N ? We + (int64_t)r * K : nullptr;
+  }
+  const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 ra[CA], rb[CB];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < CA; ++j) ra[j] = a_off[j] >= 0 ? ld8(A + a_off[j] + k0 + lc) : bf16x8{};
+#pragma unroll
+    for (int j = 0; j < CB; ++j) rb[j] = bptr[j] ? ld8(bptr[j] + k0 + lc) : bf16x8{};
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < CA; ++j)
+      *reinterpret_cast<bf16x8*>(&sA[buf * BM * LD + ((tid + 256 * j) / CPR) * LD + lc]) = ra[j];
+#pragma unroll
+    for (int j = 0; j < CB; ++j)
+      *reinterpret_cast<bf16x8*>(&sB[buf * BN * LD + ((tid + 256 * j) / CPR) * LD + lc]) = rb[j];
+  };
+  const int nk = K / BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < nk) gload((ks + 1) * BK);  // in flight during this step's MFMAs
+    const bf16* a_s = sA + cur * BM * LD;
+    const bf16* b_s = sB + cur * BN * LD;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8*>(&a_s[(wm + 16 * i + fr) * LD + kk + fk]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(&b_s[(wn + 16 * j + fr) * LD + kk + fk]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    }
+    if (ks + 1 < nk) lstore(cur ^ 1);  // the other buffer was last read before the previous barrier
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+        const int col = n0 + wn + 16 * j + (lane & 15);
+        if (row < m_end && col < N) {
+          const float b = bias != nullptr ? (float)bias[(int64_t)e * N + col] : 0.f;
+          out[(int64_t)row * ldo + col] = (bf16)(acc[i][j][r] + b);
+        }
+      }
+}
+
+static int moe_gemm_variant() {
+  const char* s = getenv("OME_MOE_GEMM");  // 1 = v1 (64x64, BK 32, single buffer); default v2
+  return s ? atoi(s) : 2;
+}
+
+// bias: optional per-expert bias [E, N] added in the epilogue.  tile_m 128: the 128x128 prefill
+// tile (max_m_tiles must then count 128-row tiles); otherwise the 64x64 decode tile.
 OME_API int ome_moe_gemm(const void* A, int64_t lda, const int* sorted_ids, int gather_div, const void* W,
                          const int* offsets, int E, int N, int K, int max_m_tiles, void* out, int64_t ldo,
-                         const void* bias, hipStream_t stream) {
+                         const void* bias, int tile_m, hipStream_t stream) {
   if (max_m_tiles <= 0) return 0;
   if (K % GBK != 0 || lda % 8 != 0) return -2;
   if (max_m_tiles > 65535) return -3;
-  dim3 grid((N + GBN - 1) / GBN, max_m_tiles);
-  moe_gemm_kernel<<<grid, 256, 0, stream>>>((const bf16*)A, lda, sorted_ids, gather_div, (const bf16*)W, offsets,
-                                            E, N, K, (bf16*)out, ldo, (const bf16*)bias);
+  const int v = moe_gemm_variant();
+  if (tile_m == 128 && v != 1) {
+    dim3 grid((N + 127) / 128, max_m_tiles);
+    moe_gemm_v2_kernel<128, 128, 32><<<grid, 256, 0, stream>>>((const bf16*)A, lda, sorted_ids, gather_div,
+                                                               (const bf16*)W, offsets, E, N, K, (bf16*)out, ldo,
+                                                               (const bf16*)bias);
+  } else {
+    if (tile_m == 128) return -4;  // the v1 kernel only has the 64-row tile
+    dim3 grid((N + GBN - 1) / GBN, max_m_tiles);
+    if (v != 1 && K % 64 == 0) {
+      moe_gemm_v2_kernel<64, 64, 64><<<grid, 256, 0, stream>>>((const bf16*)A, lda, sorted_ids, gather_div,
+                                                               (const bf16*)W, offsets, E, N, K, (bf16*)out, ldo,
+                                                               (const bf16*)bias);
+    } else {
+      moe_gemm_kernel<<<grid, 256, 0, stream>>>((const bf16*)A, lda, sorted_ids, gather_div, (const bf16*)W, offsets,
+                                                E, N, K, (bf16*)out, ldo, (const bf16*)bias);
+    }
+  }
   OME_CHECK_LAUNCH();
   return 0;
 }

@@ -4,6 +4,8 @@ native library is missing on a GPU the call raises.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import reference as ref
@@ -231,6 +233,21 @@ def moe_route(logits: torch.Tensor, k: int, renorm: bool = True, scoring: str = 
     return out_w, out_ids
 
 
+def moe_tile_m(rows: int, E: int, N: int) -> int:
+    """Row tile of the grouped GEMM (static in the shapes, so graph-safe): 128x128 when experts
+    get many rows (prefill: MFMA-bound), or in the decode regime when the wide-N GEMM still gives
+    >= 1024 workgroups of 128 (more W bytes per barrier); else the 64x64 weight-streaming tile.
+    Measured on gfx950: ``scripts/moe_gemm_bench.py`` (profiles/r01_moe_gemm_bench.txt).
+    ``OME_MOE_TILE`` overrides."""
+    env = os.environ.get("OME_MOE_TILE")
+    if env:
+        return int(env)
+    avg = rows / max(1, E)
+    if avg >= 128 or (avg >= 48 and -(-N // 128) * E >= 1024):
+        return 128
+    return 64
+
+
 def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
               act: int = 0, scale: float = 1.0, b13: torch.Tensor | None = None,
               b2: torch.Tensor | None = None) -> torch.Tensor:
@@ -250,14 +267,15 @@ def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13
     inv = torch.empty(n, dtype=torch.int32, device=dev)
     call("ome_moe_align", topk_ids.data_ptr(), n, E, offsets.data_ptr(), sorted_ids.data_ptr(), inv.data_ptr(),
          stream_ptr())
-    max_tiles = -(-n // 64) + E
+    tm = moe_tile_m(n, E, I2)
     gu = torch.empty(n, I2, dtype=x.dtype, device=dev)
     call("ome_moe_gemm", x.data_ptr(), x.stride(0), sorted_ids.data_ptr(), k, w13.data_ptr(), offsets.data_ptr(),
-         E, I2, H, max_tiles, gu.data_ptr(), gu.stride(0), ptr(b13), stream_ptr())
+         E, I2, H, -(-n // tm) + E, gu.data_ptr(), gu.stride(0), ptr(b13), tm, stream_ptr())
     h = act_and_mul(gu, act)
     y = torch.empty(n, H, dtype=x.dtype, device=dev)
+    tm = moe_tile_m(n, E, H)
     call("ome_moe_gemm", h.data_ptr(), h.stride(0), None, 0, w2.data_ptr(), offsets.data_ptr(), E, H, I,
-         max_tiles, y.data_ptr(), y.stride(0), ptr(b2), stream_ptr())
+         -(-n // tm) + E, y.data_ptr(), y.stride(0), ptr(b2), tm, stream_ptr())
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     call("ome_moe_combine", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), float(scale),
          stream_ptr())

@@ -26,7 +26,10 @@ def test_moe_route(T, E, k, dtype):
 
 @pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 256, 128), (64, 8, 2, 512, 256), (200, 16, 4, 256, 96),
                                        (7, 64, 6, 1024, 64), (513, 8, 2, 4096, 1024)])
-def test_fused_moe(T, E, k, H, I):
+@pytest.mark.parametrize("kernel,tile", [("1", "64"), ("2", "64"), ("2", "128")])  # v1 / v2 64x64 / v2 128x128
+def test_fused_moe(T, E, k, H, I, kernel, tile, monkeypatch):
+    monkeypatch.setenv("OME_MOE_GEMM", kernel)
+    monkeypatch.setenv("OME_MOE_TILE", tile)
     x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
     w13 = torch.randn(E, 2 * I, H, device=DEV, dtype=torch.bfloat16) * 0.05
     w2 = torch.randn(E, H, I, device=DEV, dtype=torch.bfloat16) * 0.05
