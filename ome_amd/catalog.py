@@ -1,0 +1,269 @@
+"""Model + runtime catalog generator (reference: ``config/runtimes/**`` — 205 ClusterServingRuntimes —
+and ``config/models/**`` — 205 ClusterBaseModels).
+
+The reference hand-maintains one SGLang/vLLM runtime YAML per model and GPU count.  Here the
+catalog is generated from one table of the model families the first-party runtime serves
+(:data:`FAMILIES`), sized for MI355X: tensor parallelism is the smallest power of two that leaves
+~40 % of each GPU's 288 GB HBM3E for the KV cache (Llama-3-70B bf16 and smaller run on ONE GPU,
+Llama-4-Scout bf16 on two, Maverick / DeepSeek-V3 on a full 8-GPU xGMI node), plus
+prefill/decode-disaggregated variants for the dense headline models and a two-node
+leader/worker variant for DeepSeek-V3 bf16.  ``python -m ome_amd.catalog --out config`` writes
+``config/runtimes/ome-amd/*.yaml`` and ``config/models/<vendor>/*.yaml``; ``tests/test_catalog_cpu.py``
+checks every entry parses into the v1beta1 API types, names a supported architecture, passes the
+runtime server's own flag parser, and is what the RuntimeSelector picks for its base model.
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import yaml
+
+HBM_GB = 288.0
+KV_HEADROOM = 0.6      # weights may use at most this fraction of a GPU
+IMAGE = "ome-amd/runtime:rocm7.2-gfx950"
+
+
+@dataclass
+class Family:
+    name: str                 # runtime / base model name stem
+    vendor: str
+    hf: str                   # hf:// repo of the real weights
+    arch: str                 # HF architectures[0]
+    params_b: float           # billions of parameters
+    preset: str | None = None  # ome_amd preset for random:// (offline) weights
+    bytes_per_param: float = 2.0
+    capabilities: list[str] = field(default_factory=lambda: ["TEXT_TO_TEXT"])
+    args: list[str] = field(default_factory=list)
+    pd: bool = False          # also emit a prefill/decode-disaggregated runtime
+    multinode: int = 0        # also emit a leader/worker runtime over this many nodes (bf16)
+    quantization: str | None = None
+    min_tp: int = 1           # e.g. DP attention over a whole node
+
+
+FAMILIES: list[Family] = [
+    Family("llama-3-8b-instruct", "meta", "meta-llama/Meta-Llama-3-8B-Instruct", "LlamaForCausalLM", 8.0,
+           "llama-3-8b", pd=True),
+    Family("llama-3-1-8b-instruct", "meta", "meta-llama/Llama-3.1-8B-Instruct", "LlamaForCausalLM", 8.0,
+           "llama-3.1-8b"),
+    Family("llama-3-70b-instruct", "meta", "meta-llama/Meta-Llama-3-70B-Instruct", "LlamaForCausalLM", 70.6,
+           "llama-3-70b", pd=True),
+    Family("llama-3-1-405b-instruct-fp8", "meta", "meta-llama/Llama-3.1-405B-Instruct-FP8", "LlamaForCausalLM",
+           405.0, None, 1.0, quantization="fp8"),
+    Family("llama-4-scout-17b-16e-instruct", "meta", "meta-llama/Llama-4-Scout-17B-16E-Instruct",
+           "Llama4ForConditionalGeneration", 109.0, "llama-4-scout-17b-16e"),
+    Family("llama-4-maverick-17b-128e-instruct-fp8", "meta", "meta-llama/Llama-4-Maverick-17B-128E-Instruct-FP8",
+           "Llama4ForConditionalGeneration", 402.0, None, 1.0, quantization="fp8"),
+    Family("mistral-7b-instruct", "mistralai", "mistralai/Mistral-7B-Instruct-v0.3", "MistralForCausalLM", 7.2),
+    Family("mixtral-8x7b-instruct", "mistralai", "mistralai/Mixtral-8x7B-Instruct-v0.1", "MixtralForCausalLM",
+           46.7, "mixtral-8x7b"),
+    Family("qwen2-5-7b-instruct", "qwen", "Qwen/Qwen2.5-7B-Instruct", "Qwen2ForCausalLM", 7.6),
+    Family("qwen2-5-72b-instruct", "qwen", "Qwen/Qwen2.5-72B-Instruct", "Qwen2ForCausalLM", 72.7),
+    Family("qwen3-8b", "qwen", "Qwen/Qwen3-8B", "Qwen3ForCausalLM", 8.2, "qwen3-8b"),
+    Family("qwen3-30b-a3b", "qwen", "Qwen/Qwen3-30B-A3B", "Qwen3MoeForCausalLM", 30.5),
+    Family("qwen2-vl-7b-instruct", "qwen", "Qwen/Qwen2-VL-7B-Instruct", "Qwen2VLForConditionalGeneration", 8.3,
+           "qwen2-vl-7b", capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("deepseek-v2-lite-chat", "deepseek-ai", "deepseek-ai/DeepSeek-V2-Lite-Chat", "DeepseekV2ForCausalLM",
+           15.7, "deepseek-v2-lite"),
+    Family("deepseek-v3", "deepseek-ai", "deepseek-ai/DeepSeek-V3", "DeepseekV3ForCausalLM", 671.0, None, 1.0,
+           args=["--enable-dp-attention", "--dp", "8"], quantization="fp8", multinode=2, min_tp=8),
+    Family("kimi-k2-instruct", "moonshotai", "moonshotai/Kimi-K2-Instruct", "DeepseekV3ForCausalLM", 1026.0, None,
+           1.0, quantization="fp8"),
+    Family("gpt-oss-20b", "openai", "openai/gpt-oss-20b", "GptOssForCausalLM", 20.9, "gpt-oss-20b"),
+    Family("gpt-oss-120b", "openai", "openai/gpt-oss-120b", "GptOssForCausalLM", 117.0),
+    Family("gemma-2-9b-it", "google", "google/gemma-2-9b-it", "Gemma2ForCausalLM", 9.2, "gemma-2-9b"),
+    Family("gemma-3-27b-it", "google", "google/gemma-3-27b-it", "Gemma3ForConditionalGeneration", 27.4),
+    Family("phi-3-mini-4k-instruct", "microsoft", "microsoft/Phi-3-mini-4k-instruct", "Phi3ForCausalLM", 3.8),
+    Family("phi-3-5-moe-instruct", "microsoft", "microsoft/Phi-3.5-MoE-instruct", "PhiMoEForCausalLM", 41.9),
+    Family("starcoder2-7b", "bigcode", "bigcode/starcoder2-7b", "Starcoder2ForCausalLM", 7.2, "starcoder2-7b"),
+    Family("pythia-1-4b", "eleutherai", "EleutherAI/pythia-1.4b", "GPTNeoXForCausalLM", 1.4, "pythia-1.4b"),
+    Family("internlm2-7b-chat", "internlm", "internlm/internlm2-chat-7b", "InternLM2ForCausalLM", 7.7),
+    Family("granite-3-1-8b-instruct", "ibm-granite", "ibm-granite/granite-3.1-8b-instruct", "GraniteForCausalLM",
+           8.2),
+    Family("smollm3-3b", "huggingfacetb", "HuggingFaceTB/SmolLM3-3B", "SmolLM3ForCausalLM", 3.1),
+    Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+]
+
+
+def tp_for(f: Family) -> int:
+    gb = f.params_b * f.bytes_per_param
+    tp = f.min_tp
+    while gb / tp > KV_HEADROOM * HBM_GB and tp < 8:
+        tp *= 2
+    return tp
+
+
+def size_label(b: float) -> str:
+    return f"{b:.0f}B" if b >= 10 else f"{b:.1f}B".replace(".0B", "B")
+
+
+def _probes() -> dict:
+    def get(path, **kw):
+        return {"httpGet": {"path": path, "port": 8080}, **kw}
+
+    return {"readinessProbe": get("/health_generate", failureThreshold=3, successThreshold=1, periodSeconds=30,
+                                  timeoutSeconds=60),
+            "livenessProbe": get("/health", failureThreshold=5, successThreshold=1, periodSeconds=30,
+                                 timeoutSeconds=30),
+            "startupProbe": get("/health_generate", failureThreshold=150, successThreshold=1, periodSeconds=6,
+                                initialDelaySeconds=10, timeoutSeconds=30)}
+
+
+def server_args(f: Family, tp: int, extra: list[str] | None = None) -> list[str]:
+    a = ["--host", "0.0.0.0", "--port", "8080", "--enable-metrics", "--model-path", "$(MODEL_PATH)",
+         "--tp-size", str(tp), "--mem-frac", "0.9", "--served-model-name", f.hf]
+    if f.quantization:
+        a += ["--quantization", f.quantization]
+    return a + list(f.args) + list(extra or [])
+
+
+def _container(f: Family, tp: int, args: list[str], name: str = "ome-container") -> dict:
+    cpu, mem = 16 * tp, f"{64 * tp}Gi"
+    return {"name": name, "image": IMAGE, "ports": [{"containerPort": 8080, "name": "http1", "protocol": "TCP"}],
+            "command": ["python3", "-m", "ome_amd.runtime.server"], "args": args,
+            "env": [{"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}, {"name": "GPU_MAX_HW_QUEUES", "value": "4"}],
+            "volumeMounts": [{"mountPath": "/dev/shm", "name": "dshm"}],
+            "resources": {"requests": {"cpu": cpu, "memory": mem, "amd.com/gpu": tp},
+                          "limits": {"cpu": cpu, "memory": mem, "amd.com/gpu": tp}},
+            **_probes()}
+
+
+def _router() -> dict:
+    return {"runner": {"name": "router", "image": "ome-amd/router:latest",
+                       "ports": [{"containerPort": 8080, "name": "http"}],
+                       "command": ["python3", "-m", "ome_amd.router", "--host", "0.0.0.0", "--port", "8080",
+                                   "--policy", "cache_aware", "--service-discovery", "--selector",
+                                   "component=engine", "ome.io/inferenceservice=$(INFERENCESERVICE_NAME)",
+                                   "--service-discovery-namespace", "$(NAMESPACE)"],
+                       "env": [{"name": "INFERENCESERVICE_NAME",
+                                "valueFrom": {"fieldRef": {"fieldPath": "metadata.labels['ome.io/inferenceservice']"}}},
+                               {"name": "NAMESPACE", "valueFrom": {"fieldRef": {"fieldPath": "metadata.namespace"}}}],
+                       "resources": {"limits": {"cpu": "2", "memory": "2Gi"}}}}
+
+
+def _formats(f: Family, priority: int = 2) -> list[dict]:
+    return [{"modelFramework": {"name": "transformers", "version": "5.0.0", "operator": "GreaterThanOrEqual"},
+             "modelFormat": {"name": "safetensors", "version": "1.0.0"}, "modelArchitecture": f.arch,
+             "autoSelect": True, "priority": priority, "version": "1.0.0",
+             **({"quantization": f.quantization} if f.quantization else {})}]
+
+
+def _spec_base(f: Family) -> dict:
+    lo, hi = f.params_b * 0.85, f.params_b * 1.15
+    return {"disabled": False, "supportedModelFormats": _formats(f), "protocolVersions": ["openAI"],
+            "modelSizeRange": {"min": size_label(lo), "max": size_label(hi)},
+            "acceleratorRequirements": {"acceleratorClasses": ["amd-mi355x", "amd-mi300x"]}}
+
+
+def runtime(f: Family) -> dict:
+    tp = tp_for(f)
+    spec = _spec_base(f)
+    spec["engineConfig"] = {"annotations": {"prometheus.io/scrape": "true", "prometheus.io/port": "8080",
+                                            "prometheus.io/path": "/metrics"},
+                            "volumes": [{"name": "dshm", "emptyDir": {"medium": "Memory"}}],
+                            "runner": _container(f, tp, server_args(f, tp))}
+    spec["routerConfig"] = _router()
+    return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterServingRuntime",
+            "metadata": {"name": f"ome-amd-{f.name}-tp{tp}"}, "spec": spec}
+
+
+def pd_runtime(f: Family) -> dict:
+    """Prefill (engine) + decode (decoder) pods on one xGMI node; KV pages move GPU to GPU."""
+    tp = tp_for(f)
+    spec = _spec_base(f)
+    spec["supportedModelFormats"][0]["priority"] = 1
+    spec["supportedModelFormats"][0]["autoSelect"] = False  # opt-in via the ISVC's runtime name
+    vol = [{"name": "dshm", "emptyDir": {"medium": "Memory"}}]
+    spec["engineConfig"] = {"volumes": vol, "runner": _container(
+        f, tp, server_args(f, tp, ["--disaggregation-mode", "prefill", "--disaggregation-bootstrap-port", "8998"]))}
+    spec["decoderConfig"] = {"volumes": vol, "runner": _container(f, tp, server_args(f, tp, ["--disaggregation-mode",
+                                                                                             "decode"]))}
+    r = _router()
+    r["runner"]["command"] += ["--pd-disaggregation"]
+    spec["routerConfig"] = r
+    return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterServingRuntime",
+            "metadata": {"name": f"ome-amd-{f.name}-pd-tp{tp}"}, "spec": spec}
+
+
+def multinode_runtime(f: Family) -> dict:
+    """Leader/worker (LeaderWorkerSet) bf16 serving over ``f.multinode`` nodes of 8 GPUs."""
+    g = copy.copy(f)
+    g.bytes_per_param, g.quantization, g.args = 2.0, None, []
+    n = f.multinode
+    tp = 8 * n
+    spec = _spec_base(g)
+    spec["supportedModelFormats"][0]["autoSelect"] = False
+    vol = [{"name": "dshm", "emptyDir": {"medium": "Memory"}}]
+    dist = ["--dist-init-addr", "$(LWS_LEADER_ADDRESS):5000", "--nnodes", str(n)]
+    leader = _container(g, 8, server_args(g, tp, dist + ["--node-rank", "0"]))
+    worker = _container(g, 8, server_args(g, tp, dist + ["--node-rank", "$(LWS_WORKER_INDEX)"]))
+    for c in (leader, worker):
+        c["resources"] = {"requests": {"cpu": 128, "memory": "1024Gi", "amd.com/gpu": 8},
+                          "limits": {"cpu": 128, "memory": "1024Gi", "amd.com/gpu": 8}}
+    spec["engineConfig"] = {"volumes": vol, "leader": {"runner": leader}, "worker": {"size": n - 1, "runner": worker}}
+    spec["routerConfig"] = _router()
+    return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterServingRuntime",
+            "metadata": {"name": f"ome-amd-{f.name}-bf16-{n}node"}, "spec": spec}
+
+
+def base_model(f: Family) -> dict:
+    uri = f"random://{f.preset}" if f.preset else f"hf://{f.hf}"
+    spec = {"vendor": f.vendor, "disabled": False, "version": "1.0.0", "displayName": f"{f.vendor}.{f.name}",
+            "modelCapabilities": list(f.capabilities), "modelArchitecture": f.arch,
+            "modelParameterSize": size_label(f.params_b),
+            "modelFormat": {"name": "safetensors", "version": "1.0.0"},
+            "modelFramework": {"name": "transformers", "version": "4.46.0"},
+            "storage": {"storageUri": uri, "path": f"/raid/models/{f.vendor}/{f.name}"}}
+    if f.quantization:
+        spec["quantization"] = f.quantization
+    if not f.preset:
+        spec["storage"]["key"] = "hf-token"
+    return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterBaseModel", "metadata": {"name": f.name}, "spec": spec}
+
+
+def generate() -> tuple[dict[str, list[dict]], dict[str, list[dict]]]:
+    """-> ({runtime file stem: docs}, {vendor: base model docs})."""
+    rts: dict[str, list[dict]] = {}
+    models: dict[str, list[dict]] = {}
+    for f in FAMILIES:
+        docs = [runtime(f)]
+        if f.pd:
+            docs.append(pd_runtime(f))
+        if f.multinode:
+            docs.append(multinode_runtime(f))
+        rts[f.name] = docs
+        models.setdefault(f.vendor, []).append(base_model(f))
+    return rts, models
+
+
+def write(out: Path) -> list[Path]:
+    rts, models = generate()
+    paths = []
+    hdr = "# Generated by `python -m ome_amd.catalog --out config` -- edit ome_amd/catalog.py, not this file.\n"
+    for stem, docs in rts.items():
+        p = out / "runtimes" / "ome-amd" / f"{stem}-rt.yaml"
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(hdr + yaml.safe_dump_all(docs, sort_keys=False))
+        paths.append(p)
+    for vendor, docs in models.items():
+        p = out / "models" / vendor / "catalog.yaml"
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(hdr + yaml.safe_dump_all(docs, sort_keys=False))
+        paths.append(p)
+    return paths
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--out", default="config")
+    a = ap.parse_args(argv)
+    for p in write(Path(a.out)):
+        print(p)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
