@@ -1,0 +1,197 @@
+// Mamba-2 (selective state space) kernels for hybrid models (NemotronH; reference catalog
+// ``NemotronHForCausalLM`` runtimes), CDNA4 / gfx950.
+//
+//   ome_ssm_conv1d       : causal depthwise conv (kernel K <= 8) + SiLU over a varlen batch of
+//                          sequences, continuing from / updating each sequence's conv state
+//   ome_ssm_scan         : the selective scan  h <- exp(dt*A) h + dt * B x,  y = C.h + D x
+//                          (dt = softplus(dt + dt_bias) clamped below), recurrent over the rows of
+//                          each sequence, state in fp32 per (slot, head, p, n)
+//   ome_gated_rmsnorm    : out = w * groupRMSNorm(y * silu(z))
+//
+// Sequences are described by cu[S+1] (row ranges), slot[S] (state row) and reset[S] (1 = start
+// from zero state: a sequence's first prefill chunk).  Decode is the S = batch, one-row case, so
+// the same launches are captured in the decode HIP graph.
+//
+// Scan layout: one 256-thread workgroup per (head, sequence); the head's P x N state is split so
+// that TPP = 256 / P consecutive lanes own one p row, NPT = N / TPP states each, held in VGPRs for
+// the whole sequence.  Per row every lane reads its NPT B and C values straight from global (the
+// TPP lanes of a p row read disjoint slices; the 256/TPP rows of the block read the same lines, so
+// each B/C line is fetched once per wave through the vector cache) -- no LDS and no barrier in the
+// time loop; y = C.h is a TPP-lane shuffle reduction.
+#include "common.h"
+
+#include <cstdlib>
+
+namespace {
+
+__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(__expf(x)); }
+__device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
+
+template <int K>
+__global__ __launch_bounds__(256) void ssm_conv1d_kernel(const bf16* __restrict__ x, int64_t x_stride,
+                                                         const bf16* __restrict__ w, const bf16* __restrict__ bias,
+                                                         bf16* __restrict__ out, int64_t out_stride,
+                                                         bf16* __restrict__ state, const int* __restrict__ cu,
+                                                         const int* __restrict__ slot, const int* __restrict__ reset,
+                                                         int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = blockIdx.y;
+  if (c >= C) return;
+  const int r0 = cu[s], r1 = cu[s + 1];
+  if (r1 <= r0) return;
+  bf16* st = state + ((int64_t)slot[s] * C + c) * (K - 1);
+  float win[K - 1];
+  const bool fresh = reset[s] != 0;
+#pragma unroll
+  for (int j = 0; j < K - 1; ++j) win[j] = fresh ? 0.f : (float)st[j];
+  float wt[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) wt[j] = (float)w[(int64_t)c * K + j];
+  const float b = bias != nullptr ? (float)bias[c] : 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const float v = (float)x[(int64_t)r * x_stride + c];
+    float acc = b + wt[K - 1] * v;
+#pragma unroll
+    for (int j = 0; j < K - 1; ++j) acc += wt[j] * win[j];
+#pragma unroll
+    for (int j = 0; j < K - 2; ++j) win[j] = win[j + 1];
+    win[K - 2] = v;
+    out[(int64_t)r * out_stride + c] = (bf16)silu_f(acc);
+  }
+#pragma unroll
+  for (int j = 0; j < K - 1; ++j) st[j] = (bf16)win[j];
+}
+
+template <int NPT>
+__global__ __launch_bounds__(256) void ssm_scan_kernel(
+    const bf16* __restrict__ x, int64_t x_stride, const bf16* __restrict__ dt, int64_t dt_stride,
+    const bf16* __restrict__ B, const bf16* __restrict__ Cm, int64_t bc_stride, const float* __restrict__ A,
+    const float* __restrict__ D, const float* __restrict__ dt_bias, float dt_min, float* __restrict__ state,
+    bf16* __restrict__ y, int64_t y_stride, const int* __restrict__ cu, const int* __restrict__ slot,
+    const int* __restrict__ reset, int H, int P, int N, int G) {
+  const int h = blockIdx.x, s = blockIdx.y;
+  const int r0 = cu[s], r1 = cu[s + 1];
+  if (r1 <= r0) return;
+  const int TPP = 256 / P;
+  const int p = threadIdx.x / TPP, q = threadIdx.x % TPP;
+  const int n0 = q * NPT;
+  const int g = h / (H / G);
+  float* st = state + (((int64_t)slot[s] * H + h) * P + p) * N + n0;
+  float hs[NPT];
+  const bool fresh = reset[s] != 0;
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) hs[j] = fresh ? 0.f : st[j];
+  const float a = A[h], d = D[h], db = dt_bias[h];
+  for (int r = r0; r < r1; ++r) {
+    float dtv = softplus_f((float)dt[(int64_t)r * dt_stride + h] + db);
+    dtv = fmaxf(dtv, dt_min);
+    const float dA = __expf(dtv * a);
+    const float xv = (float)x[(int64_t)r * x_stride + h * P + p];
+    const float dx = dtv * xv;
+    const bf16* br = B + (int64_t)r * bc_stride + g * N + n0;
+    const bf16* cr = Cm + (int64_t)r * bc_stride + g * N + n0;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NPT; j += 8) {
+      const bf16x8 bv = ld8(br + j), cv = ld8(cr + j);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        hs[j + k] = hs[j + k] * dA + dx * (float)bv[k];
+        acc += (float)cv[k] * hs[j + k];
+      }
+    }
+    for (int off = 1; off < TPP; off <<= 1) acc += __shfl_xor(acc, off);
+    if (q == 0) y[(int64_t)r * y_stride + h * P + p] = (bf16)(acc + d * xv);
+  }
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) st[j] = hs[j];
+}
+
+__global__ __launch_bounds__(256) void gated_rmsnorm_kernel(const bf16* __restrict__ y, int64_t y_stride,
+                                                            const bf16* __restrict__ z, int64_t z_stride,
+                                                            const bf16* __restrict__ w, bf16* __restrict__ out,
+                                                            int64_t out_stride, int group, float eps) {
+  __shared__ float red[4];
+  const int row = blockIdx.y, g0 = blockIdx.x * group;
+  const bf16* yr = y + (int64_t)row * y_stride + g0;
+  const bf16* zr = z + (int64_t)row * z_stride + g0;
+  float ss = 0.f;
+  for (int i = threadIdx.x; i < group; i += 256) {
+    const float v = (float)yr[i] * silu_f((float)zr[i]);
+    ss += v * v;
+  }
+  const float tot = block_sum<256>(ss, red);
+  const float rs = rsqrtf(tot / (float)group + eps);
+  bf16* orow = out + (int64_t)row * out_stride + g0;
+  for (int i = threadIdx.x; i < group; i += 256) {
+    const float v = (float)yr[i] * silu_f((float)zr[i]) * rs;
+    orow[i] = (bf16)((float)(bf16)v * (float)w[g0 + i]);  // HF: normalise, cast, then scale by w
+  }
+}
+
+}  // namespace
+
+OME_API int ome_ssm_conv1d(const void* x, int64_t x_stride, const void* w, const void* bias, void* out,
+                           int64_t out_stride, void* state, const int* cu, const int* slot, const int* reset, int S,
+                           int C, int K, hipStream_t stream) {
+  if (S <= 0 || C <= 0) return 0;
+  dim3 grid((C + 255) / 256, S);
+#define CONV_CASE(KK)                                                                                         \
+  case KK:                                                                                                     \
+    ssm_conv1d_kernel<KK><<<grid, 256, 0, stream>>>((const bf16*)x, x_stride, (const bf16*)w, (const bf16*)bias, \
+                                                    (bf16*)out, out_stride, (bf16*)state, cu, slot, reset, C);  \
+    break;
+  switch (K) {
+    CONV_CASE(2)
+    CONV_CASE(3)
+    CONV_CASE(4)
+    CONV_CASE(5)
+    CONV_CASE(6)
+    default:
+      return -2;
+  }
+#undef CONV_CASE
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+OME_API int ome_ssm_scan(const void* x, int64_t x_stride, const void* dt, int64_t dt_stride, const void* B,
+                         const void* Cm, int64_t bc_stride, const float* A, const float* D, const float* dt_bias,
+                         float dt_min, float* state, void* y, int64_t y_stride, const int* cu, const int* slot,
+                         const int* reset, int S, int H, int P, int N, int G, hipStream_t stream) {
+  if (S <= 0) return 0;
+  if (P <= 0 || 256 % P != 0 || H % G != 0) return -2;
+  const int tpp = 256 / P;
+  if (N % tpp != 0) return -2;
+  const int npt = N / tpp;
+  dim3 grid(H, S);
+#define SCAN_CASE(NN)                                                                                          \
+  case NN:                                                                                                      \
+    ssm_scan_kernel<NN><<<grid, 256, 0, stream>>>((const bf16*)x, x_stride, (const bf16*)dt, dt_stride,         \
+                                                  (const bf16*)B, (const bf16*)Cm, bc_stride, A, D, dt_bias,    \
+                                                  dt_min, state, (bf16*)y, y_stride, cu, slot, reset, H, P, N, G); \
+    break;
+  switch (npt) {
+    SCAN_CASE(8)
+    SCAN_CASE(16)
+    SCAN_CASE(32)
+    SCAN_CASE(64)
+    default:
+      return -3;
+  }
+#undef SCAN_CASE
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+OME_API int ome_gated_rmsnorm(const void* y, int64_t y_stride, const void* z, int64_t z_stride, const void* w,
+                              void* out, int64_t out_stride, int rows, int I, int group, float eps,
+                              hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (group <= 0 || I % group != 0) return -2;
+  dim3 grid(I / group, rows);
+  gated_rmsnorm_kernel<<<grid, 256, 0, stream>>>((const bf16*)y, y_stride, (const bf16*)z, z_stride,
+                                                 (const bf16*)w, (bf16*)out, out_stride, group, eps);
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -83,6 +83,8 @@ FAMILIES: list[Family] = [
     Family("granite-3-1-8b-instruct", "ibm-granite", "ibm-granite/granite-3.1-8b-instruct", "GraniteForCausalLM",
            8.2),
     Family("smollm3-3b", "huggingfacetb", "HuggingFaceTB/SmolLM3-3B", "SmolLM3ForCausalLM", 3.1),
+    Family("nemotron-h-8b-base", "nvidia", "nvidia/Nemotron-H-8B-Base-8K", "NemotronHForCausalLM", 8.1,
+           "nemotron-h-8b"),
     Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
 ]

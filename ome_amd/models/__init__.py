@@ -22,6 +22,7 @@ GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Ge
 LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM"}
 LLAMA4_ARCHS = {"Llama4ForCausalLM", "Llama4ForConditionalGeneration"}
 QWEN2_VL_ARCHS = {"Qwen2VLForConditionalGeneration"}
+NEMOTRON_H_ARCHS = {"NemotronHForCausalLM"}
 MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM", "DeepseekV2ForCausalLM",
              "DeepseekV3ForCausalLM", "PhiMoEForCausalLM"}
 
@@ -35,6 +36,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.gemma import GemmaForCausalLM
 
         return GemmaForCausalLM
+    if cfg.architecture in NEMOTRON_H_ARCHS or cfg.model_type == "nemotron_h":
+        from ome_amd.models.nemotron_h import NemotronHForCausalLM
+
+        return NemotronHForCausalLM
     if cfg.architecture in QWEN2_VL_ARCHS or cfg.model_type == "qwen2_vl":
         from ome_amd.models.qwen2_vl import Qwen2VLForConditionalGeneration
 
@@ -61,7 +66,7 @@ def model_class(cfg: ModelConfig):
 
 
 def supported(arch: str) -> bool:
-    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or \
+    return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or arch in NEMOTRON_H_ARCHS or \
         arch == "GptOssForCausalLM"
 
 

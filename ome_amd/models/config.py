@@ -107,13 +107,16 @@ class ModelConfig:
             architecture=arch,
             model_type=mt,
             hidden_size=H,
-            num_layers=text.get("num_hidden_layers", 32),
+            num_layers=len(text["layers_block_type"]) if text.get("layers_block_type") else
+            len(text["hybrid_override_pattern"]) if text.get("hybrid_override_pattern") else
+            text.get("num_hidden_layers", 32),
             num_heads=nh,
             num_kv_heads=text.get("num_key_value_heads") or nh,
             head_dim=hd,
             intermediate_size=text.get("intermediate_size", 4 * H),
             vocab_size=text.get("vocab_size", 32000),
-            rms_norm_eps=text.get("rms_norm_eps") or text.get("layer_norm_eps") or text.get("norm_epsilon") or 1e-6,
+            rms_norm_eps=text.get("rms_norm_eps") or text.get("layer_norm_eps") or text.get("norm_epsilon") or
+            text.get("layer_norm_epsilon") or 1e-6,
             rope_theta=rope_theta,
             rope_scaling=rope_scaling,
             partial_rotary_factor=float(prf),
@@ -267,6 +270,17 @@ PRESETS: dict[str, dict] = {
                           vision_config=dict(depth=2, embed_dim=128, hidden_size=256, num_heads=4, mlp_ratio=2,
                                              patch_size=14, spatial_merge_size=2, temporal_patch_size=2,
                                              in_channels=3, hidden_act="quick_gelu")),
+    "nemotron-h-8b": dict(architectures=["NemotronHForCausalLM"], model_type="nemotron_h", hidden_size=4096,
+                          hybrid_override_pattern="M-M-M-M*-M-M-M-M-M*-M-M-M-M-M*-M-M-M-M-M*-M-M-M-M-M-",
+                          num_attention_heads=32, num_key_value_heads=8, head_dim=128, intermediate_size=21504,
+                          mlp_hidden_act="relu2", mamba_num_heads=128, mamba_head_dim=64, ssm_state_size=128,
+                          n_groups=8, conv_kernel=4, vocab_size=131072, layer_norm_epsilon=1e-5,
+                          max_position_embeddings=8192, time_step_min=0.001, tie_word_embeddings=False),
+    "tiny-nemotron-h": dict(architectures=["NemotronHForCausalLM"], model_type="nemotron_h", hidden_size=256,
+                            hybrid_override_pattern="M-M*-M", num_attention_heads=4, num_key_value_heads=2,
+                            head_dim=64, intermediate_size=512, mlp_hidden_act="relu2", mamba_num_heads=8,
+                            mamba_head_dim=64, ssm_state_size=64, n_groups=2, conv_kernel=4, vocab_size=1024,
+                            layer_norm_epsilon=1e-5, max_position_embeddings=4096, time_step_min=0.001),
     "tiny-llama4": dict(architectures=["Llama4ForCausalLM"], model_type="llama4_text", hidden_size=256,
                         num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                         intermediate_size=256, intermediate_size_mlp=512, num_local_experts=8, num_experts_per_tok=1,

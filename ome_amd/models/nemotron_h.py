@@ -1,0 +1,222 @@
+"""NemotronH hybrid Mamba-2 / attention / MLP decoders (``NemotronHForCausalLM``; reference catalog
+``config/runtimes/srt/nvidia/nemotron-h-*`` runtimes) on the ome_amd kernels.
+
+Layer types (``layers_block_type`` / the legacy ``hybrid_override_pattern`` M * - E): every block
+is ``h + mixer(RMSNorm(h))`` with
+
+* ``M`` Mamba-2 mixer: in_proj GEMM -> [z | xBC | dt] -> causal depthwise conv1d + SiLU
+  (``ome_ssm_conv1d``) -> selective scan with per-head A, D, dt_bias and n_groups shared B/C
+  (``ome_ssm_scan``: recurrent, fp32 state held in VGPRs across a sequence's rows) -> gated
+  group RMSNorm ``w * norm(y * silu(z))`` (``ome_gated_rmsnorm``) -> out_proj GEMM;
+* ``*`` attention without positional encoding (GQA, the fused QKV / paged-KV kernel with
+  ``apply_rope=False``, paged decode / prefill attention) -- only these layers own KV pages;
+* ``-`` MLP ``down(relu(up(x))^2)`` (``ome_act`` ReLU^2 in place between two GEMMs).
+
+Recurrent state lives per request slot (the row of the page-table pool, ``Request.req_slot``):
+conv state [slots, conv_dim, K-1] (model dtype) and SSM state [slots, H, P, N] (fp32) per Mamba
+layer; a sequence's first prefill chunk starts from zeros (``reset``), later chunks and decode
+rows continue.  The prefix cache is disabled for this family (a prefix's SSM state is not paged).
+HIP-graph decode captures the same kernels with one-row sequences.  Tensor parallelism is not
+implemented for this family (tp must be 1).  The dt clamp ``time_step_min`` is applied on every
+row (HF clamps in its chunked prefill path only).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ome_amd import ops
+from ome_amd.models.common import AttnMeta, PagedKVCache
+from ome_amd.models.config import ModelConfig
+from ome_amd.models.llama import LlamaForCausalLM
+from ome_amd.models.quant import linear
+from ome_amd.parallel import state as pstate
+
+NEMOTRON_H_ARCHS = {"NemotronHForCausalLM"}
+_CODES = {"M": "linear_attention", "*": "full_attention", "-": "mlp", "E": "moe"}
+_LEGACY = {"mamba": "linear_attention", "attention": "full_attention", "mlp": "mlp", "moe": "moe"}
+
+
+def layer_types(hf: dict) -> list[str]:
+    t = hf.get("layers_block_type") or hf.get("layer_types")
+    if t:
+        return [_LEGACY.get(x, x) for x in t]
+    pat = hf.get("hybrid_override_pattern")
+    if pat:
+        return [_CODES[c] for c in pat]
+    return ["linear_attention", "moe", "full_attention", "mlp"]
+
+
+class NemotronHForCausalLM(LlamaForCausalLM):
+    stateful = True
+
+    def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
+        super().__init__(cfg, device, dtype, max_positions)
+        if self.tp.tp > 1 or pstate.get().pp_size > 1:
+            raise NotImplementedError("NemotronH runs on one GPU per replica (no TP / PP yet)")
+        hf = cfg.extra or {}
+        self.types = layer_types(hf)
+        if "moe" in self.types:
+            raise NotImplementedError("NemotronH MoE blocks are not implemented")
+        self.kv_layers = [i for i in self.layers if self.types[i] == "full_attention"]
+        self.mamba_layers = [i for i in self.layers if self.types[i] == "linear_attention"]
+        self.mi = {i: k for k, i in enumerate(self.mamba_layers)}
+        self.H = int(hf.get("mamba_num_heads", 128))
+        self.P = int(hf.get("mamba_head_dim", 64))
+        self.N = int(hf.get("ssm_state_size", 128))
+        self.G = int(hf.get("n_groups", 8))
+        self.K = int(hf.get("conv_kernel", 4))
+        self.I = self.H * self.P
+        self.conv_dim = self.I + 2 * self.G * self.N
+        self.dt_min = float(hf.get("time_step_min", 0.001) or 0.0)
+        self.inter = int(hf.get("intermediate_size", cfg.intermediate_size))
+        self.mlp_act = {"relu2": 4, "silu": 0, "gelu": 3}[hf.get("mlp_hidden_act", "relu2")]
+        L = cfg.num_layers
+        self.w_in: list[torch.Tensor | None] = [None] * L
+        self.conv_w: list[torch.Tensor | None] = [None] * L
+        self.conv_b: list[torch.Tensor | None] = [None] * L
+        self.A: list[torch.Tensor | None] = [None] * L
+        self.Dp: list[torch.Tensor | None] = [None] * L
+        self.dt_bias: list[torch.Tensor | None] = [None] * L
+        self.gnorm: list[torch.Tensor | None] = [None] * L
+        self.w_out: list[torch.Tensor | None] = [None] * L
+        self.conv_state: torch.Tensor | None = None
+        self.ssm_state: torch.Tensor | None = None
+
+    def alloc_state(self, slots: int) -> None:
+        nm = len(self.mamba_layers)
+        self.conv_state = torch.zeros(nm, slots, self.conv_dim, self.K - 1, dtype=self.dtype, device=self.device)
+        self.ssm_state = torch.zeros(nm, slots, self.H, self.P, self.N, dtype=torch.float32, device=self.device)
+
+    # ------------------------------------------------------------------ weights
+    def init_random(self, seed: int = 0, std: float = 0.02) -> "NemotronHForCausalLM":
+        cfg, tp, D = self.cfg, self.tp, self.D
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed)
+        Hd = cfg.hidden_size
+        f32 = dict(dtype=torch.float32, device=self.device)
+        for i in self.layers:
+            self.ln1[i] = self._alloc(Hd, std=None, gen=gen)
+            t = self.types[i]
+            if t == "linear_attention":
+                self.w_in[i] = self._alloc(self.I + self.conv_dim + self.H, Hd, std=std, gen=gen)
+                self.conv_w[i] = self._alloc(self.conv_dim, self.K, std=0.2, gen=gen)
+                self.conv_b[i] = self._alloc(self.conv_dim, std=std, gen=gen)
+                self.A[i] = -torch.arange(1, self.H + 1, **f32)
+                self.Dp[i] = torch.ones(self.H, **f32)
+                self.dt_bias[i] = torch.full((self.H,), math.log(math.expm1(0.01)), **f32)
+                self.gnorm[i] = self._alloc(self.I, std=None, gen=gen)
+                self.w_out[i] = self._alloc(Hd, self.I, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+            elif t == "full_attention":
+                self.w_qkv[i] = self._alloc((tp.hq + 2 * tp.hkv) * D, Hd, std=std, gen=gen)
+                self.w_o[i] = self._alloc(Hd, tp.hq * D, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+            else:
+                self.w_gu[i] = self._alloc(self.inter, Hd, std=std, gen=gen)
+                self.w_d[i] = self._alloc(Hd, self.inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+        self.embed = self._alloc(tp.vocab, Hd, std=1.0, gen=gen)
+        self.norm = self._alloc(Hd, std=None, gen=gen)
+        self.lm_head = self.embed if cfg.tie_word_embeddings else self._alloc(tp.vocab, Hd, std=std, gen=gen)
+        return self
+
+    def load_hf_weights(self, weights) -> "NemotronHForCausalLM":
+        def put(t, dtype=None):
+            return t.to(device=self.device, dtype=dtype or self.dtype).contiguous()
+
+        qkv: dict[int, dict[str, torch.Tensor]] = {}
+        for name, w in weights:
+            for pre in ("backbone.", "model."):
+                if name.startswith(pre):
+                    name = name[len(pre):]
+                    break
+            if name in ("embedding.weight", "embeddings.weight", "embed_tokens.weight"):
+                self.embed = put(self._vocab_shard(w))
+                continue
+            if name in ("norm_f.weight", "norm.weight"):
+                self.norm = put(w)
+                continue
+            if name == "lm_head.weight":
+                self.lm_head = put(self._vocab_shard(w))
+                continue
+            parts = name.split(".")
+            if parts[0] != "layers":
+                continue
+            i, sub = int(parts[1]), ".".join(parts[2:])
+            if i not in self._layer_set:
+                continue
+            if sub == "norm.weight":
+                self.ln1[i] = put(w)
+            elif sub == "mixer.in_proj.weight":
+                self.w_in[i] = put(w)
+            elif sub == "mixer.conv1d.weight":
+                self.conv_w[i] = put(w.reshape(w.shape[0], -1))
+            elif sub == "mixer.conv1d.bias":
+                self.conv_b[i] = put(w)
+            elif sub == "mixer.A_log":
+                self.A[i] = -torch.exp(w.float()).to(self.device)
+            elif sub == "mixer.D":
+                self.Dp[i] = put(w, torch.float32)
+            elif sub == "mixer.dt_bias":
+                self.dt_bias[i] = put(w, torch.float32)
+            elif sub == "mixer.norm.weight":
+                self.gnorm[i] = put(w)
+            elif sub == "mixer.out_proj.weight":
+                self.w_out[i] = put(w)
+            elif sub in ("mixer.q_proj.weight", "mixer.k_proj.weight", "mixer.v_proj.weight"):
+                qkv.setdefault(i, {})[sub[6]] = w
+            elif sub == "mixer.o_proj.weight":
+                self.w_o[i] = put(w)
+            elif sub == "mixer.up_proj.weight":
+                self.w_gu[i] = put(w)
+            elif sub == "mixer.down_proj.weight":
+                self.w_d[i] = put(w)
+        for i, d in qkv.items():
+            self.w_qkv[i] = put(torch.cat([d["q"], d["k"], d["v"]], 0))
+        if self.lm_head is None:
+            self.lm_head = self.embed
+        return self
+
+    def weight_bytes(self) -> int:
+        n = super().weight_bytes()
+        for lst in (self.w_in, self.conv_w, self.conv_b, self.gnorm, self.w_out):
+            n += sum(t.numel() * t.element_size() for t in lst if t is not None)
+        return n
+
+    # ------------------------------------------------------------------ forward
+    def mamba(self, i: int, x: torch.Tensor, seqs) -> torch.Tensor:
+        cu, slot, reset = seqs
+        I, cd, H, G, N = self.I, self.conv_dim, self.H, self.G, self.N
+        k = self.mi[i]
+        zxd = linear(x, self.w_in[i])
+        z, xbc, dt = zxd[:, :I], zxd[:, I:I + cd], zxd[:, I + cd:]
+        conv = ops.ssm_conv1d(xbc, self.conv_w[i], self.conv_b[i], self.conv_state[k], cu, slot, reset)
+        xs, B, C = conv[:, :I], conv[:, I:I + G * N], conv[:, I + G * N:]
+        y = ops.ssm_scan(xs, dt, B, C, self.A[i], self.Dp[i], self.dt_bias[i], self.dt_min, self.ssm_state[k], cu,
+                         slot, reset, H, self.P, N, G)
+        y = ops.gated_rmsnorm(y, z, self.gnorm[i], I // G, self.eps)
+        return linear(y, self.w_out[i])
+
+    def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: PagedKVCache,
+                input_embeds: torch.Tensor | None = None) -> torch.Tensor:
+        tp, D = self.tp, self.D
+        T = ids.shape[0]
+        seqs = meta.extra["ssm"]
+        x, residual = self._stage_input(ids, input_embeds)
+        for i in self.layers:
+            if i > 0:
+                ops.fused_add_rmsnorm(x, residual, self.ln1[i], self.eps)
+            t = self.types[i]
+            if t == "linear_attention":
+                x = self.mamba(i, x, seqs)
+            elif t == "full_attention":
+                qkv = linear(x, self.w_qkv[i])
+                q = torch.empty(T, tp.hq, D, dtype=self.dtype, device=x.device)
+                k_cache, v_cache = kv.layer(i)
+                ks, vs = kv.scales(i)
+                ops.rope_qkv_cache(qkv, meta.positions, self.cos_sin, self.cfg.rot_dim, q, k_cache, v_cache,
+                                   meta.slots, tp.hq, tp.hkv, D, False, None, None, self.eps, ks, vs)
+                attn = self.attention(q, k_cache, v_cache, meta, ks, vs)
+                x = linear(attn.view(T, tp.hq * D), self.w_o[i])
+            else:
+                x = linear(ops.act(linear(x, self.w_gu[i]), self.mlp_act), self.w_d[i])
+        return self._stage_output(x, residual)

@@ -72,12 +72,54 @@ def fused_add_layernorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: 
 
 
 def act(x: torch.Tensor, kind: int) -> torch.Tensor:
-    """In place non-gated activation: 0 SiLU, 1 GELU-tanh, 3 GELU (erf)."""
+    """In place non-gated activation: 0 SiLU, 1 GELU-tanh, 3 GELU (erf), 4 ReLU^2."""
     if not _gpu(x):
         return ref.act(x, kind)
     assert x.is_contiguous() and x.dtype == torch.bfloat16
     call("ome_act", x.data_ptr(), x.numel(), int(kind), stream_ptr())
     return x
+
+
+def ssm_conv1d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, state: torch.Tensor, cu, slot, reset,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """Mamba causal depthwise conv1d + SiLU over varlen sequences (rows ``cu[s]:cu[s+1]``), continuing
+    from and updating ``state`` [slots, C, K-1]; ``reset[s]`` = 1 starts sequence ``s`` from zeros."""
+    T, C = x.shape
+    out = torch.empty(T, C, dtype=x.dtype, device=x.device) if out is None else out
+    if not _gpu(x):
+        return ref.ssm_conv1d(x, w, bias, state, cu, slot, reset, out)
+    assert x.stride(1) == 1 and out.stride(1) == 1 and w.is_contiguous() and state.is_contiguous()
+    call("ome_ssm_conv1d", x.data_ptr(), x.stride(0), w.data_ptr(), ptr(bias), out.data_ptr(), out.stride(0),
+         state.data_ptr(), _i32(cu).data_ptr(), _i32(slot).data_ptr(), _i32(reset).data_ptr(), slot.shape[0], C,
+         w.shape[1], stream_ptr())
+    return out
+
+
+def ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min: float, state, cu, slot, reset, H: int, P: int, N: int, G: int,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    """Mamba-2 selective scan, recurrent over each sequence's rows: x [T, H*P], dt [T, H], B/C
+    [T, G*N] (row-strided views are fine), A/D/dt_bias fp32 [H], state fp32 [slots, H, P, N]."""
+    T = x.shape[0]
+    out = torch.empty(T, H * P, dtype=x.dtype, device=x.device) if out is None else out
+    if not _gpu(x):
+        return ref.ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min, state, cu, slot, reset, H, P, N, G, out)
+    assert B.stride(0) == C.stride(0) and B.stride(1) == 1 and x.stride(1) == 1 and dt.stride(1) == 1
+    call("ome_ssm_scan", x.data_ptr(), x.stride(0), dt.data_ptr(), dt.stride(0), B.data_ptr(), C.data_ptr(),
+         B.stride(0), A.data_ptr(), D.data_ptr(), dt_bias.data_ptr(), float(dt_min), state.data_ptr(),
+         out.data_ptr(), out.stride(0), _i32(cu).data_ptr(), _i32(slot).data_ptr(), _i32(reset).data_ptr(),
+         slot.shape[0], H, P, N, G, stream_ptr())
+    return out
+
+
+def gated_rmsnorm(y: torch.Tensor, z: torch.Tensor, w: torch.Tensor, group: int, eps: float) -> torch.Tensor:
+    """w * groupRMSNorm(y * silu(z)) (Mamba-2 output norm, groups of ``group`` channels)."""
+    if not _gpu(y):
+        return ref.gated_rmsnorm(y, z, w, group, eps)
+    T, I = y.shape
+    out = torch.empty(T, I, dtype=y.dtype, device=y.device)
+    call("ome_gated_rmsnorm", y.data_ptr(), y.stride(0), z.data_ptr(), z.stride(0), w.data_ptr(), out.data_ptr(),
+         out.stride(0), T, I, group, float(eps), stream_ptr())
+    return out
 
 
 #: paged KV-cache element formats understood by the kernels (csrc/kernels/common.h KVFmt)

@@ -40,10 +40,58 @@ def act(x: torch.Tensor, kind: int) -> torch.Tensor:
         y = torch.nn.functional.silu(f)
     elif kind == 1:
         y = torch.nn.functional.gelu(f, approximate="tanh")
+    elif kind == 4:
+        y = torch.relu(f).square()
     else:
         y = torch.nn.functional.gelu(f)
     x.copy_(y.to(x.dtype))
     return x
+
+
+def ssm_conv1d(x, w, bias, state, cu, slot, reset, out):
+    """Causal depthwise conv + SiLU per sequence, continuing from / updating ``state`` [slots, C, K-1]."""
+    K = w.shape[1]
+    for s in range(len(slot)):
+        r0, r1 = int(cu[s]), int(cu[s + 1])
+        if r1 <= r0:
+            continue
+        st = state[int(slot[s])]
+        prev = torch.zeros_like(st) if int(reset[s]) else st
+        seq = torch.cat([prev.float().t(), x[r0:r1].float()], 0)          # [K-1+L, C]
+        o = torch.nn.functional.conv1d(seq.t()[None], w.float()[:, None, :], None if bias is None else bias.float(),
+                                       groups=w.shape[0])[0].t()          # [L, C]
+        out[r0:r1] = torch.nn.functional.silu(o).to(out.dtype)
+        st.copy_(seq[-(K - 1):].t().to(st.dtype))
+    return out
+
+
+def ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min, state, cu, slot, reset, H, P, N, G, out):
+    """Selective scan (Mamba-2), recurrent per sequence; ``state`` [slots, H, P, N] fp32."""
+    rep = H // G
+    for s in range(len(slot)):
+        r0, r1 = int(cu[s]), int(cu[s + 1])
+        if r1 <= r0:
+            continue
+        st = state[int(slot[s])]
+        h = torch.zeros_like(st) if int(reset[s]) else st.clone()
+        for r in range(r0, r1):
+            d = torch.nn.functional.softplus(dt[r].float() + dt_bias).clamp(min=dt_min)        # [H]
+            xv = x[r].float().view(H, P)
+            b = B[r].float().view(G, N).repeat_interleave(rep, 0)                               # [H, N]
+            c = C[r].float().view(G, N).repeat_interleave(rep, 0)
+            h = h * torch.exp(d * A)[:, None, None] + (d[:, None] * xv)[..., None] * b[:, None, :]
+            y = (h * c[:, None, :]).sum(-1) + D[:, None] * xv
+            out[r] = y.reshape(-1).to(out.dtype)
+        st.copy_(h)
+    return out
+
+
+def gated_rmsnorm(y, z, w, group, eps):
+    v = y.float() * torch.nn.functional.silu(z.float())
+    T, I = v.shape
+    g = v.view(T, I // group, group)
+    g = g * torch.rsqrt(g.pow(2).mean(-1, keepdim=True) + eps)
+    return w * g.view(T, I).to(y.dtype)
 
 
 def apply_rope(x: torch.Tensor, cs: torch.Tensor, rot_dim: int) -> torch.Tensor:

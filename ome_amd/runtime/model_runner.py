@@ -107,7 +107,8 @@ class ModelRunner:
         # ---- KV cache sizing (reference: --mem-frac 0.9, llama-3-8b-instruct-rt.yaml:59-60) ----
         tp = self.model.tp
         kv_heads, k_dim, v_dim = getattr(self.model, "kv_layout", (tp.hkv, cfg.head_dim, cfg.head_dim))
-        n_local = len(self.model.layers)
+        kv_layers = getattr(self.model, "kv_layers", None)  # hybrid models: only attention layers own KV
+        n_local = len(self.model.layers if kv_layers is None else kv_layers)
         kv_dtype = kv_cache_dtype(kv_cache_dtype_name, dtype)
         if kv_dtype != dtype and getattr(self.model, "kv_layout", None) is not None:
             # MLA's latent cache (mla.hip) keeps the model dtype
@@ -129,12 +130,17 @@ class ModelRunner:
             want = min(want, -(-max_total_tokens // page_size) + 2)
         num_pages = max(min(num_pages, want), max_pages_per_seq + 2)
         self.kv = PagedKVCache(cfg.num_layers, num_pages, kv_heads, k_dim, page_size, kv_dtype, self.device, v_dim,
-                               layers=self.model.layers)
+                               layers=self.model.layers if kv_layers is None else kv_layers)
         if self.kv.is_fp8:
             self.kv.set_scales(getattr(self.model, "kv_scales", None) or {})
         self.pp = pstate.get().pp_size > 1
         self.pages = PagePool(num_pages)
         self.slots = ReqSlotPool(max_running + 1, max_pages_per_seq, self.device)
+        self.stateful = bool(getattr(self.model, "stateful", False))
+        if self.stateful:  # recurrent (SSM) state per request slot, the padding slot included
+            self.model.alloc_state(max_running + 1)
+            self._ssm_cu = torch.arange(max_running + 2, dtype=torch.int32, device=self.device)
+            self._ssm_zero = torch.zeros(max_running + 1, dtype=torch.int32, device=self.device)
         log.info("KV cache: %d pages x %d tokens (%.1f GiB), weights %.1f GiB", num_pages, page_size,
                  num_pages * page_bytes / 2**30, self.model.weight_bytes() / 2**30)
         # ---- decode graphs ----
@@ -184,6 +190,8 @@ class ModelRunner:
         bt = self.slots.table.index_select(0, d.view("req_idx", bs))
         meta = AttnMeta("decode", d.view("pos", bs), d.view("slots", bs), bt, seq_lens=d.view("seq_lens", bs),
                         decode_ws=self.decode_ws(bs), order=d.view("order", bs))
+        if self.stateful:  # one-row sequences continuing each request slot's state
+            meta.extra["ssm"] = (self._ssm_cu[:bs + 1], d.view("req_idx", bs), self._ssm_zero[:bs])
         hidden = self.model.forward(d.view("ids", bs), meta, self.kv)
         logits = self.model.compute_logits(hidden)
         pen = (d.view("rep", bs), d.view("freq", bs), d.view("pres", bs))
@@ -459,6 +467,15 @@ class ModelRunner:
             meta = AttnMeta("decode", t_pos, t_slots, self.slots.table.index_select(0, t_dreq), seq_lens=t_dlen,
                             decode_ws=ws, order=t_dord)
         self._init_penalty_rows(chunks)
+        if self.stateful:  # sequences in row order: prefill chunks, then single-token rows
+            lens = [chunks[i].length for i in pre + dec]
+            cu_s = np.zeros(len(lens) + 1, dtype=np.int32)
+            cu_s[1:] = np.cumsum(lens)
+            sl = np.asarray([chunks[i].req.req_slot for i in pre + dec], np.int32)
+            rs = np.asarray([int(chunks[i].start == 0) for i in pre + dec], np.int32)
+            pk = torch.from_numpy(np.concatenate([cu_s, sl, rs])).to(self.device, non_blocking=True)
+            S_ = len(lens)
+            meta.extra["ssm"] = (pk[:S_ + 1], pk[S_ + 1:2 * S_ + 1], pk[2 * S_ + 1:])
         embeds = None
         if getattr(self.model, "is_multimodal", False) and any(chunks[i].req.mm is not None for i in pre + dec):
             embeds = self._mm_prepare(chunks, pre + dec, T, t_ids, meta)
@@ -553,6 +570,10 @@ class ModelRunner:
                         cu_q=torch.tensor([0, 1], dtype=torch.int32, device=dv),
                         kv_lens=torch.ones(1, dtype=torch.int32, device=dv),
                         items=torch.zeros(1, 2, dtype=torch.int32, device=dv))
+        if self.stateful:
+            pad = self.slots.max_reqs - 1
+            meta.extra["ssm"] = (self._ssm_cu[:2], torch.full((1,), pad, dtype=torch.int32, device=dv),
+                                 torch.ones(1, dtype=torch.int32, device=dv))
         self.model.forward(z, meta, self.kv)
 
     def embed(self, batch: StepBatch) -> list[list[float]]:
