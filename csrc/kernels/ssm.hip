@@ -24,6 +24,8 @@
 
 namespace {
 
+typedef float f32v4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(__expf(x)); }
 __device__ __forceinline__ float silu_f(float x) { return x / (1.f + __expf(-x)); }
 
@@ -62,49 +64,81 @@ __global__ __launch_bounds__(256) void ssm_conv1d_kernel(const bf16* __restrict_
   for (int j = 0; j < K - 1; ++j) st[j] = (bf16)win[j];
 }
 
-template <int NPT>
+template <int NPT, bool NT>
 __global__ __launch_bounds__(256) void ssm_scan_kernel(
     const bf16* __restrict__ x, int64_t x_stride, const bf16* __restrict__ dt, int64_t dt_stride,
     const bf16* __restrict__ B, const bf16* __restrict__ Cm, int64_t bc_stride, const float* __restrict__ A,
     const float* __restrict__ D, const float* __restrict__ dt_bias, float dt_min, float* __restrict__ state,
     bf16* __restrict__ y, int64_t y_stride, const int* __restrict__ cu, const int* __restrict__ slot,
-    const int* __restrict__ reset, int H, int P, int N, int G) {
-  const int h = blockIdx.x, s = blockIdx.y;
+    const int* __restrict__ reset, int H, int P, int N, int G, int PB) {
+  // a workgroup owns PB of the head's P rows (P / PB workgroups per head and sequence)
+  const int split = P / PB;
+  const int h = blockIdx.x / split, s = blockIdx.y;
   const int r0 = cu[s], r1 = cu[s + 1];
   if (r1 <= r0) return;
-  const int TPP = 256 / P;
-  const int p = threadIdx.x / TPP, q = threadIdx.x % TPP;
+  const int TPP = 256 / PB;
+  const int p = (blockIdx.x % split) * PB + threadIdx.x / TPP, q = threadIdx.x % TPP;
   const int n0 = q * NPT;
   const int g = h / (H / G);
-  float* st = state + (((int64_t)slot[s] * H + h) * P + p) * N + n0;
+  // state row: NPT contiguous fp32 per lane, a wave covers one contiguous 64*NPT*4-byte span:
+  // moved with 16-B vector loads / stores (decode is bound by this state traffic)
+  f32v4* st4 = reinterpret_cast<f32v4*>(state + (((int64_t)slot[s] * H + h) * P + p) * N + n0);
   float hs[NPT];
-  const bool fresh = reset[s] != 0;
+  if (reset[s] != 0) {
 #pragma unroll
-  for (int j = 0; j < NPT; ++j) hs[j] = fresh ? 0.f : st[j];
+    for (int j = 0; j < NPT; ++j) hs[j] = 0.f;
+  } else {
+#pragma unroll
+    for (int j = 0; j < NPT / 4; ++j) {
+      const f32v4 v = NT ? __builtin_nontemporal_load(st4 + j) : st4[j];
+      hs[4 * j] = v.x, hs[4 * j + 1] = v.y, hs[4 * j + 2] = v.z, hs[4 * j + 3] = v.w;
+    }
+  }
   const float a = A[h], d = D[h], db = dt_bias[h];
+  const int64_t boff = (int64_t)g * N + n0;
+  // software pipeline: the next row's dt / x / B / C are loaded while this row's FMAs run
+  bf16x8 bn[NPT / 8], cn[NPT / 8];
+  float dtn = 0.f, xn = 0.f;
+  auto fetch = [&](int r) {
+    dtn = (float)dt[(int64_t)r * dt_stride + h];
+    xn = (float)x[(int64_t)r * x_stride + h * P + p];
+#pragma unroll
+    for (int j = 0; j < NPT / 8; ++j) {
+      bn[j] = ld8(B + (int64_t)r * bc_stride + boff + 8 * j);
+      cn[j] = ld8(Cm + (int64_t)r * bc_stride + boff + 8 * j);
+    }
+  };
+  fetch(r0);
   for (int r = r0; r < r1; ++r) {
-    float dtv = softplus_f((float)dt[(int64_t)r * dt_stride + h] + db);
-    dtv = fmaxf(dtv, dt_min);
+    bf16x8 bv[NPT / 8], cv[NPT / 8];
+#pragma unroll
+    for (int j = 0; j < NPT / 8; ++j) bv[j] = bn[j], cv[j] = cn[j];
+    const float dtr = dtn, xv = xn;
+    if (r + 1 < r1) fetch(r + 1);
+    const float dtv = fmaxf(softplus_f(dtr + db), dt_min);
     const float dA = __expf(dtv * a);
-    const float xv = (float)x[(int64_t)r * x_stride + h * P + p];
     const float dx = dtv * xv;
-    const bf16* br = B + (int64_t)r * bc_stride + g * N + n0;
-    const bf16* cr = Cm + (int64_t)r * bc_stride + g * N + n0;
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < NPT; j += 8) {
-      const bf16x8 bv = ld8(br + j), cv = ld8(cr + j);
+    for (int j = 0; j < NPT / 8; ++j)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        hs[j + k] = hs[j + k] * dA + dx * (float)bv[k];
-        acc += (float)cv[k] * hs[j + k];
+        hs[8 * j + k] = hs[8 * j + k] * dA + dx * (float)bv[j][k];
+        acc += (float)cv[j][k] * hs[8 * j + k];
       }
-    }
     for (int off = 1; off < TPP; off <<= 1) acc += __shfl_xor(acc, off);
     if (q == 0) y[(int64_t)r * y_stride + h * P + p] = (bf16)(acc + d * xv);
   }
 #pragma unroll
-  for (int j = 0; j < NPT; ++j) st[j] = hs[j];
+  for (int j = 0; j < NPT / 4; ++j)
+  {
+    const f32v4 v{hs[4 * j], hs[4 * j + 1], hs[4 * j + 2], hs[4 * j + 3]};
+    if constexpr (NT) {
+      __builtin_nontemporal_store(v, st4 + j);
+    } else {
+      st4[j] = v;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void gated_rmsnorm_kernel(const bf16* __restrict__ y, int64_t y_stride,
@@ -161,16 +195,30 @@ OME_API int ome_ssm_scan(const void* x, int64_t x_stride, const void* dt, int64_
                          const int* reset, int S, int H, int P, int N, int G, hipStream_t stream) {
   if (S <= 0) return 0;
   if (P <= 0 || 256 % P != 0 || H % G != 0) return -2;
-  const int tpp = 256 / P;
+  // rows per workgroup: the whole head (PB = P).  Splitting a head's rows over more workgroups
+  // (PB = P/4, 8 states per lane) measured SLOWER for 2 x 512-row prefill on gfx950 (812 vs 550 us,
+  // scripts/ssm_scan_bench.py): the row loop is latency-bound per step, not occupancy-bound.
+  const char* pbe = getenv("OME_SSM_PB");
+  const int PB = pbe != nullptr && atoi(pbe) > 0 && P % atoi(pbe) == 0 ? atoi(pbe) : P;
+  const int tpp = 256 / PB;
   if (N % tpp != 0) return -2;
   const int npt = N / tpp;
-  dim3 grid(H, S);
+  dim3 grid(H * (P / PB), S);
 #define SCAN_CASE(NN)                                                                                          \
   case NN:                                                                                                      \
-    ssm_scan_kernel<NN><<<grid, 256, 0, stream>>>((const bf16*)x, x_stride, (const bf16*)dt, dt_stride,         \
-                                                  (const bf16*)B, (const bf16*)Cm, bc_stride, A, D, dt_bias,    \
-                                                  dt_min, state, (bf16*)y, y_stride, cu, slot, reset, H, P, N, G); \
+    if (nt)                                                                                                     \
+      ssm_scan_kernel<NN, true><<<grid, 256, 0, stream>>>((const bf16*)x, x_stride, (const bf16*)dt, dt_stride,  \
+                                                          (const bf16*)B, (const bf16*)Cm, bc_stride, A, D,      \
+                                                          dt_bias, dt_min, state, (bf16*)y, y_stride, cu, slot,  \
+                                                          reset, H, P, N, G, PB);                                \
+    else                                                                                                        \
+      ssm_scan_kernel<NN, false><<<grid, 256, 0, stream>>>((const bf16*)x, x_stride, (const bf16*)dt, dt_stride, \
+                                                           (const bf16*)B, (const bf16*)Cm, bc_stride, A, D,     \
+                                                           dt_bias, dt_min, state, (bf16*)y, y_stride, cu, slot, \
+                                                           reset, H, P, N, G, PB);                               \
     break;
+  const char* nte = getenv("OME_SSM_NT");  // state I/O: 1 = non-temporal, 0 = plain (default)
+  const bool nt = nte != nullptr && atoi(nte) != 0;
   switch (npt) {
     SCAN_CASE(8)
     SCAN_CASE(16)
