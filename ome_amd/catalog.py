@@ -79,6 +79,7 @@ FAMILIES: list[Family] = [
     Family("phi-3-5-moe-instruct", "microsoft", "microsoft/Phi-3.5-MoE-instruct", "PhiMoEForCausalLM", 41.9),
     Family("starcoder2-7b", "bigcode", "bigcode/starcoder2-7b", "Starcoder2ForCausalLM", 7.2, "starcoder2-7b"),
     Family("pythia-1-4b", "eleutherai", "EleutherAI/pythia-1.4b", "GPTNeoXForCausalLM", 1.4, "pythia-1.4b"),
+    Family("phi-2", "microsoft", "microsoft/phi-2", "PhiForCausalLM", 2.8, "phi-2"),
     Family("internlm2-7b-chat", "internlm", "internlm/internlm2-chat-7b", "InternLM2ForCausalLM", 7.7),
     Family("granite-3-1-8b-instruct", "ibm-granite", "ibm-granite/granite-3.1-8b-instruct", "GraniteForCausalLM",
            8.2),

@@ -19,7 +19,7 @@ DENSE_ARCHS = {
     "Qwen2ForRewardModel", "Phi3ForCausalLM", "GraniteForCausalLM", "SmolLM3ForCausalLM",
 }
 GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
-LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM"}
+LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalLM"}
 LLAMA4_ARCHS = {"Llama4ForCausalLM", "Llama4ForConditionalGeneration"}
 QWEN2_VL_ARCHS = {"Qwen2VLForConditionalGeneration"}
 NEMOTRON_H_ARCHS = {"NemotronHForCausalLM"}
@@ -48,7 +48,7 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.llama4 import Llama4ForCausalLM
 
         return Llama4ForCausalLM
-    if cfg.architecture in LAYERNORM_ARCHS or cfg.model_type in ("starcoder2", "gpt_neox"):
+    if cfg.architecture in LAYERNORM_ARCHS or cfg.model_type in ("starcoder2", "gpt_neox", "phi"):
         from ome_amd.models.layernorm_lm import LayerNormForCausalLM
 
         return LayerNormForCausalLM

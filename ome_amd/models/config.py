@@ -122,7 +122,7 @@ class ModelConfig:
             partial_rotary_factor=float(prf),
             max_position_embeddings=text.get("max_position_embeddings", 4096),
             tie_word_embeddings=bool(cfg.get("tie_word_embeddings", text.get("tie_word_embeddings", False))),
-            attention_bias=bool(text.get("attention_bias", text.get("use_bias", mt in ("qwen2", "qwen2_moe", "qwen2_vl", "qwen2_vl_text")))),
+            attention_bias=bool(text.get("attention_bias", text.get("use_bias", mt in ("qwen2", "qwen2_moe", "qwen2_vl", "qwen2_vl_text", "phi")))),
             qk_norm=mt in ("qwen3", "qwen3_moe", "gemma3", "gemma3_text"),
             hidden_act=text.get("hidden_act", text.get("hidden_activation", "silu")),
             sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt in ("mistral", "starcoder2")) else None,
@@ -241,6 +241,14 @@ PRESETS: dict[str, dict] = {
                       num_hidden_layers=2, num_attention_heads=4, intermediate_size=1024, vocab_size=1024,
                       layer_norm_eps=1e-5, rotary_pct=0.25, rotary_emb_base=10000, use_parallel_residual=True,
                       hidden_act="gelu", max_position_embeddings=2048, attention_bias=True),
+    "phi-2": dict(architectures=["PhiForCausalLM"], model_type="phi", hidden_size=2560, num_hidden_layers=32,
+                  num_attention_heads=32, num_key_value_heads=32, intermediate_size=10240, vocab_size=51200,
+                  layer_norm_eps=1e-5, partial_rotary_factor=0.4, rope_theta=10000.0, hidden_act="gelu_new",
+                  max_position_embeddings=2048, qk_layernorm=False, tie_word_embeddings=False),
+    "tiny-phi": dict(architectures=["PhiForCausalLM"], model_type="phi", hidden_size=256, num_hidden_layers=2,
+                     num_attention_heads=4, num_key_value_heads=4, intermediate_size=1024, vocab_size=1024,
+                     layer_norm_eps=1e-5, partial_rotary_factor=0.5, rope_theta=10000.0, hidden_act="gelu_new",
+                     max_position_embeddings=2048, qk_layernorm=False, tie_word_embeddings=False),
     "llama-4-scout-17b-16e": dict(architectures=["Llama4ForConditionalGeneration"], model_type="llama4",
                                   text_config=dict(model_type="llama4_text", hidden_size=5120, num_hidden_layers=48,
                                                    num_attention_heads=40, num_key_value_heads=8, head_dim=128,

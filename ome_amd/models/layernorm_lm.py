@@ -1,5 +1,5 @@
-"""LayerNorm decoder families: Starcoder2 (``Starcoder2ForCausalLM``) and GPT-NeoX / Pythia
-(``GPTNeoXForCausalLM``) on the ome_amd kernels.
+"""LayerNorm decoder families: Starcoder2 (``Starcoder2ForCausalLM``), GPT-NeoX / Pythia
+(``GPTNeoXForCausalLM``) and Phi-1/1.5/2 (``PhiForCausalLM``) on the ome_amd kernels.
 
 Reference catalog entries: ``config/runtimes/srt/bigcode/starcoder2-*`` style runtimes and the
 generic HF-architecture runtime match (``pkg/runtimeselector`` picks a runtime by
@@ -19,6 +19,10 @@ from the Llama path (``llama.py``):
   ``h + attn(ln1(h)) + mlp(ln2(h))`` -- the two row-parallel partial sums are added before ONE
   TP all-reduce per layer (half the collectives of the sequential form);
 * Starcoder2: GQA, sliding window (``sliding_window``), tied embeddings.
+* Phi-2: parallel residual with ONE shared LayerNorm per layer (``h + attn(ln(h)) + mlp(ln(h))``:
+  the norm output feeds both branches, no second norm launch), partial rotary
+  (``partial_rotary_factor`` 0.4), GELU-tanh MLP ``fc1``/``fc2`` and a biased ``lm_head`` (the bias is
+  vocab-sharded with the head so each TP rank adds its slice before the all-gather).
 """
 from __future__ import annotations
 
@@ -33,7 +37,7 @@ from ome_amd.models.llama import LlamaForCausalLM
 from ome_amd.models.quant import linear
 from ome_amd.parallel import state as pstate
 
-LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM"}
+LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalLM"}
 
 _ACTS = {"gelu_pytorch_tanh": 1, "gelu_new": 1, "gelu_fast": 1, "gelu": 3, "silu": 0, "swish": 0}
 
@@ -43,7 +47,10 @@ class LayerNormForCausalLM(LlamaForCausalLM):
         super().__init__(cfg, device, dtype, max_positions)
         hf = cfg.extra or {}
         self.neox = cfg.model_type == "gpt_neox" or cfg.architecture == "GPTNeoXForCausalLM"
-        self.parallel_residual = self.neox and bool(hf.get("use_parallel_residual", True))
+        self.phi = cfg.model_type == "phi" or cfg.architecture == "PhiForCausalLM"
+        if self.phi and hf.get("qk_layernorm"):
+            raise NotImplementedError("Phi qk_layernorm")
+        self.parallel_residual = self.phi or (self.neox and bool(hf.get("use_parallel_residual", True)))
         act = cfg.hidden_act
         if act not in _ACTS:
             raise NotImplementedError(f"hidden_act {act!r}")
@@ -55,6 +62,7 @@ class LayerNormForCausalLM(LlamaForCausalLM):
         self.b_fc: list[torch.Tensor | None] = [None] * L
         self.b_d: list[torch.Tensor | None] = [None] * L
         self.norm_b: torch.Tensor | None = None
+        self.lm_head_b: torch.Tensor | None = None
 
     # ------------------------------------------------------------------ weights
     def init_random(self, seed: int = 0, std: float = 0.02) -> "LayerNormForCausalLM":
@@ -78,6 +86,8 @@ class LayerNormForCausalLM(LlamaForCausalLM):
         self.embed = self._alloc(tp.vocab, H, std=1.0, gen=gen)
         self.norm, self.norm_b = self._alloc(H, std=None, gen=gen), zeros(H)
         self.lm_head = self.embed if cfg.tie_word_embeddings else self._alloc(tp.vocab, H, std=std, gen=gen)
+        if self.phi:
+            self.lm_head_b = self._alloc(tp.vocab, std=std, gen=gen)
         self._post_load()
         return self
 
@@ -108,10 +118,13 @@ class LayerNormForCausalLM(LlamaForCausalLM):
             if name in ("embed_out.weight", "lm_head.weight"):
                 self.lm_head = put(self._vocab_shard(w))
                 continue
-            if name in ("final_layer_norm.weight", "norm.weight"):
+            if name == "lm_head.bias":
+                self.lm_head_b = put(self._vocab_shard(w[:, None])[:, 0])
+                continue
+            if name in ("final_layer_norm.weight", "norm.weight", "final_layernorm.weight"):
                 self.norm = put(w)
                 continue
-            if name in ("final_layer_norm.bias", "norm.bias"):
+            if name in ("final_layer_norm.bias", "norm.bias", "final_layernorm.bias"):
                 self.norm_b = put(w)
                 continue
             parts = name.split(".")
@@ -131,17 +144,17 @@ class LayerNormForCausalLM(LlamaForCausalLM):
                 qkv.setdefault(i, {})["q" + kind] = w.narrow(0, tp.rank * tp.hq * D, tp.hq * D)
             elif rest.startswith(("self_attn.k_proj.", "self_attn.v_proj.")):
                 qkv.setdefault(i, {})[rest[10] + kind] = w.narrow(0, tp.kv_start * D, tp.hkv * D)
-            elif rest in ("attention.dense.weight", "self_attn.o_proj.weight"):
+            elif rest in ("attention.dense.weight", "self_attn.o_proj.weight", "self_attn.dense.weight"):
                 self.w_o[i] = put(w.narrow(1, tp.rank * tp.hq * D, tp.hq * D))
-            elif rest in ("attention.dense.bias", "self_attn.o_proj.bias"):
+            elif rest in ("attention.dense.bias", "self_attn.o_proj.bias", "self_attn.dense.bias"):
                 self.b_o[i] = row_bias(w)
-            elif rest in ("mlp.dense_h_to_4h.weight", "mlp.c_fc.weight"):
+            elif rest in ("mlp.dense_h_to_4h.weight", "mlp.c_fc.weight", "mlp.fc1.weight"):
                 self.w_gu[i] = put(inter_rows(w))
-            elif rest in ("mlp.dense_h_to_4h.bias", "mlp.c_fc.bias"):
+            elif rest in ("mlp.dense_h_to_4h.bias", "mlp.c_fc.bias", "mlp.fc1.bias"):
                 self.b_fc[i] = put(inter_rows(w))
-            elif rest in ("mlp.dense_4h_to_h.weight", "mlp.c_proj.weight"):
+            elif rest in ("mlp.dense_4h_to_h.weight", "mlp.c_proj.weight", "mlp.fc2.weight"):
                 self.w_d[i] = put(w.narrow(1, tp.rank * tp.inter, min(tp.inter, w.shape[1] - tp.rank * tp.inter)))
-            elif rest in ("mlp.dense_4h_to_h.bias", "mlp.c_proj.bias"):
+            elif rest in ("mlp.dense_4h_to_h.bias", "mlp.c_proj.bias", "mlp.fc2.bias"):
                 self.b_d[i] = row_bias(w)
             elif rest.startswith("input_layernorm."):
                 (self.ln1 if kind == "weight" else self.ln1b)[i] = put(w)
@@ -161,7 +174,7 @@ class LayerNormForCausalLM(LlamaForCausalLM):
 
     def weight_bytes(self) -> int:
         n = super().weight_bytes()
-        for lst in (self.ln1b, self.ln2b, self.b_o, self.b_fc, self.b_d, [self.norm_b]):
+        for lst in (self.ln1b, self.ln2b, self.b_o, self.b_fc, self.b_d, [self.norm_b, self.lm_head_b]):
             n += sum(t.numel() * t.element_size() for t in lst if t is not None)
         return n
 
@@ -203,7 +216,7 @@ class LayerNormForCausalLM(LlamaForCausalLM):
             if i > 0:  # x holds the previous layer's block output: add it, normalise for this layer
                 ops.fused_add_layernorm(x, residual, self.ln1[i], self.ln1b[i], self.eps)
             if self.parallel_residual:
-                x2 = ops.layernorm(residual, self.ln2[i], self.ln2b[i], self.eps)
+                x2 = x if self.phi else ops.layernorm(residual, self.ln2[i], self.ln2b[i], self.eps)
                 o = self._attn_block(i, x, meta, kv)
                 x = pstate.tp_all_reduce(o + self.mlp(i, x2, reduce=False))
             else:
@@ -219,3 +232,11 @@ class LayerNormForCausalLM(LlamaForCausalLM):
             return None
         ops.fused_add_layernorm(x, residual, self.norm, self.norm_b, self.eps)
         return x
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        if self.lm_head_b is None:
+            return super().compute_logits(hidden)
+        logits = linear(hidden, self.lm_head, self.lm_head_b)
+        if self.tp.tp > 1:
+            logits = pstate.tp_all_gather(logits, dim=-1)
+        return logits[:, : self.cfg.vocab_size]

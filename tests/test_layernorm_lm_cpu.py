@@ -3,7 +3,7 @@ HF model is saved as safetensors, loaded by ome_amd and run on the CPU reference
 logits of every position must match HF's eager forward and greedy decoding must agree with
 ``generate`` -- covering LayerNorm+bias, projection biases, GELU-tanh / exact-GELU MLPs, GQA +
 sliding window (Starcoder2), fused per-head QKV, partial rotary and the parallel residual
-(GPT-NeoX, both residual forms)."""
+(GPT-NeoX, both residual forms) and Phi-2 (shared-norm parallel residual, biased lm_head)."""
 import pytest
 import torch
 
@@ -26,6 +26,11 @@ def _hf_model(kind: str, tmp_path):
                                             max_position_embeddings=512, sliding_window=16, bos_token_id=1,
                                             eos_token_id=2)
         m = transformers.Starcoder2ForCausalLM(cfg)
+    elif kind == "phi":
+        cfg = transformers.PhiConfig(vocab_size=512, hidden_size=128, intermediate_size=384, num_hidden_layers=3,
+                                     num_attention_heads=4, partial_rotary_factor=0.5, hidden_act="gelu_new",
+                                     max_position_embeddings=512, bos_token_id=1, eos_token_id=2)
+        m = transformers.PhiForCausalLM(cfg)
     else:
         cfg = transformers.GPTNeoXConfig(vocab_size=512, hidden_size=128, intermediate_size=512,
                                          num_hidden_layers=3, num_attention_heads=2, rotary_pct=0.25,
@@ -46,7 +51,7 @@ def _hf_model(kind: str, tmp_path):
     return m
 
 
-@pytest.mark.parametrize("kind", ["starcoder2", "neox", "neox_sequential"])
+@pytest.mark.parametrize("kind", ["starcoder2", "neox", "neox_sequential", "phi"])
 def test_layernorm_family_matches_hf(tmp_path, kind):
     hf = _hf_model(kind, tmp_path)
     ids = [(7 * i + 3) % 500 + 3 for i in range(40)]
@@ -58,6 +63,8 @@ def test_layernorm_family_matches_hf(tmp_path, kind):
     assert type(m).__name__ == "LayerNormForCausalLM"
     if kind == "starcoder2":
         assert m.window == 16 and m.tp.hkv == 2
+    elif kind == "phi":
+        assert m.phi and m.parallel_residual and m.cfg.rot_dim == 16 and m.lm_head_b is not None
     else:
         assert m.cfg.rot_dim == 16 and m.parallel_residual == (kind == "neox")
     got = _our_logits(eng, ids)
@@ -70,12 +77,14 @@ def test_layernorm_family_matches_hf(tmp_path, kind):
 
 
 def test_presets_and_config_parsing():
-    for name in ("starcoder2-7b", "pythia-1.4b", "tiny-starcoder2", "tiny-neox"):
+    for name in ("starcoder2-7b", "pythia-1.4b", "tiny-starcoder2", "tiny-neox", "phi-2", "tiny-phi"):
         assert preset(name).rms_norm_eps == 1e-5
     c = preset("pythia-1.4b")
     assert c.rot_dim == 32 and c.head_dim == 128
     c = preset("starcoder2-7b")
     assert c.sliding_window == 4096 and c.attention_bias and c.rope_theta == 1e6
+    c = preset("phi-2")
+    assert c.rot_dim == 32 and c.head_dim == 80 and c.attention_bias and c.hidden_act == "gelu_new"
 
 
 def test_layernorm_and_act_reference_ops():

@@ -44,7 +44,7 @@ def test_act_kernel(kind):
     assert torch.allclose(got.float(), want, atol=2e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("model", ["tiny-starcoder2", "tiny-neox"])
+@pytest.mark.parametrize("model", ["tiny-starcoder2", "tiny-neox", "tiny-phi"])
 def test_layernorm_family_engine_graph_decode(model):
     eng = Engine(EngineArgs(model=model, device="cuda", max_running_requests=8, context_length=512))
     m = eng.runner.model
