@@ -25,6 +25,7 @@ class ModelConfig:
     num_heads: int = 32
     num_kv_heads: int = 8
     head_dim: int = 128
+    attn_head_dim: int = 0  # true head dim when ``head_dim`` was padded to a kernel tile (Phi-2: 80 -> 128)
     intermediate_size: int = 14336
     vocab_size: int = 128256
     rms_norm_eps: float = 1e-5
@@ -103,6 +104,12 @@ class ModelConfig:
             prf = glob.get("partial_rotary_factor") or prf
             if glob.get("rope_type", "default") != "default":
                 rope_scaling = dict(glob)
+        attn_hd = 0
+        if mt == "phi" and hd not in (64, 128, 256):
+            # the attention / RoPE-KV kernels tile head_dim in {64, 128, 256}: zero-pad each head
+            # (q/k pad dims add 0 to every score, v pad dims feed zero columns of the padded o_proj)
+            pad = next(d for d in (64, 128, 256) if d >= hd)
+            attn_hd, prf, hd = hd, int(hd * float(prf)) / pad, pad
         c = cls(
             architecture=arch,
             model_type=mt,
@@ -113,6 +120,7 @@ class ModelConfig:
             num_heads=nh,
             num_kv_heads=text.get("num_key_value_heads") or nh,
             head_dim=hd,
+            attn_head_dim=attn_hd,
             intermediate_size=text.get("intermediate_size", 4 * H),
             vocab_size=text.get("vocab_size", 32000),
             rms_norm_eps=text.get("rms_norm_eps") or text.get("layer_norm_eps") or text.get("norm_epsilon") or

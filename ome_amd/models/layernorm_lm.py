@@ -22,7 +22,9 @@ from the Llama path (``llama.py``):
 * Phi-2: parallel residual with ONE shared LayerNorm per layer (``h + attn(ln(h)) + mlp(ln(h))``:
   the norm output feeds both branches, no second norm launch), partial rotary
   (``partial_rotary_factor`` 0.4), GELU-tanh MLP ``fc1``/``fc2`` and a biased ``lm_head`` (the bias is
-  vocab-sharded with the head so each TP rank adds its slice before the all-gather).
+  vocab-sharded with the head so each TP rank adds its slice before the all-gather).  Phi-2's
+  head_dim 80 is zero-padded per head to the 128 kernel tile at load time (``cfg.attn_head_dim``
+  keeps 80 for the softmax scale); the pad costs 1.6x KV bytes but keeps the MFMA tiles.
 """
 from __future__ import annotations
 
@@ -50,6 +52,9 @@ class LayerNormForCausalLM(LlamaForCausalLM):
         self.phi = cfg.model_type == "phi" or cfg.architecture == "PhiForCausalLM"
         if self.phi and hf.get("qk_layernorm"):
             raise NotImplementedError("Phi qk_layernorm")
+        self.Dt = cfg.attn_head_dim or self.D  # checkpoint head dim (< D when zero-padded, Phi-2)
+        if self.Dt != self.D:
+            self.scale = 1.0 / math.sqrt(self.Dt)
         self.parallel_residual = self.phi or (self.neox and bool(hf.get("use_parallel_residual", True)))
         act = cfg.hidden_act
         if act not in _ACTS:
@@ -104,6 +109,15 @@ class LayerNormForCausalLM(LlamaForCausalLM):
             n = min(tp.inter, t.shape[0] - tp.rank * tp.inter)
             return t.narrow(0, tp.rank * tp.inter, n)
 
+        Dt = self.Dt
+
+        def pad_rows(t):  # [heads * Dt, ...] -> [heads * D, ...], zero-padding every head
+            if Dt == D:
+                return t
+            t = t.reshape(-1, Dt, *t.shape[1:])
+            z = t.new_zeros(t.shape[0], D - Dt, *t.shape[2:])
+            return torch.cat([t, z], 1).reshape(-1, *t.shape[2:])
+
         def row_bias(t):  # row-parallel bias: rank 0 only
             return put(t) if r0 else torch.zeros(t.shape, dtype=self.dtype, device=self.device)
 
@@ -141,11 +155,11 @@ class LayerNormForCausalLM(LlamaForCausalLM):
                 for j, c in enumerate("qkv"):
                     d[c + kind] = t[:, j].reshape(tp.hq * D, *w.shape[1:])
             elif rest.startswith("self_attn.q_proj."):
-                qkv.setdefault(i, {})["q" + kind] = w.narrow(0, tp.rank * tp.hq * D, tp.hq * D)
+                qkv.setdefault(i, {})["q" + kind] = pad_rows(w.narrow(0, tp.rank * tp.hq * Dt, tp.hq * Dt))
             elif rest.startswith(("self_attn.k_proj.", "self_attn.v_proj.")):
-                qkv.setdefault(i, {})[rest[10] + kind] = w.narrow(0, tp.kv_start * D, tp.hkv * D)
+                qkv.setdefault(i, {})[rest[10] + kind] = pad_rows(w.narrow(0, tp.kv_start * Dt, tp.hkv * Dt))
             elif rest in ("attention.dense.weight", "self_attn.o_proj.weight", "self_attn.dense.weight"):
-                self.w_o[i] = put(w.narrow(1, tp.rank * tp.hq * D, tp.hq * D))
+                self.w_o[i] = put(pad_rows(w.narrow(1, tp.rank * tp.hq * Dt, tp.hq * Dt).t()).t())
             elif rest in ("attention.dense.bias", "self_attn.o_proj.bias", "self_attn.dense.bias"):
                 self.b_o[i] = row_bias(w)
             elif rest in ("mlp.dense_h_to_4h.weight", "mlp.c_fc.weight", "mlp.fc1.weight"):

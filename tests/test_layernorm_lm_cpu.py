@@ -27,8 +27,9 @@ def _hf_model(kind: str, tmp_path):
                                             eos_token_id=2)
         m = transformers.Starcoder2ForCausalLM(cfg)
     elif kind == "phi":
-        cfg = transformers.PhiConfig(vocab_size=512, hidden_size=128, intermediate_size=384, num_hidden_layers=3,
-                                     num_attention_heads=4, partial_rotary_factor=0.5, hidden_act="gelu_new",
+        # head_dim 80 (as Phi-2): exercises the zero-padding to the 128 kernel tile
+        cfg = transformers.PhiConfig(vocab_size=512, hidden_size=160, intermediate_size=384, num_hidden_layers=3,
+                                     num_attention_heads=2, partial_rotary_factor=0.4, hidden_act="gelu_new",
                                      max_position_embeddings=512, bos_token_id=1, eos_token_id=2)
         m = transformers.PhiForCausalLM(cfg)
     else:
@@ -64,7 +65,8 @@ def test_layernorm_family_matches_hf(tmp_path, kind):
     if kind == "starcoder2":
         assert m.window == 16 and m.tp.hkv == 2
     elif kind == "phi":
-        assert m.phi and m.parallel_residual and m.cfg.rot_dim == 16 and m.lm_head_b is not None
+        assert m.phi and m.parallel_residual and m.lm_head_b is not None
+        assert m.cfg.rot_dim == 32 and m.D == 128 and m.Dt == 80
     else:
         assert m.cfg.rot_dim == 16 and m.parallel_residual == (kind == "neox")
     got = _our_logits(eng, ids)
@@ -84,7 +86,7 @@ def test_presets_and_config_parsing():
     c = preset("starcoder2-7b")
     assert c.sliding_window == 4096 and c.attention_bias and c.rope_theta == 1e6
     c = preset("phi-2")
-    assert c.rot_dim == 32 and c.head_dim == 80 and c.attention_bias and c.hidden_act == "gelu_new"
+    assert c.rot_dim == 32 and c.head_dim == 128 and c.attn_head_dim == 80 and c.attention_bias and c.hidden_act == "gelu_new"
 
 
 def test_layernorm_and_act_reference_ops():
