@@ -113,8 +113,13 @@ __global__ __launch_bounds__(kThreads) void ar_one_shot(Peers P, int rank, int64
 }
 
 // reduce-scatter into the own buffer's chunk, then all-gather the peers' reduced chunks
+// `red_vec` = offset (in 16-B vectors) of the reduced-chunk half of every rank's buffer.  It is
+// the registered capacity, NOT the message size: a next call of a different size restages its
+// input into [0, n') only, which can never overlap the reduced chunk a slower peer is still
+// gathering from this call.
 template <int W>
-__global__ __launch_bounds__(kThreads) void ar_two_shot(Peers P, int rank, int64_t n_vec, u32x4* __restrict__ out) {
+__global__ __launch_bounds__(kThreads) void ar_two_shot(Peers P, int rank, int64_t n_vec, int64_t red_vec,
+                                                        u32x4* __restrict__ out) {
   __shared__ uint32_t s_epoch;
   Signal* self = P.sig[rank];
   if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
@@ -133,20 +138,22 @@ __global__ __launch_bounds__(kThreads) void ar_two_shot(Peers P, int rank, int64
     for (int r = 0; r < W; ++r) add8(acc, v[r]);
     const u32x4 s = pack8(acc);
     out[i] = s;
-    mine[n_vec + i] = s;  // peers gather it from the second half of our buffer
+    mine[red_vec + i] = s;  // peers gather it from the reduced half of our buffer
   }
   block_barrier(P, rank, W, epoch, 1);
   for (int r = 1; r < W; ++r) {
     const int src = (rank + r) % W;
     const int64_t s0 = src * chunk, s1 = s0 + chunk < n_vec ? s0 + chunk : n_vec;
-    const u32x4* theirs = reinterpret_cast<const u32x4*>(P.data[src]) + n_vec;
+    const u32x4* theirs = reinterpret_cast<const u32x4*>(P.data[src]) + red_vec;
     for (int64_t i = s0 + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < s1; i += (int64_t)gridDim.x * kThreads)
       out[i] = theirs[i];
   }
-  // no closing meeting is needed: a peer can only restage (first half) after its own kernel
-  // ended, i.e. after the barrier above that every reader of its input passed, and it writes its
-  // next reduced chunk (second half) only after the next call's start barrier, which this
-  // block reaches after it finished gathering.
+  // No closing meeting is needed.  (1) A peer restages its input half only after its own kernel
+  // ended, i.e. after every one of its blocks passed the barrier above, which every reader of its
+  // input passed too; the restage covers [0, n') of the input half and never the reduced half.
+  // (2) A peer's block b' writes its next reduced chunk only after the next call's start barrier
+  // for b', which needs this rank's next kernel to be running, i.e. this kernel (all of its
+  // gathering) to have ended: launches on one stream do not overlap.
   if (threadIdx.x == 0) self->epoch[blockIdx.x] = epoch;
 }
 
@@ -174,7 +181,9 @@ OME_API int ome_comm_create(int rank, int world, size_t data_bytes, void** ctx_o
   if (e != hipSuccess) return (int)e;
   e = hipMemset(c->sig, 0, sizeof(Signal));
   if (e != hipSuccess) return (int)e;
-  e = hipMalloc((void**)&c->data, 2 * data_bytes);  // input half + reduced-chunk half (two-shot)
+  data_bytes = (data_bytes + 15) & ~(size_t)15;
+  c->data_bytes = data_bytes;
+  e = hipMalloc((void**)&c->data, 2 * data_bytes);  // input half + reduced-chunk half at +data_bytes
   if (e != hipSuccess) return (int)e;
   e = hipIpcGetMemHandle((hipIpcMemHandle_t*)sig_handle, c->sig);
   if (e != hipSuccess) return (int)e;
@@ -220,11 +229,12 @@ OME_API int ome_comm_all_reduce(void* ctx, const void* in, void* out, int64_t n,
   hipError_t e = hipMemcpyAsync(c->data, in, bytes, hipMemcpyDeviceToDevice, stream);
   if (e != hipSuccess) return (int)e;
   const int64_t n_vec = n / 8;
+  const int64_t red_vec = (int64_t)(c->data_bytes / 16);
   dim3 grid(blocks), block(kThreads);
 #define OME_AR_CASE(W)                                                                               \
   case W:                                                                                            \
     if (two_shot)                                                                                    \
-      ar_two_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, (u32x4*)out);             \
+      ar_two_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, red_vec, (u32x4*)out);    \
     else                                                                                             \
       ar_one_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, (u32x4*)out);             \
     break;

@@ -76,13 +76,14 @@ class ModelConfig:
 
     def num_params(self) -> int:
         H, L, V = self.hidden_size, self.num_layers, self.vocab_size
-        D = self.head_dim
+        D = self.attn_head_dim or self.head_dim  # checkpoint head dim, not the kernel-tile padding
         attn = H * (self.num_heads * D) * 2 + H * (self.num_kv_heads * D) * 2
         if self.is_moe:
             mlp = self.num_experts * 3 * H * self.moe_intermediate_size + H * self.num_experts
             mlp += self.num_shared_experts * 3 * H * (self.shared_expert_intermediate_size or self.moe_intermediate_size)
-        else:
-            mlp = 3 * H * self.intermediate_size
+        else:  # gated (SwiGLU / GeGLU) MLPs have 3 matrices; the LayerNorm families' fc1/fc2 have 2
+            gated = self.architecture not in ("Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalLM")
+            mlp = (3 if gated else 2) * H * self.intermediate_size
         emb = V * H * (1 if self.tie_word_embeddings else 2)
         return L * (attn + mlp + 2 * H) + emb + H
 

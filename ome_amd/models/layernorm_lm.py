@@ -88,6 +88,10 @@ class LayerNormForCausalLM(LlamaForCausalLM):
             self.b_fc[i] = self._alloc(tp.inter, std=std, gen=gen)
             self.w_d[i] = self._alloc(H, tp.inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
             self.b_d[i] = self._alloc(H, std=std, gen=gen) if r0 else zeros(H)
+            if self.Dt != D:  # zero the per-head pad dims, as a padded checkpoint has them
+                self.w_qkv[i].view(-1, D, H)[:, self.Dt:].zero_()
+                self.b_qkv[i].view(-1, D)[:, self.Dt:].zero_()
+                self.w_o[i].view(H, -1, D)[:, :, self.Dt:].zero_()
         self.embed = self._alloc(tp.vocab, H, std=1.0, gen=gen)
         self.norm, self.norm_b = self._alloc(H, std=None, gen=gen), zeros(H)
         self.lm_head = self.embed if cfg.tie_word_embeddings else self._alloc(tp.vocab, H, std=std, gen=gen)

@@ -47,9 +47,21 @@ def _send_msg(sock: socket.socket, obj: dict) -> None:
     sock.sendall(struct.pack("<I", len(b)) + b)
 
 
+MAX_HEADER_BYTES = 1 << 20   # a JSON header / handshake record is a few hundred bytes
+
+
 def _recv_msg(sock: socket.socket) -> dict:
     (n,) = struct.unpack("<I", _recv_exact(sock, 4))
+    if n > MAX_HEADER_BYTES:
+        raise ConnectionError(f"KV transfer record of {n} bytes exceeds {MAX_HEADER_BYTES}")
     return json.loads(_recv_exact(sock, n))
+
+
+def default_bind_host() -> str:
+    """Address the decode-side receiver listens on: ``OME_PD_BIND_HOST``, else the pod address
+    the executor / kubelet exports (``POD_IP``), else loopback -- never every interface by
+    default, since the receiver takes page images from whoever connects."""
+    return os.environ.get("OME_PD_BIND_HOST") or os.environ.get("POD_IP") or "127.0.0.1"
 
 
 def _recv_exact(sock: socket.socket, n: int) -> bytes:
@@ -65,7 +77,7 @@ def _recv_exact(sock: socket.socket, n: int) -> bytes:
 
 
 class KVTransfer:
-    def __init__(self, engine, mode: str, port: int, host: str = "0.0.0.0"):
+    def __init__(self, engine, mode: str, port: int, host: str | None = None):
         assert mode in ("prefill", "decode")
         self.engine, self.mode = engine, mode
         self.rank = engine.pstate.rank if engine.pstate.tp_size > 1 else 0
@@ -95,7 +107,7 @@ class KVTransfer:
         if mode == "decode":
             self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
             self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-            self._sock.bind((host, port + self.rank))
+            self._sock.bind((host or default_bind_host(), port + self.rank))
             self._sock.listen(64)
             self.port = self._sock.getsockname()[1] - self.rank
             threading.Thread(target=self._accept_loop, name="kv-recv", daemon=True).start()
@@ -120,8 +132,13 @@ class KVTransfer:
                 if magic != MAGIC:
                     raise ConnectionError("bad KV transfer magic")
                 (hl,) = struct.unpack("<I", _recv_exact(conn, 4))
+                if hl > MAX_HEADER_BYTES:
+                    raise ConnectionError(f"KV header of {hl} bytes")
                 header = json.loads(_recv_exact(conn, hl))
-                payload = _recv_exact(conn, int(header["nbytes"]))
+                nbytes, cap = int(header["nbytes"]), self.max_payload_bytes()
+                if not 0 <= nbytes <= cap:
+                    raise ConnectionError(f"KV payload of {nbytes} bytes exceeds the {cap}-byte bound")
+                payload = _recv_exact(conn, nbytes)
                 conn.sendall(b"OK")
             with self.lock:
                 self.inbox[int(header["room"])] = (header, payload)
@@ -129,6 +146,14 @@ class KVTransfer:
             self.engine._wake.set()
         except Exception as e:  # noqa: BLE001
             log.warning("KV receive failed: %s", e)
+
+    def max_payload_bytes(self) -> int:
+        """Largest legal page image: every local layer's K and V pages of one full context."""
+        kv, P = self.engine.runner.kv, self.engine.runner.P
+        k0, v0 = kv.k[kv.local_layers[0]], kv.v[kv.local_layers[0]]
+        page_bytes = (k0[0].numel() + v0[0].numel()) * k0.element_size()
+        pages = -(-self.engine.max_context // P)
+        return len(kv.local_layers) * pages * page_bytes
 
     def _recv_ipc(self, conn: socket.socket) -> None:
         """Same-node handshake: RESERVE {room, n_pages, host, dtype} -> {ok, slots, pool} ->
@@ -189,9 +214,16 @@ class KVTransfer:
         sch, runner = eng.scheduler, eng.runner
         kv, P = runner.kv, runner.P
         L = int(header["n_tokens"])
-        k0 = kv.k[kv.local_layers[0]]
-        if list(header["shape_k"][1:]) != list(k0.shape[1:]) or int(header["layers"]) != len(kv.local_layers) \
-                or header.get("dtype", str(kv.dtype)) != str(kv.dtype):
+        k0, v0 = kv.k[kv.local_layers[0]], kv.v[kv.local_layers[0]]
+        n_pages = -(-L // P)
+        ok = (list(header["shape_k"][1:]) == list(k0.shape[1:]) and int(header["layers"]) == len(kv.local_layers)
+              and header.get("dtype", str(kv.dtype)) == str(kv.dtype) and 0 < L <= eng.max_context)
+        if ok and not (isinstance(payload, tuple) and payload[0] == "ipc"):
+            # TCP page image: exactly n_pages K and V pages per local layer, nothing else
+            sk, sv = list(header["shape_k"]), list(header.get("shape_v", []))
+            want = len(kv.local_layers) * n_pages * (k0[0].numel() + v0[0].numel()) * k0.element_size()
+            ok = (sk[0] == n_pages and sv == [n_pages, *v0.shape[1:]] and len(payload) == want)
+        if not ok:
             req.state, req.finish_reason = ReqState.FINISHED, "abort:kv_layout_mismatch"
             if req.on_token:
                 req.on_token(req, [], True)
@@ -201,7 +233,6 @@ class KVTransfer:
             if slot is None:
                 return False
             req.req_slot = slot
-        n_pages = -(-L // P)
         pages = sch.pages.alloc(n_pages)
         if pages is None:
             return False

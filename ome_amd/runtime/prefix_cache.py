@@ -1,7 +1,8 @@
 """Page-granular prefix (radix) cache for the paged KV pool.
 
 Full pages of finished requests stay resident, keyed by a hash chain over their token
-content (h_i = H(h_{i-1}, tokens of page i)), so a new request whose prompt shares a prefix
+content (h_i = BLAKE2b-128(h_{i-1} || tokens of page i): a collision-resistant digest, so a
+match can never hand out another prompt's KV pages), so a new request whose prompt shares a prefix
 reuses those pages instead of recomputing them (SGLang radix cache, which the reference's
 runtimes keep enabled unless ``--disable-radix-cache``).  Pages matched by running requests
 are pinned (refcount); unpinned pages are evicted LRU-deepest-first when the allocator runs
@@ -9,22 +10,29 @@ dry, and eviction of a page leaves its descendants unreachable so they are evict
 """
 from __future__ import annotations
 
+import hashlib
 import itertools
+from array import array
 
 
 class PrefixCache:
     def __init__(self, pool, page_size: int):
         self.pool, self.P = pool, page_size
-        self.by_hash: dict[int, int] = {}          # chain hash -> page
+        self.by_hash: dict[bytes, int] = {}        # chain digest -> page
         self.meta: dict[int, list] = {}            # page -> [hash, refcount, last_use, depth]
         self._clock = itertools.count()
         self.hits = 0
         self.queries = 0
 
     def _chain(self, tokens: list[int]):
-        h = 0
-        for i in range(len(tokens) // self.P):
-            h = hash((h, tuple(tokens[i * self.P:(i + 1) * self.P])))
+        n, P = len(tokens) // self.P, self.P
+        if n == 0:
+            return
+        raw = array("q", tokens[:n * P]).tobytes()
+        step = 8 * P
+        h = b""
+        for i in range(n):
+            h = hashlib.blake2b(h + raw[i * step:(i + 1) * step], digest_size=16).digest()
             yield i, h
 
     def match(self, tokens: list[int]) -> list[int]:

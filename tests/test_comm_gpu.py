@@ -35,6 +35,17 @@ def _worker(rank, world, port, q):
                 want = sum(_inputs(r, n, it).float() for r in range(world))
                 err = ((y.float().cpu() - want).abs() / (want.abs() + 1)).max().item()
                 worst = max(worst, err)
+        # back-to-back calls of growing / shrinking size with no host sync in between: a fast rank
+        # restages its next (larger) input while a slower peer may still gather this call's
+        # reduced chunk, which must live at a size-independent offset
+        sizes = [300_000, 600_000, 1 << 20, 8, 3 * (1 << 19) + 8, 200_000, 1 << 20]
+        xs = [_inputs(rank, n, 50 + k).cuda() for k, n in enumerate(sizes)]
+        torch.cuda.synchronize()
+        ys = [ar.all_reduce(x) for x in xs]
+        torch.cuda.synchronize()
+        for k, (n, y) in enumerate(zip(sizes, ys)):
+            want = sum(_inputs(r, n, 50 + k).float() for r in range(world))
+            worst = max(worst, ((y.float().cpu() - want).abs() / (want.abs() + 1)).max().item())
         # graph-captured replays keep their epochs in device memory
         x = _inputs(rank, 65536, 99).cuda()
         buf = x.clone()

@@ -101,3 +101,29 @@ def test_layernorm_and_act_reference_ops():
     assert torch.allclose(rr, x + r) and torch.allclose(xx, ref.layernorm(x + r, w, b, 1e-5), atol=1e-5)
     y = ops.act(x.clone(), 3)
     assert torch.allclose(y, torch.nn.functional.gelu(x), atol=1e-6)
+
+
+def test_phi2_param_count_uses_checkpoint_head_dim():
+    """Phi-2's heads are zero-padded 80 -> 128 for the kernels; the parameter count (memory and
+    weight estimates) must still be the checkpoint's 2.78 B."""
+    from ome_amd.models.config import preset
+
+    cfg = preset("phi-2")
+    assert cfg.head_dim == 128 and cfg.attn_head_dim == 80
+    assert abs(cfg.num_params() / 1e9 - 2.78) < 0.02
+
+
+def test_random_init_zeroes_padded_head_dims():
+    """Random-init weights of a padded-head model behave like a padded checkpoint: the pad rows of
+    q/k/v (weights and biases) and the pad columns of o_proj are zero."""
+    from ome_amd.models.layernorm_lm import LayerNormForCausalLM
+
+    cfg = preset("tiny-phi")
+    cfg.head_dim, cfg.attn_head_dim = 128, cfg.head_dim  # pad 64 -> 128 as Phi-2 pads 80 -> 128
+    m = LayerNormForCausalLM(cfg, device="cpu", dtype=torch.float32).init_random(seed=1)
+    Dt, D, H = 64, 128, cfg.hidden_size
+    for i in m.layers:
+        assert m.w_qkv[i].view(-1, D, H)[:, Dt:].abs().sum() == 0
+        assert m.b_qkv[i].view(-1, D)[:, Dt:].abs().sum() == 0
+        assert m.w_o[i].view(H, -1, D)[:, :, Dt:].abs().sum() == 0
+        assert m.w_qkv[i].view(-1, D, H)[:, :Dt].abs().sum() > 0

@@ -137,3 +137,16 @@ def test_reference_attention_consistency():
     a = ref.paged_decode(q, kc, vc, bt, sl, 0.1)
     b = ref.paged_prefill(q, kc, vc, bt, torch.tensor([0, 1, 2]), sl, 0.1)
     assert torch.allclose(a.float(), b.float(), atol=1e-2)
+
+
+def test_prefix_cache_keys_are_content_digests():
+    """Chain keys are 128-bit BLAKE2b digests of the page contents: prompts that differ in any
+    token of a page never share that page or anything after it."""
+    pc = PrefixCache(PagePool(32), 4)
+    a = list(range(100, 112))
+    pages = pc.pool.alloc(3)
+    pc.insert(a, pages)
+    assert all(isinstance(h, bytes) and len(h) == 16 for h in pc.by_hash)
+    b = a[:5] + [a[5] + 1] + a[6:]
+    assert pc.match(b) == pages[:1]
+    assert pc.match(a) == pages
