@@ -44,6 +44,11 @@ struct Scaler {
   float mul;      // scale * log2(e) (cap_inv == 0)
   float cap_inv;  // scale / cap, 0 = no soft-capping
   float cap_l2;   // cap * log2(e)
+  const float* alibi;  // ALiBi slopes per query head (Bloom / MPT / Falcon-RW), nullptr = off: the
+                       // logit gains slope * (key_pos - query_pos), i.e. alibi_l2(head) * (k - q)
+  __device__ __forceinline__ float alibi_l2(int head) const {
+    return alibi != nullptr ? alibi[head] * 1.4426950408889634f : 0.f;
+  }
   __device__ __forceinline__ float operator()(float s) const {
     if (cap_inv > 0.f) {
       const float e = fast_exp2(2.8853900817779268f * s * cap_inv);  // exp(2x)
@@ -53,9 +58,10 @@ struct Scaler {
   }
 };
 
-static inline Scaler make_scaler(float scale, float softcap) {
+static inline Scaler make_scaler(float scale, float softcap, const float* alibi = nullptr) {
   const float l2e = 1.4426950408889634f;
   Scaler r;
+  r.alibi = alibi;
   r.mul = scale * l2e;
   r.cap_inv = softcap > 0.f ? scale / softcap : 0.f;
   r.cap_l2 = softcap > 0.f ? softcap * l2e : 0.f;
@@ -304,7 +310,7 @@ __device__ __forceinline__ void kv_tile_load(KVTile<D, F>& t, const typename KVS
 template <int D, int F>
 __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf16x8 (&qf)[D / 32],
                                                 f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
-                                                int lo, Scaler scl, int g) {
+                                                int lo, Scaler scl, int g, float al, int qpos) {
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
@@ -315,8 +321,8 @@ __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf1
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k0 = kb + 4 * g + i, k1 = k0 + 16;
-    s0[i] = (k0 < p_end && k0 >= lo) ? scl(s0[i]) : OME_NEG_INF;
-    s1[i] = (k1 < p_end && k1 >= lo) ? scl(s1[i]) : OME_NEG_INF;
+    s0[i] = (k0 < p_end && k0 >= lo) ? scl(s0[i]) + al * (float)(k0 - qpos) : OME_NEG_INF;
+    s1[i] = (k1 < p_end && k1 >= lo) ? scl(s1[i]) + al * (float)(k1 - qpos) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
   mt = fmaxf(mt, __shfl_xor(mt, 16));
@@ -377,7 +383,7 @@ __device__ __forceinline__ void kv_tilep_load(KVTileP<D, F>& t, const typename K
 template <int D, int F>
 __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const bf16x8 (&qf)[D / 32],
                                                  f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
-                                                 int lo, Scaler scl, int g) {
+                                                 int lo, Scaler scl, int g, float al, int qpos) {
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
@@ -389,8 +395,8 @@ __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const b
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k0 = base + i, k1 = k0 + 4;
-    s0[i] = (k0 < p_end && k0 >= lo) ? scl(s0[i]) : OME_NEG_INF;
-    s1[i] = (k1 < p_end && k1 >= lo) ? scl(s1[i]) : OME_NEG_INF;
+    s0[i] = (k0 < p_end && k0 >= lo) ? scl(s0[i]) + al * (float)(k0 - qpos) : OME_NEG_INF;
+    s1[i] = (k1 < p_end && k1 >= lo) ? scl(s1[i]) + al * (float)(k1 - qpos) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
   mt = fmaxf(mt, __shfl_xor(mt, 16));
@@ -438,6 +444,8 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n = lane & 15, g = lane >> 4;
   const int lo = attn_lo(seq_len - 1, window);
+  const float al = n < G ? scl.alibi_l2(kvh * G + n) : 0.f;  // this lane's query head (S^T column n)
+  const int qpos = seq_len - 1;
 
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sm_m = smem;              // [4][G]
@@ -465,13 +473,13 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     for (; kb < p_end; kb += 128) {
       KVTileP<D, F> t;
       kv_tilep_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tilep_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g);
+      kv_tilep_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
     }
   } else if (MODE == 0) {
     for (; kb < p_end; kb += 128) {
       KVTile<D, F> t;
       kv_tile_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g);
+      kv_tile_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
     }
   } else if (kb < p_end) {
     KVTile<D, F> t0, t1;
@@ -480,12 +488,12 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
       const int kn = kb + 128;
       const bool more = kn < p_end;
       if (more) kv_tile_load<D, P, F>(t1, k_cache, v_cache, bt, kn, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t0, qf, o, m_i, l_i, kb, p_end, lo, scl, g);
+      kv_tile_compute<D, F>(t0, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
       if (!more) break;
       const int kn2 = kn + 128;
       const bool more2 = kn2 < p_end;
       if (more2) kv_tile_load<D, P, F>(t0, k_cache, v_cache, bt, kn2, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t1, qf, o, m_i, l_i, kn, p_end, lo, scl, g);
+      kv_tile_compute<D, F>(t1, qf, o, m_i, l_i, kn, p_end, lo, scl, g, al, qpos);
       if (!more2) break;
       kb = kn2;
     }
@@ -579,19 +587,20 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
                              const int* block_tables, int bt_stride, const int* seq_lens, void* out,
                              int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
                              int part_size, int max_parts, float scale, int window, const int* order, int kv_fmt,
-                             float k_scale, float v_scale, float softcap, const float* sinks, hipStream_t stream) {
+                             float k_scale, float v_scale, float softcap, const float* sinks, const float* alibi,
+                             hipStream_t stream) {
   if (B <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
   if (part_size % 128 != 0 || max_parts <= 0) return -4;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
-  const Scaler scl = make_scaler(scale * k_scale, softcap);
+  const Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
   dim3 grid(max_parts, Hkv, B);
   // A/B switch for benchmarking: 1 = v1, 2 = v2 (register ring), 3 = v2 without ring, 4 = v3 with
   // key-permuted tiles (16-B V loads; default: 5.38 vs 5.24 TB/s on the bench's context mix)
   const char* ve = getenv("OME_DECODE_ATTN");
   int variant = ve ? atoi(ve) : 4;
-  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks)) variant = 4;  // v1: plain bf16 D=128
+  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks || alibi)) variant = 4;  // v1: plain bf16 D=128
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
     paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(
@@ -660,6 +669,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
       for (int ks = 0; ks < KS; ++ks) qf[rb][ks] = (r < q_len) ? ld8(qr + 32 * ks + 8 * g) : bf16x8{};
     }
     float m_i[2] = {OME_NEG_INF, OME_NEG_INF}, l_i[2] = {0.f, 0.f};
+    const float al = scl.alibi_l2(head);
     f32x4 o[2][NB];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
@@ -696,8 +706,9 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float v = scl(sc[rb][X][i]);
+            const int key = kb + 16 * X + 4 * g + i;
+            if (al != 0.f) v += al * (float)(key - qpos);
             if (need_mask) {
-              const int key = kb + 16 * X + 4 * g + i;
               const bool ok = key <= qpos && key < kv_len && key >= attn_lo(qpos, window);
               v = ok ? v : OME_NEG_INF;
             }
@@ -812,6 +823,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     for (int ks = 0; ks < KS; ++ks) qf[rb][ks] = (r < q_len) ? ld8(qr + 32 * ks + 8 * g) : bf16x8{};
   }
   float m_i[2] = {OME_NEG_INF, OME_NEG_INF}, l_i[2] = {0.f, 0.f};
+  const float al = scl.alibi_l2(head);
   f32x4 o[2][NB];
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
@@ -898,8 +910,9 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float v = scl(sc[rb][X][i]);
+            const int key = kbu + 16 * X + 4 * g + i;
+            if (al != 0.f) v += al * (float)(key - qpos);
             if (need_mask) {
-              const int key = kbu + 16 * X + 4 * g + i;
               const bool ok = key <= qpos && key < kv_len && key >= attn_lo(qpos, window);
               v = ok ? v : OME_NEG_INF;
             }
@@ -997,13 +1010,13 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
                               const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
                               const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
                               int P, float scale, int window, int kv_fmt, float k_scale, float v_scale,
-                              float softcap, const float* sinks, hipStream_t stream) {
+                              float softcap, const float* sinks, const float* alibi, hipStream_t stream) {
   if (n_items <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0) return -3;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
   const int G = Hq / Hkv;
-  const Scaler scl = make_scaler(scale * k_scale, softcap);
+  const Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
   dim3 grid(n_items, Hkv);
   const char* ve = getenv("OME_PREFILL_ATTN");
   const int variant = ve ? atoi(ve) : 2;

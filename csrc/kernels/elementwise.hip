@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void act_and_mul_kernel(const bf16* __restrict
 }
 
 // Non-gated activation (Starcoder2 / GPT-NeoX MLPs), in place on a contiguous bf16 tensor:
-// ACT 1 = GELU-tanh, 3 = GELU (erf), 0 = SiLU, 4 = ReLU^2 (NemotronH)
+// ACT 1 = GELU-tanh, 3 = GELU (erf), 0 = SiLU, 4 = ReLU^2 (NemotronH, Persimmon, Arcee), 5 = ReLU (OPT)
 template <int ACT>
 __global__ __launch_bounds__(256) void act_kernel(bf16* __restrict__ x, int64_t nvec) {
   for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
@@ -48,6 +48,7 @@ __global__ __launch_bounds__(256) void act_kernel(bf16* __restrict__ x, int64_t 
       a[j] = (bf16)(ACT == 0   ? silu(f)
                      : ACT == 1 ? gelu_tanh(f)
                      : ACT == 4 ? fmaxf(f, 0.f) * fmaxf(f, 0.f)
+                     : ACT == 5 ? fmaxf(f, 0.f)
                                 : 0.5f * f * (1.f + erff(f * 0.7071067811865476f)));
     }
     st8(x + v * 8, a);
@@ -88,7 +89,9 @@ OME_API int ome_act(void* x, int64_t n, int act, hipStream_t stream) {
   if (act == 0) act_kernel<0><<<g, 256, 0, stream>>>((bf16*)x, nv);
   else if (act == 1) act_kernel<1><<<g, 256, 0, stream>>>((bf16*)x, nv);
   else if (act == 4) act_kernel<4><<<g, 256, 0, stream>>>((bf16*)x, nv);
-  else act_kernel<3><<<g, 256, 0, stream>>>((bf16*)x, nv);
+  else if (act == 5) act_kernel<5><<<g, 256, 0, stream>>>((bf16*)x, nv);
+  else if (act == 3) act_kernel<3><<<g, 256, 0, stream>>>((bf16*)x, nv);
+  else return -3;
   OME_CHECK_LAUNCH();
   return 0;
 }

@@ -86,6 +86,15 @@ FAMILIES: list[Family] = [
     Family("smollm3-3b", "huggingfacetb", "HuggingFaceTB/SmolLM3-3B", "SmolLM3ForCausalLM", 3.1),
     Family("nemotron-h-8b-base", "nvidia", "nvidia/Nemotron-H-8B-Base-8K", "NemotronHForCausalLM", 8.1,
            "nemotron-h-8b"),
+    Family("opt-125m", "facebook", "facebook/opt-125m", "OPTForCausalLM", 0.125, "opt-125m"),
+    Family("falcon-7b-instruct", "tiiuae", "tiiuae/falcon-7b-instruct", "FalconForCausalLM", 7.2, "falcon-7b"),
+    Family("gpt-j-6b", "eleutherai", "EleutherAI/gpt-j-6b", "GPTJForCausalLM", 6.1),
+    Family("stablelm-2-12b-chat", "stabilityai", "stabilityai/stablelm-2-12b-chat", "StableLmForCausalLM", 12.1),
+    Family("persimmon-8b-chat", "adept", "adept/persimmon-8b-chat", "PersimmonForCausalLM", 9.4),
+    Family("c4ai-command-r-v01", "cohereforai", "CohereForAI/c4ai-command-r-v01", "CohereForCausalLM", 35.0),
+    Family("glm-4-9b-chat", "zhipuai", "THUDM/glm-4-9b-chat-hf", "GlmForCausalLM", 9.4),
+    Family("olmo-2-1124-7b-instruct", "allenai", "allenai/OLMo-2-1124-7B-Instruct", "Olmo2ForCausalLM", 7.3),
+    Family("afm-4-5b-base", "arcee-ai", "arcee-ai/AFM-4.5B-Base", "ArceeForCausalLM", 4.6),
     Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
 ]

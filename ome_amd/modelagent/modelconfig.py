@@ -87,16 +87,17 @@ def text_params(cfg: dict) -> int:
         nkv = nh
     hd = int(_g(cfg, "head_dim", "kv_channels", default=H // nh) or H // nh)
     ffn_cfg = cfg.get("ffn_config") or {}
-    inter = int(_g(cfg, "intermediate_size", "ffn_hidden_size", "n_inner", default=0)
+    inter = int(_g(cfg, "intermediate_size", "ffn_hidden_size", "n_inner", "ffn_dim", default=0)
                 or ffn_cfg.get("ffn_hidden_size") or 4 * H)
     mt = (cfg.get("model_type") or "").lower()
     if mt == "qwen":  # Qwen v1 stores 2x the per-projection width
         inter //= 2
     gated = mt not in ("bert", "roberta", "xlm-roberta", "gpt2", "gpt_neox", "phi", "stablelm_epoch", "clip_vision_model",
-                       "starcoder2", "falcon")
+                       "starcoder2", "falcon", "opt", "gptj", "persimmon", "arcee")
     if mt in ("stablelm",):
         gated = True
     # attention
+    inter_bias = 0
     q_lora = cfg.get("q_lora_rank")
     kv_lora = cfg.get("kv_lora_rank")
     if kv_lora:  # multi-head latent attention (DeepSeek-V2/V3, Kimi-K2, MiniCPM3)
@@ -111,9 +112,12 @@ def text_params(cfg: dict) -> int:
         attn = H * nh * hd + 2 * H * nkv * hd + nh * hd * H
         if cfg.get("attention_bias") or cfg.get("qkv_bias") or mt in ("qwen2", "qwen", "bert", "chatglm"):
             attn += nh * hd + 2 * nkv * hd
+        if mt == "opt" and cfg.get("enable_bias", True):  # every projection biased (q/k/v/out, fc1/fc2)
+            attn += 3 * nh * hd + H
+            inter_bias = inter + H
     # MLP / MoE
     n_exp = int(_g(cfg, "num_local_experts", "num_experts", "n_routed_experts", default=0) or ffn_cfg.get("moe_num_experts") or 0)
-    mlp_dense = (3 if gated else 2) * H * inter
+    mlp_dense = (3 if gated else 2) * H * inter + inter_bias
     if n_exp:
         moe_inter = int(_g(cfg, "moe_intermediate_size", default=0) or inter)
         shared = int(_g(cfg, "n_shared_experts", default=0) or 0) * 3 * H * moe_inter
@@ -130,12 +134,14 @@ def text_params(cfg: dict) -> int:
         mlp_total = len(moe_layers) * moe + (L - len(moe_layers)) * mlp_dense
     else:
         mlp_total = L * mlp_dense
-    norms = 2 * H
+    norms = 4 * H if mt in ("opt", "bert") else 2 * H  # LayerNorm weight + bias
     total = L * (attn + norms) + mlp_total
     total += V * H + H  # embeddings + final norm
     tied = cfg.get("tie_word_embeddings", cfg.get("tie_embeddings", mt in ("bert", "gemma", "gemma2", "gemma3_text")))
     if not tied and "Model" != (cfg.get("architectures") or [""])[0][-5:] and mt not in ("bert",):
         total += V * H
+    if mt == "opt":  # learned positions (offset 2) and the final LayerNorm bias
+        total += (int(cfg.get("max_position_embeddings", 2048)) + 2) * H + H
     if mt == "bert":
         total += int(cfg.get("max_position_embeddings", 512)) * H + int(cfg.get("type_vocab_size", 2)) * H
     return int(total)

@@ -23,6 +23,8 @@ LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalL
 LLAMA4_ARCHS = {"Llama4ForCausalLM", "Llama4ForConditionalGeneration"}
 QWEN2_VL_ARCHS = {"Qwen2VLForConditionalGeneration"}
 NEMOTRON_H_ARCHS = {"NemotronHForCausalLM"}
+from ome_amd.models.config import PADDED_HEAD_ARCHS as DECODER_ARCHS  # noqa: E402  (models/decoder.py)
+
 MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM", "DeepseekV2ForCausalLM",
              "DeepseekV3ForCausalLM", "PhiMoEForCausalLM"}
 
@@ -48,6 +50,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.llama4 import Llama4ForCausalLM
 
         return Llama4ForCausalLM
+    if cfg.architecture in DECODER_ARCHS:
+        from ome_amd.models.decoder import DecoderForCausalLM
+
+        return DecoderForCausalLM
     if cfg.architecture in LAYERNORM_ARCHS or cfg.model_type in ("starcoder2", "gpt_neox", "phi"):
         from ome_amd.models.layernorm_lm import LayerNormForCausalLM
 
@@ -67,6 +73,7 @@ def model_class(cfg: ModelConfig):
 
 def supported(arch: str) -> bool:
     return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or arch in NEMOTRON_H_ARCHS or \
+        arch in DECODER_ARCHS or \
         arch == "GptOssForCausalLM"
 
 

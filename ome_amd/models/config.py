@@ -16,6 +16,66 @@ from typing import Any
 import torch
 
 
+# dense families of ``models/decoder.py`` (zero-padded head dims are handled there)
+PADDED_HEAD_ARCHS = {"OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM", "RWForCausalLM",
+                     "StableLmForCausalLM", "PersimmonForCausalLM", "CohereForCausalLM", "GlmForCausalLM",
+                     "Glm4ForCausalLM", "Olmo2ForCausalLM", "OlmoForCausalLM", "ArceeForCausalLM",
+                     "BloomForCausalLM", "MptForCausalLM"}
+
+
+def _standard_keys(c: dict[str, Any]) -> dict[str, Any]:
+    """Copy of an HF config with the family-specific key spellings (GPT-J ``n_embd``, OPT
+    ``ffn_dim``, Falcon ``n_head`` / ``multi_query`` ...) also present under the standard names
+    the parser reads.  Existing standard keys win."""
+    mt = c.get("model_type", "")
+    a: dict[str, Any] = {}
+    if mt == "gptj":
+        H, nh = c.get("n_embd", 4096), c.get("n_head", 16)
+        a = dict(hidden_size=H, num_hidden_layers=c.get("n_layer"), num_attention_heads=nh,
+                 intermediate_size=c.get("n_inner") or 4 * H, max_position_embeddings=c.get("n_positions"),
+                 partial_rotary_factor=(c.get("rotary_dim") or H // nh) / (H // nh),
+                 hidden_act=c.get("activation_function", "gelu_new"), layer_norm_eps=c.get("layer_norm_epsilon"),
+                 attention_bias=False, rope_theta=10000.0)
+    elif mt == "opt":
+        a = dict(intermediate_size=c.get("ffn_dim"), hidden_act=c.get("activation_function", "relu"),
+                 partial_rotary_factor=0.0, layer_norm_eps=1e-5, attention_bias=c.get("enable_bias", True),
+                 tie_word_embeddings=c.get("tie_word_embeddings", True))
+    elif mt == "falcon":
+        nh = c.get("num_attention_heads") or c.get("n_head", 71)
+        new, mq = c.get("new_decoder_architecture", False), c.get("multi_query", True)
+        H = c.get("hidden_size", 4544)
+        a = dict(num_attention_heads=nh, num_hidden_layers=c.get("num_hidden_layers") or c.get("n_layer"),
+                 num_key_value_heads=(c.get("num_kv_heads") or nh) if new else (1 if mq else nh),
+                 intermediate_size=c.get("ffn_hidden_size") or 4 * H, layer_norm_eps=c.get("layer_norm_epsilon"),
+                 hidden_act=c.get("activation", "gelu"), attention_bias=c.get("bias", False),
+                 tie_word_embeddings=c.get("tie_word_embeddings", True), multi_query=mq)
+    elif mt == "bloom":
+        H = c.get("hidden_size") or c.get("n_embed", 64)
+        a = dict(hidden_size=H, num_hidden_layers=c.get("n_layer"), num_attention_heads=c.get("n_head"),
+                 intermediate_size=4 * H, hidden_act="gelu_pytorch_tanh", layer_norm_eps=c.get("layer_norm_epsilon"),
+                 partial_rotary_factor=0.0, attention_bias=True, tie_word_embeddings=c.get("tie_word_embeddings", True))
+    elif mt == "mpt":
+        H = c.get("d_model", 2048)
+        ac = c.get("attn_config") or {}
+        a = dict(hidden_size=H, num_hidden_layers=c.get("n_layers"), num_attention_heads=c.get("n_heads"),
+                 intermediate_size=int(c.get("expansion_ratio", 4) * H), max_position_embeddings=c.get("max_seq_len"),
+                 hidden_act="gelu", layer_norm_eps=c.get("layer_norm_epsilon") or 1e-5, partial_rotary_factor=0.0,
+                 attention_bias=not c.get("no_bias", True), tie_word_embeddings=c.get("tie_word_embeddings", True),
+                 clip_qkv=ac.get("clip_qkv"))
+    elif mt == "stablelm":
+        a = dict(attention_bias=c.get("use_qkv_bias", False))
+    elif mt == "persimmon":
+        a = dict(attention_bias=True, hidden_act=c.get("hidden_act", "relu2"))
+    elif mt in ("cohere", "olmo"):
+        a = dict(layer_norm_eps=c.get("layer_norm_eps") or 1e-5, tie_word_embeddings=c.get("tie_word_embeddings",
+                                                                                         mt == "cohere"))
+    out = dict(c)
+    for k, v in a.items():
+        if v is not None and out.get(k) is None:
+            out[k] = v
+    return out
+
+
 @dataclass
 class ModelConfig:
     architecture: str = "LlamaForCausalLM"
@@ -82,14 +142,20 @@ class ModelConfig:
             mlp = self.num_experts * 3 * H * self.moe_intermediate_size + H * self.num_experts
             mlp += self.num_shared_experts * 3 * H * (self.shared_expert_intermediate_size or self.moe_intermediate_size)
         else:  # gated (SwiGLU / GeGLU) MLPs have 3 matrices; the LayerNorm families' fc1/fc2 have 2
-            gated = self.architecture not in ("Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalLM")
+            gated = self.architecture not in ("Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalLM",
+                                              "OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM",
+                                              "RWForCausalLM", "PersimmonForCausalLM", "ArceeForCausalLM",
+                                              "BloomForCausalLM", "MptForCausalLM")
             mlp = (3 if gated else 2) * H * self.intermediate_size
         emb = V * H * (1 if self.tie_word_embeddings else 2)
         return L * (attn + mlp + 2 * H) + emb + H
 
     @classmethod
     def from_hf(cls, cfg: dict[str, Any]) -> "ModelConfig":
-        text = cfg.get("text_config") or cfg
+        if cfg.get("text_config"):
+            text = _standard_keys(cfg["text_config"])
+        else:  # flat configs: keep the original keys (extra) next to the standard aliases
+            cfg = text = _standard_keys(cfg)
         arch = (cfg.get("architectures") or ["LlamaForCausalLM"])[0]
         H = text.get("hidden_size", 4096)
         nh = text.get("num_attention_heads", 32)
@@ -97,7 +163,9 @@ class ModelConfig:
         mt = text.get("model_type", cfg.get("model_type", "llama"))
         rope_theta = text.get("rope_theta", text.get("rotary_emb_base", 10000.0))
         rope_scaling = text.get("rope_scaling")
-        prf = text.get("partial_rotary_factor") or text.get("rotary_pct") or 1.0
+        prf = text.get("partial_rotary_factor")
+        if prf is None:  # 0 is meaningful (no RoPE: OPT's learned positions)
+            prf = text.get("rotary_pct") or 1.0
         rp = text.get("rope_parameters")  # transformers >= 5: {rope_type, rope_theta, ...} or per layer type
         if isinstance(rp, dict) and rp:
             glob = rp.get("full_attention", rp) if ("full_attention" in rp or "sliding_attention" in rp) else rp
@@ -106,7 +174,7 @@ class ModelConfig:
             if glob.get("rope_type", "default") != "default":
                 rope_scaling = dict(glob)
         attn_hd = 0
-        if mt == "phi" and hd not in (64, 128, 256):
+        if (mt == "phi" or arch in PADDED_HEAD_ARCHS) and hd not in (64, 128, 256):
             # the attention / RoPE-KV kernels tile head_dim in {64, 128, 256}: zero-pad each head
             # (q/k pad dims add 0 to every score, v pad dims feed zero columns of the padded o_proj)
             pad = next(d for d in (64, 128, 256) if d >= hd)
@@ -204,6 +272,19 @@ PRESETS: dict[str, dict] = {
                          num_hidden_layers=32, num_attention_heads=32, num_key_value_heads=8,
                          intermediate_size=14336, num_local_experts=8, num_experts_per_tok=2, vocab_size=32000,
                          rms_norm_eps=1e-5, rope_theta=1000000.0, max_position_embeddings=32768),
+    # BASELINE config 1 (operator plumbing on the CPU runtime): facebook/opt-125m
+    "opt-125m": dict(architectures=["OPTForCausalLM"], model_type="opt", hidden_size=768, num_hidden_layers=12,
+                     num_attention_heads=12, ffn_dim=3072, vocab_size=50272, max_position_embeddings=2048,
+                     word_embed_proj_dim=768, do_layer_norm_before=True, activation_function="relu",
+                     enable_bias=True, tie_word_embeddings=True, torch_dtype="float16"),
+    "tiny-opt": dict(architectures=["OPTForCausalLM"], model_type="opt", hidden_size=256, num_hidden_layers=2,
+                     num_attention_heads=4, ffn_dim=512, vocab_size=1024, max_position_embeddings=2048,
+                     word_embed_proj_dim=256, do_layer_norm_before=True, activation_function="relu",
+                     enable_bias=True, tie_word_embeddings=True),
+    "falcon-7b": dict(architectures=["FalconForCausalLM"], model_type="falcon", hidden_size=4544,
+                      num_hidden_layers=32, num_attention_heads=71, multi_query=True, parallel_attn=True,
+                      new_decoder_architecture=False, bias=False, alibi=False, vocab_size=65024,
+                      layer_norm_epsilon=1e-5, rope_theta=10000.0, max_position_embeddings=2048),
     "tiny-llama": dict(architectures=["LlamaForCausalLM"], model_type="llama", hidden_size=256, num_hidden_layers=2,
                        num_attention_heads=4, num_key_value_heads=2, head_dim=128, intermediate_size=512,
                        vocab_size=1024, rms_norm_eps=1e-5, rope_theta=10000.0, max_position_embeddings=2048),

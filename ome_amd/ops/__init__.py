@@ -336,13 +336,15 @@ class DecodeWorkspace:
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeWorkspace | None = None,
                  window: int = -1, out=None, order: torch.Tensor | None = None, k_scale: float = 1.0,
-                 v_scale: float = 1.0, softcap: float = 0.0, sinks: torch.Tensor | None = None) -> torch.Tensor:
-    """q [B, Hq, D] -> [B, Hq, D].  ``order`` (int32 [B], optional): sequence visit order for the
+                 v_scale: float = 1.0, softcap: float = 0.0, sinks: torch.Tensor | None = None,
+                 alibi: torch.Tensor | None = None) -> torch.Tensor:
+    """q [B, Hq, D] -> [B, Hq, D].  ``alibi``: fp32 [Hq] ALiBi slopes (logit += slope * (key - query
+    position)), or None.  ``order`` (int32 [B], optional): sequence visit order for the
     workgroup dispatcher (longest first balances the tail).  The cache may be bf16 or fp8
     (``k_scale`` / ``v_scale`` dequantise it)."""
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window, k_scale, v_scale, softcap,
-                             sinks)
+                             sinks, alibi)
         if out is not None:
             out.copy_(r)
             return out
@@ -356,12 +358,12 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeW
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(seq_lens).data_ptr(), out.data_ptr(),
          out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
          float(scale), int(window), _i32(order).data_ptr() if order is not None else None, kv_format(k_cache),
-         float(k_scale), float(v_scale), float(softcap), _sinks(sinks), stream_ptr())
+         float(k_scale), float(v_scale), float(softcap), _sinks(sinks), _sinks(alibi), stream_ptr())
     return out
 
 
 def _sinks(s: torch.Tensor | None):
-    """Attention-sink logits (GPT-OSS): fp32 [Hq] on the device, or None."""
+    """Per-head fp32 [Hq] device vector (GPT-OSS attention-sink logits, ALiBi slopes), or None."""
     if s is None:
         return None
     assert s.dtype == torch.float32 and s.is_contiguous()
@@ -424,12 +426,13 @@ def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) ->
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale, window: int = -1,
                   out=None, k_scale: float = 1.0, v_scale: float = 1.0, softcap: float = 0.0,
-                  sinks: torch.Tensor | None = None) -> torch.Tensor:
+                  sinks: torch.Tensor | None = None, alibi: torch.Tensor | None = None) -> torch.Tensor:
     """q [Tq, Hq, D]; items int32 [n, 2] from :func:`prefill_work_items`.  ``softcap`` > 0:
-    attention-logit soft-capping ``cap * tanh(score / cap)`` (Gemma-2)."""
+    attention-logit soft-capping ``cap * tanh(score / cap)`` (Gemma-2); ``alibi``: fp32 [Hq]
+    ALiBi slopes."""
     if not _gpu(q):
         r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window, k_scale, v_scale,
-                              softcap, sinks)
+                              softcap, sinks, alibi)
         if out is not None:
             out.copy_(r)
             return out
@@ -441,7 +444,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
          _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),
          int(window), kv_format(k_cache), float(k_scale), float(v_scale), float(softcap), _sinks(sinks),
-         stream_ptr())
+         _sinks(alibi), stream_ptr())
     return out
 
 

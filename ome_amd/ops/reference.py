@@ -42,6 +42,8 @@ def act(x: torch.Tensor, kind: int) -> torch.Tensor:
         y = torch.nn.functional.gelu(f, approximate="tanh")
     elif kind == 4:
         y = torch.relu(f).square()
+    elif kind == 5:
+        y = torch.relu(f)
     else:
         y = torch.nn.functional.gelu(f)
     x.copy_(y.to(x.dtype))
@@ -202,7 +204,7 @@ def attn_lo(qpos, window: int):
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, k_scale=1.0,
-                 v_scale=1.0, softcap=0.0, sinks=None) -> torch.Tensor:
+                 v_scale=1.0, softcap=0.0, sinks=None, alibi=None) -> torch.Tensor:
     B, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -217,13 +219,16 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, 
             k, v = k[lo:], v[lo:]
             qh = q[b, h * G:(h + 1) * G].float()
             s = _cap((qh @ k.T) * scale, softcap)
+            if alibi is not None:  # slope * (key - query position)
+                kp = torch.arange(lo, L, device=q.device, dtype=torch.float32) - (L - 1)
+                s = s + alibi[h * G:(h + 1) * G].float().view(G, 1).to(s.device) * kp[None]
             sk = None if sinks is None else sinks[h * G:(h + 1) * G].float().view(G, 1)
             out[b, h * G:(h + 1) * G] = (_softmax_sink(s, sk) @ v).to(q.dtype)
     return out
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window=-1, k_scale=1.0,
-                  v_scale=1.0, softcap=0.0, sinks=None) -> torch.Tensor:
+                  v_scale=1.0, softcap=0.0, sinks=None, alibi=None) -> torch.Tensor:
     Tq, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -242,6 +247,9 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, windo
             k, v = gather_kv(k_cache, v_cache, block_tables[s], L, h, P, k_scale, v_scale)
             qh = q[q0:q1, h * G:(h + 1) * G].float().transpose(0, 1)  # [G, ql, D]
             sc = _cap((qh @ k.T) * scale, softcap)
+            if alibi is not None:
+                sl = alibi[h * G:(h + 1) * G].float().view(G, 1, 1).to(sc.device)
+                sc = sc + sl * (kpos - qpos).float()[None]
             sc = sc.masked_fill(~mask[None], float("-inf"))
             sk = None if sinks is None else sinks[h * G:(h + 1) * G].float().view(G, 1, 1).expand(G, sc.shape[1], 1)
             o = _softmax_sink(sc, sk) @ v

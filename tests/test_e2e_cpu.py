@@ -162,3 +162,48 @@ def test_isvc_serves_and_benchmarks_on_cpu(tmp_path):
         assert gone
     finally:
         cl.shutdown()
+
+
+@pytest.mark.timeout(600)
+def test_baseline_config1_opt125m_on_cpu_runtime(tmp_path):
+    """BASELINE.json config 1: BaseModel + InferenceService reconcile for OPT-125m on the CPU
+    runtime.  The ISVC names no runtime: the model agent parses the (random-init) OPT-125m
+    config -- architecture, 125M parameters -- and the RuntimeSelector picks the CPU runtime by
+    ``modelArchitecture: OPTForCausalLM`` and its size range; the executor runs the real server,
+    which serves a completion through the OPT decoder (learned positions, ReLU MLP)."""
+    rt = _runtime("opt-cpu-rt")
+    fmt = rt["spec"]["supportedModelFormats"][0]
+    fmt["modelArchitecture"] = "OPTForCausalLM"
+    rt["spec"]["modelSizeRange"] = {"min": "100M", "max": "200M"}
+    cmd = rt["spec"]["engineConfig"]["runner"]["command"]
+    cmd[cmd.index("tiny")] = "opt"
+    bm = {"apiVersion": API, "kind": "ClusterBaseModel", "metadata": {"name": "opt-125m"},
+          "spec": {"vendor": "facebook", "storage": {"storageUri": "random://opt-125m",
+                                                     "path": str(tmp_path / "models" / "opt-125m")}}}
+    isvc = {"apiVersion": API, "kind": "InferenceService", "metadata": {"name": "opt", "namespace": "default"},
+            "spec": {"model": {"name": "opt-125m"}, "engine": {"minReplicas": 1, "maxReplicas": 1}}}
+    cl = Cluster(str(tmp_path / "state"), gpus=0, probe_scale=1.0)
+    try:
+        cl.apply([_runtime(), rt, bm])
+        cl.start()
+        assert cl.wait_for(lambda: (cl.store.get(API, "ClusterBaseModel", "opt-125m").get("status") or {})
+                           .get("state") == "Ready", timeout=60)
+        spec = cl.store.get(API, "ClusterBaseModel", "opt-125m")["spec"]
+        assert spec.get("modelArchitecture") == "OPTForCausalLM" and spec.get("modelParameterSize") == "125.24M"
+        cl.apply([isvc])
+        ok = cl.wait_for(lambda: _ready(cl.store.get(API, "InferenceService", "opt", "default")), timeout=300)
+        got = cl.store.get(API, "InferenceService", "opt", "default")
+        assert ok, got.get("status")
+        dep = cl.store.get("apps/v1", "Deployment", "opt-engine", "default")
+        assert dep["metadata"]["labels"].get(C.SERVING_RUNTIME_LABEL, dep["metadata"]["labels"].get(
+            "serving-runtime")) == "opt-cpu-rt"
+        os.environ["OME_LOCAL_DNS"] = cl.executor.kubelet.proxies.dns_path
+        base = resolve_url(got["status"]["url"])
+        req = urllib.request.Request(base + "/v1/completions", data=json.dumps(
+            {"model": "opt", "prompt": "hello world", "max_tokens": 5, "temperature": 0, "ignore_eos": True}).encode(),
+            headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=120) as r:
+            out = json.loads(r.read())
+        assert out["usage"]["completion_tokens"] == 5
+    finally:
+        cl.shutdown()

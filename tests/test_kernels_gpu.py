@@ -1,5 +1,6 @@
 """Numerics of every hand-written gfx950 kernel vs the plain-PyTorch fp32 reference of the same op."""
 import math
+import os
 import random
 
 import pytest
@@ -338,3 +339,38 @@ def test_fused_moe_bias_and_gptoss_act():
     tw, tid = ops.moe_route(logits, k, True)
     out = ops.fused_moe(x, tw, tid, w13, w2, 2, 1.0, b13, b2)
     _close(out, ref.fused_moe(x, tw, tid, w13, w2, 2, 1.0, b13, b2), atol=5e-2, rtol=5e-2)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(64, 16, 2), (128, 32, 8), (128, 5, 5), (256, 8, 1)])
+@pytest.mark.parametrize("parts", [4096, 256])
+def test_paged_attention_alibi(D, Hq, Hkv, parts):
+    """ALiBi slopes (Bloom / MPT) in every decode variant (incl. split-K) and both prefill kernels
+    (v2 for GQA-4 at D=128, v1 otherwise), against the fp32 reference."""
+    from ome_amd.models.decoder import alibi_slopes
+
+    P = 16
+    seq_lens = [1, 37, 300, 1000]
+    npages = sum(-(-L // P) for L in seq_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    bt = _block_tables(seq_lens, P, npages)
+    sl = torch.tensor(seq_lens, dtype=torch.int32, device=DEV)
+    al = alibi_slopes(Hq, "bloom").to(DEV)
+    q = torch.randn(len(seq_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    ws = ops.DecodeWorkspace(len(seq_lens), Hq, D, 2048, parts, DEV)
+    want = ref.paged_decode(q, kc, vc, bt, sl, D ** -0.5, -1, 1.0, 1.0, 0.0, None, al)
+    for variant in ("1", "2", "3", "4"):
+        os.environ["OME_DECODE_ATTN"] = variant
+        try:
+            out = ops.paged_decode(q, kc, vc, bt, sl, D ** -0.5, ws, alibi=al)
+        finally:
+            os.environ.pop("OME_DECODE_ATTN")
+        _close(out, want, atol=2e-2)
+    q_lens = [37, 64, 1, 100]
+    kv_lens = [37, 80, 300, 100]
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    items = torch.tensor(ops.prefill_work_items(q_lens, kv_lens), dtype=torch.int32, device=DEV)
+    bt2 = _block_tables(kv_lens, P, npages)
+    qp = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    outp = ops.paged_prefill(qp, kc, vc, bt2, cu, kl, items, D ** -0.5, alibi=al)
+    _close(outp, ref.paged_prefill(qp, kc, vc, bt2, cu, kl, D ** -0.5, -1, 1.0, 1.0, 0.0, None, al), atol=2e-2)
