@@ -14,9 +14,8 @@ import torch
 from ome_amd.models.config import ModelConfig
 
 DENSE_ARCHS = {
-    "LlamaForCausalLM", "MistralForCausalLM", "Qwen2ForCausalLM", "Qwen3ForCausalLM", "InternLM2ForCausalLM",
-    "LlamaModel", "MistralModel", "Qwen2Model", "Qwen3Model", "LlamaForSequenceClassification",
-    "Qwen2ForRewardModel", "Phi3ForCausalLM", "GraniteForCausalLM", "SmolLM3ForCausalLM",
+    "LlamaForCausalLM", "MistralForCausalLM", "Qwen2ForCausalLM", "Qwen3ForCausalLM",
+    "LlamaModel", "MistralModel", "Qwen2Model", "Qwen3Model",
 }
 GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
 LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalLM"}

@@ -20,7 +20,14 @@ import torch
 PADDED_HEAD_ARCHS = {"OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM", "RWForCausalLM",
                      "StableLmForCausalLM", "PersimmonForCausalLM", "CohereForCausalLM", "GlmForCausalLM",
                      "Glm4ForCausalLM", "Olmo2ForCausalLM", "OlmoForCausalLM", "ArceeForCausalLM",
-                     "BloomForCausalLM", "MptForCausalLM"}
+                     "BloomForCausalLM", "MptForCausalLM", "Phi3ForCausalLM", "GraniteForCausalLM",
+                     "SmolLM3ForCausalLM", "InternLM2ForCausalLM", "InternLM2ForRewardModel", "Qwen2ForRewardModel",
+                     "LlamaForSequenceClassification", "Qwen2ForSequenceClassification",
+                     "MistralForSequenceClassification", "MiMoForCausalLM", "QWenLMHeadModel", "BaichuanForCausalLM",
+                     "ExaoneForCausalLM", "OrionForCausalLM", "MiniCPMForCausalLM", "ChatGLMModel",
+                     "ChatGLMForConditionalGeneration"}
+# remote-code class names that end in "Model" but are causal LMs (not embedding models)
+CAUSAL_MODEL_CLASSES = {"ChatGLMModel", "QWenLMHeadModel", "TeleFLMModel"}
 
 
 def _standard_keys(c: dict[str, Any]) -> dict[str, Any]:
@@ -62,6 +69,29 @@ def _standard_keys(c: dict[str, Any]) -> dict[str, Any]:
                  hidden_act="gelu", layer_norm_eps=c.get("layer_norm_epsilon") or 1e-5, partial_rotary_factor=0.0,
                  attention_bias=not c.get("no_bias", True), tie_word_embeddings=c.get("tie_word_embeddings", True),
                  clip_qkv=ac.get("clip_qkv"))
+    elif mt == "qwen":  # Qwen (v1): intermediate_size is twice the per-projection width
+        nh = c.get("num_attention_heads", 32)
+        a = dict(intermediate_size=(c["intermediate_size"] // 2) if c.get("intermediate_size") else None,
+                 rope_theta=c.get("rotary_emb_base", 10000.0), rms_norm_eps=c.get("layer_norm_epsilon"),
+                 head_dim=c.get("kv_channels"), num_key_value_heads=nh, attention_bias=True,
+                 max_position_embeddings=c.get("seq_length"), partial_rotary_factor=c.get("rotary_pct"))
+    elif mt == "baichuan":
+        a = dict(max_position_embeddings=c.get("model_max_length"), num_key_value_heads=c.get("num_attention_heads"))
+    elif mt == "exaone":
+        a = dict(num_hidden_layers=c.get("num_layers"), rms_norm_eps=c.get("layer_norm_epsilon"),
+                 hidden_act=c.get("activation_function"))
+    elif mt == "chatglm":
+        mq = c.get("multi_query_attention", False)
+        a = dict(num_hidden_layers=c.get("num_layers"), vocab_size=c.get("padded_vocab_size"),
+                 head_dim=c.get("kv_channels"), intermediate_size=c.get("ffn_hidden_size"),
+                 num_key_value_heads=c.get("multi_query_group_num") if mq else c.get("num_attention_heads"),
+                 rms_norm_eps=c.get("layernorm_epsilon"), max_position_embeddings=c.get("seq_length"),
+                 rope_theta=10000.0 * float(c.get("rope_ratio", 1.0)), partial_rotary_factor=0.5,
+                 attention_bias=c.get("add_qkv_bias", True), tie_word_embeddings=False)
+    elif mt == "internlm2":
+        a = dict(attention_bias=c.get("bias", False))
+    elif mt == "mimo":
+        a = dict(attention_bias=True)
     elif mt == "stablelm":
         a = dict(attention_bias=c.get("use_qkv_bias", False))
     elif mt == "persimmon":
@@ -202,7 +232,7 @@ class ModelConfig:
             attention_bias=bool(text.get("attention_bias", text.get("use_bias", mt in ("qwen2", "qwen2_moe", "qwen2_vl", "qwen2_vl_text", "phi")))),
             qk_norm=mt in ("qwen3", "qwen3_moe", "gemma3", "gemma3_text"),
             hidden_act=text.get("hidden_act", text.get("hidden_activation", "silu")),
-            sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt in ("mistral", "starcoder2")) else None,
+            sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt in ("mistral", "starcoder2", "phi3")) else None,
             torch_dtype=str(text.get("torch_dtype", cfg.get("torch_dtype", "bfloat16"))),
         )
         # MoE variants
@@ -229,7 +259,8 @@ class ModelConfig:
         q = cfg.get("quantization_config")
         if q:
             c.quantization = q.get("quant_method") or q.get("quant_type")
-        c.is_embedding = ("Embedding" in arch) or (arch.endswith("Model") and "ForCausalLM" not in arch)
+        c.is_embedding = ("Embedding" in arch) or arch.endswith(("ForSequenceClassification", "RewardModel")) or \
+            (arch.endswith("Model") and "ForCausalLM" not in arch and arch not in CAUSAL_MODEL_CLASSES)
         c.extra = {k: v for k, v in cfg.items() if k not in ("text_config",)}
         if text is not cfg:  # multimodal wrappers: the language model's keys win
             c.extra.update({k: v for k, v in text.items() if k != "quantization_config"})
@@ -478,6 +509,16 @@ def rope_cos_sin(cfg: ModelConfig, max_pos: int, device=None) -> torch.Tensor:
             return 1.0 if s <= 1 else 0.1 * m * math.log(s) + 1.0
 
         mscale = ym(factor, ms) / ym(factor, msa) if msa else ym(factor, ms)
+    elif rtype in ("longrope", "su"):
+        # Phi-3 LongRoPE: per-frequency rescale factors -- the long set when the served context
+        # exceeds the pre-training one (a long-context deployment, as HF does for such sequences;
+        # one set for every position keeps cached keys consistent), else the short set
+        old = sc.get("original_max_position_embeddings") or cfg.extra.get("original_max_position_embeddings") or \
+            cfg.max_position_embeddings
+        factor = sc.get("factor") or cfg.max_position_embeddings / old
+        mscale = sc.get("attention_factor") or (1.0 if factor <= 1.0 else
+                                                math.sqrt(1 + math.log(factor) / math.log(old)))
+        inv = inv / torch.tensor(sc["long_factor" if max_pos > old else "short_factor"], dtype=torch.float64)
     elif rtype == "dynamic":
         factor = sc["factor"]
         old = cfg.max_position_embeddings

@@ -80,6 +80,12 @@ class DecoderSpec:
     lm_head_bias: bool = False
     alibi: str = ""              # "" | bloom (Bloom / Falcon slopes) | mpt (MPT slopes, alibi_bias_max)
     embed_norm: bool = False     # LayerNorm right after the token embedding (Bloom)
+    embed_scale: float = 1.0     # Granite embedding_multiplier, MiniCPM scale_emb
+    residual_scale: float = 1.0  # block outputs scaled before the residual add (Granite, MiniCPM)
+    attn_scale: float | None = None  # softmax scale override (Granite attention_multiplier)
+    logit_mult: float | None = None  # logits multiplier (Cohere logit_scale, 1/logits_scaling, MiniCPM)
+    head: str = ""               # "" | score (Linear, LlamaForSequenceClassification) | reward_mlp (Qwen2 RM) | v_head
+    lm_head_norm: bool = False   # Baichuan-2 NormHead: lm_head rows L2-normalised
     names: list = field(default_factory=lambda: list(_LLAMA_NAMES))
     prefixes: tuple = ()
 
@@ -182,6 +188,72 @@ def _spec_for(cfg: ModelConfig) -> DecoderSpec:
                                (r"blocks\.(\d+)\.attn\.out_proj\.weight", r"L.\1.o.weight"),
                                (r"blocks\.(\d+)\.ffn\.up_proj\.weight", r"L.\1.fc.weight"),
                                (r"blocks\.(\d+)\.ffn\.down_proj\.weight", r"L.\1.down.weight")])
+    if arch == "Phi3ForCausalLM":
+        names = list(_LLAMA_NAMES) + [(r"(?:model\.)?layers\.(\d+)\.self_attn\.qkv_proj\.weight", r"L.\1.qkv.weight")]
+        return DecoderSpec(qkv_layout="concat", names=names)
+    if arch == "GraniteForCausalLM":
+        return DecoderSpec(embed_scale=float(hf.get("embedding_multiplier", 1.0)),
+                           residual_scale=float(hf.get("residual_multiplier", 1.0)),
+                           attn_scale=hf.get("attention_multiplier"),
+                           logit_mult=1.0 / float(hf.get("logits_scaling", 1.0)))
+    if arch == "SmolLM3ForCausalLM":
+        return DecoderSpec()  # NoPE layers from ``no_rope_layers`` (DecoderForCausalLM.__init__)
+    if arch in ("InternLM2ForCausalLM", "InternLM2ForRewardModel"):
+        return DecoderSpec(qkv_layout="groups", head="v_head" if arch.endswith("RewardModel") else "",
+                           prefixes=("model.",), names=[
+                               (r"tok_embeddings\.weight", "embed"), (r"norm\.weight", "norm.weight"),
+                               (r"output\.weight", "lm_head.weight"), (r"v_head\.weight", "head.0.weight"),
+                               (r"layers\.(\d+)\.attention\.wqkv\.(weight|bias)", r"L.\1.qkv.\2"),
+                               (r"layers\.(\d+)\.attention\.wo\.(weight|bias)", r"L.\1.o.\2"),
+                               (r"layers\.(\d+)\.feed_forward\.w1\.weight", r"L.\1.gate.weight"),
+                               (r"layers\.(\d+)\.feed_forward\.w3\.weight", r"L.\1.up.weight"),
+                               (r"layers\.(\d+)\.feed_forward\.w2\.weight", r"L.\1.down.weight"),
+                               (r"layers\.(\d+)\.attention_norm\.weight", r"L.\1.ln1.weight"),
+                               (r"layers\.(\d+)\.ffn_norm\.weight", r"L.\1.ln2.weight")])
+    if arch in ("Qwen2ForRewardModel", "LlamaForSequenceClassification", "Qwen2ForSequenceClassification",
+                "MistralForSequenceClassification"):
+        names = list(_LLAMA_NAMES) + [(r"score\.(\d+)\.(weight|bias)", r"head.\1.\2"),
+                                      (r"score\.(weight|bias)", r"head.0.\1")]
+        return DecoderSpec(head="reward_mlp" if arch == "Qwen2ForRewardModel" else "score", names=names)
+    if arch == "MiMoForCausalLM":  # Qwen2 layout; the multi-token-prediction layers (mtp_layers.*) are unused
+        return DecoderSpec()
+    if arch == "QWenLMHeadModel":  # Qwen (v1): fused biased c_attn, SwiGLU as c_proj(w1(x) * silu(w2(x)))
+        return DecoderSpec(qkv_layout="concat", prefixes=("transformer.",), names=[
+            (r"wte\.weight", "embed"), (r"ln_f\.weight", "norm.weight"), (r"lm_head\.weight", "lm_head.weight"),
+            (r"h\.(\d+)\.ln_1\.weight", r"L.\1.ln1.weight"), (r"h\.(\d+)\.ln_2\.weight", r"L.\1.ln2.weight"),
+            (r"h\.(\d+)\.attn\.c_attn\.(weight|bias)", r"L.\1.qkv.\2"),
+            (r"h\.(\d+)\.attn\.c_proj\.weight", r"L.\1.o.weight"),
+            (r"h\.(\d+)\.mlp\.w1\.weight", r"L.\1.up.weight"), (r"h\.(\d+)\.mlp\.w2\.weight", r"L.\1.gate.weight"),
+            (r"h\.(\d+)\.mlp\.c_proj\.weight", r"L.\1.down.weight")])
+    if arch == "BaichuanForCausalLM":  # fused W_pack; 13B: ALiBi; Baichuan-2: NormHead
+        names = list(_LLAMA_NAMES) + [(r"(?:model\.)?layers\.(\d+)\.self_attn\.W_pack\.weight", r"L.\1.qkv.weight")]
+        big = cfg.hidden_size == 5120 and cfg.num_layers == 40
+        return DecoderSpec(qkv_layout="concat", names=names, rope="none" if big else "neox", alibi="bloom" if big else "",
+                           lm_head_norm=cfg.vocab_size == 125696)
+    if arch == "ExaoneForCausalLM":
+        return DecoderSpec(prefixes=("transformer.",), names=[
+            (r"wte\.weight", "embed"), (r"ln_f\.weight", "norm.weight"), (r"lm_head\.weight", "lm_head.weight"),
+            (r"h\.(\d+)\.ln_1\.weight", r"L.\1.ln1.weight"), (r"h\.(\d+)\.ln_2\.weight", r"L.\1.ln2.weight"),
+            (r"h\.(\d+)\.attn\.attention\.(q|k|v)_proj\.weight", r"L.\1.\2.weight"),
+            (r"h\.(\d+)\.attn\.attention\.out_proj\.weight", r"L.\1.o.weight"),
+            (r"h\.(\d+)\.mlp\.c_fc_0\.weight", r"L.\1.gate.weight"), (r"h\.(\d+)\.mlp\.c_fc_1\.weight", r"L.\1.up.weight"),
+            (r"h\.(\d+)\.mlp\.c_proj\.weight", r"L.\1.down.weight")])
+    if arch == "OrionForCausalLM":  # Llama with LayerNorm (weight + bias)
+        return DecoderSpec(norm="ln")
+    if arch == "MiniCPMForCausalLM":
+        return DecoderSpec(embed_scale=float(hf.get("scale_emb", 1.0)),
+                           residual_scale=float(hf.get("scale_depth", 1.0)) / math.sqrt(cfg.num_layers),
+                           logit_mult=float(hf.get("dim_model_base", cfg.hidden_size)) / cfg.hidden_size)
+    if arch in ("ChatGLMModel", "ChatGLMForConditionalGeneration"):  # ChatGLM2/3, GLM-4 (THUDM remote code)
+        return DecoderSpec(rope="interleaved", qkv_layout="concat", prefixes=("transformer.",), names=[
+            (r"embedding\.word_embeddings\.weight", "embed"), (r"encoder\.final_layernorm\.weight", "norm.weight"),
+            (r"output_layer\.weight", "lm_head.weight"),
+            (r"encoder\.layers\.(\d+)\.input_layernorm\.weight", r"L.\1.ln1.weight"),
+            (r"encoder\.layers\.(\d+)\.post_attention_layernorm\.weight", r"L.\1.ln2.weight"),
+            (r"encoder\.layers\.(\d+)\.self_attention\.query_key_value\.(weight|bias)", r"L.\1.qkv.\2"),
+            (r"encoder\.layers\.(\d+)\.self_attention\.dense\.weight", r"L.\1.o.weight"),
+            (r"encoder\.layers\.(\d+)\.mlp\.dense_h_to_4h\.weight", r"L.\1.gate_up.weight"),
+            (r"encoder\.layers\.(\d+)\.mlp\.dense_4h_to_h\.weight", r"L.\1.down.weight")])
     if arch == "OlmoForCausalLM":
         return DecoderSpec(norm="ln_noaffine")
     if arch == "ArceeForCausalLM":
@@ -279,7 +351,13 @@ class DecoderForCausalLM(LlamaForCausalLM):
             raise NotImplementedError(f"hidden_act {act!r} for a {sp.mlp} MLP")
         self.act = plain[act]
         self.clip_qkv = hf.get("clip_qkv")
-        self.logit_scale = float(hf.get("logit_scale") or 1.0)
+        self.logit_scale = float(sp.logit_mult if sp.logit_mult is not None else (hf.get("logit_scale") or 1.0))
+        if sp.attn_scale is not None:
+            self.scale = float(sp.attn_scale)
+        # per-layer RoPE on/off (SmolLM3 ``no_rope_layers``: 1 = rotate, 0 = NoPE)
+        nrl = hf.get("no_rope_layers")
+        self.rope_on = [bool(nrl[i]) if nrl else True for i in range(cfg.num_layers)]
+        self.head_w: list[torch.Tensor] = []  # classification / reward head (weight, bias, ...)
         if sp.qk_norm == "rms_full" and self.tp.tp > cfg.num_kv_heads:
             raise NotImplementedError("full-width q/k RMSNorm with replicated KV heads")
         L = cfg.num_layers
@@ -289,6 +367,7 @@ class DecoderForCausalLM(LlamaForCausalLM):
         self.qnb, self.knb = none(), none()
         self.norm_b = self.lm_head_b = self.pos_embed = self.proj_in = self.proj_out = None
         self.emb_ln = self.emb_ln_b = None
+        self.num_labels = int(hf.get("num_labels") or len(hf.get("id2label") or {}) or 1)
         self.alibi = None
         if sp.alibi:
             sl = alibi_slopes(cfg.num_heads, sp.alibi, float((hf.get("attn_config") or {}).get("alibi_bias_max", 8)))
@@ -361,6 +440,11 @@ class DecoderForCausalLM(LlamaForCausalLM):
         self.lm_head = self.embed if cfg.tie_word_embeddings else self._alloc(tp.vocab, H, std=std, gen=gen)
         if sp.lm_head_bias:
             self.lm_head_b = self._alloc(tp.vocab, std=std, gen=gen)
+        if sp.head == "reward_mlp":
+            self.head_w = [zeros(H), self._alloc(H, H, std=std, gen=gen), zeros(self.num_labels),
+                           self._alloc(self.num_labels, H, std=std, gen=gen)]
+        elif sp.head:
+            self.head_w = [self._alloc(self.num_labels, H, std=std, gen=gen)]
         self._finish()
         return self
 
@@ -400,6 +484,16 @@ class DecoderForCausalLM(LlamaForCausalLM):
         self.norm_b = put(glob["norm.bias"]) if "norm.bias" in glob else None
         if "pos_embed" in glob:
             self.pos_embed = put(glob["pos_embed"])
+        sp = self.spec
+        if sp.head:
+            hk = sorted(k for k in glob if k.startswith("head."))
+            self.head_w = [put(glob[k]) for k in hk]  # head.0.bias, head.0.weight, head.2.bias, head.2.weight
+        if sp.lm_head_norm:
+            self.lm_head = put(torch.nn.functional.normalize(glob["lm_head.weight"].float(), dim=-1)[
+                self.tp.vocab_start:self.tp.vocab_end]) if "lm_head.weight" in glob else self.lm_head
+            if self.lm_head.shape[0] < self.tp.vocab:
+                self.lm_head = torch.cat([self.lm_head, self.lm_head.new_zeros(self.tp.vocab - self.lm_head.shape[0],
+                                                                               self.lm_head.shape[1])], 0)
         if "emb_ln.weight" in glob:
             self.emb_ln, self.emb_ln_b = put(glob["emb_ln.weight"]), put(glob["emb_ln.bias"])
         if "proj_in.weight" in glob:
@@ -578,7 +672,7 @@ class DecoderForCausalLM(LlamaForCausalLM):
         ks, vs = kv.scales(i)
         kern_norm = sp.qk_norm == "rms_head"
         ops.rope_qkv_cache(qkv, meta.positions, self.cos_sin, self.rot_k, q, k_cache, v_cache, meta.slots,
-                           tp.hq, tp.hkv, D, self.rot_k > 0, self.qn[i] if kern_norm else None,
+                           tp.hq, tp.hkv, D, self.rot_k > 0 and self.rope_on[i], self.qn[i] if kern_norm else None,
                            self.kn[i] if kern_norm else None, self.eps, ks, vs)
         attn = self.attention(q, k_cache, v_cache, meta, ks, vs)
         return linear(attn.view(T, tp.hq * D), self.w_o[i], self.b_o[i])
@@ -600,6 +694,8 @@ class DecoderForCausalLM(LlamaForCausalLM):
             h = h + ops.embedding(meta.positions + self.spec.pos_offset, self.pos_embed)
         if self.emb_ln is not None:
             h = ops.layernorm(h, self.emb_ln, self.emb_ln_b, self.eps)
+        if self.spec.embed_scale != 1.0:
+            h = h * self.spec.embed_scale
         return h
 
     def attention(self, q, k_cache, v_cache, meta: AttnMeta, ks: float = 1.0, vs: float = 1.0) -> torch.Tensor:
@@ -625,7 +721,12 @@ class DecoderForCausalLM(LlamaForCausalLM):
                 input_embeds: torch.Tensor | None = None) -> torch.Tensor:
         st, mode = pstate.get(), self.spec.residual
         T, H = ids.shape[0], self.cfg.hidden_size
-        ar = pstate.tp_all_reduce
+        rs = self.spec.residual_scale
+
+        def ar(t):  # TP all-reduce of a block output (+ Granite / MiniCPM residual scaling)
+            t = pstate.tp_all_reduce(t)
+            return t if rs == 1.0 else t.mul_(rs)
+
         if st.pp_size > 1 and not st.is_first_pp:
             x, residual = pstate.pp_recv(((T, H), self.dtype, ids.device), ((T, H), self.dtype, ids.device))
         else:
@@ -676,6 +777,17 @@ class DecoderForCausalLM(LlamaForCausalLM):
             return ops.rmsnorm(residual, self.norm, self.eps)
         self._add_norm(x, residual, self.norm, self.norm_b)
         return x if self.proj_out is None else linear(x, self.proj_out)
+
+    def pool(self, hidden: torch.Tensor, cu: torch.Tensor) -> torch.Tensor:
+        """Embedding / reward / classification output per sequence (rows ``cu[s]:cu[s+1]``):
+        last-token pooling, then the model's head (scores, un-normalised) or L2 normalisation."""
+        if not self.spec.head:
+            return ops.pool(hidden, cu, 0, True)
+        last = hidden.index_select(0, (cu[1:] - 1).long())
+        w = self.head_w
+        if self.spec.head == "reward_mlp":  # score = Linear(ReLU(Linear(h)))
+            return linear(torch.relu(linear(last, w[1], w[0])), w[3], w[2]).float()
+        return linear(last, w[-1], w[0] if len(w) > 1 else None).float()
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = linear(hidden, self.lm_head, self.lm_head_b)

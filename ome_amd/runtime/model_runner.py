@@ -578,6 +578,7 @@ class ModelRunner:
 
     def embed(self, batch: StepBatch) -> list[list[float]]:
         """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts."""
+        self.slots.flush()  # block-table rows of the newly admitted requests
         P = self.P
         ids, pos, slots, q_lens, req_idx = [], [], [], [], []
         for c in batch.chunks:
@@ -597,4 +598,6 @@ class ModelRunner:
         meta = AttnMeta("prefill", t(pos), t(slots), bt, cu_q=t(cu), kv_lens=t(q_lens),
                         items=t(items).view(-1, 2) if items else torch.zeros(0, 2, dtype=torch.int32, device=dv))
         hidden = self.model.forward(t(ids), meta, self.kv)
-        return ops.pool(hidden, t(cu), 0, True).cpu().tolist()
+        pool = getattr(self.model, "pool", None)  # classification / reward heads (models/decoder.py)
+        out = pool(hidden, t(cu)) if pool is not None else ops.pool(hidden, t(cu), 0, True)
+        return out.cpu().tolist()

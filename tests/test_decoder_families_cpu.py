@@ -75,6 +75,25 @@ def _cfg(kind: str):
         return T.MptForCausalLM, T.MptConfig(d_model=192, n_heads=3, n_layers=3, max_seq_len=512,
                                              attn_config={"alibi": True, "alibi_bias_max": 8, "clip_qkv": 0.5},
                                              **common)
+    if kind.startswith("phi3"):  # head_dim 96: zero-padded to 128
+        kw = dict(hidden_size=192, intermediate_size=256, num_hidden_layers=3, num_attention_heads=2,
+                  num_key_value_heads=2, max_position_embeddings=512, sliding_window=24, **common)
+        if kind == "phi3_longrope":
+            kw.update(max_position_embeddings=1024, original_max_position_embeddings=32, rope_scaling={
+                "type": "longrope", "short_factor": [1.0 + 0.05 * i for i in range(48)],
+                "long_factor": [1.5 + 0.1 * i for i in range(48)]})
+        return T.Phi3ForCausalLM, T.Phi3Config(**kw)
+    if kind == "granite":
+        return T.GraniteForCausalLM, T.GraniteConfig(hidden_size=128, intermediate_size=256, num_hidden_layers=3,
+                                                     num_attention_heads=2, num_key_value_heads=1,
+                                                     embedding_multiplier=6.0, residual_multiplier=0.3,
+                                                     attention_multiplier=0.05, logits_scaling=4.0,
+                                                     max_position_embeddings=512, **common)
+    if kind == "smollm3":
+        return T.SmolLM3ForCausalLM, T.SmolLM3Config(hidden_size=128, intermediate_size=256, num_hidden_layers=4,
+                                                     num_attention_heads=2, num_key_value_heads=1,
+                                                     no_rope_layers=[1, 0, 1, 0], max_position_embeddings=512,
+                                                     **common)
     if kind == "arcee":
         return T.ArceeForCausalLM, T.ArceeConfig(hidden_size=128, intermediate_size=256, num_hidden_layers=3,
                                                  num_attention_heads=2, num_key_value_heads=1, hidden_act="relu2",
@@ -101,7 +120,8 @@ def _hf_model(kind: str, tmp_path):
 
 
 KINDS = ["opt", "opt_postln", "gptj", "falcon_7b", "falcon_40b", "falcon_rw", "stablelm", "stablelm_parallel",
-         "persimmon", "cohere", "glm", "glm4", "olmo2", "olmo", "arcee", "bloom", "mpt"]
+         "persimmon", "cohere", "glm", "glm4", "olmo2", "olmo", "arcee", "bloom", "mpt", "phi3", "phi3_longrope",
+         "granite", "smollm3"]
 
 
 @pytest.mark.parametrize("kind", KINDS)

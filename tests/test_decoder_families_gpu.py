@@ -46,3 +46,21 @@ def test_decoder_family_on_gpu(tmp_path, kind):
         seq = r.prompt_ids + r.output_ids
         top = m.compute_logits(_hidden_prefill(eng, seq[:-1])[-12:]).float().argmax(-1).cpu().tolist()
         assert sum(int(a == b) for a, b in zip(top, r.output_ids)) >= 10, (top, r.output_ids)
+
+
+@pytest.mark.parametrize("kind", ["internlm2", "qwen1", "mimo", "baichuan2", "exaone", "orion", "minicpm", "chatglm"])
+def test_remote_family_on_gpu(tmp_path, kind):
+    """Remote-code checkpoint layouts (``test_decoder_remote_families_cpu``) served in bf16."""
+    from tests.test_decoder_remote_families_cpu import IDS, _convert
+
+    hf = _convert(kind, tmp_path)
+    with torch.no_grad():
+        want = hf(torch.tensor([IDS])).logits[0].float()
+    eng = Engine(EngineArgs(model_path=str(tmp_path), device="cuda", max_running_requests=8, context_length=512))
+    m = eng.runner.model
+    got = m.compute_logits(_hidden_prefill(eng, IDS)).float().cpu()
+    cos = torch.nn.functional.cosine_similarity(got, want, dim=-1)
+    assert cos.min().item() > 0.995, cos.min().item()
+    r = eng.generate([IDS], SamplingParams(max_new_tokens=10, ignore_eos=True))[0]
+    top = m.compute_logits(_hidden_prefill(eng, (r.prompt_ids + r.output_ids)[:-1])[-10:]).float().argmax(-1)
+    assert sum(int(a == b) for a, b in zip(top.cpu().tolist(), r.output_ids)) >= 8
