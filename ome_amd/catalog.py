@@ -95,6 +95,19 @@ FAMILIES: list[Family] = [
     Family("glm-4-9b-chat", "zhipuai", "THUDM/glm-4-9b-chat-hf", "GlmForCausalLM", 9.4),
     Family("olmo-2-1124-7b-instruct", "allenai", "allenai/OLMo-2-1124-7B-Instruct", "Olmo2ForCausalLM", 7.3),
     Family("afm-4-5b-base", "arcee-ai", "arcee-ai/AFM-4.5B-Base", "ArceeForCausalLM", 4.6),
+    Family("bloomz-7b1", "bigscience", "bigscience/bloomz-7b1", "BloomForCausalLM", 7.1),
+    Family("mpt-7b", "mosaicml", "mosaicml/mpt-7b", "MPTForCausalLM", 6.7),
+    Family("internlm2-7b-reward", "internlm", "internlm/internlm2-7b-reward", "InternLM2ForRewardModel", 7.7,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("qwen-7b-chat", "qwen", "Qwen/Qwen-7B-Chat", "QWenLMHeadModel", 7.7),
+    Family("baichuan2-7b-chat", "baichuan-inc", "baichuan-inc/Baichuan2-7B-Chat", "BaichuanForCausalLM", 7.5),
+    Family("baichuan2-13b-chat", "baichuan-inc", "baichuan-inc/Baichuan2-13B-Chat", "BaichuanForCausalLM", 13.9),
+    Family("exaone-3-5-7-8b-instruct", "lgai-exaone", "LGAI-EXAONE/EXAONE-3.5-7.8B-Instruct", "ExaoneForCausalLM",
+           7.8),
+    Family("orion-14b-base", "orionstarai", "OrionStarAI/Orion-14B-Base", "OrionForCausalLM", 14.5),
+    Family("minicpm-2b-sft-bf16", "openbmb", "openbmb/MiniCPM-2B-sft-bf16", "MiniCPMForCausalLM", 2.7),
+    Family("chatglm2-6b", "thudm", "THUDM/chatglm2-6b", "ChatGLMModel", 6.2),
+    Family("mimo-7b-rl", "xiaomimimo", "XiaomiMiMo/MiMo-7B-RL", "MiMoForCausalLM", 7.8),
     Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
 ]

@@ -20,7 +20,7 @@ import torch
 PADDED_HEAD_ARCHS = {"OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM", "RWForCausalLM",
                      "StableLmForCausalLM", "PersimmonForCausalLM", "CohereForCausalLM", "GlmForCausalLM",
                      "Glm4ForCausalLM", "Olmo2ForCausalLM", "OlmoForCausalLM", "ArceeForCausalLM",
-                     "BloomForCausalLM", "MptForCausalLM", "Phi3ForCausalLM", "GraniteForCausalLM",
+                     "BloomForCausalLM", "MptForCausalLM", "MPTForCausalLM", "Phi3ForCausalLM", "GraniteForCausalLM",
                      "SmolLM3ForCausalLM", "InternLM2ForCausalLM", "InternLM2ForRewardModel", "Qwen2ForRewardModel",
                      "LlamaForSequenceClassification", "Qwen2ForSequenceClassification",
                      "MistralForSequenceClassification", "MiMoForCausalLM", "QWenLMHeadModel", "BaichuanForCausalLM",

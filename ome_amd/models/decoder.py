@@ -176,7 +176,7 @@ def _spec_for(cfg: ModelConfig) -> DecoderSpec:
                                (r"h\.(\d+)\.post_attention_layernorm\.(weight|bias)", r"L.\1.ln2.\2"),
                                (r"h\.(\d+)\.mlp\.dense_h_to_4h\.(weight|bias)", r"L.\1.fc.\2"),
                                (r"h\.(\d+)\.mlp\.dense_4h_to_h\.(weight|bias)", r"L.\1.down.\2")])
-    if arch == "MptForCausalLM":
+    if arch in ("MptForCausalLM", "MPTForCausalLM"):  # HF port and the mosaicml remote class: same names
         return DecoderSpec(norm="ln_nobias", mlp="plain", rope="none", qkv_layout="concat",
                            alibi="mpt" if (hf.get("attn_config") or {}).get("alibi", True) else "",
                            prefixes=("transformer.",), names=[
