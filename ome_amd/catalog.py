@@ -108,6 +108,13 @@ FAMILIES: list[Family] = [
     Family("minicpm-2b-sft-bf16", "openbmb", "openbmb/MiniCPM-2B-sft-bf16", "MiniCPMForCausalLM", 2.7),
     Family("chatglm2-6b", "thudm", "THUDM/chatglm2-6b", "ChatGLMModel", 6.2),
     Family("mimo-7b-rl", "xiaomimimo", "XiaomiMiMo/MiMo-7B-RL", "MiMoForCausalLM", 7.8),
+    Family("olmoe-1b-7b-0924", "allenai", "allenai/OLMoE-1B-7B-0924", "OlmoeForCausalLM", 6.9),
+    Family("granite-3-0-3b-a800m-instruct", "ibm-granite", "ibm-granite/granite-3.0-3b-a800m-instruct",
+           "GraniteMoeForCausalLM", 3.3),
+    Family("dbrx-instruct", "databricks", "databricks/dbrx-instruct", "DbrxForCausalLM", 132.0),
+    Family("ernie-4-5-21b-a3b-pt", "baidu", "baidu/ERNIE-4.5-21B-A3B-PT", "Ernie4_5_MoeForCausalLM", 21.8),
+    Family("minimax-m2", "minimax", "MiniMaxAI/MiniMax-M2", "MiniMaxM2ForCausalLM", 229.0, None, 1.0,
+           quantization="fp8"),
     Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
 ]

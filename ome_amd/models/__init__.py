@@ -50,6 +50,10 @@ def model_class(cfg: ModelConfig):
 
         return Llama4ForCausalLM
     if cfg.architecture in DECODER_ARCHS:
+        from ome_amd.models.decoder_moe import DECODER_MOE_ARCHS, DecoderMoEForCausalLM
+
+        if cfg.architecture in DECODER_MOE_ARCHS:
+            return DecoderMoEForCausalLM
         from ome_amd.models.decoder import DecoderForCausalLM
 
         return DecoderForCausalLM

@@ -25,7 +25,8 @@ PADDED_HEAD_ARCHS = {"OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM", "
                      "LlamaForSequenceClassification", "Qwen2ForSequenceClassification",
                      "MistralForSequenceClassification", "MiMoForCausalLM", "QWenLMHeadModel", "BaichuanForCausalLM",
                      "ExaoneForCausalLM", "OrionForCausalLM", "MiniCPMForCausalLM", "ChatGLMModel",
-                     "ChatGLMForConditionalGeneration"}
+                     "ChatGLMForConditionalGeneration", "OlmoeForCausalLM", "GraniteMoeForCausalLM", "DbrxForCausalLM",
+                     "Ernie4_5_MoeForCausalLM", "MiniMaxM2ForCausalLM"}
 # remote-code class names that end in "Model" but are causal LMs (not embedding models)
 CAUSAL_MODEL_CLASSES = {"ChatGLMModel", "QWenLMHeadModel", "TeleFLMModel"}
 
@@ -92,6 +93,22 @@ def _standard_keys(c: dict[str, Any]) -> dict[str, Any]:
         a = dict(attention_bias=c.get("bias", False))
     elif mt == "mimo":
         a = dict(attention_bias=True)
+    elif mt == "dbrx":
+        ac, fc = c.get("attn_config") or {}, c.get("ffn_config") or {}
+        a = dict(hidden_size=c.get("d_model"), num_attention_heads=c.get("n_heads"), num_hidden_layers=c.get("n_layers"),
+                 max_position_embeddings=c.get("max_seq_len"), num_key_value_heads=ac.get("kv_n_heads"),
+                 rope_theta=ac.get("rope_theta"), clip_qkv=ac.get("clip_qkv"),
+                 num_local_experts=fc.get("moe_num_experts"), num_experts_per_tok=fc.get("moe_top_k"),
+                 intermediate_size=fc.get("ffn_hidden_size"), moe_intermediate_size=fc.get("ffn_hidden_size"),
+                 norm_topk_prob=fc.get("moe_normalize_expert_weights") is not None, layer_norm_eps=1e-5,
+                 hidden_act=(fc.get("ffn_act_fn") or {}).get("name", "silu"), tie_word_embeddings=False)
+    elif mt == "ernie4_5_moe":
+        a = dict(num_experts=c.get("moe_num_experts"), num_experts_per_tok=c.get("moe_k"),
+                 attention_bias=c.get("use_bias", False), tie_word_embeddings=c.get("tie_word_embeddings", True))
+    elif mt == "minimax_m2":
+        hd = c.get("head_dim") or c.get("hidden_size", 3072) // c.get("num_attention_heads", 48)
+        a = dict(partial_rotary_factor=(c["rotary_dim"] / hd) if c.get("rotary_dim") else None,
+                 moe_intermediate_size=c.get("intermediate_size"))
     elif mt == "stablelm":
         a = dict(attention_bias=c.get("use_qkv_bias", False))
     elif mt == "persimmon":

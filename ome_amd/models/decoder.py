@@ -254,6 +254,22 @@ def _spec_for(cfg: ModelConfig) -> DecoderSpec:
             (r"encoder\.layers\.(\d+)\.self_attention\.dense\.weight", r"L.\1.o.weight"),
             (r"encoder\.layers\.(\d+)\.mlp\.dense_h_to_4h\.weight", r"L.\1.gate_up.weight"),
             (r"encoder\.layers\.(\d+)\.mlp\.dense_4h_to_h\.weight", r"L.\1.down.weight")])
+    if arch in ("OlmoeForCausalLM", "MiniMaxM2ForCausalLM"):  # full-width q/k RMSNorm + experts (decoder_moe.py)
+        return DecoderSpec(qk_norm="rms_full")
+    if arch == "GraniteMoeForCausalLM":
+        return DecoderSpec(embed_scale=float(hf.get("embedding_multiplier", 1.0)),
+                           residual_scale=float(hf.get("residual_multiplier", 1.0)),
+                           attn_scale=hf.get("attention_multiplier"),
+                           logit_mult=1.0 / float(hf.get("logits_scaling", 1.0)))
+    if arch == "Ernie4_5_MoeForCausalLM":
+        return DecoderSpec(rope="interleaved")
+    if arch == "DbrxForCausalLM":
+        return DecoderSpec(norm="ln_nobias", qkv_layout="concat", prefixes=("transformer.",), names=[
+            (r"wte\.weight", "embed"), (r"norm_f\.weight", "norm.weight"), (r"lm_head\.weight", "lm_head.weight"),
+            (r"blocks\.(\d+)\.norm_attn_norm\.norm_1\.weight", r"L.\1.ln1.weight"),
+            (r"blocks\.(\d+)\.norm_attn_norm\.norm_2\.weight", r"L.\1.ln2.weight"),
+            (r"blocks\.(\d+)\.norm_attn_norm\.attn\.Wqkv\.weight", r"L.\1.qkv.weight"),
+            (r"blocks\.(\d+)\.norm_attn_norm\.attn\.out_proj\.weight", r"L.\1.o.weight")])
     if arch == "OlmoForCausalLM":
         return DecoderSpec(norm="ln_noaffine")
     if arch == "ArceeForCausalLM":
@@ -415,13 +431,17 @@ class DecoderForCausalLM(LlamaForCausalLM):
                     self.ln1b[i], self.ln2b[i] = zeros(H), zeros(H)
             if sp.residual in ("sandwich", "post"):
                 self.post_attn[i], self.post_mlp[i] = self._alloc(H, std=None, gen=gen), self._alloc(H, std=None, gen=gen)
-            if sp.mlp == "gated":
+            if i in getattr(self, "moe_layers", ()):  # experts allocated by DecoderMoEForCausalLM
+                pass
+            elif sp.mlp == "gated":
                 self.w_gu[i] = self._alloc(2 * tp.inter, H, std=std, gen=gen)
             else:
                 self.w_fc[i] = self._alloc(tp.inter, H, std=std, gen=gen)
                 self.b_fc[i] = self._alloc(tp.inter, std=std, gen=gen) if bias else None
-            self.w_d[i] = self._alloc(H, tp.inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
-            self.b_d[i] = (self._alloc(H, std=std, gen=gen) if r0 else zeros(H)) if (bias and sp.mlp == "plain") else None
+            if i not in getattr(self, "moe_layers", ()):
+                self.w_d[i] = self._alloc(H, tp.inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+                self.b_d[i] = (self._alloc(H, std=std, gen=gen) if r0 else zeros(H)) if (bias and sp.mlp == "plain") \
+                    else None
             if sp.qk_norm == "rms_head":
                 self.qn[i], self.kn[i] = self._alloc(D, std=None, gen=gen), self._alloc(D, std=None, gen=gen)
             elif sp.qk_norm == "ln_head":
@@ -561,6 +581,19 @@ class DecoderForCausalLM(LlamaForCausalLM):
         self.w_o[i] = put(wo.narrow(1, tp.rank * tp.hq * D, tp.hq * D))
         if "o.bias" in p:
             self.b_o[i] = put(p["o.bias"]) if r0 else torch.zeros(H, dtype=self.dtype, device=self.device)
+        self._load_mlp(i, p, put)
+        for nm, wl, bl in (("ln1", self.ln1, self.ln1b), ("ln2", self.ln2, self.ln2b)):
+            if f"{nm}.weight" in p:
+                wl[i] = put(p[f"{nm}.weight"])
+            if f"{nm}.bias" in p:
+                bl[i] = put(p[f"{nm}.bias"])
+        if "post_attn.weight" in p:
+            self.post_attn[i], self.post_mlp[i] = put(p["post_attn.weight"]), put(p["post_mlp.weight"])
+        self._load_qk_norm(i, p, put)
+
+    def _load_mlp(self, i: int, p: dict, put) -> None:
+        tp, sp, H = self.tp, self.spec, self.cfg.hidden_size
+        r0 = tp.rank == 0
 
         def inter_rows(t):
             n = min(tp.inter, t.shape[0] - tp.rank * tp.inter)
@@ -580,14 +613,6 @@ class DecoderForCausalLM(LlamaForCausalLM):
         self.w_d[i] = put(wd.narrow(1, tp.rank * tp.inter, min(tp.inter, wd.shape[1] - tp.rank * tp.inter)))
         if "down.bias" in p:
             self.b_d[i] = put(p["down.bias"]) if r0 else torch.zeros(H, dtype=self.dtype, device=self.device)
-        for nm, wl, bl in (("ln1", self.ln1, self.ln1b), ("ln2", self.ln2, self.ln2b)):
-            if f"{nm}.weight" in p:
-                wl[i] = put(p[f"{nm}.weight"])
-            if f"{nm}.bias" in p:
-                bl[i] = put(p[f"{nm}.bias"])
-        if "post_attn.weight" in p:
-            self.post_attn[i], self.post_mlp[i] = put(p["post_attn.weight"]), put(p["post_mlp.weight"])
-        self._load_qk_norm(i, p, put)
 
     def _load_qk_norm(self, i: int, p: dict, put) -> None:
         cfg, tp, D, Dt, sp = self.cfg, self.tp, self.D, self.Dt, self.spec

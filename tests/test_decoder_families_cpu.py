@@ -94,6 +94,33 @@ def _cfg(kind: str):
                                                      num_attention_heads=2, num_key_value_heads=1,
                                                      no_rope_layers=[1, 0, 1, 0], max_position_embeddings=512,
                                                      **common)
+    if kind == "olmoe":
+        return T.OlmoeForCausalLM, T.OlmoeConfig(hidden_size=128, intermediate_size=64, num_hidden_layers=2,
+                                                 num_attention_heads=2, num_key_value_heads=2, num_experts=8,
+                                                 num_experts_per_tok=3, norm_topk_prob=False,
+                                                 max_position_embeddings=512, **common)
+    if kind == "granitemoe":
+        return T.GraniteMoeForCausalLM, T.GraniteMoeConfig(hidden_size=128, intermediate_size=64, num_hidden_layers=2,
+                                                           num_attention_heads=2, num_key_value_heads=1,
+                                                           num_local_experts=6, num_experts_per_tok=2,
+                                                           embedding_multiplier=4.0, residual_multiplier=0.4,
+                                                           attention_multiplier=0.06, logits_scaling=3.0,
+                                                           max_position_embeddings=512, **common)
+    if kind == "dbrx":
+        return T.DbrxForCausalLM, T.DbrxConfig(d_model=128, n_heads=2, n_layers=2, max_seq_len=512,
+                                               attn_config={"kv_n_heads": 1, "clip_qkv": 1.5, "rope_theta": 10000.0},
+                                               ffn_config={"ffn_hidden_size": 64, "moe_num_experts": 4, "moe_top_k": 2},
+                                               **common)
+    if kind == "ernie_moe":
+        return T.Ernie4_5_MoeForCausalLM, T.Ernie4_5_MoeConfig(
+            hidden_size=128, intermediate_size=192, num_hidden_layers=3, num_attention_heads=2, num_key_value_heads=1,
+            moe_intermediate_size=64, moe_num_experts=8, moe_k=2, moe_num_shared_experts=1, moe_layer_start_index=1,
+            moe_layer_end_index=2, max_position_embeddings=512, **common)
+    if kind == "minimax_m2":
+        return T.MiniMaxM2ForCausalLM, T.MiniMaxM2Config(hidden_size=128, intermediate_size=64, num_hidden_layers=2,
+                                                         num_attention_heads=2, num_key_value_heads=1, head_dim=64,
+                                                         num_local_experts=8, num_experts_per_tok=2,
+                                                         max_position_embeddings=512, **common)
     if kind == "arcee":
         return T.ArceeForCausalLM, T.ArceeConfig(hidden_size=128, intermediate_size=256, num_hidden_layers=3,
                                                  num_attention_heads=2, num_key_value_heads=1, hidden_act="relu2",
@@ -106,8 +133,15 @@ def _hf_model(kind: str, tmp_path):
     cls, cfg = _cfg(kind)
     m = cls(cfg)
     with torch.no_grad():
+        for n, b in m.named_buffers():
+            if n.endswith("e_score_correction_bias"):  # exercise the selection-only router bias
+                b.copy_(torch.randn_like(b.float()) * 0.05)
         for n, p in m.named_parameters():
-            if ("norm" in n or "ln" in n.split(".")[-2]) and n.endswith("weight"):
+            if n.endswith("e_score_correction_bias"):
+                p.copy_(torch.randn_like(p) * 0.05)
+            elif kind == "dbrx" and "router" in n:  # well-separated routing: bf16 must not flip experts
+                p.normal_(0.0, 1.0)
+            elif ("norm" in n or "ln" in n.split(".")[-2]) and n.endswith("weight"):
                 p.normal_(1.0, 0.2)
             elif p.dim() == 2:
                 p.normal_(0.0, 0.08)
@@ -121,7 +155,7 @@ def _hf_model(kind: str, tmp_path):
 
 KINDS = ["opt", "opt_postln", "gptj", "falcon_7b", "falcon_40b", "falcon_rw", "stablelm", "stablelm_parallel",
          "persimmon", "cohere", "glm", "glm4", "olmo2", "olmo", "arcee", "bloom", "mpt", "phi3", "phi3_longrope",
-         "granite", "smollm3"]
+         "granite", "smollm3", "olmoe", "granitemoe", "dbrx", "ernie_moe", "minimax_m2"]
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -133,7 +167,7 @@ def test_decoder_family_matches_hf(tmp_path, kind):
     eng = Engine(EngineArgs(model_path=str(tmp_path), device="cpu", dtype="float32", max_running_requests=4,
                             context_length=256))
     m = eng.runner.model
-    assert type(m).__name__ == "DecoderForCausalLM"
+    assert type(m).__name__ in ("DecoderForCausalLM", "DecoderMoEForCausalLM")
     if kind.startswith("stablelm"):
         assert m.D == 128 and m.Dt == 80 and m.rot_true == 20 and m.rot_k == 32 and m.perm is not None
     got = _our_logits(eng, ids)
