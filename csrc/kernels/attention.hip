@@ -307,7 +307,7 @@ __device__ __forceinline__ void kv_tile_load(KVTile<D, F>& t, const typename KVS
   }
 }
 
-template <int D, int F>
+template <int D, int F, bool AL = false>
 __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf16x8 (&qf)[D / 32],
                                                 f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
                                                 int lo, Scaler scl, int g, float al, int qpos) {
@@ -321,8 +321,8 @@ __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf1
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k0 = kb + 4 * g + i, k1 = k0 + 16;
-    s0[i] = (k0 < p_end && k0 >= lo) ? scl(s0[i]) + al * (float)(k0 - qpos) : OME_NEG_INF;
-    s1[i] = (k1 < p_end && k1 >= lo) ? scl(s1[i]) + al * (float)(k1 - qpos) : OME_NEG_INF;
+    s0[i] = (k0 < p_end && k0 >= lo) ? (AL ? scl(s0[i]) + al * (float)(k0 - qpos) : scl(s0[i])) : OME_NEG_INF;
+    s1[i] = (k1 < p_end && k1 >= lo) ? (AL ? scl(s1[i]) + al * (float)(k1 - qpos) : scl(s1[i])) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
   mt = fmaxf(mt, __shfl_xor(mt, 16));
@@ -380,7 +380,7 @@ __device__ __forceinline__ void kv_tilep_load(KVTileP<D, F>& t, const typename K
   for (int nb = 0; nb < D / 16; ++nb) t.v[nb] = k8_load<F>(vp + (16 * nb + n) * P);
 }
 
-template <int D, int F>
+template <int D, int F, bool AL = false>
 __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const bf16x8 (&qf)[D / 32],
                                                  f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
                                                  int lo, Scaler scl, int g, float al, int qpos) {
@@ -395,8 +395,8 @@ __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const b
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k0 = base + i, k1 = k0 + 4;
-    s0[i] = (k0 < p_end && k0 >= lo) ? scl(s0[i]) + al * (float)(k0 - qpos) : OME_NEG_INF;
-    s1[i] = (k1 < p_end && k1 >= lo) ? scl(s1[i]) + al * (float)(k1 - qpos) : OME_NEG_INF;
+    s0[i] = (k0 < p_end && k0 >= lo) ? (AL ? scl(s0[i]) + al * (float)(k0 - qpos) : scl(s0[i])) : OME_NEG_INF;
+    s1[i] = (k1 < p_end && k1 >= lo) ? (AL ? scl(s1[i]) + al * (float)(k1 - qpos) : scl(s1[i])) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
   mt = fmaxf(mt, __shfl_xor(mt, 16));
@@ -424,7 +424,7 @@ __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const b
   }
 }
 
-template <int D, int P, int MODE, int F>
+template <int D, int P, int MODE, int F, bool AL = false>
 __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -473,13 +473,13 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     for (; kb < p_end; kb += 128) {
       KVTileP<D, F> t;
       kv_tilep_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tilep_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
+      kv_tilep_compute<D, F, AL>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
     }
   } else if (MODE == 0) {
     for (; kb < p_end; kb += 128) {
       KVTile<D, F> t;
       kv_tile_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
+      kv_tile_compute<D, F, AL>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
     }
   } else if (kb < p_end) {
     KVTile<D, F> t0, t1;
@@ -488,12 +488,12 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
       const int kn = kb + 128;
       const bool more = kn < p_end;
       if (more) kv_tile_load<D, P, F>(t1, k_cache, v_cache, bt, kn, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t0, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
+      kv_tile_compute<D, F, AL>(t0, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
       if (!more) break;
       const int kn2 = kn + 128;
       const bool more2 = kn2 < p_end;
       if (more2) kv_tile_load<D, P, F>(t0, k_cache, v_cache, bt, kn2, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F>(t1, qf, o, m_i, l_i, kn, p_end, lo, scl, g, al, qpos);
+      kv_tile_compute<D, F, AL>(t1, qf, o, m_i, l_i, kn, p_end, lo, scl, g, al, qpos);
       if (!more2) break;
       kb = kn2;
     }
@@ -547,9 +547,12 @@ static void launch_decode_v2(int variant, dim3 grid, size_t smem, hipStream_t st
                              int bt_stride, const int* seq_lens, void* out, int64_t out_stride, void* part_o,
                              void* part_ml, int Hq, int Hkv, int part_size, int max_parts, Scaler scl,
                              int window, const int* order, float v_scale, const float* sinks) {
-  auto kern = variant == 2   ? paged_decode_v2_kernel<D, 16, 1, F>
-              : variant == 4 ? paged_decode_v2_kernel<D, 16, 2, F>
-                             : paged_decode_v2_kernel<D, 16, 0, F>;
+  // ALiBi (Bloom / MPT) runs the key-permuted variant only, compiled with the bias term; the
+  // other instantiations carry no trace of it
+  auto kern = scl.alibi != nullptr ? paged_decode_v2_kernel<D, 16, 2, F, true>
+              : variant == 2       ? paged_decode_v2_kernel<D, 16, 1, F>
+              : variant == 4       ? paged_decode_v2_kernel<D, 16, 2, F>
+                                   : paged_decode_v2_kernel<D, 16, 0, F>;
   kern<<<grid, 256, smem, stream>>>((const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache,
                                     (const typename KVStore<F>::T*)v_cache, block_tables, bt_stride, seq_lens,
                                     (bf16*)out, out_stride, (float*)part_o, (float*)part_ml, Hq, Hkv, part_size,
