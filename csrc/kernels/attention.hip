@@ -46,6 +46,8 @@ struct Scaler {
   float cap_l2;   // cap * log2(e)
   const float* alibi;  // ALiBi slopes per query head (Bloom / MPT / Falcon-RW), nullptr = off: the
                        // logit gains slope * (key_pos - query_pos), i.e. alibi_l2(head) * (k - q)
+  const int* row_lo;   // decode only: per-row first visible key (nullptr = 0) -- Mllama cross
+                       // attention reads one [lo, seq_len) range of a request's vision-token cache
   __device__ __forceinline__ float alibi_l2(int head) const {
     return alibi != nullptr ? alibi[head] * 1.4426950408889634f : 0.f;
   }
@@ -62,6 +64,7 @@ static inline Scaler make_scaler(float scale, float softcap, const float* alibi 
   const float l2e = 1.4426950408889634f;
   Scaler r;
   r.alibi = alibi;
+  r.row_lo = nullptr;
   r.mul = scale * l2e;
   r.cap_inv = softcap > 0.f ? scale / softcap : 0.f;
   r.cap_l2 = softcap > 0.f ? softcap * l2e : 0.f;
@@ -443,7 +446,7 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
   const int G = Hq / Hkv;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n = lane & 15, g = lane >> 4;
-  const int lo = attn_lo(seq_len - 1, window);
+  const int lo = scl.row_lo != nullptr ? max(attn_lo(seq_len - 1, window), scl.row_lo[b]) : attn_lo(seq_len - 1, window);
   const float al = n < G ? scl.alibi_l2(kvh * G + n) : 0.f;  // this lane's query head (S^T column n)
   const int qpos = seq_len - 1;
 
@@ -591,19 +594,20 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
                              int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
                              int part_size, int max_parts, float scale, int window, const int* order, int kv_fmt,
                              float k_scale, float v_scale, float softcap, const float* sinks, const float* alibi,
-                             hipStream_t stream) {
+                             const int* row_lo, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
   if (part_size % 128 != 0 || max_parts <= 0) return -4;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
-  const Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
+  Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
+  scl.row_lo = row_lo;
   dim3 grid(max_parts, Hkv, B);
   // A/B switch for benchmarking: 1 = v1, 2 = v2 (register ring), 3 = v2 without ring, 4 = v3 with
   // key-permuted tiles (16-B V loads; default: 5.38 vs 5.24 TB/s on the bench's context mix)
   const char* ve = getenv("OME_DECODE_ATTN");
   int variant = ve ? atoi(ve) : 4;
-  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks || alibi)) variant = 4;  // v1: plain bf16 D=128
+  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks || alibi || row_lo)) variant = 4;  // v1: plain bf16 D=128
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
     paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(

@@ -49,6 +49,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.llama4 import Llama4ForCausalLM
 
         return Llama4ForCausalLM
+    if cfg.architecture == "MllamaForConditionalGeneration" or cfg.model_type == "mllama":
+        from ome_amd.models.mllama import MllamaForConditionalGeneration
+
+        return MllamaForConditionalGeneration
     if cfg.architecture in DECODER_ARCHS:
         from ome_amd.models.decoder_moe import DECODER_MOE_ARCHS, DecoderMoEForCausalLM
 
@@ -76,7 +80,7 @@ def model_class(cfg: ModelConfig):
 
 def supported(arch: str) -> bool:
     return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or arch in NEMOTRON_H_ARCHS or \
-        arch in DECODER_ARCHS or \
+        arch in DECODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
         arch == "GptOssForCausalLM"
 
 

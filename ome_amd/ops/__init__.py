@@ -337,14 +337,15 @@ class DecodeWorkspace:
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeWorkspace | None = None,
                  window: int = -1, out=None, order: torch.Tensor | None = None, k_scale: float = 1.0,
                  v_scale: float = 1.0, softcap: float = 0.0, sinks: torch.Tensor | None = None,
-                 alibi: torch.Tensor | None = None) -> torch.Tensor:
+                 alibi: torch.Tensor | None = None, row_lo: torch.Tensor | None = None) -> torch.Tensor:
     """q [B, Hq, D] -> [B, Hq, D].  ``alibi``: fp32 [Hq] ALiBi slopes (logit += slope * (key - query
-    position)), or None.  ``order`` (int32 [B], optional): sequence visit order for the
+    position)), or None.  ``row_lo``: int32 [B], row b attends keys [row_lo[b], seq_lens[b]) only
+    (Mllama cross attention over a range of a request's vision-token cache).  ``order`` (int32 [B], optional): sequence visit order for the
     workgroup dispatcher (longest first balances the tail).  The cache may be bf16 or fp8
     (``k_scale`` / ``v_scale`` dequantise it)."""
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window, k_scale, v_scale, softcap,
-                             sinks, alibi)
+                             sinks, alibi, row_lo)
         if out is not None:
             out.copy_(r)
             return out
@@ -358,7 +359,8 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeW
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(seq_lens).data_ptr(), out.data_ptr(),
          out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
          float(scale), int(window), _i32(order).data_ptr() if order is not None else None, kv_format(k_cache),
-         float(k_scale), float(v_scale), float(softcap), _sinks(sinks), _sinks(alibi), stream_ptr())
+         float(k_scale), float(v_scale), float(softcap), _sinks(sinks), _sinks(alibi),
+         _i32(row_lo).data_ptr() if row_lo is not None else None, stream_ptr())
     return out
 
 

@@ -204,7 +204,7 @@ def attn_lo(qpos, window: int):
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, k_scale=1.0,
-                 v_scale=1.0, softcap=0.0, sinks=None, alibi=None) -> torch.Tensor:
+                 v_scale=1.0, softcap=0.0, sinks=None, alibi=None, row_lo=None) -> torch.Tensor:
     B, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -214,6 +214,8 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, 
         if L <= 0:
             continue
         lo = int(attn_lo(torch.tensor(L - 1), window))
+        if row_lo is not None:
+            lo = max(lo, int(row_lo[b]))
         for h in range(Hkv):
             k, v = gather_kv(k_cache, v_cache, block_tables[b], L, h, P, k_scale, v_scale)
             k, v = k[lo:], v[lo:]

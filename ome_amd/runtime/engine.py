@@ -160,6 +160,9 @@ class Engine:
         m = self.runner.model
         if not getattr(m, "is_multimodal", False):
             raise ValueError(f"{self.cfg.architecture} does not accept image inputs")
+        if hasattr(m, "make_mm_input"):  # model-specific inputs (Mllama: tiles + cross-attention ranges)
+            ids, mm = m.make_mm_input(list(prompt_ids), images)
+            return self.make_request(ids, params, mm=mm, **kw)
         pvs, grids = [], []
         for im in images:
             if isinstance(im, tuple):

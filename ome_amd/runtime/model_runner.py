@@ -477,7 +477,10 @@ class ModelRunner:
             S_ = len(lens)
             meta.extra["ssm"] = (pk[:S_ + 1], pk[S_ + 1:2 * S_ + 1], pk[2 * S_ + 1:])
         embeds = None
-        if getattr(self.model, "is_multimodal", False) and any(chunks[i].req.mm is not None for i in pre + dec):
+        if hasattr(self.model, "prepare_chunks"):  # e.g. Mllama: vision tower + vision-token cache at first chunks
+            self.model.prepare_chunks([chunks[i] for i in pre + dec])
+        if getattr(self.model, "is_multimodal", False) and not getattr(self.model, "mm_cross", False) and \
+                any(chunks[i].req.mm is not None for i in pre + dec):
             embeds = self._mm_prepare(chunks, pre + dec, T, t_ids, meta)
         hidden = self.model.forward(t_ids, meta, self.kv, embeds)
         if hidden is None:  # an earlier pipeline stage: tokens arrive from the last stage

@@ -123,6 +123,10 @@ class Scheduler:
                 self.pages.free([p for p in req.pages if self.prefix_cache is None or not self.prefix_cache.owns(p)])
             req.pages = []
         if req.req_slot >= 0:
+            rel = getattr(req.mm, "release", None)
+            if rel is not None:  # model-owned per-request state (Mllama vision-token cache)
+                rel()
+                req.mm.release = None
             self.slots.free(req.req_slot)
             req.req_slot = -1
         req.pen_init = False

@@ -264,7 +264,8 @@ def create_app(engine, ns=None):
             for k, seg in enumerate(segs):
                 ids.extend(tok.encode(seg) if seg else [])
                 if k + 1 < len(segs):
-                    ids.extend([m.vision_start_id, m.image_token_id, m.vision_end_id])
+                    ids.extend(m.image_prompt_ids() if hasattr(m, "image_prompt_ids") else
+                               [m.vision_start_id, m.image_token_id, m.vision_end_id])
             return ids, images
         p = body.get("prompt", body.get("text"))
         images = list(body.get("image_data") or [])  # SGLang /generate spelling
