@@ -135,6 +135,8 @@ __global__ __launch_bounds__(256) void pool_kernel(const bf16* __restrict__ hidd
     float v = 0.f;
     if (mode == 0) {
       v = (float)hidden[(int64_t)(e - 1) * H + d];
+    } else if (mode == 2) {  // first token (CLS pooling: BERT / XLM-RoBERTa encoders)
+      v = (float)hidden[(int64_t)b * H + d];
     } else {
       for (int t = b; t < e; ++t) v += (float)hidden[(int64_t)t * H + d];
       v /= (float)(e - b > 0 ? e - b : 1);

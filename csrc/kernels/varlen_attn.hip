@@ -1,0 +1,224 @@
+// ome_amd — varlen attention over contiguous (non-paged) Q/K/V for encoder models and vision
+// towers: BERT / XLM-RoBERTa embedders and rerankers, the Qwen2-VL / Mllama ViTs.  SURVEY.md
+// §2.9 K14 (embedding serving) and the multimodal towers behind the reference's VLM runtimes
+// (e.g. config/runtimes/srt/BAAI/bge-m3-rt.yaml, .../Qwen/Qwen2.5-VL-7B-Instruct-rt.yaml).
+//
+// Sequences are packed back to back ([T, H, D] rows, any per-token stride so a fused QKV GEMM
+// output is read in place) and delimited by cu_seqlens.  Bidirectional by default (encoders,
+// ViT windows), causal on request.
+//
+// One workgroup = (128-query-row item of one sequence, one query head); its 4 waves own 32 rows
+// each and share every 32-key K/V tile through double-buffered LDS:
+//   K  [32 keys][DP + 8]  (272 B rows for DP = 128: 16 rows start on distinct bank quads)
+//   V^T[DP dims][32 + 8]  keys in the k-slot order of the S^T accumulators, so a lane's A
+//                         fragment of O^T = V^T P^T is one 16-B ds_read.
+// S^T = K Q^T and O^T = V^T P^T run on v_mfma_f32_16x16x32_bf16 with the online softmax in
+// registers (exp2 domain).  Head dims that are not a multiple of 32 (ViT-H 80) are zero-padded
+// to DP inside the kernel: padded dims contribute 0 to QK^T and are never stored.
+#include "common.h"
+
+#define VA_NEG_INF (-__builtin_inff())
+
+namespace {
+
+__device__ __forceinline__ f32x4 va_mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float va_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// k-slot of key kk (0..31) in an S^T accumulator pair: lane group g holds keys 4g..4g+3 (X = 0)
+// and 16+4g..16+4g+3 (X = 1) as slots 8g..8g+7
+__device__ __forceinline__ int va_slot(int kk) { return 8 * ((kk & 15) >> 2) + (kk & 3) + ((kk >> 4) << 2); }
+
+template <int DP>
+__global__ __launch_bounds__(256) void varlen_attn_kernel(
+    const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k, int64_t k_stride,
+    const bf16* __restrict__ v, int64_t v_stride, const int* __restrict__ cu, const int2* __restrict__ items,
+    bf16* __restrict__ out, int64_t o_stride, int Hq, int Hkv, int D, float scale_log2, int causal) {
+  constexpr int KS = DP / 32, NB = DP / 16, KLD = DP + 8, VLD = 32 + 8, CPR = DP / 8;
+  constexpr int KCH = 32 * CPR;                       // 16-B chunks per 32-key tile (per operand)
+  constexpr int NCH = (KCH + 255) / 256;              // chunks per thread
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 32 * KLD + 2 * DP * VLD];
+  bf16* sK = smem;                 // [2][32 * KLD]
+  bf16* sV = smem + 2 * 32 * KLD;  // [2][DP * VLD]
+
+  const int2 it = items[blockIdx.x];
+  const int s = it.x, r0_item = it.y;
+  const int head = blockIdx.y, kvh = head / (Hq / Hkv);
+  const int t0 = cu[s], L = cu[s + 1] - t0;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int n = lane & 15, g = lane >> 4;
+  const int r0 = r0_item + 32 * wave;
+  const int kv_end = causal ? min(L, r0_item + 128) : L;
+
+  // ---- this wave's query fragments (rows r0..r0+31), zero past L and past D ----
+  bf16x8 qf[2][KS];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int r = r0 + 16 * rb + n;
+    const bf16* qr = q + (int64_t)(t0 + r) * q_stride + (int64_t)head * D;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int d0 = 32 * ks + 8 * g;
+      qf[rb][ks] = (r < L && d0 < D) ? ld8(qr + d0) : bf16x8{};
+    }
+  }
+  float m_i[2] = {VA_NEG_INF, VA_NEG_INF}, l_i[2] = {0.f, 0.f};
+  f32x4 o[2][NB];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) o[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 rk[NCH], rv[NCH];
+  auto load_tile = [&](int kb) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + 256 * i;
+      const int key = c / CPR, d0 = (c % CPR) * 8;
+      const bool ok = c < KCH && kb + key < L && d0 < D;
+      const int64_t row = (int64_t)(t0 + kb + key);
+      rk[i] = ok ? ld8(k + row * k_stride + (int64_t)kvh * D + d0) : bf16x8{};
+      rv[i] = ok ? ld8(v + row * v_stride + (int64_t)kvh * D + d0) : bf16x8{};
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int c = tid + 256 * i;
+      if (c < KCH) {
+        const int key = c / CPR, d0 = (c % CPR) * 8;
+        *reinterpret_cast<bf16x8*>(&sK[buf * 32 * KLD + key * KLD + d0]) = rk[i];
+        bf16* vt = &sV[buf * DP * VLD + va_slot(key)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) vt[(d0 + j) * VLD] = rv[i][j];
+      }
+    }
+  };
+
+  const bool active = r0 < L;
+  int buf = 0;
+  if (kv_end > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+  for (int kb = 0; kb < kv_end; kb += 32) {
+    const bool more = kb + 32 < kv_end;
+    if (more) load_tile(kb + 32);  // in flight while this tile is consumed from LDS
+    if (active && (!causal || kb <= r0 + 31)) {
+      const bf16* Kt = sK + buf * 32 * KLD;
+      const bf16* Vt = sV + buf * DP * VLD;
+      f32x4 sc[2][2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) sc[rb][0] = sc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&Kt[n * KLD + 32 * ks + 8 * g]);
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&Kt[(16 + n) * KLD + 32 * ks + 8 * g]);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          sc[rb][0] = va_mfma(a0, qf[rb][ks], sc[rb][0]);
+          sc[rb][1] = va_mfma(a1, qf[rb][ks], sc[rb][1]);
+        }
+      }
+      const bool need_mask = kb + 32 > L || (causal && kb + 32 > r0 + 1);
+      bf16x8 pb[2];
+      float alpha[2];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int qpos = r0 + 16 * rb + n;
+        float mt = VA_NEG_INF;
+#pragma unroll
+        for (int X = 0; X < 2; ++X)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float val = sc[rb][X][i] * scale_log2;
+            if (need_mask) {
+              const int key = kb + 16 * X + 4 * g + i;
+              const bool ok = key < L && (!causal || key <= qpos);
+              val = ok ? val : VA_NEG_INF;
+            }
+            sc[rb][X][i] = val;
+            mt = fmaxf(mt, val);
+          }
+        mt = fmaxf(mt, __shfl_xor(mt, 16));
+        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        const float m_new = fmaxf(m_i[rb], mt);
+        const float m_use = (m_new == VA_NEG_INF) ? 0.f : m_new;
+        alpha[rb] = va_exp2(m_i[rb] - m_use);
+        float rs = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p0 = va_exp2(sc[rb][0][i] - m_use), p1 = va_exp2(sc[rb][1][i] - m_use);
+          pb[rb][i] = (bf16)p0;
+          pb[rb][4 + i] = (bf16)p1;
+          rs += p0 + p1;
+        }
+        rs += __shfl_xor(rs, 16);
+        rs += __shfl_xor(rs, 32);
+        l_i[rb] = l_i[rb] * alpha[rb] + rs;
+        m_i[rb] = m_new;
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Vt[(16 * nb + n) * VLD + 8 * g]);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          o[rb][nb] = o[rb][nb] * alpha[rb];
+          o[rb][nb] = va_mfma(a, pb[rb], o[rb][nb]);
+        }
+      }
+    }
+    if (more) store_tile(buf ^ 1);  // the other buffer was last read before the previous barrier
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (!active) return;
+  // ---- epilogue: O^T accumulators hold O[row n][dims 16nb + 4g .. +3] ----
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int r = r0 + 16 * rb + n;
+    if (r < L) {
+      const float inv = l_i[rb] > 0.f ? 1.f / l_i[rb] : 0.f;
+      bf16* orow = out + (int64_t)(t0 + r) * o_stride + (int64_t)head * D;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        if (16 * nb < D) {
+          bf16x4 w;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) w[i] = (bf16)(o[rb][nb][i] * inv);
+          *reinterpret_cast<bf16x4*>(orow + 16 * nb + 4 * g) = w;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// items: int2 (sequence, first row) per 128-row work item, n_items of them (host-built).
+// Strides are in elements per token; head h of a token starts at h * D.  D % 16 == 0, D <= 128;
+// every pointer and stride 16-B aligned.
+OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k, int64_t k_stride, const void* v,
+                                 int64_t v_stride, const int* cu, const int* items, int n_items, void* out,
+                                 int64_t o_stride, int Hq, int Hkv, int D, float scale, int causal,
+                                 hipStream_t stream) {
+  if (n_items <= 0) return 0;
+  if (D <= 0 || D > 128 || D % 16 != 0) return -2;
+  if (Hkv <= 0 || Hq % Hkv != 0) return -3;
+  if ((q_stride | k_stride | v_stride | o_stride) % 8 != 0) return -4;
+  if (Hq > 65535) return -5;
+  const float sl2 = scale * 1.4426950408889634f;
+  dim3 grid(n_items, Hq);
+#define ARGS                                                                                                  \
+  (const bf16*)q, q_stride, (const bf16*)k, k_stride, (const bf16*)v, v_stride, cu, (const int2*)items,       \
+      (bf16*)out, o_stride, Hq, Hkv, D, sl2, causal
+  if (D <= 64) varlen_attn_kernel<64><<<grid, 256, 0, stream>>>(ARGS);
+  else if (D <= 96) varlen_attn_kernel<96><<<grid, 256, 0, stream>>>(ARGS);
+  else varlen_attn_kernel<128><<<grid, 256, 0, stream>>>(ARGS);
+#undef ARGS
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -119,6 +119,12 @@ FAMILIES: list[Family] = [
     Family("ernie-4-5-21b-a3b-pt", "baidu", "baidu/ERNIE-4.5-21B-A3B-PT", "Ernie4_5_MoeForCausalLM", 21.8),
     Family("minimax-m2", "minimax", "MiniMaxAI/MiniMax-M2", "MiniMaxM2ForCausalLM", 229.0, None, 1.0,
            quantization="fp8"),
+    Family("bge-large-en-v1-5", "baai", "BAAI/bge-large-en-v1.5", "BertModel", 0.335,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("bge-m3", "baai", "BAAI/bge-m3", "XLMRobertaModel", 0.568,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("bge-reranker-v2-m3", "baai", "BAAI/bge-reranker-v2-m3", "XLMRobertaForSequenceClassification", 0.568,
+           capabilities=["TEXT_RERANK"], args=["--is-embedding"]),
     Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
 ]

@@ -24,6 +24,8 @@ QWEN2_VL_ARCHS = {"Qwen2VLForConditionalGeneration"}
 NEMOTRON_H_ARCHS = {"NemotronHForCausalLM"}
 from ome_amd.models.config import PADDED_HEAD_ARCHS as DECODER_ARCHS  # noqa: E402  (models/decoder.py)
 
+ENCODER_ARCHS = {"BertModel", "BertForSequenceClassification", "RobertaModel", "RobertaForSequenceClassification",
+                 "XLMRobertaModel", "XLMRobertaForSequenceClassification"}  # models/bert.py
 MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM", "DeepseekV2ForCausalLM",
              "DeepseekV3ForCausalLM", "PhiMoEForCausalLM"}
 
@@ -53,6 +55,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.mllama import MllamaForConditionalGeneration
 
         return MllamaForConditionalGeneration
+    if cfg.architecture in ENCODER_ARCHS:
+        from ome_amd.models.bert import EncoderModel
+
+        return EncoderModel
     if cfg.architecture in DECODER_ARCHS:
         from ome_amd.models.decoder_moe import DECODER_MOE_ARCHS, DecoderMoEForCausalLM
 
@@ -80,7 +86,7 @@ def model_class(cfg: ModelConfig):
 
 def supported(arch: str) -> bool:
     return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or arch in NEMOTRON_H_ARCHS or \
-        arch in DECODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
+        arch in DECODER_ARCHS or arch in ENCODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
         arch == "GptOssForCausalLM"
 
 

@@ -278,6 +278,9 @@ class ModelConfig:
             c.quantization = q.get("quant_method") or q.get("quant_type")
         c.is_embedding = ("Embedding" in arch) or arch.endswith(("ForSequenceClassification", "RewardModel")) or \
             (arch.endswith("Model") and "ForCausalLM" not in arch and arch not in CAUSAL_MODEL_CLASSES)
+        if mt in ("roberta", "xlm-roberta") and c.max_position_embeddings > 2:
+            # positions start at padding_idx + 1: the usable length is that much shorter
+            c.max_position_embeddings -= int(text.get("pad_token_id", 1)) + 1
         c.extra = {k: v for k, v in cfg.items() if k not in ("text_config",)}
         if text is not cfg:  # multimodal wrappers: the language model's keys win
             c.extra.update({k: v for k, v in text.items() if k != "quantization_config"})

@@ -115,12 +115,8 @@ class Qwen2VisionTower:
             h = self._ln(x, p + "norm1")
             qkv = linear(h, self.w[p + "attn.qkv.weight"], self.w[p + "attn.qkv.bias"]).view(N, 3, Hh, D)
             q, k, v = rope(qkv[:, 0]), rope(qkv[:, 1]), qkv[:, 2]
-            outs, s = [], 0
-            for n in lens:  # bidirectional attention within each image / frame
-                qs, ks, vs = (t[s:s + n].transpose(0, 1)[None] for t in (q, k, v))
-                outs.append(F.scaled_dot_product_attention(qs, ks, vs)[0].transpose(0, 1))
-                s += n
-            a = torch.cat(outs, 0).reshape(N, E)
+            # bidirectional attention within each image / frame: one varlen MFMA launch
+            a = ops.varlen_attention(q, k, v, lens, D ** -0.5).reshape(N, E)
             x = x + linear(a, self.w[p + "attn.proj.weight"], self.w[p + "attn.proj.bias"])
             h = self._ln(x, p + "norm2")
             f = linear(h, self.w[p + "mlp.fc1.weight"], self.w[p + "mlp.fc1.bias"])

@@ -450,6 +450,38 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     return out
 
 
+def varlen_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lengths: list[int], scale: float,
+                     causal: bool = False, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Attention over packed variable-length sequences with contiguous (non-paged) K/V: encoder
+    models and vision towers.  q [T, Hq, D], k / v [T, Hkv, D] -- any per-token stride (views of a
+    fused QKV projection are read in place), head dim contiguous; ``lengths``: the host-side
+    sequence lengths (sum == T).  Bidirectional unless ``causal``."""
+    T, Hq, D = q.shape
+    Hkv = k.shape[1]
+    if not _gpu(q):
+        r = ref.varlen_attention(q, k, v, lengths, scale, causal)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    for t in (q, k, v):
+        assert t.dtype == torch.bfloat16 and t.stride(-1) == 1 and t.stride(-2) == D, "head-contiguous bf16 rows"
+    assert sum(lengths) == T, (sum(lengths), T)
+    out = torch.empty(T, Hq, D, dtype=q.dtype, device=q.device) if out is None else out
+    cu, items = [0], []
+    for s, n in enumerate(lengths):
+        cu.append(cu[-1] + n)
+        items.extend((s, r) for r in range(0, n, 128))
+    if not items:
+        return out
+    # items (int2, 8-B aligned) first, then cu_seqlens
+    meta = torch.tensor([x for it in items for x in it] + cu, dtype=torch.int32).to(q.device, non_blocking=True)
+    call("ome_varlen_attention", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
+         meta[2 * len(items):].data_ptr(), meta.data_ptr(), len(items), out.data_ptr(), out.stride(0), Hq, Hkv, D,
+         float(scale), int(bool(causal)), stream_ptr())
+    return out
+
+
 def sample(logits: torch.Tensor, temperature=None, top_k=None, top_p=None, min_p=None, seeds=None, step: int = 0,
            out_ids=None, out_logprob=None):
     """Returns (ids int32 [B], logprobs f32 [B])."""

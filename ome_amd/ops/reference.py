@@ -304,12 +304,29 @@ def sample(logits, temperature=None, top_k=None, top_p=None, min_p=None, generat
     return ids, lps
 
 
+def varlen_attention(q, k, v, lengths, scale, causal=False) -> torch.Tensor:
+    T, Hq, D = q.shape
+    G = Hq // k.shape[1]
+    out = torch.empty(T, Hq, D, dtype=q.dtype, device=q.device)
+    t0 = 0
+    for n in lengths:
+        qs = q[t0:t0 + n].float().transpose(0, 1)
+        ks = k[t0:t0 + n].float().repeat_interleave(G, 1).transpose(0, 1)
+        vs = v[t0:t0 + n].float().repeat_interleave(G, 1).transpose(0, 1)
+        s = (qs @ ks.transpose(1, 2)) * scale
+        if causal:
+            s = s.masked_fill(torch.ones(n, n, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
+        out[t0:t0 + n] = (s.softmax(-1) @ vs).transpose(0, 1).to(q.dtype)
+        t0 += n
+    return out
+
+
 def pool(hidden, cu_lens, mode: int = 0, normalize: bool = True) -> torch.Tensor:
     S = len(cu_lens) - 1
     outs = []
     for s in range(S):
         b, e = int(cu_lens[s]), int(cu_lens[s + 1])
-        h = hidden[e - 1].float() if mode == 0 else hidden[b:e].float().mean(0)
+        h = hidden[e - 1].float() if mode == 0 else hidden[b].float() if mode == 2 else hidden[b:e].float().mean(0)
         outs.append(h)
     out = torch.stack(outs)
     if normalize:

@@ -111,7 +111,8 @@ class Engine:
                                   cuda_graph_max_bs=args.cuda_graph_max_bs, seed=args.seed,
                                   kv_cache_dtype_name=args.kv_cache_dtype)
         prefix = None
-        if not args.disable_radix_cache and not getattr(self.runner.model, "stateful", False):
+        m = self.runner.model
+        if not args.disable_radix_cache and not getattr(m, "stateful", False) and not getattr(m, "encoder_only", False):
             from ome_amd.runtime.prefix_cache import PrefixCache
 
             prefix = PrefixCache(self.runner.pages, args.page_size)

@@ -116,7 +116,8 @@ class ModelRunner:
                         kv_cache_dtype_name, dtype)
             kv_dtype = dtype
         self.kv_dtype = kv_dtype
-        page_bytes = PagedKVCache.bytes_per_page(n_local, kv_heads, k_dim, page_size, kv_dtype, v_dim)
+        # encoders own no KV at all (page bookkeeping only)
+        page_bytes = max(1, PagedKVCache.bytes_per_page(n_local, kv_heads, k_dim, page_size, kv_dtype, v_dim))
         if self.is_cuda:
             free, total = torch.cuda.mem_get_info(self.device)
             used_by_others = total - free
@@ -164,7 +165,7 @@ class ModelRunner:
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
         # pipeline stages run eagerly: the stage hand-off is a blocking p2p exchange
-        self.use_graph = cuda_graph and self.is_cuda and not self.pp
+        self.use_graph = cuda_graph and self.is_cuda and not self.pp and not getattr(self.model, "encoder_only", False)
         if self.use_graph:
             self.capture_graphs()
 
@@ -600,6 +601,7 @@ class ModelRunner:
         bt = self.slots.table.index_select(0, t(req_idx))
         meta = AttnMeta("prefill", t(pos), t(slots), bt, cu_q=t(cu), kv_lens=t(q_lens),
                         items=t(items).view(-1, 2) if items else torch.zeros(0, 2, dtype=torch.int32, device=dv))
+        meta.extra["lengths"] = q_lens  # host copy (encoders' varlen attention work items)
         hidden = self.model.forward(t(ids), meta, self.kv)
         pool = getattr(self.model, "pool", None)  # classification / reward heads (models/decoder.py)
         out = pool(hidden, t(cu)) if pool is not None else ops.pool(hidden, t(cu), 0, True)

@@ -153,6 +153,11 @@ def create_app(engine, ns=None):
     app = FastAPI(title="ome_amd runtime")
     tok = engine.tokenizer
     model_name = engine.served_model_name
+    encoder = bool(getattr(getattr(engine, "runner", None), "model", None) is not None and
+                   getattr(engine.runner.model, "encoder_only", False))
+
+    def encode_text(text: str) -> list[int]:  # encoders take [CLS] ... [SEP]
+        return tok.encode_special(text) if encoder else tok.encode(text)
     created = int(time.time())
     default_max = 128
     app.state.engine = engine
@@ -391,16 +396,50 @@ def create_app(engine, ns=None):
         from ome_amd.runtime.request import SamplingParams
 
         for i, x in enumerate(items):
-            ids = list(x) if isinstance(x, list) else tok.encode(str(x))
+            ids = list(x) if isinstance(x, list) else encode_text(str(x))
             total += len(ids)
-            req, stream = await run_request(ids, SamplingParams(max_new_tokens=0))
-            req.is_embedding = True
-            while True:
-                _, fin = await stream.q.get()
-                if fin:
-                    break
-            out.append({"object": "embedding", "index": i, "embedding": req.embedding or []})
+            out.append({"object": "embedding", "index": i, "embedding": await _embed_ids(ids)})
         return {"object": "list", "data": out, "model": model_name,
+                "usage": {"prompt_tokens": total, "total_tokens": total}}
+
+    async def _embed_ids(ids: list[int]) -> list[float]:
+        from ome_amd.runtime.request import SamplingParams
+
+        req, stream = await run_request(ids, SamplingParams(max_new_tokens=0))
+        req.is_embedding = True
+        while True:
+            _, fin = await stream.q.get()
+            if fin:
+                break
+        return req.embedding or []
+
+    @app.post("/v1/rerank")
+    async def rerank(request: Request):
+        """Cross-encoder reranking (SGLang's ``/v1/rerank``): score every (query, document) pair with
+        a sequence-classification encoder; results sorted by relevance (the head's first logit)."""
+        body = await request.json()
+        if not encoder:
+            return JSONResponse({"error": {"message": "rerank needs a cross-encoder model",
+                                           "type": "invalid_request_error"}}, status_code=400)
+        query, docs = body.get("query"), body.get("documents") or []
+        if not isinstance(query, str) or not isinstance(docs, list):
+            return JSONResponse({"error": {"message": "query (str) and documents (list) are required",
+                                           "type": "invalid_request_error"}}, status_code=400)
+        texts = [d if isinstance(d, str) else (d or {}).get("text", "") for d in docs]
+        pairs = [tok.encode_special(query, text) for text in texts]
+        total = sum(len(ids) for ids in pairs)
+        scores = await asyncio.gather(*[_embed_ids(ids) for ids in pairs])  # one batched engine step
+        res = []
+        for i, (text, score) in enumerate(zip(texts, scores)):
+            item = {"index": i, "relevance_score": float(score[0]) if score else 0.0}
+            if body.get("return_documents", True):
+                item["document"] = {"text": text}
+            res.append(item)
+        res.sort(key=lambda r: -r["relevance_score"])
+        top_n = body.get("top_n")
+        if top_n:
+            res = res[:int(top_n)]
+        return {"id": f"rerank-{uuid.uuid4().hex[:12]}", "model": model_name, "results": res,
                 "usage": {"prompt_tokens": total, "total_tokens": total}}
 
     if getattr(engine, "kv_transfer", None) is not None:

@@ -18,6 +18,13 @@ class ByteTokenizer:
         ids = [b + 3 for b in text.encode("utf-8")]
         return ([self.bos_token_id] if add_bos else []) + ids
 
+    def encode_special(self, text: str, pair: str | None = None) -> list[int]:
+        """Encoder input: <bos> text <eos> [pair <eos>] (the [CLS] / [SEP] stand-ins)."""
+        ids = [self.bos_token_id] + self.encode(text) + [self.eos_token_id]
+        if pair is not None:
+            ids += self.encode(pair) + [self.eos_token_id]
+        return ids
+
     def decode(self, ids, skip_special: bool = True) -> str:
         out = bytearray()
         for i in ids:
@@ -68,6 +75,11 @@ class HFTokenizer:
         if add_bos and self.bos_token_id is not None:
             ids = [self.bos_token_id] + ids
         return ids
+
+    def encode_special(self, text: str, pair: str | None = None) -> list[int]:
+        """Encoder input with the tokenizer's own post-processor: [CLS] a [SEP] (b [SEP]) for BERT,
+        <s> a </s></s> b </s> for (XLM-)RoBERTa."""
+        return self.tok.encode(text, pair, add_special_tokens=True).ids
 
     def decode(self, ids, skip_special: bool = True) -> str:
         return self.tok.decode([int(i) for i in ids], skip_special_tokens=skip_special)
