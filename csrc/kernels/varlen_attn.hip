@@ -8,7 +8,7 @@
 // ViT windows), causal on request.
 //
 // One workgroup = (128-query-row item of one sequence, one query head); its 4 waves own 32 rows
-// each and share every 32-key K/V tile through double-buffered LDS:
+// each and share every K/V stage (2 x 32 keys) through double-buffered LDS:
 //   K  [32 keys][DP + 8]  (272 B rows for DP = 128: 16 rows start on distinct bank quads)
 //   V^T[DP dims][32 + 8]  keys in the k-slot order of the S^T accumulators, so a lane's A
 //                         fragment of O^T = V^T P^T is one 16-B ds_read.
@@ -37,11 +37,15 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
     const bf16* __restrict__ v, int64_t v_stride, const int* __restrict__ cu, const int2* __restrict__ items,
     bf16* __restrict__ out, int64_t o_stride, int Hq, int Hkv, int D, float scale_log2, int causal) {
   constexpr int KS = DP / 32, NB = DP / 16, KLD = DP + 8, VLD = 32 + 8, CPR = DP / 8;
-  constexpr int KCH = 32 * CPR;                       // 16-B chunks per 32-key tile (per operand)
-  constexpr int NCH = (KCH + 255) / 256;              // chunks per thread
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 32 * KLD + 2 * DP * VLD];
-  bf16* sK = smem;                 // [2][32 * KLD]
-  bf16* sV = smem + 2 * 32 * KLD;  // [2][DP * VLD]
+  constexpr int KCH = 32 * CPR;                       // 16-B K chunks per 32-key subtile
+  constexpr int NCH = (KCH + 255) / 256;              // K chunks per thread per subtile
+  constexpr int VG = 8 * CPR;                         // V groups (4 keys x 8 dims) per subtile
+  constexpr int NVG = (VG + 255) / 256;
+  constexpr int SUB = 1;                              // 32-key subtiles per pipeline stage (2: -20 % at D 128, occupancy)
+  constexpr int KT = 32 * KLD, VT = DP * VLD;         // elements per subtile image
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * SUB * (KT + VT)];
+  bf16* sK = smem;                      // [2][SUB][32 * KLD]
+  bf16* sV = smem + 2 * SUB * KT;       // [2][SUB][DP * VLD]
 
   const int2 it = items[blockIdx.x];
   const int s = it.x, r0_item = it.y;
@@ -71,28 +75,55 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) o[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 rk[NCH], rv[NCH];
-  auto load_tile = [&](int kb) {
+  // K: one 16-B chunk (8 dims of one key) per slot; V: groups of 4 consecutive keys x 8 dims, so
+  // the transposed V image is written 4 keys (8 B) at a time
+  bf16x8 rk[SUB][NCH], rv[SUB][NVG][4];
+  auto load_tile = [&](int kb0) {
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = tid + 256 * i;
-      const int key = c / CPR, d0 = (c % CPR) * 8;
-      const bool ok = c < KCH && kb + key < L && d0 < D;
-      const int64_t row = (int64_t)(t0 + kb + key);
-      rk[i] = ok ? ld8(k + row * k_stride + (int64_t)kvh * D + d0) : bf16x8{};
-      rv[i] = ok ? ld8(v + row * v_stride + (int64_t)kvh * D + d0) : bf16x8{};
+    for (int u = 0; u < SUB; ++u) {
+      const int kb = kb0 + 32 * u;
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) {
+        const int c = tid + 256 * i;
+        const int key = c / CPR, d0 = (c % CPR) * 8;
+        const bool ok = c < KCH && kb + key < L && d0 < D;
+        rk[u][i] = ok ? ld8(k + (int64_t)(t0 + kb + key) * k_stride + (int64_t)kvh * D + d0) : bf16x8{};
+      }
+#pragma unroll
+      for (int i = 0; i < NVG; ++i) {
+        const int c = tid + 256 * i;
+        const int kq = c / CPR, d0 = (c % CPR) * 8;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = 4 * kq + j;
+          const bool ok = c < VG && kb + key < L && d0 < D;
+          rv[u][i][j] = ok ? ld8(v + (int64_t)(t0 + kb + key) * v_stride + (int64_t)kvh * D + d0) : bf16x8{};
+        }
+      }
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      const int c = tid + 256 * i;
-      if (c < KCH) {
-        const int key = c / CPR, d0 = (c % CPR) * 8;
-        *reinterpret_cast<bf16x8*>(&sK[buf * 32 * KLD + key * KLD + d0]) = rk[i];
-        bf16* vt = &sV[buf * DP * VLD + va_slot(key)];
+    for (int u = 0; u < SUB; ++u) {
+      bf16* Ks = sK + (buf * SUB + u) * KT;
+      bf16* Vs = sV + (buf * SUB + u) * VT;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) vt[(d0 + j) * VLD] = rv[i][j];
+      for (int i = 0; i < NCH; ++i) {
+        const int c = tid + 256 * i;
+        if (c < KCH) *reinterpret_cast<bf16x8*>(&Ks[(c / CPR) * KLD + (c % CPR) * 8]) = rk[u][i];
+      }
+#pragma unroll
+      for (int i = 0; i < NVG; ++i) {
+        const int c = tid + 256 * i;
+        if (c < VG) {
+          const int kq = c / CPR, d0 = (c % CPR) * 8;
+          bf16* vt = &Vs[d0 * VLD + va_slot(4 * kq)];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            bf16x4 w = {rv[u][i][0][j], rv[u][i][1][j], rv[u][i][2][j], rv[u][i][3][j]};
+            *reinterpret_cast<bf16x4*>(vt + j * VLD) = w;
+          }
+        }
       }
     }
   };
@@ -104,12 +135,15 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
     store_tile(0);
   }
   __syncthreads();
-  for (int kb = 0; kb < kv_end; kb += 32) {
-    const bool more = kb + 32 < kv_end;
-    if (more) load_tile(kb + 32);  // in flight while this tile is consumed from LDS
-    if (active && (!causal || kb <= r0 + 31)) {
-      const bf16* Kt = sK + buf * 32 * KLD;
-      const bf16* Vt = sV + buf * DP * VLD;
+  for (int kb0 = 0; kb0 < kv_end; kb0 += 32 * SUB) {
+    const bool more = kb0 + 32 * SUB < kv_end;
+    if (more) load_tile(kb0 + 32 * SUB);  // in flight while this stage is consumed from LDS
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) {
+      const int kb = kb0 + 32 * u;
+      if (!(active && kb < kv_end && (!causal || kb <= r0 + 31))) continue;
+      const bf16* Kt = sK + (buf * SUB + u) * KT;
+      const bf16* Vt = sV + (buf * SUB + u) * VT;
       f32x4 sc[2][2];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) sc[rb][0] = sc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};

@@ -1,12 +1,15 @@
 """Varlen bidirectional attention (``ome_varlen_attention``) vs torch SDPA on the same packed
 batches: BERT-large embedding batch, Qwen2-VL ViT images (head dim 80), long single sequences.
 Prints per-shape time, TFLOP/s and the max error against SDPA.  Random bf16 operands."""
+import os
+import sys
 import time
 
 import torch
 import torch.nn.functional as F
 
-from ome_amd import ops
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ome_amd import ops  # noqa: E402
 
 
 def bench(fn, iters=20):
