@@ -65,6 +65,10 @@ FAMILIES: list[Family] = [
     Family("qwen3-30b-a3b", "qwen", "Qwen/Qwen3-30B-A3B", "Qwen3MoeForCausalLM", 30.5),
     Family("qwen2-vl-7b-instruct", "qwen", "Qwen/Qwen2-VL-7B-Instruct", "Qwen2VLForConditionalGeneration", 8.3,
            "qwen2-vl-7b", capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("qwen2-5-vl-7b-instruct", "qwen", "Qwen/Qwen2.5-VL-7B-Instruct", "Qwen2_5_VLForConditionalGeneration", 8.3,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("mimo-vl-7b-rl", "xiaomimimo", "XiaomiMiMo/MiMo-VL-7B-RL", "Qwen2_5_VLForConditionalGeneration", 8.3,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("llama-3-2-11b-vision-instruct", "meta", "meta-llama/Llama-3.2-11B-Vision-Instruct",
            "MllamaForConditionalGeneration", 10.7, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("llama-3-2-90b-vision-instruct", "meta", "meta-llama/Llama-3.2-90B-Vision-Instruct",
