@@ -133,6 +133,10 @@ class Engine:
         self.kv_transfer = None  # PD disaggregation hook (ome_amd.runtime.disagg)
         # overlapped scheduling: (batch, handle, launch time) of the step whose tokens are in flight
         self._inflight = None
+        # host-side time split of the serving loop (seconds, cumulative): schedule / launch
+        # (input packing + kernel / graph enqueue) / wait (blocked on the GPU) / commit
+        self.host_times = {"schedule": 0.0, "launch": 0.0, "wait": 0.0, "commit": 0.0, "steps": 0}
+        self.host_trace: list | None = None   # per-call (kind, rows, t_a, t_b) when profiling
         ov = self.runner.is_cuda if args.overlap_schedule is None else bool(args.overlap_schedule)
         self.overlap = ov and not self.cfg.is_embedding and self.pstate.pp_size == 1 and not self.dp
 
@@ -284,6 +288,8 @@ class Engine:
         if self.dp:
             return self._dp_step()
         prev = self._inflight
+        ht = self.host_times
+        ts = time.perf_counter()
         batch = self.scheduler.schedule()
         launched = None
         if batch is not None:
@@ -291,6 +297,10 @@ class Engine:
             handle = self.runner.launch(batch, prev[1] if prev else None)
             self.scheduler.launch_commit(batch)
             launched = (batch, handle, t0)
+            ht["schedule"] += t0 - ts
+            ht["launch"] += time.perf_counter() - t0
+            if self.host_trace is not None:
+                self.host_trace.append((batch.mode, len(batch.chunks), t0 - ts, time.perf_counter() - t0))
         done: list[Request] = []
         if not self.overlap:
             if launched:
@@ -302,11 +312,18 @@ class Engine:
         return done
 
     def _complete(self, batch, handle, t0) -> list[Request]:
+        ht = self.host_times
+        tw = time.perf_counter()
         ids, lps = handle.result()
         now = time.perf_counter()
         done = self.scheduler.final_commit(batch, ids, lps, now, self.eos_ids)
         self.step_count += 1
         self.metrics.on_step(batch, now - t0, done, self.scheduler, self.runner.pages)
+        ht["wait"] += now - tw
+        if self.host_trace is not None:
+            self.host_trace.append(("wait", 0, now - tw, time.perf_counter() - now))
+        ht["commit"] += time.perf_counter() - now
+        ht["steps"] += 1
         return done
 
     def _dp_step(self) -> list[Request]:

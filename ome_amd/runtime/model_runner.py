@@ -330,7 +330,7 @@ class ModelRunner:
     @staticmethod
     def _src_row(r, pos: int, prev: "StepHandle | None") -> int:
         """Row of ``prev``'s sampled output holding the token at ``pos`` if it is pending."""
-        if prev is None or not r.n_pending or pos != r.seq_len - 1 or r.all_ids[pos] != PENDING:
+        if prev is None or not r.n_pending or pos != r.seq_len - 1 or r.token_at(pos) != PENDING:
             return -1
         return r.pending_row
 
@@ -346,36 +346,43 @@ class ModelRunner:
         h[off["src"]:off["src"] + bs] = -1
         seeds = h[off["seeds"]:off["seeds"] + 2 * bs].view(np.uint64)
         any_pending = False
-        for i, c in enumerate(batch.chunks):
+        P = self.P
+        toks, poss, slots, lens, rsl, srcs, sds = [], [], [], [], [], [], []
+        tk, tmp, tp, mp, rep, frq, prs = [], [], [], [], [], [], []
+        for c in batch.chunks:  # python lists, one numpy store per field (not per element)
             r = c.req
             pos = c.start
-            tok = r.all_ids[pos]
             src = self._src_row(r, pos, prev)
             if src >= 0:
-                h[off["src"] + i] = src
                 any_pending = True
-                tok = 0
-            h[off["ids"] + i] = tok
-            h[off["pos"] + i] = pos + (r.mm.rope_delta if r.mm is not None else 0)  # M-RoPE text offset
-            h[off["slots"] + i] = r.pages[pos // self.P] * self.P + pos % self.P
-            h[off["seq_lens"] + i] = pos + 1
-            h[off["req_idx"] + i] = r.req_slot
+                toks.append(0)
+            else:
+                toks.append(r.token_at(pos))
+            srcs.append(src)
+            poss.append(pos + (r.mm.rope_delta if r.mm is not None else 0))  # M-RoPE text offset
+            slots.append(r.pages[pos // P] * P + pos % P)
+            lens.append(pos + 1)
+            rsl.append(r.req_slot)
             p = r.params
-            h[off["top_k"] + i] = p.top_k
-            hf[off["temp"] + i] = p.temperature
-            hf[off["top_p"] + i] = p.top_p
-            hf[off["min_p"] + i] = p.min_p
-            hf[off["rep"] + i] = p.repetition_penalty
-            hf[off["freq"] + i] = p.frequency_penalty
-            hf[off["pres"] + i] = p.presence_penalty
-            seeds[i] = self._seed(r, pos + 1)  # keyed by the position of the token being drawn
-        for i in range(B, bs):
-            hf[off["temp"] + i] = 0.0
-            hf[off["top_p"] + i] = 1.0
-            h[off["top_k"] + i] = -1
-            hf[off["rep"] + i] = 1.0
-            hf[off["freq"] + i] = 0.0
-            hf[off["pres"] + i] = 0.0
+            tk.append(p.top_k)
+            tmp.append(p.temperature)
+            tp.append(p.top_p)
+            mp.append(p.min_p)
+            rep.append(p.repetition_penalty)
+            frq.append(p.frequency_penalty)
+            prs.append(p.presence_penalty)
+            sds.append(self._seed(r, pos + 1))  # keyed by the position of the token being drawn
+        for name, vals in (("ids", toks), ("src", srcs), ("pos", poss), ("slots", slots), ("seq_lens", lens),
+                           ("req_idx", rsl), ("top_k", tk)):
+            h[off[name]:off[name] + B] = vals
+        for name, vals in (("temp", tmp), ("top_p", tp), ("min_p", mp), ("rep", rep), ("freq", frq),
+                           ("pres", prs)):
+            hf[off[name]:off[name] + B] = vals
+        seeds[:B] = np.asarray(sds, dtype=np.uint64)
+        if bs > B:  # neutral sampling parameters on the padding rows
+            for name, v in (("temp", 0.0), ("top_p", 1.0), ("rep", 1.0), ("freq", 0.0), ("pres", 0.0)):
+                hf[off[name] + B:off[name] + bs] = v
+            h[off["top_k"] + B:off["top_k"] + bs] = -1
         # attention visits sequences longest-first (padding rows, seq_len 0, last)
         h[off["order"]:off["order"] + bs] = np.argsort(-h[off["seq_lens"]:off["seq_lens"] + bs], kind="stable")
         self._init_penalty_rows(batch.chunks)
@@ -404,32 +411,49 @@ class ModelRunner:
             c = chunks[i]
             r = c.req
             t0 = len(ids)
-            ids.extend(r.all_ids[c.start:c.start + c.length])
-            src.extend([-1] * c.length)
-            s_row = self._src_row(r, c.start + c.length - 1, prev)
-            if s_row >= 0:
-                src[t0 + c.length - 1] = s_row
-                ids[t0 + c.length - 1] = 0
-                any_pending = True
-            pp = range(c.start, c.start + c.length)
-            pos.extend(pp)
+            a, n = c.start, c.length
             pages = r.pages
-            slots.extend(pages[x // P] * P + x % P for x in pp)
-            if c.length > 1:
-                q_lens.append(c.length)
-                kv_lens.append(c.start + c.length)
+            if n > 1:
+                ids.extend(r.ids_range(a, a + n))
+                src.extend([-1] * n)
+                pp = np.arange(a, a + n, dtype=np.int64)
+                pos.append(pp)
+                slots.append(np.asarray(pages, np.int64)[pp // P] * P + pp % P)
+                q_lens.append(n)
+                kv_lens.append(a + n)
                 req_idx.append(r.req_slot)
             else:
-                dec_lens.append(c.start + 1)
+                ids.append(r.token_at(a))
+                src.append(-1)
+                pos.append(a)
+                slots.append(pages[a // P] * P + a % P)
+                dec_lens.append(a + 1)
                 dec_req.append(r.req_slot)
+            s_row = self._src_row(r, a + n - 1, prev)
+            if s_row >= 0:
+                src[t0 + n - 1] = s_row
+                ids[t0 + n - 1] = 0
+                any_pending = True
             last_row[i] = len(ids) - 1
         items = ops.prefill_work_items(q_lens, kv_lens) if q_lens else []
-        T, S, n_it, nd = len(ids), len(q_lens), len(items), len(dec_lens)
+        T, S, n_it, nd, B = len(ids), len(q_lens), len(items), len(dec_lens), len(chunks)
         cu = np.zeros(S + 1, dtype=np.int32)
         cu[1:] = np.cumsum(q_lens)
         dec_order = np.argsort(-np.asarray(dec_lens, np.int64), kind="stable").astype(np.int32) if nd else \
             np.zeros(0, np.int32)
-        packed = np.concatenate([np.asarray(ids, np.int32), np.asarray(pos, np.int32), np.asarray(slots, np.int32),
+
+        def flat(parts):  # per-chunk numpy arrays (prefill) and scalars (single-token rows)
+            return np.concatenate([np.atleast_1d(np.asarray(x)).astype(np.int32) for x in parts]) if parts else \
+                np.zeros(0, np.int32)
+
+        # sampling parameters ride in the same pinned H2D copy: int64 seeds first (8-B aligned),
+        # then fp32 fields as raw 32-bit words
+        sv = [self._seed(c.req, c.start + c.length) for c in chunks]
+        seeds = np.asarray([v - (1 << 64) if v >= (1 << 63) else v for v in sv], np.int64).view(np.int32)
+        fp = np.asarray([[c.req.params.temperature, c.req.params.top_p, c.req.params.min_p] for c in chunks],
+                        np.float32).T.copy().view(np.int32).reshape(-1)
+        top_k = np.asarray([c.req.params.top_k for c in chunks], np.int32)
+        packed = np.concatenate([seeds, fp, top_k, np.asarray(ids, np.int32), flat(pos), flat(slots),
                                  cu, np.asarray(kv_lens, np.int32), np.asarray(req_idx, np.int32),
                                  np.asarray(last_row, np.int32), np.asarray(src, np.int32),
                                  np.asarray(dec_lens, np.int32), np.asarray(dec_req, np.int32), dec_order,
@@ -446,8 +470,11 @@ class ModelRunner:
             o += n
             return t
 
+        t_seeds = take(2 * B).view(torch.int64)
+        t_temp, t_top_p, t_min_p = (take(B).view(torch.float32) for _ in range(3))
+        t_top_k = take(B)
         t_ids, t_pos, t_slots = take(T), take(T), take(T)
-        t_cu, t_kv, t_req, t_rows = take(S + 1), take(S), take(S), take(len(chunks))
+        t_cu, t_kv, t_req, t_rows = take(S + 1), take(S), take(S), take(B)
         t_src = take(T)
         t_dlen, t_dreq, t_dord = take(nd), take(nd), take(nd)
         t_items = take(2 * n_it).view(n_it, 2)
@@ -507,16 +534,7 @@ class ModelRunner:
                 pen[1] = torch.where(keep, pen[1], torch.zeros_like(pen[1]))
                 pen[2] = torch.where(keep, pen[2], torch.zeros_like(pen[2]))
             ops.apply_penalties(logits, self.counts, pslot, *pen)
-        temp = torch.tensor([c.req.params.temperature for c in chunks], dtype=torch.float32)
-        top_k = torch.tensor([c.req.params.top_k for c in chunks], dtype=torch.int32)
-        top_p = torch.tensor([c.req.params.top_p for c in chunks], dtype=torch.float32)
-        min_p = torch.tensor([c.req.params.min_p for c in chunks], dtype=torch.float32)
-        sv = [self._seed(c.req, c.start + c.length) for c in chunks]
-        seeds = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in sv], dtype=torch.int64)
-        if self.is_cuda:
-            temp, top_k, top_p, min_p, seeds = (x.to(self.device, non_blocking=True)
-                                                for x in (temp, top_k, top_p, min_p, seeds))
-        out_ids, out_lp = ops.sample(logits, temp, top_k, top_p, min_p, seeds, 0)
+        out_ids, out_lp = ops.sample(logits, t_temp, t_top_k, t_top_p, t_min_p, t_seeds, 0)
         out_ids = out_ids.to(torch.int32)
         if pen is not None:
             ops.update_counts(self.counts, pslot, out_ids, *pen)

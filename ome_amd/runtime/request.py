@@ -89,6 +89,20 @@ class Request:
     def all_ids(self) -> list[int]:
         return self.prompt_ids + self.output_ids
 
+    def token_at(self, pos: int) -> int:
+        """``all_ids[pos]`` without building the concatenated list (hot in the step packing)."""
+        n = len(self.prompt_ids)
+        return self.prompt_ids[pos] if pos < n else self.output_ids[pos - n]
+
+    def ids_range(self, a: int, b: int) -> list[int]:
+        """``all_ids[a:b]`` without building the concatenated list."""
+        n = len(self.prompt_ids)
+        if b <= n:
+            return self.prompt_ids[a:b]
+        if a >= n:
+            return self.output_ids[a - n:b - n]
+        return self.prompt_ids[a:] + self.output_ids[:b - n]
+
     @property
     def seq_len(self) -> int:
         return len(self.prompt_ids) + len(self.output_ids)

@@ -13,6 +13,6 @@ rc=$?
 cd $R
 grep -v amdgpu.ids gpurun_out/${PROF_NAME:-prof}_bench.log | tail -2 | cut -c1-300
 [ $rc -eq 0 ] || exit $rc
-python scripts/prof_summary.py gpurun_out/${PROF_NAME:-prof} $STEPS > gpurun_out/${PROF_NAME:-prof}/summary.md && head -40 gpurun_out/${PROF_NAME:-prof}/summary.md
+python scripts/prof_summary.py gpurun_out/${PROF_NAME:-prof} $((STEPS * 8)) > gpurun_out/${PROF_NAME:-prof}/summary.md && head -40 gpurun_out/${PROF_NAME:-prof}/summary.md
 find gpurun_out/${PROF_NAME:-prof} -name "*kernel_trace.csv" -delete
 exit 0

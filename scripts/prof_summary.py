@@ -94,6 +94,35 @@ def main(d: str, last_steps: int = 0) -> None:
           f"{sum(kinds['mixed'].values()) / 1e3 / max(1, nk['mixed']):.0f} |")
     print(f"| **span** | {span['decode'] / 1e3 / max(1, nk['decode']):.0f} | {span['mixed'] / 1e3 / max(1, nk['mixed']):.0f} |")
     print(f"| steps | {nk['decode']} | {nk['mixed']} |")
+    # ---- idle time: gaps between consecutive kernels (the device is serial here), split into the
+    # gap before a step's first kernel (host scheduling / launch latency between steps) and gaps
+    # inside a step, attributed to the kernel that started late
+    inter = {"decode": 0, "mixed": 0}
+    intra = {"decode": collections.Counter(), "mixed": collections.Counter()}
+    step_rows, prev_end, pending_inter = [], None, 0
+    for r in rows:
+        st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        if prev_end is not None:
+            gap = max(0, st - prev_end)
+            if not step_rows:
+                pending_inter = gap
+            elif gap > 2000:
+                step_rows.append(("gap", cat_of(r["Kernel_Name"]), gap))
+        step_rows.append(("k", r["Kernel_Name"], 0))
+        prev_end = en if prev_end is None else max(prev_end, en)
+        if "sample_kernel" in r["Kernel_Name"]:
+            k = "mixed" if any(t == "k" and "paged_prefill" in n for t, n, _ in step_rows) else "decode"
+            inter[k] += pending_inter
+            for t, n, g in step_rows:
+                if t == "gap":
+                    intra[k][n] += g
+            step_rows, pending_inter = [], 0
+    print("\n## Idle gaps (us per step)\n\n| | decode-only | mixed |\n|---|---:|---:|")
+    print(f"| before the step's first kernel | {inter['decode'] / 1e3 / max(1, nk['decode']):.0f} | "
+          f"{inter['mixed'] / 1e3 / max(1, nk['mixed']):.0f} |")
+    for c in sorted(set(intra["decode"]) | set(intra["mixed"]), key=lambda c: -(intra["decode"][c] + intra["mixed"][c])):
+        print(f"| inside, before a {c} kernel (gaps > 2 us) | {intra['decode'][c] / 1e3 / max(1, nk['decode']):.0f} | "
+              f"{intra['mixed'][c] / 1e3 / max(1, nk['mixed']):.0f} |")
     print("\n## GEMMs by kernel+grid\n\n| total ms | calls | avg us | kernel / grid |\n|---:|---:|---:|---|")
     for n, v in grids.most_common(20):
         print(f"| {v / 1e6:.2f} | {gcnt[n]} | {v / gcnt[n] / 1e3:.1f} | `{n}` |")
