@@ -13,7 +13,7 @@
 //   V^T[DP dims][32 + 8]  keys in the k-slot order of the S^T accumulators, so a lane's A
 //                         fragment of O^T = V^T P^T is one 16-B ds_read.
 // S^T = K Q^T and O^T = V^T P^T run on v_mfma_f32_16x16x32_bf16 with the online softmax in
-// registers (exp2 domain).  Head dims that are not a multiple of 32 (ViT-H 80) are zero-padded
+// registers (exp2 domain).  Head dims that are not a multiple of 32 (ViT-H 80, Llama-4 ViT 88) are zero-padded
 // to DP inside the kernel: padded dims contribute 0 to QK^T and are never stored.
 #include "common.h"
 
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
       bf16* orow = out + (int64_t)(t0 + r) * o_stride + (int64_t)head * D;
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
-        if (16 * nb < D) {
+        if (16 * nb + 4 * g < D) {  // D % 8 == 0: a lane's 4 dims are all in or all out
           bf16x4 w;
 #pragma unroll
           for (int i = 0; i < 4; ++i) w[i] = (bf16)(o[rb][nb][i] * inv);
@@ -233,14 +233,14 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
 }  // namespace
 
 // items: int2 (sequence, first row) per 128-row work item, n_items of them (host-built).
-// Strides are in elements per token; head h of a token starts at h * D.  D % 16 == 0, D <= 128;
+// Strides are in elements per token; head h of a token starts at h * D.  D % 8 == 0, D <= 128;
 // every pointer and stride 16-B aligned.
 OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k, int64_t k_stride, const void* v,
                                  int64_t v_stride, const int* cu, const int* items, int n_items, void* out,
                                  int64_t o_stride, int Hq, int Hkv, int D, float scale, int causal,
                                  hipStream_t stream) {
   if (n_items <= 0) return 0;
-  if (D <= 0 || D > 128 || D % 16 != 0) return -2;
+  if (D <= 0 || D > 128 || D % 8 != 0) return -2;
   if (Hkv <= 0 || Hq % Hkv != 0) return -3;
   if ((q_stride | k_stride | v_stride | o_stride) % 8 != 0) return -4;
   if (Hq > 65535) return -5;

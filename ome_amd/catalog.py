@@ -53,9 +53,11 @@ FAMILIES: list[Family] = [
     Family("llama-3-1-405b-instruct-fp8", "meta", "meta-llama/Llama-3.1-405B-Instruct-FP8", "LlamaForCausalLM",
            405.0, None, 1.0, quantization="fp8"),
     Family("llama-4-scout-17b-16e-instruct", "meta", "meta-llama/Llama-4-Scout-17B-16E-Instruct",
-           "Llama4ForConditionalGeneration", 109.0, "llama-4-scout-17b-16e"),
+           "Llama4ForConditionalGeneration", 109.0, "llama-4-scout-17b-16e",
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("llama-4-maverick-17b-128e-instruct-fp8", "meta", "meta-llama/Llama-4-Maverick-17B-128E-Instruct-FP8",
-           "Llama4ForConditionalGeneration", 402.0, None, 1.0, quantization="fp8"),
+           "Llama4ForConditionalGeneration", 402.0, None, 1.0, quantization="fp8",
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("mistral-7b-instruct", "mistralai", "mistralai/Mistral-7B-Instruct-v0.3", "MistralForCausalLM", 7.2),
     Family("mixtral-8x7b-instruct", "mistralai", "mistralai/Mixtral-8x7B-Instruct-v0.1", "MixtralForCausalLM",
            46.7, "mixtral-8x7b"),

@@ -51,6 +51,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.qwen2_vl import Qwen2VLForConditionalGeneration
 
         return Qwen2VLForConditionalGeneration
+    if cfg.architecture == "Llama4ForConditionalGeneration" and (cfg.extra or {}).get("vision_config"):
+        from ome_amd.models.llama4_vision import Llama4ForConditionalGeneration
+
+        return Llama4ForConditionalGeneration
     if cfg.architecture in LLAMA4_ARCHS or cfg.model_type in ("llama4", "llama4_text"):
         from ome_amd.models.llama4 import Llama4ForCausalLM
 

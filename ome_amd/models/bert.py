@@ -57,8 +57,8 @@ class EncoderModel:
         self.tp = _TP(cfg)
         self.H, self.nh = cfg.hidden_size, cfg.num_heads
         self.D = self.H // self.nh
-        if self.D % 16 or self.D > 128:
-            raise NotImplementedError(f"encoder head dim {self.D} (multiple of 16, <= 128)")
+        if self.D % 8 or self.D > 128:
+            raise NotImplementedError(f"encoder head dim {self.D} (multiple of 8, <= 128)")
         self.scale = 1.0 / math.sqrt(self.D)
         self.eps = float(hf.get("layer_norm_eps", 1e-12))
         self.act = _ACT.get(str(hf.get("hidden_act", "gelu")), 3)

@@ -129,7 +129,7 @@ class Llama4ForCausalLM(MoEForCausalLM):
         for i, d in experts.items():
             gu, dn = d["gate_up_proj"], d["down_proj"]  # [E, H, 2I], [E, I, H]
             Ifull = gu.shape[-1] // 2
-            sel = torch.tensor(idx(i), dtype=torch.long)
+            sel = torch.tensor(idx(i), dtype=torch.long, device=gu.device)
             gu, dn = gu.index_select(0, sel), dn.index_select(0, sel)
             n = min(I, Ifull - tp.rank * I)
             g = gu[..., tp.rank * I: tp.rank * I + n]

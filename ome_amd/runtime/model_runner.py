@@ -560,11 +560,14 @@ class ModelRunner:
                 p3[:, row:row + L] = xs
             else:
                 plen = len(r.prompt_ids)
-                blk = np.empty((3, L), dtype=np.int64)
-                inside = xs < plen
-                blk[:, inside] = mm.mrope_pos[:, xs[inside]]
-                blk[:, ~inside] = xs[~inside] + mm.rope_delta
-                p3[:, row:row + L] = blk
+                if mm.mrope_pos is None:  # plain 1D positions (Llama 4)
+                    p3[:, row:row + L] = xs
+                else:
+                    blk = np.empty((3, L), dtype=np.int64)
+                    inside = xs < plen
+                    blk[:, inside] = mm.mrope_pos[:, xs[inside]]
+                    blk[:, ~inside] = xs[~inside] + mm.rope_delta
+                    p3[:, row:row + L] = blk
                 off = 0
                 for s, n in mm.spans:
                     lo, hi = max(s, c.start), min(s + n, c.start + L)
@@ -578,7 +581,8 @@ class ModelRunner:
                     mm.features = None  # prompt fully scheduled: image features no longer needed
             row += L
         dv = self.device
-        meta.extra["rope"] = (torch.arange(T, dtype=torch.int32, device=dv), m.mrope_table(torch.from_numpy(p3)))
+        if any(chunks[i].req.mm is not None and chunks[i].req.mm.mrope_pos is not None for i in order):
+            meta.extra["rope"] = (torch.arange(T, dtype=torch.int32, device=dv), m.mrope_table(torch.from_numpy(p3)))
         r_dev = torch.tensor(rows, dtype=torch.long, device=dv)
         f = torch.cat(feats, 0) if feats else torch.zeros(0, m.cfg.hidden_size, dtype=m.dtype, device=dv)
         return m.embed_with_images(t_ids, r_dev, f)

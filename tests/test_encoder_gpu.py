@@ -9,7 +9,7 @@ from ome_amd.ops import reference as ref
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("D", [64, 80, 128])
+@pytest.mark.parametrize("D", [64, 80, 88, 128])
 @pytest.mark.parametrize("causal", [False, True])
 def test_varlen_attention_kernel(D, causal):
     torch.manual_seed(D)
