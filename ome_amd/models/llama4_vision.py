@@ -262,42 +262,51 @@ class Llama4ForConditionalGeneration(Llama4ForCausalLM):
     def image_prompt_ids(self) -> list[int]:
         return [self.image_id]
 
-    def _image_tokens(self, ratio: tuple[int, int]) -> list[int]:
+    def _image_tokens(self, ratio: tuple[int, int], patch: int) -> tuple[list[int], list[tuple[int, int]]]:
+        """Token layout of one image and its patch runs (offset, length) within it."""
         rh, rw = ratio
         n = self.visual.tokens_per_tile
-        ids = [self.boi_id]
+        ids, runs = [self.boi_id], []
+
+        def patches():
+            runs.append((len(ids), n))
+            ids.extend([patch] * n)
+
         if rh * rw > 1:
             for _ in range(rh):
                 for x in range(rw):
-                    ids += [self.patch_id] * n
+                    patches()
                     if x < rw - 1:
                         ids.append(self.tile_x)
                 ids.append(self.tile_y)
-        return ids + [self.image_id] + [self.patch_id] * n + [self.eoi_id]
+        ids.append(self.image_id)
+        patches()
+        ids.append(self.eoi_id)
+        return ids, runs
 
     def make_mm_input(self, prompt_ids: list[int], images: list):
-        """Expand each ``<|image|>`` of the prompt into the image's tile-token layout."""
+        """Expand each ``<|image|>`` of the prompt into the image's tile-token layout.  The patch
+        rows carry a content-hash id (:func:`ome_amd.multimodal.inputs.pad_token_id`) so the
+        prefix cache only ever matches identical images; the rows are overwritten by the vision
+        features, so the id is never embedded."""
+        from ome_amd.multimodal.inputs import pad_token_id
+
         where = [i for i, t in enumerate(prompt_ids) if t == self.image_id]
         if len(where) != len(images):
             raise ValueError(f"prompt has {len(where)} <|image|> tokens for {len(images)} images")
-        ids, pvs, grids, last = [], [], [], 0
+        ids, pvs, grids, spans, last = [], [], [], [], 0
         for i, im in zip(where, images):
             tiles, ratio = im if isinstance(im, tuple) else preprocess_llama4(im, self.visual.image,
                                                                                 self.max_patches)
-            ids += prompt_ids[last:i] + self._image_tokens(ratio)
+            ids += prompt_ids[last:i]
+            toks, runs = self._image_tokens(ratio, pad_token_id(tiles, self.cfg.vocab_size))
+            spans += [(len(ids) + o, n) for o, n in runs]
+            ids += toks
             pvs.append(tiles)
             grids.append((tiles.shape[0], *ratio))
             last = i + 1
         ids += prompt_ids[last:]
-        spans, s = [], None
-        for j, t in enumerate(ids + [-1]):  # maximal runs of patch tokens
-            if t == self.patch_id and s is None:
-                s = j
-            elif t != self.patch_id and s is not None:
-                spans.append((s, j - s))
-                s = None
-        mm = MMInput(torch.cat(pvs, 0), grids, spans)
-        return ids, mm
+        return ids, MMInput(torch.cat(pvs, 0), grids, spans)
 
     def encode_images(self, pixel_values: torch.Tensor, grids) -> torch.Tensor:
         return self.visual.forward(pixel_values)

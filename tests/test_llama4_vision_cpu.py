@@ -77,11 +77,14 @@ def test_llama4_vision_tower_and_generate_match_hf(tmp_path):
 
     prompt = [1, 9, 17, IMAGE, 33, 41, 12, 7]
     req = eng.make_mm_request(prompt, [img], SamplingParams(max_new_tokens=6, ignore_eos=True, logprobs=True))
-    ex = req.prompt_ids
+    ex = list(req.prompt_ids)
+    for s0, k in req.mm.spans:   # content-hash ids on the patch rows -> the reference's <|patch|>
+        assert len(set(ex[s0:s0 + k])) == 1
+        ex[s0:s0 + k] = [PATCH] * k
     n = m.visual.tokens_per_tile
     row = [PATCH] * n + [TX] + [PATCH] * n + [TX] + [PATCH] * n + [TY]
     assert ex[3:4 + 2 * len(row)] == [BOI] + row + row and ex.count(PATCH) == 7 * n
-    assert ex[4 + 2 * len(row):] [:n + 2] == [IMAGE] + [PATCH] * n + [EOI]
+    assert ex[4 + 2 * len(row):][:n + 2] == [IMAGE] + [PATCH] * n + [EOI]
     eng.add_request(req)
     while not req.finished:
         eng.step()

@@ -7,7 +7,7 @@ import torch
 from ome_amd.models.llama4_vision import preprocess_llama4
 from ome_amd.runtime.engine import Engine, EngineArgs
 from ome_amd.runtime.request import SamplingParams
-from tests.test_llama4_vision_cpu import IMAGE, _hf_model, _image
+from tests.test_llama4_vision_cpu import IMAGE, PATCH, _hf_model, _image
 
 pytestmark = pytest.mark.gpu
 
@@ -30,7 +30,10 @@ def test_llama4_vision_on_gpu(tmp_path):
     eng.add_request(req)
     while not req.finished:
         eng.step()
+    ex = list(req.prompt_ids)
+    for s0, k in req.mm.spans:
+        ex[s0:s0 + k] = [PATCH] * k
     with torch.no_grad():
-        ref = hf.generate(torch.tensor([req.prompt_ids]), pixel_values=tiles, max_new_tokens=8,
-                          do_sample=False)[0, len(req.prompt_ids):].tolist()
+        ref = hf.generate(torch.tensor([ex]), pixel_values=tiles, max_new_tokens=8,
+                          do_sample=False)[0, len(ex):].tolist()
     assert sum(int(a == b) for a, b in zip(req.output_ids, ref)) >= 6, (req.output_ids, ref)
