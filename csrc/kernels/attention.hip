@@ -644,7 +644,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
     bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale,
-    const float* __restrict__ sinks) {
+    const float* __restrict__ sinks, const int* __restrict__ row_hi) {
   static_assert(P == 16, "prefill kernel assumes 16-token pages");
   constexpr int NB = D / 16, KS = D / 32;
   const int2 it = items[blockIdx.x];
@@ -659,7 +659,9 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n = lane & 15, g = lane >> 4;
   const int r_hi = min(r0 + 32, q_len);
-  const int kv_end = min(kv_len, prefix + r_hi);
+  // row_hi (optional, per query row): last visible key beyond the causal one (Gemma 3 image
+  // blocks attend bidirectionally); keys up to the sequence end may then be visible
+  const int kv_end = row_hi ? kv_len : min(kv_len, prefix + r_hi);
   int kv_lo = 0;
   kv_lo = attn_lo(prefix + r0, window) & ~31;
   const int* bt = block_tables + (int64_t)s * bt_stride;
@@ -707,6 +709,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
         const int qpos = prefix + r0 + 16 * rb + n;
+        const int qlim = row_hi ? max(qpos, row_hi[q0 + min(r0 + 16 * rb + n, q_len - 1)]) : qpos;
         float mt = OME_NEG_INF;
 #pragma unroll
         for (int X = 0; X < 2; ++X)
@@ -716,7 +719,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
             const int key = kb + 16 * X + 4 * g + i;
             if (al != 0.f) v += al * (float)(key - qpos);
             if (need_mask) {
-              const bool ok = key <= qpos && key < kv_len && key >= attn_lo(qpos, window);
+              const bool ok = key <= qlim && key < kv_len && key >= attn_lo(qpos, window);
               v = ok ? v : OME_NEG_INF;
             }
             sc[rb][X][i] = v;
@@ -794,7 +797,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
     bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale,
-    const float* __restrict__ sinks) {
+    const float* __restrict__ sinks, const int* __restrict__ row_hi) {
   constexpr int D = 128, P = 16, NB = D / 16, KS = D / 32;
   typedef typename KVRaw<F>::K8 Raw8;  // 8 consecutive cache elements
   __shared__ __attribute__((aligned(16))) bf16 sK[2][SUB][32 * PF_KLD];
@@ -814,7 +817,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   const int head = kvh * G + hl;
   const int r0 = r0_item + 32 * rblk;
   const int item_hi = min(r0_item + rows_per_item, q_len);
-  const int kv_end = min(kv_len, prefix + item_hi);
+  const int kv_end = row_hi ? kv_len : min(kv_len, prefix + item_hi);
   int kv_lo = 0;
   kv_lo = attn_lo(prefix + r0_item, window) & ~31;
   const int* bt = block_tables + (int64_t)s * bt_stride;
@@ -911,6 +914,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
         const int qpos = prefix + r0 + 16 * rb + n;
+        const int qlim = row_hi ? max(qpos, row_hi[q0 + min(r0 + 16 * rb + n, q_len - 1)]) : qpos;
         float mt = OME_NEG_INF;
 #pragma unroll
         for (int X = 0; X < 2; ++X)
@@ -920,7 +924,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
             const int key = kbu + 16 * X + 4 * g + i;
             if (al != 0.f) v += al * (float)(key - qpos);
             if (need_mask) {
-              const bool ok = key <= qpos && key < kv_len && key >= attn_lo(qpos, window);
+              const bool ok = key <= qlim && key < kv_len && key >= attn_lo(qpos, window);
               v = ok ? v : OME_NEG_INF;
             }
             sc[rb][X][i] = v;
@@ -982,20 +986,21 @@ template <int D, int F>
 static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, const void* q, int64_t q_stride,
                            const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                            const int* cu_q, const int* kv_lens, const int* items, void* out, int64_t out_stride,
-                           int Hq, int Hkv, Scaler scl, int window, float v_scale, const float* sinks) {
+                           int Hq, int Hkv, Scaler scl, int window, float v_scale, const float* sinks,
+                           const int* row_hi) {
   typedef typename KVStore<F>::T T;
   if constexpr (D == 128) {
     if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
       paged_prefill_v2_kernel<2, F><<<grid, 256, 0, stream>>>(
           (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks);
+          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi);
       return;
     }
   }
   const int nw = G < 8 ? G : 8;
   paged_prefill_kernel<D, 16, F><<<grid, 64 * nw, 0, stream>>>(
       (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks);
+      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi);
 }
 
 template <int D>
@@ -1003,10 +1008,10 @@ static void prefill_dispatch(int kv_fmt, int variant, int G, dim3 grid, hipStrea
                              int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                              int bt_stride, const int* cu_q, const int* kv_lens, const int* items, void* out,
                              int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale,
-                             const float* sinks) {
+                             const float* sinks, const int* row_hi) {
 #define ARGS                                                                                                   \
   variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, out, \
-      out_stride, Hq, Hkv, scl, window, v_scale, sinks
+      out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi
   if (kv_fmt == KV_BF16) launch_prefill<D, KV_BF16>(ARGS);
   else if (kv_fmt == KV_E4M3) launch_prefill<D, KV_E4M3>(ARGS);
   else launch_prefill<D, KV_E5M2>(ARGS);
@@ -1017,7 +1022,8 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
                               const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
                               const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
                               int P, float scale, int window, int kv_fmt, float k_scale, float v_scale,
-                              float softcap, const float* sinks, const float* alibi, hipStream_t stream) {
+                              float softcap, const float* sinks, const float* alibi, const int* row_hi,
+                              hipStream_t stream) {
   if (n_items <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0) return -3;
@@ -1029,7 +1035,7 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
   const int variant = ve ? atoi(ve) : 2;
 #define ARGS                                                                                                     \
   kv_fmt, variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, \
-      out, out_stride, Hq, Hkv, scl, window, v_scale, sinks
+      out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi
   if (D == 64) prefill_dispatch<64>(ARGS);
   else if (D == 256) prefill_dispatch<256>(ARGS);
   else prefill_dispatch<128>(ARGS);

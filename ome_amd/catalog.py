@@ -84,7 +84,8 @@ FAMILIES: list[Family] = [
     Family("gpt-oss-20b", "openai", "openai/gpt-oss-20b", "GptOssForCausalLM", 20.9, "gpt-oss-20b"),
     Family("gpt-oss-120b", "openai", "openai/gpt-oss-120b", "GptOssForCausalLM", 117.0),
     Family("gemma-2-9b-it", "google", "google/gemma-2-9b-it", "Gemma2ForCausalLM", 9.2, "gemma-2-9b"),
-    Family("gemma-3-27b-it", "google", "google/gemma-3-27b-it", "Gemma3ForConditionalGeneration", 27.4),
+    Family("gemma-3-27b-it", "google", "google/gemma-3-27b-it", "Gemma3ForConditionalGeneration", 27.4,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("phi-3-mini-4k-instruct", "microsoft", "microsoft/Phi-3-mini-4k-instruct", "Phi3ForCausalLM", 3.8),
     Family("phi-3-5-moe-instruct", "microsoft", "microsoft/Phi-3.5-MoE-instruct", "PhiMoEForCausalLM", 41.9),
     Family("starcoder2-7b", "bigcode", "bigcode/starcoder2-7b", "Starcoder2ForCausalLM", 7.2, "starcoder2-7b"),

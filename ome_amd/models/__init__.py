@@ -35,6 +35,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.gpt_oss import GptOssForCausalLM
 
         return GptOssForCausalLM
+    if cfg.architecture == "Gemma3ForConditionalGeneration" and (cfg.extra or {}).get("vision_config"):
+        from ome_amd.models.gemma3_vision import Gemma3ForConditionalGeneration
+
+        return Gemma3ForConditionalGeneration
     if cfg.architecture in GEMMA_ARCHS or cfg.model_type in ("gemma", "gemma2", "gemma3", "gemma3_text"):
         from ome_amd.models.gemma import GemmaForCausalLM
 

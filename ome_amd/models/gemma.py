@@ -173,16 +173,18 @@ class GemmaForCausalLM(LlamaForCausalLM):
         if meta.is_decode:
             return ops.paged_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale, meta.decode_ws,
                                     w, order=meta.order, k_scale=ks, v_scale=vs, softcap=cap)
+        hi = meta.extra.get("row_hi") if meta.extra else None  # Gemma 3 bidirectional image blocks
         if meta.mode == "mixed":
             n = meta.num_prefill
             out = torch.empty_like(q)
             ops.paged_prefill(q[:n], k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
-                              self.scale, w, out=out[:n], k_scale=ks, v_scale=vs, softcap=cap)
+                              self.scale, w, out=out[:n], k_scale=ks, v_scale=vs, softcap=cap,
+                              row_hi=None if hi is None else hi[:n])
             ops.paged_decode(q[n:], k_cache, v_cache, meta.dec_block_tables, meta.seq_lens, self.scale,
                              meta.decode_ws, w, out=out[n:], order=meta.order, k_scale=ks, v_scale=vs, softcap=cap)
             return out
         return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
-                                 self.scale, w, k_scale=ks, v_scale=vs, softcap=cap)
+                                 self.scale, w, k_scale=ks, v_scale=vs, softcap=cap, row_hi=hi)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = super().compute_logits(hidden)

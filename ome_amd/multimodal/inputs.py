@@ -30,6 +30,7 @@ class MMInput:
     mrope_pos: np.ndarray | None = None        # [3, prompt_len] int64 (None: plain 1D positions)
     rope_delta: int = 0                        # decode position offset (max mrope pos + 1 - len)
     features: torch.Tensor | None = field(default=None, repr=False)  # [sum tokens, H] on device
+    atomic: bool = False                       # spans attend bidirectionally: never split a span across chunks
 
     @property
     def num_tokens(self) -> int:

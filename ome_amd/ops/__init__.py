@@ -428,13 +428,15 @@ def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) ->
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale, window: int = -1,
                   out=None, k_scale: float = 1.0, v_scale: float = 1.0, softcap: float = 0.0,
-                  sinks: torch.Tensor | None = None, alibi: torch.Tensor | None = None) -> torch.Tensor:
+                  sinks: torch.Tensor | None = None, alibi: torch.Tensor | None = None,
+                  row_hi: torch.Tensor | None = None) -> torch.Tensor:
     """q [Tq, Hq, D]; items int32 [n, 2] from :func:`prefill_work_items`.  ``softcap`` > 0:
     attention-logit soft-capping ``cap * tanh(score / cap)`` (Gemma-2); ``alibi``: fp32 [Hq]
-    ALiBi slopes."""
+    ALiBi slopes; ``row_hi``: int32 [Tq], per query row the last key position it may see
+    beyond the causal one (-1: causal) -- Gemma 3's bidirectional image blocks."""
     if not _gpu(q):
         r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window, k_scale, v_scale,
-                              softcap, sinks, alibi)
+                              softcap, sinks, alibi, row_hi)
         if out is not None:
             out.copy_(r)
             return out
@@ -446,7 +448,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
          _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),
          int(window), kv_format(k_cache), float(k_scale), float(v_scale), float(softcap), _sinks(sinks),
-         _sinks(alibi), stream_ptr())
+         _sinks(alibi), None if row_hi is None else _i32(row_hi).data_ptr(), stream_ptr())
     return out
 
 

@@ -230,7 +230,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, 
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window=-1, k_scale=1.0,
-                  v_scale=1.0, softcap=0.0, sinks=None, alibi=None) -> torch.Tensor:
+                  v_scale=1.0, softcap=0.0, sinks=None, alibi=None, row_hi=None) -> torch.Tensor:
     Tq, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -243,7 +243,8 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, windo
             continue
         qpos = torch.arange(L - ql, L, device=q.device)[:, None]
         kpos = torch.arange(L, device=q.device)[None, :]
-        mask = kpos <= qpos
+        qlim = qpos if row_hi is None else torch.maximum(qpos, row_hi[q0:q1].to(q.device).long()[:, None])
+        mask = kpos <= qlim
         mask &= kpos >= attn_lo(qpos, window)
         for h in range(Hkv):
             k, v = gather_kv(k_cache, v_cache, block_tables[s], L, h, P, k_scale, v_scale)

@@ -550,6 +550,8 @@ class ModelRunner:
         that reaches one of its images; freed once the prompt is fully cached)."""
         m = self.model
         p3 = np.empty((3, T), dtype=np.int64)
+        bidir = getattr(m, "bidirectional_images", False)
+        hi_rows = np.full(T, -1, dtype=np.int32) if bidir else None   # last visible key per row (image blocks)
         rows, feats, row = [], [], 0
         for i in order:
             c = chunks[i]
@@ -576,11 +578,15 @@ class ModelRunner:
                             mm.features = m.encode_images(mm.pixel_values, mm.grid_thw)
                         rows.extend(range(row + lo - c.start, row + hi - c.start))
                         feats.append(mm.features[off + lo - s: off + hi - s])
+                        if bidir:
+                            hi_rows[row + lo - c.start:row + hi - c.start] = s + n - 1
                     off += n
                 if c.start + L >= plen:
                     mm.features = None  # prompt fully scheduled: image features no longer needed
             row += L
         dv = self.device
+        if bidir:
+            meta.extra["row_hi"] = torch.from_numpy(hi_rows).to(dv)
         if any(chunks[i].req.mm is not None and chunks[i].req.mm.mrope_pos is not None for i in order):
             meta.extra["rope"] = (torch.arange(T, dtype=torch.int32, device=dv), m.mrope_table(torch.from_numpy(p3)))
         r_dev = torch.tensor(rows, dtype=torch.long, device=dv)

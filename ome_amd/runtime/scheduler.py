@@ -165,6 +165,20 @@ class Scheduler:
             return batch
         return self._schedule_decode()
 
+    @staticmethod
+    def _span_safe(r, n: int) -> int:
+        """Chunk length that does not end inside an atomic multimodal span (bidirectional image
+        blocks): cut before the span, or take the whole span when the chunk starts inside it."""
+        mm = r.mm
+        if mm is None or not getattr(mm, "atomic", False):
+            return n
+        a, end = r.num_cached, r.num_cached + n
+        for s, k in mm.spans:
+            if s < end < s + k:
+                end = s if s > a else s + k
+                break
+        return max(1, min(end, r.seq_len) - a)
+
     def _schedule_prefill(self) -> StepBatch | None:
         budget = self.chunk
         chunks: list[ScheduledChunk] = []
@@ -173,7 +187,7 @@ class Scheduler:
             if budget <= 0:
                 break
             if r.num_cached < r.seq_len - 1:
-                n = min(r.seq_len - r.num_cached, budget)
+                n = self._span_safe(r, min(r.seq_len - r.num_cached, budget))
                 if not self._grow(r, r.num_cached + n):
                     break
                 chunks.append(ScheduledChunk(r, r.num_cached, n, r.num_cached + n == r.seq_len))
@@ -197,7 +211,7 @@ class Scheduler:
                     r.pages = list(hit_pages)
                     self.slots.set_pages(r.req_slot, 0, hit_pages)
                     r.num_cached = r.num_prefix_hit = len(hit_pages) * self.P
-            n = min(r.seq_len - r.num_cached, budget)
+            n = self._span_safe(r, min(r.seq_len - r.num_cached, budget))
             if not self._grow(r, r.num_cached + n):
                 if not self.running and not chunks:
                     # cannot fit even alone: fail the request instead of spinning
