@@ -132,6 +132,10 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
     Family("bge-reranker-v2-m3", "baai", "BAAI/bge-reranker-v2-m3", "XLMRobertaForSequenceClassification", 0.568,
            capabilities=["TEXT_RERANK"], args=["--is-embedding"]),
+    Family("llama-3-3-nemotron-super-49b-v1", "nvidia", "nvidia/Llama-3_3-Nemotron-Super-49B-v1", "DeciLMForCausalLM",
+           49.9),
+    Family("llama-3-1-nemotron-ultra-253b-v1", "nvidia", "nvidia/Llama-3_1-Nemotron-Ultra-253B-v1", "DeciLMForCausalLM",
+           253.0, None, 1.0, quantization="fp8"),
     Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
 ]

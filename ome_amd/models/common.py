@@ -73,13 +73,17 @@ class PagedKVCache:
         slice of it); ``None``: same width as the keys.  ``layers``: the global layer ids held
         here (a pipeline stage's slice); other entries of ``k`` / ``v`` are None."""
         self.num_layers, self.num_pages, self.page_size = num_layers, num_pages, page_size
-        self.num_kv_heads, self.head_dim, self.dtype = num_kv_heads, head_dim, dtype
+        # ``num_kv_heads``: one count, or a {layer: heads} map (DeciLM / Nemotron-NAS: per-layer GQA)
+        per = num_kv_heads if isinstance(num_kv_heads, dict) else None
+        self.num_kv_heads = max(per.values()) if per else num_kv_heads
+        self.head_dim, self.dtype = head_dim, dtype
         self.v_dim = head_dim if v_dim is None else v_dim
         self.local_layers = list(range(num_layers)) if layers is None else list(layers)
         own = set(self.local_layers)
-        self.k = [torch.zeros(num_pages, num_kv_heads, page_size, head_dim, dtype=dtype, device=device)
+        hk = (lambda i: per[i]) if per else (lambda i: num_kv_heads)  # noqa: E731
+        self.k = [torch.zeros(num_pages, hk(i), page_size, head_dim, dtype=dtype, device=device)
                   if i in own else None for i in range(num_layers)]
-        self.v = [torch.zeros(num_pages, num_kv_heads, self.v_dim, page_size, dtype=dtype, device=device)
+        self.v = [torch.zeros(num_pages, hk(i), self.v_dim, page_size, dtype=dtype, device=device)
                   if i in own else None for i in range(num_layers)]
         self.k_scale = [1.0] * num_layers
         self.v_scale = [1.0] * num_layers
@@ -101,7 +105,8 @@ class PagedKVCache:
     def bytes_per_page(num_layers: int, num_kv_heads: int, head_dim: int, page_size: int, dtype=torch.bfloat16,
                        v_dim: int | None = None) -> int:
         v = head_dim if v_dim is None else v_dim
-        return num_layers * num_kv_heads * (head_dim + v) * page_size * torch.tensor([], dtype=dtype).element_size()
+        heads = sum(num_kv_heads.values()) if isinstance(num_kv_heads, dict) else num_layers * num_kv_heads
+        return heads * (head_dim + v) * page_size * torch.tensor([], dtype=dtype).element_size()
 
     def layer(self, i: int) -> tuple[torch.Tensor, torch.Tensor]:
         return self.k[i], self.v[i]

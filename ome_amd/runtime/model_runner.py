@@ -109,6 +109,8 @@ class ModelRunner:
         kv_heads, k_dim, v_dim = getattr(self.model, "kv_layout", (tp.hkv, cfg.head_dim, cfg.head_dim))
         kv_layers = getattr(self.model, "kv_layers", None)  # hybrid models: only attention layers own KV
         n_local = len(self.model.layers if kv_layers is None else kv_layers)
+        if getattr(self.model, "kv_heads_per_layer", None):   # per-layer GQA (DeciLM): {layer: local heads}
+            kv_heads = dict(self.model.kv_heads_per_layer)
         kv_dtype = kv_cache_dtype(kv_cache_dtype_name, dtype)
         if kv_dtype != dtype and getattr(self.model, "kv_layout", None) is not None:
             # MLA's latent cache (mla.hip) keeps the model dtype
