@@ -71,6 +71,10 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("mimo-vl-7b-rl", "xiaomimimo", "XiaomiMiMo/MiMo-VL-7B-RL", "Qwen2_5_VLForConditionalGeneration", 8.3,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("llava-v1-5-13b", "liuhaotian", "liuhaotian/llava-v1.5-13b", "LlavaLlamaForCausalLM", 13.4,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("llava-1-5-7b-hf", "llava-hf", "llava-hf/llava-1.5-7b-hf", "LlavaForConditionalGeneration", 7.1,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("llama-3-2-11b-vision-instruct", "meta", "meta-llama/Llama-3.2-11B-Vision-Instruct",
            "MllamaForConditionalGeneration", 10.7, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("llama-3-2-90b-vision-instruct", "meta", "meta-llama/Llama-3.2-90B-Vision-Instruct",
