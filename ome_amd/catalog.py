@@ -140,6 +140,8 @@ FAMILIES: list[Family] = [
            49.9),
     Family("llama-3-1-nemotron-ultra-253b-v1", "nvidia", "nvidia/Llama-3_1-Nemotron-Ultra-253B-v1", "DeciLMForCausalLM",
            253.0, None, 1.0, quantization="fp8"),
+    Family("clip-vit-large-patch14-336", "openai", "openai/clip-vit-large-patch14-336", "CLIPModel", 0.428,
+           capabilities=["TEXT_EMBEDDINGS", "EMBEDDING"], args=["--is-embedding"]),
     Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
 ]

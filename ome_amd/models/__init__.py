@@ -67,6 +67,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.mllama import MllamaForConditionalGeneration
 
         return MllamaForConditionalGeneration
+    if cfg.architecture == "CLIPModel":
+        from ome_amd.models.clip import CLIPModel
+
+        return CLIPModel
     if cfg.architecture in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM"):
         from ome_amd.models.llava import LlavaForConditionalGeneration
 
@@ -108,6 +112,7 @@ def supported(arch: str) -> bool:
     return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or arch in NEMOTRON_H_ARCHS or \
         arch in DECODER_ARCHS or arch in ENCODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
         arch == "DeciLMForCausalLM" or arch in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM") or \
+        arch == "CLIPModel" or \
         arch == "GptOssForCausalLM"
 
 

@@ -611,8 +611,22 @@ class ModelRunner:
         self.model.forward(z, meta, self.kv)
 
     def embed(self, batch: StepBatch) -> list[list[float]]:
-        """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts."""
+        """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts
+        (model-specific pooling / heads via ``model.pool``; image requests of models with
+        ``embed_images``, e.g. CLIP, go through the vision side in one batch)."""
         self.slots.flush()  # block-table rows of the newly admitted requests
+        m = self.model
+        if hasattr(m, "embed_images") and any(c.req.mm is not None for c in batch.chunks):
+            img = [k for k, c in enumerate(batch.chunks) if c.req.mm is not None]
+            txt = [k for k, c in enumerate(batch.chunks) if c.req.mm is None]
+            res: list = [None] * len(batch.chunks)
+            e = m.embed_images(torch.cat([batch.chunks[k].req.mm.pixel_values for k in img]))
+            for k, v in zip(img, e.cpu().tolist()):
+                res[k] = v
+            if txt:
+                for k, v in zip(txt, self.embed(StepBatch(batch.mode, [batch.chunks[k] for k in txt]))):
+                    res[k] = v
+            return res
         P = self.P
         ids, pos, slots, q_lens, req_idx = [], [], [], [], []
         for c in batch.chunks:

@@ -396,16 +396,23 @@ def create_app(engine, ns=None):
         from ome_amd.runtime.request import SamplingParams
 
         for i, x in enumerate(items):
-            ids = list(x) if isinstance(x, list) else encode_text(str(x))
-            total += len(ids)
-            out.append({"object": "embedding", "index": i, "embedding": await _embed_ids(ids)})
+            if isinstance(x, dict) and ("image" in x or "image_url" in x):   # CLIP-style image embedding
+                im = x.get("image") or (x.get("image_url") or {}).get("url")
+                emb = await _embed_ids([], images=[im])
+            else:
+                if isinstance(x, dict):
+                    x = x.get("text", "")
+                ids = list(x) if isinstance(x, list) else encode_text(str(x))
+                total += len(ids)
+                emb = await _embed_ids(ids)
+            out.append({"object": "embedding", "index": i, "embedding": emb})
         return {"object": "list", "data": out, "model": model_name,
                 "usage": {"prompt_tokens": total, "total_tokens": total}}
 
-    async def _embed_ids(ids: list[int]) -> list[float]:
+    async def _embed_ids(ids: list[int], images=None) -> list[float]:
         from ome_amd.runtime.request import SamplingParams
 
-        req, stream = await run_request(ids, SamplingParams(max_new_tokens=0))
+        req, stream = await run_request(ids, SamplingParams(max_new_tokens=0), images=images)
         req.is_embedding = True
         while True:
             _, fin = await stream.q.get()
