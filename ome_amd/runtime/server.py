@@ -82,6 +82,11 @@ def build_parser() -> argparse.ArgumentParser:
     a("--disaggregation-bootstrap-port", type=int, default=8998)
     a("--log-requests", action="store_true")
     a("--num-layers", type=int, default=None, help="debug: truncate the model")
+    a("--tool-call-parser", default=None,
+      help="llama3_json | pythonic | qwen3_coder | hermes | qwen25 | nano_v3 | gpt-oss | mistral")
+    a("--reasoning-parser", default=None, help="deepseek-r1 | qwen3 | nano_v3 | gpt-oss")
+    a("--enable-auto-tool-choice", action="store_true", help="accepted (tool_choice=auto is the default)")
+    a("--chat-template", default=None, help="path of a Jinja chat template replacing the tokenizer's")
     return ap
 
 
@@ -153,6 +158,16 @@ def create_app(engine, ns=None):
     app = FastAPI(title="ome_amd runtime")
     tok = engine.tokenizer
     model_name = engine.served_model_name
+    from ome_amd.runtime.parsers import ReasoningParser, ToolParser
+
+    tool_kind = getattr(ns, "tool_call_parser", None) if ns is not None else None
+    reason_kind = getattr(ns, "reasoning_parser", None) if ns is not None else None
+    if tool_kind:
+        ToolParser(tool_kind)  # validate the name at startup
+    tpl = getattr(ns, "chat_template", None) if ns is not None else None
+    if tpl and os.path.exists(tpl) and hasattr(tok, "chat_template"):
+        with open(tpl) as f:
+            tok.chat_template = f.read()
     encoder = bool(getattr(getattr(engine, "runner", None), "model", None) is not None and
                    getattr(engine.runner.model, "encoder_only", False))
 
@@ -258,7 +273,8 @@ def create_app(engine, ns=None):
             if not isinstance(msgs, list) or not msgs:
                 raise ValueError("messages must be a non-empty list")
             msgs, images = _chat_images(msgs)
-            text = tok.apply_chat_template(msgs, add_generation_prompt=True)
+            tools = body.get("tools") if body.get("tool_choice", "auto") != "none" else None
+            text = tok.apply_chat_template(msgs, add_generation_prompt=True, tools=tools)
             if not images:
                 return tok.encode(text), []
             m = engine.runner.model
@@ -304,10 +320,16 @@ def create_app(engine, ns=None):
             return {"prompt_tokens": len(ids), "completion_tokens": len(req.output_ids),
                     "total_tokens": len(ids) + len(req.output_ids)}
 
+        use_tools = bool(chat and tool_kind and body.get("tools") and body.get("tool_choice", "auto") != "none")
+        use_reason = bool(chat and reason_kind and body.get("separate_reasoning", True))
+
         if body.get("stream"):
             async def gen():
                 sent = ""
                 first = True
+                rp = ReasoningParser(reason_kind) if use_reason else None
+                tp = ToolParser(tool_kind) if use_tools else None
+                content_all, content_sent, calls_started = "", 0, False
                 while True:
                     toks, fin = await stream.q.get()
                     text = tok.decode(req.output_ids)
@@ -318,17 +340,50 @@ def create_app(engine, ns=None):
                     delta = text[len(sent):]
                     sent = text
                     if chat:
-                        d = {"content": delta}
+                        d: dict = {}
+                        if rp is not None:
+                            rd, cd = rp.feed(delta)
+                            if fin:
+                                fr, fc = rp.flush()
+                                rd, cd = rd + fr, cd + fc
+                            if rd:
+                                d["reasoning_content"] = rd
+                        else:
+                            cd = delta
+                        content_all += cd
+                        if tp is not None and not calls_started:
+                            i = tp.start_index(content_all)
+                            if i >= 0:
+                                calls_started = True
+                                cd = content_all[content_sent:i]
+                            else:   # hold back a suffix that may still become a call marker
+                                cd = content_all[content_sent:len(content_all) if fin else tp.safe_len(content_all)]
+                        elif tp is not None:
+                            cd = ""
+                        content_sent += len(cd)
+                        if cd or not d:
+                            d["content"] = cd
                         if first:
                             d["role"] = "assistant"
+                        finish = None
+                        if fin and calls_started:
+                            _, calls = tp.parse(content_all)
+                            if calls:
+                                d["tool_calls"] = [{"index": k, **c} for k, c in enumerate(calls)]
+                                finish = "tool_calls"
+                            elif content_all[content_sent:]:   # not a call after all: release the text
+                                d["content"] = d.get("content", "") + content_all[content_sent:]
                         choice = {"index": 0, "delta": d, "finish_reason": None}
                         chunk_obj = "chat.completion.chunk"
+                        if finish:
+                            choice["_finish"] = finish
                     else:
                         choice = {"index": 0, "text": delta, "finish_reason": None}
                         chunk_obj = "text_completion"
                     first = False
+                    forced = choice.pop("_finish", None)
                     if fin:
-                        choice["finish_reason"] = "stop" if cut is not None else _finish(req)
+                        choice["finish_reason"] = forced or ("stop" if cut is not None else _finish(req))
                     out = {"id": rid, "object": chunk_obj, "created": int(time.time()), "model": model_name,
                            "choices": [choice]}
                     if fin and (body.get("stream_options") or {}).get("include_usage", True):
@@ -354,7 +409,15 @@ def create_app(engine, ns=None):
         if cut is not None:
             text, reason = text[:cut], "stop"
         if chat:
-            choice = {"index": 0, "message": {"role": "assistant", "content": text}, "finish_reason": reason}
+            msg: dict = {"role": "assistant", "content": text}
+            if use_reason:
+                r, msg["content"] = ReasoningParser(reason_kind).split(text)
+                msg["reasoning_content"] = r
+            if use_tools:
+                content, calls = ToolParser(tool_kind).parse(msg["content"])
+                if calls:
+                    msg["content"], msg["tool_calls"], reason = content or None, calls, "tool_calls"
+            choice = {"index": 0, "message": msg, "finish_reason": reason}
         else:
             choice = {"index": 0, "text": text, "finish_reason": reason, "logprobs": None}
         if params.logprobs:

@@ -37,8 +37,10 @@ class ByteTokenizer:
                 out.extend(f"<{i}>".encode())
         return out.decode("utf-8", errors="replace")
 
-    def apply_chat_template(self, messages: list[dict], add_generation_prompt: bool = True) -> str:
+    def apply_chat_template(self, messages: list[dict], add_generation_prompt: bool = True, tools=None) -> str:
         parts = []
+        if tools:
+            parts.append("<|tools|>\n" + json.dumps(tools) + "\n")
         for m in messages:
             content = m.get("content", "")
             if isinstance(content, list):
@@ -84,16 +86,19 @@ class HFTokenizer:
     def decode(self, ids, skip_special: bool = True) -> str:
         return self.tok.decode([int(i) for i in ids], skip_special_tokens=skip_special)
 
-    def apply_chat_template(self, messages: list[dict], add_generation_prompt: bool = True) -> str:
+    def apply_chat_template(self, messages: list[dict], add_generation_prompt: bool = True, tools=None) -> str:
         if self.chat_template:
             try:
                 import jinja2
 
-                t = jinja2.Environment().from_string(self.chat_template)
-                return t.render(messages=messages, add_generation_prompt=add_generation_prompt, bos_token="")
+                env = jinja2.Environment()
+                env.filters.setdefault("tojson", lambda v, indent=None: json.dumps(v, indent=indent))
+                t = env.from_string(self.chat_template)
+                return t.render(messages=messages, add_generation_prompt=add_generation_prompt, bos_token="",
+                                tools=tools)
             except Exception:  # noqa: BLE001 — template dialects vary; fall back to plain format
                 pass
-        return ByteTokenizer.apply_chat_template(self, messages, add_generation_prompt)  # type: ignore[arg-type]
+        return ByteTokenizer.apply_chat_template(self, messages, add_generation_prompt, tools)  # type: ignore[arg-type]
 
 
 def get_tokenizer(model_path: str | None, vocab_size: int = 128256):
