@@ -433,6 +433,53 @@ def create_app(engine, ns=None):
     async def chat(request: Request):
         return await _complete(await request.json(), True)
 
+    @app.post("/v1/responses")
+    async def responses(request: Request):
+        """OpenAI Responses API (``OPENAI_V1_RESPONSES`` in the API capabilities), mapped onto the
+        chat path: ``input`` (string or message list) + ``instructions`` -> messages; the reply
+        becomes ``output`` items (reasoning, message with ``output_text``, function calls)."""
+        body = await request.json()
+        inp = body.get("input")
+        msgs = [{"role": "system", "content": body["instructions"]}] if body.get("instructions") else []
+        if isinstance(inp, str):
+            msgs.append({"role": "user", "content": inp})
+        elif isinstance(inp, list):
+            for m in inp:
+                c = m.get("content")
+                if isinstance(c, list):   # input_text / input_image parts -> chat parts
+                    c = [{"type": "text", "text": p.get("text", "")} if p.get("type") in ("input_text", "text")
+                         else {"type": "image_url", "image_url": {"url": p.get("image_url")}} for p in c]
+                msgs.append({"role": m.get("role", "user"), "content": c})
+        else:
+            return err(400, "input must be a string or a list of messages")
+        tools = [{"type": "function", "function": {k: t[k] for k in ("name", "description", "parameters") if k in t}}
+                 if "function" not in t else t for t in (body.get("tools") or [])]
+        chat_body = {"messages": msgs, "max_tokens": body.get("max_output_tokens"), "temperature": body.get("temperature"),
+                     "top_p": body.get("top_p"), "tools": tools or None, "tool_choice": body.get("tool_choice", "auto")}
+        res = await _complete({k: v for k, v in chat_body.items() if v is not None}, True)
+        if not isinstance(res, dict):
+            return res
+        m = res["choices"][0]["message"]
+        out = []
+        if m.get("reasoning_content"):
+            out.append({"type": "reasoning", "id": f"rs_{uuid.uuid4().hex[:16]}",
+                        "summary": [{"type": "summary_text", "text": m["reasoning_content"]}]})
+        for c in m.get("tool_calls") or []:
+            out.append({"type": "function_call", "id": f"fc_{uuid.uuid4().hex[:16]}", "call_id": c["id"],
+                        "name": c["function"]["name"], "arguments": c["function"]["arguments"], "status": "completed"})
+        if m.get("content"):
+            out.append({"type": "message", "id": f"msg_{uuid.uuid4().hex[:16]}", "role": "assistant",
+                        "status": "completed", "content": [{"type": "output_text", "text": m["content"],
+                                                            "annotations": []}]})
+        u = res["usage"]
+        done = res["choices"][0]["finish_reason"] != "length"
+        return {"id": f"resp_{uuid.uuid4().hex[:24]}", "object": "response", "created_at": int(time.time()),
+                "model": model_name, "status": "completed" if done else "incomplete",
+                "incomplete_details": None if done else {"reason": "max_output_tokens"}, "output": out,
+                "output_text": m.get("content") or "",
+                "usage": {"input_tokens": u["prompt_tokens"], "output_tokens": u["completion_tokens"],
+                          "total_tokens": u["total_tokens"]}}
+
     @app.post("/v1/completions")
     async def completions(request: Request):
         return await _complete(await request.json(), False)

@@ -131,3 +131,16 @@ def test_chat_plain_text_with_parsers(scripted):
     r = c.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "hi"}], "tools": TOOLS}).json()
     m = r["choices"][0]["message"]
     assert m["content"] == "Just an answer." and "tool_calls" not in m and m["reasoning_content"] is None
+
+
+def test_responses_api(scripted):
+    c = scripted('weigh it</think>Final. <|python_tag|>{"name": "get_weather", "parameters": {"city": "Oslo"}}')
+    r = c.post("/v1/responses", json={"input": "weather in Oslo?", "instructions": "be brief",
+                                      "tools": [{"type": "function", "name": "get_weather",
+                                                 "parameters": {"type": "object"}}]}).json()
+    kinds = [o["type"] for o in r["output"]]
+    assert r["object"] == "response" and r["status"] == "completed"
+    assert kinds == ["reasoning", "function_call", "message"], kinds
+    fc = r["output"][1]
+    assert fc["name"] == "get_weather" and json.loads(fc["arguments"]) == {"city": "Oslo"}
+    assert r["output_text"] == "Final." and r["usage"]["output_tokens"] > 0
