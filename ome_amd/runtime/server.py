@@ -304,7 +304,34 @@ def create_app(engine, ns=None):
         idx = [text.find(s) for s in stops if s and s in text]
         return min(idx) if idx else None
 
+    def _logprobs(req, chat: bool):
+        toks = [tok.decode([t], skip_special=False) for t in req.output_ids]
+        if chat:
+            return {"content": [{"token": t, "logprob": lp, "bytes": list(t.encode("utf-8")), "top_logprobs": []}
+                                for t, lp in zip(toks, req.output_logprobs)]}
+        offs, o = [], 0
+        for t in toks:
+            offs.append(o)
+            o += len(t)
+        return {"tokens": toks, "token_logprobs": list(req.output_logprobs), "top_logprobs": None,
+                "text_offset": offs}
+
     async def _complete(body: dict, chat: bool):
+        n = int(body.get("n") or 1)
+        if n > 1:   # n choices = n independent requests (distinct seeds), one batched engine run
+            if body.get("stream"):
+                return err(400, "n > 1 is not supported with stream=true")
+            seed = body.get("seed")
+            subs = await asyncio.gather(*[_complete({**body, "n": 1, "seed": None if seed is None else seed + i},
+                                                    chat) for i in range(n)])
+            for s_ in subs:
+                if not isinstance(s_, dict):
+                    return s_
+            out = subs[0]
+            out["choices"] = [{**s_["choices"][0], "index": i} for i, s_ in enumerate(subs)]
+            ct = sum(s_["usage"]["completion_tokens"] for s_ in subs)
+            out["usage"] = {**out["usage"], "completion_tokens": ct, "total_tokens": out["usage"]["prompt_tokens"] + ct}
+            return out
         try:
             ids, images = _encode(body, chat)
             params = _sampling_from(body, default_max)
@@ -421,7 +448,7 @@ def create_app(engine, ns=None):
         else:
             choice = {"index": 0, "text": text, "finish_reason": reason, "logprobs": None}
         if params.logprobs:
-            choice["logprobs"] = {"token_logprobs": req.output_logprobs, "tokens": req.output_ids}
+            choice["logprobs"] = _logprobs(req, chat)
         return {"id": rid, "object": obj, "created": int(time.time()), "model": model_name, "choices": [choice],
                 "usage": usage()}
 

@@ -93,3 +93,16 @@ def test_chat_with_image_data_url():
     eng2 = Engine(EngineArgs(model="tiny-llama", device="cpu", max_running_requests=4, context_length=256))
     with TestClient(create_app(eng2)) as c:
         assert c.post("/v1/chat/completions", json={"messages": msg}).status_code == 400
+
+
+def test_n_choices_and_logprobs_format(client):
+    r = client.post("/v1/chat/completions", json={
+        "model": "tiny", "messages": [{"role": "user", "content": "hi"}], "max_tokens": 3, "n": 3, "seed": 7,
+        "temperature": 1.0, "ignore_eos": True, "logprobs": True}).json()
+    assert [c["index"] for c in r["choices"]] == [0, 1, 2] and r["usage"]["completion_tokens"] == 9
+    lp = r["choices"][0]["logprobs"]["content"]
+    assert len(lp) == 3 and all(isinstance(x["logprob"], float) and x["logprob"] <= 0 for x in lp)
+    c = client.post("/v1/completions", json={"model": "tiny", "prompt": "abc", "max_tokens": 2, "logprobs": 1,
+                                             "temperature": 0, "ignore_eos": True}).json()
+    lp = c["choices"][0]["logprobs"]
+    assert len(lp["tokens"]) == 2 and len(lp["token_logprobs"]) == 2 and lp["text_offset"][0] == 0
