@@ -137,6 +137,7 @@ class Engine:
         # (input packing + kernel / graph enqueue) / wait (blocked on the GPU) / commit
         self.host_times = {"schedule": 0.0, "launch": 0.0, "wait": 0.0, "commit": 0.0, "steps": 0}
         self.host_trace: list | None = None   # per-call (kind, rows, t_a, t_b) when profiling
+        self.metrics.host_times = self.host_times
         ov = self.runner.is_cuda if args.overlap_schedule is None else bool(args.overlap_schedule)
         self.overlap = ov and not self.cfg.is_embedding and self.pstate.pp_size == 1 and not self.dp
 

@@ -67,6 +67,7 @@ class EngineMetrics:
         self.step_decode = Histogram()
         self._window: list[tuple[float, int]] = []
         self.preemptions = 0
+        self.host_times: dict | None = None   # engine's host phase split (schedule / launch / wait / commit)
 
     def on_arrival(self, req) -> None:
         with self.lock:
@@ -125,6 +126,10 @@ class EngineMetrics:
                 lines += [f"# TYPE {k} gauge", f"{k}{{{m}}} {v}"]
             for k, v in counters.items():
                 lines += [f"# TYPE {k} counter", f"{k}{{{m}}} {v}"]
+            if self.host_times:   # per-phase host time of the serving loop (SURVEY §5.1 step timer)
+                lines.append("# TYPE ome:host_phase_seconds_total counter")
+                lines += [f'ome:host_phase_seconds_total{{{m},phase="{ph}"}} {self.host_times[ph]}'
+                          for ph in ("schedule", "launch", "wait", "commit") if ph in self.host_times]
             for name, h in (("sglang:time_to_first_token_seconds", self.ttft),
                             ("vllm:time_to_first_token_seconds", self.ttft),
                             ("sglang:time_per_output_token_seconds", self.tpot),

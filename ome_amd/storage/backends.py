@@ -63,17 +63,24 @@ def _md5(path: Path) -> str:
 
 
 def _copy(src: Path, dst: Path) -> None:
+    """Copy into ``<dst>.ome-part`` then rename: a crashed or cancelled download never leaves a
+    full-size partial file behind, so a resumed fetch (size check in :func:`_copy_tree`) redoes
+    exactly the files that did not complete (the reference's OCI multipart temp-file + atomic
+    rename, ``pkg/ociobjectstore/os_parallel_download.go:110-200``)."""
     dst.parent.mkdir(parents=True, exist_ok=True)
+    part = dst.with_name(dst.name + ".ome-part")
     try:
         from ome_amd.io import native
 
         if native.available():
-            native.copy_file(src, dst, threads=8)
-            shutil.copystat(src, dst)
+            native.copy_file(src, part, threads=8)
+            shutil.copystat(src, part)
+            os.replace(part, dst)
             return
     except ImportError:
         pass
-    shutil.copy2(src, dst)
+    shutil.copy2(src, part)
+    os.replace(part, dst)
 
 
 def _copy_tree(src: Path, dest: Path, progress: Progress | None, verify: dict | None = None) -> FetchResult:

@@ -47,7 +47,8 @@ def test_chat_stream(client):
 def test_metrics_names(client):
     txt = client.get("/metrics").text
     for name in ("vllm:request_success_total", "vllm:avg_generation_throughput_toks_per_s",
-                 "sglang:time_to_first_token_seconds_bucket", "sglang:num_running_reqs"):
+                 "sglang:time_to_first_token_seconds_bucket", "sglang:num_running_reqs",
+                 'ome:host_phase_seconds_total{model_name="tiny",phase="launch"}'):
         assert name in txt
 
 
