@@ -71,6 +71,11 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("mimo-vl-7b-rl", "xiaomimimo", "XiaomiMiMo/MiMo-VL-7B-RL", "Qwen2_5_VLForConditionalGeneration", 8.3,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("qwen3-vl-8b-instruct", "qwen", "Qwen/Qwen3-VL-8B-Instruct", "Qwen3VLForConditionalGeneration", 8.8,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("qwen3-vl-235b-a22b-instruct", "qwen", "Qwen/Qwen3-VL-235B-A22B-Instruct",
+           "Qwen3VLMoeForConditionalGeneration", 236.0, None, 1.0, quantization="fp8",
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("llava-v1-5-13b", "liuhaotian", "liuhaotian/llava-v1.5-13b", "LlavaLlamaForCausalLM", 13.4,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("llava-1-5-7b-hf", "llava-hf", "llava-hf/llava-1.5-7b-hf", "LlavaForConditionalGeneration", 7.1,

@@ -20,7 +20,8 @@ DENSE_ARCHS = {
 GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
 LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalLM"}
 LLAMA4_ARCHS = {"Llama4ForCausalLM", "Llama4ForConditionalGeneration"}
-QWEN2_VL_ARCHS = {"Qwen2VLForConditionalGeneration", "Qwen2_5_VLForConditionalGeneration"}
+QWEN2_VL_ARCHS = {"Qwen2VLForConditionalGeneration", "Qwen2_5_VLForConditionalGeneration",
+                  "Qwen3VLForConditionalGeneration", "Qwen3VLMoeForConditionalGeneration"}
 NEMOTRON_H_ARCHS = {"NemotronHForCausalLM"}
 from ome_amd.models.config import PADDED_HEAD_ARCHS as DECODER_ARCHS  # noqa: E402  (models/decoder.py)
 
@@ -47,6 +48,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.nemotron_h import NemotronHForCausalLM
 
         return NemotronHForCausalLM
+    if cfg.architecture in ("Qwen3VLForConditionalGeneration", "Qwen3VLMoeForConditionalGeneration"):
+        from ome_amd.models.qwen3_vl import Qwen3VLForConditionalGeneration, Qwen3VLMoeForConditionalGeneration
+
+        return Qwen3VLMoeForConditionalGeneration if cfg.is_moe else Qwen3VLForConditionalGeneration
     if cfg.architecture == "Qwen2_5_VLForConditionalGeneration" or cfg.model_type == "qwen2_5_vl":
         from ome_amd.models.qwen2_vl import Qwen2_5_VLForConditionalGeneration
 

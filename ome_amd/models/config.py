@@ -247,7 +247,8 @@ class ModelConfig:
             max_position_embeddings=text.get("max_position_embeddings", 4096),
             tie_word_embeddings=bool(cfg.get("tie_word_embeddings", text.get("tie_word_embeddings", False))),
             attention_bias=bool(text.get("attention_bias", text.get("use_bias", mt in ("qwen2", "qwen2_moe", "qwen2_vl", "qwen2_vl_text", "qwen2_5_vl", "qwen2_5_vl_text", "phi")))),
-            qk_norm=mt in ("qwen3", "qwen3_moe", "gemma3", "gemma3_text"),
+            qk_norm=mt in ("qwen3", "qwen3_moe", "gemma3", "gemma3_text", "qwen3_vl", "qwen3_vl_text", "qwen3_vl_moe",
+                           "qwen3_vl_moe_text"),
             hidden_act=text.get("hidden_act", text.get("hidden_activation", "silu")),
             sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt in ("mistral", "starcoder2", "phi3")) else None,
             torch_dtype=str(text.get("torch_dtype", cfg.get("torch_dtype", "bfloat16"))),

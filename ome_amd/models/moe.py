@@ -77,6 +77,7 @@ class MoEForCausalLM(LlamaForCausalLM):
         tp = self.tp
         I, SI = self.moe_inter, self.shared_inter
         experts: dict[int, dict[int, dict[str, torch.Tensor]]] = {}
+        fused: dict[int, dict[str, torch.Tensor]] = {}
         shared: dict[int, dict[str, torch.Tensor]] = {}
         rest_iter = []
         if self.fp8:
@@ -102,6 +103,8 @@ class MoEForCausalLM(LlamaForCausalLM):
                 sub = ".".join(parts[3:])
                 if sub == "gate.weight":
                     self.w_router[i] = put(w)
+                elif sub in ("experts.gate_up_proj", "experts.down_proj"):   # fused per layer (Qwen3-VL-MoE)
+                    fused.setdefault(i, {})[parts[4]] = w
                 elif sub.startswith("experts."):
                     e = int(parts[4])
                     kind = parts[5]  # w1/w2/w3 (Mixtral) or gate_proj/up_proj/down_proj
@@ -127,6 +130,20 @@ class MoEForCausalLM(LlamaForCausalLM):
                 ds.append(cols(dn, I))
             self.w13[i] = put(torch.stack(gs))
             self.w2[i] = put(torch.stack(ds))
+            self.w_gu[i] = self.w_d[i] = None
+        H = self.cfg.hidden_size
+        for i, d in fused.items():   # gate_up [E, H, 2I] (or [E, 2I, H]), down [E, I, H] (or [E, H, I])
+            gu, dn = d["gate_up_proj"], d["down_proj"]
+            if gu.shape[1] == H and gu.shape[2] != H:
+                gu = gu.transpose(1, 2)
+            if dn.shape[2] == H and dn.shape[1] != H:
+                dn = dn.transpose(1, 2)
+            sel = torch.tensor(self.local_experts(i), dtype=torch.long, device=gu.device)
+            gu, dn = gu.index_select(0, sel), dn.index_select(0, sel)
+            g, u = gu.chunk(2, 1)
+            self.w13[i] = put(torch.cat([g.narrow(1, tp.rank * I, min(I, g.shape[1] - tp.rank * I)),
+                                         u.narrow(1, tp.rank * I, min(I, u.shape[1] - tp.rank * I))], 1))
+            self.w2[i] = put(dn.narrow(2, tp.rank * I, min(I, dn.shape[2] - tp.rank * I)))
             self.w_gu[i] = self.w_d[i] = None
         for i, d in shared.items():
             self.w_sgu[i] = put(torch.cat([rows(d["gate_proj"], SI), rows(d["up_proj"], SI)], 0))

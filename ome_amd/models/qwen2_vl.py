@@ -195,6 +195,7 @@ class Qwen2VLForConditionalGeneration(LlamaForCausalLM):
             return super().forward(ids, meta, kv, input_embeds)
         cfg, tp, D = self.cfg, self.tp, self.D
         rpos, table = rope
+        ds = meta.extra.get("deepstack")
         T = ids.shape[0]
         x, residual = self._stage_input(ids, input_embeds)
         for i in self.layers:
@@ -210,6 +211,8 @@ class Qwen2VLForConditionalGeneration(LlamaForCausalLM):
             o = pstate.tp_all_reduce(linear(attn.view(T, tp.hq * D), self.w_o[i]))
             ops.fused_add_rmsnorm(o, residual, self.ln2[i], self.eps)
             x = self.mlp(i, o)
+            if ds is not None and i < len(ds[1]):   # Qwen3-VL deepstack: layer i output += level-i features
+                x.index_add_(0, ds[0], ds[1][i].to(x.dtype))
         return self._stage_output(x, residual)
 
 

@@ -174,7 +174,8 @@ class Engine:
             if isinstance(im, tuple):
                 pv, g = im
             else:
-                pv, g = preprocess_image(im, patch=m.visual.patch, merge=m.merge, temporal=m.visual.temporal)
+                pv, g = preprocess_image(im, patch=m.visual.patch, merge=m.merge, temporal=m.visual.temporal,
+                                         **getattr(m, "image_processor_kwargs", {}))
             pvs.append(torch.as_tensor(pv, dtype=torch.float32))
             grids.append(tuple(int(v) for v in g))
         ids, spans = expand_image_tokens(list(prompt_ids), m.image_token_id, grids, m.merge, pvs,

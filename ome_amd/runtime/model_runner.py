@@ -555,6 +555,7 @@ class ModelRunner:
         bidir = getattr(m, "bidirectional_images", False)
         hi_rows = np.full(T, -1, dtype=np.int32) if bidir else None   # last visible key per row (image blocks)
         rows, feats, row = [], [], 0
+        deep: list[list[torch.Tensor]] = []
         for i in order:
             c = chunks[i]
             r, L = c.req, c.length
@@ -579,7 +580,13 @@ class ModelRunner:
                         if mm.features is None:
                             mm.features = m.encode_images(mm.pixel_values, mm.grid_thw)
                         rows.extend(range(row + lo - c.start, row + hi - c.start))
-                        feats.append(mm.features[off + lo - s: off + hi - s])
+                        main = mm.features[0] if isinstance(mm.features, tuple) else mm.features
+                        feats.append(main[off + lo - s: off + hi - s])
+                        if isinstance(mm.features, tuple):   # (main, [deepstack level features]) -- Qwen3-VL
+                            for lvl, d in enumerate(mm.features[1]):
+                                if len(deep) <= lvl:
+                                    deep.append([])
+                                deep[lvl].append(d[off + lo - s: off + hi - s])
                         if bidir:
                             hi_rows[row + lo - c.start:row + hi - c.start] = s + n - 1
                     off += n
@@ -592,6 +599,8 @@ class ModelRunner:
         if any(chunks[i].req.mm is not None and chunks[i].req.mm.mrope_pos is not None for i in order):
             meta.extra["rope"] = (torch.arange(T, dtype=torch.int32, device=dv), m.mrope_table(torch.from_numpy(p3)))
         r_dev = torch.tensor(rows, dtype=torch.long, device=dv)
+        if deep:
+            meta.extra["deepstack"] = (r_dev, [torch.cat(d, 0) for d in deep])
         f = torch.cat(feats, 0) if feats else torch.zeros(0, m.cfg.hidden_size, dtype=m.dtype, device=dv)
         return m.embed_with_images(t_ids, r_dev, f)
 
