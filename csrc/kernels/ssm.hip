@@ -6,7 +6,7 @@
 //   ome_ssm_scan         : the selective scan  h <- exp(dt*A) h + dt * B x,  y = C.h + D x
 //                          (dt = softplus(dt + dt_bias) clamped below), recurrent over the rows of
 //                          each sequence, state in fp32 per (slot, head, p, n)
-//   ome_gated_rmsnorm    : out = w * groupRMSNorm(y * silu(z))
+//   ome_gated_rmsnorm    : out = w * groupRMSNorm(y * silu(z))  (norm_first: w[:group] * groupRMSNorm(y) * silu(z))
 //
 // Sequences are described by cu[S+1] (row ranges), slot[S] (state row) and reset[S] (1 = start
 // from zero state: a sequence's first prefill chunk).  Decode is the S = batch, one-row case, so
@@ -144,22 +144,27 @@ __global__ __launch_bounds__(256) void ssm_scan_kernel(
 __global__ __launch_bounds__(256) void gated_rmsnorm_kernel(const bf16* __restrict__ y, int64_t y_stride,
                                                             const bf16* __restrict__ z, int64_t z_stride,
                                                             const bf16* __restrict__ w, bf16* __restrict__ out,
-                                                            int64_t out_stride, int group, float eps) {
+                                                            int64_t out_stride, int group, float eps, int norm_first) {
   __shared__ float red[4];
   const int row = blockIdx.y, g0 = blockIdx.x * group;
   const bf16* yr = y + (int64_t)row * y_stride + g0;
   const bf16* zr = z + (int64_t)row * z_stride + g0;
   float ss = 0.f;
   for (int i = threadIdx.x; i < group; i += 256) {
-    const float v = (float)yr[i] * silu_f((float)zr[i]);
+    const float v = norm_first ? (float)yr[i] : (float)yr[i] * silu_f((float)zr[i]);
     ss += v * v;
   }
   const float tot = block_sum<256>(ss, red);
   const float rs = rsqrtf(tot / (float)group + eps);
   bf16* orow = out + (int64_t)row * out_stride + g0;
   for (int i = threadIdx.x; i < group; i += 256) {
-    const float v = (float)yr[i] * silu_f((float)zr[i]) * rs;
-    orow[i] = (bf16)((float)(bf16)v * (float)w[g0 + i]);  // HF: normalise, cast, then scale by w
+    if (norm_first) {   // Qwen3-Next: w (per group channel) * norm(y), then * silu(z)
+      const float t = (float)(bf16)((float)(bf16)((float)yr[i] * rs) * (float)w[i]);
+      orow[i] = (bf16)(t * silu_f((float)zr[i]));
+    } else {
+      const float v = (float)yr[i] * silu_f((float)zr[i]) * rs;
+      orow[i] = (bf16)((float)(bf16)v * (float)w[g0 + i]);  // HF: normalise, cast, then scale by w
+    }
   }
 }
 
@@ -234,12 +239,13 @@ OME_API int ome_ssm_scan(const void* x, int64_t x_stride, const void* dt, int64_
 
 OME_API int ome_gated_rmsnorm(const void* y, int64_t y_stride, const void* z, int64_t z_stride, const void* w,
                               void* out, int64_t out_stride, int rows, int I, int group, float eps,
-                              hipStream_t stream) {
+                              int norm_first, hipStream_t stream) {
   if (rows <= 0) return 0;
   if (group <= 0 || I % group != 0) return -2;
   dim3 grid(I / group, rows);
   gated_rmsnorm_kernel<<<grid, 256, 0, stream>>>((const bf16*)y, y_stride, (const bf16*)z, z_stride,
-                                                 (const bf16*)w, (bf16*)out, out_stride, group, eps);
+                                                 (const bf16*)w, (bf16*)out, out_stride, group, eps,
+                                                 norm_first);
   OME_CHECK_LAUNCH();
   return 0;
 }

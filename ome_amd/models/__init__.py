@@ -48,6 +48,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.nemotron_h import NemotronHForCausalLM
 
         return NemotronHForCausalLM
+    if cfg.architecture == "Qwen3NextForCausalLM" or cfg.model_type == "qwen3_next":
+        from ome_amd.models.qwen3_next import Qwen3NextForCausalLM
+
+        return Qwen3NextForCausalLM
     if cfg.architecture in ("Qwen3VLForConditionalGeneration", "Qwen3VLMoeForConditionalGeneration"):
         from ome_amd.models.qwen3_vl import Qwen3VLForConditionalGeneration, Qwen3VLMoeForConditionalGeneration
 
@@ -117,7 +121,7 @@ def supported(arch: str) -> bool:
     return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or arch in NEMOTRON_H_ARCHS or \
         arch in DECODER_ARCHS or arch in ENCODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
         arch == "DeciLMForCausalLM" or arch in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM") or \
-        arch == "CLIPModel" or \
+        arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or \
         arch == "GptOssForCausalLM"
 
 

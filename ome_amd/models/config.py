@@ -248,7 +248,7 @@ class ModelConfig:
             tie_word_embeddings=bool(cfg.get("tie_word_embeddings", text.get("tie_word_embeddings", False))),
             attention_bias=bool(text.get("attention_bias", text.get("use_bias", mt in ("qwen2", "qwen2_moe", "qwen2_vl", "qwen2_vl_text", "qwen2_5_vl", "qwen2_5_vl_text", "phi")))),
             qk_norm=mt in ("qwen3", "qwen3_moe", "gemma3", "gemma3_text", "qwen3_vl", "qwen3_vl_text", "qwen3_vl_moe",
-                           "qwen3_vl_moe_text"),
+                           "qwen3_vl_moe_text", "qwen3_next"),
             hidden_act=text.get("hidden_act", text.get("hidden_activation", "silu")),
             sliding_window=text.get("sliding_window") if text.get("use_sliding_window", mt in ("mistral", "starcoder2", "phi3")) else None,
             torch_dtype=str(text.get("torch_dtype", cfg.get("torch_dtype", "bfloat16"))),
@@ -431,6 +431,22 @@ PRESETS: dict[str, dict] = {
                             head_dim=64, intermediate_size=512, mlp_hidden_act="relu2", mamba_num_heads=8,
                             mamba_head_dim=64, ssm_state_size=64, n_groups=2, conv_kernel=4, vocab_size=1024,
                             layer_norm_epsilon=1e-5, max_position_embeddings=4096, time_step_min=0.001),
+    # Qwen3-Next-80B-A3B shape (48 layers: 3 Gated-DeltaNet + 1 gated attention, 512 experts top-10)
+    "qwen3-next-80b-a3b": dict(architectures=["Qwen3NextForCausalLM"], model_type="qwen3_next", hidden_size=2048,
+                               num_hidden_layers=48, num_attention_heads=16, num_key_value_heads=2, head_dim=256,
+                               intermediate_size=5120, moe_intermediate_size=512,
+                               shared_expert_intermediate_size=512, num_experts=512, num_experts_per_tok=10,
+                               norm_topk_prob=True, linear_num_key_heads=16, linear_num_value_heads=32,
+                               linear_key_head_dim=128, linear_value_head_dim=128, linear_conv_kernel_dim=4,
+                               full_attention_interval=4, partial_rotary_factor=0.25, rope_theta=10000000.0,
+                               vocab_size=151936, rms_norm_eps=1e-6, max_position_embeddings=262144),
+    "tiny-qwen3-next": dict(architectures=["Qwen3NextForCausalLM"], model_type="qwen3_next", hidden_size=256,
+                            num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
+                            intermediate_size=512, moe_intermediate_size=128, shared_expert_intermediate_size=128,
+                            num_experts=8, num_experts_per_tok=2, norm_topk_prob=True, linear_num_key_heads=2,
+                            linear_num_value_heads=4, linear_key_head_dim=128, linear_value_head_dim=128,
+                            linear_conv_kernel_dim=4, full_attention_interval=4, partial_rotary_factor=0.25,
+                            rope_theta=10000.0, vocab_size=1024, rms_norm_eps=1e-6, max_position_embeddings=4096),
     "tiny-llama4": dict(architectures=["Llama4ForCausalLM"], model_type="llama4_text", hidden_size=256,
                         num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                         intermediate_size=256, intermediate_size_mlp=512, num_local_experts=8, num_experts_per_tok=1,

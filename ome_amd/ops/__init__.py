@@ -111,14 +111,36 @@ def ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min: float, state, cu, slot, reset, 
     return out
 
 
-def gated_rmsnorm(y: torch.Tensor, z: torch.Tensor, w: torch.Tensor, group: int, eps: float) -> torch.Tensor:
-    """w * groupRMSNorm(y * silu(z)) (Mamba-2 output norm, groups of ``group`` channels)."""
+def gdn_scan(q, k, v, a, b, A_log, dt_bias, state, cu, slot, reset, Hv: int, Hk: int,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    """Gated DeltaNet recurrence (Qwen3-Next), per sequence rows ``cu[s]:cu[s+1]``: q / k [T, Hk*dk]
+    and v [T, Hv*dv] are row-strided views of one buffer, a / b [T, Hv] views of another, A_log /
+    dt_bias fp32 [Hv], state fp32 [slots, Hv, dk, dv].  q / k are L2-normalised in the kernel."""
+    T = q.shape[0]
+    dk, dv = state.shape[2], state.shape[3]
+    out = torch.empty(T, Hv * dv, dtype=v.dtype, device=v.device) if out is None else out
+    if not _gpu(q):
+        return ref.gdn_scan(q, k, v, a, b, A_log, dt_bias, state, cu, slot, reset, Hv, Hk, out)
+    assert q.stride(0) == k.stride(0) == v.stride(0) and a.stride(0) == b.stride(0)
+    assert q.stride(1) == k.stride(1) == v.stride(1) == a.stride(1) == 1 and out.stride(1) == 1
+    assert state.is_contiguous() and state.dtype == torch.float32 and q.dtype == torch.bfloat16
+    call("ome_gdn_scan", q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), a.data_ptr(), b.data_ptr(),
+         a.stride(0), A_log.data_ptr(), dt_bias.data_ptr(), state.data_ptr(), out.data_ptr(), out.stride(0),
+         _i32(cu).data_ptr(), _i32(slot).data_ptr(), _i32(reset).data_ptr(), slot.shape[0], Hv, Hk, dk, dv,
+         stream_ptr())
+    return out
+
+
+def gated_rmsnorm(y: torch.Tensor, z: torch.Tensor, w: torch.Tensor, group: int, eps: float,
+                  norm_first: bool = False) -> torch.Tensor:
+    """w * groupRMSNorm(y * silu(z)) (Mamba-2 output norm, groups of ``group`` channels);
+    ``norm_first``: w[:group] * groupRMSNorm(y) * silu(z) (Qwen3-Next, ``w`` shared by the groups)."""
     if not _gpu(y):
-        return ref.gated_rmsnorm(y, z, w, group, eps)
+        return ref.gated_rmsnorm(y, z, w, group, eps, norm_first)
     T, I = y.shape
     out = torch.empty(T, I, dtype=y.dtype, device=y.device)
     call("ome_gated_rmsnorm", y.data_ptr(), y.stride(0), z.data_ptr(), z.stride(0), w.data_ptr(), out.data_ptr(),
-         out.stride(0), T, I, group, float(eps), stream_ptr())
+         out.stride(0), T, I, group, float(eps), int(norm_first), stream_ptr())
     return out
 
 

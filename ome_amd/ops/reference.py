@@ -88,9 +88,40 @@ def ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min, state, cu, slot, reset, H, P, N
     return out
 
 
-def gated_rmsnorm(y, z, w, group, eps):
+def gdn_scan(q, k, v, a, b, A_log, dt_bias, state, cu, slot, reset, Hv, Hk, out):
+    """Gated delta rule, recurrent per sequence; ``state`` [slots, Hv, dk, dv] fp32."""
+    dk, dv = state.shape[2], state.shape[3]
+    rep = Hv // Hk
+    for s in range(len(slot)):
+        r0, r1 = int(cu[s]), int(cu[s + 1])
+        if r1 <= r0:
+            continue
+        st = state[int(slot[s])]
+        S = torch.zeros_like(st) if int(reset[s]) else st.clone()                              # [Hv, dk, dv]
+        for r in range(r0, r1):
+            kr = k[r].float().view(Hk, dk)
+            kr = kr * torch.rsqrt(kr.pow(2).sum(-1, keepdim=True) + 1e-6)
+            qr = q[r].float().view(Hk, dk)
+            qr = qr * torch.rsqrt(qr.pow(2).sum(-1, keepdim=True) + 1e-6) * dk ** -0.5
+            qr, kr = qr.repeat_interleave(rep, 0), kr.repeat_interleave(rep, 0)                 # [Hv, dk]
+            g = -torch.exp(A_log) * torch.nn.functional.softplus(a[r].float() + dt_bias)
+            beta = torch.sigmoid(b[r].float())
+            S = S * torch.exp(g)[:, None, None]
+            kv = (S * kr[..., None]).sum(1)                                                     # [Hv, dv]
+            delta = (v[r].float().view(Hv, dv) - kv) * beta[:, None]
+            S = S + kr[..., None] * delta[:, None, :]
+            out[r] = (S * qr[..., None]).sum(1).reshape(-1).to(out.dtype)
+        st.copy_(S)
+    return out
+
+
+def gated_rmsnorm(y, z, w, group, eps, norm_first=False):
+    T, I = y.shape
+    if norm_first:
+        g = y.float().view(T, I // group, group)
+        g = (g * torch.rsqrt(g.pow(2).mean(-1, keepdim=True) + eps)).to(y.dtype)
+        return ((w * g).float() * torch.nn.functional.silu(z.float().view(T, I // group, group))).view(T, I).to(y.dtype)
     v = y.float() * torch.nn.functional.silu(z.float())
-    T, I = v.shape
     g = v.view(T, I // group, group)
     g = g * torch.rsqrt(g.pow(2).mean(-1, keepdim=True) + eps)
     return w * g.view(T, I).to(y.dtype)

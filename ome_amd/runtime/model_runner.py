@@ -104,6 +104,12 @@ class ModelRunner:
         self.model = build_model(cfg, self.device, dtype, max_positions=max_context + page_size,
                                  model_path=model_path, load_format=load_format, seed=seed)
         self.load_time = time.perf_counter() - t0
+        self.stateful = bool(getattr(self.model, "stateful", False))
+        if self.stateful:  # recurrent (SSM) state per request slot, the padding slot included; before
+            # the KV sizing below so the page budget sees it
+            self.model.alloc_state(max_running + 1)
+            self._ssm_cu = torch.arange(max_running + 2, dtype=torch.int32, device=self.device)
+            self._ssm_zero = torch.zeros(max_running + 1, dtype=torch.int32, device=self.device)
         # ---- KV cache sizing (reference: --mem-frac 0.9, llama-3-8b-instruct-rt.yaml:59-60) ----
         tp = self.model.tp
         kv_heads, k_dim, v_dim = getattr(self.model, "kv_layout", (tp.hkv, cfg.head_dim, cfg.head_dim))
@@ -139,11 +145,6 @@ class ModelRunner:
         self.pp = pstate.get().pp_size > 1
         self.pages = PagePool(num_pages)
         self.slots = ReqSlotPool(max_running + 1, max_pages_per_seq, self.device)
-        self.stateful = bool(getattr(self.model, "stateful", False))
-        if self.stateful:  # recurrent (SSM) state per request slot, the padding slot included
-            self.model.alloc_state(max_running + 1)
-            self._ssm_cu = torch.arange(max_running + 2, dtype=torch.int32, device=self.device)
-            self._ssm_zero = torch.zeros(max_running + 1, dtype=torch.int32, device=self.device)
         log.info("KV cache: %d pages x %d tokens (%.1f GiB), weights %.1f GiB", num_pages, page_size,
                  num_pages * page_bytes / 2**30, self.model.weight_bytes() / 2**30)
         # ---- decode graphs ----
