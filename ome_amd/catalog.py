@@ -108,6 +108,11 @@ FAMILIES: list[Family] = [
     Family("granite-3-1-8b-instruct", "ibm-granite", "ibm-granite/granite-3.1-8b-instruct", "GraniteForCausalLM",
            8.2),
     Family("smollm3-3b", "huggingfacetb", "HuggingFaceTB/SmolLM3-3B", "SmolLM3ForCausalLM", 3.1),
+    Family("nvidia-nemotron-nano-9b-v2", "nvidia", "nvidia/NVIDIA-Nemotron-Nano-9B-v2", "NemotronHForCausalLM", 8.9,
+           args=['--reasoning-parser', 'nano_v3', '--tool-call-parser', 'nano_v3']),
+    Family("nvidia-nemotron-3-nano-30b-a3b-bf16", "nvidia", "nvidia/NVIDIA-Nemotron-3-Nano-30B-A3B-BF16",
+           "NemotronHForCausalLM", 31.6, "nemotron-3-nano-30b-a3b",
+           args=['--reasoning-parser', 'nano_v3', '--tool-call-parser', 'qwen3_coder']),
     Family("nemotron-h-8b-base", "nvidia", "nvidia/Nemotron-H-8B-Base-8K", "NemotronHForCausalLM", 8.1,
            "nemotron-h-8b"),
     Family("opt-125m", "facebook", "facebook/opt-125m", "OPTForCausalLM", 0.125, "opt-125m"),

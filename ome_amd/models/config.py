@@ -431,6 +431,24 @@ PRESETS: dict[str, dict] = {
                             head_dim=64, intermediate_size=512, mlp_hidden_act="relu2", mamba_num_heads=8,
                             mamba_head_dim=64, ssm_state_size=64, n_groups=2, conv_kernel=4, vocab_size=1024,
                             layer_norm_epsilon=1e-5, max_position_embeddings=4096, time_step_min=0.001),
+    # Nemotron-3-Nano-30B-A3B shape (52 layers: Mamba-2 / MoE / attention, 128 ReLU^2 experts top-6)
+    "nemotron-3-nano-30b-a3b": dict(architectures=["NemotronHForCausalLM"], model_type="nemotron_h",
+                                    hidden_size=2688, num_attention_heads=32, num_key_value_heads=2, head_dim=128,
+                                    hybrid_override_pattern="MEMEM*EMEMEM*EMEMEM*EMEMEM*EMEMEM*EMEMEMEM*EMEMEMEME",
+                                    intermediate_size=1856, mlp_hidden_act="relu2", mamba_num_heads=64,
+                                    mamba_head_dim=64, ssm_state_size=128, n_groups=8, conv_kernel=4,
+                                    vocab_size=131072, layer_norm_epsilon=1e-5, max_position_embeddings=262144,
+                                    time_step_min=0.001, n_routed_experts=128, num_experts_per_tok=6,
+                                    moe_intermediate_size=1856, moe_shared_expert_intermediate_size=3712, n_group=1,
+                                    topk_group=1, routed_scaling_factor=2.5, norm_topk_prob=True),
+    "tiny-nemotron-h-moe": dict(architectures=["NemotronHForCausalLM"], model_type="nemotron_h", hidden_size=256,
+                                hybrid_override_pattern="ME*EME", num_attention_heads=4, num_key_value_heads=2,
+                                head_dim=64, intermediate_size=512, mlp_hidden_act="relu2", mamba_num_heads=8,
+                                mamba_head_dim=64, ssm_state_size=64, n_groups=2, conv_kernel=4, vocab_size=1024,
+                                layer_norm_epsilon=1e-5, max_position_embeddings=4096, time_step_min=0.001,
+                                n_routed_experts=16, num_experts_per_tok=4, moe_intermediate_size=128,
+                                moe_shared_expert_intermediate_size=256, n_group=4, topk_group=2,
+                                routed_scaling_factor=2.5, norm_topk_prob=True),
     # Qwen3-Next-80B-A3B shape (48 layers: 3 Gated-DeltaNet + 1 gated attention, 512 experts top-10)
     "qwen3-next-80b-a3b": dict(architectures=["Qwen3NextForCausalLM"], model_type="qwen3_next", hidden_size=2048,
                                num_hidden_layers=48, num_attention_heads=16, num_key_value_heads=2, head_dim=256,

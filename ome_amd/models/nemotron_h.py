@@ -10,7 +10,12 @@ is ``h + mixer(RMSNorm(h))`` with
   group RMSNorm ``w * norm(y * silu(z))`` (``ome_gated_rmsnorm``) -> out_proj GEMM;
 * ``*`` attention without positional encoding (GQA, the fused QKV / paged-KV kernel with
   ``apply_rope=False``, paged decode / prefill attention) -- only these layers own KV pages;
-* ``-`` MLP ``down(relu(up(x))^2)`` (``ome_act`` ReLU^2 in place between two GEMMs).
+* ``-`` MLP ``down(relu(up(x))^2)`` (``ome_act`` ReLU^2 in place between two GEMMs);
+* ``E`` sparse MoE (Nemotron-3 Nano / Super): fp32 router logits -> sigmoid scores with the
+  ``e_score_correction_bias`` used for selection only, grouped top-k (``ome_moe_route`` noaux_tc
+  mode), renormalised and scaled by ``routed_scaling_factor``; NON-gated ReLU^2 experts on the
+  grouped MFMA GEMMs (``fused_moe(gated=False)``), optionally inside a latent projection
+  (``moe_latent_size``), plus an always-on ReLU^2 shared expert.
 
 Recurrent state lives per request slot (the row of the page-table pool, ``Request.req_slot``):
 conv state [slots, conv_dim, K-1] (model dtype) and SSM state [slots, H, P, N] (fp32) per Mamba
@@ -57,8 +62,6 @@ class NemotronHForCausalLM(LlamaForCausalLM):
             raise NotImplementedError("NemotronH runs on one GPU per replica (no TP / PP yet)")
         hf = cfg.extra or {}
         self.types = layer_types(hf)
-        if "moe" in self.types:
-            raise NotImplementedError("NemotronH MoE blocks are not implemented")
         self.kv_layers = [i for i in self.layers if self.types[i] == "full_attention"]
         self.mamba_layers = [i for i in self.layers if self.types[i] == "linear_attention"]
         self.mi = {i: k for k, i in enumerate(self.mamba_layers)}
@@ -83,6 +86,24 @@ class NemotronHForCausalLM(LlamaForCausalLM):
         self.w_out: list[torch.Tensor | None] = [None] * L
         self.conv_state: torch.Tensor | None = None
         self.ssm_state: torch.Tensor | None = None
+        # MoE blocks
+        self.E = int(hf.get("n_routed_experts") or hf.get("num_local_experts") or 0)
+        self.topk = int(hf.get("num_experts_per_tok", 2))
+        self.moe_I = int(hf.get("moe_intermediate_size", 0) or 0)
+        self.shared_I = int(hf.get("moe_shared_expert_intermediate_size", 0) or 0)
+        self.latent = int(hf.get("moe_latent_size") or 0)
+        self.n_group = int(hf.get("n_group", 1) or 1)
+        self.topk_group = int(hf.get("topk_group", 1) or 1)
+        self.routed_scale = float(hf.get("routed_scaling_factor", 1.0) or 1.0)
+        self.renorm = bool(hf.get("norm_topk_prob", True))
+        self.w_router: list[torch.Tensor | None] = [None] * L      # fp32 [E, H]
+        self.e_bias: list[torch.Tensor | None] = [None] * L        # fp32 [E]
+        self.w_eu: list[torch.Tensor | None] = [None] * L          # [E, I, H'] (H' = latent or hidden)
+        self.w_ed: list[torch.Tensor | None] = [None] * L          # [E, H', I]
+        self.w_su: list[torch.Tensor | None] = [None] * L
+        self.w_sd: list[torch.Tensor | None] = [None] * L
+        self.w_l1: list[torch.Tensor | None] = [None] * L          # latent in / out projections
+        self.w_l2: list[torch.Tensor | None] = [None] * L
 
     def alloc_state(self, slots: int) -> None:
         nm = len(self.mamba_layers)
@@ -111,6 +132,17 @@ class NemotronHForCausalLM(LlamaForCausalLM):
             elif t == "full_attention":
                 self.w_qkv[i] = self._alloc((tp.hq + 2 * tp.hkv) * D, Hd, std=std, gen=gen)
                 self.w_o[i] = self._alloc(Hd, tp.hq * D, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
+            elif t == "moe":
+                Hl, dstd = self.latent or Hd, std / math.sqrt(2 * cfg.num_layers)
+                self.w_router[i] = torch.randn(self.E, Hd, generator=gen, **f32) * std
+                self.e_bias[i] = torch.zeros(self.E, **f32)
+                self.w_eu[i] = self._alloc(self.E, self.moe_I, Hl, std=std, gen=gen)
+                self.w_ed[i] = self._alloc(self.E, Hl, self.moe_I, std=dstd, gen=gen)
+                self.w_su[i] = self._alloc(self.shared_I, Hd, std=std, gen=gen)
+                self.w_sd[i] = self._alloc(Hd, self.shared_I, std=dstd, gen=gen)
+                if self.latent:
+                    self.w_l1[i] = self._alloc(Hl, Hd, std=std, gen=gen)
+                    self.w_l2[i] = self._alloc(Hd, Hl, std=std, gen=gen)
             else:
                 self.w_gu[i] = self._alloc(self.inter, Hd, std=std, gen=gen)
                 self.w_d[i] = self._alloc(Hd, self.inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
@@ -124,6 +156,7 @@ class NemotronHForCausalLM(LlamaForCausalLM):
             return t.to(device=self.device, dtype=dtype or self.dtype).contiguous()
 
         qkv: dict[int, dict[str, torch.Tensor]] = {}
+        experts: dict[int, dict[tuple[int, str], torch.Tensor]] = {}
         for name, w in weights:
             for pre in ("backbone.", "model."):
                 if name.startswith(pre):
@@ -170,6 +203,34 @@ class NemotronHForCausalLM(LlamaForCausalLM):
                 self.w_gu[i] = put(w)
             elif sub == "mixer.down_proj.weight":
                 self.w_d[i] = put(w)
+            elif sub == "mixer.gate.weight":
+                self.w_router[i] = put(w, torch.float32)
+            elif sub == "mixer.gate.e_score_correction_bias":
+                self.e_bias[i] = put(w, torch.float32)
+            elif sub == "mixer.experts.up_proj":             # fused [E, I, H']
+                self.w_eu[i] = put(w)
+            elif sub == "mixer.experts.down_proj":
+                self.w_ed[i] = put(w)
+            elif sub.startswith("mixer.experts.") and sub.endswith(".weight"):   # per expert
+                e, kind = int(sub.split(".")[2]), sub.split(".")[3]
+                experts.setdefault(i, {})[(e, kind)] = w
+            elif sub == "mixer.shared_experts.up_proj.weight":
+                self.w_su[i] = put(w)
+            elif sub == "mixer.shared_experts.down_proj.weight":
+                self.w_sd[i] = put(w)
+            elif sub == "mixer.fc1_latent_proj.weight":
+                self.w_l1[i] = put(w)
+            elif sub == "mixer.fc2_latent_proj.weight":
+                self.w_l2[i] = put(w)
+        for i, d in experts.items():
+            self.w_eu[i] = put(torch.stack([d[(e, "up_proj")] for e in range(self.E)]))
+            self.w_ed[i] = put(torch.stack([d[(e, "down_proj")] for e in range(self.E)]))
+        for i in self.layers:
+            if self.types[i] == "moe":
+                if self.e_bias[i] is None:
+                    self.e_bias[i] = torch.zeros(self.E, dtype=torch.float32, device=self.device)
+                if self.w_router[i] is None or self.w_eu[i] is None or self.w_ed[i] is None:
+                    raise ValueError(f"layer {i}: incomplete MoE weights")
         for i, d in qkv.items():
             self.w_qkv[i] = put(torch.cat([d["q"], d["k"], d["v"]], 0))
         if self.lm_head is None:
@@ -178,7 +239,8 @@ class NemotronHForCausalLM(LlamaForCausalLM):
 
     def weight_bytes(self) -> int:
         n = super().weight_bytes()
-        for lst in (self.w_in, self.conv_w, self.conv_b, self.gnorm, self.w_out):
+        for lst in (self.w_in, self.conv_w, self.conv_b, self.gnorm, self.w_out, self.w_router, self.w_eu, self.w_ed,
+                    self.w_su, self.w_sd, self.w_l1, self.w_l2):
             n += sum(t.numel() * t.element_size() for t in lst if t is not None)
         return n
 
@@ -195,6 +257,18 @@ class NemotronHForCausalLM(LlamaForCausalLM):
                          slot, reset, H, self.P, N, G)
         y = ops.gated_rmsnorm(y, z, self.gnorm[i], I // G, self.eps)
         return linear(y, self.w_out[i])
+
+    def moe(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        logits = torch.nn.functional.linear(x.float(), self.w_router[i])      # HF routes in fp32
+        tw, tid = ops.moe_route(logits, self.topk, self.renorm, "sigmoid", bias=self.e_bias[i],
+                                n_group=self.n_group, topk_group=self.topk_group, group_mode=2)
+        h = linear(x, self.w_l1[i]) if self.latent else x
+        out = ops.fused_moe(h, tw, tid, self.w_eu[i], self.w_ed[i], self.mlp_act, self.routed_scale, gated=False)
+        if self.latent:
+            out = linear(out, self.w_l2[i])
+        if self.w_su[i] is not None:
+            out = out + linear(ops.act(linear(x, self.w_su[i]), self.mlp_act), self.w_sd[i])
+        return out
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: PagedKVCache,
                 input_embeds: torch.Tensor | None = None) -> torch.Tensor:
@@ -217,6 +291,8 @@ class NemotronHForCausalLM(LlamaForCausalLM):
                                    meta.slots, tp.hq, tp.hkv, D, False, None, None, self.eps, ks, vs)
                 attn = self.attention(q, k_cache, v_cache, meta, ks, vs)
                 x = linear(attn.view(T, tp.hq * D), self.w_o[i])
+            elif t == "moe":
+                x = self.moe(i, x)
             else:
                 x = linear(ops.act(linear(x, self.w_gu[i]), self.mlp_act), self.w_d[i])
         return self._stage_output(x, residual)

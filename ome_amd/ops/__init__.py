@@ -80,6 +80,9 @@ def act(x: torch.Tensor, kind: int) -> torch.Tensor:
     return x
 
 
+_act_inplace = act   # for callers whose ``act`` argument shadows the op
+
+
 def ssm_conv1d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, state: torch.Tensor, cu, slot, reset,
                out: torch.Tensor | None = None) -> torch.Tensor:
     """Mamba causal depthwise conv1d + SiLU over varlen sequences (rows ``cu[s]:cu[s+1]``), continuing
@@ -314,15 +317,16 @@ def moe_tile_m(rows: int, E: int, N: int) -> int:
 
 def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
               act: int = 0, scale: float = 1.0, b13: torch.Tensor | None = None,
-              b2: torch.Tensor | None = None) -> torch.Tensor:
+              b2: torch.Tensor | None = None, gated: bool = True) -> torch.Tensor:
     """Sparse MoE MLP on MFMA: align (counting sort by expert, on device) -> grouped GEMM gate_up
     with gathered A rows -> SiLU*mul -> grouped GEMM down -> weighted combine.  Shapes are
-    static given T (graph-capturable); per-expert counts never leave the GPU."""
+    static given T (graph-capturable); per-expert counts never leave the GPU.  ``gated=False``:
+    w13 holds only up rows [E, I, H] and the activation is applied in place (NemotronH ReLU^2)."""
     if not _gpu(x):
-        return ref.fused_moe(x, topk_w, topk_ids, w13, w2, act, scale, b13, b2)
+        return ref.fused_moe(x, topk_w, topk_ids, w13, w2, act, scale, b13, b2, gated)
     T, H = x.shape
     E, I2, _ = w13.shape
-    I = I2 // 2
+    I = I2 // 2 if gated else I2
     k = topk_ids.shape[1]
     n = T * k
     dev = x.device
@@ -335,7 +339,7 @@ def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13
     gu = torch.empty(n, I2, dtype=x.dtype, device=dev)
     call("ome_moe_gemm", x.data_ptr(), x.stride(0), sorted_ids.data_ptr(), k, w13.data_ptr(), offsets.data_ptr(),
          E, I2, H, -(-n // tm) + E, gu.data_ptr(), gu.stride(0), ptr(b13), tm, stream_ptr())
-    h = act_and_mul(gu, act)
+    h = act_and_mul(gu, act) if gated else _act_inplace(gu, act)
     y = torch.empty(n, H, dtype=x.dtype, device=dev)
     tm = moe_tile_m(n, E, H)
     call("ome_moe_gemm", h.data_ptr(), h.stride(0), None, 0, w2.data_ptr(), offsets.data_ptr(), E, H, I,

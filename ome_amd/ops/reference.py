@@ -50,6 +50,9 @@ def act(x: torch.Tensor, kind: int) -> torch.Tensor:
     return x
 
 
+_act_inplace = act   # for callers whose ``act`` argument shadows the op
+
+
 def ssm_conv1d(x, w, bias, state, cu, slot, reset, out):
     """Causal depthwise conv + SiLU per sequence, continuing from / updating ``state`` [slots, C, K-1]."""
     K = w.shape[1]
@@ -388,7 +391,7 @@ def moe_route(logits, k: int, renorm: bool, scoring: str = "softmax", bias=None,
     return w.float(), ids.to(torch.int32)
 
 
-def fused_moe(x, topk_w, topk_ids, w13, w2, act: int = 0, scale: float = 1.0, b13=None, b2=None):
+def fused_moe(x, topk_w, topk_ids, w13, w2, act: int = 0, scale: float = 1.0, b13=None, b2=None, gated=True):
     """x [T, H]; w13 [E, 2I, H] (gate rows then up rows); w2 [E, H, I]; optional per-expert
     biases b13 [E, 2I], b2 [E, H] (GPT-OSS)."""
     T, H = x.shape
@@ -399,7 +402,7 @@ def fused_moe(x, topk_w, topk_ids, w13, w2, act: int = 0, scale: float = 1.0, b1
         gu = xf[tok] @ w13[e].float().t()
         if b13 is not None:
             gu = gu + b13[e].float()
-        h = act_and_mul(gu.to(x.dtype), act).float()
+        h = (act_and_mul(gu.to(x.dtype), act) if gated else _act_inplace(gu.to(x.dtype), act)).float()
         y = h.to(x.dtype).float() @ w2[e].float().t()
         if b2 is not None:
             y = y + b2[e].float()

@@ -18,15 +18,18 @@ from ome_amd.runtime.engine import Engine, EngineArgs  # noqa: E402
 from ome_amd.runtime.request import SamplingParams  # noqa: E402
 
 
-def _hf_model(tmp_path):
+def _hf_model(tmp_path, pattern="M-M*-M", **kw):
     torch.manual_seed(0)
     cfg = transformers.NemotronHConfig(
         vocab_size=512, hidden_size=128, num_attention_heads=4, num_key_value_heads=2, head_dim=32,
         intermediate_size=256, mamba_num_heads=8, mamba_head_dim=16, ssm_state_size=32, n_groups=2, conv_kernel=4,
-        hybrid_override_pattern="M-M*-M", max_position_embeddings=512, chunk_size=16, pad_token_id=0,
-        bos_token_id=1, eos_token_id=2)
+        hybrid_override_pattern=pattern, max_position_embeddings=512, chunk_size=16, pad_token_id=0,
+        bos_token_id=1, eos_token_id=2, **kw)
     m = transformers.NemotronHForCausalLM(cfg)
     with torch.no_grad():
+        for n, b in m.named_buffers():
+            if n.endswith("e_score_correction_bias"):
+                b.normal_(0.0, 0.05)
         for n, p in m.named_parameters():
             if n.endswith("norm.weight") or n.endswith("norm_f.weight"):
                 p.normal_(1.0, 0.1)
@@ -95,6 +98,27 @@ def test_nemotron_h_logits_and_generate_match_hf(tmp_path):
     with torch.no_grad():
         ref9 = hf.generate(torch.tensor([ids[:9]]), max_new_tokens=8, do_sample=False)[0, 9:].tolist()
     assert reqs[1].output_ids == ref9
+
+
+@pytest.mark.parametrize("latent", [None, 64])
+def test_nemotron_h_moe_matches_hf(tmp_path, latent):
+    """``E`` blocks: sigmoid grouped routing with correction bias, ReLU^2 experts (+ latent
+    projection), shared expert."""
+    hf = _hf_model(tmp_path, "ME*E", n_routed_experts=8, num_experts_per_tok=2, moe_intermediate_size=64,
+                   moe_shared_expert_intermediate_size=96, n_group=2, topk_group=1, routed_scaling_factor=2.5,
+                   norm_topk_prob=True, moe_latent_size=latent)
+    ids = [(5 * i + 11) % 500 + 3 for i in range(30)]
+    with torch.no_grad():
+        want = hf(torch.tensor([ids])).logits[0].float()
+    eng = Engine(EngineArgs(model_path=str(tmp_path), device="cpu", dtype="float32", max_running_requests=4,
+                            context_length=256))
+    m = eng.runner.model
+    assert m.types == ["linear_attention", "moe", "full_attention", "moe"] and m.E == 8
+    got = _prefill_logits(eng, ids, [30])
+    assert (got - want).abs().max().item() < 2e-3 * max(1.0, want.abs().max().item())
+    with torch.no_grad():
+        ref = hf.generate(torch.tensor([ids]), max_new_tokens=6, do_sample=False)[0, len(ids):].tolist()
+    assert eng.generate([ids], SamplingParams(max_new_tokens=6, ignore_eos=True))[0].output_ids == ref
 
 
 def test_ssm_scan_reference_matches_recurrence():

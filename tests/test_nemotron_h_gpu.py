@@ -59,12 +59,30 @@ def test_relu2_act():
     assert torch.equal(ops.act(x.clone(), 4), want)
 
 
-def test_nemotron_h_engine_graph_vs_eager():
+def test_ungated_relu2_moe_matches_reference():
+    torch.manual_seed(0)
+    T, H, I, E, k = 37, 256, 128, 16, 4
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    wu = (torch.randn(E, I, H, device=DEV) * 0.05).to(torch.bfloat16)
+    wd = (torch.randn(E, H, I, device=DEV) * 0.05).to(torch.bfloat16)
+    logits = torch.randn(T, E, device=DEV)
+    bias = torch.randn(E, device=DEV) * 0.05
+    tw, tid = ops.moe_route(logits, k, True, "sigmoid", bias=bias, n_group=4, topk_group=2, group_mode=2)
+    rw, rid = ref.moe_route(logits.cpu(), k, True, "sigmoid", bias.cpu(), 4, 2, 2)
+    assert torch.equal(tid.cpu().sort(1)[0], rid.sort(1)[0].to(torch.int32))
+    got = ops.fused_moe(x, tw, tid, wu, wd, 4, 2.5, gated=False)
+    want = ref.fused_moe(x.cpu(), tw.cpu(), tid.cpu(), wu.cpu(), wd.cpu(), 4, 2.5, gated=False)
+    assert (got.float().cpu() - want.float()).abs().max().item() < 3e-2 * max(1.0, want.float().abs().max().item())
+
+
+@pytest.mark.parametrize("model", ["tiny-nemotron-h", "tiny-nemotron-h-moe"])
+def test_nemotron_h_engine_graph_vs_eager(model):
     outs = []
     for graph in (True, False):
-        eng = Engine(EngineArgs(model="tiny-nemotron-h", device="cuda", max_running_requests=8, context_length=512,
+        eng = Engine(EngineArgs(model=model, device="cuda", max_running_requests=8, context_length=512,
                                 cuda_graph=graph))
-        assert eng.runner.use_graph == graph and eng.runner.model.kv_layers == [3]
+        assert eng.runner.use_graph == graph and eng.runner.model.kv_layers == ([3] if model == "tiny-nemotron-h"
+                                                                                  else [2])
         prompts = [[11 + (i * 13 + j) % 900 for j in range(5 + 70 * i)] for i in range(3)]
         reqs = eng.generate(prompts, SamplingParams(max_new_tokens=16, ignore_eos=True))
         outs.append([r.output_ids for r in reqs])
