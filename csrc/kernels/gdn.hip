@@ -17,6 +17,8 @@
 // later optimisation; decode rows are the same launch with one row per sequence.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace {
 
 __device__ __forceinline__ float gdn_softplus(float x) { return x > 20.f ? x : log1pf(__expf(x)); }
@@ -101,6 +103,104 @@ __global__ __launch_bounds__(128) void gdn_scan_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// v2 (default): no LDS, no barriers.  Each state column j is split over L = DK / 8 lanes of one
+// DPP row (8 fp32 entries per lane), so a wave covers 64 / L columns and the grid is
+// (sequence, v-head, dv / (4 * 64 / L)) -- 8x more workgroups than v1 and an 8-deep FMA chain
+// per dot product instead of DK.  Per row every lane loads its 8-element slices of raw q and k
+// (one 16-byte load each, the next row's loads issued before the current row's math), forms five
+// partial sums (|q|^2, |k|^2, q.k, S^T k, S^T q) and all-reduces them over its L lanes with DPP
+// (quad_perm xor 1 / xor 2, row_half_mirror, row_mirror).  Normalisation is applied to the
+// reduced scalars instead of the vectors:
+//   kv = decay * |k|^-1 * (S^T k),   delta = (v - kv) * beta,
+//   o  = decay * iq * (S^T q) + delta * iq * |k|^-1 * (q.k),   S <- decay * S + (|k|^-1 delta) k
+// with iq = |q|^-1 / sqrt(dk) -- the same function as v1 with one pass over S per row.
+template <int L>
+__device__ __forceinline__ float dpp_allreduce(float v) {
+  if constexpr (L >= 2)
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  if constexpr (L >= 4)
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  if constexpr (L >= 8)
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  if constexpr (L >= 16)
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+template <int DK>
+__global__ __launch_bounds__(256) void gdn_scan_v2_kernel(
+    const bf16* __restrict__ q, const bf16* __restrict__ k, const bf16* __restrict__ v, int64_t qkv_stride,
+    const bf16* __restrict__ a, const bf16* __restrict__ b, int64_t ab_stride, const float* __restrict__ A_log,
+    const float* __restrict__ dt_bias, float* __restrict__ state, bf16* __restrict__ out, int64_t out_stride,
+    const int* __restrict__ cu, const int* __restrict__ slot, const int* __restrict__ reset, int Hv, int Hk,
+    int dv) {
+  constexpr int L = DK / 8, CPW = 64 / L, CPB = 4 * CPW;
+  const int s = blockIdx.x, h = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.z * CPB + w * CPW + lane / L;   // state column
+  const int e0 = (lane % L) * 8;                         // first of this lane's 8 state rows
+  const int r0 = cu[s], r1 = cu[s + 1];
+  if (r1 <= r0) return;   // uniform per block
+  const bool col = j < dv;
+  const int jc = col ? j : 0;
+  const int hk = h / (Hv / Hk);
+  float* st = state + ((int64_t)slot[s] * Hv + h) * DK * dv + jc;
+  float S[8];
+  const bool fresh = reset[s] != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) S[i] = (fresh || !col) ? 0.f : st[(int64_t)(e0 + i) * dv];
+  const float negA = -__expf(A_log[h]), dtb = dt_bias[h];
+  const float qscale = rsqrtf((float)DK);
+  const bf16* qp = q + (int64_t)hk * DK + e0;
+  const bf16* kp = k + (int64_t)hk * DK + e0;
+  const bf16* vp = v + (int64_t)h * dv + jc;
+
+  bf16x8 qn = ld8(qp + (int64_t)r0 * qkv_stride), kn = ld8(kp + (int64_t)r0 * qkv_stride);
+  bf16 vn = vp[(int64_t)r0 * qkv_stride];
+  bf16 an = a[(int64_t)r0 * ab_stride + h], bn = b[(int64_t)r0 * ab_stride + h];
+  for (int r = r0; r < r1; ++r) {
+    const bf16x8 qc = qn, kc = kn;
+    const float vj = (float)vn, av = (float)an, bv = (float)bn;
+    if (r + 1 < r1) {   // prefetch the next row
+      const int64_t o = (int64_t)(r + 1) * qkv_stride;
+      qn = ld8(qp + o);
+      kn = ld8(kp + o);
+      vn = vp[o];
+      an = a[(int64_t)(r + 1) * ab_stride + h];
+      bn = b[(int64_t)(r + 1) * ab_stride + h];
+    }
+    float qq = 0.f, kk = 0.f, qk = 0.f, sk = 0.f, sq = 0.f, kf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float qi = (float)qc[i], ki = (float)kc[i];
+      kf[i] = ki;
+      qq += qi * qi;
+      kk += ki * ki;
+      qk += qi * ki;
+      sk += S[i] * ki;
+      sq += S[i] * qi;
+    }
+    qq = dpp_allreduce<L>(qq);
+    kk = dpp_allreduce<L>(kk);
+    qk = dpp_allreduce<L>(qk);
+    sk = dpp_allreduce<L>(sk);
+    sq = dpp_allreduce<L>(sq);
+    const float decay = __expf(negA * gdn_softplus(av + dtb)), beta = 1.f / (1.f + __expf(-bv));
+    const float ik = rsqrtf(kk + 1e-6f), iq = rsqrtf(qq + 1e-6f) * qscale;
+    const float delta = (vj - decay * ik * sk) * beta;
+    const float o = decay * iq * sq + delta * iq * ik * qk;
+    const float dk_ = ik * delta;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) S[i] = S[i] * decay + kf[i] * dk_;
+    if (col && (lane % L) == 0) out[(int64_t)r * out_stride + (int64_t)h * dv + j] = (bf16)o;
+  }
+  if (col) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[(int64_t)(e0 + i) * dv] = S[i];
+  }
+}
+
 }  // namespace
 
 // q / k / v: row-major views (shared row stride qkv_stride, in elements) of the conv output,
@@ -112,6 +212,21 @@ OME_API int ome_gdn_scan(const void* q, const void* k, const void* v, int64_t qk
                          int Hv, int Hk, int dk, int dv, hipStream_t stream) {
   if (S <= 0) return 0;
   if (dv <= 0 || dv > 128 || Hk <= 0 || Hv % Hk != 0) return -2;
+  static const bool v1 = getenv("OME_GDN_V1") && getenv("OME_GDN_V1")[0] == '1';
+  // v2 reads q / k slices with 16-byte loads; unaligned views take v1
+  if (!v1 && qkv_stride % 8 == 0 && !((uintptr_t)q & 15) && !((uintptr_t)k & 15)) {
+    const int cpb = 4 * 64 / (dk / 8);
+    dim3 grid2(S, Hv, (dv + cpb - 1) / cpb);
+#define GDN2_ARGS                                                                                               \
+  (const bf16*)q, (const bf16*)k, (const bf16*)v, qkv_stride, (const bf16*)a, (const bf16*)b, ab_stride, A_log, \
+      dt_bias, state, (bf16*)out, out_stride, cu, slot, reset, Hv, Hk, dv
+    if (dk == 128) gdn_scan_v2_kernel<128><<<grid2, 256, 0, stream>>>(GDN2_ARGS);
+    else if (dk == 64) gdn_scan_v2_kernel<64><<<grid2, 256, 0, stream>>>(GDN2_ARGS);
+    else return -3;
+#undef GDN2_ARGS
+    OME_CHECK_LAUNCH();
+    return 0;
+  }
   dim3 grid(S, Hv);
 #define GDN_ARGS                                                                                                \
   (const bf16*)q, (const bf16*)k, (const bf16*)v, qkv_stride, (const bf16*)a, (const bf16*)b, ab_stride, A_log, \

@@ -75,6 +75,9 @@ FAMILIES: list[Family] = [
            "qwen3-next-80b-a3b", args=['--tool-call-parser', 'hermes']),
     Family("qwen3-next-80b-a3b-thinking", "qwen", "Qwen/Qwen3-Next-80B-A3B-Thinking", "Qwen3NextForCausalLM", 81.3,
            "qwen3-next-80b-a3b", args=['--reasoning-parser', 'deepseek-r1']),
+    Family("mistral-small-3-1-24b-instruct-2503", "mistralai", "mistralai/Mistral-Small-3.1-24B-Instruct-2503",
+           "Mistral3ForConditionalGeneration", 24.0, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"],
+           args=['--tool-call-parser', 'mistral']),
     Family("qwen3-vl-8b-instruct", "qwen", "Qwen/Qwen3-VL-8B-Instruct", "Qwen3VLForConditionalGeneration", 8.8,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("qwen3-vl-235b-a22b-instruct", "qwen", "Qwen/Qwen3-VL-235B-A22B-Instruct",

@@ -76,6 +76,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.mllama import MllamaForConditionalGeneration
 
         return MllamaForConditionalGeneration
+    if cfg.architecture == "Mistral3ForConditionalGeneration" or cfg.model_type == "mistral3":
+        from ome_amd.models.mistral3 import Mistral3ForConditionalGeneration
+
+        return Mistral3ForConditionalGeneration
     if cfg.architecture == "CLIPModel":
         from ome_amd.models.clip import CLIPModel
 
@@ -122,6 +126,7 @@ def supported(arch: str) -> bool:
         arch in DECODER_ARCHS or arch in ENCODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
         arch == "DeciLMForCausalLM" or arch in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM") or \
         arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or \
+        arch == "Mistral3ForConditionalGeneration" or \
         arch == "GptOssForCausalLM"
 
 

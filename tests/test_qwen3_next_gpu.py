@@ -14,13 +14,16 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.mark.parametrize("aligned", [True, False])
 @pytest.mark.parametrize("dk,dv,Hk,Hv", [(128, 128, 2, 4), (64, 128, 4, 4), (128, 64, 1, 2)])
-def test_gdn_scan_matches_reference(dk, dv, Hk, Hv):
+def test_gdn_scan_matches_reference(dk, dv, Hk, Hv, aligned):
     torch.manual_seed(0)
     kd, vd = Hk * dk, Hv * dv
     lens = [5, 1, 70]
     T = sum(lens)
-    proj = (torch.randn(T, 2 * kd + vd + 2 * Hv + 8, device=DEV)).to(torch.bfloat16)
+    # row stride % 8 == 0 -> the v2 kernel (the model's conv output always is); odd -> the v1 fallback
+    pad = 8 - (2 * Hv) % 8 if aligned else 1
+    proj = (torch.randn(T, 2 * kd + vd + 2 * Hv + pad, device=DEV)).to(torch.bfloat16)
     q, k, v = proj[:, :kd], proj[:, kd:2 * kd], proj[:, 2 * kd:2 * kd + vd]
     b, a = proj[:, 2 * kd + vd:2 * kd + vd + Hv], proj[:, 2 * kd + vd + Hv:2 * kd + vd + 2 * Hv]
     A_log = torch.rand(Hv, device=DEV) * 2 - 1
