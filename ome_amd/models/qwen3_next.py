@@ -10,7 +10,7 @@ grouped-GEMM experts, a shared expert scaled by ``sigmoid(shared_expert_gate(x))
   per-tensor blocks, so the conv input and the recurrence read plain row-strided views) ->
   causal depthwise conv1d + SiLU over q|k|v (``ome_ssm_conv1d``, per-slot conv state) ->
   ``ome_gdn_scan`` (L2-norm of q / k, ``g`` / ``beta`` from a / b, the delta-rule recurrence with
-  the fp32 [dk, dv] state of every v-head kept in VGPRs, per request slot) -> norm-then-gate
+  each v-head's fp32 state spread over DPP rows of lanes in VGPRs, per request slot) -> norm-then-gate
   RMSNorm ``w * norm(o) * silu(z)`` (``ome_gated_rmsnorm`` norm_first) -> out_proj GEMM.
 * Gated attention: q_proj's per-head [query | gate] halves are split at load into one fused
   [q | k | v | gate] projection; per-head q / k RMSNorm + partial NeoX RoPE (rot_dim = D / 4)
@@ -20,8 +20,8 @@ grouped-GEMM experts, a shared expert scaled by ``sigmoid(shared_expert_gate(x))
 
 Only the attention layers own KV pages (``kv_layers``); recurrent state lives per request slot
 (``alloc_state``: conv [n_lin, slots, conv_dim, K-1] in the model dtype, delta-rule state
-[n_lin, slots, Hv, dk, dv] fp32 -- ~2 MiB per layer-slot at the 80B shape, sized before the KV
-pool).  The prefix cache is off for stateful models.  One GPU per replica: 80B bf16 weights
+[n_lin, slots, Hv, dv, dk] fp32, transposed -- ~2 MiB per layer-slot at the 80B shape, sized
+before the KV pool).  The prefix cache is off for stateful models.  One GPU per replica: 80B bf16 weights
 (~160 GB) fit one MI355X, so TP / PP are not implemented for this family.
 """
 from __future__ import annotations
@@ -86,7 +86,7 @@ class Qwen3NextForCausalLM(MoEForCausalLM):
     def alloc_state(self, slots: int) -> None:
         n = len(self.lin_layers)
         self.conv_state = torch.zeros(n, slots, self.conv_dim, self.K - 1, dtype=self.dtype, device=self.device)
-        self.rec_state = torch.zeros(n, slots, self.Hv, self.dk, self.dv, dtype=torch.float32, device=self.device)
+        self.rec_state = torch.zeros(n, slots, self.Hv, self.dv, self.dk, dtype=torch.float32, device=self.device)
 
     # ------------------------------------------------------------------ weights
     def init_random(self, seed: int = 0, std: float = 0.02) -> "Qwen3NextForCausalLM":

@@ -115,22 +115,25 @@ def ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min: float, state, cu, slot, reset, 
 
 
 def gdn_scan(q, k, v, a, b, A_log, dt_bias, state, cu, slot, reset, Hv: int, Hk: int,
-             out: torch.Tensor | None = None) -> torch.Tensor:
+             out: torch.Tensor | None = None, v1: bool = False) -> torch.Tensor:
     """Gated DeltaNet recurrence (Qwen3-Next), per sequence rows ``cu[s]:cu[s+1]``: q / k [T, Hk*dk]
     and v [T, Hv*dv] are row-strided views of one buffer, a / b [T, Hv] views of another, A_log /
-    dt_bias fp32 [Hv], state fp32 [slots, Hv, dk, dv].  q / k are L2-normalised in the kernel."""
+    dt_bias fp32 [Hv], state fp32 [slots, Hv, dv, dk] (S transposed: columns contiguous).  q / k
+    are L2-normalised in the kernel (prep pass + DPP-row scan; ``v1`` selects the
+    one-lane-per-column kernel)."""
     T = q.shape[0]
-    dk, dv = state.shape[2], state.shape[3]
+    dv, dk = state.shape[2], state.shape[3]
     out = torch.empty(T, Hv * dv, dtype=v.dtype, device=v.device) if out is None else out
     if not _gpu(q):
         return ref.gdn_scan(q, k, v, a, b, A_log, dt_bias, state, cu, slot, reset, Hv, Hk, out)
     assert q.stride(0) == k.stride(0) == v.stride(0) and a.stride(0) == b.stride(0)
     assert q.stride(1) == k.stride(1) == v.stride(1) == a.stride(1) == 1 and out.stride(1) == 1
     assert state.is_contiguous() and state.dtype == torch.float32 and q.dtype == torch.bfloat16
+    ws = None if v1 else torch.empty(T * (2 * Hk * dk + Hk + 2 * Hv), dtype=torch.float32, device=q.device)
     call("ome_gdn_scan", q.data_ptr(), k.data_ptr(), v.data_ptr(), q.stride(0), a.data_ptr(), b.data_ptr(),
          a.stride(0), A_log.data_ptr(), dt_bias.data_ptr(), state.data_ptr(), out.data_ptr(), out.stride(0),
-         _i32(cu).data_ptr(), _i32(slot).data_ptr(), _i32(reset).data_ptr(), slot.shape[0], Hv, Hk, dk, dv,
-         stream_ptr())
+         _i32(cu).data_ptr(), _i32(slot).data_ptr(), _i32(reset).data_ptr(), slot.shape[0], T, Hv, Hk, dk, dv,
+         ptr(ws), stream_ptr())
     return out
 
 

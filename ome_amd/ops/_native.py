@@ -35,7 +35,7 @@ _SIGNATURES = {
         "ome_ssm_scan": [vp, i64, vp, i64, vp, vp, i64, vp, vp, vp, f32, vp, vp, i64, vp, vp, vp, i32, i32, i32,
                          i32, i32, vp],
         "ome_gdn_scan": [vp, vp, vp, i64, vp, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32,
-                         vp],
+                         i32, vp, vp],
         "ome_gated_rmsnorm": [vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, f32, i32, vp],
         "ome_layernorm": [vp, i64, vp, i64, vp, vp, vp, i64, i32, i32, f32, vp],
         "ome_embedding": [vp, vp, vp, i32, i32, i32, i32, vp],

@@ -92,15 +92,16 @@ def ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min, state, cu, slot, reset, H, P, N
 
 
 def gdn_scan(q, k, v, a, b, A_log, dt_bias, state, cu, slot, reset, Hv, Hk, out):
-    """Gated delta rule, recurrent per sequence; ``state`` [slots, Hv, dk, dv] fp32."""
-    dk, dv = state.shape[2], state.shape[3]
+    """Gated delta rule, recurrent per sequence; ``state`` [slots, Hv, dv, dk] fp32 (S transposed)."""
+    dv, dk = state.shape[2], state.shape[3]
     rep = Hv // Hk
     for s in range(len(slot)):
         r0, r1 = int(cu[s]), int(cu[s + 1])
         if r1 <= r0:
             continue
         st = state[int(slot[s])]
-        S = torch.zeros_like(st) if int(reset[s]) else st.clone()                              # [Hv, dk, dv]
+        S = torch.zeros(Hv, dk, dv) if int(reset[s]) else st.transpose(1, 2).clone()             # [Hv, dk, dv]
+        S = S.to(st.device)
         for r in range(r0, r1):
             kr = k[r].float().view(Hk, dk)
             kr = kr * torch.rsqrt(kr.pow(2).sum(-1, keepdim=True) + 1e-6)
@@ -114,7 +115,7 @@ def gdn_scan(q, k, v, a, b, A_log, dt_bias, state, cu, slot, reset, Hv, Hk, out)
             delta = (v[r].float().view(Hv, dv) - kv) * beta[:, None]
             S = S + kr[..., None] * delta[:, None, :]
             out[r] = (S * qr[..., None]).sum(1).reshape(-1).to(out.dtype)
-        st.copy_(S)
+        st.copy_(S.transpose(1, 2))
     return out
 
 

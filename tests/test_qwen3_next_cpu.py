@@ -84,7 +84,7 @@ def test_gdn_reference_matches_recurrence():
     q, k, v = torch.randn(T, Hk * dk), torch.randn(T, Hk * dk), torch.randn(T, Hv * dv)
     a, b = torch.randn(T, Hv), torch.randn(T, Hv)
     A_log, dtb = torch.rand(Hv), torch.randn(Hv)
-    st = torch.zeros(2, Hv, dk, dv)
+    st = torch.zeros(2, Hv, dv, dk)
     cu, slot, reset = (torch.tensor(x, dtype=torch.int32) for x in ([0, T], [1], [1]))
     y = ops.gdn_scan(q, k, v, a, b, A_log, dtb, st, cu, slot, reset, Hv, Hk)
     S = torch.zeros(Hv, dk, dv)
@@ -97,4 +97,4 @@ def test_gdn_reference_matches_recurrence():
         S = S + torch.einsum("hk,hv->hkv", kr, (v[r].view(Hv, dv) - kv) * torch.sigmoid(b[r])[:, None])
         want = torch.einsum("hkv,hk->hv", S, qr)
         assert torch.allclose(y[r].view(Hv, dv), want, atol=1e-4)
-    assert torch.allclose(st[1], S, atol=1e-5) and st[0].abs().max() == 0
+    assert torch.allclose(st[1], S.transpose(1, 2), atol=1e-5) and st[0].abs().max() == 0

@@ -14,15 +14,15 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
+@pytest.mark.parametrize("v1", [False, True])
 @pytest.mark.parametrize("aligned", [True, False])
 @pytest.mark.parametrize("dk,dv,Hk,Hv", [(128, 128, 2, 4), (64, 128, 4, 4), (128, 64, 1, 2)])
-def test_gdn_scan_matches_reference(dk, dv, Hk, Hv, aligned):
+def test_gdn_scan_matches_reference(dk, dv, Hk, Hv, aligned, v1):
     torch.manual_seed(0)
     kd, vd = Hk * dk, Hv * dv
     lens = [5, 1, 70]
     T = sum(lens)
-    # row stride % 8 == 0 -> the v2 kernel (the model's conv output always is); odd -> the v1 fallback
-    pad = 8 - (2 * Hv) % 8 if aligned else 1
+    pad = 8 - (2 * Hv) % 8 if aligned else 1   # row stride % 8 == 0 (the model's conv output) or odd
     proj = (torch.randn(T, 2 * kd + vd + 2 * Hv + pad, device=DEV)).to(torch.bfloat16)
     q, k, v = proj[:, :kd], proj[:, kd:2 * kd], proj[:, 2 * kd:2 * kd + vd]
     b, a = proj[:, 2 * kd + vd:2 * kd + vd + Hv], proj[:, 2 * kd + vd + Hv:2 * kd + vd + 2 * Hv]
@@ -31,9 +31,9 @@ def test_gdn_scan_matches_reference(dk, dv, Hk, Hv, aligned):
     cu = torch.tensor([0, 5, 6, 76], dtype=torch.int32, device=DEV)
     slot = torch.tensor([2, 0, 3], dtype=torch.int32, device=DEV)
     reset = torch.tensor([1, 0, 0], dtype=torch.int32, device=DEV)
-    st0 = torch.randn(4, Hv, dk, dv, device=DEV) * 0.1
+    st0 = torch.randn(4, Hv, dv, dk, device=DEV) * 0.1
     st_k, st_r = st0.clone(), st0.clone().cpu()
-    y_k = ops.gdn_scan(q, k, v, a, b, A_log, dtb, st_k, cu, slot, reset, Hv, Hk)
+    y_k = ops.gdn_scan(q, k, v, a, b, A_log, dtb, st_k, cu, slot, reset, Hv, Hk, v1=v1)
     c = lambda t: t.cpu()  # noqa: E731
     y_r = ref.gdn_scan(c(q), c(k), c(v), c(a), c(b), c(A_log), c(dtb), st_r, c(cu), c(slot), c(reset), Hv, Hk,
                        torch.empty(T, vd, dtype=torch.bfloat16))
