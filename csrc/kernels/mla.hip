@@ -1,8 +1,9 @@
 // Multi-head latent attention (DeepSeek-V2/V3, Kimi-K2) in the absorbed
 // form, for gfx950.
 //
-// Every layer caches one 576-wide latent row per token: [c_kv (512, kv_a_layernorm'd) | k_pe
-// (64, roped)], paged as cache[pages, 16, 576] bf16.  With W_UK folded into the query
+// Every layer caches one latent row per token: [c_kv (kv_lora_rank, kv_a_layernorm'd) | k_pe
+// (roped)], paged as cache[pages, 16, DK] bf16 -- DK = 576 = 512 + 64 for DeepSeek-V2/V3 / Kimi-K2,
+// 288 = 256 + 32 for MiniCPM3 (template instances below).  With W_UK folded into the query
 // (q_lat = [q_nope . W_UK | q_pe], 576 wide) and W_UV applied after the attention, MLA is
 // multi-QUERY attention over that latent: scores use all 576 dims, values are the first 512.
 // The same kernel serves decode, prefill and chunked prefill: a work item is one query token
@@ -25,15 +26,18 @@
 
 namespace {
 
-constexpr int DK = 576, DV = 512, CH = DK / 8;  // 72 chunks of 8 bf16 per key row
-constexpr int KT = 32;                          // keys per iteration (two 16-token pages)
+constexpr int KT = 32;   // keys per iteration (two 16-token pages)
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4 mfma16x32(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * CH + (chunk ^ (row & 7)); }
+// LDS row stride in 16-byte chunks, padded to a multiple of 8 so the xor swizzle stays in the row
+template <int DK>
+constexpr int lds_chunks() { return ((DK / 8) + 7) / 8 * 8; }
+template <int DK>
+__device__ __forceinline__ int swz(int row, int chunk) { return row * lds_chunks<DK>() + (chunk ^ (row & 7)); }
 
 __device__ __forceinline__ bf16x4 tr_read(const bf16* lds_base, int byte_off) {
   const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -44,12 +48,14 @@ __device__ __forceinline__ bf16x4 tr_read(const bf16* lds_base, int byte_off) {
 
 }  // namespace
 
+template <int DK, int DV>
 __global__ __launch_bounds__(256) void mla_attn_kernel(
     const bf16* __restrict__ q, int64_t q_stride_t, const bf16* __restrict__ cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_row,
     const int* __restrict__ kv_lens, int H, float scale_log2, int parts, bf16* __restrict__ out,
     int64_t out_stride_t, float* __restrict__ ws_o, float* __restrict__ ws_ml) {
-  __shared__ __attribute__((aligned(16))) bf16 sK[KT * DK];
+  constexpr int CH = DK / 8, NB = DV / 64, NST = (KT * CH + 255) / 256;   // NB 16-dim blocks per wave
+  __shared__ __attribute__((aligned(16))) bf16 sK[KT * lds_chunks<DK>() * 8];
   const int t = blockIdx.x, h0 = blockIdx.y * 16, part = blockIdx.z;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int col = lane & 15, g = lane >> 4;
@@ -61,23 +67,26 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
   const int* bt = block_tables + (int64_t)tok_row[t] * bt_stride;
   const int64_t ws_row = ((int64_t)t * H + h0 + col) * parts + part;
 
+  const bool hv = h0 + col < H;   // head groups are 16 wide; the last may be partial (MiniCPM3: 40)
+
   // ---- Q^T operand: lane (col, g) holds Q[h0+col][32 s + 8 g + j] ----
   bf16x8 qf[DK / 32];
-  const bf16* qp = q + (int64_t)t * q_stride_t + (int64_t)(h0 + col) * DK + 8 * g;
+  const bf16* qp = q + (int64_t)t * q_stride_t + (int64_t)(hv ? h0 + col : 0) * DK + 8 * g;
 #pragma unroll
-  for (int s = 0; s < DK / 32; ++s) qf[s] = ld8(qp + 32 * s);
+  for (int s = 0; s < DK / 32; ++s) qf[s] = hv ? ld8(qp + 32 * s) : bf16x8{};
 
-  f32x4 o[8];
+  f32x4 o[NB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < NB; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = OME_NEG_INF, lsum = 0.f;
 
-  // staging: 32 keys x 72 chunks = 2304 chunks, 9 per thread; chunk c -> (key c/72, x c%72)
-  bf16x8 stage[9];
+  // staging: 32 keys x CH chunks, NST per thread; chunk c -> (key c / CH, x c % CH)
+  bf16x8 stage[NST];
   auto load_pair = [&](int pr) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < NST; ++i) {
       const int c = tid + 256 * i;
+      if ((KT * CH) % 256 != 0 && c >= KT * CH) break;
       const int key = c / CH, x = c - key * CH;
       const int pg = 2 * pr + (key >> 4);
       const int page = bt[pg < n_pages ? pg : 0];
@@ -89,10 +98,11 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
   for (int pr = pair_begin; pr < pair_end; ++pr) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
+    for (int i = 0; i < NST; ++i) {
       const int c = tid + 256 * i;
+      if ((KT * CH) % 256 != 0 && c >= KT * CH) break;
       const int key = c / CH, x = c - key * CH;
-      *reinterpret_cast<bf16x8*>(&sK[swz(key, x) * 8]) = stage[i];
+      *reinterpret_cast<bf16x8*>(&sK[swz<DK>(key, x) * 8]) = stage[i];
     }
     __syncthreads();
     if (pr + 1 < pair_end) load_pair(pr + 1);
@@ -101,8 +111,8 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < DK / 32; ++s) {
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[swz(col, 4 * s + g) * 8]);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[swz(16 + col, 4 * s + g) * 8]);
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[swz<DK>(col, 4 * s + g) * 8]);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[swz<DK>(16 + col, 4 * s + g) * 8]);
       s0 = mfma16x32(a0, qf[s], s0);
       s1 = mfma16x32(a1, qf[s], s1);
     }
@@ -133,16 +143,16 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
     ps += __shfl_xor(ps, 32);
     lsum = lsum * alpha + ps;
     m = m_new;
-    // ---- O^T [this wave's 128 dims x 16 heads] += V^T . P^T ----
+    // ---- O^T [this wave's DV / 4 dims x 16 heads] += V^T . P^T ----
     // tr-read block: rows = keys 4g + q (+16 for page B), cols = 16 dims; lane 4q+p of the
     // group addresses row q, columns 4p..4p+3.
     const int qrow = (lane & 15) >> 2, pcol = lane & 3;
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb) {
-      const int d0 = wave * 128 + 16 * nb + 4 * pcol;  // first of this lane's 4 dims
+    for (int nb = 0; nb < NB; ++nb) {
+      const int d0 = wave * (DV / 4) + 16 * nb + 4 * pcol;  // first of this lane's 4 dims
       const int ra = 4 * g + qrow, rb = 16 + 4 * g + qrow;
-      const int oa = swz(ra, d0 >> 3) * 16 + (d0 & 7) * 2;
-      const int ob = swz(rb, d0 >> 3) * 16 + (d0 & 7) * 2;
+      const int oa = swz<DK>(ra, d0 >> 3) * 16 + (d0 & 7) * 2;
+      const int ob = swz<DK>(rb, d0 >> 3) * 16 + (d0 & 7) * 2;
       const bf16x4 va = tr_read(sK, oa), vb = tr_read(sK, ob);
       bf16x8 a;
       a[0] = va[0]; a[1] = va[1]; a[2] = va[2]; a[3] = va[3];
@@ -155,19 +165,20 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
 
   // ---- epilogue: O^T lane map dim = 16 nb + 4 g + i, head = col ----
   const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  if (!hv) return;
   if (parts == 1) {
-    bf16* op = out + (int64_t)t * out_stride_t + (int64_t)(h0 + col) * DV + wave * 128 + 4 * g;
+    bf16* op = out + (int64_t)t * out_stride_t + (int64_t)(h0 + col) * DV + wave * (DV / 4) + 4 * g;
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
       bf16x4 v;
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = (bf16)(o[nb][i] * inv);
       *reinterpret_cast<bf16x4*>(op + 16 * nb) = v;
     }
   } else {
-    float* wp = ws_o + ws_row * DV + wave * 128 + 4 * g;
+    float* wp = ws_o + ws_row * DV + wave * (DV / 4) + 4 * g;
 #pragma unroll
-    for (int nb = 0; nb < 8; ++nb)
+    for (int nb = 0; nb < NB; ++nb)
       *reinterpret_cast<f32x4*>(wp + 16 * nb) = f32x4{o[nb][0] * inv, o[nb][1] * inv, o[nb][2] * inv,
                                                        o[nb][3] * inv};
     if (wave == 0 && g == 0) {
@@ -177,7 +188,8 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
   }
 }
 
-// merge split-K partitions: one workgroup per (token, head), 128 threads x 4 dims
+// merge split-K partitions: one workgroup per (token, head), DV / 4 threads x 4 dims
+template <int DV>
 __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict__ ws_o,
                                                          const float* __restrict__ ws_ml, int H, int parts,
                                                          bf16* __restrict__ out, int64_t out_stride_t) {
@@ -203,23 +215,37 @@ __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict
   *reinterpret_cast<bf16x4*>(out + (int64_t)t * out_stride_t + (int64_t)h * DV + 4 * threadIdx.x) = r;
 }
 
-// q [T, H, 576] (token stride q_stride_t), cache [pages, 16, 576], out [T, H, 512].
-// tok_row[t] = block-table row of token t; kv_lens[t] = keys visible to token t (causal).
-// parts > 1 needs ws_o [T*H*parts*512] f32 and ws_ml [T*H*parts*2] f32.
+// q [T, H, DK] (token stride q_stride_t), cache [pages, 16, DK], out [T, H, DV] with
+// (DK, DV) = (576, 512) or (288, 256).  tok_row[t] = block-table row of token t; kv_lens[t] =
+// keys visible to token t (causal).  parts > 1 needs ws_o [T*H*parts*DV] f32 and ws_ml
+// [T*H*parts*2] f32.
+template <int DK, int DV>
+static void mla_launch(const void* q, int64_t q_stride_t, const void* cache, const int* block_tables, int bt_stride,
+                       const int* tok_row, const int* kv_lens, int T, int H, float scale_log2, int parts, void* out,
+                       int64_t out_stride_t, float* ws_o, float* ws_ml, hipStream_t stream) {
+  dim3 grid(T, (H + 15) / 16, parts);
+  mla_attn_kernel<DK, DV><<<grid, 256, 0, stream>>>((const bf16*)q, q_stride_t, (const bf16*)cache, block_tables,
+                                                    bt_stride, tok_row, kv_lens, H, scale_log2, parts, (bf16*)out,
+                                                    out_stride_t, ws_o, ws_ml);
+  if (parts > 1)
+    mla_reduce_kernel<DV><<<dim3(T, H), DV / 4, 0, stream>>>(ws_o, ws_ml, H, parts, (bf16*)out, out_stride_t);
+}
+
 OME_API int ome_mla_attn(const void* q, int64_t q_stride_t, const void* cache, const int* block_tables,
-                         int bt_stride, const int* tok_row, const int* kv_lens, int T, int H, float scale,
-                         int parts, void* out, int64_t out_stride_t, float* ws_o, float* ws_ml, hipStream_t stream) {
+                         int bt_stride, const int* tok_row, const int* kv_lens, int T, int H, int dk, int dv,
+                         float scale, int parts, void* out, int64_t out_stride_t, float* ws_o, float* ws_ml,
+                         hipStream_t stream) {
   if (T <= 0) return 0;
-  if (H % 16 || parts < 1 || (parts > 1 && (!ws_o || !ws_ml))) return -2;
+  if (H <= 0 || parts < 1 || (parts > 1 && (!ws_o || !ws_ml))) return -2;
   const float scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(T, H / 16, parts);
-  mla_attn_kernel<<<grid, 256, 0, stream>>>((const bf16*)q, q_stride_t, (const bf16*)cache, block_tables, bt_stride,
-                                            tok_row, kv_lens, H, scale_log2, parts, (bf16*)out, out_stride_t, ws_o,
-                                            ws_ml);
+  if (dk == 576 && dv == 512)
+    mla_launch<576, 512>(q, q_stride_t, cache, block_tables, bt_stride, tok_row, kv_lens, T, H, scale_log2, parts, out,
+                         out_stride_t, ws_o, ws_ml, stream);
+  else if (dk == 288 && dv == 256)
+    mla_launch<288, 256>(q, q_stride_t, cache, block_tables, bt_stride, tok_row, kv_lens, T, H, scale_log2, parts, out,
+                         out_stride_t, ws_o, ws_ml, stream);
+  else
+    return -3;
   OME_CHECK_LAUNCH();
-  if (parts > 1) {
-    mla_reduce_kernel<<<dim3(T, H), 128, 0, stream>>>(ws_o, ws_ml, H, parts, (bf16*)out, out_stride_t);
-    OME_CHECK_LAUNCH();
-  }
   return 0;
 }

@@ -78,6 +78,7 @@ FAMILIES: list[Family] = [
     Family("mistral-small-3-1-24b-instruct-2503", "mistralai", "mistralai/Mistral-Small-3.1-24B-Instruct-2503",
            "Mistral3ForConditionalGeneration", 24.0, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"],
            args=['--tool-call-parser', 'mistral']),
+    Family("minicpm3-4b", "openbmb", "openbmb/MiniCPM3-4B", "MiniCPM3ForCausalLM", 4.1),
     Family("qwen3-vl-8b-instruct", "qwen", "Qwen/Qwen3-VL-8B-Instruct", "Qwen3VLForConditionalGeneration", 8.8,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("qwen3-vl-235b-a22b-instruct", "qwen", "Qwen/Qwen3-VL-235B-A22B-Instruct",

@@ -108,6 +108,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.layernorm_lm import LayerNormForCausalLM
 
         return LayerNormForCausalLM
+    if cfg.architecture == "MiniCPM3ForCausalLM" or cfg.model_type == "minicpm3":
+        from ome_amd.models.minicpm3 import MiniCPM3ForCausalLM
+
+        return MiniCPM3ForCausalLM
     if cfg.is_mla:
         from ome_amd.models.deepseek import DeepseekForCausalLM
 
@@ -126,7 +130,7 @@ def supported(arch: str) -> bool:
         arch in DECODER_ARCHS or arch in ENCODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
         arch == "DeciLMForCausalLM" or arch in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM") or \
         arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or \
-        arch == "Mistral3ForConditionalGeneration" or \
+        arch == "Mistral3ForConditionalGeneration" or arch == "MiniCPM3ForCausalLM" or \
         arch == "GptOssForCausalLM"
 
 

@@ -36,6 +36,8 @@ from ome_amd.parallel import state as pstate
 
 KV_LATENT = 512
 ROPE_DIM = 64
+#: (kv_lora_rank, qk_rope_head_dim) pairs with a compiled MLA kernel (csrc/kernels/mla.hip)
+MLA_SHAPES = {(512, 64), (256, 32)}
 
 
 def _yarn_mscale(scale: float, m: float) -> float:
@@ -44,8 +46,8 @@ def _yarn_mscale(scale: float, m: float) -> float:
 
 class DeepseekForCausalLM(LlamaForCausalLM):
     def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
-        if cfg.kv_lora_rank != KV_LATENT or cfg.qk_rope_head_dim != ROPE_DIM:
-            raise ValueError(f"MLA kernel is built for kv_lora_rank={KV_LATENT}, qk_rope_head_dim={ROPE_DIM} "
+        if (cfg.kv_lora_rank, cfg.qk_rope_head_dim) not in MLA_SHAPES:
+            raise ValueError(f"MLA kernel is built for (kv_lora_rank, qk_rope_head_dim) in {sorted(MLA_SHAPES)} "
                              f"(got {cfg.kv_lora_rank}, {cfg.qk_rope_head_dim})")
         # the dense base sets up TP shapes from num_heads; MLA has no kv heads of its own
         super().__init__(cfg, device, dtype, max_positions)
@@ -54,6 +56,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
             raise ValueError("num_heads must divide by tp")
         self.Hl = cfg.num_heads // st.tp_size
         self.nope, self.rope, self.vd = cfg.qk_nope_head_dim, cfg.qk_rope_head_dim, cfg.v_head_dim
+        self.lat = cfg.kv_lora_rank      # latent width; cache rows are [lat | rope]
         self.qk_dim = self.nope + self.rope
         self.qlr = cfg.q_lora_rank
         scale = self.qk_dim ** -0.5
@@ -100,7 +103,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         self.w2: list = [None] * L
         self.w_sgu: list = [None] * L
         self.w_sd: list = [None] * L
-        self.kv_layout = (1, KV_LATENT + ROPE_DIM, 0)
+        self.kv_layout = (1, self.lat + self.rope, 0)
         self.tune_gemms = False  # TunableOp pre-capture tuning is validated on the dense family only
         self._ws = None
         self._arange = None
@@ -115,13 +118,13 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         st = pstate.get()
         inter = -(-cfg.intermediate_size // st.tp_size)
         for i in self.layers:
-            self.w_qa[i] = self._alloc(self.qlr + KV_LATENT + ROPE_DIM, H, std=std, gen=gen)
+            self.w_qa[i] = self._alloc(self.qlr + self.lat + self.rope, H, std=std, gen=gen)
             if self.qlr:
                 self.qa_ln[i] = self._alloc(self.qlr, std=None, gen=gen)
             self.w_qb[i] = self._alloc(Hl * self.qk_dim, self.qlr or H, std=std, gen=gen)
-            self.kva_ln[i] = self._alloc(KV_LATENT, std=None, gen=gen)
-            self.w_uk[i] = self._alloc(Hl, self.nope, KV_LATENT, std=std, gen=gen)
-            self.w_uv[i] = self._alloc(Hl, KV_LATENT, self.vd, std=std, gen=gen)
+            self.kva_ln[i] = self._alloc(self.lat, std=None, gen=gen)
+            self.w_uk[i] = self._alloc(Hl, self.nope, self.lat, std=std, gen=gen)
+            self.w_uv[i] = self._alloc(Hl, self.lat, self.vd, std=std, gen=gen)
             self.w_o[i] = self._alloc(H, Hl * self.vd, std=out_std, gen=gen)
             self.ln1[i] = self._alloc(H, std=None, gen=gen)
             self.ln2[i] = self._alloc(H, std=None, gen=gen)
@@ -161,10 +164,11 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         projection rows once so the rope dims come out as [evens | odds] (NeoX layout)."""
         if not self.interleaved_rope:
             return w
-        perm = torch.cat([torch.arange(0, ROPE_DIM, 2), torch.arange(1, ROPE_DIM, 2)])
+        R = self.rope
+        perm = torch.cat([torch.arange(0, R, 2), torch.arange(1, R, 2)])
         idx = []
         for h in range(n_heads):
-            base = h * head_dim + head_dim - ROPE_DIM
+            base = h * head_dim + head_dim - R
             idx.append(torch.arange(h * head_dim, base))
             idx.append(base + perm)
         return w[torch.cat(idx).to(w.device)]
@@ -212,7 +216,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 full = self._deinterleave_rows(w, self.qk_dim, cfg.num_heads)
                 self.w_qb[i] = put(rows(full, Hl * self.qk_dim))
             elif rest == "self_attn.kv_b_proj.weight":
-                kvb = rows(w, Hl * (self.nope + self.vd)).reshape(Hl, self.nope + self.vd, KV_LATENT)
+                kvb = rows(w, Hl * (self.nope + self.vd)).reshape(Hl, self.nope + self.vd, self.lat)
                 self.w_uk[i] = put(kvb[:, : self.nope, :])
                 self.w_uv[i] = put(kvb[:, self.nope:, :].transpose(1, 2))
             elif rest == "self_attn.o_proj.weight":
@@ -233,7 +237,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 d[rest] = w
         for i, d in parts.items():
             if "self_attn.kv_a_proj_with_mqa.weight" in d:
-                kva = self._deinterleave_rows(d["self_attn.kv_a_proj_with_mqa.weight"], KV_LATENT + ROPE_DIM, 1)
+                kva = self._deinterleave_rows(d["self_attn.kv_a_proj_with_mqa.weight"], self.lat + self.rope, 1)
                 qa = d.get("self_attn.q_a_proj.weight")
                 self.w_qa[i] = put(torch.cat([qa, kva], 0) if qa is not None else kva)
             if "mlp.gate_proj.weight" in d:
@@ -285,7 +289,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
     # ------------------------------------------------------------------ forward
     def _rope(self, x: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
         cs = self.cos_sin.index_select(0, positions.long())
-        half = ROPE_DIM // 2
+        half = self.rope // 2
         cos, sin = cs[:, :half], cs[:, half:]
         if x.dim() == 3:
             cos, sin = cos[:, None, :], sin[:, None, :]
@@ -319,23 +323,24 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         else:
             q = linear(x, self.w_qb[i])
         ckv = a[:, self.qlr:]
-        c = ops.rmsnorm(ckv[:, :KV_LATENT].contiguous(), self.kva_ln[i], self.eps)
+        lat = self.lat
+        c = ops.rmsnorm(ckv[:, :lat].contiguous(), self.kva_ln[i], self.eps)
         q = q.view(T, Hl, self.qk_dim)
         q_pe = self._rope(q[..., self.nope:], meta.positions)
-        k_pe = self._rope(ckv[:, KV_LATENT:], meta.positions)
+        k_pe = self._rope(ckv[:, lat:], meta.positions)
         cache = kv.k[i]
-        flat = cache.view(-1, KV_LATENT + ROPE_DIM)
+        flat = cache.view(-1, lat + self.rope)
         # padding rows carry slot -1: park them in the scratch page 0
         flat.index_copy_(0, meta.slots.long().clamp_min(0), torch.cat([c, k_pe], -1))
         q_nope = q[..., : self.nope].transpose(0, 1).contiguous()         # [Hl, T, nope]
-        q_lat = torch.bmm(q_nope, self.w_uk[i])                           # [Hl, T, 512]
-        q_full = torch.cat([q_lat.transpose(0, 1), q_pe], -1).contiguous()  # [T, Hl, 576]
-        o_lat = torch.empty(T, Hl, KV_LATENT, dtype=x.dtype, device=x.device)
+        q_lat = torch.bmm(q_nope, self.w_uk[i])                           # [Hl, T, lat]
+        q_full = torch.cat([q_lat.transpose(0, 1), q_pe], -1).contiguous()  # [T, Hl, lat + rope]
+        o_lat = torch.empty(T, Hl, lat, dtype=x.dtype, device=x.device)
         if x.is_cuda and self._ws is None:
             self._ws = ops.MLAWorkspace(x.device)
-        cache3 = cache.view(cache.shape[0], -1, KV_LATENT + ROPE_DIM)
+        cache3 = cache.view(cache.shape[0], -1, lat + self.rope)
         for s, e, bt, rows, lens in self._token_rows(meta, T):
-            ops.mla_attn(q_full[s:e], cache3, bt, rows, lens, self.scale, self._ws, out=o_lat[s:e])
+            ops.mla_attn(q_full[s:e], cache3, bt, rows, lens, self.scale, self._ws, out=o_lat[s:e], dv=lat)
         o = torch.bmm(o_lat.transpose(0, 1).contiguous(), self.w_uv[i])   # [Hl, T, vd]
         o = o.transpose(0, 1).reshape(T, Hl * self.vd)
         return pstate.tp_all_reduce(linear(o, self.w_o[i]))

@@ -415,31 +415,33 @@ class MLAWorkspace:
 
     @classmethod
     def parts(cls, T: int, H: int) -> int:
-        wgs = T * (H // 16)
+        wgs = T * -(-H // 16)
         return 1 if wgs >= cls.TARGET_WGS else max(1, min(cls.MAX_PARTS, cls.TARGET_WGS // max(wgs, 1)))
 
 
 def mla_attn(q, cache, block_tables, tok_row, kv_lens, scale: float, ws: MLAWorkspace | None = None,
-             out: torch.Tensor | None = None) -> torch.Tensor:
-    """Absorbed multi-head latent attention (DeepSeek MLA) over the paged latent cache:
-    q [T, H, 576] (latent-projected nope part | roped pe part), cache [pages, 16, 576]
-    -> out [T, H, 512].  Token t sees keys [0, kv_lens[t]) of block-table row tok_row[t]."""
+             out: torch.Tensor | None = None, dv: int = 512) -> torch.Tensor:
+    """Absorbed multi-head latent attention (MLA) over the paged latent cache: q [T, H, DK]
+    (latent-projected nope part | roped pe part), cache [pages, 16, DK] -> out [T, H, dv] (values
+    = the first dv latent dims); (DK, dv) = (576, 512) DeepSeek / Kimi-K2 or (288, 256) MiniCPM3.
+    Token t sees keys [0, kv_lens[t]) of block-table row tok_row[t]."""
     if not _gpu(q):
-        r = ref.mla_attn(q, cache, block_tables, tok_row, kv_lens, scale)
+        r = ref.mla_attn(q, cache, block_tables, tok_row, kv_lens, scale, dv)
         if out is not None:
             out.copy_(r)
             return out
         return r
     T, H, DK = q.shape
-    assert DK == 576 and H % 16 == 0 and q.stride(2) == 1 and q.stride(1) == DK and cache.shape[-1] == 576
+    assert (DK, dv) in ((576, 512), (288, 256)), (DK, dv)
+    assert q.stride(2) == 1 and q.stride(1) == DK and cache.shape[-1] == DK
     if out is None:
-        out = torch.empty(T, H, 512, dtype=q.dtype, device=q.device)
+        out = torch.empty(T, H, dv, dtype=q.dtype, device=q.device)
     parts = MLAWorkspace.parts(T, H)
     if parts > 1 and ws is None:
         ws = MLAWorkspace(q.device)
     call("ome_mla_attn", q.data_ptr(), q.stride(0), cache.data_ptr(), _i32(block_tables).data_ptr(),
-         block_tables.stride(0), _i32(tok_row).data_ptr(), _i32(kv_lens).data_ptr(), T, H, float(scale), parts,
-         out.data_ptr(), out.stride(0), ws.ws_o.data_ptr() if parts > 1 else None,
+         block_tables.stride(0), _i32(tok_row).data_ptr(), _i32(kv_lens).data_ptr(), T, H, DK, dv, float(scale),
+         parts, out.data_ptr(), out.stride(0), ws.ws_o.data_ptr() if parts > 1 else None,
          ws.ws_ml.data_ptr() if parts > 1 else None, stream_ptr())
     return out
 

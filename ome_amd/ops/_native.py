@@ -44,7 +44,7 @@ _SIGNATURES = {
         "ome_apply_penalties": [vp, i32, i64, i32, i32, vp, i64, vp, vp, vp, vp, vp],
         "ome_update_counts": [vp, i64, vp, vp, vp, vp, vp, i32, vp],
         "ome_moe_route": [vp, i32, i64, i32, i32, i32, i32, i32, vp, i32, i32, i32, vp, vp, vp],
-        "ome_mla_attn": [vp, i64, vp, vp, i32, vp, vp, i32, i32, f32, i32, vp, i64, vp, vp, vp],
+        "ome_mla_attn": [vp, i64, vp, vp, i32, vp, vp, i32, i32, i32, i32, f32, i32, vp, i64, vp, vp, vp],
         "ome_moe_align": [vp, i32, i32, vp, vp, vp, vp],
         "ome_moe_gemm": [vp, i64, vp, i32, vp, vp, i32, i32, i32, i32, vp, i64, vp, i32, vp],
         "ome_moe_combine": [vp, vp, vp, i32, i32, i32, vp, f32, vp],

@@ -475,17 +475,17 @@ def fp8_gemm(qa, sa, qw, sw, block: int, bias=None, out_dtype=torch.bfloat16):
     return out.to(out_dtype)
 
 
-def mla_attn(q, cache, block_tables, tok_row, kv_lens, scale):
-    """Absorbed MLA: q [T, H, 576], cache [pages, 16, 576] -> out [T, H, 512] (values = the first
-    512 latent dims)."""
+def mla_attn(q, cache, block_tables, tok_row, kv_lens, scale, dv=512):
+    """Absorbed MLA: q [T, H, DK], cache [pages, 16, DK] -> out [T, H, dv] (values = the first dv
+    latent dims)."""
     T, H, DK = q.shape
     P = cache.shape[-2]
-    out = torch.empty(T, H, 512, dtype=q.dtype, device=q.device)
+    out = torch.empty(T, H, dv, dtype=q.dtype, device=q.device)
     flat = cache.reshape(-1, P, DK)
     for t in range(T):
         L = int(kv_lens[t])
         pages = block_tables[int(tok_row[t])][: -(-L // P)].long()
         kv = flat[pages].reshape(-1, DK)[:L].float()
         s = (q[t].float() @ kv.t()) * scale
-        out[t] = (torch.softmax(s, -1) @ kv[:, :512]).to(q.dtype)
+        out[t] = (torch.softmax(s, -1) @ kv[:, :dv]).to(q.dtype)
     return out

@@ -11,11 +11,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _setup(lens, seed=0):
+def _setup(lens, seed=0, dk=576):
     g = torch.Generator().manual_seed(seed)
     pages_per_row = -(-max(lens) // 16) + 1
     num_pages = len(lens) * pages_per_row + 1
-    cache = (torch.randn(num_pages, 16, 576, generator=g) * 0.5).to(torch.bfloat16)
+    cache = (torch.randn(num_pages, 16, dk, generator=g) * 0.5).to(torch.bfloat16)
     rows = len(lens)
     perm = torch.randperm(num_pages - 1, generator=g)[: rows * pages_per_row] + 1
     bt = perm.view(rows, pages_per_row).to(torch.int32)
@@ -51,6 +51,21 @@ def test_mla_prefill_causal(H):
     kl = torch.tensor(kv, dtype=torch.int32, device=DEV)
     out = ops.mla_attn(q, cache, bt, rows, kl, 0.0723)
     want = ref.mla_attn(q.cpu(), cache.cpu(), bt.cpu(), rows.cpu(), kl.cpu(), 0.0723)
+    assert (out.float().cpu() - want.float()).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("H", [40, 16, 8])
+@pytest.mark.parametrize("lens", [[1], [17, 33, 1000, 5], [64] * 40])
+def test_mla_minicpm3_shape(H, lens):
+    """(kv_lora_rank 256 | rope 32) latent rows, head counts that are not a multiple of 16."""
+    cache, bt = _setup(lens, dk=288)
+    T = len(lens)
+    q = (torch.randn(T, H, 288, device=DEV) * 0.3).to(torch.bfloat16)
+    rows = torch.arange(T, dtype=torch.int32, device=DEV)
+    kl = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    out = ops.mla_attn(q, cache, bt, rows, kl, 0.0723, dv=256)
+    want = ref.mla_attn(q.cpu(), cache.cpu(), bt.cpu(), rows.cpu(), kl.cpu(), 0.0723, 256)
+    assert out.shape == (T, H, 256)
     assert (out.float().cpu() - want.float()).abs().max().item() < 2e-2
 
 
