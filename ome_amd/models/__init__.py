@@ -76,6 +76,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.mllama import MllamaForConditionalGeneration
 
         return MllamaForConditionalGeneration
+    if cfg.architecture in ("InternVLChatModel", "InternVLForConditionalGeneration"):
+        from ome_amd.models.internvl import internvl_class
+
+        return internvl_class(cfg)
     if cfg.architecture == "Mistral3ForConditionalGeneration" or cfg.model_type == "mistral3":
         from ome_amd.models.mistral3 import Mistral3ForConditionalGeneration
 
@@ -131,6 +135,7 @@ def supported(arch: str) -> bool:
         arch == "DeciLMForCausalLM" or arch in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM") or \
         arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or \
         arch == "Mistral3ForConditionalGeneration" or arch == "MiniCPM3ForCausalLM" or \
+        arch in ("InternVLChatModel", "InternVLForConditionalGeneration") or \
         arch == "GptOssForCausalLM"
 
 

@@ -28,7 +28,7 @@ PADDED_HEAD_ARCHS = {"OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM", "
                      "ChatGLMForConditionalGeneration", "OlmoeForCausalLM", "GraniteMoeForCausalLM", "DbrxForCausalLM",
                      "Ernie4_5_MoeForCausalLM", "MiniMaxM2ForCausalLM"}
 # remote-code class names that end in "Model" but are causal LMs (not embedding models)
-CAUSAL_MODEL_CLASSES = {"ChatGLMModel", "QWenLMHeadModel", "TeleFLMModel"}
+CAUSAL_MODEL_CLASSES = {"ChatGLMModel", "QWenLMHeadModel", "TeleFLMModel", "InternVLChatModel"}
 
 
 def _standard_keys(c: dict[str, Any]) -> dict[str, Any]:
@@ -199,8 +199,8 @@ class ModelConfig:
 
     @classmethod
     def from_hf(cls, cfg: dict[str, Any]) -> "ModelConfig":
-        if cfg.get("text_config"):
-            text = _standard_keys(cfg["text_config"])
+        if cfg.get("text_config") or cfg.get("llm_config"):   # llm_config: InternVLChatModel
+            text = _standard_keys(cfg.get("text_config") or cfg["llm_config"])
         else:  # flat configs: keep the original keys (extra) next to the standard aliases
             cfg = text = _standard_keys(cfg)
         arch = (cfg.get("architectures") or ["LlamaForCausalLM"])[0]
