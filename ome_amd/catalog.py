@@ -81,6 +81,8 @@ FAMILIES: list[Family] = [
     Family("minicpm3-4b", "openbmb", "openbmb/MiniCPM3-4B", "MiniCPM3ForCausalLM", 4.1),
     Family("internvl2-5-8b", "opengvlab", "OpenGVLab/InternVL2_5-8B", "InternVLChatModel", 8.1,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("janus-pro-7b", "deepseek-ai", "deepseek-ai/Janus-Pro-7B", "JanusMultiModalityCausalLM", 7.4,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("qwen3-vl-8b-instruct", "qwen", "Qwen/Qwen3-VL-8B-Instruct", "Qwen3VLForConditionalGeneration", 8.8,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("qwen3-vl-235b-a22b-instruct", "qwen", "Qwen/Qwen3-VL-235B-A22B-Instruct",

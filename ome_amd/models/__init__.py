@@ -76,6 +76,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.mllama import MllamaForConditionalGeneration
 
         return MllamaForConditionalGeneration
+    if cfg.architecture in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM"):
+        from ome_amd.models.janus import JanusForConditionalGeneration
+
+        return JanusForConditionalGeneration
     if cfg.architecture in ("InternVLChatModel", "InternVLForConditionalGeneration"):
         from ome_amd.models.internvl import internvl_class
 
@@ -136,6 +140,7 @@ def supported(arch: str) -> bool:
         arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or \
         arch == "Mistral3ForConditionalGeneration" or arch == "MiniCPM3ForCausalLM" or \
         arch in ("InternVLChatModel", "InternVLForConditionalGeneration") or \
+        arch in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM") or \
         arch == "GptOssForCausalLM"
 
 

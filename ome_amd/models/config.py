@@ -199,8 +199,9 @@ class ModelConfig:
 
     @classmethod
     def from_hf(cls, cfg: dict[str, Any]) -> "ModelConfig":
-        if cfg.get("text_config") or cfg.get("llm_config"):   # llm_config: InternVLChatModel
-            text = _standard_keys(cfg.get("text_config") or cfg["llm_config"])
+        if cfg.get("text_config") or cfg.get("llm_config") or cfg.get("language_config"):
+            # llm_config: InternVLChatModel; language_config: Janus / DeepSeek-VL2 originals
+            text = _standard_keys(cfg.get("text_config") or cfg.get("llm_config") or cfg["language_config"])
         else:  # flat configs: keep the original keys (extra) next to the standard aliases
             cfg = text = _standard_keys(cfg)
         arch = (cfg.get("architectures") or ["LlamaForCausalLM"])[0]
