@@ -83,6 +83,10 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("janus-pro-7b", "deepseek-ai", "deepseek-ai/Janus-Pro-7B", "JanusMultiModalityCausalLM", 7.4,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("llava-onevision-qwen2-7b-ov", "lmms-lab", "lmms-lab/llava-onevision-qwen2-7b-ov", "LlavaQwenForCausalLM",
+           8.0, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("llava-next-72b", "lmms-lab", "lmms-lab/llava-next-72b", "LlavaQwenForCausalLM", 72.7,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("qwen3-vl-8b-instruct", "qwen", "Qwen/Qwen3-VL-8B-Instruct", "Qwen3VLForConditionalGeneration", 8.8,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("qwen3-vl-235b-a22b-instruct", "qwen", "Qwen/Qwen3-VL-235B-A22B-Instruct",

@@ -76,6 +76,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.mllama import MllamaForConditionalGeneration
 
         return MllamaForConditionalGeneration
+    if cfg.architecture in ("LlavaQwenForCausalLM", "LlavaOnevisionForConditionalGeneration"):
+        from ome_amd.models.llava_onevision import LlavaOnevisionForConditionalGeneration
+
+        return LlavaOnevisionForConditionalGeneration
     if cfg.architecture in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM"):
         from ome_amd.models.janus import JanusForConditionalGeneration
 
@@ -141,6 +145,7 @@ def supported(arch: str) -> bool:
         arch == "Mistral3ForConditionalGeneration" or arch == "MiniCPM3ForCausalLM" or \
         arch in ("InternVLChatModel", "InternVLForConditionalGeneration") or \
         arch in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM") or \
+        arch in ("LlavaQwenForCausalLM", "LlavaOnevisionForConditionalGeneration") or \
         arch == "GptOssForCausalLM"
 
 

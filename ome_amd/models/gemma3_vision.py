@@ -113,15 +113,16 @@ class SiglipVisionTower:
                 return
             self.w[f"layers.{b}.{self._REN[mod]}.{kind}"] = self._t(t)
 
-    def forward(self, pixels: torch.Tensor) -> torch.Tensor:
-        """pixels [n, C, S, S] -> last hidden state [n, n_patch, E] (post-LayerNorm)."""
+    def forward(self, pixels: torch.Tensor, n_layers: int | None = None, post_norm: bool = True) -> torch.Tensor:
+        """pixels [n, C, S, S] -> last hidden state [n, n_patch, E] (post-LayerNorm); ``n_layers`` /
+        ``post_norm=False``: the hidden state after that many layers (LLaVA-OneVision features)."""
         w, E, n, ps, s = self.w, self.E, pixels.shape[0], self.patch, self.side
         x = pixels.to(device=self.device, dtype=self.dtype)
         x = x.reshape(n, self.C, s, ps, s, ps).permute(0, 2, 4, 1, 3, 5).reshape(n * self.n_patch, -1)
         x = (linear(x, w["patch.weight"], w["patch.bias"]).view(n, self.n_patch, E) + w["pos"]).reshape(-1, E)
         T = x.shape[0]
         lens = [self.n_patch] * n
-        for b in range(self.depth):
+        for b in range(self.depth if n_layers is None else n_layers):
             p = f"layers.{b}."
             h = ops.layernorm(x.contiguous(), w[p + "ln1.weight"], w[p + "ln1.bias"], self.eps)
             qkv = linear(h, w[p + "qkv.weight"], w[p + "qkv.bias"]).view(T, 3, self.heads, self.D)
@@ -131,6 +132,8 @@ class SiglipVisionTower:
             f = linear(h, w[p + "fc1.weight"], w[p + "fc1.bias"])
             f = ops.act(f, self.act) if self.act is not None else f * torch.sigmoid(1.702 * f)
             x = x + linear(f, w[p + "fc2.weight"], w[p + "fc2.bias"])
+        if not post_norm:
+            return x.view(n, self.n_patch, E)
         return ops.layernorm(x, w["post_ln.weight"], w["post_ln.bias"], self.eps).view(n, self.n_patch, E)
 
 
