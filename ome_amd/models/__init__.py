@@ -76,6 +76,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.mllama import MllamaForConditionalGeneration
 
         return MllamaForConditionalGeneration
+    if cfg.architecture == "XverseMoeForCausalLM" or cfg.model_type == "xverse_moe":
+        from ome_amd.models.xverse import XverseMoeForCausalLM
+
+        return XverseMoeForCausalLM
     if cfg.architecture == "BailingMoeForCausalLM" or cfg.model_type == "bailing_moe":
         from ome_amd.models.bailing import BailingMoeForCausalLM
 
@@ -150,7 +154,7 @@ def supported(arch: str) -> bool:
         arch in ("InternVLChatModel", "InternVLForConditionalGeneration") or \
         arch in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM") or \
         arch in ("LlavaQwenForCausalLM", "LlavaOnevisionForConditionalGeneration") or \
-        arch == "BailingMoeForCausalLM" or \
+        arch in ("BailingMoeForCausalLM", "XverseMoeForCausalLM") or \
         arch == "GptOssForCausalLM"
 
 

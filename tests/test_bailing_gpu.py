@@ -1,4 +1,5 @@
-"""Bailing MoE (Ling) on gfx950: the mapped checkpoint of ``test_bailing_cpu`` in bf16 (grouped
+"""Bailing MoE (Ling) and XVERSE MoE on gfx950: the mapped checkpoints of ``test_bailing_cpu`` /
+``test_xverse_cpu`` in bf16 (grouped
 MFMA MoE GEMMs, fused shared expert, normalised head) with HIP-graph decode, every greedy token a
 near-argmax of the fp32 transformers reference on the same prefix."""
 import pytest
@@ -7,12 +8,14 @@ import torch
 from ome_amd.runtime.engine import Engine, EngineArgs
 from ome_amd.runtime.request import SamplingParams
 from tests.test_bailing_cpu import _models
+from tests.test_xverse_cpu import _models as _xverse_models
 
 pytestmark = pytest.mark.gpu
 
 
-def test_bailing_on_gpu(tmp_path):
-    hf = _models(tmp_path)
+@pytest.mark.parametrize("family", ["bailing", "xverse"])
+def test_bailing_on_gpu(tmp_path, family):
+    hf = (_models if family == "bailing" else _xverse_models)(tmp_path)
     prompts = [[(7 * i + 3 + 5 * s) % 500 + 3 for i in range(12 + 20 * s)] for s in range(3)]
     eng = Engine(EngineArgs(model_path=str(tmp_path), device="cuda", max_running_requests=4, context_length=256))
     for p, r in zip(prompts, eng.generate(prompts, SamplingParams(max_new_tokens=8, ignore_eos=True))):
