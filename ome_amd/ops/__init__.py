@@ -446,6 +446,63 @@ def mla_attn(q, cache, block_tables, tok_row, kv_lens, scale: float, ws: MLAWork
     return out
 
 
+class _SkinnyWorkspace:
+    """Split-K partial tiles + per-tile counters of :func:`skinny_gemm` (one per device; launches on
+    one stream are ordered, so calls share it).  The counters are re-armed by the kernel."""
+
+    def __init__(self, device):
+        self.ws = torch.empty(0, dtype=torch.float32, device=device)
+        self.cnt = torch.zeros(1 << 14, dtype=torch.int32, device=device)
+
+    def get(self, floats: int) -> torch.Tensor:
+        if self.ws.numel() < floats:
+            self.ws = torch.empty(floats, dtype=torch.float32, device=self.cnt.device)
+        return self.ws
+
+
+_skinny_ws: dict = {}
+
+
+def skinny_splits(M: int, N: int, K: int) -> int:
+    """Split-K factor: 1 when the weight has >= 256 64-row tiles, else enough to reach ~2 workgroups
+    per CU (capped; every split streams >= 512 K)."""
+    env = os.environ.get("OME_SKINNY_SPLITS")
+    tiles = N // 64
+    if env:
+        return max(1, min(int(env), K // 64))
+    if tiles >= 256:
+        return 1
+    return max(1, min(-(-512 // tiles), 8, K // 512))
+
+
+def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
+                out: torch.Tensor | None = None, splits: int | None = None) -> torch.Tensor:
+    """out[M, N] = x[M, K] . w[N, K]^T (+ bias) for decode-shaped M <= 256 (``skinny_gemm.hip``:
+    every weight byte streamed once, split-K when N has few 64-row tiles)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not _gpu(x):
+        r = torch.nn.functional.linear(x.float(), w.float(), None if bias is None else bias.float()).to(x.dtype)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    assert x.stride(1) == 1 and w.is_contiguous() and x.dtype == w.dtype == torch.bfloat16
+    out = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
+    s = splits or skinny_splits(M, N, K)
+    ws = cnt = None
+    if s > 1:
+        st = _skinny_ws.get(x.device)
+        if st is None:
+            st = _skinny_ws[x.device] = _SkinnyWorkspace(x.device)
+        mp = 64 if M <= 64 else 128 if M <= 128 else 256
+        ws, cnt = st.get((N // 64) * s * mp * 64), st.cnt
+        assert N // 64 <= cnt.numel()
+    call("ome_skinny_gemm", x.data_ptr(), x.stride(0), w.data_ptr(), ptr(bias), out.data_ptr(), out.stride(0), M, N,
+         K, s, ptr(ws), ptr(cnt), stream_ptr())
+    return out
+
+
 def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) -> list[tuple[int, int]]:
     """(seq, row_start) work items, heaviest (longest key range) first."""
     items = []
