@@ -52,6 +52,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.qwen3_next import Qwen3NextForCausalLM
 
         return Qwen3NextForCausalLM
+    if cfg.architecture == "Glm4vMoeForConditionalGeneration" or cfg.model_type == "glm4v_moe":
+        from ome_amd.models.glm4v import Glm4vMoeForConditionalGeneration
+
+        return Glm4vMoeForConditionalGeneration
     if cfg.architecture in ("Qwen3VLForConditionalGeneration", "Qwen3VLMoeForConditionalGeneration"):
         from ome_amd.models.qwen3_vl import Qwen3VLForConditionalGeneration, Qwen3VLMoeForConditionalGeneration
 
@@ -154,7 +158,7 @@ def supported(arch: str) -> bool:
         arch in ("InternVLChatModel", "InternVLForConditionalGeneration") or \
         arch in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM") or \
         arch in ("LlavaQwenForCausalLM", "LlavaOnevisionForConditionalGeneration") or \
-        arch in ("BailingMoeForCausalLM", "XverseMoeForCausalLM") or \
+        arch in ("BailingMoeForCausalLM", "XverseMoeForCausalLM", "Glm4vMoeForConditionalGeneration") or \
         arch == "GptOssForCausalLM"
 
 
