@@ -90,6 +90,8 @@ FAMILIES: list[Family] = [
     Family("ling-lite", "inclusionai", "inclusionAI/Ling-lite", "BailingMoeForCausalLM", 16.8),
     Family("ling-plus", "inclusionai", "inclusionAI/Ling-plus", "BailingMoeForCausalLM", 290.0),
     Family("xverse-moe-a36b", "xverse", "xverse/XVERSE-MoE-A36B", "XverseMoeForCausalLM", 255.0),
+    Family("kimi-vl-a3b-instruct", "moonshotai", "moonshotai/Kimi-VL-A3B-Instruct", "KimiVLForConditionalGeneration",
+           16.4, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("glm-4-5v", "zai-org", "zai-org/GLM-4.5V", "Glm4vMoeForConditionalGeneration", 108.0,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("qwen3-vl-8b-instruct", "qwen", "Qwen/Qwen3-VL-8B-Instruct", "Qwen3VLForConditionalGeneration", 8.8,

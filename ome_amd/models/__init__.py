@@ -136,6 +136,11 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.minicpm3 import MiniCPM3ForCausalLM
 
         return MiniCPM3ForCausalLM
+    if cfg.architecture in ("KimiVLForConditionalGeneration", "Kimi_K25ForConditionalGeneration") or \
+            cfg.model_type in ("kimi_vl", "kimi_k25"):
+        from ome_amd.models.kimi_vl import KimiVLForConditionalGeneration
+
+        return KimiVLForConditionalGeneration
     if cfg.is_mla:
         from ome_amd.models.deepseek import DeepseekForCausalLM
 
@@ -159,7 +164,7 @@ def supported(arch: str) -> bool:
         arch in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM") or \
         arch in ("LlavaQwenForCausalLM", "LlavaOnevisionForConditionalGeneration") or \
         arch in ("BailingMoeForCausalLM", "XverseMoeForCausalLM", "Glm4vMoeForConditionalGeneration") or \
-        arch == "GptOssForCausalLM"
+        arch == "GptOssForCausalLM" or arch in ("KimiVLForConditionalGeneration", "Kimi_K25ForConditionalGeneration")
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,

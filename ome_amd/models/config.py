@@ -266,7 +266,8 @@ class ModelConfig:
             c.first_k_dense_replace = text.get("first_k_dense_replace", 0)
             c.moe_layer_freq = text.get("moe_layer_freq", 1) or 1
             c.routed_scaling_factor = text.get("routed_scaling_factor", 1.0) or 1.0
-            c.scoring_func = text.get("scoring_func", "softmax")
+            # transformers' DeepSeek-V3 configs omit the key: that model always scores with sigmoid
+            c.scoring_func = text.get("scoring_func", "sigmoid" if mt in ("deepseek_v3", "kimi_k2") else "softmax")
             c.n_group = text.get("n_group", 1) or 1
             c.topk_group = text.get("topk_group", 1) or 1
         if text.get("kv_lora_rank"):

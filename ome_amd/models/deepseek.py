@@ -209,7 +209,15 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 continue
             i, rest = int(p[1]), ".".join(p[2:])
             d = parts.setdefault(i, {})
-            if rest.startswith("mlp.experts."):
+            if rest in ("mlp.experts.gate_up_proj", "mlp.experts.down_proj"):
+                # transformers >= 5 fused expert tensors: [E, 2I, H] (gate | up) / [E, H, I]
+                for e in range(w.shape[0]):
+                    de = experts.setdefault(i, {}).setdefault(e, {})
+                    if p[4] == "down_proj":
+                        de["down_proj"] = w[e]
+                    else:
+                        de["gate_proj"], de["up_proj"] = w[e].chunk(2, 0)
+            elif rest.startswith("mlp.experts."):
                 e = int(p[4])
                 experts.setdefault(i, {}).setdefault(e, {})[p[5]] = w
             elif rest in ("self_attn.q_proj.weight", "self_attn.q_b_proj.weight"):
