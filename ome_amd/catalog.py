@@ -90,6 +90,8 @@ FAMILIES: list[Family] = [
     Family("ling-lite", "inclusionai", "inclusionAI/Ling-lite", "BailingMoeForCausalLM", 16.8),
     Family("ling-plus", "inclusionai", "inclusionAI/Ling-plus", "BailingMoeForCausalLM", 290.0),
     Family("xverse-moe-a36b", "xverse", "xverse/XVERSE-MoE-A36B", "XverseMoeForCausalLM", 255.0),
+    Family("phi-4-multimodal-instruct", "microsoft", "microsoft/Phi-4-multimodal-instruct", "Phi4MMForCausalLM", 5.6,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("kimi-vl-a3b-instruct", "moonshotai", "moonshotai/Kimi-VL-A3B-Instruct", "KimiVLForConditionalGeneration",
            16.4, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("glm-4-5v", "zai-org", "zai-org/GLM-4.5V", "Glm4vMoeForConditionalGeneration", 108.0,

@@ -136,6 +136,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.minicpm3 import MiniCPM3ForCausalLM
 
         return MiniCPM3ForCausalLM
+    if cfg.architecture in ("Phi4MMForCausalLM", "Phi4MultimodalForCausalLM") or cfg.model_type == "phi4_multimodal":
+        from ome_amd.models.phi4mm import Phi4MMForCausalLM
+
+        return Phi4MMForCausalLM
     if cfg.architecture in ("KimiVLForConditionalGeneration", "Kimi_K25ForConditionalGeneration") or \
             cfg.model_type in ("kimi_vl", "kimi_k25"):
         from ome_amd.models.kimi_vl import KimiVLForConditionalGeneration
@@ -164,7 +168,8 @@ def supported(arch: str) -> bool:
         arch in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM") or \
         arch in ("LlavaQwenForCausalLM", "LlavaOnevisionForConditionalGeneration") or \
         arch in ("BailingMoeForCausalLM", "XverseMoeForCausalLM", "Glm4vMoeForConditionalGeneration") or \
-        arch == "GptOssForCausalLM" or arch in ("KimiVLForConditionalGeneration", "Kimi_K25ForConditionalGeneration")
+        arch == "GptOssForCausalLM" or arch in ("KimiVLForConditionalGeneration", "Kimi_K25ForConditionalGeneration") or \
+        arch in ("Phi4MMForCausalLM", "Phi4MultimodalForCausalLM")
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,
