@@ -65,9 +65,14 @@ def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
 
 
 def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None) -> torch.Tensor:
-    """Dispatch: plain tensor -> hipBLASLt GEMM; Fp8Weight -> W8A8 MFMA path."""
+    """Dispatch: plain tensor -> hipBLASLt GEMM, or the weight-streaming MFMA GEMM for decode
+    shapes where it was measured faster (``ops.decode_gemm_plan``); Fp8Weight -> W8A8 MFMA path."""
     if isinstance(w, Fp8Weight):
         return ops.fp8_linear(x, w.q, w.scale, w.block, bias)
+    if x.dim() == 2 and x.shape[0] <= 256 and x.is_cuda:
+        plan = ops.decode_gemm_plan(x, w, bias)
+        if plan is not None:
+            return ops.stream_gemm(x, w, bias, nf=plan[0], splits=plan[1])
     return F.linear(x, w, bias)
 
 

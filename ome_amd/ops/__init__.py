@@ -503,6 +503,126 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = No
     return out
 
 
+_stream_ws: dict = {}
+
+
+def stream_gemm_plan(M: int, N: int, K: int) -> tuple[int, int]:
+    """(nf, splits) of :func:`stream_gemm`: 256-row weight tiles (nf = 2) only at M <= 128 (VGPR
+    budget), and split-K up to ~256 workgroups when the weight has few tiles (every split keeps
+    >= 4 K steps).  ``OME_STREAM_SPLITS`` overrides the split count."""
+    nf = 2 if M <= 128 and N % 256 == 0 and N // 256 >= 256 else 1
+    tiles = N // (128 * nf)
+    env = os.environ.get("OME_STREAM_SPLITS")
+    if env:
+        return nf, max(1, min(int(env), K // 64))
+    if tiles >= 192:
+        return nf, 1
+    return nf, max(1, min(-(-256 // tiles), K // 256))
+
+
+def stream_gemm_ok(M: int, N: int, K: int) -> bool:
+    return 1 <= M <= 256 and N % 128 == 0 and K % 64 == 0
+
+
+def stream_gemm_reserve(device, floats: int) -> None:
+    """Pre-size the split-K workspace (call before HIP-graph capture so capture never allocates)."""
+    ws = _stream_ws.get(device)
+    if ws is None or ws.numel() < floats:
+        _stream_ws[device] = torch.empty(floats, dtype=torch.float32, device=device)
+
+
+def stream_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
+                out: torch.Tensor | None = None, splits: int | None = None, nf: int | None = None) -> torch.Tensor:
+    """out[M, N] = x[M, K] . w[N, K]^T (+ bias) for decode-shaped M <= 256 (``stream_gemm.hip``: the
+    weight streams from HBM straight into MFMA operands, activations shared through LDS, split-K
+    partials reduced by a second kernel)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not _gpu(x):
+        r = torch.nn.functional.linear(x.float(), w.float(), None if bias is None else bias.float()).to(x.dtype)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    assert x.stride(1) == 1 and w.is_contiguous() and x.dtype == w.dtype == torch.bfloat16
+    assert stream_gemm_ok(M, N, K), (M, N, K)
+    out = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
+    pnf, ps = stream_gemm_plan(M, N, K)
+    nf, s = nf or pnf, splits or ps
+    ws = None
+    if s > 1:
+        stream_gemm_reserve(x.device, s * M * N)
+        ws = _stream_ws[x.device]
+    call("ome_stream_gemm", x.data_ptr(), x.stride(0), w.data_ptr(), ptr(bias), out.data_ptr(), out.stride(0), M, N,
+         K, nf, s, ptr(ws), stream_ptr())
+    return out
+
+
+# ---- decode GEMM routing: ome_stream_gemm where it measured faster than hipBLASLt --------------
+# Filled during the engine's eager pre-capture pass (``decode_gemm_tuning``): every (M, N, K, bias)
+# a decode bucket issues is timed once against the library GEMM and the winner recorded; graphs
+# captured afterwards bake the choice in.  hipBLASLt keeps every shape it wins (at M = 256 all of
+# them on an 8B model: profiles/r02_stream_gemm_bench.txt).
+_gemm_route: dict = {}
+_gemm_tuning = [False]
+
+
+class decode_gemm_tuning:
+    """Context manager: record stream-vs-library choices for the GEMMs issued inside."""
+
+    def __enter__(self):
+        self.prev = _gemm_tuning[0]
+        _gemm_tuning[0] = os.environ.get("OME_STREAM_GEMM", "0") == "1"
+        return self
+
+    def __exit__(self, *exc):
+        _gemm_tuning[0] = self.prev
+        return False
+
+
+def _time_us(fn, iters: int = 20) -> float:
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1000.0 / iters
+
+
+def decode_gemm_plan(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None):
+    """(nf, splits) when ``stream_gemm`` is the recorded winner for this shape, else None."""
+    M, K = x.shape
+    N = w.shape[0]
+    key = (M, N, K, bias is not None, x.device)
+    if key in _gemm_route:
+        return _gemm_route[key]
+    if not _gemm_tuning[0]:
+        return None
+    plan = None
+    if (stream_gemm_ok(M, N, K) and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and w.is_contiguous() and _gpu(x)):
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        t_lib = _time_us(lambda: torch.nn.functional.linear(x, w, bias))
+        nf0, s0 = stream_gemm_plan(M, N, K)
+        cands = {(nf0, s0), (1, 1)}
+        cands |= {(1, s) for s in (2, 4, 8) if s <= K // 256}
+        if M <= 128 and N % 256 == 0:
+            cands |= {(2, 1), (2, 2)}
+        cands = {(nf, sp) for nf, sp in cands if sp <= K // 64 and N % (128 * nf) == 0 and (nf == 1 or M <= 128)}
+        best = None
+        for nf, sp in sorted(cands):
+            t = _time_us(lambda: stream_gemm(x, w, bias, out=out, splits=sp, nf=nf))
+            if best is None or t < best[0]:
+                best = (t, nf, sp)
+        if best is not None and best[0] < 0.95 * t_lib:
+            plan = (best[1], best[2])
+    _gemm_route[key] = plan
+    return plan
+
+
 def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) -> list[tuple[int, int]]:
     """(seq, row_start) work items, heaviest (longest key range) first."""
     items = []

@@ -259,9 +259,9 @@ class ModelRunner:
         torch.cuda.synchronize(self.device)
         stream = torch.cuda.Stream(self.device)
         stream.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(stream):
+        with torch.cuda.stream(stream), ops.decode_gemm_tuning():
             for bs in reversed(self.buckets):
-                self._decode_forward(bs)  # warm-up (allocations, hipBLASLt heuristics / tuning)
+                self._decode_forward(bs)  # warm-up (allocations, hipBLASLt heuristics / tuning, GEMM routing)
         torch.cuda.current_stream(self.device).wait_stream(stream)
         torch.cuda.synchronize(self.device)
         if tuning:
