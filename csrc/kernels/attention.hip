@@ -246,6 +246,14 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
   }
 }
 
+// Split-K partition span of a sequence: a fixed ``part_size`` (multiple of 128), or with
+// part_size == 0 the sequence's own length spread over ``max_parts`` partitions (128-key granules),
+// so short contexts still fill every partition instead of leaving all but the first idle.
+__device__ __forceinline__ int decode_part_span(int part_size, int seq_len, int max_parts) {
+  if (part_size > 0) return part_size;
+  return max(128, (((seq_len + max_parts - 1) / max_parts) + 127) & ~127);
+}
+
 template <int D>
 __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const int* __restrict__ seq_lens,
                                                                  const float* __restrict__ part_o,
@@ -255,7 +263,8 @@ __global__ __launch_bounds__(D) void paged_decode_reduce_kernel(const int* __res
                                                                  const float* __restrict__ sinks = nullptr) {
   const int b = blockIdx.y, head = blockIdx.x, d = threadIdx.x;
   const int seq_len = seq_lens[b];
-  const int nparts = (seq_len + part_size - 1) / part_size;
+  const int psz = decode_part_span(part_size, seq_len, max_parts);
+  const int nparts = (seq_len + psz - 1) / psz;
   if (nparts <= 1) return;
   const int64_t base = ((int64_t)b * Hq + head) * max_parts;
   float M = OME_NEG_INF;
@@ -440,9 +449,10 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
   // hands out workgroups in grid order, so the long tail starts first instead of last)
   const int part = blockIdx.x, kvh = blockIdx.y, b = order ? order[blockIdx.z] : blockIdx.z;
   const int seq_len = seq_lens[b];
-  const int p_start = part * part_size;
+  const int psz = decode_part_span(part_size, seq_len, max_parts);
+  const int p_start = part * psz;
   if (p_start >= seq_len) return;
-  const int p_end = min(seq_len, p_start + part_size);
+  const int p_end = min(seq_len, p_start + psz);
   const int G = Hq / Hkv;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n = lane & 15, g = lane >> 4;
@@ -513,7 +523,7 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
       for (int i = 0; i < 4; ++i) sm_o[(wave * G + n) * D + 16 * nb + 4 * g + i] = o[nb][i];
   }
   __syncthreads();
-  const int nparts = (seq_len + part_size - 1) / part_size;
+  const int nparts = (seq_len + psz - 1) / psz;
   for (int idx = threadIdx.x; idx < G * D; idx += 256) {
     const int h = idx / D, d = idx % D;
     float M = OME_NEG_INF;
@@ -598,7 +608,7 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   if (B <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
-  if (part_size % 128 != 0 || max_parts <= 0) return -4;
+  if (part_size < 0 || part_size % 128 != 0 || max_parts <= 0) return -4;   // 0: per-sequence span
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
   Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
   scl.row_lo = row_lo;
@@ -607,7 +617,8 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   // key-permuted tiles (16-B V loads; default: 5.38 vs 5.24 TB/s on the bench's context mix)
   const char* ve = getenv("OME_DECODE_ATTN");
   int variant = ve ? atoi(ve) : 4;
-  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks || alibi || row_lo)) variant = 4;  // v1: plain bf16 D=128
+  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks || alibi || row_lo || part_size == 0))
+    variant = 4;  // v1: plain bf16 D=128, fixed partitions
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
     paged_decode_kernel<128, 16><<<grid, 256, smem, stream>>>(

@@ -356,9 +356,17 @@ def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13
 class DecodeWorkspace:
     """Split-K partial buffers for paged decode, sized once (graph-capture safe)."""
 
-    def __init__(self, max_batch: int, Hq: int, D: int, max_context: int, part_size: int = 512, device="cuda"):
+    def __init__(self, max_batch: int, Hq: int, D: int, max_context: int, part_size: int = 512, device="cuda",
+                 parts: int | None = None):
+        """``part_size`` > 0: fixed 128-multiple key spans; ``part_size`` == 0: every sequence is split
+        into ``parts`` spans of its own length (128-key granules), so short contexts use every
+        partition."""
         self.part_size = part_size
-        self.max_parts = max(1, -(-max_context // part_size))
+        if part_size == 0:
+            assert parts and parts >= 1
+            self.max_parts = parts
+        else:
+            self.max_parts = max(1, -(-max_context // part_size))
         self.part_o = torch.empty(max_batch * Hq * self.max_parts * D, dtype=torch.float32, device=device)
         self.part_ml = torch.empty(max_batch * Hq * self.max_parts * 2, dtype=torch.float32, device=device)
 

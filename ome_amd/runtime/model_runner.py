@@ -182,10 +182,13 @@ class ModelRunner:
             hkv = self.model.tp.hkv
             parts = max(1, math.ceil(1024 / max(1, bs * hkv)))
             span = self.max_context + self.P  # seq_lens never exceed this: one part covers it all
-            part = max(256, -(-span // parts))
-            part = -(-part // 128) * 128
-            ws = ops.DecodeWorkspace(bs, self.model.tp.hq, self.cfg.head_dim, self.max_context + self.P, part,
-                                     self.device)
+            if parts > 1 and os.environ.get("OME_DECODE_DYN_PARTS", "1") == "1":
+                # split each sequence by its own length (short contexts fill every partition)
+                ws = ops.DecodeWorkspace(bs, self.model.tp.hq, self.cfg.head_dim, span, 0, self.device, parts=parts)
+            else:
+                part = max(256, -(-span // parts))
+                part = -(-part // 128) * 128
+                ws = ops.DecodeWorkspace(bs, self.model.tp.hq, self.cfg.head_dim, span, part, self.device)
             self._ws_cache[bs] = ws
         return ws
 

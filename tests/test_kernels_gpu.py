@@ -374,3 +374,22 @@ def test_paged_attention_alibi(D, Hq, Hkv, parts):
     qp = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
     outp = ops.paged_prefill(qp, kc, vc, bt2, cu, kl, items, D ** -0.5, alibi=al)
     _close(outp, ref.paged_prefill(qp, kc, vc, bt2, cu, kl, D ** -0.5, -1, 1.0, 1.0, 0.0, None, al), atol=2e-2)
+
+
+@pytest.mark.parametrize("parts", [2, 5, 8])
+@pytest.mark.parametrize("window", [-1, 128])
+def test_paged_decode_dynamic_partitions(parts, window):
+    """part_size 0: every sequence split into ``parts`` spans of its own length (the decode graphs'
+    small-batch workspace), incl. sinks / sliding window and lengths below one 128-key granule."""
+    Hq, Hkv, D, P = 32, 8, 128, 16
+    seq_lens = [1, 17, 127, 128, 129, 630, 1000, 2049]
+    npages = sum(-(-L // P) for L in seq_lens) + 4
+    kc, vc = _cache(npages, Hkv, D)
+    bt = _block_tables(seq_lens, P, npages)
+    sl = torch.tensor(seq_lens, dtype=torch.int32, device=DEV)
+    q = torch.randn(len(seq_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    ws = ops.DecodeWorkspace(len(seq_lens), Hq, D, 4096, 0, DEV, parts=parts)
+    sinks = torch.randn(Hq, device=DEV, dtype=torch.float32)
+    for sk in (None, sinks):
+        out = ops.paged_decode(q, kc, vc, bt, sl, D ** -0.5, ws, window=window, sinks=sk)
+        _close(out, ref.paged_decode(q, kc, vc, bt, sl, D ** -0.5, window, 1.0, 1.0, 0.0, sk), atol=2e-2)
