@@ -39,8 +39,9 @@ def test_stream_gemm_default_plan_llama_shapes():
             assert (got - ref).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item()), (M, N, K)
 
 
-def test_decode_gemm_routing_records_winner_and_matches():
+def test_decode_gemm_routing_records_winner_and_matches(monkeypatch):
     from ome_amd.models.quant import linear
+    monkeypatch.setenv("OME_STREAM_GEMM", "1")        # routing is opt-in
     torch.manual_seed(0)
     x = torch.randn(16, 4096, device="cuda").to(torch.bfloat16)
     w = (torch.randn(4096, 4096, device="cuda") * 0.02).to(torch.bfloat16)
@@ -55,9 +56,10 @@ def test_decode_gemm_routing_records_winner_and_matches():
 
 
 @pytest.mark.parametrize("M,N,K", [(8, 256, 64), (100, 384, 128), (200, 256, 192)])
-def test_decode_gemm_routing_tiny_k(M, N, K):
+def test_decode_gemm_routing_tiny_k(M, N, K, monkeypatch):
     """Shapes of tiny test models (K below one split step): every timed candidate must be valid."""
     from ome_amd.models.quant import linear
+    monkeypatch.setenv("OME_STREAM_GEMM", "1")
     x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     w = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16)
     with ops.decode_gemm_tuning():
