@@ -302,7 +302,7 @@ class LlamaForCausalLM:
         return x
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(hidden, self.lm_head)
+        logits = linear(hidden, self.lm_head)
         if self.tp.tp > 1:
             logits = pstate.tp_all_gather(logits, dim=-1)
         return logits[:, : self.cfg.vocab_size]

@@ -18,6 +18,7 @@ block structure and ``amax/448`` scales that round-trip is exact.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -64,12 +65,19 @@ def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
     return Fp8Weight(q, s.contiguous(), 0)
 
 
+# rows up to which plain bf16 projections run on the GEMV stream kernel (0 disables)
+_GEMV_ROWS = int(os.environ.get("OME_GEMV_ROWS", "4"))
+
+
 def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None) -> torch.Tensor:
-    """Dispatch: plain tensor -> hipBLASLt GEMM, or the weight-streaming MFMA GEMM for decode
-    shapes where it was measured faster (``ops.decode_gemm_plan``); Fp8Weight -> W8A8 MFMA path."""
+    """Dispatch: plain tensor -> hipBLASLt GEMM; single-row decode -> the GEMV stream kernel
+    (``ops.gemv``, ``OME_GEMV_ROWS``); the weight-streaming MFMA GEMM for decode shapes where it
+    was measured faster (``ops.decode_gemm_plan``, opt-in); Fp8Weight -> W8A8 MFMA path."""
     if isinstance(w, Fp8Weight):
         return ops.fp8_linear(x, w.q, w.scale, w.block, bias)
     if x.dim() == 2 and x.shape[0] <= 256 and x.is_cuda:
+        if x.shape[0] <= _GEMV_ROWS and ops.gemv_ok(x, w):
+            return ops.gemv(x, w, bias)
         plan = ops.decode_gemm_plan(x, w, bias)
         if plan is not None:
             return ops.stream_gemm(x, w, bias, nf=plan[0], splits=plan[1])

@@ -566,6 +566,31 @@ def stream_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = No
     return out
 
 
+def gemv_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.dim() == 2 and 1 <= x.shape[0] <= 4 and x.shape[1] % 8 == 0 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and w.is_contiguous())
+
+
+def gemv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
+         out: torch.Tensor | None = None) -> torch.Tensor:
+    """out[M, N] = x[M, K] . w[N, K]^T (+ bias) for M <= 4 (``gemv.hip``: a pure weight stream,
+    R rows per wave, several K steps of 16-B loads in flight, no LDS)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not _gpu(x):
+        r = torch.nn.functional.linear(x.float(), w.float(), None if bias is None else bias.float()).to(x.dtype)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    assert gemv_ok(x, w), (tuple(x.shape), x.stride(), w.shape)
+    out = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
+    call("ome_gemv", x.data_ptr(), x.stride(0), w.data_ptr(), ptr(bias), out.data_ptr(), out.stride(0), M, N, K,
+         stream_ptr())
+    return out
+
+
 # ---- decode GEMM routing: ome_stream_gemm where it measured faster than hipBLASLt --------------
 # Filled during the engine's eager pre-capture pass (``decode_gemm_tuning``): every (M, N, K, bias)
 # a decode bucket issues is timed once against the library GEMM and the winner recorded; graphs

@@ -42,6 +42,11 @@ def main():
             wb = N * K * 2
             ws = [w] + [w.clone() for _ in range(max(1, -(-640 * 2**20 // wb)) - 1)]
             line = [f"M={M:4d} {name:8s} hipblaslt={timeit(lambda w_: F.linear(x, w_), ws):7.1f}us"]
+            if M <= 4:
+                og = ops.gemv(x, w)
+                err = (og.float() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+                t = timeit(lambda w_: ops.gemv(x, w_, out=og), ws)
+                line.append(f"gemv={t:6.1f}us({wb / t / 1e6:4.2f}TB/s,err {err:.0e})")
             nf0, s0 = ops.stream_gemm_plan(M, N, K)
             cands = sorted({(nf0, s0), (1, 1), (1, 2), (1, 4), (1, 8), (1, max(1, s0 // 2)), (1, s0 * 2)})
             if M <= 128 and N % 256 == 0:
