@@ -1,11 +1,11 @@
-// Batch-1..4 decode GEMV for gfx950: out[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 4
+// Batch-1..8 decode GEMV for gfx950: out[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 8
 // (decode-skinny shapes at the low end of the BenchmarkJob concurrency sweep).
 //
 // At one to four rows a projection has no operand reuse worth an MFMA tile: it is a pure
 // HBM stream of the weight.  Each wave owns R consecutive weight rows and walks K with 16-byte
 // loads (lane l covers k = 8 l + 512 i), the R row loads of several K steps in flight at once
 // (unrolled; no LDS, no barriers, ~30 VGPRs so many waves per SIMD hide the HBM latency).  The
-// activation rows (<= 4 x K bf16, read by every wave) are served by L1 / L2.  Each wave reduces
+// activation rows (<= 8 x K bf16, read by every wave) are served by L1 / L2.  Each wave reduces
 // its M x R fp32 partial dot products across the 64 lanes with xor shuffles and stores them.
 #include "common.h"
 
@@ -81,20 +81,24 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16* __restrict__ X, i
 }  // namespace
 
 // X [M, K] (row stride ldx, 16-byte aligned rows), W [N, K] contiguous, out [M, N] (row stride ldo);
-// 1 <= M <= 4, K % 8 == 0.
+// 1 <= M <= 8, K % 8 == 0.
 OME_API int ome_gemv(const void* X, int64_t ldx, const void* W, const void* bias, void* out, int64_t ldo, int M, int N,
                      int K, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
-  if (M > 4 || K % 8 || ldx % 8 || K <= 0) return -2;
+  if (M > 8 || K % 8 || ldx % 8 || K <= 0) return -2;
   constexpr int R = 4;
   const dim3 grid((N + 4 * R - 1) / (4 * R));
 #define GV(MV) \
-  gemv_kernel<MV, R, 4><<<grid, 256, 0, stream>>>((const bf16*)X, ldx, (const bf16*)W, (const bf16*)bias, (bf16*)out, ldo, N, K)
+  gemv_kernel<MV, R, (MV <= 4 ? 4 : 2)><<<grid, 256, 0, stream>>>((const bf16*)X, ldx, (const bf16*)W, (const bf16*)bias, (bf16*)out, ldo, N, K)
   switch (M) {
     case 1: GV(1); break;
     case 2: GV(2); break;
     case 3: GV(3); break;
-    default: GV(4); break;
+    case 4: GV(4); break;
+    case 5: GV(5); break;
+    case 6: GV(6); break;
+    case 7: GV(7); break;
+    default: GV(8); break;
   }
 #undef GV
   OME_CHECK_LAUNCH();

@@ -567,14 +567,14 @@ def stream_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = No
 
 
 def gemv_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return (x.dim() == 2 and 1 <= x.shape[0] <= 4 and x.shape[1] % 8 == 0 and x.stride(1) == 1
+    return (x.dim() == 2 and 1 <= x.shape[0] <= 8 and x.shape[1] % 8 == 0 and x.stride(1) == 1
             and x.stride(0) % 8 == 0 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
             and w.is_contiguous())
 
 
 def gemv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
          out: torch.Tensor | None = None) -> torch.Tensor:
-    """out[M, N] = x[M, K] . w[N, K]^T (+ bias) for M <= 4 (``gemv.hip``: a pure weight stream,
+    """out[M, N] = x[M, K] . w[N, K]^T (+ bias) for M <= 8 (``gemv.hip``: a pure weight stream,
     R rows per wave, several K steps of 16-B loads in flight, no LDS)."""
     M, K = x.shape
     N = w.shape[0]

@@ -42,7 +42,7 @@ def main():
             wb = N * K * 2
             ws = [w] + [w.clone() for _ in range(max(1, -(-640 * 2**20 // wb)) - 1)]
             line = [f"M={M:4d} {name:8s} hipblaslt={timeit(lambda w_: F.linear(x, w_), ws):7.1f}us"]
-            if M <= 4:
+            if M <= 8:
                 og = ops.gemv(x, w)
                 err = (og.float() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
                 t = timeit(lambda w_: ops.gemv(x, w_, out=og), ws)

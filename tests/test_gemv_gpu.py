@@ -1,4 +1,4 @@
-"""``ome_gemv`` (batch-1..4 weight-streaming GEMV, ``csrc/kernels/gemv.hip``) vs an fp32 PyTorch
+"""``ome_gemv`` (batch-1..8 weight-streaming GEMV, ``csrc/kernels/gemv.hip``) vs an fp32 PyTorch
 reference: every row count, N not a multiple of the 16-row workgroup span, K tails below one
 512-element step, bias, strided activations and output."""
 import pytest
@@ -9,7 +9,7 @@ from ome_amd import ops
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("M", [1, 2, 3, 4, 5, 8])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (4096, 14336), (1000, 1032), (37, 200), (16, 8),
                                  (2048, 2560)])
 def test_gemv_matches_reference(M, N, K):
