@@ -598,6 +598,7 @@ def gemv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
 # them on an 8B model: profiles/r02_stream_gemm_bench.txt).
 _gemm_route: dict = {}
 _gemm_tuning = [False]
+_STREAM_STATIC = os.environ.get("OME_STREAM_GEMM", "0") == "static"
 
 
 class decode_gemm_tuning:
@@ -632,6 +633,12 @@ def decode_gemm_plan(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None
     key = (M, N, K, bias is not None, x.device)
     if key in _gemm_route:
         return _gemm_route[key]
+    if _STREAM_STATIC and 5 <= M <= 16 and K <= 4096 and stream_gemm_ok(M, N, K) and _gpu(x):
+        # rule from the cold-weight microbenchmark (profiles/r02_stream_gemm_bench_cold.txt): wide
+        # weights (gate_up-like) at split 4, square o-like weights at split 8, the rest on hipBLASLt
+        plan = (1, 4) if N >= 16384 else (1, 8) if N <= 4096 else None
+        _gemm_route[key] = plan
+        return plan
     if not _gemm_tuning[0]:
         return None
     plan = None
