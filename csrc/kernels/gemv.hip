@@ -86,10 +86,16 @@ OME_API int ome_gemv(const void* X, int64_t ldx, const void* W, const void* bias
                      int K, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (M > 8 || K % 8 || ldx % 8 || K <= 0) return -2;
-  constexpr int R = 4;
-  const dim3 grid((N + 4 * R - 1) / (4 * R));
-#define GV(MV) \
-  gemv_kernel<MV, R, (MV <= 4 ? 4 : 2)><<<grid, 256, 0, stream>>>((const bf16*)X, ldx, (const bf16*)W, (const bf16*)bias, (bf16*)out, ldo, N, K)
+  // narrow weights: 2 rows per wave (twice the waves to spread over 256 CUs); long rows (K >= 8192,
+  // the down projection) with <= 2 activation rows: 8 K steps in flight per wave
+  const bool narrow = N <= 4096, deep = K >= 8192 && M <= 2;
+#define GV_L(MV, RV, UV)                                                                                    \
+  gemv_kernel<MV, RV, UV><<<dim3((N + 4 * RV - 1) / (4 * RV)), 256, 0, stream>>>(                          \
+      (const bf16*)X, ldx, (const bf16*)W, (const bf16*)bias, (bf16*)out, ldo, N, K)
+#define GV(MV)                                                                              \
+  if (MV <= 2 && deep) { if (narrow) GV_L(MV, 2, 8); else GV_L(MV, 4, 8); }                \
+  else if (narrow) GV_L(MV, 2, (MV <= 4 ? 4 : 2));                                          \
+  else GV_L(MV, 4, (MV <= 4 ? 4 : 2))
   switch (M) {
     case 1: GV(1); break;
     case 2: GV(2); break;
@@ -100,6 +106,7 @@ OME_API int ome_gemv(const void* X, int64_t ldx, const void* W, const void* bias
     case 7: GV(7); break;
     default: GV(8); break;
   }
+#undef GV_L
 #undef GV
   OME_CHECK_LAUNCH();
   return 0;
