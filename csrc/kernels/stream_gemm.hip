@@ -28,7 +28,7 @@ template <int MF, int NF>   // MF: 32-row activation fragments (Mp = 32 MF); NF:
 __global__ __launch_bounds__(256) void stream_gemm_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                           const bf16* __restrict__ W, const bf16* __restrict__ bias,
                                                           bf16* __restrict__ out, int64_t ldo, int M, int N, int K,
-                                                          int splits, float* __restrict__ ws) {
+                                                          int splits, float* __restrict__ ws, int* __restrict__ cnt) {
   constexpr int MP = 32 * MF;
   __shared__ __attribute__((aligned(16))) bf16 sX[2][MP * KB];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, lr = lane & 31, lh = lane >> 5;
@@ -137,6 +137,39 @@ __global__ __launch_bounds__(256) void stream_gemm_kernel(const bf16* __restrict
           }
       }
     }
+    if (cnt == nullptr) return;   // two-launch form: stream_gemm_reduce_kernel sums the slabs
+    // In-launch combine (one agent-scope release per writer, one acquire in the tile's last
+    // arriver; correct for any placement of a tile's splits over XCDs): the last of the tile's
+    // `splits` workgroups sums every slab in fixed split order and stores bf16.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // every wave has left the K loop: the LDS image is free for the flag
+    int* flag = reinterpret_cast<int*>(&sX[0][0]);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int t = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = t == splits - 1;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm (graph replay)
+    }
+    __syncthreads();
+    constexpr int NWG = 128 * NF, V = NWG / 4;   // tile columns, float4 columns per row
+    const int c0 = tile * NWG;
+    for (int e = tid; e < M * V; e += 256) {
+      const int row = e / V, n = c0 + 4 * (e - row * V);
+      f32x4 sum = *reinterpret_cast<const f32x4*>(ws + (int64_t)row * N + n);
+      for (int sp = 1; sp < splits; ++sp)
+        sum += *reinterpret_cast<const f32x4*>(ws + ((int64_t)sp * M + row) * N + n);
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (bf16)(sum[r] + (bias ? (float)bias[n + r] : 0.f));
+      *reinterpret_cast<bf16x4*>(out + (int64_t)row * ldo + n) = v;
+    }
     return;
   }
 #pragma unroll
@@ -189,9 +222,11 @@ __global__ __launch_bounds__(256) void stream_gemm_reduce_kernel(const float* __
 
 // X [M, K] (row stride ldx), W [N, K] contiguous, out [M, N] (row stride ldo); 1 <= M <= 256,
 // nf in {1, 2} (2 only for M <= 128), N % (128 nf) == 0, K % 64 == 0, 1 <= splits <= K / 64.  splits > 1 needs ws with
-// >= splits * M * N floats (no other state: HIP-graph replayable).
+// >= splits * M * N floats; with cnt (>= N / (128 nf) ints, zero before the first launch, re-armed by
+// the kernel: HIP-graph replayable) the tile's last split combines the slabs in the same launch,
+// without it a second kernel does.
 OME_API int ome_stream_gemm(const void* X, int64_t ldx, const void* W, const void* bias, void* out, int64_t ldo, int M,
-                            int N, int K, int nf, int splits, float* ws, hipStream_t stream) {
+                            int N, int K, int nf, int splits, float* ws, int* cnt, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (M > 256 || (nf != 1 && nf != 2) || N % (128 * nf) || K % KB || ldx % 8 || ldo % 8 || splits < 1 ||
       splits > K / KB)
@@ -202,7 +237,7 @@ OME_API int ome_stream_gemm(const void* X, int64_t ldx, const void* W, const voi
   const int mf = (M + 31) / 32;
 #define SG(MFV, NFV)                                                                                          \
   stream_gemm_kernel<MFV, NFV><<<grid, 256, 0, stream>>>((const bf16*)X, ldx, (const bf16*)W, (const bf16*)bias, \
-                                                         (bf16*)out, ldo, M, N, K, splits, ws)
+                                                         (bf16*)out, ldo, M, N, K, splits, ws, cnt)
 #define SG_NF(MFV) \
   if (nf == 1) SG(MFV, 1); else SG(MFV, 2)
   switch (mf) {
@@ -218,7 +253,7 @@ OME_API int ome_stream_gemm(const void* X, int64_t ldx, const void* W, const voi
 #undef SG_NF
 #undef SG
   OME_CHECK_LAUNCH();
-  if (splits > 1) {
+  if (splits > 1 && cnt == nullptr) {
     const int64_t threads = (int64_t)M * N / 8;
     stream_gemm_reduce_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, stream>>>(ws, (const bf16*)bias, (bf16*)out,
                                                                                      ldo, M, N, splits);

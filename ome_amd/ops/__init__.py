@@ -512,6 +512,7 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = No
 
 
 _stream_ws: dict = {}
+_stream_cnt: dict = {}   # per-device tile arrival counters of the single-launch split-K
 
 
 def stream_gemm_plan(M: int, N: int, K: int) -> tuple[int, int]:
@@ -557,12 +558,17 @@ def stream_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = No
     out = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
     pnf, ps = stream_gemm_plan(M, N, K)
     nf, s = nf or pnf, splits or ps
-    ws = None
+    ws = cnt = None
     if s > 1:
         stream_gemm_reserve(x.device, s * M * N)
         ws = _stream_ws[x.device]
+        if os.environ.get("OME_STREAM_INKERNEL", "0") == "1":   # opt-in single launch: last split combines (measured slower)
+            cnt = _stream_cnt.get(x.device)
+            if cnt is None:
+                cnt = _stream_cnt[x.device] = torch.zeros(1 << 13, dtype=torch.int32, device=x.device)
+            assert N // (128 * nf) <= cnt.numel()
     call("ome_stream_gemm", x.data_ptr(), x.stride(0), w.data_ptr(), ptr(bias), out.data_ptr(), out.stride(0), M, N,
-         K, nf, s, ptr(ws), stream_ptr())
+         K, nf, s, ptr(ws), ptr(cnt), stream_ptr())
     return out
 
 
