@@ -50,11 +50,16 @@ __device__ __forceinline__ uint32_t ld_acquire(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// all ranks' block b meet here; `which` 0 = start flags, 1 = end flags
+// all ranks' block b meet here; `which` 0 = start flags, 1 = end flags.
+// Publish order (MI355X_MICROARCH.md, inter-workgroup visibility): every wave drains its stores
+// (`s_waitcnt vmcnt(0)`), workgroup barrier, then the flag lanes release at system scope and wait
+// once more before the flag store (ROCm 7.2 may drop the fence's own wait).
 __device__ __forceinline__ void block_barrier(const Peers& P, int rank, int world, uint32_t epoch, int which) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < world) {
     __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     Signal* peer = P.sig[threadIdx.x];
     st_release(which ? &peer->end[blockIdx.x][rank] : &peer->start[blockIdx.x][rank], epoch);
     Signal* self = P.sig[rank];
@@ -157,6 +162,114 @@ __global__ __launch_bounds__(kThreads) void ar_two_shot(Peers P, int rank, int64
   if (threadIdx.x == 0) self->epoch[blockIdx.x] = epoch;
 }
 
+
+// One-shot all-reduce fused with the residual add + RMSNorm that follows every row-parallel
+// projection in a decoder layer: per token row,
+//   a = bf16(sum over ranks of the staged inputs)        (what ar_one_shot would write)
+//   res <- bf16(a + res) ; x <- bf16(rmsnorm(res) * w)    (ops.fused_add_rmsnorm semantics)
+// Block b of every rank handles rows b, b + grid, ... (the per-block barrier pairs them), one
+// 512-lane pass per row with VPT 16-byte vectors per lane (H <= 512 * 8 * VPT).
+template <int W, int VPT>
+__global__ __launch_bounds__(kThreads) void ar_one_shot_add_rmsnorm(Peers P, int rank, int rows, int H,
+                                                                    u32x4* __restrict__ x, u32x4* __restrict__ res,
+                                                                    const u32x4* __restrict__ w, float eps) {
+  __shared__ uint32_t s_epoch;
+  __shared__ float red[kThreads / 64];
+  Signal* self = P.sig[rank];
+  if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  block_barrier(P, rank, W, epoch, 0);
+  const int hv = H >> 3;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    float v[VPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < VPT; ++c) {
+      const int i = threadIdx.x + c * kThreads;
+      if (i < hv) {
+        const int64_t e = (int64_t)row * hv + i;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        u32x4 in[W];
+#pragma unroll
+        for (int r = 0; r < W; ++r) in[r] = reinterpret_cast<const u32x4*>(P.data[(rank + r) % W])[e];
+#pragma unroll
+        for (int r = 0; r < W; ++r) add8(acc, in[r]);
+        const u32x4 a = pack8(acc);   // the all-reduce result, rounded to bf16
+        float fa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        add8(fa, a);
+        add8(fa, res[e]);
+        const u32x4 sres = pack8(fa);  // residual stream stays bf16
+        res[e] = sres;
+        float fs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        add8(fs, sres);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[c][j] = fs[j];
+          ss += fs[j] * fs[j];
+        }
+      }
+    }
+    // block reduction of the row's sum of squares
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < kThreads / 64; ++k) tot += red[k];
+    __syncthreads();
+    const float rs = rsqrtf(tot / (float)H + eps);
+#pragma unroll
+    for (int c = 0; c < VPT; ++c) {
+      const int i = threadIdx.x + c * kThreads;
+      if (i < hv) {
+        float fw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        add8(fw, w[i]);
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = v[c][j] * rs * fw[j];
+        x[(int64_t)row * hv + i] = pack8(o);
+      }
+    }
+  }
+  block_barrier(P, rank, W, epoch, 1);  // nobody may restage its buffer while a peer still reads it
+  if (threadIdx.x == 0) self->epoch[blockIdx.x] = epoch;
+}
+
+// All-gather along the last dim: every rank stages in[rows][cols] (its own slice, written into its
+// IPC buffer by this kernel), out[rows][W * cols] = concat over ranks (rank-major per row), the
+// layout of torch.cat(parts, dim=-1) for vocab-parallel logits.  Block b stages and gathers the
+// same vector indices on every rank, so the per-block barrier orders each hand-off.
+template <int W>
+__global__ __launch_bounds__(kThreads) void ag_one_shot(Peers P, int rank, const u32x4* __restrict__ in,
+                                                       int64_t rows, int64_t cvec, u32x4* __restrict__ out) {
+  __shared__ uint32_t s_epoch;
+  Signal* self = P.sig[rank];
+  if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  const int64_t n = rows * cvec;
+  u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]);
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const u32x4 v = in[i];
+    mine[i] = v;
+    const int64_t r = i / cvec, c = i - r * cvec;
+    out[r * (W * cvec) + rank * cvec + c] = v;
+  }
+  block_barrier(P, rank, W, epoch, 0);
+  for (int q = 1; q < W; ++q) {
+    const int src = (rank + q) % W;
+    const u32x4* theirs = reinterpret_cast<const u32x4*>(P.data[src]);
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+      const int64_t r = i / cvec, c = i - r * cvec;
+      out[r * (W * cvec) + src * cvec + c] = theirs[i];
+    }
+  }
+  block_barrier(P, rank, W, epoch, 1);
+  if (threadIdx.x == 0) self->epoch[blockIdx.x] = epoch;
+}
+
 struct Ctx {
   int rank, world;
   size_t data_bytes;
@@ -226,8 +339,11 @@ OME_API int ome_comm_all_reduce(void* ctx, const void* in, void* out, int64_t n,
   const size_t bytes = (size_t)n * 2;
   if (bytes > c->data_bytes) return -3;
   if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
-  hipError_t e = hipMemcpyAsync(c->data, in, bytes, hipMemcpyDeviceToDevice, stream);
-  if (e != hipSuccess) return (int)e;
+  hipError_t e = hipSuccess;
+  if (in != c->data) {  // callers that produced the input straight into the IPC buffer skip the copy
+    e = hipMemcpyAsync(c->data, in, bytes, hipMemcpyDeviceToDevice, stream);
+    if (e != hipSuccess) return (int)e;
+  }
   const int64_t n_vec = n / 8;
   const int64_t red_vec = (int64_t)(c->data_bytes / 16);
   dim3 grid(blocks), block(kThreads);
@@ -248,6 +364,61 @@ OME_API int ome_comm_all_reduce(void* ctx, const void* in, void* out, int64_t n,
 #undef OME_AR_CASE
   e = hipGetLastError();
   return (int)e;
+}
+
+// base address of this rank's IPC input buffer (callers may produce an all-reduce input into it)
+OME_API void* ome_comm_buffer(void* ctx) { return ((Ctx*)ctx)->data; }
+
+// x, res: [rows][H] bf16 (contiguous); the reduced input is the staged buffer (`in`, copied into
+// the IPC buffer unless it already is it).  res <- bf16(allreduce(in) + res); x <- rmsnorm(res) * w
+OME_API int ome_comm_all_reduce_add_rmsnorm(void* ctx, const void* in, void* x, void* res, const void* w,
+                                            int rows, int H, float eps, int blocks, hipStream_t stream) {
+  Ctx* c = (Ctx*)ctx;
+  if (H % 8 || rows <= 0) return rows == 0 ? 0 : -2;
+  const size_t bytes = (size_t)rows * H * 2;
+  if (bytes > c->data_bytes) return -3;
+  const int vpt = (H / 8 + kThreads - 1) / kThreads;
+  if (vpt > 4) return -2;
+  if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
+  if (blocks > rows) blocks = rows;
+  hipError_t e = hipSuccess;
+  if (in != c->data) {
+    e = hipMemcpyAsync(c->data, in, bytes, hipMemcpyDeviceToDevice, stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  dim3 grid(blocks), block(kThreads);
+#define OME_ARN_CASE(W, V)                                                                                 \
+  if (c->world == W && vpt <= V && vpt > V / 2) {                                                         \
+    ar_one_shot_add_rmsnorm<W, V><<<grid, block, 0, stream>>>(c->peers, c->rank, rows, H, (u32x4*)x,       \
+                                                              (u32x4*)res, (const u32x4*)w, eps);         \
+    return (int)hipGetLastError();                                                                         \
+  }
+#define OME_ARN_W(W) OME_ARN_CASE(W, 1) OME_ARN_CASE(W, 2) OME_ARN_CASE(W, 4)
+  OME_ARN_W(2)
+  OME_ARN_W(4)
+  OME_ARN_W(8)
+#undef OME_ARN_W
+#undef OME_ARN_CASE
+  return -2;
+}
+
+// out[rows][world * cols] = concat over ranks of in[rows][cols] (bf16/fp16, cols * 2 % 16 == 0)
+OME_API int ome_comm_all_gather(void* ctx, const void* in, void* out, int64_t rows, int64_t cols, int blocks,
+                                hipStream_t stream) {
+  Ctx* c = (Ctx*)ctx;
+  if ((cols * 2) % 16 || rows < 0) return -2;
+  if ((size_t)rows * cols * 2 > c->data_bytes) return -3;
+  if (rows == 0) return 0;
+  if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
+  const int64_t cvec = cols * 2 / 16;
+  dim3 grid(blocks), block(kThreads);
+  switch (c->world) {
+    case 2: ag_one_shot<2><<<grid, block, 0, stream>>>(c->peers, c->rank, (const u32x4*)in, rows, cvec, (u32x4*)out); break;
+    case 4: ag_one_shot<4><<<grid, block, 0, stream>>>(c->peers, c->rank, (const u32x4*)in, rows, cvec, (u32x4*)out); break;
+    case 8: ag_one_shot<8><<<grid, block, 0, stream>>>(c->peers, c->rank, (const u32x4*)in, rows, cvec, (u32x4*)out); break;
+    default: return -2;
+  }
+  return (int)hipGetLastError();
 }
 
 OME_API int ome_comm_error(void* ctx) {

@@ -80,22 +80,26 @@ def _build_lib(name: str, sources: list[Path], headers: list[Path], compiler: st
     return lib
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> list[Path]:
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True,
+          only: tuple[str, ...] | None = None) -> list[Path]:
+    """Build the native libraries (``only``: a subset of ome_kernels / omeio / ome_comm)."""
     jobs = jobs or min(8, os.cpu_count() or 4)
     hipcc = _hipcc()
     built = []
     kdir = CSRC / "kernels"
-    built.append(_build_lib("ome_kernels", sorted(kdir.glob("*.hip")), sorted(kdir.glob("*.h")), hipcc,
-                            HIP_FLAGS, [], force, jobs))
+    want = set(only or ("ome_kernels", "omeio", "ome_comm"))
+    if "ome_kernels" in want:
+        built.append(_build_lib("ome_kernels", sorted(kdir.glob("*.hip")), sorted(kdir.glob("*.h")), hipcc,
+                                HIP_FLAGS, [], force, jobs))
     iodir = CSRC / "omeio"
     io_src = sorted(iodir.glob("*.cpp"))
-    if io_src:
+    if io_src and "omeio" in want:
         built.append(_build_lib("omeio", io_src, sorted(iodir.glob("*.h")), hipcc,
                                 [f for f in HIP_FLAGS if not f.startswith("--offload")] + ["-pthread", "-D__HIP_PLATFORM_AMD__"],
                                 ["-pthread", "-L/opt/rocm/lib", "-lamdhip64", "-lcrypto"], force, jobs))
     cdir = CSRC / "comm"
     comm_src = sorted(cdir.glob("*.hip"))
-    if comm_src:
+    if comm_src and "ome_comm" in want:
         built.append(_build_lib("ome_comm", comm_src, sorted(cdir.glob("*.h")) + [kdir / "common.h"], hipcc,
                                 HIP_FLAGS + [f"-I{kdir}"], [], force, jobs))
     if verbose:

@@ -252,9 +252,34 @@ class LlamaForCausalLM:
                                  self.scale, self.window, k_scale=ks, v_scale=vs)
 
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        return pstate.tp_all_reduce(self._mlp_partial(i, x))
+
+    def _mlp_partial(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        """gate_up -> SiLU*mul -> down: this rank's partial sums (before the TP all-reduce),
+        written straight into the all-reduce's staging buffer when there is one."""
         gu = linear(x, self.w_gu[i])
         a = ops.act_and_mul(gu, self.act)
-        return pstate.tp_all_reduce(linear(a, self.w_d[i]))
+        return self._row_parallel(a, self.w_d[i])
+
+    def _row_parallel(self, a: torch.Tensor, w, bias=None) -> torch.Tensor:
+        if self.tp.tp > 1:
+            st = pstate.tp_ar_staging((a.shape[0], self.cfg.hidden_size), self.dtype, a.device)
+            if st is not None:
+                return linear(a, w, bias, out=st)
+        return linear(a, w, bias)
+
+    def _reduce_add_norm(self, part: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                         reduce: bool = True) -> torch.Tensor:
+        """residual += allreduce(part); return rmsnorm(residual) * w -- one fused xGMI kernel at
+        decode sizes under TP, all-reduce + fused_add_rmsnorm otherwise (``reduce=False``: the
+        input is already reduced)."""
+        if self.tp.tp > 1 and reduce:
+            y = pstate.tp_all_reduce_add_rmsnorm(part, residual, w, self.eps)
+            if y is not None:
+                return y
+            part = pstate.tp_all_reduce(part)
+        ops.fused_add_rmsnorm(part, residual, w, self.eps)
+        return part
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: PagedKVCache,
                 input_embeds: torch.Tensor | None = None) -> torch.Tensor:
@@ -262,9 +287,14 @@ class LlamaForCausalLM:
         cfg, tp, D = self.cfg, self.tp, self.D
         T = ids.shape[0]
         x, residual = self._stage_input(ids, input_embeds)
+        st = pstate.get()
+        first = self.layers[0] if self.layers else 0
+        # subclasses that override mlp() (MoE) return already-reduced outputs
+        partial = type(self).mlp is LlamaForCausalLM.mlp
         for i in self.layers:
-            if i > 0:
-                ops.fused_add_rmsnorm(x, residual, self.ln1[i], self.eps)
+            if i > 0:  # the previous layer's MLP partial sums -> all-reduce + add + norm (a pipeline
+                # stage's first layer receives the previous stage's already-reduced output)
+                x = self._reduce_add_norm(x, residual, self.ln1[i], reduce=partial and i > first)
             qkv = linear(x, self.w_qkv[i], self.b_qkv[i])
             q = torch.empty(T, tp.hq, D, dtype=self.dtype, device=x.device)
             k_cache, v_cache = kv.layer(i)
@@ -272,9 +302,13 @@ class LlamaForCausalLM:
             ops.rope_qkv_cache(qkv, meta.positions, self.cos_sin, cfg.rot_dim, q, k_cache, v_cache, meta.slots,
                                tp.hq, tp.hkv, D, True, self.qn[i], self.kn[i], self.eps, ks, vs)
             attn = self.attention(q, k_cache, v_cache, meta, ks, vs)
-            o = pstate.tp_all_reduce(linear(attn.view(T, tp.hq * D), self.w_o[i]))
-            ops.fused_add_rmsnorm(o, residual, self.ln2[i], self.eps)
-            x = self.mlp(i, o)
+            o = self._reduce_add_norm(self._row_parallel(attn.view(T, tp.hq * D), self.w_o[i]), residual,
+                                      self.ln2[i])
+            x = self._mlp_partial(i, o) if partial else self.mlp(i, o)
+        if self.layers and (st.pp_size == 1 or st.is_last_pp):
+            return self._reduce_add_norm(x, residual, self.norm, reduce=partial)   # final norm
+        if self.layers and partial:
+            x = pstate.tp_all_reduce(x)
         return self._stage_output(x, residual)
 
     def _stage_input(self, ids: torch.Tensor, input_embeds: torch.Tensor | None):

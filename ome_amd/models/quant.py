@@ -69,10 +69,19 @@ def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
 _GEMV_ROWS = int(os.environ.get("OME_GEMV_ROWS", "4"))
 
 
-def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None) -> torch.Tensor:
+def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """Dispatch: plain tensor -> hipBLASLt GEMM; single-row decode -> the GEMV stream kernel
     (``ops.gemv``, ``OME_GEMV_ROWS``); the weight-streaming MFMA GEMM for decode shapes where it
-    was measured faster (``ops.decode_gemm_plan``, opt-in); Fp8Weight -> W8A8 MFMA path."""
+    was measured faster (``ops.decode_gemm_plan``, opt-in); Fp8Weight -> W8A8 MFMA path.
+    ``out``: write the result there (e.g. the TP all-reduce's IPC staging buffer)."""
+    if out is not None:
+        if isinstance(w, torch.Tensor) and x.dim() == 2 and x.is_cuda and not (x.shape[0] <= _GEMV_ROWS and
+                                                                                ops.gemv_ok(x, w)):
+            if bias is None:
+                return torch.matmul(x, w.t(), out=out)
+            return torch.addmm(bias, x, w.t(), out=out)
+        out.copy_(linear(x, w, bias))
+        return out
     if isinstance(w, Fp8Weight):
         return ops.fp8_linear(x, w.q, w.scale, w.block, bias)
     if x.dim() == 2 and x.shape[0] <= 256 and x.is_cuda:

@@ -65,6 +65,8 @@ _SIGNATURES = {
         "ome_comm_handle_size": [],
         "ome_comm_open": [vp, vp, vp],
         "ome_comm_all_reduce": [vp, vp, vp, i64, i32, i32, vp],
+        "ome_comm_all_reduce_add_rmsnorm": [vp, vp, vp, vp, vp, i32, i32, f32, i32, vp],
+        "ome_comm_all_gather": [vp, vp, vp, i64, i64, i32, vp],
         "ome_comm_error": [vp],
         "ome_comm_destroy": [vp],
         "ome_kvlink_export": [vp, vp, C.POINTER(i64)],

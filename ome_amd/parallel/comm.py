@@ -44,6 +44,10 @@ class CustomAllReduce:
         if rc != 0:
             raise _native.NativeError(f"ome_comm_create failed ({rc})")
         self._lib, self._ctx = lib, ctx
+        lib.ome_comm_buffer.argtypes = [C.c_void_p]
+        lib.ome_comm_buffer.restype = C.c_void_p
+        self._buf_ptr = int(lib.ome_comm_buffer(ctx))
+        self._buf = None
         mine = (bytes(sig_h), bytes(dat_h))
         allh = [None] * self.world
         dist.all_gather_object(allh, mine, group=cpu_group)
@@ -69,6 +73,59 @@ class CustomAllReduce:
             raise _native.NativeError(f"ome_comm_all_reduce failed ({rc})")
         return out
 
+    def staging(self, shape, dtype=torch.bfloat16, device=None) -> torch.Tensor | None:
+        """A tensor view of this rank's registered IPC input buffer: a producer (the row-parallel
+        GEMM) that writes its output here lets the next :meth:`all_reduce` skip the staging copy.
+        None when the shape does not fit."""
+        n = 1
+        for d in shape:
+            n *= int(d)
+        if dtype != torch.bfloat16 or n * 2 > self.max_bytes or n % 8:
+            return None
+        if self._buf is None:
+            try:
+                self._buf = _wrap_device_ptr(self._buf_ptr, self.max_bytes // 2, torch.bfloat16,
+                                             device or torch.device("cuda", torch.cuda.current_device()))
+            except Exception as e:  # noqa: BLE001 — the staged-copy path stays correct
+                log.warning("IPC staging buffer not wrappable as a tensor (%s); all-reduce keeps its copy", e)
+                self._buf = False
+        if self._buf is False:
+            return None
+        return self._buf[:n].view(*shape)
+
+    def all_reduce_add_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor,
+                               eps: float) -> torch.Tensor | None:
+        """``residual += allreduce(x); return rmsnorm(residual) * weight`` in ONE kernel (one-shot
+        sizes only; ``x`` may be the :meth:`staging` buffer).  None (nothing done) when the message
+        is too large for one-shot.  The normed rows go to a fresh tensor: writing them over the
+        staged input would race with peers still reading it."""
+        rows, H = x.shape
+        if x.numel() * 2 > self.one_shot_max or H % 8 or H > 512 * 8 * 4 or not residual.is_contiguous():
+            return None
+        out = torch.empty_like(x)
+        rc = self._lib.ome_comm_all_reduce_add_rmsnorm(
+            self._ctx, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()), C.c_void_p(residual.data_ptr()),
+            C.c_void_p(weight.data_ptr()), rows, H, float(eps), self.blocks,
+            C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        if rc != 0:
+            raise _native.NativeError(f"ome_comm_all_reduce_add_rmsnorm failed ({rc})")
+        return out
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor | None:
+        """concat over ranks along the last dim (x: [rows, cols] bf16 contiguous), or None when the
+        shape does not fit the one-shot gather."""
+        if x.dtype not in (torch.bfloat16, torch.float16) or not x.is_contiguous() or x.dim() != 2:
+            return None
+        rows, cols = x.shape
+        if (cols * 2) % 16 or rows * cols * 2 > self.max_bytes:
+            return None
+        out = torch.empty(rows, cols * self.world, dtype=x.dtype, device=x.device)
+        rc = self._lib.ome_comm_all_gather(self._ctx, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()), rows,
+                                           cols, self.blocks, C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        if rc != 0:
+            raise _native.NativeError(f"ome_comm_all_gather failed ({rc})")
+        return out
+
     def error(self) -> int:
         return self._lib.ome_comm_error(self._ctx)
 
@@ -76,6 +133,20 @@ class CustomAllReduce:
         if self._ctx:
             self._lib.ome_comm_destroy(self._ctx)
             self._ctx = None
+
+
+def _wrap_device_ptr(ptr: int, numel: int, dtype: torch.dtype, device: torch.device) -> torch.Tensor:
+    """A torch tensor over memory this library allocated (the IPC buffer lives as long as the
+    communicator; torch never frees it)."""
+    class _Holder:
+        pass
+
+    h = _Holder()
+    itemsize = torch.empty(0, dtype=dtype).element_size()
+    h.__cuda_array_interface__ = {"shape": (numel,), "typestr": {torch.bfloat16: "<i2", torch.float16: "<f2"}[dtype],
+                                  "data": (ptr, False), "version": 3, "strides": (itemsize,)}
+    t = torch.as_tensor(h, device=device)
+    return t.view(dtype)
 
 
 class TPCommunicator:
@@ -95,3 +166,20 @@ class TPCommunicator:
             return self.custom.all_reduce(x)
         dist.all_reduce(x, group=self.group)
         return x
+
+    def staging(self, shape, dtype, device) -> torch.Tensor | None:
+        return self.custom.staging(shape, dtype, device) if self.custom is not None else None
+
+    def all_reduce_add_rmsnorm(self, x, residual, weight, eps) -> torch.Tensor | None:
+        if self.custom is None or not self.custom.usable(x):
+            return None
+        return self.custom.all_reduce_add_rmsnorm(x, residual, weight, eps)
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        if self.custom is not None:
+            out = self.custom.all_gather_last(x)
+            if out is not None:
+                return out
+        parts = [torch.empty_like(x) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(parts, x.contiguous(), group=self.group)
+        return torch.cat(parts, dim=-1)

@@ -36,6 +36,14 @@ class ParallelState:
     backend: str = "nccl"
     comm: object | None = None  # ome_amd.parallel.comm.TPCommunicator
     tbo: bool = False           # two-batch overlap of the EP MoE all-to-alls (parallel/ep.py)
+    cpu_group: object | None = None  # gloo group of this engine group (control-plane broadcasts)
+    global_rank: int = 0        # rank in the whole job (several engine replicas per job)
+    replica: int = 0
+    replicas: int = 1
+    base: int = 0               # global rank of this group's rank 0
+
+    def to_global(self, r: int) -> int:
+        return self.base + r
 
     @property
     def is_first_pp(self) -> bool:
@@ -61,19 +69,31 @@ def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_in
     ``dp_size > 1`` is DP attention (SGLang ``--tp N --dp N --enable-dp-attention``): every rank
     runs attention and dense layers for its OWN requests with full weights (attention TP = 1),
     while MoE experts are partitioned over all N ranks (EP = N) and tokens travel to their
-    experts by all-to-all (:mod:`ome_amd.parallel.ep`)."""
+    experts by all-to-all (:mod:`ome_amd.parallel.ep`).
+
+    A world larger than one engine group (``tp * pp * dp`` ranks) holds several independent
+    engine REPLICAS (e.g. ``bench.py --gpus 8 --tp 2``: four TP=2 engines): ranks
+    ``[r * g, (r + 1) * g)`` form replica ``r``; ``rank`` / ``world_size`` of the returned state
+    are the group-local ones, ``global_rank`` / ``replica`` locate the process in the job."""
     global _STATE
     if dp_size > 1:
         if tp_size not in (1, dp_size) or pp_size != 1:
             raise ValueError("DP attention needs tp_size == dp_size and pp_size == 1")
         tp_size = 1
-    world = world_size if world_size is not None else int(os.environ.get("WORLD_SIZE", tp_size * pp_size * dp_size))
-    rk = rank if rank is not None else int(os.environ.get("RANK", 0))
-    if world != tp_size * pp_size * dp_size:
-        raise ValueError(f"world_size {world} != tp {tp_size} * pp {pp_size} * dp {dp_size}")
+    gsize = tp_size * pp_size * dp_size
+    world = world_size if world_size is not None else int(os.environ.get("WORLD_SIZE", gsize))
+    grk = rank if rank is not None else int(os.environ.get("RANK", 0))
+    if world % gsize:
+        raise ValueError(f"world_size {world} is not a multiple of tp {tp_size} * pp {pp_size} * dp {dp_size}")
+    replicas = world // gsize
+    base = (grk // gsize) * gsize
+    rk = grk - base
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-    st = ParallelState(tp_size=tp_size, pp_size=pp_size, world_size=world, rank=rk, backend=backend)
+        # OME_DIST_BACKEND=gloo: several ranks sharing one GPU (tests on a 1-GPU box; RCCL refuses
+        # two ranks on one device) -- the TP collectives then run on the xGMI/IPC peer kernels
+        backend = os.environ.get("OME_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    st = ParallelState(tp_size=tp_size, pp_size=pp_size, world_size=gsize, rank=rk, backend=backend)
+    st.global_rank, st.replica, st.replicas, st.base = grk, grk // gsize, replicas, base
     st.dp_size, st.dp_rank = dp_size, (rk if dp_size > 1 else 0)
     st.tp_rank, st.pp_rank = rk % tp_size, (rk // tp_size) % pp_size
     st.ep_size = dp_size if dp_size > 1 else 1
@@ -82,26 +102,37 @@ def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_in
         if not dist.is_initialized():
             init_method = f"tcp://{dist_init_addr}" if dist_init_addr else None
             kw = {}
-            if backend == "nccl":
-                lr = local_rank if local_rank is not None else int(os.environ.get("LOCAL_RANK", rk % max(1, torch.cuda.device_count())))
+            if torch.cuda.is_available():
+                lr = local_rank if local_rank is not None else int(os.environ.get("LOCAL_RANK", grk % max(1, torch.cuda.device_count())))
+                lr = lr if lr < torch.cuda.device_count() else 0
                 torch.cuda.set_device(lr)
-                kw["device_id"] = torch.device("cuda", lr)
-            dist.init_process_group(backend=backend, init_method=init_method, rank=rk, world_size=world, **kw)
+                if backend == "nccl":
+                    kw["device_id"] = torch.device("cuda", lr)
+            dist.init_process_group(backend=backend, init_method=init_method, rank=grk, world_size=world, **kw)
         tp_cpu = None
-        for p in range(pp_size):
-            ranks = list(range(p * tp_size, (p + 1) * tp_size))
-            g = dist.new_group(ranks) if tp_size > 1 else None
-            gc = dist.new_group(ranks, backend="gloo") if tp_size > 1 else None
-            if p == st.pp_rank:
-                st.tp_group, tp_cpu = g, gc
-        for t in range(tp_size):
-            ranks = [p * tp_size + t for p in range(pp_size)]
-            g = dist.new_group(ranks) if pp_size > 1 else None
-            if t == st.tp_rank:
-                st.pp_group = g
-        st.ep_group = dist.group.WORLD if dp_size > 1 else None
+        # new_group is collective over the whole job: every rank creates every replica's groups
+        for rep in range(replicas):
+            b = rep * gsize
+            mine = rep == st.replica
+            grp = list(range(b, b + gsize))
+            cg = dist.new_group(grp, backend="gloo") if gsize > 1 else None
+            eg = (dist.group.WORLD if replicas == 1 else dist.new_group(grp)) if dp_size > 1 else None
+            if mine:
+                st.cpu_group, st.ep_group = cg, eg
+            for p in range(pp_size):
+                ranks = [b + r for r in range(p * tp_size, (p + 1) * tp_size)]
+                g = dist.new_group(ranks) if tp_size > 1 else None
+                gc = dist.new_group(ranks, backend="gloo") if tp_size > 1 else None
+                if mine and p == st.pp_rank:
+                    st.tp_group, tp_cpu = g, gc
+            for t in range(tp_size):
+                ranks = [b + p * tp_size + t for p in range(pp_size)]
+                g = dist.new_group(ranks) if pp_size > 1 else None
+                if mine and t == st.tp_rank:
+                    st.pp_group = g
         single_node = int(os.environ.get("LOCAL_WORLD_SIZE", world)) >= world
-        if backend == "nccl" and tp_size in (2, 4, 8) and single_node and os.environ.get("OME_CUSTOM_AR", "1") != "0":
+        if torch.cuda.is_available() and tp_size in (2, 4, 8) and single_node and \
+                os.environ.get("OME_CUSTOM_AR", "1") != "0":
             from ome_amd.parallel.comm import TPCommunicator
 
             st.comm = TPCommunicator(st.tp_group, cpu_group=tp_cpu)
@@ -124,10 +155,31 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def tp_ar_staging(shape, dtype: torch.dtype, device) -> torch.Tensor | None:
+    """A buffer a row-parallel projection can write its partial sums into so that the following
+    :func:`tp_all_reduce` needs no staging copy (None: allocate normally)."""
+    st = _STATE
+    if st.tp_size == 1 or st.comm is None or not torch.device(device).type == "cuda":
+        return None
+    return st.comm.staging(shape, dtype, device)
+
+
+def tp_all_reduce_add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor,
+                              eps: float) -> torch.Tensor | None:
+    """``residual += allreduce(x); return rmsnorm(residual) * weight`` fused into the all-reduce
+    kernel.  None when not applicable (the caller then all-reduces and norms separately)."""
+    st = _STATE
+    if st.tp_size == 1 or st.comm is None or not x.is_cuda:
+        return None
+    return st.comm.all_reduce_add_rmsnorm(x, residual, weight, eps)
+
+
 def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     st = _STATE
     if st.tp_size == 1:
         return x
+    if st.comm is not None and x.is_cuda and x.dim() == 2 and dim in (-1, 1):
+        return st.comm.all_gather_last(x.contiguous())
     parts = [torch.empty_like(x) for _ in range(st.tp_size)]
     dist.all_gather(parts, x.contiguous(), group=st.tp_group)
     return torch.cat(parts, dim=dim)
@@ -140,7 +192,7 @@ def stage_layers(num_layers: int, pp_size: int, pp_rank: int) -> list[int]:
 
 def _pp_peer(stage: int) -> int:
     st = _STATE
-    return stage * st.tp_size + st.tp_rank
+    return st.base + stage * st.tp_size + st.tp_rank
 
 
 def pp_send(*tensors: torch.Tensor) -> None:

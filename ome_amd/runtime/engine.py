@@ -131,6 +131,8 @@ class Engine:
         self._stop_pending = False
         self.step_count = 0
         self.kv_transfer = None  # PD disaggregation hook (ome_amd.runtime.disagg)
+        # what a failed lockstep step does to a multi-rank group (tests replace it)
+        self.on_fatal = lambda: os._exit(70)
         # overlapped scheduling: (batch, handle, launch time) of the step whose tokens are in flight
         self._inflight = None
         # host-side time split of the serving loop (seconds, cumulative): schedule / launch
@@ -235,10 +237,21 @@ class Engine:
         if self.dp and self.pstate.rank == 0:
             for r in new:  # DP attention: least-loaded rank owns the request
                 r.dp_rank = self._dp_assign()
+        leader = self.pstate.to_global(0)
+        stop = bool(stop or self._stop_pending)
+        # fixed-size header first: the common step with nothing new costs one small broadcast,
+        # not a pickle round trip
+        hdr = torch.tensor([len(new), len(aborts), int(stop)] if self.pstate.rank == 0 else [0, 0, 0],
+                           dtype=torch.int64)
+        dist.broadcast(hdr, src=leader, group=self._cpu_group())
+        if not int(hdr[0]) and not int(hdr[1]):
+            if int(hdr[2]):
+                self._stop = True
+            return (new, aborts) if self.pstate.rank == 0 else ([], [])
         payload = [[(r.rid, r.prompt_ids, asdict(r.params), r.bootstrap, getattr(r, "dp_rank", 0)) for r in new],
-                   aborts, stop or self._stop_pending]
+                   aborts, stop]
         obj = [payload if self.pstate.rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0, group=self._cpu_group())
+        dist.broadcast_object_list(obj, src=leader, group=self._cpu_group())
         if obj[0][2]:
             self._stop = True
         if self.pstate.rank == 0:
@@ -271,7 +284,7 @@ class Engine:
         import torch.distributed as dist
 
         if not hasattr(self, "_gloo"):
-            self._gloo = dist.new_group(backend="gloo")
+            self._gloo = self.pstate.cpu_group if self.pstate.cpu_group is not None else dist.new_group(backend="gloo")
         return self._gloo
 
     def step(self) -> list[Request]:
@@ -283,6 +296,8 @@ class Engine:
         and detokenisation hide behind the GPU.  Returned requests are those finished by step k.
         """
         self._drain_inbox()
+        if self._stop and self.pstate.world_size > 1:
+            return []   # the leader's stop broadcast: it runs no further lockstep step
         if self.kv_transfer is not None and self.kv_transfer.mode == "decode":
             self.kv_transfer.poll()
         if self.cfg.is_embedding:
@@ -357,7 +372,7 @@ class Engine:
                             r.finish_reason))
             r._reported = len(r.output_ids)
         gathered = [None] * self.pstate.world_size if self.pstate.rank == 0 else None
-        dist.gather_object(updates, gathered, dst=0, group=self._cpu_group())
+        dist.gather_object(updates, gathered, dst=self.pstate.to_global(0), group=self._cpu_group())
         if self.pstate.rank == 0:
             now = time.perf_counter()
             for rank_updates in gathered[1:]:
@@ -431,12 +446,20 @@ class Engine:
                     continue
             try:
                 self.step()
-            except Exception:  # noqa: BLE001 — surface and keep serving other requests
+            except Exception:  # noqa: BLE001 — surface; single engines keep serving other requests
                 log.exception("engine step failed")
                 for r in list(self.scheduler.running):
                     self.scheduler.finish(r, "abort:error")
                     if r.on_token:
                         r.on_token(r, [], True)
+                if self.pstate.world_size > 1:
+                    # a multi-rank group runs in lockstep: a rank that skips a step would leave
+                    # its peers blocked in the next collective.  Fail the whole group instead
+                    # (non-zero exit -> the LeaderWorkerSet RecreateGroupOnPodRestart policy).
+                    log.critical("rank %d of a %d-rank engine group failed a step; exiting",
+                                 self.pstate.rank, self.pstate.world_size)
+                    self.on_fatal()
+                    return
 
     def start(self) -> threading.Thread:
         t = threading.Thread(target=self.run_forever, name="ome-engine", daemon=True)

@@ -62,6 +62,28 @@ def _worker(rank, world, port, q):
             g.replay()
             torch.cuda.synchronize()
             worst = max(worst, ((buf.float().cpu() - want).abs() / (want.abs() + 1)).max().item())
+        # fused all-reduce + residual add + RMSNorm, input produced straight into the IPC buffer
+        for rows, H in ((1, 4096), (5, 512), (16, 4096), (3, 8192)):
+            part = _inputs(rank, rows * H, 300 + rows).view(rows, H).cuda()
+            res0 = _inputs(99, rows * H, 7).view(rows, H).cuda()  # same residual on every rank
+            w = (1 + 0.1 * _inputs(98, H, 8)).cuda()
+            st = ar.staging((rows, H))
+            assert st is not None
+            st.copy_(part)
+            res = res0.clone()
+            y = ar.all_reduce_add_rmsnorm(st, res, w, 1e-5)
+            assert y is not None
+            a = sum(_inputs(r, rows * H, 300 + rows).float() for r in range(world)).view(rows, H)
+            r_ref = (a.bfloat16().float() + res0.float().cpu()).bfloat16().float()
+            y_ref = r_ref * torch.rsqrt(r_ref.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float().cpu()
+            worst = max(worst, ((res.float().cpu() - r_ref).abs() / (r_ref.abs() + 1)).max().item())
+            worst = max(worst, ((y.float().cpu() - y_ref).abs() / (y_ref.abs() + 1)).max().item())
+        # all-gather along the last dim (vocab-parallel logits)
+        for rows, cols in ((1, 512), (7, 1024), (256, 16032)):
+            x = _inputs(rank, rows * cols, 400 + rows).view(rows, cols).cuda()
+            y = ar.all_gather_last(x)
+            want = torch.cat([_inputs(r, rows * cols, 400 + rows).view(rows, cols) for r in range(world)], -1)
+            worst = max(worst, (y.float().cpu() - want.float()).abs().max().item())
         dist.barrier()
         q.put((rank, worst, ar.error(), None))
         ar.close()
