@@ -158,6 +158,7 @@ def create_app(engine, ns=None):
     app = FastAPI(title="ome_amd runtime")
     tok = engine.tokenizer
     model_name = engine.served_model_name
+    from ome_amd.runtime.detok import IncrementalDetokenizer, StopMatcher, special_strings, strip_special
     from ome_amd.runtime.parsers import ReasoningParser, ToolParser
 
     tool_kind = getattr(ns, "tool_call_parser", None) if ns is not None else None
@@ -300,10 +301,6 @@ def create_app(engine, ns=None):
             raise ValueError("prompt must be a string or a list of token ids")
         return tok.encode(p), images
 
-    def _stop_hit(text: str, stops: list[str]) -> int | None:
-        idx = [text.find(s) for s in stops if s and s in text]
-        return min(idx) if idx else None
-
     def _logprobs(req, chat: bool):
         toks = [tok.decode([t], skip_special=False) for t in req.output_ids]
         if chat:
@@ -349,23 +346,38 @@ def create_app(engine, ns=None):
 
         use_tools = bool(chat and tool_kind and body.get("tools") and body.get("tool_choice", "auto") != "none")
         use_reason = bool(chat and reason_kind and body.get("separate_reasoning", True))
+        # parsers look for special-token markers (harmony <|channel|>/<|call|>, [TOOL_CALLS]):
+        # decode with them kept, strip them from what the client sees
+        raw_mode = use_tools or use_reason
+        specials = special_strings(tok) if raw_mode else []
+        harmony_tools = use_tools and tool_kind == "gpt-oss"
+        det = IncrementalDetokenizer(tok, skip_special=not raw_mode)
+        stopm = StopMatcher(stops)
+
+        def pull(fin: bool) -> tuple[str, bool]:
+            """New text since the last call (incremental, O(new tokens)), cut at a stop string."""
+            delta = det.push(req.output_ids[len(det.ids):])
+            if fin:
+                delta += det.flush()
+            cut = stopm.find(det.text, len(delta))
+            if cut is not None:
+                delta = delta[:max(0, cut - (len(det.text) - len(delta)))]
+                return delta, True
+            return delta, False
 
         if body.get("stream"):
             async def gen():
-                sent = ""
                 first = True
                 rp = ReasoningParser(reason_kind) if use_reason else None
                 tp = ToolParser(tool_kind) if use_tools else None
-                content_all, content_sent, calls_started = "", 0, False
+                content_all, content_sent, calls_started, raw_all = "", 0, False, ""
                 while True:
-                    toks, fin = await stream.q.get()
-                    text = tok.decode(req.output_ids)
-                    cut = _stop_hit(text, stops)
-                    if cut is not None:
-                        text, fin = text[:cut], True
+                    _, fin = await stream.q.get()
+                    delta, stopped = pull(fin)
+                    if stopped:
+                        fin = True
                         engine.abort(req.rid)
-                    delta = text[len(sent):]
-                    sent = text
+                    raw_all += delta
                     if chat:
                         d: dict = {}
                         if rp is not None:
@@ -373,44 +385,49 @@ def create_app(engine, ns=None):
                             if fin:
                                 fr, fc = rp.flush()
                                 rd, cd = rd + fr, cd + fc
+                            rd = strip_special(rd, specials)
                             if rd:
                                 d["reasoning_content"] = rd
                         else:
                             cd = delta
                         content_all += cd
                         if tp is not None and not calls_started:
-                            i = tp.start_index(content_all)
+                            i = tp.start_index(raw_all if harmony_tools else content_all)
                             if i >= 0:
                                 calls_started = True
-                                cd = content_all[content_sent:i]
+                                cd = content_all[content_sent:] if harmony_tools else content_all[content_sent:i]
+                            elif harmony_tools:   # harmony content is already channel-filtered
+                                cd = content_all[content_sent:]
                             else:   # hold back a suffix that may still become a call marker
                                 cd = content_all[content_sent:len(content_all) if fin else tp.safe_len(content_all)]
                         elif tp is not None:
-                            cd = ""
+                            cd = content_all[content_sent:] if harmony_tools else ""
                         content_sent += len(cd)
+                        cd = strip_special(cd, specials)
                         if cd or not d:
                             d["content"] = cd
                         if first:
                             d["role"] = "assistant"
                         finish = None
                         if fin and calls_started:
-                            _, calls = tp.parse(content_all)
+                            _, calls = tp.parse(raw_all if harmony_tools else content_all)
                             if calls:
                                 d["tool_calls"] = [{"index": k, **c} for k, c in enumerate(calls)]
                                 finish = "tool_calls"
                             elif content_all[content_sent:]:   # not a call after all: release the text
-                                d["content"] = d.get("content", "") + content_all[content_sent:]
+                                d["content"] = d.get("content", "") + strip_special(content_all[content_sent:],
+                                                                                    specials)
                         choice = {"index": 0, "delta": d, "finish_reason": None}
                         chunk_obj = "chat.completion.chunk"
                         if finish:
                             choice["_finish"] = finish
                     else:
-                        choice = {"index": 0, "text": delta, "finish_reason": None}
+                        choice = {"index": 0, "text": strip_special(delta, specials), "finish_reason": None}
                         chunk_obj = "text_completion"
                     first = False
                     forced = choice.pop("_finish", None)
                     if fin:
-                        choice["finish_reason"] = forced or ("stop" if cut is not None else _finish(req))
+                        choice["finish_reason"] = forced or ("stop" if stopped else _finish(req))
                     out = {"id": rid, "object": chunk_obj, "created": int(time.time()), "model": model_name,
                            "choices": [choice]}
                     if fin and (body.get("stream_options") or {}).get("include_usage", True):
@@ -421,17 +438,18 @@ def create_app(engine, ns=None):
                 yield "data: [DONE]\n\n"
 
             return StreamingResponse(gen(), media_type="text/event-stream")
+        stopped = False
         while True:
             _, fin = await stream.q.get()
-            if stops:
-                cut = _stop_hit(tok.decode(req.output_ids), stops)
-                if cut is not None:
+            if stopm.stops:
+                _, stopped = pull(fin)
+                if stopped:
                     engine.abort(req.rid)
                     break
             if fin:
                 break
-        text = tok.decode(req.output_ids)
-        cut = _stop_hit(text, stops)
+        text = tok.decode(req.output_ids, skip_special=not raw_mode)
+        cut = stopm.find(text, len(text))
         reason = _finish(req)
         if cut is not None:
             text, reason = text[:cut], "stop"
@@ -439,14 +457,17 @@ def create_app(engine, ns=None):
             msg: dict = {"role": "assistant", "content": text}
             if use_reason:
                 r, msg["content"] = ReasoningParser(reason_kind).split(text)
-                msg["reasoning_content"] = r
+                msg["reasoning_content"] = strip_special(r, specials)
             if use_tools:
-                content, calls = ToolParser(tool_kind).parse(msg["content"])
+                # the tool parser sees the raw output: harmony calls live in the commentary
+                # channel, which the reasoning split above does not keep
+                content, calls = ToolParser(tool_kind).parse(text if harmony_tools else msg["content"])
                 if calls:
                     msg["content"], msg["tool_calls"], reason = content or None, calls, "tool_calls"
+            msg["content"] = strip_special(msg["content"], specials)
             choice = {"index": 0, "message": msg, "finish_reason": reason}
         else:
-            choice = {"index": 0, "text": text, "finish_reason": reason, "logprobs": None}
+            choice = {"index": 0, "text": strip_special(text, specials), "finish_reason": reason, "logprobs": None}
         if params.logprobs:
             choice["logprobs"] = _logprobs(req, chat)
         return {"id": rid, "object": obj, "created": int(time.time()), "model": model_name, "choices": [choice],

@@ -37,6 +37,9 @@ class ByteTokenizer:
                 out.extend(f"<{i}>".encode())
         return out.decode("utf-8", errors="replace")
 
+    def special_strings(self) -> list[str]:
+        return [f"<{i}>" for i in range(3)]
+
     def apply_chat_template(self, messages: list[dict], add_generation_prompt: bool = True, tools=None) -> str:
         parts = []
         if tools:
@@ -85,6 +88,12 @@ class HFTokenizer:
 
     def decode(self, ids, skip_special: bool = True) -> str:
         return self.tok.decode([int(i) for i in ids], skip_special_tokens=skip_special)
+
+    def special_strings(self) -> list[str]:
+        try:
+            return [t.content for t in self.tok.get_added_tokens_decoder().values() if t.special]
+        except AttributeError:  # older tokenizers releases
+            return []
 
     def apply_chat_template(self, messages: list[dict], add_generation_prompt: bool = True, tools=None) -> str:
         if self.chat_template:
