@@ -802,19 +802,31 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
 // ------------------------------------------------------------------------------------------
 constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
 
-template <int SUB, int F>
+// SPLIT: the item's key range is cut into chunks of `chunk` keys run by separate workgroups
+// (items4 = {seq, row0, chunk start, part}; part < 0 = the only chunk, written as final output).
+// A short prefill (a few hundred keys per row) otherwise leaves most CUs idle and every
+// workgroup latency-bound on its serial chain of K/V tile loads; partial (O, m, l) per part go
+// to fp32 workspaces and prefill_combine_kernel merges them.
+template <int SUB, int F, bool SPLIT>
 __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
     bf16* __restrict__ out, int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale,
-    const float* __restrict__ sinks, const int* __restrict__ row_hi) {
+    const float* __restrict__ sinks, const int* __restrict__ row_hi, int chunk, float* __restrict__ part_o,
+    float* __restrict__ part_ml) {
   constexpr int D = 128, P = 16, NB = D / 16, KS = D / 32;
   typedef typename KVRaw<F>::K8 Raw8;  // 8 consecutive cache elements
   __shared__ __attribute__((aligned(16))) bf16 sK[2][SUB][32 * PF_KLD];
   __shared__ __attribute__((aligned(16))) bf16 sV[2][SUB][D * PF_VLD];
-  const int2 it = items[blockIdx.x];
-  const int s = it.x, r0_item = it.y;
+  int s, r0_item, c_lo = 0, part = -1;
+  if constexpr (SPLIT) {
+    const int4 it4 = reinterpret_cast<const int4*>(items)[blockIdx.x];
+    s = it4.x, r0_item = it4.y, c_lo = it4.z, part = it4.w;
+  } else {
+    const int2 it = items[blockIdx.x];
+    s = it.x, r0_item = it.y;
+  }
   const int kvh = blockIdx.y;
   const int q0 = cu_q[s];
   const int q_len = cu_q[s + 1] - q0;
@@ -828,9 +840,13 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   const int head = kvh * G + hl;
   const int r0 = r0_item + 32 * rblk;
   const int item_hi = min(r0_item + rows_per_item, q_len);
-  const int kv_end = row_hi ? kv_len : min(kv_len, prefix + item_hi);
+  int kv_end = row_hi ? kv_len : min(kv_len, prefix + item_hi);
   int kv_lo = 0;
   kv_lo = attn_lo(prefix + r0_item, window) & ~31;
+  if constexpr (SPLIT) {   // chunk starts are multiples of 64 keys: kv_lo stays 32-aligned
+    kv_lo = max(kv_lo, c_lo);
+    kv_end = min(kv_end, c_lo + chunk);
+  }
   const int* bt = block_tables + (int64_t)s * bt_stride;
   const int64_t kpage = (int64_t)Hkv * P * D;
 
@@ -853,8 +869,11 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
 
   // ---- cooperative tile staging: per 32-key subtile, 2 x 8 elements of K and 2 x 8 of V per
   // thread; a pipeline stage is SUB subtiles (32*SUB keys), so SUB x more bytes are in flight ----
-  Raw8 rk[SUB][2], rv[SUB][2];
-  auto load_tile = [&](int kb0) {
+  // Two register stages (A, B) in flight: a tile's global loads are issued two compute phases
+  // before its LDS write, so each load has ~2 x (64 MFMA + softmax) per wave to land.  With one
+  // stage the loop was latency-bound at ~3.9 us per 64-key step (profiles/r03_prefill_*).
+  Raw8 rkA[SUB][2], rvA[SUB][2], rkB[SUB][2], rvB[SUB][2];
+  auto load_tile = [&](Raw8 (&rk)[SUB][2], Raw8 (&rv)[SUB][2], int kb0) {
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       const int kb = kb0 + 32 * u;
@@ -873,7 +892,7 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
       }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](const Raw8 (&rk)[SUB][2], const Raw8 (&rv)[SUB][2], int buf) {
 #pragma unroll
     for (int u = 0; u < SUB; ++u)
 #pragma unroll
@@ -891,90 +910,114 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
       }
   };
 
-  int kb = kv_lo;
-  if (kb < kv_end) {
-    load_tile(kb);
-    store_tile(0);
-  }
-  __syncthreads();
-  int buf = 0;
   const bool active = r0 < q_len;  // a wave whose rows are all past q_len still stages tiles
-  for (; kb < kv_end; kb += 32 * SUB) {
-    const bool more = kb + 32 * SUB < kv_end;
-    if (more) load_tile(kb + 32 * SUB);
+  auto compute = [&](int buf, int kb) {
+    if (!active) return;
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
-    const int kbu = kb + 32 * u;
-    if (active && kbu < kv_end) {
-      f32x4 sc[2][2];
+      const int kbu = kb + 32 * u;
+      if (kbu < kv_end) {
+        f32x4 sc[2][2];
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) sc[rb][0] = sc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int rb = 0; rb < 2; ++rb) sc[rb][0] = sc[rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[buf][u][n * PF_KLD + 32 * ks + 8 * g]);
-        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[buf][u][(16 + n) * PF_KLD + 32 * ks + 8 * g]);
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[buf][u][n * PF_KLD + 32 * ks + 8 * g]);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[buf][u][(16 + n) * PF_KLD + 32 * ks + 8 * g]);
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            sc[rb][0] = mfma16(a0, qf[rb][ks], sc[rb][0]);
+            sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
+          }
+        }
+        const bool need_mask =
+            (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0 || window < -1);
+        bf16x8 pb[2];
+        float alpha[2];
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
-          sc[rb][0] = mfma16(a0, qf[rb][ks], sc[rb][0]);
-          sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
-        }
-      }
-      const bool need_mask = (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0 || window < -1);
-      bf16x8 pb[2];
-      float alpha[2];
+          const int qpos = prefix + r0 + 16 * rb + n;
+          const int qlim = row_hi ? max(qpos, row_hi[q0 + min(r0 + 16 * rb + n, q_len - 1)]) : qpos;
+          float mt = OME_NEG_INF;
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) {
-        const int qpos = prefix + r0 + 16 * rb + n;
-        const int qlim = row_hi ? max(qpos, row_hi[q0 + min(r0 + 16 * rb + n, q_len - 1)]) : qpos;
-        float mt = OME_NEG_INF;
+          for (int X = 0; X < 2; ++X)
 #pragma unroll
-        for (int X = 0; X < 2; ++X)
+            for (int i = 0; i < 4; ++i) {
+              float v = scl(sc[rb][X][i]);
+              const int key = kbu + 16 * X + 4 * g + i;
+              if (al != 0.f) v += al * (float)(key - qpos);
+              if (need_mask) {
+                const bool ok = key <= qlim && key < kv_len && key >= attn_lo(qpos, window);
+                v = ok ? v : OME_NEG_INF;
+              }
+              sc[rb][X][i] = v;
+              mt = fmaxf(mt, v);
+            }
+          mt = fmaxf(mt, __shfl_xor(mt, 16));
+          mt = fmaxf(mt, __shfl_xor(mt, 32));
+          const float m_new = fmaxf(m_i[rb], mt);
+          const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
+          alpha[rb] = fast_exp2(m_i[rb] - m_use);
+          float rs = 0.f;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            float v = scl(sc[rb][X][i]);
-            const int key = kbu + 16 * X + 4 * g + i;
-            if (al != 0.f) v += al * (float)(key - qpos);
-            if (need_mask) {
-              const bool ok = key <= qlim && key < kv_len && key >= attn_lo(qpos, window);
-              v = ok ? v : OME_NEG_INF;
-            }
-            sc[rb][X][i] = v;
-            mt = fmaxf(mt, v);
+            const float p0 = fast_exp2(sc[rb][0][i] - m_use), p1 = fast_exp2(sc[rb][1][i] - m_use);
+            pb[rb][i] = (bf16)p0;
+            pb[rb][4 + i] = (bf16)p1;
+            rs += p0 + p1;
           }
-        mt = fmaxf(mt, __shfl_xor(mt, 16));
-        mt = fmaxf(mt, __shfl_xor(mt, 32));
-        const float m_new = fmaxf(m_i[rb], mt);
-        const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
-        alpha[rb] = fast_exp2(m_i[rb] - m_use);
-        float rs = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p0 = fast_exp2(sc[rb][0][i] - m_use), p1 = fast_exp2(sc[rb][1][i] - m_use);
-          pb[rb][i] = (bf16)p0;
-          pb[rb][4 + i] = (bf16)p1;
-          rs += p0 + p1;
+          rs += __shfl_xor(rs, 16);
+          rs += __shfl_xor(rs, 32);
+          l_i[rb] = l_i[rb] * alpha[rb] + rs;
+          m_i[rb] = m_new;
         }
-        rs += __shfl_xor(rs, 16);
-        rs += __shfl_xor(rs, 32);
-        l_i[rb] = l_i[rb] * alpha[rb] + rs;
-        m_i[rb] = m_new;
-      }
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sV[buf][u][(16 * nb + n) * PF_VLD + 8 * g]);
+        for (int nb = 0; nb < NB; ++nb) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sV[buf][u][(16 * nb + n) * PF_VLD + 8 * g]);
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb) {
-          o[rb][nb] = o[rb][nb] * alpha[rb];
-          o[rb][nb] = mfma16(a, pb[rb], o[rb][nb]);
+          for (int rb = 0; rb < 2; ++rb) {
+            o[rb][nb] = o[rb][nb] * alpha[rb];
+            o[rb][nb] = mfma16(a, pb[rb], o[rb][nb]);
+          }
         }
       }
     }
-    }
-    if (more) store_tile(buf ^ 1);
+  };
+
+  constexpr int STEP = 32 * SUB;
+  int kb = kv_lo;
+  if (kb < kv_end) {
+    load_tile(rkA, rvA, kb);
+    if (kb + STEP < kv_end) load_tile(rkB, rvB, kb + STEP);
+    store_tile(rkA, rvA, 0);
+  }
+  __syncthreads();
+  if (kb + 2 * STEP < kv_end) load_tile(rkA, rvA, kb + 2 * STEP);
+  // invariant at the top: LDS buf 0 = tile kb, registers B = tile kb + STEP, A = tile kb + 2 STEP
+  for (; kb < kv_end; kb += 2 * STEP) {
+    compute(0, kb);
+    if (kb + STEP < kv_end) store_tile(rkB, rvB, 1);
     __syncthreads();
-    buf ^= 1;
+    if (kb + STEP >= kv_end) break;
+    if (kb + 3 * STEP < kv_end) load_tile(rkB, rvB, kb + 3 * STEP);
+    compute(1, kb + STEP);
+    if (kb + 2 * STEP < kv_end) store_tile(rkA, rvA, 0);
+    __syncthreads();
+    if (kb + 4 * STEP < kv_end) load_tile(rkA, rvA, kb + 4 * STEP);
   }
   if (!active) return;
+  if (SPLIT && part >= 0) {   // unnormalised partial: O^T rows of this wave + (m, l) per row
+    const int64_t pw = ((int64_t)part * Hkv + kvh) * 4 + wave;
+    float* po = part_o + pw * 32 * D;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int row = 16 * rb + n;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) *reinterpret_cast<f32x4*>(po + row * D + 16 * nb + 4 * g) = o[rb][nb];
+      if (g == 0) *reinterpret_cast<float2*>(part_ml + (pw * 32 + row) * 2) = make_float2(m_i[rb], l_i[rb]);
+    }
+    return;
+  }
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
     const int r = r0 + 16 * rb + n;
@@ -993,6 +1036,47 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   }
 }
 
+// Merge the split-KV partials of paged_prefill_v2_kernel<SPLIT>: comb = {seq, row0, first part,
+// parts}.  grid (4 x combine items, Hq): block = 8 query rows x 32 lanes of 4 dims for one head,
+// every thread independent (no serial row loop), part loop unrolled so loads overlap.
+__global__ __launch_bounds__(256) void prefill_combine_kernel(const int4* __restrict__ comb,
+                                                              const int* __restrict__ cu_q,
+                                                              const float* __restrict__ part_o,
+                                                              const float* __restrict__ part_ml,
+                                                              bf16* __restrict__ out, int64_t out_stride, int Hkv,
+                                                              float v_scale, const float* __restrict__ sinks) {
+  constexpr int D = 128;
+  const int4 c = comb[blockIdx.x >> 2];
+  const int s = c.x, p0 = c.z, np = c.w;
+  const int head = blockIdx.y, kvh = head >> 2, w = head & 3;
+  const int r = 8 * (blockIdx.x & 3) + (threadIdx.x >> 5), quad = threadIdx.x & 31;
+  const int q0 = cu_q[s], q_len = cu_q[s + 1] - q0;
+  const int row = c.y + r;
+  if (row >= q_len) return;
+  const float sink = sinks ? sinks[head] * 1.4426950408889634f : OME_NEG_INF;
+  auto pw_of = [&](int p) -> int64_t { return ((int64_t)(p0 + p) * Hkv + kvh) * 4 + w; };
+  float M = sink;
+#pragma unroll 4
+  for (int p = 0; p < np; ++p) M = fmaxf(M, part_ml[(pw_of(p) * 32 + r) * 2]);
+  const float Mu = M == OME_NEG_INF ? 0.f : M;
+  float L = sinks ? fast_exp2(sink - Mu) : 0.f;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int p = 0; p < np; ++p) {
+    const int64_t pw = pw_of(p);
+    const float2 ml = *reinterpret_cast<const float2*>(part_ml + (pw * 32 + r) * 2);
+    const f32x4 ov = *reinterpret_cast<const f32x4*>(part_o + (pw * 32 + r) * D + 4 * quad);
+    const float wt = fast_exp2(ml.x - Mu);
+    L += wt * ml.y;
+    acc += wt * ov;
+  }
+  const float inv = L > 0.f ? v_scale / L : 0.f;
+  bf16x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = (bf16)(acc[i] * inv);
+  *reinterpret_cast<bf16x4*>(out + (int64_t)(q0 + row) * out_stride + (int64_t)head * D + 4 * quad) = v;
+}
+
 template <int D, int F>
 static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, const void* q, int64_t q_stride,
                            const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
@@ -1002,9 +1086,10 @@ static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, co
   typedef typename KVStore<F>::T T;
   if constexpr (D == 128) {
     if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
-      paged_prefill_v2_kernel<2, F><<<grid, 256, 0, stream>>>(
+      paged_prefill_v2_kernel<2, F, false><<<grid, 256, 0, stream>>>(
           (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi);
+          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi, 0, nullptr,
+          nullptr);
       return;
     }
   }
@@ -1052,5 +1137,36 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
   else prefill_dispatch<128>(ARGS);
 #undef ARGS
   OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// Split-KV prefill (D = 128, P = 16, G = Hq / Hkv = 4, no row_hi): items4 [n_items][4], comb
+// [n_comb][4]; part_o [parts][Hkv][4][32][128] and part_ml [parts][Hkv][4][32][2] fp32 workspaces.
+OME_API int ome_paged_prefill_split(const void* q, int64_t q_stride, const void* k_cache, const void* v_cache,
+                                    const int* block_tables, int bt_stride, const int* cu_q, const int* kv_lens,
+                                    const int* items4, int n_items, const int* comb, int n_comb, int chunk,
+                                    void* part_o, void* part_ml, void* out, int64_t out_stride, int Hq, int Hkv,
+                                    float scale, int window, int kv_fmt, float k_scale, float v_scale, float softcap,
+                                    const float* sinks, const float* alibi, hipStream_t stream) {
+  if (n_items <= 0) return 0;
+  if (Hq != 4 * Hkv || chunk % 64 || kv_fmt < 0 || kv_fmt > 2) return -2;
+  const Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
+  dim3 grid(n_items, Hkv);
+#define OME_PFS(F)                                                                                             \
+  paged_prefill_v2_kernel<2, F, true><<<grid, 256, 0, stream>>>(                                               \
+      (const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache, (const typename KVStore<F>::T*)v_cache, \
+      block_tables, bt_stride, cu_q, kv_lens, (const int2*)items4, (bf16*)out, out_stride, Hq, Hkv, scl, window,  \
+      v_scale, sinks, nullptr, chunk, (float*)part_o, (float*)part_ml)
+  if (kv_fmt == KV_BF16) OME_PFS(KV_BF16);
+  else if (kv_fmt == KV_E4M3) OME_PFS(KV_E4M3);
+  else OME_PFS(KV_E5M2);
+#undef OME_PFS
+  OME_CHECK_LAUNCH();
+  if (n_comb > 0) {
+    prefill_combine_kernel<<<dim3(4 * n_comb, Hq), 256, 0, stream>>>((const int4*)comb, cu_q, (const float*)part_o,
+                                                                  (const float*)part_ml, (bf16*)out, out_stride, Hkv,
+                                                                  v_scale, sinks);
+    OME_CHECK_LAUNCH();
+  }
   return 0;
 }

@@ -680,6 +680,63 @@ def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) ->
     return [(s, r) for _, s, r in items]
 
 
+class PrefillPlan:
+    """Work decomposition of one prefill attention call, built host-side by
+    :func:`prefill_plan` and uploaded with the step's other inputs.  ``items`` is the classic
+    [n, 2] (seq, row0) list; ``split`` [n4, 4] (seq, row0, chunk start, part) and ``comb``
+    [nc, 4] (seq, row0, first part, parts) are the split-KV form (empty when nothing splits)."""
+
+    __slots__ = ("items", "split", "comb", "chunk", "parts")
+
+    def __init__(self, items, split, comb, chunk: int, parts: int):
+        self.items, self.split, self.comb, self.chunk, self.parts = items, split, comb, chunk, parts
+
+    @property
+    def shape(self):
+        return self.items.shape
+
+
+PREFILL_SPLIT_TARGET = int(os.environ.get("OME_PREFILL_SPLIT_ITEMS", "128"))
+
+
+def prefill_plan(q_lens: list[int], kv_lens: list[int], tile: int = 32, target: int | None = None,
+                 kv_heads: int = 8, force: bool = False):
+    """(classic items, split items, combine items, chunk, parts) for the split-KV prefill kernel.
+
+    A short prefill leaves most CUs idle and each workgroup latency-bound on its serial chain of
+    32-key K/V tile loads (profiles/r03_*: 43 us per layer for ~700 rows x <= 480 keys).  Items
+    whose key range exceeds ``chunk`` keys are cut into chunks run by separate workgroups (then
+    merged); ``chunk`` (a multiple of 64, >= 128) grows with the total work so that about
+    ``target`` split items exist -- long prompts already have plenty of items and stay unsplit.
+    Measured (profiles/r03_prefill_split_bench.txt): splitting pays when the classic grid is
+    smaller than the chip (items x kv heads < 256 workgroups) AND some item has a long key range
+    (> 512 keys), e.g. 256 new rows over a 4096-token prefix 243 -> 68 us; at ~900 rows over
+    <= 480 keys the classic grid is already full and splitting costs the partial round trip."""
+    target = target or PREFILL_SPLIT_TARGET
+    items = prefill_work_items(q_lens, kv_lens, tile)
+    work = 0
+    ends = []
+    for s, r in items:
+        e = (kv_lens[s] - q_lens[s]) + min(r + tile, q_lens[s])
+        ends.append(e)
+        work += e
+    if not force and (len(items) * kv_heads >= 256 or max(ends, default=0) <= 512):
+        return items, [], [], 0, 0
+    chunk = max(128, -(-(-(-work // max(1, target))) // 64) * 64)
+    split, comb, parts = [], [], 0
+    for (s, r), e in zip(items, ends):
+        n = -(-e // chunk)
+        if n <= 1:
+            split.append((s, r, 0, -1))
+            continue
+        comb.append((s, r, parts, n))
+        split.extend((s, r, c * chunk, parts + c) for c in range(n))
+        parts += n
+    if not comb:
+        split = []
+    return items, split, comb, chunk, parts
+
+
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale, window: int = -1,
                   out=None, k_scale: float = 1.0, v_scale: float = 1.0, softcap: float = 0.0,
                   sinks: torch.Tensor | None = None, alibi: torch.Tensor | None = None,
@@ -698,6 +755,19 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     Tq, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     out = torch.empty_like(q) if out is None else out
+    if isinstance(items, PrefillPlan):
+        plan, items = items, items.items
+        if (plan.parts and D == 128 and P == 16 and Hq == 4 * Hkv and row_hi is None and
+                os.environ.get("OME_PREFILL_ATTN", "2") == "2"):
+            po = torch.empty(plan.parts * Hkv * 4 * 32 * 128, dtype=torch.float32, device=q.device)
+            pml = torch.empty(plan.parts * Hkv * 4 * 32 * 2, dtype=torch.float32, device=q.device)
+            call("ome_paged_prefill_split", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                 _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(),
+                 _i32(kv_lens).data_ptr(), plan.split.data_ptr(), plan.split.shape[0], plan.comb.data_ptr(),
+                 plan.comb.shape[0], int(plan.chunk), po.data_ptr(), pml.data_ptr(), out.data_ptr(), out.stride(0),
+                 Hq, Hkv, float(scale), int(window), kv_format(k_cache), float(k_scale), float(v_scale),
+                 float(softcap), _sinks(sinks), _sinks(alibi), stream_ptr())
+            return out
     call("ome_paged_prefill", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
          _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),

@@ -441,8 +441,9 @@ class ModelRunner:
                 ids[t0 + n - 1] = 0
                 any_pending = True
             last_row[i] = len(ids) - 1
-        items = ops.prefill_work_items(q_lens, kv_lens) if q_lens else []
+        items, split, comb, chunk, parts = ops.prefill_plan(q_lens, kv_lens, kv_heads=self.model.tp.hkv) if q_lens else ([], [], [], 0, 0)
         T, S, n_it, nd, B = len(ids), len(q_lens), len(items), len(dec_lens), len(chunks)
+        n_sp, n_cb = len(split), len(comb)
         cu = np.zeros(S + 1, dtype=np.int32)
         cu[1:] = np.cumsum(q_lens)
         dec_order = np.argsort(-np.asarray(dec_lens, np.int64), kind="stable").astype(np.int32) if nd else \
@@ -463,7 +464,9 @@ class ModelRunner:
                                  cu, np.asarray(kv_lens, np.int32), np.asarray(req_idx, np.int32),
                                  np.asarray(last_row, np.int32), np.asarray(src, np.int32),
                                  np.asarray(dec_lens, np.int32), np.asarray(dec_req, np.int32), dec_order,
-                                 np.asarray(items, np.int32).reshape(-1) if n_it else np.zeros(0, np.int32)])
+                                 np.asarray(items, np.int32).reshape(-1) if n_it else np.zeros(0, np.int32),
+                                 np.asarray(split, np.int32).reshape(-1) if n_sp else np.zeros(0, np.int32),
+                                 np.asarray(comb, np.int32).reshape(-1) if n_cb else np.zeros(0, np.int32)])
         host = torch.from_numpy(packed)
         if self.is_cuda:
             host = host.pin_memory()
@@ -484,6 +487,9 @@ class ModelRunner:
         t_src = take(T)
         t_dlen, t_dreq, t_dord = take(nd), take(nd), take(nd)
         t_items = take(2 * n_it).view(n_it, 2)
+        if n_sp:   # split-KV prefill attention (ops.prefill_plan)
+            t_items = ops.PrefillPlan(t_items, take(4 * n_sp).view(n_sp, 4), take(4 * n_cb).view(n_cb, 4), chunk,
+                                      parts)
         if any_pending:
             ops.fill_pending(t_ids, t_src, prev.ids_dev)
         ws = None

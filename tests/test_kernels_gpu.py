@@ -159,6 +159,34 @@ def test_paged_prefill(Hq, Hkv, q_lens, kv_lens, variant, monkeypatch):
     _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884), atol=2e-2)
 
 
+def _plan(q_lens, kv_lens, target):
+    items, split, comb, chunk, parts = ops.prefill_plan(q_lens, kv_lens, target=target, force=True)
+    t = lambda a, c: torch.tensor(a, dtype=torch.int32, device=DEV).view(-1, c)  # noqa: E731
+    return ops.PrefillPlan(t(items, 2), t(split, 4) if split else None, t(comb, 4) if comb else None, chunk, parts)
+
+
+@pytest.mark.parametrize("window", [-1, 100])
+@pytest.mark.parametrize("sinks", [False, True])
+@pytest.mark.parametrize("target", [32, 128, 4096])
+def test_paged_prefill_split_kv(window, sinks, target):
+    """Split-KV prefill (chunks of the key range on separate workgroups, merged by the combine
+    kernel) == the fp32 reference, with prefixes, short and long rows, windows and sinks."""
+    D, P, Hq, Hkv = 128, 16, 32, 8
+    q_lens, kv_lens = [480, 37, 1, 300, 700], [480, 600, 900, 300, 1400]
+    npages = sum(-(-L // P) for L in kv_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    bt = _block_tables(kv_lens, P, npages)
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    plan = _plan(q_lens, kv_lens, target)
+    if target >= 128:
+        assert plan.parts > 0, "expected a split plan"
+    q = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    sk = torch.randn(Hq, device=DEV) if sinks else None
+    out = ops.paged_prefill(q, kc, vc, bt, cu, kl, plan, 0.0884, window=window, sinks=sk)
+    _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884, window, 1.0, 1.0, 0.0, sk), atol=2e-2)
+
+
 @pytest.mark.parametrize("window", [100, -128, -48])
 @pytest.mark.parametrize("variant", ["1", "2"])
 def test_paged_prefill_window(window, variant, monkeypatch):
