@@ -7,6 +7,7 @@ from __future__ import annotations
 import os
 
 import torch
+import torch.nn.functional as F
 
 from . import reference as ref
 from ._native import NativeError, available, call, ptr, stream_ptr  # noqa: F401
@@ -264,9 +265,18 @@ def fp8_gemm(qa, sa, qw, sw, block: int = 0, bias=None, out: torch.Tensor | None
     assert qw.shape[1] == K and qa.is_contiguous() and qw.is_contiguous()
     if out is None:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=qa.device)
+    if N % 256 == 0 and K % 128 == 0 and M >= FP8_MX_MIN_ROWS:
+        # 256 x 256 MX-scaled MFMA tile (csrc/kernels/gemm.hip): twice the bf16 MFMA rate
+        call("ome_fp8_gemm_mx", qa.data_ptr(), qa.stride(0), sa.data_ptr(), qw.data_ptr(), qw.stride(0),
+             sw.data_ptr(), M, N, K, block, out.data_ptr(), out.stride(0), ptr(bias), stream_ptr())
+        return out
     call("ome_fp8_gemm", qa.data_ptr(), qa.stride(0), sa.data_ptr(), qw.data_ptr(), sw.data_ptr(), M, N, K, block,
          out.data_ptr(), out.stride(0), ptr(bias), stream_ptr())
     return out
+
+
+# rows from which the dense fp8 GEMM uses the 256 x 256 MX tile (smaller M: the 64 x 64 kernel)
+FP8_MX_MIN_ROWS = int(os.environ.get("OME_FP8_MX_MIN_ROWS", "65"))
 
 
 def fp8_linear(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0, bias=None) -> torch.Tensor:
@@ -678,6 +688,49 @@ def prefill_work_items(q_lens: list[int], kv_lens: list[int], tile: int = 32) ->
             items.append((pre + min(r + tile, ql), s, r))
     items.sort(key=lambda x: -x[0])
     return [(s, r) for _, s, r in items]
+
+
+def gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, epi: int = 0, splits: int = 1,
+         ws: torch.Tensor | None = None) -> torch.Tensor:
+    """``csrc/kernels/gemm.hip``: out = x @ w.T (bf16, fp32 accumulate) on a 256 x 256 MFMA tile.
+    ``epi=2``: w holds gate/up rows interleaved in 16-row blocks (:func:`interleave_gate_up`) and
+    out = SiLU(gate) * up ([M, N/2]).  ``splits`` > 1 splits K over workgroups (fp32 slabs in
+    ``ws`` + a reduce launch).  Requires N % 256 == 0, K % (64 * splits) == 0."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not _gpu(x):
+        y = x.float() @ w.float().t()
+        if epi == 2:
+            g, u = deinterleave_gate_up(y)
+            y = F.silu(g) * u
+        y = y.to(x.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == 2 else N, dtype=x.dtype, device=x.device)
+    if splits > 1 and ws is None:
+        ws = torch.empty(splits * M * N, dtype=torch.float32, device=x.device)
+    call("ome_gemm", x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), out.data_ptr(), out.stride(0), M, N, K,
+         epi, splits, None if ws is None else ws.data_ptr(), stream_ptr())
+    return out
+
+
+def interleave_gate_up(w_gu: torch.Tensor, block: int = 16) -> torch.Tensor:
+    """[2I, H] (gate rows, then up rows) -> rows in blocks of ``block`` gate / ``block`` up, the
+    layout of gemm(..., epi=2)."""
+    two_i, H = w_gu.shape
+    i = two_i // 2
+    g, u = w_gu[:i].view(i // block, block, H), w_gu[i:].view(i // block, block, H)
+    return torch.stack([g, u], 1).reshape(two_i, H).contiguous()
+
+
+def deinterleave_gate_up(y: torch.Tensor, block: int = 16):
+    """Columns of a product with an interleaved gate/up weight -> (gate, up)."""
+    M, N = y.shape
+    v = y.view(M, N // (2 * block), 2, block)
+    return v[:, :, 0].reshape(M, N // 2), v[:, :, 1].reshape(M, N // 2)
 
 
 class PrefillPlan:

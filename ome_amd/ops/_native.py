@@ -58,6 +58,9 @@ _SIGNATURES = {
         "ome_skinny_gemm": [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp, vp],
         "ome_stream_gemm": [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp],
         "ome_gemv": [vp, i64, vp, vp, vp, i64, i32, i32, i32, vp],
+        "ome_gemm": [vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, i32, vp, vp],
+        "ome_gemm_set_variant": [i32],
+        "ome_fp8_gemm_mx": [vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, vp, i64, vp, vp],
         "ome_fp8_quant": [vp, i64, i32, i32, vp, vp, i32, vp],
         "ome_fp8_gemm": [vp, i64, vp, vp, vp, i32, i32, i32, i32, vp, i64, vp, vp],
         "ome_sample": [vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, u64, vp, vp, vp],

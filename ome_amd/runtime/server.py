@@ -371,8 +371,11 @@ def create_app(engine, ns=None):
                 rp = ReasoningParser(reason_kind) if use_reason else None
                 tp = ToolParser(tool_kind) if use_tools else None
                 content_all, content_sent, calls_started, raw_all = "", 0, False, ""
+                every_usage = bool((body.get("stream_options") or {}).get("continuous_usage_stats"))
                 while True:
                     _, fin = await stream.q.get()
+                    while not fin and not stream.q.empty():   # coalesce steps the loop fell behind on
+                        _, fin = stream.q.get_nowait()
                     delta, stopped = pull(fin)
                     if stopped:
                         fin = True
@@ -430,7 +433,7 @@ def create_app(engine, ns=None):
                         choice["finish_reason"] = forced or ("stop" if stopped else _finish(req))
                     out = {"id": rid, "object": chunk_obj, "created": int(time.time()), "model": model_name,
                            "choices": [choice]}
-                    if fin and (body.get("stream_options") or {}).get("include_usage", True):
+                    if every_usage or (fin and (body.get("stream_options") or {}).get("include_usage", True)):
                         out["usage"] = usage()
                     yield f"data: {json.dumps(out)}\n\n"
                     if fin:

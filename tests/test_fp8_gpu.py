@@ -27,7 +27,7 @@ def test_fp8_quant(group, M, K):
 
 @pytest.mark.parametrize("block", [0, 128])
 @pytest.mark.parametrize("M,N,K", [(1, 64, 128), (5, 6144, 4096), (64, 128, 256), (257, 4096, 14336),
-                                   (1000, 512, 1024)])
+                                   (1000, 512, 1024), (700, 6144, 4096), (129, 768, 384), (66, 256, 128)])
 def test_fp8_gemm(block, M, N, K):
     torch.manual_seed(1)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
