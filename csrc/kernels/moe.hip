@@ -510,3 +510,176 @@ OME_API int ome_moe_combine(const void* Y, const float* w, const int* inv, int n
   OME_CHECK_LAUNCH();
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------
+// FP8 block-scaled grouped GEMM (DeepSeek-V3 / Kimi-K2 `quantization: fp8` experts, SURVEY.md
+// §2.9 K11): out[p, :] = dequant(A[row(p), :]) . dequant(W[e(p)])^T, A e4m3 with 1x128 group
+// scales sa[row][K/128] (row = the gathered source row), W e4m3 [E][N][K] with 128x128 block scales
+// sw[E][N/128][K/128].  The experts stay fp8 in HBM (half the bytes of the bf16 path, which is
+// what a decode-time MoE layer is bound by).  64 x 128 tile, 4 waves (2 x 2, 32 x 64 each), one
+// 128-deep K block per step = ONE v_mfma_scale_f32_16x16x128_f8f6f4 per 16 x 16 block at unit MX
+// scales (2x the bf16 MFMA rate), the block's fp32 scales applied to its product with a VALU FMA.
+// Operands go global -> LDS by global_load_lds (per-lane gathered source rows, lane-linear
+// destination, XOR-swizzled chunks), double buffered.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void moe_lds_t;
+typedef __attribute__((address_space(1))) void moe_glb_t;
+typedef int mi32x8 __attribute__((ext_vector_type(8)));
+typedef int mi32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int mswz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ mi32x8 mfrag32(const char* lds, int row, int c) {
+  const mi32x4 lo = *reinterpret_cast<const mi32x4*>(lds + row * 128 + mswz(row, 2 * c) * 16);
+  const mi32x4 hi = *reinterpret_cast<const mi32x4*>(lds + row * 128 + mswz(row, 2 * c + 1) * 16);
+  return mi32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int BMF, int BNF>
+__global__ __launch_bounds__(256) void moe_gemm_fp8_kernel(const uint8_t* __restrict__ A, int64_t lda,
+                                                           const float* __restrict__ sa, const int* __restrict__ sorted_ids,
+                                                           int gather_div, const uint8_t* __restrict__ W,
+                                                           const float* __restrict__ sw, const int* __restrict__ offsets,
+                                                           int E, int N, int K, bf16* __restrict__ out, int64_t ldo) {
+  constexpr int ABYTES = BMF * 128, WBYTES = BNF * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (ABYTES + WBYTES)];
+  __shared__ int s_tile[3];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid == 0) s_tile[0] = -1;
+  __syncthreads();
+  if (wave == 0) {   // (expert, first row) of this m-tile: prefix sum of per-expert tile counts
+    int base = 0;
+    const int y = blockIdx.y;
+    for (int e0 = 0; e0 < E; e0 += 64) {
+      const int e = e0 + lane;
+      const int nt = e < E ? (offsets[e + 1] - offsets[e] + BMF - 1) / BMF : 0;
+      int incl = nt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      const int t = y - base;
+      if (t >= incl - nt && t < incl) {
+        s_tile[0] = e;
+        s_tile[1] = offsets[e] + (t - (incl - nt)) * BMF;
+        s_tile[2] = offsets[e + 1];
+      }
+      base += __shfl(incl, 63);
+      if (y < base) break;
+    }
+  }
+  __syncthreads();
+  const int e = s_tile[0];
+  if (e < 0) return;
+  const int m0 = s_tile[1], m_end = s_tile[2];
+  const int n0 = blockIdx.x * BNF;
+  const int KB = K / 128, nt = KB;
+  const uint8_t* We = W + (int64_t)e * N * K;
+  const float* swe = sw + ((int64_t)e * (N / 128) + n0 / 128) * KB;
+  // per-lane staging sources (gathered A rows, W rows), fixed over K
+  constexpr int AI = BMF / 32, WI = BNF / 32;   // wave instructions per operand per wave (8 rows each)
+  const uint8_t* asrc[AI];
+  const uint8_t* wsrc[WI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int r = (wave * AI + j) * 8 + (lane >> 3);
+    int p = m0 + r;
+    p = p < m_end ? p : m_end - 1;
+    const int srow = gather_div > 0 ? sorted_ids[p] / gather_div : p;
+    asrc[j] = A + (int64_t)srow * lda + mswz(r, lane & 7) * 16;
+  }
+#pragma unroll
+  for (int j = 0; j < WI; ++j) {
+    const int r = (wave * WI + j) * 8 + (lane >> 3);
+    const int n = min(n0 + r, N - 1);
+    wsrc[j] = We + (int64_t)n * K + mswz(r, lane & 7) * 16;
+  }
+  auto stage = [&](int buf, int kt) {
+    char* la = smem + buf * (ABYTES + WBYTES);
+    char* lw = la + ABYTES;
+#pragma unroll
+    for (int j = 0; j < AI; ++j)
+      __builtin_amdgcn_global_load_lds((moe_glb_t*)(asrc[j] + kt * 128), (moe_lds_t*)(la + (wave * AI + j) * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int j = 0; j < WI; ++j)
+      __builtin_amdgcn_global_load_lds((moe_glb_t*)(wsrc[j] + kt * 128), (moe_lds_t*)(lw + (wave * WI + j) * 1024), 16,
+                                       0, 0);
+  };
+  const int wm = wave >> 1, wn = wave & 1;   // wave tile: rows [wm*BMF/2, +BMF/2), cols [wn*BNF/2, +BNF/2)
+  constexpr int MJ = BMF / 32, NI = BNF / 32;
+  const int fr = lane & 15, fc = lane >> 4;
+  int srow[MJ];
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) {
+    int p = m0 + wm * (BMF / 2) + j * 16 + fr;
+    p = p < m_end ? p : m_end - 1;
+    srow[j] = gather_div > 0 ? sorted_ids[p] / gather_div : p;
+  }
+  f32x4 acc[NI][MJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nt) stage(cur ^ 1, t + 1);
+    const char* la = smem + cur * (ABYTES + WBYTES);
+    const char* lw = la + ABYTES;
+    const float swv = swe[t];
+    mi32x8 xa[MJ];
+    float s[MJ];
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      xa[j] = mfrag32(la, wm * (BMF / 2) + j * 16 + fr, fc);
+      s[j] = sa[(int64_t)srow[j] * KB + t] * swv;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const mi32x8 wf = mfrag32(lw, wn * (BNF / 2) + i * 16 + fr, fc);
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        const f32x4 p = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wf, xa[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0,
+                                                                        127, 0, 127);
+        acc[i][j] += p * s[j];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // lane (fr, fc) of block (i, j): row p = m0 + wm*BMF/2 + j*16 + fr, cols n = n0 + wn*BNF/2 + i*16 + 4fc .. +3
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) {
+    const int p = m0 + wm * (BMF / 2) + j * 16 + fr;
+    if (p >= m_end) continue;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int n = n0 + wn * (BNF / 2) + i * 16 + 4 * fc;
+      if (n >= N) continue;
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (bf16)acc[i][j][r];
+      *reinterpret_cast<bf16x4*>(out + (int64_t)p * ldo + n) = v;
+    }
+  }
+}
+
+// A [rows][K] e4m3 (gathered through sorted_ids / gather_div when gather_div > 0), sa [rows][K/128];
+// W [E][N][K] e4m3, sw [E][N/128][K/128]; out [n_assign][N] bf16 in sorted order.  N % 128 == 0,
+// K % 128 == 0.  max_m_tiles: static upper bound of 64-row tiles (n_assign / 64 + E).
+OME_API int ome_moe_gemm_fp8(const void* A, int64_t lda, const float* sa, const int* sorted_ids, int gather_div,
+                             const void* W, const float* sw, const int* offsets, int E, int N, int K,
+                             int max_m_tiles, void* out, int64_t ldo, hipStream_t stream) {
+  if (max_m_tiles <= 0) return 0;
+  if (N % 128 || K % 128 || lda % 16 || ((uintptr_t)A | (uintptr_t)W) % 16) return -2;
+  if (max_m_tiles > 65535) return -3;
+  dim3 grid(N / 128, max_m_tiles);
+  moe_gemm_fp8_kernel<64, 128><<<grid, 256, 0, stream>>>((const uint8_t*)A, lda, sa, sorted_ids, gather_div,
+                                                         (const uint8_t*)W, sw, offsets, E, N, K, (bf16*)out, ldo);
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -152,12 +152,13 @@ class DeepseekForCausalLM(LlamaForCausalLM):
     def _post_load(self) -> None:
         if not self.fp8:
             return
-        from ome_amd.models.quant import quantize_weight
+        from ome_amd.models.quant import quantize_moe_experts, quantize_weight
 
         for lst in (self.w_qa, self.w_qb, self.w_o, self.w_gu, self.w_d, self.w_sgu, self.w_sd):
             for i in self.layers:
                 if self._quantizable(lst[i]):
                     lst[i] = quantize_weight(lst[i], self.fp8_block)
+        quantize_moe_experts(self)   # routed experts stay fp8 (block-scaled grouped GEMM)
 
     def _deinterleave_rows(self, w: torch.Tensor, head_dim: int, n_heads: int) -> torch.Tensor:
         """HF DeepSeek rotates interleaved (x0,x1),(x2,x3)... pairs of the rope dims; permute the
@@ -287,7 +288,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                     self.w_gu, self.w_d, self.w_router, self.w13, self.w2, self.w_sgu, self.w_sd,
                     [self.embed, self.norm, self.lm_head]):
             for t in lst:
-                if isinstance(t, Fp8Weight):
+                if isinstance(t, Fp8Weight) or hasattr(t, "nbytes") and callable(getattr(t, "nbytes", None)):
                     n += t.nbytes()
                 elif t is not None and t.data_ptr() not in seen:
                     seen.add(t.data_ptr())

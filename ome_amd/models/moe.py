@@ -71,6 +71,7 @@ class MoEForCausalLM(LlamaForCausalLM):
                 self.w_sgu[i] = self._alloc(2 * self.shared_inter, H, std=std, gen=gen)
                 self.w_sd[i] = self._alloc(H, self.shared_inter, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
                 self.w_sgate[i] = self._alloc(1, H, std=std, gen=gen)
+        self._quantize_experts()
         return self
 
     def load_hf_weights(self, weights) -> "MoEForCausalLM":
@@ -148,6 +149,7 @@ class MoEForCausalLM(LlamaForCausalLM):
         for i, d in shared.items():
             self.w_sgu[i] = put(torch.cat([rows(d["gate_proj"], SI), rows(d["up_proj"], SI)], 0))
             self.w_sd[i] = put(cols(d["down_proj"], SI))
+        self._quantize_experts()
         return self
 
     def _load_base(self, weights) -> None:
@@ -161,6 +163,14 @@ class MoEForCausalLM(LlamaForCausalLM):
             if self.w_gu[i] is placeholder:
                 self.w_gu[i] = saved[i]
 
+    def _quantize_experts(self) -> None:
+        """``quantization: fp8``: routed experts are stored as fp8 with 128x128 block scales and
+        run on the block-scaled grouped GEMM (no dequantisation to bf16 at load)."""
+        if self.fp8:
+            from ome_amd.models.quant import quantize_moe_experts
+
+            quantize_moe_experts(self)
+
     def local_experts(self, i: int) -> list[int]:
         from ome_amd.parallel import eplb
 
@@ -169,7 +179,7 @@ class MoEForCausalLM(LlamaForCausalLM):
     def weight_bytes(self) -> int:
         n = super().weight_bytes()
         for lst in (self.w_router, self.w13, self.w2, self.w_sgu, self.w_sd, self.w_sgate):
-            n += sum(t.numel() * t.element_size() for t in lst if t is not None)
+            n += sum(t.nbytes() if hasattr(t, "scale") else t.numel() * t.element_size() for t in lst if t is not None)
         return n
 
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:

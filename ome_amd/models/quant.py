@@ -45,6 +45,62 @@ class Fp8Weight:
         return ref.fp8_dequant_weight(self.q, self.scale, self.block).to(dtype)
 
 
+@dataclass
+class Fp8Experts:
+    """MoE expert weights kept in FP8 (``quantization: fp8``, 128x128 block scales): q [E, N, K]
+    float8_e4m3fn, scale [E, N/128, K/128] float32.  Consumed by ``ops.fused_moe`` through the
+    block-scaled grouped GEMM (csrc/kernels/moe.hip ``ome_moe_gemm_fp8``)."""
+    q: torch.Tensor
+    scale: torch.Tensor
+    block: int = 128
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    def nbytes(self) -> int:
+        return self.q.numel() + self.scale.numel() * 4
+
+    def dequant(self, dtype=torch.bfloat16) -> torch.Tensor:
+        return torch.stack([ref.fp8_dequant_weight(self.q[e], self.scale[e], self.block)
+                            for e in range(self.q.shape[0])]).to(dtype)
+
+    def index_select(self, dim: int, idx: torch.Tensor) -> "Fp8Experts":
+        assert dim == 0
+        return Fp8Experts(self.q.index_select(0, idx), self.scale.index_select(0, idx), self.block)
+
+
+def quantize_experts(w: torch.Tensor, block: int = 128) -> Fp8Experts:
+    """[E, N, K] bf16 -> Fp8Experts with amax/448 scales per 128x128 block of every expert
+    (N, K multiples of 128: DeepSeek-V3 2I = 4096 / H = 7168)."""
+    E, N, K = w.shape
+    if N % block or K % block:
+        raise ValueError(f"expert weight {tuple(w.shape)} is not {block}x{block}-tileable")
+    blocks = w.float().reshape(E, N // block, block, K // block, block)
+    amax = blocks.abs().amax(dim=(2, 4))
+    s = torch.where(amax > 0, amax / ref.FP8_MAX, torch.ones_like(amax))
+    q = (blocks / s[:, :, None, :, None]).clamp(-ref.FP8_MAX, ref.FP8_MAX).to(torch.float8_e4m3fn)
+    return Fp8Experts(q.reshape(E, N, K).contiguous(), s.contiguous(), block)
+
+
+def quantize_moe_experts(model) -> int:
+    """``quantization: fp8`` MoE models: turn every MoE layer's stacked expert weights (w13 / w2,
+    bf16 [E_local, N, K]) into :class:`Fp8Experts` with 128x128 block scales, so the experts are
+    stored and streamed as fp8 (no load-time dequantisation to bf16).  Returns how many stayed bf16
+    (shapes that do not tile by 128)."""
+    kept = 0
+    for i in getattr(model, "moe_layers", ()):
+        for name in ("w13", "w2"):
+            lst = getattr(model, name, None)
+            w = lst[i] if lst is not None else None
+            if isinstance(w, torch.Tensor) and w.dim() == 3 and w.numel():
+                if w.shape[1] % 128 == 0 and w.shape[2] % 128 == 0:
+                    lst[i] = quantize_experts(w)
+                else:
+                    kept += 1
+    return kept
+
+
 def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
     """bf16/fp32 [N, K] -> Fp8Weight (amax/448 scales per row, or per 128x128 block)."""
     N, K = w.shape

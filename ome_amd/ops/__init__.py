@@ -335,6 +335,8 @@ def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13
     with gathered A rows -> SiLU*mul -> grouped GEMM down -> weighted combine.  Shapes are
     static given T (graph-capturable); per-expert counts never leave the GPU.  ``gated=False``:
     w13 holds only up rows [E, I, H] and the activation is applied in place (NemotronH ReLU^2)."""
+    if hasattr(w13, "scale") and hasattr(w13, "q"):   # Fp8Experts (models/quant.py)
+        return fused_moe_fp8(x, topk_w, topk_ids, w13, w2, act, scale)
     if not _gpu(x):
         return ref.fused_moe(x, topk_w, topk_ids, w13, w2, act, scale, b13, b2, gated)
     T, H = x.shape
@@ -357,6 +359,40 @@ def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13
     tm = moe_tile_m(n, E, H)
     call("ome_moe_gemm", h.data_ptr(), h.stride(0), None, 0, w2.data_ptr(), offsets.data_ptr(), E, H, I,
          -(-n // tm) + E, y.data_ptr(), y.stride(0), ptr(b2), tm, stream_ptr())
+    out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    call("ome_moe_combine", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), float(scale),
+         stream_ptr())
+    return out
+
+
+def fused_moe_fp8(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13, w2, act: int = 0,
+                  scale: float = 1.0) -> torch.Tensor:
+    """FP8 experts (``Fp8Experts``: e4m3 + 128x128 block scales): the token rows are quantised once
+    (1x128 groups) and gathered by the grouped GEMM, the SiLU*mul output re-quantised for the down
+    projection; both grouped GEMMs are ``ome_moe_gemm_fp8`` (experts never leave fp8)."""
+    if not _gpu(x):
+        return ref.fused_moe_fp8(x, topk_w, topk_ids, w13.q, w13.scale, w2.q, w2.scale, act, scale, w13.block)
+    T, H = x.shape
+    E, I2, _ = w13.q.shape
+    I = I2 // 2
+    k = topk_ids.shape[1]
+    n = T * k
+    dev = x.device
+    offsets = torch.empty(E + 1, dtype=torch.int32, device=dev)
+    sorted_ids = torch.empty(n, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    call("ome_moe_align", topk_ids.data_ptr(), n, E, offsets.data_ptr(), sorted_ids.data_ptr(), inv.data_ptr(),
+         stream_ptr())
+    qx, sx = fp8_quant(x, 128)
+    tiles = -(-n // 64) + E
+    gu = torch.empty(n, I2, dtype=x.dtype, device=dev)
+    call("ome_moe_gemm_fp8", qx.data_ptr(), qx.stride(0), sx.data_ptr(), sorted_ids.data_ptr(), k, w13.q.data_ptr(),
+         w13.scale.data_ptr(), offsets.data_ptr(), E, I2, H, tiles, gu.data_ptr(), gu.stride(0), stream_ptr())
+    h = act_and_mul(gu, act)
+    qh, sh = fp8_quant(h, 128)
+    y = torch.empty(n, H, dtype=x.dtype, device=dev)
+    call("ome_moe_gemm_fp8", qh.data_ptr(), qh.stride(0), sh.data_ptr(), None, 0, w2.q.data_ptr(),
+         w2.scale.data_ptr(), offsets.data_ptr(), E, H, I, tiles, y.data_ptr(), y.stride(0), stream_ptr())
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     call("ome_moe_combine", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), float(scale),
          stream_ptr())

@@ -412,6 +412,24 @@ def fused_moe(x, topk_w, topk_ids, w13, w2, act: int = 0, scale: float = 1.0, b1
     return (out * scale).to(x.dtype)
 
 
+def fused_moe_fp8(x, topk_w, topk_ids, w13q, w13s, w2q, w2s, act: int = 0, scale: float = 1.0, block: int = 128):
+    """The fp8 MoE path exactly as the GPU computes it: x and the activation h are quantised to
+    e4m3 with 1x128 group scales, experts are e4m3 with 128x128 block scales, products in fp32."""
+    T, H = x.shape
+    out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
+    qx, sx = fp8_quant(x, block)
+    xd = qx.float() * sx.repeat_interleave(block, 1)
+    for e in torch.unique(topk_ids).tolist():
+        tok, slot = (topk_ids == e).nonzero(as_tuple=True)
+        gu = (xd[tok] @ fp8_dequant_weight(w13q[e], w13s[e], block).t()).to(x.dtype)
+        h = act_and_mul(gu, act)
+        qh, sh = fp8_quant(h, block)
+        hd = qh.float() * sh.repeat_interleave(block, 1)
+        y = (hd @ fp8_dequant_weight(w2q[e], w2s[e], block).t()).to(x.dtype).float()
+        out.index_add_(0, tok, y * topk_w[tok, slot].float()[:, None])
+    return (out * scale).to(x.dtype)
+
+
 SEEN_BIT = 1 << 24
 
 

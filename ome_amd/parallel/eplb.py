@@ -237,8 +237,17 @@ def rebalance_model(model) -> dict[int, float]:
 
     if getattr(model, "eplb", None) is None:
         return {}
-    ws = {i: [model.w13[i], model.w2[i]] for i in model.eplb.placement}
+    from ome_amd.models.quant import Fp8Experts
+
+    def parts(w):   # fp8 experts migrate their codes and block scales slot by slot
+        return [w.q, w.scale] if isinstance(w, Fp8Experts) else [w]
+
+    ws = {i: parts(model.w13[i]) + parts(model.w2[i]) for i in model.eplb.placement}
     res = model.eplb.rebalance(ws, pstate.get().ep_group)
-    for i, (w13, w2) in ws.items():
-        model.w13[i], model.w2[i] = w13, w2
+    for i, lst in ws.items():
+        if isinstance(model.w13[i], Fp8Experts):
+            model.w13[i] = Fp8Experts(lst[0], lst[1], model.w13[i].block)
+            model.w2[i] = Fp8Experts(lst[2], lst[3], model.w2[i].block)
+        else:
+            model.w13[i], model.w2[i] = lst
     return res

@@ -1,10 +1,14 @@
 """Microbenchmark: Llama-3-8B projection shapes, bf16 hipBLASLt vs ome_fp8_gemm (per-channel and
 128x128 block scales), including the activation-quant kernel.  Prints one line per shape."""
+import os
+import sys
+
 import torch
 import torch.nn.functional as F
 
-from ome_amd import ops
-from ome_amd.models.quant import quantize_weight
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ome_amd import ops  # noqa: E402
+from ome_amd.models.quant import quantize_weight  # noqa: E402
 
 
 def t(fn, n=50):

@@ -133,3 +133,28 @@ def test_engine_fp8_generates():
     assert isinstance(eng.runner.model.w_o[0], Fp8Weight)
     reqs = eng.generate([[5, 6, 7, 8], [9, 10]], SamplingParams(max_new_tokens=6, temperature=0.0, ignore_eos=True))
     assert all(len(r.output_ids) == 6 for r in reqs)
+
+
+def test_fp8_moe_experts_quantized_and_reference_path():
+    """quantization: fp8 on an MoE model keeps the experts fp8 (Fp8Experts, 128x128 blocks) and
+    the CPU reference path of fused_moe runs the quantised emulation."""
+    import torch
+
+    from ome_amd import ops
+    from ome_amd.models import build_model
+    from ome_amd.models.config import preset
+    from ome_amd.models.quant import Fp8Experts, quantize_experts
+
+    cfg = preset("tiny-moe")
+    cfg.quantization = "fp8"
+    m = build_model(cfg, "cpu", torch.float32, load_format="dummy", seed=1)
+    i = sorted(m.moe_layers)[0]
+    assert isinstance(m.w13[i], Fp8Experts) and m.w13[i].q.dtype == torch.float8_e4m3fn
+    w = torch.randn(4, 256, 384) * 0.05
+    q = quantize_experts(w)
+    assert q.scale.shape == (4, 2, 3)
+    assert (q.dequant(torch.float32) - w).abs().max() < 0.06 * w.abs().max()
+    x = torch.randn(5, 256)
+    tw, tid = ops.moe_route(torch.randn(5, 8), 2)
+    y = ops.fused_moe(x, tw, tid, m.w13[i], m.w2[i], 0, 1.0)
+    assert y.shape == (5, 256) and torch.isfinite(y).all()
