@@ -399,6 +399,47 @@ def fused_moe_fp8(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor,
     return out
 
 
+def moe_experts_sorted(rows: torch.Tensor, ids: torch.Tensor, w13, w2, act: int, n_experts: int):
+    """Expert MLP over already-dispatched rows (expert parallelism): ``rows`` [n, H], ``ids`` [n]
+    local expert per row, ``n_experts`` = a null id for empty slots (never computed).  Returns
+    (y [n, H] in the grouped GEMM's sorted order, inv [n] = the sorted position of row i).
+    bf16 experts or Fp8Experts; nothing leaves the device (graph-capturable)."""
+    n, H = rows.shape
+    dev = rows.device
+    E1 = n_experts + 1
+    offsets = torch.empty(E1 + 1, dtype=torch.int32, device=dev)
+    sorted_ids = torch.empty(n, dtype=torch.int32, device=dev)
+    inv = torch.empty(n, dtype=torch.int32, device=dev)
+    call("ome_moe_align", ids.data_ptr(), n, E1, offsets.data_ptr(), sorted_ids.data_ptr(), inv.data_ptr(),
+         stream_ptr())
+    y = torch.empty(n, H, dtype=rows.dtype, device=dev)
+    if hasattr(w13, "scale") and hasattr(w13, "q"):
+        I2 = w13.q.shape[1]
+        tiles = -(-n // 64) + n_experts
+        qx, sx = fp8_quant(rows, 128)
+        gu = torch.empty(n, I2, dtype=rows.dtype, device=dev)
+        call("ome_moe_gemm_fp8", qx.data_ptr(), qx.stride(0), sx.data_ptr(), sorted_ids.data_ptr(), 1,
+             w13.q.data_ptr(), w13.scale.data_ptr(), offsets.data_ptr(), n_experts, I2, H, tiles, gu.data_ptr(),
+             gu.stride(0), stream_ptr())
+        h = act_and_mul(gu, act)
+        qh, sh = fp8_quant(h, 128)
+        call("ome_moe_gemm_fp8", qh.data_ptr(), qh.stride(0), sh.data_ptr(), None, 0, w2.q.data_ptr(),
+             w2.scale.data_ptr(), offsets.data_ptr(), n_experts, H, I2 // 2, tiles, y.data_ptr(), y.stride(0),
+             stream_ptr())
+        return y, inv
+    I2 = w13.shape[1]
+    tm = moe_tile_m(n, n_experts, I2)
+    gu = torch.empty(n, I2, dtype=rows.dtype, device=dev)
+    call("ome_moe_gemm", rows.data_ptr(), rows.stride(0), sorted_ids.data_ptr(), 1, w13.data_ptr(),
+         offsets.data_ptr(), n_experts, I2, H, -(-n // tm) + n_experts, gu.data_ptr(), gu.stride(0), None, tm,
+         stream_ptr())
+    h = act_and_mul(gu, act)
+    tm = moe_tile_m(n, n_experts, H)
+    call("ome_moe_gemm", h.data_ptr(), h.stride(0), None, 0, w2.data_ptr(), offsets.data_ptr(), n_experts, H,
+         I2 // 2, -(-n // tm) + n_experts, y.data_ptr(), y.stride(0), None, tm, stream_ptr())
+    return y, inv
+
+
 class DecodeWorkspace:
     """Split-K partial buffers for paged decode, sized once (graph-capture safe)."""
 

@@ -75,6 +75,12 @@ _SIGNATURES = {
         "ome_comm_all_gather": [vp, vp, vp, i64, i64, i32, vp],
         "ome_comm_error": [vp],
         "ome_comm_destroy": [vp],
+        "ome_ep_create": [i32, i32, i32, i32, C.POINTER(vp), vp, vp],
+        "ome_ep_open": [vp, vp, vp],
+        "ome_ep_dispatch": [vp, vp, i64, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp],
+        "ome_ep_combine": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp, i64, vp],
+        "ome_ep_error": [vp],
+        "ome_ep_destroy": [vp],
         "ome_kvlink_export": [vp, vp, C.POINTER(i64)],
         "ome_kvlink_handle_size": [],
         "ome_kvlink_open": [vp, C.POINTER(vp)],
