@@ -76,19 +76,38 @@ __global__ void ep_begin_kernel(EpSig* self) {
   if (threadIdx.x == 0) self->epoch = self->epoch + 1;
 }
 
-// one workgroup: assignment a = t * k + j -> (owner, slot); counts per owner in MY S[p] counts
+// one workgroup: assignment a = t * k + j -> (owner, slot, owner-local expert slot); counts per
+// owner in MY S[p] counts.  Without EPLB tables rank r owns experts [r * e_local, (r+1) * e_local);
+// with them (rep_rank / rep_slot [E][rmax], n_rep [E], ome_amd.parallel.eplb) the assignment goes
+// to replica (a mod n_rep[e]) of its expert, as in the normal-mode all-to-all.
 __global__ __launch_bounds__(1024) void ep_plan_kernel(const int* __restrict__ topk_ids, int n, int e_local, int W,
-                                                       int cap, int* __restrict__ a_dst, int* __restrict__ a_slot,
-                                                       EpSig* self, char* mybuf, Layout L) {
+                                                       int n_experts, int cap, int* __restrict__ a_dst,
+                                                       int* __restrict__ a_slot,
+                                                       int* __restrict__ a_local, const int64_t* __restrict__ rep_rank,
+                                                       const int64_t* __restrict__ rep_slot,
+                                                       const int64_t* __restrict__ n_rep, int rmax, EpSig* self,
+                                                       char* mybuf, Layout L) {
   __shared__ int cnt[kMaxRanks];
   if (threadIdx.x < kMaxRanks) cnt[threadIdx.x] = 0;
   __syncthreads();
   for (int a = threadIdx.x; a < n; a += blockDim.x) {
-    const int id = topk_ids[a];
-    int dst = id / e_local;
-    dst = dst < W ? dst : W - 1;
+    int id = topk_ids[a];
+    id = id < 0 ? 0 : (id < n_experts ? id : n_experts - 1);   // never index tables / peers out of range
+    int dst, loc;
+    if (rep_rank != nullptr) {
+      const int nr = (int)n_rep[id];
+      const int j = nr > 0 ? a % nr : 0;
+      dst = (int)rep_rank[(int64_t)id * rmax + j];
+      loc = (int)rep_slot[(int64_t)id * rmax + j];
+    } else {
+      dst = id / e_local;
+      loc = id - dst * e_local;
+    }
+    dst = dst < 0 ? 0 : (dst < W ? dst : W - 1);
+    loc = loc < 0 ? 0 : (loc < e_local ? loc : e_local - 1);
     const int slot = atomicAdd(&cnt[dst], 1);
     a_dst[a] = dst;
+    a_local[a] = loc;
     a_slot[a] = slot < cap ? slot : -1;  // over capacity: dropped (recorded below)
   }
   __syncthreads();
@@ -103,7 +122,7 @@ __global__ __launch_bounds__(1024) void ep_plan_kernel(const int* __restrict__ t
 
 // grid = assignments; row x[a / k] -> S[p][dst][slot], id -> S ids
 __global__ __launch_bounds__(256) void ep_pack_kernel(const bf16* __restrict__ x, int64_t ldx, int H, int k,
-                                                      const int* __restrict__ topk_ids, int e_local,
+                                                      const int* __restrict__ a_local,
                                                       const int* __restrict__ a_dst, const int* __restrict__ a_slot,
                                                       int cap, const EpSig* self, char* mybuf, Layout L) {
   const int a = blockIdx.x;
@@ -114,7 +133,7 @@ __global__ __launch_bounds__(256) void ep_pack_kernel(const bf16* __restrict__ x
     const u32x4* src = reinterpret_cast<const u32x4*>(x + (int64_t)(a / k) * ldx);
     u32x4* dstp = reinterpret_cast<u32x4*>(base + ((int64_t)dst * cap + slot) * H * 2);
     for (int v = threadIdx.x; v < H / 8; v += blockDim.x) dstp[v] = src[v];
-    if (threadIdx.x == 0) reinterpret_cast<int*>(base + L.rows)[dst * cap + slot] = topk_ids[a] % e_local;
+    if (threadIdx.x == 0) reinterpret_cast<int*>(base + L.rows)[dst * cap + slot] = a_local[a];
   }
   block_release();
 }
@@ -265,15 +284,21 @@ OME_API int ome_ep_open(void* ctx, const void* sig_handles, const void* buf_hand
 
 // dispatch: plan + pack + signal + wait + pull.  Outputs (device, caller-allocated): a_dst, a_slot
 // [T*k]; R [W*cap][H] received rows, rids [W*cap] local expert ids (e_local = empty slot), rcount [W].
+// a_local [T*k] scratch; rep_rank / rep_slot / n_rep: optional EPLB tables (int64, [E][rmax], [E]).
 OME_API int ome_ep_dispatch(void* ctx, const void* x, int64_t ldx, const int* topk_ids, int T, int k, int e_local,
-                            int* a_dst, int* a_slot, void* R, int* rids, int* rcount, hipStream_t stream) {
+                            int n_experts, int* a_dst, int* a_slot, int* a_local, const int64_t* rep_rank,
+                            const int64_t* rep_slot, const int64_t* n_rep, int rmax, void* R, int* rids, int* rcount,
+                            hipStream_t stream) {
   EpCtx* c = (EpCtx*)ctx;
   const int n = T * k;
+  if (e_local <= 0 || n_experts <= 0) return -2;
   ep_begin_kernel<<<1, 64, 0, stream>>>(c->sig);
-  ep_plan_kernel<<<1, 1024, 0, stream>>>(topk_ids, n, e_local, c->world, c->cap, a_dst, a_slot, c->sig, c->buf, c->L);
+  ep_plan_kernel<<<1, 1024, 0, stream>>>(topk_ids, n, e_local, c->world, n_experts, c->cap, a_dst, a_slot, a_local,
+                                         rep_rank,
+                                         rep_slot, n_rep, rmax, c->sig, c->buf, c->L);
   if (n > 0)
-    ep_pack_kernel<<<n, 256, 0, stream>>>((const bf16*)x, ldx, c->H, k, topk_ids, e_local, a_dst, a_slot, c->cap,
-                                          c->sig, c->buf, c->L);
+    ep_pack_kernel<<<n, 256, 0, stream>>>((const bf16*)x, ldx, c->H, k, a_local, a_dst, a_slot, c->cap, c->sig,
+                                          c->buf, c->L);
   ep_signal_kernel<<<1, 64, 0, stream>>>(c->peers, c->rank, c->world, 0, c->sig);
   ep_wait_kernel<<<1, 64, 0, stream>>>(c->sig, c->world, 0);
   ep_pull_kernel<<<dim3(c->cap, c->world), 256, 0, stream>>>(c->peers, c->rank, c->H, c->cap, e_local, c->L, c->sig,

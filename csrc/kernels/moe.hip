@@ -142,6 +142,10 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const T* __restrict__ lo
         bi = oi;
       }
     }
+    if (bi >= E) {   // no key beat the floor (NaN logits): still emit a valid expert id
+      bi = j < E ? j : E - 1;
+      bw = 0.f;
+    }
     if (lane == 0) {
       topk_w[(int64_t)t * k + j] = bw;
       topk_ids[(int64_t)t * k + j] = bi;
@@ -185,7 +189,8 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
   int* cur = sh + E;
   for (int e = threadIdx.x; e < E; e += blockDim.x) cnt[e] = 0;
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[topk_ids[i]], 1);
+  // ids outside [0, E) (never produced by moe_route) are clamped rather than indexing LDS out of range
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&cnt[min(max(topk_ids[i], 0), E - 1)], 1);
   __syncthreads();
   if (threadIdx.x == 0) {
     int acc = 0;
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__
   __syncthreads();
   // stable within an expert is not required (the combine uses the inverse map)
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int p = atomicAdd(&cur[topk_ids[i]], 1);
+    const int p = atomicAdd(&cur[min(max(topk_ids[i], 0), E - 1)], 1);
     sorted_ids[p] = i;
     inv[i] = p;
   }

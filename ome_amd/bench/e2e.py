@@ -107,11 +107,19 @@ async def _client(base: str, scen: Scenario, concurrency: int, vocab: int, max_i
                         first = False
                     seen = n
 
+    errors: list[str] = []
+
     async def worker(wid):
         rng = random.Random(seed * 7919 + wid)
         async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=3600)) as session:
             while not stop.is_set():
-                await one(session, rng)
+                try:
+                    await one(session, rng)
+                except asyncio.CancelledError:
+                    raise
+                except Exception as e:  # noqa: BLE001 — counted and reported, the loop keeps its load
+                    errors.append(f"{type(e).__name__}: {e}")
+                    await asyncio.sleep(0.05)
 
     tasks = [asyncio.create_task(worker(i)) for i in range(concurrency)]
     await asyncio.sleep(max(0.0, t1 - time.perf_counter()))
@@ -122,7 +130,7 @@ async def _client(base: str, scen: Scenario, concurrency: int, vocab: int, max_i
     toks = sum(n for ts, n in events if t0 <= ts < t1)
     ttfts = sorted(tt for ts, tt in firsts if t0 <= ts < t1)
     return {"tokens": toks, "window_s": timed_s, "p50_ttft_ms": 1000 * ttfts[len(ttfts) // 2] if ttfts else None,
-            "requests_started_in_window": len(ttfts)}
+            "requests_started_in_window": len(ttfts), "errors": len(errors), "first_error": errors[0] if errors else None}
 
 
 def run(model: str, scenario: str, concurrency: int, context_length: int, steps: int, warmup: int,

@@ -363,14 +363,13 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                                 bias=self.b_router[i], n_group=cfg.n_group, topk_group=cfg.topk_group,
                                 group_mode=self.group_mode)
         if self.ep > 1:
-            from ome_amd.parallel.ep import moe_ep_forward, moe_ep_forward_tbo
+            from ome_amd.parallel.ep import moe_ep
 
             tables = None
             if self.eplb is not None:
                 self.eplb.record(i, tid)
                 tables = self.eplb.tables[i]
-            fwd = moe_ep_forward_tbo if pstate.get().tbo else moe_ep_forward
-            out = fwd(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale, self.E, tables)
+            out = moe_ep(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale, self.E, tables)
         else:
             out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale)
         if self.w_sgu[i] is not None:

@@ -159,14 +159,13 @@ class Llama4ForCausalLM(MoEForCausalLM):
             tid = tid.reshape(T * self.k, 1)
         ones = torch.ones(tid.shape, dtype=torch.float32, device=x.device)
         if self.ep > 1:
-            from ome_amd.parallel.ep import moe_ep_forward, moe_ep_forward_tbo
+            from ome_amd.parallel.ep import moe_ep
 
             tables = None
             if self.eplb is not None:
                 self.eplb.record(i, tid)
                 tables = self.eplb.tables[i]
-            fwd = moe_ep_forward_tbo if pstate.get().tbo else moe_ep_forward
-            out = fwd(xr, ones, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E, tables)
+            out = moe_ep(xr, ones, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E, tables)
         else:
             out = ops.fused_moe(xr, ones, tid, self.w13[i], self.w2[i], self.act)
         if self.k > 1:

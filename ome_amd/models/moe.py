@@ -188,14 +188,13 @@ class MoEForCausalLM(LlamaForCausalLM):
         logits = F.linear(x, self.w_router[i])
         tw, tid = ops.moe_route(logits, self.k, self.renorm)
         if self.ep > 1:
-            from ome_amd.parallel.ep import moe_ep_forward, moe_ep_forward_tbo
+            from ome_amd.parallel.ep import moe_ep
 
             tables = None
             if self.eplb is not None:
                 self.eplb.record(i, tid)
                 tables = self.eplb.tables[i]
-            fwd = moe_ep_forward_tbo if pstate.get().tbo else moe_ep_forward
-            out = fwd(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E, tables)
+            out = moe_ep(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E, tables)
         else:
             out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act)
         if self.w_sgu[i] is not None:

@@ -265,7 +265,7 @@ def fp8_gemm(qa, sa, qw, sw, block: int = 0, bias=None, out: torch.Tensor | None
     assert qw.shape[1] == K and qa.is_contiguous() and qw.is_contiguous()
     if out is None:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=qa.device)
-    if N % 256 == 0 and K % 128 == 0 and M >= FP8_MX_MIN_ROWS:
+    if N % 256 == 0 and K % 128 == 0 and M >= FP8_MX_MIN_ROWS and -(-M // 256) * (N // 256) >= FP8_MX_MIN_TILES:
         # 256 x 256 MX-scaled MFMA tile (csrc/kernels/gemm.hip): twice the bf16 MFMA rate
         call("ome_fp8_gemm_mx", qa.data_ptr(), qa.stride(0), sa.data_ptr(), qw.data_ptr(), qw.stride(0),
              sw.data_ptr(), M, N, K, block, out.data_ptr(), out.stride(0), ptr(bias), stream_ptr())
@@ -277,6 +277,9 @@ def fp8_gemm(qa, sa, qw, sw, block: int = 0, bias=None, out: torch.Tensor | None
 
 # rows from which the dense fp8 GEMM uses the 256 x 256 MX tile (smaller M: the 64 x 64 kernel)
 FP8_MX_MIN_ROWS = int(os.environ.get("OME_FP8_MX_MIN_ROWS", "65"))
+# ...and from this many 256 x 256 output tiles (profiles/r03_fp8_gemm_bench.txt: below ~128 tiles
+# the grid under-fills the 256 CUs and the 64 x 64 kernel is the better choice)
+FP8_MX_MIN_TILES = int(os.environ.get("OME_FP8_MX_MIN_TILES", "112"))
 
 
 def fp8_linear(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0, bias=None) -> torch.Tensor:

@@ -77,7 +77,7 @@ _SIGNATURES = {
         "ome_comm_destroy": [vp],
         "ome_ep_create": [i32, i32, i32, i32, C.POINTER(vp), vp, vp],
         "ome_ep_open": [vp, vp, vp],
-        "ome_ep_dispatch": [vp, vp, i64, vp, i32, i32, i32, vp, vp, vp, vp, vp, vp],
+        "ome_ep_dispatch": [vp, vp, i64, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp],
         "ome_ep_combine": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp, i64, vp],
         "ome_ep_error": [vp],
         "ome_ep_destroy": [vp],

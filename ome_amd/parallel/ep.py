@@ -182,3 +182,39 @@ def moe_ep_forward_tbo(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Te
         unsorted.index_copy_(0, mb["order"], mb["back"])
     out = (unsorted.view(T, k, H).float() * topk_w.float().view(T, k, 1)).sum(1) * scale
     return out.to(x.dtype)
+
+
+def moe_ep(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13_local, w2_local, act: int,
+           scale: float, num_experts: int, tables=None) -> torch.Tensor:
+    """Expert-parallel MoE block: the device-only low-latency exchange
+    (:mod:`ome_amd.parallel.ep_ll`) when this lockstep step allows it (``state.ep_ll_ok``: every
+    rank's batch fits the fixed buckets; set per step by the engine, so all ranks pick the same
+    mode), the RCCL all-to-all (normal / two-batch-overlap) otherwise.  EPLB replica tables are
+    honoured by both."""
+    st = pstate.get()
+    ll = getattr(st, "ep_ll", None)
+    if ll is not None and x.is_cuda and st.ep_ll_ok:
+        e_local = w13_local.shape[0]   # expert slots per rank (redundant replicas included)
+        return ll.forward(x, topk_w, topk_ids, w13_local, w2_local, act, scale, e_local, tables)
+    fwd = moe_ep_forward_tbo if st.tbo else moe_ep_forward
+    return fwd(x, topk_w, topk_ids, w13_local, w2_local, act, scale, num_experts, tables)
+
+
+def attach_low_latency(model, max_tokens: int) -> bool:
+    """Create the low-latency EP exchange for an MoE model under DP attention on GPU (one node):
+    buckets of ``max_tokens`` x top-k rows per peer.  Collective over the EP group (every rank
+    calls it at model build).  Returns True when installed."""
+    import os
+
+    st = pstate.get()
+    if st.ep_size <= 1 or not torch.cuda.is_available() or os.environ.get("OME_EP_LL", "1") == "0":
+        return False
+    k = getattr(model, "k", 0)
+    if not k or getattr(model, "E", 0) % st.ep_size:
+        return False
+    from ome_amd.parallel.ep_ll import LowLatencyEP
+
+    st.ep_ll = LowLatencyEP(st.ep_group, model.cfg.hidden_size, max_tokens, k, cpu_group=st.cpu_group)
+    st.ep_ll_cap = max_tokens
+    st.ep_ll_ok = True
+    return True

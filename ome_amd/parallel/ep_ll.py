@@ -24,6 +24,10 @@ from ome_amd.ops import _native
 log = logging.getLogger("ome_amd.ep_ll")
 
 
+def _ptr(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
 class LowLatencyEP:
     def __init__(self, group, hidden: int, max_tokens: int, top_k: int, cpu_group=None):
         self.group = group
@@ -46,9 +50,10 @@ class LowLatencyEP:
             raise _native.NativeError(f"ome_ep_open failed ({rc}): peers not reachable over xGMI/IPC")
 
     def forward(self, x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13, w2, act: int,
-                scale: float, e_local: int) -> torch.Tensor:
+                scale: float, e_local: int, tables=None) -> torch.Tensor:
         """x [T, H] this rank's tokens, routing [T, k] over global experts (rank r owns
-        [r * e_local, (r + 1) * e_local)); w13 / w2 this rank's experts (bf16 or Fp8Experts)."""
+        [r * e_local, (r + 1) * e_local), or the EPLB replica ``tables``); w13 / w2 this rank's
+        expert slots (bf16 or Fp8Experts)."""
         T, H = x.shape
         k = topk_ids.shape[1]
         if T > self.max_tokens or k != self.k or H != self.H:
@@ -57,13 +62,22 @@ class LowLatencyEP:
         n = T * k
         a_dst = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         a_slot = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        a_local = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        rr = rs = nr = None
+        rmax = 0
+        n_experts = e_local * self.world
+        if tables is not None:
+            rr, rs, nr = (t if t.dtype == torch.int64 else t.long() for t in tables)
+            rmax = rr.shape[1]
+            n_experts = rr.shape[0]
         R = torch.empty(self.world * self.cap, H, dtype=x.dtype, device=dev)
         rids = torch.empty(self.world * self.cap, dtype=torch.int32, device=dev)
         rcount = torch.empty(self.world, dtype=torch.int32, device=dev)
         ids = topk_ids.to(torch.int32).contiguous()
         s = _native.stream_ptr(dev)
         rc = self._lib.ome_ep_dispatch(self._ctx, C.c_void_p(x.data_ptr()), x.stride(0), C.c_void_p(ids.data_ptr()),
-                                       T, k, e_local, C.c_void_p(a_dst.data_ptr()), C.c_void_p(a_slot.data_ptr()),
+                                       T, k, e_local, n_experts, C.c_void_p(a_dst.data_ptr()), C.c_void_p(a_slot.data_ptr()),
+                                       C.c_void_p(a_local.data_ptr()), _ptr(rr), _ptr(rs), _ptr(nr), rmax,
                                        C.c_void_p(R.data_ptr()), C.c_void_p(rids.data_ptr()),
                                        C.c_void_p(rcount.data_ptr()), C.c_void_p(s))
         if rc != 0:

@@ -64,10 +64,11 @@ class ExpertPlacement:
                 out[e].append((r, s))
         return out
 
-    def tables(self, device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        """(rep_rank [E, Rmax], rep_slot [E, Rmax], n_rep [E]) int64 dispatch tables."""
+    def tables(self, device, rmax: int | None = None) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """(rep_rank [E, Rmax], rep_slot [E, Rmax], n_rep [E]) int64 dispatch tables (``rmax``:
+        a fixed replica width, so re-placements can be copied into the same tensors)."""
         reps = self.replicas()
-        rmax = max(len(v) for v in reps.values())
+        rmax = max(rmax or 0, max(len(v) for v in reps.values()))
         rank = torch.zeros(self.num_experts, rmax, dtype=torch.int64)
         slot = torch.zeros(self.num_experts, rmax, dtype=torch.int64)
         n = torch.zeros(self.num_experts, dtype=torch.int64)
@@ -168,7 +169,10 @@ class EPLBState:
     def __init__(self, layers, num_experts: int, ep: int, rank: int, redundant: int, device):
         self.ep, self.rank, self.device = ep, rank, device
         self.placement = {i: ExpertPlacement.default(num_experts, ep, redundant) for i in layers}
-        self.tables = {i: p.tables(device) for i, p in self.placement.items()}
+        # fixed width (an expert never has more than 1 + redundant replicas): tables are updated in
+        # place after a re-placement, so HIP graphs that captured them stay valid
+        self.rmax = 1 + max(0, int(redundant))
+        self.tables = {i: p.tables(device, self.rmax) for i, p in self.placement.items()}
         self.load = {i: torch.zeros(num_experts, dtype=torch.float64, device=device) for i in layers}
         self.rounds = 0
 
@@ -198,9 +202,14 @@ class EPLBState:
             if new.phys_to_log != old.phys_to_log:
                 ws = weights[i]
                 for j, w in enumerate(ws):
-                    ws[j] = migrate(old, new, w, self.rank, group)
+                    moved = migrate(old, new, w, self.rank, group)
+                    if moved.shape == w.shape:
+                        w.copy_(moved)   # in place: captured graphs keep reading this tensor
+                    else:
+                        ws[j] = moved
                 self.placement[i] = new
-                self.tables[i] = new.tables(self.device)
+                for dst, src in zip(self.tables[i], new.tables(self.device, self.rmax)):
+                    dst.copy_(src)
             out[i] = new.imbalance(lv)
             self.load[i].zero_()
         self.rounds += 1

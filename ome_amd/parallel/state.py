@@ -41,6 +41,9 @@ class ParallelState:
     replica: int = 0
     replicas: int = 1
     base: int = 0               # global rank of this group's rank 0
+    ep_ll: object | None = None # ome_amd.parallel.ep_ll.LowLatencyEP (DP attention on one node)
+    ep_ll_ok: bool = False      # this lockstep step may use it (every rank's batch fits the buckets)
+    ep_ll_cap: int = 0          # tokens per rank the low-latency buckets hold
 
     def to_global(self, r: int) -> int:
         return self.base + r

@@ -87,7 +87,9 @@ class Router:
             log.info("removed worker %s", url)
 
     def healthy(self, role: str) -> list[Worker]:
-        return [w for w in self.workers.values() if w.healthy and w.role == role]
+        # a decode worker is routable only once its KV bootstrap port is known (first probe)
+        return [w for w in self.workers.values()
+                if w.healthy and w.role == role and (role != "decode" or w.bootstrap_port is not None)]
 
     async def _probe(self, w: Worker) -> None:
         try:

@@ -234,6 +234,10 @@ class KVTransfer:
                 return False
             req.req_slot = slot
         pages = sch.pages.alloc(n_pages)
+        if pages is None and sch.prefix_cache is not None:
+            # finished decodes leave their pages in the radix cache: reclaim before waiting
+            sch.prefix_cache.evict(n_pages - sch.pages.num_free)
+            pages = sch.pages.alloc(n_pages)
         if pages is None:
             return False
         req.pages = list(pages)

@@ -107,7 +107,7 @@ class Engine:
                                   load_format=args.load_format,
                                   page_size=args.page_size, mem_fraction_static=args.mem_fraction_static,
                                   max_total_tokens=args.max_total_tokens, max_running=args.max_running_requests,
-                                  max_context=self.max_context, cuda_graph=args.cuda_graph and not self.dp,
+                                  max_context=self.max_context, cuda_graph=args.cuda_graph,
                                   cuda_graph_max_bs=args.cuda_graph_max_bs, seed=args.seed,
                                   kv_cache_dtype_name=args.kv_cache_dtype)
         prefix = None
@@ -355,14 +355,20 @@ class Engine:
         dist.all_gather(allw, mine, group=self._cpu_group())
         if not any(int(w) for w in allw):
             return []
+        # every rank sees the same token counts, so all pick the same MoE exchange mode: the
+        # device-only low-latency buckets when every rank's batch fits, RCCL all-to-all otherwise
+        st = self.pstate
+        st.ep_ll_ok = st.ep_ll is not None and max(int(w) for w in allw) <= st.ep_ll_cap
         done: list[Request] = []
         touched = []
         if batch is not None:
             t0 = time.perf_counter()
-            handle = self.runner.launch(batch)
+            handle = self.runner.launch(batch, allow_graph=st.ep_ll_ok)
             self.scheduler.launch_commit(batch)
             done = self._complete(batch, handle, t0)
             touched = list({id(c.req): c.req for c in batch.chunks}.values())
+        elif st.ep_ll_ok:
+            self.runner.idle_decode()
         else:
             self.runner.idle_forward()
         updates = []

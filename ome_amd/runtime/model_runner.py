@@ -104,6 +104,13 @@ class ModelRunner:
         self.model = build_model(cfg, self.device, dtype, max_positions=max_context + page_size,
                                  model_path=model_path, load_format=load_format, seed=seed)
         self.load_time = time.perf_counter() - t0
+        # DP attention + expert parallelism on GPU: the device-only low-latency EP exchange makes
+        # the MoE layers capturable, so the decode graphs stay on (ome_amd.parallel.ep_ll)
+        self.ep_ll = False
+        if pstate.get().ep_size > 1 and self.device.type == "cuda":
+            from ome_amd.parallel.ep import attach_low_latency
+
+            self.ep_ll = attach_low_latency(self.model, max(max_running, 8))
         self.stateful = bool(getattr(self.model, "stateful", False))
         if self.stateful:  # recurrent (SSM) state per request slot, the padding slot included; before
             # the KV sizing below so the page budget sees it
@@ -167,8 +174,11 @@ class ModelRunner:
         self.counts = torch.zeros(max_running + 1, cfg.vocab_size, dtype=torch.int32, device=self.device)
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
-        # pipeline stages run eagerly: the stage hand-off is a blocking p2p exchange
-        self.use_graph = cuda_graph and self.is_cuda and not self.pp and not getattr(self.model, "encoder_only", False)
+        # pipeline stages run eagerly: the stage hand-off is a blocking p2p exchange; DP attention
+        # replays graphs only with the low-latency EP exchange (cuda_graph=None: "if possible")
+        dp_ok = pstate.get().ep_size <= 1 or self.ep_ll
+        self.use_graph = bool(cuda_graph) and self.is_cuda and not self.pp and dp_ok and \
+            not getattr(self.model, "encoder_only", False)
         if self.use_graph:
             self.capture_graphs()
 
@@ -291,15 +301,35 @@ class ModelRunner:
         """Synchronous step: enqueue + wait."""
         return self.launch(batch).result()
 
-    def launch(self, batch: StepBatch, prev: "StepHandle | None" = None) -> "StepHandle":
+    def launch(self, batch: StepBatch, prev: "StepHandle | None" = None, allow_graph: bool = True) -> "StepHandle":
         """Enqueue one step.  Rows whose input token is PENDING (sampled by ``prev``, still in
-        flight) get it on the device from ``prev``'s output — no host round trip."""
+        flight) get it on the device from ``prev``'s output — no host round trip.
+        ``allow_graph=False``: run eagerly even for a decode batch (DP attention steps whose MoE
+        exchange must take the normal RCCL mode on every rank)."""
         self.slots.flush()
         if batch.mode == "decode" and not self.pp and all(c.length == 1 for c in batch.chunks):
             bs = next((b for b in self.buckets if b >= len(batch.chunks)), None)
             if bs is not None:
-                return self._launch_decode(batch, bs, prev)
+                return self._launch_decode(batch, bs, prev, graph=allow_graph)
         return self._launch_eager(batch, prev)
+
+    def idle_decode(self) -> None:
+        """DP attention, low-latency EP: this rank has nothing scheduled while its peers decode --
+        replay the smallest decode graph on one padding row (scratch slot, sequence length 0) so
+        every MoE exchange has all participants."""
+        d, bs = self.dbuf, self.buckets[0]
+        h, off = d.hnp, d.off
+        for name, v in (("ids", 0), ("slots", -1), ("seq_lens", 0), ("pos", 0), ("src", -1), ("order", 0),
+                        ("top_k", -1)):
+            h[off[name]:off[name] + bs] = v
+        h[off["req_idx"]:off["req_idx"] + bs] = self.slots.max_reqs - 1
+        for name, v in (("temp", 0.0), ("top_p", 1.0), ("min_p", 0.0), ("rep", 1.0), ("freq", 0.0), ("pres", 0.0)):
+            d.hf[off[name]:off[name] + bs] = v
+        d.dev.copy_(d.host, non_blocking=True)
+        if self.use_graph:
+            self.graphs[bs].replay()
+        else:
+            self._decode_forward(bs)
 
     def _finish_launch(self, ids_dev: torch.Tensor, lp_dev: torch.Tensor, n: int) -> "StepHandle":
         hi, hl = self._host_out[self._ring]
@@ -340,7 +370,8 @@ class ModelRunner:
             return -1
         return r.pending_row
 
-    def _launch_decode(self, batch: StepBatch, bs: int, prev: "StepHandle | None") -> "StepHandle":
+    def _launch_decode(self, batch: StepBatch, bs: int, prev: "StepHandle | None",
+                       graph: bool = True) -> "StepHandle":
         B = len(batch.chunks)
         d = self.dbuf
         h, hf, off = d.hnp, d.hf, d.off
@@ -395,7 +426,7 @@ class ModelRunner:
         d.dev.copy_(d.host, non_blocking=True)
         if any_pending:
             ops.fill_pending(d.view("ids", bs), d.view("src", bs), prev.ids_dev)
-        if self.use_graph:
+        if self.use_graph and graph:
             self.graphs[bs].replay()
         else:
             self._decode_forward(bs)

@@ -233,6 +233,7 @@ def create_app(engine, ns=None):
                 "context_length": engine.max_context}
 
     @app.get("/get_server_info")
+    @app.get("/server_info")
     async def server_info():
         a = engine.args
         return {"tp_size": a.tp_size, "pp_size": a.pp_size, "page_size": a.page_size,
@@ -610,8 +611,6 @@ def create_app(engine, ns=None):
         return {"id": f"rerank-{uuid.uuid4().hex[:12]}", "model": model_name, "results": res,
                 "usage": {"prompt_tokens": total, "total_tokens": total}}
 
-    if getattr(engine, "kv_transfer", None) is not None:
-        engine.kv_transfer.mount(app)
     return app
 
 

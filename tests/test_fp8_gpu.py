@@ -28,7 +28,9 @@ def test_fp8_quant(group, M, K):
 @pytest.mark.parametrize("block", [0, 128])
 @pytest.mark.parametrize("M,N,K", [(1, 64, 128), (5, 6144, 4096), (64, 128, 256), (257, 4096, 14336),
                                    (1000, 512, 1024), (700, 6144, 4096), (129, 768, 384), (66, 256, 128)])
-def test_fp8_gemm(block, M, N, K):
+@pytest.mark.parametrize("mx_tiles", [112, 1])   # 1: force the 256x256 MX tile wherever it applies
+def test_fp8_gemm(block, M, N, K, mx_tiles, monkeypatch):
+    monkeypatch.setattr(ops, "FP8_MX_MIN_TILES", mx_tiles)
     torch.manual_seed(1)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
