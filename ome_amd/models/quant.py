@@ -131,8 +131,9 @@ def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None, out: torch.Tens
     was measured faster (``ops.decode_gemm_plan``, opt-in); Fp8Weight -> W8A8 MFMA path.
     ``out``: write the result there (e.g. the TP all-reduce's IPC staging buffer)."""
     if out is not None:
-        if isinstance(w, torch.Tensor) and x.dim() == 2 and x.is_cuda and not (x.shape[0] <= _GEMV_ROWS and
-                                                                                ops.gemv_ok(x, w)):
+        if x.is_cuda and x.shape[0] <= _GEMV_ROWS and ops.gemv_ok(x, w, bias, out):
+            return ops.gemv(x, w, bias, out=out)
+        if isinstance(w, torch.Tensor) and x.dim() == 2 and x.is_cuda:
             if bias is None:
                 return torch.matmul(x, w.t(), out=out)
             return torch.addmm(bias, x, w.t(), out=out)
@@ -141,7 +142,7 @@ def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None, out: torch.Tens
     if isinstance(w, Fp8Weight):
         return ops.fp8_linear(x, w.q, w.scale, w.block, bias)
     if x.dim() == 2 and x.shape[0] <= 256 and x.is_cuda:
-        if x.shape[0] <= _GEMV_ROWS and ops.gemv_ok(x, w):
+        if x.shape[0] <= _GEMV_ROWS and ops.gemv_ok(x, w, bias):
             return ops.gemv(x, w, bias)
         plan = ops.decode_gemm_plan(x, w, bias)
         if plan is not None:

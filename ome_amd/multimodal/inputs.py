@@ -36,6 +36,34 @@ class MMInput:
     def num_tokens(self) -> int:
         return sum(n for _, n in self.spans)
 
+    def cache_key(self) -> tuple[bytes, int]:
+        """(salt, first prompt index it applies from) for the prefix cache: see :func:`mm_cache_key`."""
+        return mm_cache_key(self, min((s for s, _ in self.spans), default=0))
+
+
+def mm_cache_key(mm, salt_from: int) -> tuple[bytes, int]:
+    """128-bit BLAKE2b digest of EVERYTHING the request's KV depends on besides its token ids
+    (pixel values, grids, spans, image positions), cached on ``mm``.  The prefix cache mixes it
+    into the hash chain of every page from ``salt_from`` on, so two requests with identical text
+    but different images can never share KV pages -- the placeholder ids alone are a hash reduced
+    modulo the vocabulary (:func:`pad_token_id`) and collide at ~1/vocab per image pair."""
+    got = getattr(mm, "_cache_key", None)
+    if got is None:
+        h = hashlib.blake2b(digest_size=16)
+        for name, v in sorted(vars(mm).items()):
+            if name.startswith("_") or name in ("features", "release") or callable(v):
+                continue
+            if isinstance(v, torch.Tensor):
+                h.update(v.detach().cpu().contiguous().view(torch.uint8).numpy().tobytes())
+            elif isinstance(v, np.ndarray):
+                h.update(np.ascontiguousarray(v).tobytes())
+            else:
+                h.update(repr(v).encode())
+            h.update(name.encode())
+        got = (h.digest(), salt_from)
+        mm._cache_key = got
+    return got
+
 
 def load_image(src):
     """PIL image from a ``data:`` URL, raw base64, a local path, bytes or a PIL image (no network:

@@ -97,6 +97,12 @@ class CrossMMInput:
     rope_delta: int = 0                 # plain 1D RoPE (no M-RoPE offset for generated tokens)
     release: object = None              # frees the model-side vision-token cache (set by the model)
 
+    def cache_key(self) -> tuple[bytes, int]:
+        """Cross-attention feeds the image into every text row: salt the whole prompt."""
+        from ome_amd.multimodal.inputs import mm_cache_key
+
+        return mm_cache_key(self, 0)
+
     def segments(self, tokens_per_tile: int, max_tiles: int) -> list[tuple[int, int, int, int]]:
         """``(text_start, lo, hi, mlp_on)`` per visibility segment, in text order: rows at
         positions >= text_start (up to the next segment) attend keys [lo, hi) of the request's

@@ -623,10 +623,18 @@ def stream_gemm_ok(M: int, N: int, K: int) -> bool:
     return 1 <= M <= 256 and N % 128 == 0 and K % 64 == 0
 
 
+_stream_ws_retired: list = []
+
+
 def stream_gemm_reserve(device, floats: int) -> None:
-    """Pre-size the split-K workspace (call before HIP-graph capture so capture never allocates)."""
+    """Pre-size the split-K workspace (call before HIP-graph capture so capture never allocates).
+    Growing it later keeps the old buffer alive: graphs captured earlier replay into it."""
     ws = _stream_ws.get(device)
     if ws is None or ws.numel() < floats:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"split-K workspace must be reserved before capture ({floats} floats needed)")
+        if ws is not None:
+            _stream_ws_retired.append(ws)
         _stream_ws[device] = torch.empty(floats, dtype=torch.float32, device=device)
 
 
@@ -662,10 +670,18 @@ def stream_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = No
     return out
 
 
-def gemv_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return (x.dim() == 2 and 1 <= x.shape[0] <= 8 and x.shape[1] % 8 == 0 and x.stride(1) == 1
-            and x.stride(0) % 8 == 0 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
-            and w.is_contiguous())
+def gemv_ok(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
+            out: torch.Tensor | None = None) -> bool:
+    """gemv.hip reads x and w in 16-byte chunks: both must start on a 16-B boundary with 16-B
+    row pitch; bias (if any) is a contiguous bf16 [N]; out rows are unit-stride."""
+    return (isinstance(w, torch.Tensor) and x.dim() == 2 and 1 <= x.shape[0] <= 8 and x.shape[1] % 8 == 0
+            and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous() and w.shape[1] == x.shape[1]
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+            and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous()
+                                  and bias.numel() == w.shape[0]))
+            and (out is None or (out.dtype == torch.bfloat16 and out.dim() == 2 and out.stride(1) == 1
+                                 and tuple(out.shape) == (x.shape[0], w.shape[0]))))
 
 
 def gemv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
@@ -680,7 +696,7 @@ def gemv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
             out.copy_(r)
             return out
         return r
-    assert gemv_ok(x, w), (tuple(x.shape), x.stride(), w.shape)
+    assert gemv_ok(x, w, bias, out), (tuple(x.shape), x.stride(), w.shape)
     out = torch.empty(M, N, dtype=x.dtype, device=x.device) if out is None else out
     call("ome_gemv", x.data_ptr(), x.stride(0), w.data_ptr(), ptr(bias), out.data_ptr(), out.stride(0), M, N, K,
          stream_ptr())

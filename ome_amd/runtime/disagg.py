@@ -94,6 +94,13 @@ class KVTransfer:
         self.ipc_sent = 0
         self.ipc_received = 0
         runner = engine.runner
+        kv = runner.kv
+        shapes = {(tuple(kv.k[i].shape[1:]), tuple(kv.v[i].shape[1:])) for i in kv.local_layers}
+        if len(shapes) != 1:
+            # the page image format carries one K/V page shape for all layers (DeciLM / Nemotron-NAS
+            # vary KV heads per layer): refuse at start-up rather than fail every transfer
+            raise ValueError("PD disaggregation needs one KV page shape across layers; this model has "
+                             f"{len(shapes)} (per-layer KV heads)")
         use_ipc = os.environ.get("OME_PD_IPC", "1") == "1"
         if mode == "decode" and use_ipc:
             from ome_amd.runtime import kvlink

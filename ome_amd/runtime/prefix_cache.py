@@ -7,6 +7,10 @@ reuses those pages instead of recomputing them (SGLang radix cache, which the re
 runtimes keep enabled unless ``--disable-radix-cache``).  Pages matched by running requests
 are pinned (refcount); unpinned pages are evicted LRU-deepest-first when the allocator runs
 dry, and eviction of a page leaves its descendants unreachable so they are evicted next.
+
+Multimodal requests pass a ``salt`` (digest of their images, :func:`ome_amd.multimodal.inputs.
+mm_cache_key`) mixed into every page from the first image position on: their KV depends on pixels
+the token ids do not capture.
 """
 from __future__ import annotations
 
@@ -24,7 +28,7 @@ class PrefixCache:
         self.hits = 0
         self.queries = 0
 
-    def _chain(self, tokens: list[int]):
+    def _chain(self, tokens: list[int], salt: bytes = b"", salt_from: int = 0):
         n, P = len(tokens) // self.P, self.P
         if n == 0:
             return
@@ -32,15 +36,16 @@ class PrefixCache:
         step = 8 * P
         h = b""
         for i in range(n):
-            h = hashlib.blake2b(h + raw[i * step:(i + 1) * step], digest_size=16).digest()
+            extra = salt if salt and (i + 1) * P > salt_from else b""
+            h = hashlib.blake2b(h + raw[i * step:(i + 1) * step] + extra, digest_size=16).digest()
             yield i, h
 
-    def match(self, tokens: list[int]) -> list[int]:
+    def match(self, tokens: list[int], salt: bytes = b"", salt_from: int = 0) -> list[int]:
         """Pin and return the cached pages covering the longest full-page prefix of ``tokens``."""
         self.queries += 1
         out = []
         t = next(self._clock)
-        for _, h in self._chain(tokens):
+        for _, h in self._chain(tokens, salt, salt_from):
             p = self.by_hash.get(h)
             if p is None:
                 break
@@ -52,12 +57,12 @@ class PrefixCache:
             self.hits += 1
         return out
 
-    def insert(self, tokens: list[int], pages: list[int]) -> set[int]:
+    def insert(self, tokens: list[int], pages: list[int], salt: bytes = b"", salt_from: int = 0) -> set[int]:
         """Offer a finished request's pages; returns the pages now owned by the cache (the
         caller frees the rest).  Unpins pages the request had matched."""
         kept: set[int] = set()
         t = next(self._clock)
-        for i, h in self._chain(tokens):
+        for i, h in self._chain(tokens, salt, salt_from):
             if i >= len(pages):
                 break
             page = pages[i]

@@ -45,6 +45,12 @@ class StepBatch:
         return sum(c.length for c in self.chunks)
 
 
+def _mm_salt(req) -> tuple[bytes, int]:
+    """Prefix-cache salt of a multimodal request (image digest, first image position)."""
+    key = getattr(req.mm, "cache_key", None)
+    return key() if key is not None else (b"", 0)
+
+
 class Scheduler:
     def __init__(self, pages: PagePool, slots: ReqSlotPool, page_size: int, max_running: int = 256,
                  chunked_prefill_size: int = 8192, max_context: int = 8192, enable_mixed_chunk: bool = False,
@@ -114,7 +120,7 @@ class Scheduler:
     def _release(self, req: Request, cache_prefix: bool = False) -> None:
         if req.pages:
             if cache_prefix and self.prefix_cache is not None:
-                kept = self.prefix_cache.insert(req.all_ids[: req.num_cached], req.pages)
+                kept = self.prefix_cache.insert(req.all_ids[: req.num_cached], req.pages, *_mm_salt(req))
                 rest = [p for p in req.pages if p not in kept]
                 self.pages.free(rest)
             else:
@@ -206,7 +212,7 @@ class Scheduler:
                     break
                 r.req_slot = slot
             if self.prefix_cache is not None and r.num_cached == 0 and not r.pages:
-                hit_pages = self.prefix_cache.match(r.all_ids[: r.seq_len - 1])
+                hit_pages = self.prefix_cache.match(r.all_ids[: r.seq_len - 1], *_mm_salt(r))
                 if hit_pages:
                     r.pages = list(hit_pages)
                     self.slots.set_pages(r.req_slot, 0, hit_pages)

@@ -94,6 +94,28 @@ def test_prefix_cache_unit():
     assert pc.evict(5) == 3 and pc.num_pages == 0
 
 
+def test_prefix_cache_image_digest_salt():
+    """Same token ids (placeholder-id collision forced), different pixels: no KV page sharing
+    from the first image position on; text pages before the image stay shared."""
+    from ome_amd.multimodal.inputs import MMInput
+    from ome_amd.runtime.scheduler import _mm_salt
+
+    pool = PagePool(40)
+    pc = PrefixCache(pool, 4)
+    toks = list(range(8)) + [777] * 8 + [1, 2, 3, 4]
+    a = MMInput(torch.zeros(4, 6), [(1, 2, 2)], [(8, 8)])
+    b = MMInput(torch.ones(4, 6), [(1, 2, 2)], [(8, 8)])
+    pages = pool.alloc(5)
+    pc.insert(toks, pages, *_mm_salt(type("R", (), {"mm": a})()))
+    got_b = pc.match(toks, *_mm_salt(type("R", (), {"mm": b})()))
+    assert got_b == pages[:2]                   # only the two text pages before the image
+    pc.release(got_b)
+    got_a = pc.match(toks, *a.cache_key())
+    assert got_a == pages                       # same image: full reuse
+    pc.release(got_a)
+    assert pc.match(toks) == pages[:2]          # a text-only request never sees image pages
+
+
 def test_scenarios():
     rng = random.Random(0)
     for s in ["N(480,240)/(300,150)", "D(100,100)", "U(10,20)/(5,6)", "E(128)", "I(512,512)"]:
