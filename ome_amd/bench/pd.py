@@ -9,7 +9,9 @@ path: router -> prefill engine (prompt + first token) -> KV pages to the decode 
 same-node IPC fast path, csrc/comm/kvlink.hip) -> decode engine streams the rest.
 With at least P + D GPUs every server gets its own device (prefill i -> GPU i, decode j -> GPU
 P + j); on a smaller box they share the visible devices round-robin, each bounded by
-``--max-total-tokens`` so the co-located engines fit side by side.
+``--max-total-tokens`` so the co-located engines fit side by side.  A prefill engine only holds
+the prompts in flight (64K tokens of KV); a decode engine holds every running request's whole
+context (512K tokens: 256 requests x ~800 tokens without preemption).
 """
 from __future__ import annotations
 
@@ -29,8 +31,20 @@ def _gpu_count() -> int:
     return torch.cuda.device_count()   # does not initialise the GPU on this stack
 
 
+def _server_info(url: str) -> dict:
+    import json
+    import urllib.request
+
+    try:
+        with urllib.request.urlopen(url + "/get_server_info", timeout=10) as r:
+            return json.loads(r.read())
+    except OSError:
+        return {}
+
+
 def run(model: str, scenario: str, concurrency: int, context_length: int, steps: int, warmup: int, step_s: float,
-        n_prefill: int = 1, n_decode: int = 1, max_total_tokens: int = 131072, log_dir: str | None = None,
+        n_prefill: int = 1, n_decode: int = 1, max_total_tokens: int = 65536, decode_total_tokens: int = 524288,
+        log_dir: str | None = None,
         extra: list[str] | None = None) -> dict:
     ngpu = max(1, _gpu_count())
     procs: list[subprocess.Popen] = []
@@ -44,7 +58,8 @@ def run(model: str, scenario: str, concurrency: int, context_length: int, steps:
             args = [sys.executable, "-m", "ome_amd.runtime.server", "--model-path", f"random://{model}", "--host",
                     "127.0.0.1", "--port", str(port), "--max-running-requests", str(concurrency),
                     "--context-length", str(context_length), "--disaggregation-mode", role,
-                    "--max-total-tokens", str(max_total_tokens), "--mem-frac", "0.95", *(extra or [])]
+                    "--max-total-tokens", str(max_total_tokens if role == "prefill" else decode_total_tokens),
+                    "--mem-frac", "0.95", *(extra or [])]
             if role == "decode":
                 args += ["--disaggregation-bootstrap-port", str(e2e._free_port())]
             out = open(os.path.join(log_dir, f"{role}{i}.log"), "w") if log_dir else subprocess.DEVNULL
@@ -70,6 +85,7 @@ def run(model: str, scenario: str, concurrency: int, context_length: int, steps:
         scen = Scenario.parse(scenario)
         res = asyncio.run(e2e._client(base, scen, concurrency, preset(model).vocab_size, context_length - 2, warmup * step_s,
                                       steps * step_s, 4321))
+        res["kv_transfer"] = [_server_info(u).get("kv_transfer") for u in prefill_urls]
     finally:
         for p in reversed(procs):
             e2e.stop_server(p)

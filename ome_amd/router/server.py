@@ -12,7 +12,7 @@ import time
 from dataclasses import dataclass, field
 from urllib.parse import urlsplit
 
-from aiohttp import ClientSession, ClientTimeout, web
+from aiohttp import ClientSession, ClientTimeout, TCPConnector, web
 
 from ome_amd.executor.dns import resolve_url
 from ome_amd.router.policy import Policy, make_policy
@@ -148,7 +148,9 @@ class Router:
             await asyncio.sleep(self.discovery.get("interval", 5.0))
 
     async def start(self, app=None) -> None:
-        self.session = ClientSession(timeout=self.timeout)
+        # no pool cap: aiohttp's default (100 connections) would park PD prefill calls behind
+        # >= 100 long-lived decode streams, and those streams wait for that very prefill's KV
+        self.session = ClientSession(timeout=self.timeout, connector=TCPConnector(limit=0, limit_per_host=0))
         self._tasks.append(asyncio.create_task(self._health_loop()))
         if self.discovery:
             await self._discover_once()

@@ -93,6 +93,8 @@ class KVTransfer:
         self.peers: dict = {}      # prefill side: (host, port) -> kvlink.PeerMapping
         self.ipc_sent = 0
         self.ipc_received = 0
+        self.bytes_sent = 0        # page-image bytes pushed (prefill side)
+        self.write_s = 0.0         # seconds inside the device-to-device page writes (IPC path)
         runner = engine.runner
         kv = runner.kv
         shapes = {(tuple(kv.k[i].shape[1:]), tuple(kv.v[i].shape[1:])) for i in kv.local_layers}
@@ -368,7 +370,13 @@ class KVTransfer:
                     self.peers[key] = peer
                 try:
                     stream = self._ipc_stream()
+                    t0 = time.perf_counter()
                     peer.write(ks, vs, rep["slots"], stream)
+                    dt = time.perf_counter() - t0
+                    nb = sum(t.numel() * t.element_size() for t in (*ks, *vs))
+                    with self.lock:
+                        self.write_s += dt
+                        self.bytes_sent += nb
                 except Exception as e:
                     _send_msg(s, {"ok": False, "error": str(e)})
                     raise
@@ -399,11 +407,22 @@ class KVTransfer:
                     if _recv_exact(s, 2) != b"OK":
                         raise ConnectionError("no ack")
                 self.sent += 1
+                with self.lock:
+                    self.bytes_sent += len(blob)
                 return
             except OSError as e:
                 log.warning("KV push to %s:%d failed (%s), retry %d", host, port, e, attempt + 1)
                 time.sleep(min(2.0, 0.1 * 2 ** attempt))
         log.error("KV push for room %s dropped", header["room"])
+
+    def stats(self) -> dict:
+        """Transfer counters for ``/get_server_info`` (``bench.py --pd`` reports the kvlink rate:
+        page-image bytes over the seconds spent in the device-to-device writes)."""
+        with self.lock:
+            return {"mode": self.mode, "sent": self.sent, "received": self.received, "ipc_sent": self.ipc_sent,
+                    "ipc_received": self.ipc_received, "bytes_sent": self.bytes_sent,
+                    "ipc_write_s": round(self.write_s, 6),
+                    "ipc_write_gbps": round(self.bytes_sent / self.write_s / 1e9, 3) if self.write_s > 0 else None}
 
     def close(self) -> None:
         if self._sock is not None:

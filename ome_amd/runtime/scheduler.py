@@ -256,6 +256,8 @@ class Scheduler:
             if r.state != ReqState.RUNNING or len(r.pages) * self.P < r.seq_len:
                 continue
             chunks.append(ScheduledChunk(r, r.seq_len - 1, 1, True))
+        # a later request's page growth may have preempted one already picked (LIFO victim)
+        chunks = [c for c in chunks if c.req.state == ReqState.RUNNING and len(c.req.pages) * self.P >= c.req.seq_len]
         return StepBatch("decode", chunks) if chunks else None
 
     # ------------------------------------------------------------------ post-step

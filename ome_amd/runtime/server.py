@@ -240,7 +240,9 @@ def create_app(engine, ns=None):
                 "max_running_requests": a.max_running_requests, "chunked_prefill_size": a.chunked_prefill_size,
                 "kv_pages": engine.runner.kv.num_pages, "cuda_graph_buckets": engine.runner.buckets,
                 "disaggregation_mode": a.disaggregation_mode,
-                "disaggregation_bootstrap_port": getattr(engine.kv_transfer, "port", None), **engine.health()}
+                "disaggregation_bootstrap_port": getattr(engine.kv_transfer, "port", None),
+                "kv_transfer": engine.kv_transfer.stats() if engine.kv_transfer is not None else None,
+                **engine.health()}
 
     @app.get("/metrics")
     async def metrics():

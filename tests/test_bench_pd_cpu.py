@@ -12,7 +12,7 @@ def test_pd_bench_end_to_end_cpu(tmp_path):
     from ome_amd.bench import pd
 
     r = pd.run("tiny-llama", "D(24,10)", concurrency=3, context_length=256, steps=2, warmup=1, step_s=3.0,
-               n_prefill=1, n_decode=1, max_total_tokens=4096, log_dir=str(tmp_path),
+               n_prefill=1, n_decode=1, max_total_tokens=4096, decode_total_tokens=4096, log_dir=str(tmp_path),
                extra=["--device", "cpu", "--disable-cuda-graph"])
     assert r["errors"] == 0 and r["tokens"] > 0, (r, open(tmp_path / "decode0.log").read()[-3000:])
     assert r["p50_ttft_ms"] is not None

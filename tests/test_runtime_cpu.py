@@ -72,6 +72,24 @@ def test_preemption_under_kv_pressure():
     assert pages.num_free + sum(len(r.pages) for r in s.running) == 11
 
 
+def test_decode_batch_drops_requests_preempted_while_scheduling():
+    """The newest request needs a page, the only victim is an older one already picked for this
+    decode step: the step must not carry the preempted (page-less) request."""
+    pages, slots = PagePool(5), ReqSlotPool(9, 64)
+    s = Scheduler(pages, slots, 16, max_running=8, chunked_prefill_size=1000, max_context=1000)
+    a = Request(prompt_ids=list(range(20)), params=SamplingParams(max_new_tokens=50))
+    b = Request(prompt_ids=list(range(32)), params=SamplingParams(max_new_tokens=50))
+    s.add(a)
+    s.add(b)
+    bt = s.schedule()
+    assert len(bt.chunks) == 2 and pages.num_free == 0
+    s.commit(bt, [1, 1], None, 0.0, set())
+    bt = s.schedule()
+    assert bt.mode == "decode" and [c.req for c in bt.chunks] == [b]
+    assert a.state.name == "WAITING" and s.num_preemptions == 1
+    assert all(len(c.req.pages) * 16 >= c.req.seq_len for c in bt.chunks)
+
+
 def test_stop_conditions():
     pages, slots = PagePool(100), ReqSlotPool(9, 64)
     s = Scheduler(pages, slots, 16, max_running=8, chunked_prefill_size=1000, max_context=1000)
