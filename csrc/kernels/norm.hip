@@ -181,11 +181,29 @@ OME_API int ome_rmsnorm(const void* x, int64_t x_stride, const void* w, void* ou
   return 0;
 }
 
+static int g_norm_threads = 0;  // 0 = measured default; 128 / 256 / 512 for experiments
+OME_API int ome_norm_set_threads(int nt) {
+  if (nt != 0 && nt != 128 && nt != 256 && nt != 512) return -1;
+  g_norm_threads = nt;
+  return 0;
+}
+
 OME_API int ome_fused_add_rmsnorm(void* x, int64_t x_stride, void* res, int64_t res_stride, const void* w,
                                   int rows, int H, float eps, hipStream_t stream) {
   if (H % 8 != 0 || rows <= 0) return rows == 0 ? 0 : -2;
-  if (rows < 512) {
+  if (g_norm_threads == 512) {
+    DISPATCH_CHUNKS(H, 512, (fused_add_rmsnorm_kernel<512, CH><<<rows, 512, 0, stream>>>(
+                                (bf16*)x, x_stride, (bf16*)res, res_stride, (const bf16*)w, H, eps)));
+  } else if (g_norm_threads == 256) {
+    DISPATCH_CHUNKS(H, 256, (fused_add_rmsnorm_kernel<256, CH><<<rows, 256, 0, stream>>>(
+                                (bf16*)x, x_stride, (bf16*)res, res_stride, (const bf16*)w, H, eps)));
+  } else if (g_norm_threads == 128) {
     DISPATCH_CHUNKS(H, 128, (fused_add_rmsnorm_kernel<128, CH><<<rows, 128, 0, stream>>>(
+                                (bf16*)x, x_stride, (bf16*)res, res_stride, (const bf16*)w, H, eps)));
+  } else if (rows < 512) {
+    // decode batches: 8 waves per row (3.05 vs 4.15 us for 128 threads at 256 x 4096,
+    // profiles/r03_small_kernels.txt)
+    DISPATCH_CHUNKS(H, 512, (fused_add_rmsnorm_kernel<512, CH><<<rows, 512, 0, stream>>>(
                                 (bf16*)x, x_stride, (bf16*)res, res_stride, (const bf16*)w, H, eps)));
   } else {
     DISPATCH_CHUNKS(H, 256, (fused_add_rmsnorm_kernel<256, CH><<<rows, 256, 0, stream>>>(

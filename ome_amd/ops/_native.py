@@ -25,6 +25,8 @@ _SIGNATURES = {
     "ome_kernels": {
         "ome_rmsnorm": [vp, i64, vp, vp, i64, i32, i32, f32, vp],
         "ome_fused_add_rmsnorm": [vp, i64, vp, i64, vp, i32, i32, f32, vp],
+        "ome_norm_set_threads": [i32],
+        "ome_rope_set_split": [i32],
         # KV-cache ops end in (kv_fmt, k_scale, v_scale, stream)
         "ome_rope_qkv_cache": [vp, i64, vp, vp, i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, f32,
                                i32, f32, f32, vp],
