@@ -176,3 +176,38 @@ OME_API int ome_fill_pending(int* ids, const int* src, const int* prev, int n, h
   OME_CHECK_LAUNCH();
   return 0;
 }
+
+// Byte copy between any two device-visible addresses, one of which may be pinned host memory
+// mapped into the GPU's address space (hipHostMalloc).  The per-step metadata H2D and the sampled
+// ids D2H go through this kernel instead of hipMemcpyAsync, so every per-step transfer is a plain
+// kernel dispatch on the compute stream (no copy-engine / runtime blit path, no per-step pinning).
+__global__ __launch_bounds__(256) void copy_mapped_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                          int64_t n16, const unsigned char* __restrict__ src_tail,
+                                                          unsigned char* __restrict__ dst_tail, int tail) {
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = i0; i < n16; i += (int64_t)gridDim.x * blockDim.x) dst[i] = src[i];
+  if (i0 < tail) dst_tail[i0] = src_tail[i0];
+}
+
+OME_API int ome_copy_mapped(const void* src, void* dst, int64_t nbytes, hipStream_t stream) {
+  if (nbytes <= 0) return 0;
+  // 16-B vectors when both ends are 16-B aligned, bytes otherwise
+  const bool vec = ((uintptr_t)src % 16 == 0) && ((uintptr_t)dst % 16 == 0);
+  const int64_t n16 = vec ? nbytes / 16 : 0;
+  const int64_t tail = nbytes - n16 * 16;
+  if (tail > (1 << 20)) return -2;  // unaligned bulk copies are not this kernel's job
+  const int64_t work = n16 > tail ? n16 : tail;
+  int grid = (int)((work + 255) / 256);
+  grid = grid < 1 ? 1 : (grid > 1024 ? 1024 : grid);
+  if (tail > (int64_t)grid * 256) grid = (int)((tail + 255) / 256);
+  copy_mapped_kernel<<<grid, 256, 0, stream>>>((const uint4*)src, (uint4*)dst, n16,
+                                               (const unsigned char*)src + n16 * 16, (unsigned char*)dst + n16 * 16,
+                                               (int)tail);
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// Device address of a pinned host allocation (identity on ROCm for hipHostMalloc memory).
+OME_API int ome_host_device_ptr(void* host, void** dev) {
+  return hipHostGetDevicePointer(dev, host, 0) == hipSuccess ? 0 : -1;
+}

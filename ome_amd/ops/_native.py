@@ -26,6 +26,8 @@ _SIGNATURES = {
         "ome_rmsnorm": [vp, i64, vp, vp, i64, i32, i32, f32, vp],
         "ome_fused_add_rmsnorm": [vp, i64, vp, i64, vp, i32, i32, f32, vp],
         "ome_norm_set_threads": [i32],
+        "ome_copy_mapped": [vp, vp, i64, vp],
+        "ome_host_device_ptr": [vp, vp],
         "ome_rope_set_split": [i32],
         # KV-cache ops end in (kv_fmt, k_scale, v_scale, stream)
         "ome_rope_qkv_cache": [vp, i64, vp, vp, i32, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, f32,

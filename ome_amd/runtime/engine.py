@@ -306,6 +306,9 @@ class Engine:
             return self._dp_step()
         prev = self._inflight
         ht = self.host_times
+        idle0 = None
+        if self.host_trace is not None and prev and prev[1].event is not None:
+            idle0 = bool(prev[1].event.query())
         ts = time.perf_counter()
         batch = self.scheduler.schedule()
         launched = None
@@ -317,7 +320,10 @@ class Engine:
             ht["schedule"] += t0 - ts
             ht["launch"] += time.perf_counter() - t0
             if self.host_trace is not None:
-                self.host_trace.append((batch.mode, len(batch.chunks), t0 - ts, time.perf_counter() - t0))
+                # did the GPU run dry before / while this step was enqueued (previous step done)?
+                ev = prev[1].event if prev else None
+                self.host_trace.append((batch.mode, len(batch.chunks), t0 - ts, time.perf_counter() - t0,
+                                        idle0, bool(ev.query()) if ev is not None else None))
         done: list[Request] = []
         if not self.overlap:
             if launched:

@@ -26,6 +26,7 @@ from ome_amd.parallel import state as pstate
 from ome_amd.runtime.page_pool import PagePool, ReqSlotPool
 from ome_amd.runtime.request import PENDING
 from ome_amd.runtime.scheduler import StepBatch
+from ome_amd.runtime.staging import copy_d2h, copy_h2d
 
 log = logging.getLogger("ome_amd.runtime")
 
@@ -152,6 +153,11 @@ class ModelRunner:
         self.pp = pstate.get().pp_size > 1
         self.pages = PagePool(num_pages)
         self.slots = ReqSlotPool(max_running + 1, max_pages_per_seq, self.device)
+        from ome_amd.runtime.staging import H2DStaging
+
+        self.staging = H2DStaging(self.device)
+        if self.is_cuda:
+            self.slots.staging = self.staging
         log.info("KV cache: %d pages x %d tokens (%.1f GiB), weights %.1f GiB", num_pages, page_size,
                  num_pages * page_bytes / 2**30, self.model.weight_bytes() / 2**30)
         # ---- decode graphs ----
@@ -306,12 +312,22 @@ class ModelRunner:
         flight) get it on the device from ``prev``'s output — no host round trip.
         ``allow_graph=False``: run eagerly even for a decode batch (DP attention steps whose MoE
         exchange must take the normal RCCL mode on every rank)."""
+        self.probe = None
+        if self.probe_log is not None:
+            self.probe = (time.perf_counter(), prev.event if prev is not None else None)
         self.slots.flush()
         if batch.mode == "decode" and not self.pp and all(c.length == 1 for c in batch.chunks):
             bs = next((b for b in self.buckets if b >= len(batch.chunks)), None)
             if bs is not None:
                 return self._launch_decode(batch, bs, prev, graph=allow_graph)
         return self._launch_eager(batch, prev)
+
+    probe_log: list | None = None   # (mode, host ms from launch start to the input copy, prev step done?)
+
+    def _probe_mark(self, mode: str) -> None:
+        if self.probe is not None:
+            t0, ev = self.probe
+            self.probe_log.append((mode, 1000 * (time.perf_counter() - t0), bool(ev.query()) if ev is not None else None))
 
     def idle_decode(self) -> None:
         """DP attention, low-latency EP: this rank has nothing scheduled while its peers decode --
@@ -325,7 +341,7 @@ class ModelRunner:
         h[off["req_idx"]:off["req_idx"] + bs] = self.slots.max_reqs - 1
         for name, v in (("temp", 0.0), ("top_p", 1.0), ("min_p", 0.0), ("rep", 1.0), ("freq", 0.0), ("pres", 0.0)):
             d.hf[off[name]:off[name] + bs] = v
-        d.dev.copy_(d.host, non_blocking=True)
+        copy_h2d(d.dev, d.host) if self.is_cuda else d.dev.copy_(d.host)
         if self.use_graph:
             self.graphs[bs].replay()
         else:
@@ -334,9 +350,12 @@ class ModelRunner:
     def _finish_launch(self, ids_dev: torch.Tensor, lp_dev: torch.Tensor, n: int) -> "StepHandle":
         hi, hl = self._host_out[self._ring]
         self._ring ^= 1
-        if n:
-            hi[:n].copy_(ids_dev[:n], non_blocking=True)
-            hl[:n].copy_(lp_dev[:n], non_blocking=True)
+        if n and self.is_cuda:
+            copy_d2h(hi[:n], ids_dev[:n].contiguous())
+            copy_d2h(hl[:n], lp_dev[:n].float().contiguous())
+        elif n:
+            hi[:n].copy_(ids_dev[:n])
+            hl[:n].copy_(lp_dev[:n])
         ev = None
         if self.is_cuda:
             ev = torch.cuda.Event()
@@ -423,7 +442,8 @@ class ModelRunner:
         # attention visits sequences longest-first (padding rows, seq_len 0, last)
         h[off["order"]:off["order"] + bs] = np.argsort(-h[off["seq_lens"]:off["seq_lens"] + bs], kind="stable")
         self._init_penalty_rows(batch.chunks)
-        d.dev.copy_(d.host, non_blocking=True)
+        self._probe_mark("decode")
+        copy_h2d(d.dev, d.host) if self.is_cuda else d.dev.copy_(d.host)
         if any_pending:
             ops.fill_pending(d.view("ids", bs), d.view("src", bs), prev.ids_dev)
         if self.use_graph and graph:
@@ -498,10 +518,8 @@ class ModelRunner:
                                  np.asarray(items, np.int32).reshape(-1) if n_it else np.zeros(0, np.int32),
                                  np.asarray(split, np.int32).reshape(-1) if n_sp else np.zeros(0, np.int32),
                                  np.asarray(comb, np.int32).reshape(-1) if n_cb else np.zeros(0, np.int32)])
-        host = torch.from_numpy(packed)
-        if self.is_cuda:
-            host = host.pin_memory()
-        dev = host.to(self.device, non_blocking=True)
+        self._probe_mark(batch.mode)
+        dev = self.staging.to_device(packed)
         o = 0
 
         def take(n):

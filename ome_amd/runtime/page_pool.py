@@ -48,6 +48,7 @@ class ReqSlotPool:
         self._rows: list[int] = []
         self._cols: list[int] = []
         self._vals: list[int] = []
+        self.staging = None   # runtime.staging.H2DStaging (set by the model runner on a GPU)
 
     def alloc(self) -> int | None:
         return self._free.pop() if self._free else None
@@ -66,11 +67,12 @@ class ReqSlotPool:
     def flush(self) -> None:
         if not self._rows:
             return
-        n = len(self._rows)
-        host = torch.tensor([self._rows, self._cols, self._vals], dtype=torch.int64)
-        if self.table.is_cuda:
-            host = host.pin_memory()
-        dev = host.to(self.table.device, non_blocking=True)
+        import numpy as np
+
+        host = np.asarray([self._rows, self._cols, self._vals], dtype=np.int64)
+        if self.staging is not None:
+            dev = self.staging.to_device(host)
+        else:
+            dev = torch.from_numpy(host).to(self.table.device)
         self.table.index_put_((dev[0], dev[1]), dev[2].to(torch.int32))
         self._rows, self._cols, self._vals = [], [], []
-        del n

@@ -51,6 +51,13 @@ def main():
     print("\nidle (gaps > 20 us) by (previous, following), ms:")
     for k, v in by_pair.most_common(15):
         print(f"  {v / 1e6:8.2f}  {k[0]}  ->  {k[1]}")
+    # context of the three largest gaps: the ops around each (start relative to the gap, duration)
+    idx = sorted(range(1, len(ops)), key=lambda i: ops[i][0] - max(o[1] for o in ops[max(0, i - 8):i]), reverse=True)
+    for i in idx[:3]:
+        g0 = max(o[1] for o in ops[max(0, i - 8):i])
+        print(f"\ncontext of a {(ops[i][0] - g0) / 1e3:.1f} us gap:")
+        for s_, e_, n_ in ops[max(0, i - 10):i + 4]:
+            print(f"  {(s_ - g0) / 1e3:10.1f} us  dur {(e_ - s_) / 1e3:8.1f}  {n_[:90]}")
     print(f"\ntop {top} gaps:")
     for g, p, n in sorted(gaps, reverse=True)[:top]:
         print(f"  {g / 1e3:9.1f} us  {p[:60]}  ->  {n[:60]}")
