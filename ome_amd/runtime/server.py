@@ -375,6 +375,16 @@ def create_app(engine, ns=None):
                 tp = ToolParser(tool_kind) if use_tools else None
                 content_all, content_sent, calls_started, raw_all = "", 0, False, ""
                 every_usage = bool((body.get("stream_options") or {}).get("continuous_usage_stats"))
+                try:
+                    async for chunk in body_chunks(first, rp, tp, content_all, content_sent, calls_started, raw_all,
+                                                   every_usage):
+                        yield chunk
+                finally:
+                    # client gone (generator closed mid-stream): stop generating for it
+                    if req.finish_reason is None:
+                        engine.abort(req.rid)
+
+            async def body_chunks(first, rp, tp, content_all, content_sent, calls_started, raw_all, every_usage):
                 while True:
                     _, fin = await stream.q.get()
                     while not fin and not stream.q.empty():   # coalesce steps the loop fell behind on
