@@ -165,6 +165,14 @@ def _upload(src: Path, target: str) -> str:
     from ome_amd.storage.uri import parse
 
     u = parse(target) if "://" in target else None
+    if u is not None and u.type in ("S3", "OCI", "GCS", "AZURE"):
+        from ome_amd.storage import objstore
+
+        remote = objstore.client_for(u.parts, u.type)
+        if remote is not None:   # real endpoint: parallel multipart upload
+            client, bucket, prefix = remote
+            objstore.upload_tree(client, bucket, prefix, src)
+            return target
     if u is None or u.type == "LOCAL":
         dst = Path(u.parts["path"] if u else target)
     elif u.type == "PVC":

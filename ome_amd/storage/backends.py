@@ -193,6 +193,27 @@ def object_store_path(uri: str) -> Path:
 
 
 def fetch_object_store(uri: str, dest: str, progress: Progress | None = None, **_) -> FetchResult:
+    """Remote endpoint configured (:func:`ome_amd.storage.objstore.client_for`): multipart ranged
+    parallel download with per-object MD5 verification.  Otherwise the filesystem object-store
+    root with its manifest."""
+    from ome_amd.storage import objstore
+
+    u = parse(uri)
+    remote = objstore.client_for(u.parts, u.type)
+    if remote is not None:
+        client, bucket, prefix = remote
+        try:
+            st = objstore.download_prefix(client, bucket, prefix, dest,
+                                          part_size=int(os.environ.get("OME_DOWNLOAD_PART_SIZE",
+                                                                       objstore.DEFAULT_PART_SIZE)),
+                                          workers=int(os.environ.get("OME_DOWNLOAD_WORKERS",
+                                                                     objstore.DEFAULT_WORKERS)),
+                                          progress=progress)
+        except objstore.ObjectStoreError as e:
+            raise FetchError(str(e)) from e
+        sha = hashlib.sha256(json.dumps(st["md5_manifest"], sort_keys=True).encode()).hexdigest()[:40]
+        return FetchResult(str(dest), sha=sha, files=st["files"], bytes=st["bytes"],
+                           extra={k: st[k] for k in ("parts", "fetched_parts", "verified")})
     src = object_store_path(uri)
     if not src.exists():
         raise FetchError(f"object {uri} not found (object-store root {object_store_root()})")
