@@ -65,8 +65,12 @@ class Cluster:
 
     def __init__(self, state_dir: str = "/tmp/ome-state", node_name: str = "mi355x-node-0", gpus: int | None = None,
                  simulate: bool = False, models_root: str | None = None, with_agent: bool = True,
-                 with_executor: bool = True, probe_scale: float = 1.0, agent_kw: dict | None = None):
-        self.store = Store()
+                 with_executor: bool = True, probe_scale: float = 1.0, agent_kw: dict | None = None,
+                 store: Store | None = None):
+        # a KubeStore (ome_amd.store.kube) runs the same controllers against a real API server;
+        # its writes skip the local hooks (the API server calls ours at /admission instead),
+        # which read the cluster state from the KubeStore's cache
+        self.store = store if store is not None else Store()
         webhooks.install(self.store)
         self.manager = Manager(self.store)
         self.state_dir = os.path.abspath(state_dir)
@@ -193,6 +197,13 @@ def create_api(cluster: Cluster):
 
     app = FastAPI(title="ome-amd manager")
     st = cluster.store
+
+    @app.post("/admission")
+    async def admission(review: dict):
+        """admission.k8s.io/v1 AdmissionReview (mutating + validating) for a real API server."""
+        from ome_amd.store.kube import admission_review
+
+        return admission_review(st, review)
 
     def err(e: Exception):
         code = {S.NotFound: 404, S.AlreadyExists: 409, S.Conflict: 409, S.Invalid: 422}.get(type(e), 400)
@@ -337,10 +348,18 @@ def main(argv=None) -> int:
     ap.add_argument("--port", type=int, default=9443)
     ap.add_argument("--simulate", action="store_true", help="do not launch pod processes (control-plane only)")
     ap.add_argument("--no-agent", action="store_true")
+    ap.add_argument("--kubeconfig", default=None, help="reconcile a real cluster through this kubeconfig")
+    ap.add_argument("--in-cluster", action="store_true", help="reconcile the cluster we run in (service account)")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    store = None
+    if args.kubeconfig or args.in_cluster:
+        from ome_amd.store import kube
+
+        client = kube.KubeClient.in_cluster() if args.in_cluster else kube.KubeClient.from_kubeconfig(args.kubeconfig)
+        store = kube.KubeStore(client, kube.MANAGER_KINDS)
     cl = Cluster(args.state_dir, args.node_name, args.gpus, simulate=args.simulate, models_root=args.models_root_dir,
-                 with_agent=not args.no_agent)
+                 with_agent=not args.no_agent and store is None, with_executor=store is None, store=store)
     for c in args.catalog:
         log.info("applied %d objects from %s", cl.load_catalog(c), c)
     cl.start()
