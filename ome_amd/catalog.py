@@ -245,9 +245,21 @@ def _formats(f: Family, priority: int = 2) -> list[dict]:
              **({"quantization": f.quantization} if f.quantization else {})}]
 
 
+def _priority(f: Family) -> int:
+    """Runtimes that auto-select for the same format / architecture / size range must carry
+    distinct priorities (the ServingRuntime admission rule, ``servingruntime_webhook.go:202``):
+    the first family keeps 2, later look-alikes (e.g. Llama-3 8B vs 3.1 8B) step up by one."""
+    def key(g: Family):
+        return (g.arch, g.quantization, size_label(g.params_b * 0.85), size_label(g.params_b * 1.15))
+
+    k = key(f)
+    same = [g.name for g in FAMILIES if key(g) == k]
+    return 2 + same.index(f.name) if f.name in same else 2
+
+
 def _spec_base(f: Family) -> dict:
     lo, hi = f.params_b * 0.85, f.params_b * 1.15
-    return {"disabled": False, "supportedModelFormats": _formats(f), "protocolVersions": ["openAI"],
+    return {"disabled": False, "supportedModelFormats": _formats(f, _priority(f)), "protocolVersions": ["openAI"],
             "modelSizeRange": {"min": size_label(lo), "max": size_label(hi)},
             "acceleratorRequirements": {"acceleratorClasses": ["amd-mi355x", "amd-mi300x"]}}
 
@@ -283,9 +295,10 @@ def pd_runtime(f: Family) -> dict:
 
 
 def multinode_runtime(f: Family) -> dict:
-    """Leader/worker (LeaderWorkerSet) bf16 serving over ``f.multinode`` nodes of 8 GPUs."""
+    """Leader/worker (LeaderWorkerSet) serving over ``f.multinode`` nodes of 8 GPUs (TP across the
+    nodes, the checkpoint's own precision: the family's model must admit to it)."""
     g = copy.copy(f)
-    g.bytes_per_param, g.quantization, g.args = 2.0, None, []
+    g.args = []
     n = f.multinode
     tp = 8 * n
     spec = _spec_base(g)
@@ -300,7 +313,7 @@ def multinode_runtime(f: Family) -> dict:
     spec["engineConfig"] = {"volumes": vol, "leader": {"runner": leader}, "worker": {"size": n - 1, "runner": worker}}
     spec["routerConfig"] = _router()
     return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterServingRuntime",
-            "metadata": {"name": f"ome-amd-{f.name}-bf16-{n}node"}, "spec": spec}
+            "metadata": {"name": f"ome-amd-{f.name}-{n}node"}, "spec": spec}
 
 
 def base_model(f: Family) -> dict:
@@ -316,6 +329,61 @@ def base_model(f: Family) -> dict:
     if not f.preset:
         spec["storage"]["key"] = "hf-token"
     return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterBaseModel", "metadata": {"name": f.name}, "spec": spec}
+
+
+def isvc_samples(f: Family) -> dict[str, dict]:
+    """InferenceService samples for a family (``config/samples/isvc/<vendor>/*.yaml``): the
+    default runtime, plus the PD-disaggregated and multi-node runtimes where the family has them."""
+    def isvc(name: str, rt: dict, extra: dict | None = None) -> dict:
+        spec = {"model": {"name": f.name}, "runtime": {"name": rt["metadata"]["name"]},
+                "engine": {"minReplicas": 1, "maxReplicas": 1}}
+        if "TEXT_TO_TEXT" in f.capabilities or "IMAGE_TEXT_TO_TEXT" in f.capabilities:
+            spec["router"] = {"minReplicas": 1, "maxReplicas": 1}
+        spec.update(extra or {})
+        return {"apiVersion": "ome.io/v1beta1", "kind": "InferenceService",
+                "metadata": {"name": name, "namespace": name}, "spec": spec}
+
+    out = {f.name: isvc(f.name, runtime(f))}
+    if f.pd:
+        out[f"{f.name}-pd"] = isvc(f"{f.name}-pd", pd_runtime(f),
+                                   {"decoder": {"minReplicas": 1, "maxReplicas": 1},
+                                    "router": {"minReplicas": 1, "maxReplicas": 1}})
+    if f.multinode:
+        out[f"{f.name}-{f.multinode}node"] = isvc(f"{f.name}-{f.multinode}node", multinode_runtime(f))
+    return out
+
+
+SCENARIOS = ["N(480,240)/(300,150)", "D(100,100)", "D(100,1000)", "D(2000,200)", "D(7800,200)"]
+CONCURRENCY = [1, 2, 4, 8, 16, 32, 64, 128, 256]
+
+
+def benchmark_samples() -> dict[str, list[dict]]:
+    """BenchmarkJob samples: the protocol sweep on a text model, an embeddings run, the PD
+    DeepSeek deployment and the Hugging Face secret the tokenizer download uses."""
+    def job(name, isvc, task, scenarios, conc, ns, extra=None):
+        spec = {"huggingFaceSecretReference": {"name": "huggingface-secret"},
+                "endpoint": {"inferenceService": {"name": isvc, "namespace": isvc}}, "task": task,
+                "trafficScenarios": scenarios, "numConcurrency": conc, "maxTimePerIteration": 15,
+                "maxRequestsPerIteration": 100, "additionalRequestParams": {"temperature": "0.0"},
+                "outputLocation": {"storageUri": f"oci://n/ome-ns/b/ome-benchmark-results/o/{name}",
+                                   "parameters": {"auth": "instance_principal"}}}
+        spec.update(extra or {})
+        return {"apiVersion": "ome.io/v1beta1", "kind": "BenchmarkJob", "metadata": {"name": name, "namespace": ns},
+                "spec": spec}
+
+    secret = {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "huggingface-secret", "namespace": "default"},
+              "type": "Opaque", "data": {"HUGGINGFACE_API_KEY": "cmVwbGFjZS1tZQ=="}}
+    return {
+        "llama3-8b-instruct": [job("llama-3-8b-benchmark", "llama-3-8b-instruct", "text-to-text", SCENARIOS,
+                                   CONCURRENCY, "llama-3-8b-instruct")],
+        "llama3-70b-instruct-pd": [job("llama-3-70b-pd-benchmark", "llama-3-70b-instruct-pd", "text-to-text",
+                                       SCENARIOS, CONCURRENCY, "llama-3-70b-instruct-pd")],
+        "e5-mistral-7b-instruct": [job("e5-mistral-7b-benchmark", "e5-mistral-7b-instruct", "text-to-embeddings",
+                                       ["E(64)", "E(512)", "E(1024)"], [1, 8, 32, 128], "e5-mistral-7b-instruct")],
+        "deepseek-v3": [job("deepseek-v3-benchmark", "deepseek-v3", "text-to-text", SCENARIOS[:3],
+                            [1, 16, 64, 256], "deepseek-v3", {"maxTimePerIteration": 30})],
+        "huggingface-secret": [secret],
+    }
 
 
 def generate() -> tuple[dict[str, list[dict]], dict[str, list[dict]]]:
@@ -344,6 +412,17 @@ def write(out: Path) -> list[Path]:
         paths.append(p)
     for vendor, docs in models.items():
         p = out / "models" / vendor / "catalog.yaml"
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(hdr + yaml.safe_dump_all(docs, sort_keys=False))
+        paths.append(p)
+    for f in FAMILIES:
+        for stem, doc in isvc_samples(f).items():
+            p = out / "samples" / "isvc" / f.vendor / f"{stem}.yaml"
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_text(hdr + yaml.safe_dump(doc, sort_keys=False))
+            paths.append(p)
+    for stem, docs in benchmark_samples().items():
+        p = out / "samples" / "benchmark" / f"{stem}.yaml"
         p.parent.mkdir(parents=True, exist_ok=True)
         p.write_text(hdr + yaml.safe_dump_all(docs, sort_keys=False))
         paths.append(p)
