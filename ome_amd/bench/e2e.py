@@ -25,6 +25,18 @@ import time
 from ome_amd.bench.scenarios import Scenario
 
 
+_REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def child_env(extra: dict | None = None) -> dict:
+    """Environment for server / router children: the repo importable from any working directory
+    (e.g. under ``cd /tmp && rocprofv3 ... -- python3 /path/bench.py``)."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = _REPO + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    env.update(extra or {})
+    return env
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -38,7 +50,7 @@ def start_server(model: str, concurrency: int, context_length: int, extra: list[
            "127.0.0.1", "--port", str(port), "--max-running-requests", str(concurrency), "--context-length",
            str(context_length), *(extra or [])]
     out = open(log_path, "w") if log_path else subprocess.DEVNULL
-    p = subprocess.Popen(cmd, stdout=out, stderr=subprocess.STDOUT, start_new_session=True)
+    p = subprocess.Popen(cmd, stdout=out, stderr=subprocess.STDOUT, start_new_session=True, env=child_env())
     return p, f"http://127.0.0.1:{port}"
 
 

@@ -52,8 +52,7 @@ def run(model: str, scenario: str, concurrency: int, context_length: int, steps:
     try:
         roles = [("prefill", i) for i in range(n_prefill)] + [("decode", j) for j in range(n_decode)]
         for idx, (role, i) in enumerate(roles):
-            env = dict(os.environ)
-            env["HIP_VISIBLE_DEVICES"] = str(idx % ngpu)
+            env = e2e.child_env({"HIP_VISIBLE_DEVICES": str(idx % ngpu)})
             port = e2e._free_port()
             args = [sys.executable, "-m", "ome_amd.runtime.server", "--model-path", f"random://{model}", "--host",
                     "127.0.0.1", "--port", str(port), "--max-running-requests", str(concurrency),
@@ -75,7 +74,7 @@ def run(model: str, scenario: str, concurrency: int, context_length: int, steps:
         for u in decode_urls:
             rargs += ["--decode", u]
         out = open(os.path.join(log_dir, "router.log"), "w") if log_dir else subprocess.DEVNULL
-        rp = subprocess.Popen(rargs, stdout=out, stderr=subprocess.STDOUT, start_new_session=True)
+        rp = subprocess.Popen(rargs, stdout=out, stderr=subprocess.STDOUT, start_new_session=True, env=e2e.child_env())
         procs.append(rp)
         base = f"http://127.0.0.1:{rport}"
         e2e.wait_ready(base, rp, timeout=120)

@@ -15,6 +15,7 @@ the token ids do not capture.
 from __future__ import annotations
 
 import hashlib
+import heapq
 import itertools
 from array import array
 
@@ -25,6 +26,11 @@ class PrefixCache:
         self.by_hash: dict[bytes, int] = {}        # chain digest -> page
         self.meta: dict[int, list] = {}            # page -> [hash, refcount, last_use, depth]
         self._clock = itertools.count()
+        # eviction candidates: (last_use, -depth, page), pushed whenever a page becomes unpinned;
+        # stale entries (re-pinned, re-used, evicted) are skipped when popped.  O(log n) per page
+        # instead of sorting every cached page on each allocation miss (which stalled the engine
+        # for tens of ms per step once the pool was full of cached prefixes).
+        self._heap: list[tuple[int, int, int]] = []
         self.hits = 0
         self.queries = 0
 
@@ -72,37 +78,53 @@ class PrefixCache:
                     continue
                 self.by_hash[h] = page
                 self.meta[page] = [h, 0, t, i]
+                heapq.heappush(self._heap, (t, -i, page))
                 kept.add(page)
             elif cur == page:
                 m = self.meta[page]
                 m[1] = max(0, m[1] - 1)
                 m[2] = t
+                if m[1] == 0:
+                    heapq.heappush(self._heap, (t, -m[3], page))
                 kept.add(page)
         # pages the request matched beyond its own computed prefix are still pinned: release
         for p in pages:
             if p in self.meta and p not in kept:
-                self.meta[p][1] = max(0, self.meta[p][1] - 1)
+                self._unpin(p)
                 kept.add(p)
         return kept
 
+    def _unpin(self, p: int) -> None:
+        m = self.meta[p]
+        m[1] = max(0, m[1] - 1)
+        if m[1] == 0:
+            heapq.heappush(self._heap, (m[2], -m[3], p))
+
     def release(self, pages: list[int]) -> None:
         for p in pages:
-            m = self.meta.get(p)
-            if m is not None:
-                m[1] = max(0, m[1] - 1)
+            if p in self.meta:
+                self._unpin(p)
 
     def owns(self, page: int) -> bool:
         return page in self.meta
 
     def evict(self, n: int) -> int:
+        """Free up to ``n`` unpinned pages, least recently used (deepest first among equals)."""
         if n <= 0:
             return 0
-        cand = sorted((m[2], -m[3], p) for p, m in self.meta.items() if m[1] == 0)
         freed = []
-        for _, _, p in cand[:n]:
+        heap = self._heap
+        while heap and len(freed) < n:
+            t, negd, p = heapq.heappop(heap)
+            m = self.meta.get(p)
+            if m is None or m[1] != 0 or m[2] != t:
+                continue            # stale: evicted, re-pinned or re-used since this push
             h = self.meta.pop(p)[0]
             self.by_hash.pop(h, None)
             freed.append(p)
+        if len(heap) > 4 * max(64, len(self.meta)):   # drop accumulated stale entries
+            self._heap = [(m[2], -m[3], p) for p, m in self.meta.items() if m[1] == 0]
+            heapq.heapify(self._heap)
         self.pool.free(freed)
         return len(freed)
 

@@ -112,6 +112,32 @@ def test_prefix_cache_unit():
     assert pc.evict(5) == 3 and pc.num_pages == 0
 
 
+def test_prefix_cache_eviction_lru_and_scales():
+    """Eviction pops least-recently-used unpinned pages (deepest first among equals), never a
+    pinned one, and stays cheap with a pool full of cached prefixes (the e2e sweep found
+    per-allocation full sorts stalling the engine once ~120k pages were cached)."""
+    import time as _t
+
+    pool = PagePool(200_001)
+    pc = PrefixCache(pool, 4)
+    seqs = []
+    for r in range(25_000):            # 25k cached 2-page prefixes = 50k cached pages
+        toks = [r * 8 + j for j in range(8)]
+        pages = pool.alloc(2)
+        pc.insert(toks, pages)
+        seqs.append((toks, pages))
+    hot = pc.match(seqs[0][0])         # pin the oldest prefix: it must survive
+    t0 = _t.perf_counter()
+    freed = sum(pc.evict(4) for _ in range(2000))
+    assert _t.perf_counter() - t0 < 1.0
+    assert freed == 8000 and all(p in pc.meta for p in hot)
+    # the 4000 oldest unpinned prefixes went first; within a prefix the deeper page first
+    assert seqs[1][1][1] not in pc.meta and seqs[1][1][0] not in pc.meta
+    assert seqs[4001][1][0] in pc.meta
+    pc.release(hot)                    # unpinned, but recently used: not the next victim
+    assert pc.evict(1) == 1 and seqs[4001][1][1] not in pc.meta and all(p in pc.meta for p in hot)
+
+
 def test_prefix_cache_image_digest_salt():
     """Same token ids (placeholder-id collision forced), different pixels: no KV page sharing
     from the first image position on; text pages before the image stay shared."""
