@@ -143,32 +143,49 @@ def fetch_random(uri: str, dest: str, progress: Progress | None = None, **_) -> 
 
 
 def fetch_hf(uri: str, dest: str, progress: Progress | None = None, token: str | None = None, **_) -> FetchResult:
+    """Online: our own hub client (:mod:`ome_amd.storage.hfhub`: repo listing, multipart ranged
+    parallel download, LFS SHA-256 verification) against ``HF_ENDPOINT``.  Offline
+    (``HF_HUB_OFFLINE=1``): the local ``huggingface_hub`` cache."""
     u = parse(uri)
+    repo, rev = u.parts["model_id"], u.parts["branch"]
+    if os.environ.get("HF_HUB_OFFLINE") != "1":
+        from ome_amd.storage import hfhub
+
+        try:
+            st = hfhub.snapshot_download(repo, dest, rev, token=token,
+                                         allow_patterns=_split_env("OME_HF_ALLOW_PATTERNS"),
+                                         ignore_patterns=_split_env("OME_HF_IGNORE_PATTERNS"),
+                                         workers=int(os.environ.get("OME_DOWNLOAD_WORKERS", "8")),
+                                         part_size=int(os.environ.get("OME_DOWNLOAD_PART_SIZE", 64 << 20)),
+                                         progress=progress)
+            return FetchResult(str(dest), sha=st["sha"], files=st["files"], bytes=st["bytes"],
+                               extra={k: st[k] for k in ("parts", "fetched_parts", "verified")})
+        except hfhub.HfHubError as e:
+            if e.status in (401, 403, 404):
+                raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}") from e
+            raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}") from e
+        except (hfhub.O.ObjectStoreError, OSError) as e:
+            raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}") from e
     try:
         from huggingface_hub import snapshot_download
-        from huggingface_hub import HfApi
     except ImportError as e:  # pragma: no cover
-        raise FetchError("huggingface_hub is not installed") from e
-    repo, rev = u.parts["model_id"], u.parts["branch"]
-    sha = ""
-    offline = os.environ.get("HF_HUB_OFFLINE") == "1"
-    if not offline:
-        try:
-            sha = HfApi(token=token).model_info(repo, revision=rev).sha or ""
-        except Exception:  # noqa: BLE001 — no network: fall back to the local cache
-            offline = True
+        raise FetchError("huggingface_hub is not installed (needed for the offline cache)") from e
     try:
-        path = snapshot_download(repo_id=repo, revision=rev, local_dir=dest, token=token, local_files_only=offline)
+        path = snapshot_download(repo_id=repo, revision=rev, local_dir=dest, token=token, local_files_only=True)
     except Exception as e:  # noqa: BLE001
-        raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}") from e
-    if not sha:
-        ref = Path(path) / ".cache" / "huggingface"
-        sha = ref.name if ref.exists() else hashlib.sha256(f"{repo}@{rev}".encode()).hexdigest()[:40]
+        raise FetchError(f"Hugging Face cache lookup of {repo}@{rev} failed: {e}") from e
+    ref = Path(path) / ".cache" / "huggingface"
+    sha = ref.name if ref.exists() else hashlib.sha256(f"{repo}@{rev}".encode()).hexdigest()[:40]
     n = sum(1 for p in Path(path).rglob("*") if p.is_file())
     if progress:
         progress({"phase": "Finalizing", "totalFiles": n, "completedFiles": n, "totalBytes": 0, "completedBytes": 0,
                   "speedBytesPerSec": 0.0})
     return FetchResult(str(path), sha=sha, files=n)
+
+
+def _split_env(name: str) -> list[str] | None:
+    v = os.environ.get(name)
+    return [x for x in v.split(",") if x] if v else None
 
 
 def object_store_root() -> Path:

@@ -57,6 +57,7 @@ class ObjectInfo:
     size: int
     md5_hex: str | None = None      # whole-object MD5 when the provider knows it
     etag: str = ""
+    sha256_hex: str | None = None   # content SHA-256 (Hugging Face LFS objects)
 
 
 def _md5_of(etag_or_md5: str | None, b64: bool) -> str | None:
@@ -409,6 +410,23 @@ def _file_md5(path: Path) -> str:
     return h.hexdigest()
 
 
+def _file_sha256(path: Path) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(8 << 20), b""):
+            h.update(b)
+    return h.hexdigest()
+
+
+def _digest_ok(path: Path, obj: ObjectInfo) -> bool | None:
+    """None: nothing to verify against; else whether the file matches the known digest."""
+    if obj.sha256_hex:
+        return _file_sha256(path) == obj.sha256_hex
+    if obj.md5_hex:
+        return _file_md5(path) == obj.md5_hex
+    return None
+
+
 def download_object(client: ObjectStoreClient, bucket: str, obj: ObjectInfo, dest: str | Path,
                     part_size: int = DEFAULT_PART_SIZE, workers: int = DEFAULT_WORKERS,
                     progress: Progress | None = None, verify: bool = True) -> dict:
@@ -416,9 +434,9 @@ def download_object(client: ObjectStoreClient, bucket: str, obj: ObjectInfo, des
     Returns ``{"parts", "fetched_parts", "bytes", "md5_verified"}``."""
     dest = Path(dest)
     dest.parent.mkdir(parents=True, exist_ok=True)
-    if dest.exists() and dest.stat().st_size == obj.size and (not verify or obj.md5_hex is None
-                                                              or _file_md5(dest) == obj.md5_hex):
-        return {"parts": 0, "fetched_parts": 0, "bytes": 0, "md5_verified": obj.md5_hex is not None, "skipped": True}
+    if dest.exists() and dest.stat().st_size == obj.size and (not verify or _digest_ok(dest, obj) in (None, True)):
+        return {"parts": 0, "fetched_parts": 0, "bytes": 0,
+                "md5_verified": bool(obj.md5_hex or obj.sha256_hex), "skipped": True}
     pdir = dest.with_name(dest.name + ".ome-parts")
     pdir.mkdir(exist_ok=True)
     ranges = [(i, a, min(a + part_size, obj.size) - 1) for i, a in enumerate(range(0, max(obj.size, 1), part_size))]
@@ -450,13 +468,11 @@ def download_object(client: ObjectStoreClient, bucket: str, obj: ObjectInfo, des
         for i, _, _ in ranges:
             with open(pdir / f"part-{i:05d}", "rb") as src:
                 shutil.copyfileobj(src, out, 8 << 20)
-    ok = None
-    if verify and obj.md5_hex is not None:
-        ok = _file_md5(part) == obj.md5_hex
-        if not ok:
-            part.unlink(missing_ok=True)
-            shutil.rmtree(pdir, ignore_errors=True)
-            raise ObjectStoreError(f"MD5 mismatch for {obj.name}")
+    ok = _digest_ok(part, obj) if verify else None
+    if ok is False:
+        part.unlink(missing_ok=True)
+        shutil.rmtree(pdir, ignore_errors=True)
+        raise ObjectStoreError(f"{'SHA-256' if obj.sha256_hex else 'MD5'} mismatch for {obj.name}")
     os.replace(part, dest)
     shutil.rmtree(pdir, ignore_errors=True)
     return {"parts": len(ranges), "fetched_parts": fetched[0], "bytes": obj.size, "md5_verified": bool(ok)}
