@@ -19,7 +19,25 @@ __device__ __forceinline__ float dot8(bf16x8 a, bf16x8 b, float acc) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(a, a, 6, 7), __builtin_shufflevector(b, b, 6, 7), acc, false);
 }
 
-template <int M, int R, int U>   // U: K steps in flight (fewer for more rows: VGPR budget)
+// SwiGLU operand on the fly: X holds [gate | up] (2K wide); the dot product sees
+// bf16(silu(g) * u), bit-identical to act_and_mul followed by the plain GEMV.
+__device__ __forceinline__ bf16x8 silu_mul8(bf16x8 g, bf16x8 u) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float gf = (float)g[j];
+    o[j] = (bf16)(gf / (1.f + __expf(-gf)) * (float)u[j]);
+  }
+  return o;
+}
+
+template <bool ACT>
+__device__ __forceinline__ bf16x8 ldx8(const bf16* p, int K) {
+  if constexpr (ACT) return silu_mul8(ld8(p), ld8(p + K));
+  else return ld8(p);
+}
+
+template <int M, int R, int U, bool ACT = false>   // U: K steps in flight (fewer for more rows: VGPR budget)
 __global__ __launch_bounds__(256) void gemv_kernel(const bf16* __restrict__ X, int64_t ldx, const bf16* __restrict__ W,
                                                    const bf16* __restrict__ bias, bf16* __restrict__ out, int64_t ldo,
                                                    int N, int K) {
@@ -46,7 +64,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16* __restrict__ X, i
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int m = 0; m < M; ++m) x[u][m] = ld8(X + m * ldx + k + 512 * u);
+      for (int m = 0; m < M; ++m) x[u][m] = ldx8<ACT>(X + m * ldx + k + 512 * u, K);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -59,7 +77,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16* __restrict__ X, i
 #pragma unroll
     for (int r = 0; r < R; ++r) w[r] = ld8(wr[r] + k);
 #pragma unroll
-    for (int m = 0; m < M; ++m) x[m] = ld8(X + m * ldx + k);
+    for (int m = 0; m < M; ++m) x[m] = ldx8<ACT>(X + m * ldx + k, K);
 #pragma unroll
     for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -81,16 +99,16 @@ __global__ __launch_bounds__(256) void gemv_kernel(const bf16* __restrict__ X, i
 }  // namespace
 
 // X [M, K] (row stride ldx, 16-byte aligned rows), W [N, K] contiguous, out [M, N] (row stride ldo);
-// 1 <= M <= 8, K % 8 == 0.
-OME_API int ome_gemv(const void* X, int64_t ldx, const void* W, const void* bias, void* out, int64_t ldo, int M, int N,
-                     int K, hipStream_t stream) {
-  if (M <= 0 || N <= 0) return 0;
-  if (M > 8 || K % 8 || ldx % 8 || K <= 0) return -2;
+// 1 <= M <= 8, K % 8 == 0.  act = 1: X is the fused gate/up projection [M, 2K] and the operand is
+// SiLU(gate) * up (the down projection with the SwiGLU folded into its operand load).
+template <bool ACT>
+static int gemv_launch(const void* X, int64_t ldx, const void* W, const void* bias, void* out, int64_t ldo, int M,
+                       int N, int K, hipStream_t stream) {
   // narrow weights: 2 rows per wave (twice the waves to spread over 256 CUs); long rows (K >= 8192,
   // the down projection) with <= 2 activation rows: 8 K steps in flight per wave
   const bool narrow = N <= 4096, deep = K >= 8192 && M <= 2;
 #define GV_L(MV, RV, UV)                                                                                    \
-  gemv_kernel<MV, RV, UV><<<dim3((N + 4 * RV - 1) / (4 * RV)), 256, 0, stream>>>(                          \
+  gemv_kernel<MV, RV, UV, ACT><<<dim3((N + 4 * RV - 1) / (4 * RV)), 256, 0, stream>>>(                     \
       (const bf16*)X, ldx, (const bf16*)W, (const bf16*)bias, (bf16*)out, ldo, N, K)
 #define GV(MV)                                                                              \
   if (MV <= 2 && deep) { if (narrow) GV_L(MV, 2, 8); else GV_L(MV, 4, 8); }                \
@@ -110,4 +128,18 @@ OME_API int ome_gemv(const void* X, int64_t ldx, const void* W, const void* bias
 #undef GV
   OME_CHECK_LAUNCH();
   return 0;
+}
+
+OME_API int ome_gemv(const void* X, int64_t ldx, const void* W, const void* bias, void* out, int64_t ldo, int M, int N,
+                     int K, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 8 || K % 8 || ldx % 8 || K <= 0) return -2;
+  return gemv_launch<false>(X, ldx, W, bias, out, ldo, M, N, K, stream);
+}
+
+OME_API int ome_gemv_act(const void* X, int64_t ldx, const void* W, const void* bias, void* out, int64_t ldo, int M,
+                         int N, int K, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 8 || K % 8 || ldx % 8 || K <= 0 || ldx < 2 * (int64_t)K) return -2;
+  return gemv_launch<true>(X, ldx, W, bias, out, ldo, M, N, K, stream);
 }

@@ -10,6 +10,7 @@ vocab-parallel embedding and LM head.  KV heads are replicated when tp > num_kv_
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -17,8 +18,13 @@ import torch.nn.functional as F
 from ome_amd import ops
 from ome_amd.models.common import AttnMeta, PagedKVCache
 from ome_amd.models.config import ModelConfig, rope_cos_sin
-from ome_amd.models.quant import Fp8Weight, dequant_fp8_stream, fp8_block_size, linear, quantize_weight
+from ome_amd.models.quant import _GEMV_ROWS, Fp8Weight, dequant_fp8_stream, fp8_block_size, linear, quantize_weight
 from ome_amd.parallel import state as pstate
+
+# fused SwiGLU + down GEMV at batch <= 4: opt-in.  Measured slower at c=1 (256.9 vs 279.0 tok/s):
+# every wave of the GEMV recomputes SiLU over the whole K (N/R waves x K exps), which costs more
+# VALU time than the act_and_mul launch it removes.
+_GEMV_ACT = os.environ.get("OME_GEMV_ACT", "0") == "1"
 
 
 def _dtype(name: str) -> torch.dtype:
@@ -258,8 +264,16 @@ class LlamaForCausalLM:
         """gate_up -> SiLU*mul -> down: this rank's partial sums (before the TP all-reduce),
         written straight into the all-reduce's staging buffer when there is one."""
         gu = linear(x, self.w_gu[i])
+        wd = self.w_d[i]
+        if _GEMV_ACT and self.act == 0 and gu.is_cuda and type(wd) is torch.Tensor and gu.dim() == 2 and \
+                gu.shape[0] <= _GEMV_ROWS and gu.dtype == wd.dtype == torch.bfloat16 and gu.stride(1) == 1 and \
+                gu.stride(0) % 8 == 0 and gu.data_ptr() % 16 == 0 and wd.data_ptr() % 16 == 0:
+            # decode at batch <= 4: SwiGLU folded into the down-projection GEMV's operand load
+            st = pstate.tp_ar_staging((gu.shape[0], self.cfg.hidden_size), self.dtype, gu.device) \
+                if self.tp.tp > 1 else None
+            return ops.gemv_act(gu, wd, out=st)
         a = ops.act_and_mul(gu, self.act)
-        return self._row_parallel(a, self.w_d[i])
+        return self._row_parallel(a, wd)
 
     def _row_parallel(self, a: torch.Tensor, w, bias=None) -> torch.Tensor:
         if self.tp.tp > 1:

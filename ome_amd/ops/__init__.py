@@ -703,6 +703,22 @@ def gemv(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
     return out
 
 
+def gemv_act(gu: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """out = (SiLU(gu[:, :I]) * gu[:, I:]) . w^T for M <= 8 rows: the decode down projection with
+    the SwiGLU folded into the GEMV's operand load (no act_and_mul launch, no intermediate)."""
+    M, I2 = gu.shape
+    I = I2 // 2
+    N = w.shape[0]
+    if not _gpu(gu):
+        return torch.nn.functional.linear(ref.act_and_mul(gu, 0).float(), w.float()).to(gu.dtype)
+    assert gu.stride(1) == 1 and gu.stride(0) % 8 == 0 and w.is_contiguous() and w.shape[1] == I and I % 8 == 0
+    assert gu.dtype == w.dtype == torch.bfloat16 and gu.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+    out = torch.empty(M, N, dtype=gu.dtype, device=gu.device) if out is None else out
+    call("ome_gemv_act", gu.data_ptr(), gu.stride(0), w.data_ptr(), None, out.data_ptr(), out.stride(0), M, N, I,
+         stream_ptr())
+    return out
+
+
 # ---- decode GEMM routing: ome_stream_gemm where it measured faster than hipBLASLt --------------
 # Filled during the engine's eager pre-capture pass (``decode_gemm_tuning``): every (M, N, K, bias)
 # a decode bucket issues is timed once against the library GEMM and the winner recorded; graphs

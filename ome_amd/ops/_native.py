@@ -63,6 +63,7 @@ _SIGNATURES = {
         "ome_skinny_gemm": [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp, vp],
         "ome_stream_gemm": [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp],
         "ome_gemv": [vp, i64, vp, vp, vp, i64, i32, i32, i32, vp],
+        "ome_gemv_act": [vp, i64, vp, vp, vp, i64, i32, i32, i32, vp],
         "ome_gemm": [vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, i32, vp, vp],
         "ome_gemm_set_variant": [i32],
         "ome_fp8_gemm_mx": [vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, vp, i64, vp, vp],

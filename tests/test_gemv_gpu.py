@@ -25,3 +25,22 @@ def test_gemv_matches_reference(M, N, K):
         got = ops.gemv(x, w, bias, out=big[:, :N]).float()
         assert (got - ref).abs().max().item() < 1e-2 * max(1.0, ref.abs().max().item())
         assert (big[:, N:] == 7.0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,I", [(4096, 14336), (2048, 8192), (1024, 512)])
+def test_gemv_act_equals_act_then_gemv(M, N, I):
+    """Down projection with SwiGLU folded into the operand load: bit-identical to act_and_mul
+    followed by the plain GEMV (same bf16 rounding of the activation), close to fp32."""
+    from ome_amd import ops
+    from ome_amd.ops import reference as ref
+
+    torch.manual_seed(M * 7 + N)
+    gu = torch.randn(M, 2 * I, device="cuda", dtype=torch.bfloat16) * 2
+    w = torch.randn(N, I, device="cuda", dtype=torch.bfloat16) * 0.05
+    fused = ops.gemv_act(gu, w)
+    two = ops.gemv(ops.act_and_mul(gu, 0), w)
+    assert torch.equal(fused, two)
+    want = torch.nn.functional.linear(ref.act_and_mul(gu.float().cpu(), 0), w.float().cpu())
+    assert torch.allclose(fused.float().cpu(), want, atol=2e-2 * want.abs().max().item(), rtol=2e-2)
