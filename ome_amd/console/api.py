@@ -391,6 +391,42 @@ def create_router(store, catalog_roots: list[str] | None = None, models_root: st
     def get_accelerator(name: str):
         return get_obj("AcceleratorClass", name)
 
+    # ------------------------------------------------------------------ benchmarks
+    @r.get("/benchmarks")
+    def list_benchmarks(namespace: str | None = None):
+        return items("BenchmarkJob", namespace)
+
+    @r.get("/benchmarks/{name}")
+    def get_benchmark(name: str, namespace: str = "default"):
+        return get_obj("BenchmarkJob", name, namespace)
+
+    @r.post("/benchmarks", status_code=201)
+    async def create_benchmark(req: Request, namespace: str = "default"):
+        data = await body(req)
+        return post_obj("BenchmarkJob", data, data.get("metadata", {}).get("namespace") or namespace)
+
+    @r.delete("/benchmarks/{name}")
+    def delete_benchmark(name: str, namespace: str = "default"):
+        return del_obj("BenchmarkJob", name, namespace)
+
+    @r.get("/summary")
+    def summary():
+        """Dashboard counters: objects per kind and how many are ready."""
+        def ready(o):
+            st = o.get("status") or {}
+            if st.get("state"):
+                return st["state"] == "Ready"
+            return any(c.get("type") == "Ready" and c.get("status") == "True" for c in st.get("conditions") or [])
+
+        out = {}
+        for key, kind in (("models", "ClusterBaseModel"), ("namespacedModels", "BaseModel"),
+                          ("runtimes", "ClusterServingRuntime"), ("services", "InferenceService"),
+                          ("accelerators", "AcceleratorClass"), ("benchmarks", "BenchmarkJob")):
+            objs = store.list(API, kind)
+            out[key] = {"total": len(objs), "ready": sum(1 for o in objs if ready(o))}
+        out["nodes"] = len(store.list("v1", "Node"))
+        return out
+
     # ------------------------------------------------------------------ validation
     @r.post("/validate/yaml")
     async def validate_yaml(req: Request):

@@ -237,3 +237,32 @@ def test_remote_store_console(cl):
         rs.close()
         srv.should_exit = True
         t.join(timeout=5)
+
+
+def test_spa_assets_summary_and_benchmarks(client, cl):
+    """The multi-page console: shell + app.js + style.css served; dashboard counters and the
+    benchmark-job routes the views call."""
+    assert 'src="static/app.js"' in client.get("/").text
+    js = client.get("/static/app.js")
+    assert js.status_code == 200 and "ServiceDeploy" in js.text and "ROUTES" in js.text
+    assert client.get("/static/style.css").status_code == 200
+    assert client.get("/static/../api.py").status_code == 404
+    s = client.get("/api/v1/summary").json()
+    assert set(s) >= {"models", "runtimes", "services", "accelerators", "benchmarks", "nodes"}
+    bj = """apiVersion: ome.io/v1beta1
+kind: BenchmarkJob
+metadata: {name: b1, namespace: default}
+spec:
+  endpoint: {endpoint: {url: "http://127.0.0.1:1/v1", apiFormat: openai, modelName: m}}
+  task: text-to-text
+  trafficScenarios: ["D(100,100)"]
+  numConcurrency: [1]
+  maxTimePerIteration: 1
+  maxRequestsPerIteration: 1
+  outputLocation: {storageUri: "local:///tmp/ome-bench-results"}
+"""
+    r = client.post("/api/v1/benchmarks", content=bj, headers={"Content-Type": "application/yaml"})
+    assert r.status_code == 201, r.text
+    assert client.get("/api/v1/benchmarks").json()["total"] == 1
+    assert client.get("/api/v1/benchmarks/b1").json()["spec"]["task"] == "text-to-text"
+    assert client.delete("/api/v1/benchmarks/b1").status_code == 200
