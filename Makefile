@@ -3,7 +3,7 @@ PY ?= python
 JOBS ?= 6
 COVERAGE_MIN ?= 48
 
-.PHONY: build lint test test-shard test-gpu coverage bench catalog crds verify-generated clean
+.PHONY: build lint test test-shard test-gpu coverage bench catalog crds deploy verify-generated clean
 
 build:            ## compile every HIP extension for gfx950 + the native IO/runtime library
 	$(PY) -c "import __graft_entry__ as g; g.build()"
@@ -40,8 +40,12 @@ catalog:          ## regenerate runtimes, model catalog and samples
 crds:
 	$(PY) -c "from ome_amd.api import schema; schema.write_all('config/crd')"
 
+deploy:           ## regenerate the kustomize overlays (rbac, webhook, certmanager, model-agent, configmap, default)
+	$(PY) -m ome_amd.deploy
+
 verify-generated: catalog
 	git diff --exit-code -- config/runtimes config/models config/samples
+	$(PY) -m ome_amd.deploy --check
 
 clean:
 	rm -rf ome_amd/_lib/*.so build/

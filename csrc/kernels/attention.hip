@@ -807,7 +807,15 @@ constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
 // A short prefill (a few hundred keys per row) otherwise leaves most CUs idle and every
 // workgroup latency-bound on its serial chain of K/V tile loads; partial (O, m, l) per part go
 // to fp32 workspaces and prefill_combine_kernel merges them.
-template <int SUB, int F, bool SPLIT>
+//
+// FAST: plain causal attention (no soft-capping, ALiBi, window or row_hi) -- the Llama / Qwen /
+// Mixtral prefill.  The generic per-score code (soft-cap select, ALiBi term, window and row_hi
+// bounds, each a per-element branch) made the loop VALU-issue bound at ~3.3 us per 64-key step
+// (8x the MFMA time, profiles/r03_prefill_attn_fast.txt).  The fast body keeps raw scores, masks
+// only diagonal subtiles (key <= qpos also bounds kv_len), folds the scale into the exp2 FMA,
+// keeps per-lane partial row sums (reduced across the row's 4 lanes once, at the end) and skips
+// the O rescale when no row of the wave raised its max.
+template <int SUB, int F, bool SPLIT, bool FAST = false>
 __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -930,10 +938,10 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
             sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
           }
         }
-        const bool need_mask =
-            (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0 || window < -1);
         bf16x8 pb[2];
         float alpha[2];
+        const bool need_mask =
+            (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0 || window < -1);
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           const int qpos = prefix + r0 + 16 * rb + n;
@@ -984,6 +992,84 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     }
   };
 
+  // FAST body: one online-softmax update per 32*SUB-key stage (one max reduction, one O
+  // rescale) instead of per 32-key subtile.  Subtiles past kv_end are skipped in both MFMA
+  // passes; their keys lie past every row's causal limit, so the diagonal mask covers them.
+  auto compute_fast = [&](int buf, int kb) __attribute__((always_inline)) {
+    if (!active) return;
+    f32x4 sc[SUB][2][2];
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) sc[u][rb][0] = sc[u][rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (kb + 32 * u < kv_end) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&sK[buf][u][n * PF_KLD + 32 * ks + 8 * g]);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&sK[buf][u][(16 + n) * PF_KLD + 32 * ks + 8 * g]);
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            sc[u][rb][0] = mfma16(a0, qf[rb][ks], sc[u][rb][0]);
+            sc[u][rb][1] = mfma16(a1, qf[rb][ks], sc[u][rb][1]);
+          }
+        }
+      }
+    }
+    const bool diag = kb + 32 * SUB > prefix + r0 + 1;   // wave-uniform
+    bf16x8 pb[SUB][2];
+    float alpha[2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int lim = diag ? prefix + r0 + 16 * rb + n - kb : (1 << 30);   // last visible key offset
+      float mt = OME_NEG_INF;
+#pragma unroll
+      for (int u = 0; u < SUB; ++u)
+#pragma unroll
+        for (int X = 0; X < 2; ++X)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float v = (32 * u + 16 * X + 4 * g + i <= lim) ? sc[u][rb][X][i] : OME_NEG_INF;
+            sc[u][rb][X][i] = v;
+            mt = fmaxf(mt, v);
+          }
+      mt = fmaxf(mt, __shfl_xor(mt, 16));
+      mt = fmaxf(mt, __shfl_xor(mt, 32));
+      const float m_new = fmaxf(m_i[rb], mt * scl.mul);   // log2 domain
+      const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
+      alpha[rb] = fast_exp2(m_i[rb] - m_use);
+      float rs = 0.f;
+#pragma unroll
+      for (int u = 0; u < SUB; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p0 = fast_exp2(__builtin_fmaf(sc[u][rb][0][i], scl.mul, -m_use));
+          const float p1 = fast_exp2(__builtin_fmaf(sc[u][rb][1][i], scl.mul, -m_use));
+          pb[u][rb][i] = (bf16)p0;
+          pb[u][rb][4 + i] = (bf16)p1;
+          rs += p0 + p1;
+        }
+      l_i[rb] = l_i[rb] * alpha[rb] + rs;   // this lane's partial row sum
+      m_i[rb] = m_new;
+    }
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) o[rb][nb] = o[rb][nb] * alpha[rb];
+#pragma unroll
+      for (int u = 0; u < SUB; ++u) {
+        if (kb + 32 * u < kv_end) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sV[buf][u][(16 * nb + n) * PF_VLD + 8 * g]);
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) o[rb][nb] = mfma16(a, pb[u][rb], o[rb][nb]);
+        }
+      }
+    }
+  };
+  auto step = [&](int buf, int kb) __attribute__((always_inline)) {
+    if constexpr (FAST) compute_fast(buf, kb);
+    else compute(buf, kb);
+  };
+
   constexpr int STEP = 32 * SUB;
   int kb = kv_lo;
   if (kb < kv_end) {
@@ -995,17 +1081,24 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   if (kb + 2 * STEP < kv_end) load_tile(rkA, rvA, kb + 2 * STEP);
   // invariant at the top: LDS buf 0 = tile kb, registers B = tile kb + STEP, A = tile kb + 2 STEP
   for (; kb < kv_end; kb += 2 * STEP) {
-    compute(0, kb);
+    step(0, kb);
     if (kb + STEP < kv_end) store_tile(rkB, rvB, 1);
     __syncthreads();
     if (kb + STEP >= kv_end) break;
     if (kb + 3 * STEP < kv_end) load_tile(rkB, rvB, kb + 3 * STEP);
-    compute(1, kb + STEP);
+    step(1, kb + STEP);
     if (kb + 2 * STEP < kv_end) store_tile(rkA, rvA, 0);
     __syncthreads();
     if (kb + 4 * STEP < kv_end) load_tile(rkA, rvA, kb + 4 * STEP);
   }
   if (!active) return;
+  if constexpr (FAST) {   // per-lane partial row sums -> the row's total (its 4 lane groups)
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      l_i[rb] += __shfl_xor(l_i[rb], 16);
+      l_i[rb] += __shfl_xor(l_i[rb], 32);
+    }
+  }
   if (SPLIT && part >= 0) {   // unnormalised partial: O^T rows of this wave + (m, l) per row
     const int64_t pw = ((int64_t)part * Hkv + kvh) * 4 + wave;
     float* po = part_o + pw * 32 * D;
@@ -1077,6 +1170,16 @@ __global__ __launch_bounds__(256) void prefill_combine_kernel(const int4* __rest
   *reinterpret_cast<bf16x4*>(out + (int64_t)(q0 + row) * out_stride + (int64_t)head * D + 4 * quad) = v;
 }
 
+// the FAST body of paged_prefill_v2_kernel applies: causal only (OME_PREFILL_FAST=0 forces the
+// generic body, for A/B runs)
+static bool prefill_fast(const Scaler& scl, int window, const int* row_hi) {
+  static const bool off = [] {
+    const char* e = getenv("OME_PREFILL_FAST");
+    return e && atoi(e) == 0;
+  }();
+  return !off && scl.cap_inv == 0.f && scl.alibi == nullptr && row_hi == nullptr && (window == -1 || window == 0);
+}
+
 template <int D, int F>
 static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, const void* q, int64_t q_stride,
                            const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
@@ -1086,10 +1189,13 @@ static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, co
   typedef typename KVStore<F>::T T;
   if constexpr (D == 128) {
     if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
-      paged_prefill_v2_kernel<2, F, false><<<grid, 256, 0, stream>>>(
-          (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,
-          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi, 0, nullptr,
-          nullptr);
+#define OME_PF2(FAST)                                                                                             \
+  paged_prefill_v2_kernel<2, F, false, FAST><<<grid, 256, 0, stream>>>(                                           \
+      (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,      \
+      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi, 0, nullptr, nullptr)
+      if (prefill_fast(scl, window, row_hi)) OME_PF2(true);
+      else OME_PF2(false);
+#undef OME_PF2
       return;
     }
   }
@@ -1152,14 +1258,22 @@ OME_API int ome_paged_prefill_split(const void* q, int64_t q_stride, const void*
   if (Hq != 4 * Hkv || chunk % 64 || kv_fmt < 0 || kv_fmt > 2) return -2;
   const Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
   dim3 grid(n_items, Hkv);
-#define OME_PFS(F)                                                                                             \
-  paged_prefill_v2_kernel<2, F, true><<<grid, 256, 0, stream>>>(                                               \
+#define OME_PFS(F, FAST)                                                                                       \
+  paged_prefill_v2_kernel<2, F, true, FAST><<<grid, 256, 0, stream>>>(                                         \
       (const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache, (const typename KVStore<F>::T*)v_cache, \
       block_tables, bt_stride, cu_q, kv_lens, (const int2*)items4, (bf16*)out, out_stride, Hq, Hkv, scl, window,  \
       v_scale, sinks, nullptr, chunk, (float*)part_o, (float*)part_ml)
-  if (kv_fmt == KV_BF16) OME_PFS(KV_BF16);
-  else if (kv_fmt == KV_E4M3) OME_PFS(KV_E4M3);
-  else OME_PFS(KV_E5M2);
+  const bool fast = prefill_fast(scl, window, nullptr);
+  if (kv_fmt == KV_BF16) {
+    if (fast) OME_PFS(KV_BF16, true);
+    else OME_PFS(KV_BF16, false);
+  } else if (kv_fmt == KV_E4M3) {
+    if (fast) OME_PFS(KV_E4M3, true);
+    else OME_PFS(KV_E4M3, false);
+  } else {
+    if (fast) OME_PFS(KV_E5M2, true);
+    else OME_PFS(KV_E5M2, false);
+  }
 #undef OME_PFS
   OME_CHECK_LAUNCH();
   if (n_comb > 0) {

@@ -350,6 +350,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-agent", action="store_true")
     ap.add_argument("--kubeconfig", default=None, help="reconcile a real cluster through this kubeconfig")
     ap.add_argument("--in-cluster", action="store_true", help="reconcile the cluster we run in (service account)")
+    ap.add_argument("--tls-cert-dir", default=None,
+                    help="serve HTTPS with tls.crt / tls.key from this dir (the API server calls /admission over TLS)")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(levelname)s %(message)s")
     store = None
@@ -366,7 +368,11 @@ def main(argv=None) -> int:
     import uvicorn
 
     try:
-        uvicorn.run(create_api(cl), host=args.host, port=args.port, log_level="warning")
+        tls = {}
+        if args.tls_cert_dir:
+            tls = {"ssl_certfile": os.path.join(args.tls_cert_dir, "tls.crt"),
+                   "ssl_keyfile": os.path.join(args.tls_cert_dir, "tls.key")}
+        uvicorn.run(create_api(cl), host=args.host, port=args.port, log_level="warning", **tls)
     finally:
         cl.shutdown()
     return 0
