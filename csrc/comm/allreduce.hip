@@ -97,10 +97,18 @@ __device__ __forceinline__ u32x4 pack8(const float* a) {
 }
 
 template <int W>
-__global__ __launch_bounds__(kThreads) void ar_one_shot(Peers P, int rank, int64_t n_vec, u32x4* __restrict__ out) {
+__global__ __launch_bounds__(kThreads) void ar_one_shot(Peers P, int rank, int64_t n_vec, const u32x4* __restrict__ in,
+                                                        u32x4* __restrict__ out) {
   __shared__ uint32_t s_epoch;
   Signal* self = P.sig[rank];
   if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
+  // in-kernel staging (no D2D copy node): block b stages exactly the vectors block b of every
+  // rank reads below; the start barrier publishes them
+  if (in != nullptr) {
+    u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]);
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n_vec; i += (int64_t)gridDim.x * kThreads)
+      mine[i] = in[i];
+  }
   __syncthreads();
   const uint32_t epoch = s_epoch;
   block_barrier(P, rank, W, epoch, 0);
@@ -124,13 +132,21 @@ __global__ __launch_bounds__(kThreads) void ar_one_shot(Peers P, int rank, int64
 // gathering from this call.
 template <int W>
 __global__ __launch_bounds__(kThreads) void ar_two_shot(Peers P, int rank, int64_t n_vec, int64_t red_vec,
-                                                        u32x4* __restrict__ out) {
+                                                        const u32x4* __restrict__ in, u32x4* __restrict__ out) {
   __shared__ uint32_t s_epoch;
   Signal* self = P.sig[rank];
   if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
+  const int64_t chunk = (n_vec + W - 1) / W;
+  if (in != nullptr) {   // stage what block b of every rank reduces from us: its slice of each chunk
+    u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]);
+    for (int c = 0; c < W; ++c) {
+      const int64_t lo = c * chunk, hi = lo + chunk < n_vec ? lo + chunk : n_vec;
+      for (int64_t i = lo + (int64_t)blockIdx.x * kThreads + threadIdx.x; i < hi; i += (int64_t)gridDim.x * kThreads)
+        mine[i] = in[i];
+    }
+  }
   __syncthreads();
   const uint32_t epoch = s_epoch;
-  const int64_t chunk = (n_vec + W - 1) / W;
   block_barrier(P, rank, W, epoch, 0);
   const int64_t c0 = rank * chunk, c1 = c0 + chunk < n_vec ? c0 + chunk : n_vec;
   u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]);
@@ -171,16 +187,22 @@ __global__ __launch_bounds__(kThreads) void ar_two_shot(Peers P, int rank, int64
 // 512-lane pass per row with VPT 16-byte vectors per lane (H <= 512 * 8 * VPT).
 template <int W, int VPT>
 __global__ __launch_bounds__(kThreads) void ar_one_shot_add_rmsnorm(Peers P, int rank, int rows, int H,
+                                                                    const u32x4* __restrict__ src,
                                                                     u32x4* __restrict__ x, u32x4* __restrict__ res,
                                                                     const u32x4* __restrict__ w, float eps) {
   __shared__ uint32_t s_epoch;
   __shared__ float red[kThreads / 64];
   Signal* self = P.sig[rank];
   if (threadIdx.x == 0) s_epoch = self->epoch[blockIdx.x] + 1;
+  const int hv = H >> 3;
+  if (src != nullptr) {   // stage this block's rows (the rows block b of every rank reduces)
+    u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]);
+    for (int row = blockIdx.x; row < rows; row += gridDim.x)
+      for (int i = threadIdx.x; i < hv; i += kThreads) mine[(int64_t)row * hv + i] = src[(int64_t)row * hv + i];
+  }
   __syncthreads();
   const uint32_t epoch = s_epoch;
   block_barrier(P, rank, W, epoch, 0);
-  const int hv = H >> 3;
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
     float v[VPT][8];
     float ss = 0.f;
@@ -340,19 +362,17 @@ OME_API int ome_comm_all_reduce(void* ctx, const void* in, void* out, int64_t n,
   if (bytes > c->data_bytes) return -3;
   if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
   hipError_t e = hipSuccess;
-  if (in != c->data) {  // callers that produced the input straight into the IPC buffer skip the copy
-    e = hipMemcpyAsync(c->data, in, bytes, hipMemcpyDeviceToDevice, stream);
-    if (e != hipSuccess) return (int)e;
-  }
+  // callers that produced the input straight into the IPC buffer skip the staging pass
+  const u32x4* src = in != c->data ? (const u32x4*)in : nullptr;
   const int64_t n_vec = n / 8;
   const int64_t red_vec = (int64_t)(c->data_bytes / 16);
   dim3 grid(blocks), block(kThreads);
 #define OME_AR_CASE(W)                                                                               \
   case W:                                                                                            \
     if (two_shot)                                                                                    \
-      ar_two_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, red_vec, (u32x4*)out);    \
-    else                                                                                             \
-      ar_one_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, (u32x4*)out);             \
+      ar_two_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, red_vec, src, (u32x4*)out); \
+    else                                                                                               \
+      ar_one_shot<W><<<grid, block, 0, stream>>>(c->peers, c->rank, n_vec, src, (u32x4*)out);          \
     break;
   switch (c->world) {
     OME_AR_CASE(2)
@@ -381,15 +401,11 @@ OME_API int ome_comm_all_reduce_add_rmsnorm(void* ctx, const void* in, void* x, 
   if (vpt > 4) return -2;
   if (blocks <= 0 || blocks > kMaxBlocks) blocks = kMaxBlocks;
   if (blocks > rows) blocks = rows;
-  hipError_t e = hipSuccess;
-  if (in != c->data) {
-    e = hipMemcpyAsync(c->data, in, bytes, hipMemcpyDeviceToDevice, stream);
-    if (e != hipSuccess) return (int)e;
-  }
+  const u32x4* src = in != c->data ? (const u32x4*)in : nullptr;   // staged in-kernel unless produced there
   dim3 grid(blocks), block(kThreads);
 #define OME_ARN_CASE(W, V)                                                                                 \
   if (c->world == W && vpt <= V && vpt > V / 2) {                                                         \
-    ar_one_shot_add_rmsnorm<W, V><<<grid, block, 0, stream>>>(c->peers, c->rank, rows, H, (u32x4*)x,       \
+    ar_one_shot_add_rmsnorm<W, V><<<grid, block, 0, stream>>>(c->peers, c->rank, rows, H, src, (u32x4*)x,  \
                                                               (u32x4*)res, (const u32x4*)w, eps);         \
     return (int)hipGetLastError();                                                                         \
   }

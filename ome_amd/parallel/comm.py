@@ -57,6 +57,15 @@ class CustomAllReduce:
         if rc != 0:
             raise _native.NativeError(f"ome_comm_open failed ({rc}): peers not reachable over xGMI/IPC")
 
+    def _grid(self, n: int, two_shot: bool) -> int:
+        """Workgroups for an n-element reduction: each one costs a flag hand-off with every peer
+        (system-scope release + acquire spin), about 0.35 us per workgroup measured with 2 ranks
+        (profiles/r03_comm_latency.txt: 1 row 6.6 us, 64 rows 28.8 us), so small messages use
+        few of them -- at least 4 16-B vectors per lane (2 per lane and rank's chunk in two-shot)."""
+        vec = n // 8
+        per = 512 * (2 * self.world if two_shot else 4)
+        return max(1, min(self.blocks, -(-vec // per)))
+
     def usable(self, x: torch.Tensor) -> bool:
         n = x.numel()
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and n % 8 == 0 and
@@ -67,7 +76,7 @@ class CustomAllReduce:
         out = x if out is None else out
         two = x.numel() * 2 > self.one_shot_max
         rc = self._lib.ome_comm_all_reduce(self._ctx, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()),
-                                           x.numel(), int(two), self.blocks,
+                                           x.numel(), int(two), self._grid(x.numel(), two),
                                            C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
         if rc != 0:
             raise _native.NativeError(f"ome_comm_all_reduce failed ({rc})")
@@ -105,7 +114,7 @@ class CustomAllReduce:
         out = torch.empty_like(x)
         rc = self._lib.ome_comm_all_reduce_add_rmsnorm(
             self._ctx, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()), C.c_void_p(residual.data_ptr()),
-            C.c_void_p(weight.data_ptr()), rows, H, float(eps), self.blocks,
+            C.c_void_p(weight.data_ptr()), rows, H, float(eps), max(1, min(self.blocks, -(-rows // 4))),
             C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
         if rc != 0:
             raise _native.NativeError(f"ome_comm_all_reduce_add_rmsnorm failed ({rc})")
