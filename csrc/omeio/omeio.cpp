@@ -95,6 +95,9 @@ std::string hex(const unsigned char* d, unsigned n) {
 
 OMEIO_API const char* omeio_last_error() { return g_err.c_str(); }
 
+// shared with the other translation units of the library (xet.cpp)
+int omeio_fail(int code, const char* msg) { return fail(code, msg); }
+
 OMEIO_API int omeio_st_header(const char* path, char* buf, size_t cap, uint64_t* header_len, uint64_t* data_offset) {
   Fd f(open(path, O_RDONLY | O_CLOEXEC));
   if (f.fd < 0) return fail(-ENOENT, std::string("open ") + path + ": " + strerror(errno));

@@ -47,3 +47,19 @@ OMEIO_API int omeio_aes_gcm_decrypt(const uint8_t* in, size_t in_len, const uint
                                     size_t* out_len);
 OMEIO_API int omeio_aes_gcm_encrypt(const uint8_t* in, size_t in_len, const uint8_t* key32, const uint8_t* nonce12,
                                     uint8_t* out, size_t* out_len);
+
+// ---- Xet CAS chunk decoding (xet.cpp) -------------------------------------------------------
+// A xorb byte range is a run of chunks, each an 8-byte header
+//   [version u8][compressed length u24 LE][scheme u8][uncompressed length u24 LE]
+// followed by its payload; scheme 0 = stored, 1 = LZ4 frame, 2 = byte-grouping-4 then LZ4 frame.
+// omeio_xet_scan: number of chunks and total decoded size of `src` (validates the headers).
+OMEIO_API int omeio_xet_scan(const uint8_t* src, size_t len, uint64_t* n_chunks, uint64_t* total);
+// omeio_xet_decode: decodes every chunk into `dst` (capacity `cap`); offsets[i] / offsets[i + 1]
+// bound chunk i in `dst` (`offsets` holds max_chunks + 1 entries).  Returns the chunk count.
+OMEIO_API int64_t omeio_xet_decode(const uint8_t* src, size_t len, uint8_t* dst, size_t cap, uint64_t* offsets,
+                                   uint64_t max_chunks);
+// raw LZ4 block / frame decoders (exposed for tests and other callers); return bytes written or < 0
+OMEIO_API int64_t omeio_lz4_block_decode(const uint8_t* src, size_t len, uint8_t* dst, size_t cap);
+OMEIO_API int64_t omeio_lz4_frame_decode(const uint8_t* src, size_t len, uint8_t* dst, size_t cap);
+
+int omeio_fail(int code, const char* msg);

@@ -84,6 +84,44 @@ int main(int argc, char** argv) {
   CHECK(omeio_aes_gcm_decrypt_file((dir + "/big.tampered").c_str(), (dir + "/big.dec").c_str(), key) != 0);
   CHECK(omeio_aes_gcm_decrypt_file((dir + "/big.enc").c_str(), (dir + "/big.dec").c_str(), key) == 0);
   CHECK(read_file(dir + "/big.dec") == big);
+  // Xet chunk runs: a valid run (stored chunk + LZ4-frame chunk with an overlapping match), then
+  // thousands of random mutations / truncations that must fail cleanly, never read or write out
+  // of bounds (this is network input)
+  {
+    std::vector<uint8_t> run;
+    const char* stored = "stored-bytes";
+    const uint32_t sl = (uint32_t)std::strlen(stored);
+    uint8_t h0[8] = {0, (uint8_t)sl, 0, 0, 0, (uint8_t)sl, 0, 0};
+    run.insert(run.end(), h0, h0 + 8);
+    run.insert(run.end(), stored, stored + sl);
+    // LZ4 frame: magic, FLG (v01 | independent), BD, HC, one block "ab" + match(off 2, len 10) + "!", end mark
+    const uint8_t blk[] = {(2 << 4) | 6, 'a', 'b', 2, 0, 0x10, '!'};
+    std::vector<uint8_t> fr = {0x04, 0x22, 0x4D, 0x18, 0x60, 0x40, 0x00, (uint8_t)sizeof(blk), 0, 0, 0};
+    fr.insert(fr.end(), blk, blk + sizeof(blk));
+    fr.insert(fr.end(), {0, 0, 0, 0});
+    uint8_t h1[8] = {0, (uint8_t)fr.size(), 0, 0, 1, 13, 0, 0};
+    run.insert(run.end(), h1, h1 + 8);
+    run.insert(run.end(), fr.begin(), fr.end());
+    uint64_t n = 0, tot = 0;
+    CHECK(omeio_xet_scan(run.data(), run.size(), &n, &tot) == 0 && n == 2 && tot == sl + 13);
+    std::vector<uint8_t> out(tot);
+    uint64_t offs[3];
+    CHECK(omeio_xet_decode(run.data(), run.size(), out.data(), out.size(), offs, 2) == 2);
+    CHECK(std::memcmp(out.data() + sl, "abababababab!", 13) == 0 && offs[2] == tot);
+    unsigned seed = 12345;
+    auto rnd = [&]() { return seed = seed * 1103515245u + 12345u; };
+    for (int it = 0; it < 20000; ++it) {
+      std::vector<uint8_t> m(run);
+      const int flips = 1 + (int)(rnd() % 4);
+      for (int f = 0; f < flips; ++f) m[rnd() % m.size()] = (uint8_t)rnd();
+      m.resize(m.size() - (rnd() % 3 == 0 ? rnd() % m.size() : 0));
+      std::vector<uint8_t> dst(64);
+      uint64_t o[8];
+      (void)omeio_xet_decode(m.data(), m.size(), dst.data(), dst.size(), o, 7);
+      (void)omeio_lz4_block_decode(m.data(), m.size(), dst.data(), dst.size());
+      (void)omeio_lz4_frame_decode(m.data(), m.size(), dst.data(), dst.size());
+    }
+  }
   std::printf("omeio selftest OK\n");
   return 0;
 }

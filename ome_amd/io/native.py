@@ -54,6 +54,13 @@ def load():
                                    ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
         "omeio_aes_gcm_decrypt": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p,
                                    ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "omeio_xet_scan": ([ctypes.c_char_p, ctypes.c_size_t, u64p, u64p], ctypes.c_int),
+        "omeio_xet_decode": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, u64p,
+                              ctypes.c_uint64], ctypes.c_int64),
+        "omeio_lz4_block_decode": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t],
+                                   ctypes.c_int64),
+        "omeio_lz4_frame_decode": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t],
+                                   ctypes.c_int64),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -165,3 +172,28 @@ def iter_tensors_to_device(files, device):
         if offs:
             load_ranges(f, offs, sizes, ptrs, stream=stream, threads=min(16, max(2, len(offs))))
         yield from tensors
+
+
+def xet_decode(data: bytes) -> tuple[bytes, list[int]]:
+    """Decode a run of Xet chunks (csrc/omeio/xet.cpp): (decoded bytes, chunk offsets incl. end)."""
+    lib = load()
+    n = ctypes.c_uint64()
+    tot = ctypes.c_uint64()
+    if lib.omeio_xet_scan(data, len(data), ctypes.byref(n), ctypes.byref(tot)) != 0:
+        raise OmeIOError(lib.omeio_last_error().decode())
+    out = ctypes.create_string_buffer(max(1, tot.value))
+    offs = (ctypes.c_uint64 * (n.value + 1))()
+    got = lib.omeio_xet_decode(data, len(data), out, tot.value, offs, n.value)
+    if got < 0:
+        raise OmeIOError(lib.omeio_last_error().decode())
+    return out.raw[:tot.value], list(offs)
+
+
+def lz4_decode(data: bytes, size: int, frame: bool = True) -> bytes:
+    lib = load()
+    out = ctypes.create_string_buffer(max(1, size))
+    fn = lib.omeio_lz4_frame_decode if frame else lib.omeio_lz4_block_decode
+    got = fn(data, len(data), out, size)
+    if got < 0:
+        raise OmeIOError(lib.omeio_last_error().decode())
+    return out.raw[:got]

@@ -112,8 +112,15 @@ def _wanted(path: str, allow: list[str] | None, ignore: list[str] | None) -> boo
 def snapshot_download(repo: str, local_dir: str | Path, revision: str = "main", token: str | None = None,
                       endpoint: str | None = None, allow_patterns: list[str] | None = None,
                       ignore_patterns: list[str] | None = None, part_size: int = O.DEFAULT_PART_SIZE,
-                      workers: int = O.DEFAULT_WORKERS, progress=None) -> dict:
+                      workers: int = O.DEFAULT_WORKERS, progress=None, use_xet: bool = True) -> dict:
+    """``use_xet``: LFS files that the hub serves from Xet storage (``X-Xet-Hash``) are rebuilt
+    from their CAS xorbs (:mod:`.xet`); everything else goes through ranged HTTP."""
     hub = HfHub(endpoint, token)
+    xc = None
+    if use_xet and os.environ.get("OME_HF_XET", "1") != "0":
+        from ome_amd.storage.xet import XetClient
+
+        xc = XetClient(hub, workers=workers)
     sha, files = hub.files(repo, revision)
     files = [f for f in files if _wanted(f.name, allow_patterns, ignore_patterns)]
     local = Path(local_dir)
@@ -127,10 +134,21 @@ def snapshot_download(repo: str, local_dir: str | Path, revision: str = "main", 
             progress({"phase": "Downloading", "totalBytes": total, "completedBytes": done[0],
                       "totalFiles": len(files)})
 
-    stats = {"sha": sha, "files": 0, "bytes": 0, "parts": 0, "fetched_parts": 0, "verified": 0}
+    stats = {"sha": sha, "files": 0, "bytes": 0, "parts": 0, "fetched_parts": 0, "verified": 0, "xet_files": 0}
     for f in files:
         if f.size == 0:   # small non-LFS files: the API may not report a size
             f.size = hub.file_metadata(repo, f.name, sha or revision)["size"]
+        fd = xc.file_data(repo, f.name, sha or revision) if xc is not None and f.sha256_hex else None
+        dest = local / f.name
+        if fd is not None:
+            if not (dest.exists() and dest.stat().st_size == f.size and O._file_sha256(dest) == f.sha256_hex):
+                xc.download(repo, f.name, dest, sha or revision, size=f.size, sha256_hex=f.sha256_hex, fdata=fd)
+            tick(f.size)
+            stats["files"] += 1
+            stats["xet_files"] += 1
+            stats["bytes"] += f.size
+            stats["verified"] += 1
+            continue
         r = O.download_object(hub, f"{repo}@{sha or revision}", f, local / f.name, part_size, workers, tick)
         stats["files"] += 1
         stats["bytes"] += f.size

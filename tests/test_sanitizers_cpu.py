@@ -17,6 +17,7 @@ def test_omeio_asan_ubsan(tmp_path):
     exe = tmp_path / "omeio_selftest"
     cmd = [cxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
            "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", str(ROOT / "csrc/omeio/omeio.cpp"),
+           str(ROOT / "csrc/omeio/xet.cpp"),
            str(ROOT / "csrc/tests/omeio_selftest.cpp"), "-o", str(exe), "-L/opt/rocm/lib", "-lamdhip64",
            "-lcrypto", "-pthread", "-Wl,-rpath,/opt/rocm/lib"]
     r = subprocess.run(cmd, capture_output=True, text=True)
