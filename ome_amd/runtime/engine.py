@@ -32,6 +32,7 @@ class EngineArgs:
     served_model_name: str | None = None
     tp_size: int = 1
     pp_size: int = 1
+    pp_microbatches: int = 0               # micro-batches per pipeline step (0 = pp_size)
     dp_size: int = 1
     mem_fraction_static: float = 0.9
     max_running_requests: int = 256
@@ -110,6 +111,7 @@ class Engine:
                                   max_context=self.max_context, cuda_graph=args.cuda_graph,
                                   cuda_graph_max_bs=args.cuda_graph_max_bs, seed=args.seed,
                                   kv_cache_dtype_name=args.kv_cache_dtype)
+        self.runner.pp_microbatches = args.pp_microbatches
         prefix = None
         m = self.runner.model
         if not args.disable_radix_cache and not getattr(m, "stateful", False) and not getattr(m, "encoder_only", False):

@@ -88,6 +88,25 @@ class StepHandle:
         return self.host_ids[:self.n].tolist(), self.host_lp[:self.n].tolist()
 
 
+def _split_balanced(chunks: list, m: int) -> list[list]:
+    """Contiguous split of ``chunks`` into at most ``m`` non-empty groups of similar token count
+    (chunk order kept: the concatenated outputs stay in ``chunks`` order)."""
+    m = min(m, len(chunks))
+    total = sum(c.length for c in chunks)
+    groups, cur, acc = [], [], 0
+    for i, c in enumerate(chunks):
+        cur.append(c)
+        acc += c.length
+        left_groups = m - len(groups) - 1
+        left_chunks = len(chunks) - i - 1
+        if left_groups > 0 and (acc >= total * (len(groups) + 1) / m or left_chunks == left_groups):
+            groups.append(cur)
+            cur = []
+    if cur:
+        groups.append(cur)
+    return groups
+
+
 class ModelRunner:
     def __init__(self, cfg: ModelConfig, device: str | torch.device = "cuda", dtype=torch.bfloat16,
                  model_path: str | None = None, load_format: str = "auto", page_size: int = 16,
@@ -452,12 +471,37 @@ class ModelRunner:
             self._decode_forward(bs)
         return self._finish_launch(self.out_ids, self.out_lp, B)
 
+    pp_microbatches = 0   # pipeline parallel: micro-batches per step (0 = one per stage)
+
     def _launch_eager(self, batch: StepBatch, prev: "StepHandle | None") -> "StepHandle":
-        """Eager step for prefill / mixed batches.  Token rows are laid out prefill chunks first,
-        then single-token rows (decodes riding along, or 1-token prompt tails), which attention
-        routes to the decode kernel; sampled rows keep ``batch.chunks`` order."""
-        P = self.P
+        """Eager step for prefill / mixed batches (and every step of a pipeline-parallel engine).
+
+        Pipeline parallel: the step's chunks are cut into token-balanced micro-batches that run
+        through the stages back to back -- each stage's stream holds [forward mb0, send mb0,
+        forward mb1, send mb1, ...] and the stage-to-stage hand-offs are stream-ordered RCCL
+        p2p, so stage s works on micro-batch i while stage s+1 works on micro-batch i-1.  The
+        sampled tokens of all micro-batches return in ONE broadcast from the last stage, issued
+        after every micro-batch (a per-micro-batch broadcast would stall stage 0 on the last
+        stage's sampling of micro-batch 0 and serialise the pipeline)."""
         chunks = batch.chunks
+        m = self.pp_microbatches or pstate.get().pp_size
+        if self.pp and m > 1 and len(chunks) > 1:
+            outs = [self._eager_forward(g, prev, batch.mode) for g in _split_balanced(chunks, m)]
+            out_ids = torch.cat([o[0] for o in outs])
+            out_lp = torch.cat([o[1].float() for o in outs])
+        else:
+            out_ids, out_lp = self._eager_forward(chunks, prev, batch.mode)
+        if self.pp:
+            pstate.pp_broadcast_from_last(out_ids)
+            pstate.pp_broadcast_from_last(out_lp)
+        return self._finish_launch(out_ids, out_lp, len(chunks))
+
+    def _eager_forward(self, chunks, prev: "StepHandle | None", mode: str) -> tuple[torch.Tensor, torch.Tensor]:
+        """One eager forward over ``chunks``: (sampled ids int32, log-probs fp32) in chunk order;
+        on an earlier pipeline stage, empty tensors the last stage's broadcast fills.  Token rows
+        are laid out prefill chunks first, then single-token rows (decodes riding along, or
+        1-token prompt tails), which attention routes to the decode kernel."""
+        P = self.P
         pre = [i for i, c in enumerate(chunks) if c.length > 1]
         dec = [i for i, c in enumerate(chunks) if c.length == 1]
         ids, pos, slots, q_lens, kv_lens, req_idx, src = [], [], [], [], [], [], []
@@ -518,7 +562,7 @@ class ModelRunner:
                                  np.asarray(items, np.int32).reshape(-1) if n_it else np.zeros(0, np.int32),
                                  np.asarray(split, np.int32).reshape(-1) if n_sp else np.zeros(0, np.int32),
                                  np.asarray(comb, np.int32).reshape(-1) if n_cb else np.zeros(0, np.int32)])
-        self._probe_mark(batch.mode)
+        self._probe_mark(mode)
         dev = self.staging.to_device(packed)
         o = 0
 
@@ -573,11 +617,8 @@ class ModelRunner:
             embeds = self._mm_prepare(chunks, pre + dec, T, t_ids, meta)
         hidden = self.model.forward(t_ids, meta, self.kv, embeds)
         if hidden is None:  # an earlier pipeline stage: tokens arrive from the last stage
-            out_ids = torch.empty(len(chunks), dtype=torch.int32, device=self.device)
-            out_lp = torch.empty(len(chunks), dtype=torch.float32, device=self.device)
-            pstate.pp_broadcast_from_last(out_ids)
-            pstate.pp_broadcast_from_last(out_lp)
-            return self._finish_launch(out_ids, out_lp, len(chunks))
+            return (torch.empty(len(chunks), dtype=torch.int32, device=self.device),
+                    torch.empty(len(chunks), dtype=torch.float32, device=self.device))
         logits = self.model.compute_logits(hidden.index_select(0, t_rows))
         pen = None
         if any(c.req.params.has_penalties for c in chunks):
@@ -599,10 +640,7 @@ class ModelRunner:
         out_ids = out_ids.to(torch.int32)
         if pen is not None:
             ops.update_counts(self.counts, pslot, out_ids, *pen)
-        if self.pp:
-            pstate.pp_broadcast_from_last(out_ids)
-            pstate.pp_broadcast_from_last(out_lp.float().contiguous())
-        return self._finish_launch(out_ids, out_lp, len(chunks))
+        return out_ids, out_lp.float().contiguous()
 
     def _mm_prepare(self, chunks, order, T: int, t_ids: torch.Tensor, meta: AttnMeta):
         """Multimodal rows of an eager step: per-row 3D M-RoPE positions -> a row-indexed cos/sin

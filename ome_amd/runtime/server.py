@@ -42,6 +42,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--served-model-name", default=os.environ.get("SERVED_MODEL_NAME"))
     a("--tp-size", "--tp", "--tensor-parallel-size", dest="tp_size", type=int, default=1)
     a("--pp-size", "--pp", "--pipeline-parallel-size", dest="pp_size", type=int, default=1)
+    a("--pp-microbatches", type=int, default=0,
+      help="pipeline parallel: micro-batches per step that flow through the stages back to back (0 = pp size)")
     a("--dp-size", "--dp", "--data-parallel-size", dest="dp_size", type=int, default=1)
     a("--mem-frac", "--mem-fraction-static", "--gpu-memory-utilization", dest="mem_frac", type=float, default=0.88)
     a("--context-length", "--max-model-len", dest="context_length", type=int, default=None)
@@ -102,7 +104,8 @@ def engine_args_from(ns, rank_tp: int | None = None):
         # a model directory without a config (synthetic benchmark nodes): fall back to a preset
         preset = os.environ.get("OME_MODEL_PRESET", "llama-3-8b")
     return EngineArgs(model_path=mp, model=preset, served_model_name=ns.served_model_name, tp_size=ns.tp_size,
-                      pp_size=ns.pp_size, dp_size=ns.dp_size, mem_fraction_static=ns.mem_frac,
+                      pp_size=ns.pp_size, pp_microbatches=ns.pp_microbatches, dp_size=ns.dp_size,
+                      mem_fraction_static=ns.mem_frac,
                       max_running_requests=ns.max_running_requests, max_total_tokens=ns.max_total_tokens,
                       chunked_prefill_size=ns.chunked_prefill_size, context_length=ns.context_length,
                       page_size=ns.page_size, cuda_graph=not ns.disable_cuda_graph,
