@@ -812,9 +812,9 @@ constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
 // Mixtral prefill.  The generic per-score code (soft-cap select, ALiBi term, window and row_hi
 // bounds, each a per-element branch) made the loop VALU-issue bound at ~3.3 us per 64-key step
 // (8x the MFMA time, profiles/r03_prefill_attn_fast.txt).  The fast body keeps raw scores, masks
-// only diagonal subtiles (key <= qpos also bounds kv_len), folds the scale into the exp2 FMA,
-// keeps per-lane partial row sums (reduced across the row's 4 lanes once, at the end) and skips
-// the O rescale when no row of the wave raised its max.
+// only diagonal stages (key <= qpos also bounds kv_len), folds the scale into the exp2 FMA,
+// keeps per-lane partial row sums (reduced across the row's 4 lanes once, at the end) and
+// rescales O / l lazily (only when some row's max grew by more than 2^8).
 template <int SUB, int F, bool SPLIT, bool FAST = false>
 __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
@@ -1016,27 +1016,54 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
       }
     }
     const bool diag = kb + 32 * SUB > prefix + r0 + 1;   // wave-uniform
-    bf16x8 pb[SUB][2];
-    float alpha[2];
+    if (diag) {   // only the diagonal stage masks (a real branch: the asm keeps it from being speculated)
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int lim = prefix + r0 + 16 * rb + n - kb;   // last visible key offset of this row
+#pragma unroll
+        for (int u = 0; u < SUB; ++u)
+#pragma unroll
+          for (int X = 0; X < 2; ++X)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (32 * u + 16 * X + 4 * g + i > lim) sc[u][rb][X][i] = OME_NEG_INF;
+      }
+    }
+    float mt[2];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
-      const int lim = diag ? prefix + r0 + 16 * rb + n - kb : (1 << 30);   // last visible key offset
-      float mt = OME_NEG_INF;
+      float v = OME_NEG_INF;
 #pragma unroll
       for (int u = 0; u < SUB; ++u)
 #pragma unroll
         for (int X = 0; X < 2; ++X)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float v = (32 * u + 16 * X + 4 * g + i <= lim) ? sc[u][rb][X][i] : OME_NEG_INF;
-            sc[u][rb][X][i] = v;
-            mt = fmaxf(mt, v);
-          }
-      mt = fmaxf(mt, __shfl_xor(mt, 16));
-      mt = fmaxf(mt, __shfl_xor(mt, 32));
-      const float m_new = fmaxf(m_i[rb], mt * scl.mul);   // log2 domain
-      const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
-      alpha[rb] = fast_exp2(m_i[rb] - m_use);
+          for (int i = 0; i < 4; ++i) v = fmaxf(v, sc[u][rb][X][i]);
+      v = fmaxf(v, __shfl_xor(v, 16));
+      mt[rb] = fmaxf(v, __shfl_xor(v, 32)) * scl.mul;   // log2 domain
+    }
+    // lazy rescale (FA-3 style): keep the running max while no row of the wave grew it by more
+    // than 8 (p <= 2^8 then, exact in fp32 and bf16's range); O and l are rescaled only on the
+    // stages where some row did -- the first stage always, afterwards rarely
+    const bool grow = __ballot(mt[0] > m_i[0] + 8.f || mt[1] > m_i[1] + 8.f) != 0;
+    if (grow) {
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const float m_new = fmaxf(m_i[rb], mt[rb]);
+        const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
+        const float alpha = fast_exp2(m_i[rb] - m_use);
+        l_i[rb] *= alpha;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) o[rb][nb] = o[rb][nb] * alpha;
+        m_i[rb] = m_new;
+      }
+    }
+    bf16x8 pb[SUB][2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const float m_use = (m_i[rb] == OME_NEG_INF) ? 0.f : m_i[rb];
       float rs = 0.f;
 #pragma unroll
       for (int u = 0; u < SUB; ++u)
@@ -1048,16 +1075,13 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
           pb[u][rb][4 + i] = (bf16)p1;
           rs += p0 + p1;
         }
-      l_i[rb] = l_i[rb] * alpha[rb] + rs;   // this lane's partial row sum
-      m_i[rb] = m_new;
+      l_i[rb] += rs;   // this lane's partial row sum
     }
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
+    for (int u = 0; u < SUB; ++u) {
+      if (kb + 32 * u < kv_end) {
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) o[rb][nb] = o[rb][nb] * alpha[rb];
-#pragma unroll
-      for (int u = 0; u < SUB; ++u) {
-        if (kb + 32 * u < kv_end) {
+        for (int nb = 0; nb < NB; ++nb) {
           const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sV[buf][u][(16 * nb + n) * PF_VLD + 8 * g]);
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb) o[rb][nb] = mfma16(a, pb[u][rb], o[rb][nb]);
