@@ -258,11 +258,16 @@ class ModelRunner:
         tun = torch.cuda.tunable
         self.TUNED_DIR.mkdir(parents=True, exist_ok=True)
         arch = torch.cuda.get_device_properties(self.device).gcnArchName.split(":")[0]
-        fname = str(self.TUNED_DIR / f"tunableop_{arch}.csv")
+        fname = os.environ.get("OME_TUNE_FILE") or str(self.TUNED_DIR / f"tunableop_{arch}.csv")
         tun.enable(True)
         tun.tuning_enable(True)
         tun.set_max_tuning_duration(int(os.environ.get("OME_TUNE_MS", "40")))
         tun.set_max_tuning_iterations(int(os.environ.get("OME_TUNE_ITERS", "30")))
+        # decode GEMMs stream cold weights (a layer stack is far larger than the 256 MB Infinity
+        # Cache): OME_TUNE_ROTATING_MB > 256 times every candidate on rotating operand copies
+        rot = int(os.environ.get("OME_TUNE_ROTATING_MB", "0"))
+        if rot > 0:
+            tun.set_rotating_buffer_size(rot)
         if os.path.exists(fname):
             tun.read_file(fname)
         # one writer for the in-tree table: other ranks of a multi-GPU job keep their results in
