@@ -56,6 +56,77 @@ __device__ float block_sumf(float v, float* red) {
   return t;
 }
 
+// ---- threshold select by a two-level histogram (top-k by count, top-p by mass) ----
+// The kept set of a constraint is {z >= t} for the LARGEST t that still keeps >= target of
+// count / mass.  Level 1 bins z in [-64, 0] into HB bins of 1/32 (z below -64, p < e^-64, all in
+// the last bin), the crossing bin is found by a block prefix scan, and level 2 splits that bin
+// into HB sub-bins (z resolution 1.5e-5, finer than a bf16 logit step): three row passes instead
+// of the 26 bisection passes per constraint.  Values in the crossing sub-bin are all kept (the
+// same tie rule as a threshold compare).
+constexpr int HB = 2048;
+constexpr float HZ = 64.f;
+
+// inclusive block scan of one value per thread (NT threads), returns the prefix
+__device__ float block_scan(float v, float* wtot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wtot[w] = x;
+  __syncthreads();
+  float before = 0.f;
+  for (int k = 0; k < w; ++k) before += wtot[k];
+  __syncthreads();
+  return x + before;
+}
+
+template <typename Row>
+__device__ float hist_threshold(const Row& row, float mx, float invT, bool mass, float target, float* hist,
+                                float* wtot, int* sel) {
+  float upper = 0.f, width = HZ / HB;
+  float carried = 0.f;
+  for (int level = 0; level < 2; ++level) {
+    for (int b = threadIdx.x; b < HB; b += NT) hist[b] = 0.f;
+    __syncthreads();
+    const float lo_edge = upper - HB * width;
+    row([&](float l) {
+      const float z = (l - mx) * invT;
+      if (level == 1 && (z > upper || z <= lo_edge)) return;   // outside the refined bin
+      int b = (int)((upper - z) * (1.f / width));
+      b = b < 0 ? 0 : (b > HB - 1 ? HB - 1 : b);
+      atomicAdd(&hist[b], mass ? __expf(z) : 1.f);
+    });
+    __syncthreads();
+    // each thread owns bins 2t, 2t+1 (HB == 2 * NT)
+    const float v0 = hist[2 * threadIdx.x], v1 = hist[2 * threadIdx.x + 1];
+    const float incl = block_scan(v0 + v1, wtot) + carried;
+    const float excl = incl - v0 - v1;
+    if (threadIdx.x == 0) *sel = -1;
+    __syncthreads();
+    if (excl < target && incl >= target) *sel = (excl + v0 >= target) ? 2 * threadIdx.x : 2 * threadIdx.x + 1;
+    __syncthreads();
+    const int b = *sel;
+    if (b < 0) return -__builtin_inff();   // the whole row does not reach the target: keep all
+    if (b == HB - 1 && level == 0) return -__builtin_inff();   // crossing in the underflow bin
+    // mass / count above the crossing bin carries into the next level
+    float above = 0.f;
+    {
+      float part = 0.f;
+      for (int i = threadIdx.x; i < b; i += NT) part += hist[i];
+      above = block_sumf(part, wtot);
+    }
+    __syncthreads();
+    if (level == 1) return upper - (b + 1) * width;   // lower edge of the crossing sub-bin
+    carried += above;
+    upper = upper - b * width;
+    width = width / HB;
+  }
+  return -__builtin_inff();
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void sample_kernel(const T* __restrict__ logits, int64_t stride, int V,
                                                     const float* __restrict__ temperature,
@@ -136,43 +207,47 @@ __global__ __launch_bounds__(NT) void sample_kernel(const T* __restrict__ logits
   // count(z >= t) and mass(z >= t) are monotone non-increasing in t, so each constraint's
   // threshold is the LARGEST t that still keeps >= k tokens (top-k) / >= p of the mass
   // (top-p).  The kept set is the intersection: the max of the two thresholds.
-  for (int which = 0; which < 2; ++which) {
-    if ((which == 0 && !need_k) || (which == 1 && !need_p)) continue;
-    float lo = -80.f, hi = 0.f;
-    for (int it = 0; it < 26; ++it) {
-      const float mid = 0.5f * (lo + hi);
-      float acc = 0.f;
-      auto visit = [&](float l) {
-        const float z = (l - mx) * invT;
-        if (z >= mid) acc += which == 0 ? 1.f : __expf(z);
-      };
+  if (need_k || need_p) {
+    __shared__ float hist[HB];
+    __shared__ float wtot[NT / 64];
+    __shared__ int sel;
+    auto row = [&](auto&& f) {
       if (vec) {
         if constexpr (sizeof(T) == 2) {
           for (int v = threadIdx.x; v < V / 8; v += NT) {
             const bf16x8 x = ld8(reinterpret_cast<const bf16*>(lr) + 8 * v);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) visit((float)x[j]);
+            for (int j = 0; j < 8; ++j) f((float)x[j]);
           }
         }
       } else {
-        for (int i = threadIdx.x; i < V; i += NT) visit(ldf(lr, i));
+        for (int i = threadIdx.x; i < V; i += NT) f(ldf(lr, i));
       }
-      acc = block_sumf(acc, sv);
-      const bool big_enough = which == 0 ? (acc >= (float)k) : (acc / den >= pp);
-      if (big_enough) lo = mid; else hi = mid;
-    }
-    thr = fmaxf(thr, lo);
+    };
+    if (need_k) thr = fmaxf(thr, hist_threshold(row, mx, invT, false, (float)k, hist, wtot, &sel));
+    if (need_p) thr = fmaxf(thr, hist_threshold(row, mx, invT, true, pp * den, hist, wtot, &sel));
   }
   // Gumbel-max over the kept set
   const uint64_t seed = seeds ? seeds[row] : 0x1234ull;
   ValIdx pick{-__builtin_inff(), best.i};
-  for (int i = threadIdx.x; i < V; i += NT) {
-    const float z = (ldf(lr, i) - mx) * invT;
+  auto gumbel = [&](float l, int i) {
+    const float z = (l - mx) * invT;
     if (z >= thr) {
       const uint64_t h = splitmix64(seed ^ splitmix64(step * 0x100000001B3ull + (uint64_t)i));
       const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
       pick = vi_max(pick, ValIdx{z - __logf(-__logf(u)), i});
     }
+  };
+  if (vec) {
+    if constexpr (sizeof(T) == 2) {
+      for (int v = threadIdx.x; v < V / 8; v += NT) {
+        const bf16x8 x = ld8(reinterpret_cast<const bf16*>(lr) + 8 * v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) gumbel((float)x[j], 8 * v + j);
+      }
+    }
+  } else {
+    for (int i = threadIdx.x; i < V; i += NT) gumbel(ldf(lr, i), i);
   }
   pick = block_argmax(pick, sv, si);
   if (threadIdx.x == 0) {

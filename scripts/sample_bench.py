@@ -44,3 +44,9 @@ for name, t, k, p in (("greedy", 0.0, -1, 1.0), ("T0.8 top_p 0.9", 0.8, -1, 0.9)
     ids, _ = ops.sample(logits, temp, tk, tp, mp, seeds, 0)
     ok = bool((ids == logits.float().argmax(-1).int()).all()) if t == 0 else True
     print(f"{name:26s} {us:8.1f} us per step (B={B}, V={V})" + ("  argmax ok" if ok and t == 0 else ""), flush=True)
+
+# kept-set sizes on this synthetic row distribution (how much the Gumbel pass must hash)
+z = logits[0].float() / 0.8
+p = torch.softmax(z, 0)
+srt = torch.sort(p, descending=True).values
+print(f"tokens kept by top_p 0.9 on row 0: {int((torch.cumsum(srt, 0) < 0.9).sum()) + 1} of {V}")

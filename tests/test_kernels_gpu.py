@@ -236,6 +236,36 @@ def test_sample_distribution():
     assert int(ids.max()) <= 1
 
 
+def test_sample_topk_topp_kept_set():
+    """The histogram threshold select keeps exactly the top-k / top-p sets (ties at the boundary
+    value included): every draw lands in the exact set computed by sorting on the host, and the
+    draws cover it."""
+    B, V = 1024, 128256
+    g = torch.Generator().manual_seed(3)
+    row = (torch.randn(V, generator=g) * 3).to(torch.bfloat16)
+    logits = row.to(DEV).repeat(B, 1)
+    seeds = torch.arange(B, device=DEV, dtype=torch.int64) * 7919 + 1
+    t = torch.full((B,), 0.7, device=DEV)
+    z = row.float() / 0.7
+    srt, order = torch.sort(z, descending=True)
+    # top-k = 20: the kept set is every token >= the 20th largest value
+    tk = torch.full((B,), 20, dtype=torch.int32, device=DEV)
+    ids, _ = ops.sample(logits, t, tk, None, None, seeds)
+    kth = srt[19]
+    got = z[ids.long().cpu()]
+    assert bool((got >= kth).all())
+    assert len(set(ids.tolist())) >= 15
+    # top-p = 0.6: smallest prefix of the sorted distribution holding >= 60 % of the mass
+    p = torch.softmax(z.double(), 0)[order]
+    cut = int(torch.searchsorted(torch.cumsum(p, 0), torch.tensor(0.6, dtype=torch.float64))) 
+    boundary = srt[cut]
+    tp = torch.full((B,), 0.6, device=DEV)
+    ids, _ = ops.sample(logits, t, None, tp, None, seeds)
+    got = z[ids.long().cpu()]
+    assert bool((got >= boundary - 1e-4).all())
+    assert len(set(ids.tolist())) >= min(cut + 1, 50) // 2
+
+
 def test_pool():
     h = torch.randn(50, 256, device=DEV, dtype=torch.bfloat16)
     cu = torch.tensor([0, 10, 50], dtype=torch.int32, device=DEV)
