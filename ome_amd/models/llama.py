@@ -16,7 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from ome_amd import ops
-from ome_amd.models.common import AttnMeta, PagedKVCache
+from ome_amd.models.common import AttnMeta, PagedKVCache, mixed_attention
 from ome_amd.models.config import ModelConfig, rope_cos_sin
 from ome_amd.models.quant import _GEMV_ROWS, Fp8Weight, dequant_fp8_stream, fp8_block_size, linear, quantize_weight
 from ome_amd.parallel import state as pstate
@@ -247,13 +247,13 @@ class LlamaForCausalLM:
             return ops.paged_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale,
                                     meta.decode_ws, self.window, order=meta.order, k_scale=ks, v_scale=vs)
         if meta.mode == "mixed":
-            n = meta.num_prefill
-            out = torch.empty_like(q)
-            ops.paged_prefill(q[:n], k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
-                              self.scale, self.window, out=out[:n], k_scale=ks, v_scale=vs)
-            ops.paged_decode(q[n:], k_cache, v_cache, meta.dec_block_tables, meta.seq_lens, self.scale,
-                             meta.decode_ws, self.window, out=out[n:], order=meta.order, k_scale=ks, v_scale=vs)
-            return out
+            return mixed_attention(
+                q, meta.num_prefill,
+                lambda qp, op: ops.paged_prefill(qp, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens,
+                                                 meta.items, self.scale, self.window, out=op, k_scale=ks, v_scale=vs),
+                lambda qd, od: ops.paged_decode(qd, k_cache, v_cache, meta.dec_block_tables, meta.seq_lens,
+                                                self.scale, meta.decode_ws, self.window, out=od, order=meta.order,
+                                                k_scale=ks, v_scale=vs))
         return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
                                  self.scale, self.window, k_scale=ks, v_scale=vs)
 
