@@ -641,6 +641,14 @@ def _worker_main(rank: int, world: int, ns_dict: dict, addr: str, local_rank: in
 
 def main(argv=None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    # the engine thread shares the GIL with the asyncio HTTP loop: a shorter switch interval than
+    # CPython's 5 ms default bounds how long the engine waits to launch the next step while the
+    # loop formats SSE chunks for hundreds of streams
+    sw = float(os.environ.get("OME_GIL_SWITCH_S", "0") or 0)
+    if sw > 0:
+        import sys as _sys
+
+        _sys.setswitchinterval(sw)
     ap = build_parser()
     ns, unknown = ap.parse_known_args(argv)
     if unknown:
