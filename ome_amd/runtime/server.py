@@ -124,15 +124,60 @@ def engine_args_from(ns, rank_tp: int | None = None):
 
 
 # ------------------------------------------------------------------ request plumbing
+class _Delivery:
+    """Engine thread -> event loop hand-off for ALL streams of one loop: an engine step that
+    produces tokens for N requests wakes the loop once (one ``call_soon_threadsafe``, one
+    self-pipe write) instead of N times; the loop then fans the batch out to the per-request
+    queues.  At 256 streams x ~60 steps/s that is ~15k fewer wake-ups (and GIL hand-offs) per
+    second on the thread that also launches the GPU steps."""
+
+    _by_loop: dict = {}
+
+    def __init__(self, loop):
+        self.loop = loop
+        self.pending: list = []
+        self.scheduled = False
+        self.lock = threading.Lock()
+
+    @classmethod
+    def of(cls, loop) -> "_Delivery":
+        d = cls._by_loop.get(id(loop))
+        if d is None or d.loop is not loop:
+            d = cls._by_loop[id(loop)] = cls(loop)
+        return d
+
+    def push(self, q, item) -> None:
+        with self.lock:
+            self.pending.append((q, item))
+            if self.scheduled:
+                return
+            self.scheduled = True
+        self.loop.call_soon_threadsafe(self._flush)
+
+    def _flush(self) -> None:
+        with self.lock:
+            items, self.pending = self.pending, []
+            self.scheduled = False
+        for q, item in items:
+            q.put_nowait(item)
+
+
 class _Stream:
     """Thread-safe bridge: engine thread -> asyncio queue of (new_token_ids, finished)."""
 
     def __init__(self, loop):
         self.loop = loop
         self.q: asyncio.Queue = asyncio.Queue()
+        self.delivery = _Delivery.of(loop)
 
     def __call__(self, req, toks, finished):
-        self.loop.call_soon_threadsafe(self.q.put_nowait, (list(toks), finished))
+        if _BATCHED_DELIVERY:
+            self.delivery.push(self.q, (list(toks), finished))
+        else:
+            self.loop.call_soon_threadsafe(self.q.put_nowait, (list(toks), finished))
+
+
+_BATCHED_DELIVERY = os.environ.get("OME_BATCHED_DELIVERY", "1") == "1"
 
 
 def _sampling_from(body: dict, default_max: int):
