@@ -47,20 +47,20 @@ FAMILIES: list[Family] = [
     Family("llama-3-8b-instruct", "meta", "meta-llama/Meta-Llama-3-8B-Instruct", "LlamaForCausalLM", 8.0,
            "llama-3-8b", pd=True),
     Family("llama-3-1-8b-instruct", "meta", "meta-llama/Llama-3.1-8B-Instruct", "LlamaForCausalLM", 8.0,
-           "llama-3.1-8b", args=['--tool-call-parser', 'llama3_json']),
+           "llama-3.1-8b", args=['--tool-call-parser', 'llama3_json'], pd=True),
     Family("llama-3-70b-instruct", "meta", "meta-llama/Meta-Llama-3-70B-Instruct", "LlamaForCausalLM", 70.6,
            "llama-3-70b", pd=True),
     Family("llama-3-1-405b-instruct-fp8", "meta", "meta-llama/Llama-3.1-405B-Instruct-FP8", "LlamaForCausalLM",
-           405.0, None, 1.0, quantization="fp8", args=['--tool-call-parser', 'llama3_json']),
+           405.0, None, 1.0, quantization="fp8", args=['--tool-call-parser', 'llama3_json'], multinode=2),
     Family("llama-4-scout-17b-16e-instruct", "meta", "meta-llama/Llama-4-Scout-17B-16E-Instruct",
            "Llama4ForConditionalGeneration", 109.0, "llama-4-scout-17b-16e",
-           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], args=['--tool-call-parser', 'pythonic']),
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], args=['--tool-call-parser', 'pythonic'], pd=True),
     Family("llama-4-maverick-17b-128e-instruct-fp8", "meta", "meta-llama/Llama-4-Maverick-17B-128E-Instruct-FP8",
            "Llama4ForConditionalGeneration", 402.0, None, 1.0, quantization="fp8",
-           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], args=['--tool-call-parser', 'pythonic']),
-    Family("mistral-7b-instruct", "mistralai", "mistralai/Mistral-7B-Instruct-v0.3", "MistralForCausalLM", 7.2),
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], args=['--tool-call-parser', 'pythonic'], pd=True),
+    Family("mistral-7b-instruct", "mistralai", "mistralai/Mistral-7B-Instruct-v0.3", "MistralForCausalLM", 7.2, pd=True),
     Family("mixtral-8x7b-instruct", "mistralai", "mistralai/Mixtral-8x7B-Instruct-v0.1", "MixtralForCausalLM",
-           46.7, "mixtral-8x7b"),
+           46.7, "mixtral-8x7b", pd=True),
     Family("qwen2-5-7b-instruct", "qwen", "Qwen/Qwen2.5-7B-Instruct", "Qwen2ForCausalLM", 7.6),
     Family("qwen2-5-72b-instruct", "qwen", "Qwen/Qwen2.5-72B-Instruct", "Qwen2ForCausalLM", 72.7),
     Family("qwen3-8b", "qwen", "Qwen/Qwen3-8B", "Qwen3ForCausalLM", 8.2, "qwen3-8b"),
@@ -112,9 +112,9 @@ FAMILIES: list[Family] = [
     Family("deepseek-v2-lite-chat", "deepseek-ai", "deepseek-ai/DeepSeek-V2-Lite-Chat", "DeepseekV2ForCausalLM",
            15.7, "deepseek-v2-lite"),
     Family("deepseek-v3", "deepseek-ai", "deepseek-ai/DeepSeek-V3", "DeepseekV3ForCausalLM", 671.0, None, 1.0,
-           args=["--enable-dp-attention", "--dp", "8"], quantization="fp8", multinode=2, min_tp=8),
+           args=["--enable-dp-attention", "--dp", "8"], quantization="fp8", multinode=2, min_tp=8, pd=True),
     Family("kimi-k2-instruct", "moonshotai", "moonshotai/Kimi-K2-Instruct", "DeepseekV3ForCausalLM", 1026.0, None,
-           1.0, quantization="fp8"),
+           1.0, quantization="fp8", pd=True, multinode=2),
     Family("gpt-oss-20b", "openai", "openai/gpt-oss-20b", "GptOssForCausalLM", 20.9, "gpt-oss-20b", args=['--tool-call-parser', 'gpt-oss', '--reasoning-parser', 'gpt-oss']),
     Family("gpt-oss-120b", "openai", "openai/gpt-oss-120b", "GptOssForCausalLM", 117.0, args=['--tool-call-parser', 'gpt-oss', '--reasoning-parser', 'gpt-oss']),
     Family("gemma-2-9b-it", "google", "google/gemma-2-9b-it", "Gemma2ForCausalLM", 9.2, "gemma-2-9b"),
