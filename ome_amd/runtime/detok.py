@@ -26,18 +26,32 @@ class IncrementalDetokenizer:
         self.read = 0
         self.text = ""
 
+    _cache: tuple | None = None   # (prefix, end, text): the last decode of ids[prefix:end]
+
+    def _decode(self, a: int, b: int) -> str:
+        c = self._cache
+        if c is not None and c[0] == a and c[1] == b:
+            return c[2]
+        return self.tok.decode(self.ids[a:b], skip_special=self.skip)
+
     def push(self, new_ids) -> str:
-        """Append tokens; return the newly completed text (may be "")."""
+        """Append tokens; return the newly completed text (may be "").
+
+        One tokenizer call per push in the steady state: the context window only slides in
+        jumps (when it has grown to twice ``_WINDOW``), so ``decode(ids[prefix:read])`` is
+        usually the previous push's ``after`` and comes from the cache."""
         self.ids.extend(int(t) for t in new_ids)
         if self.read >= len(self.ids):
             return ""
-        before = self.tok.decode(self.ids[self.prefix:self.read], skip_special=self.skip)
+        before = self._decode(self.prefix, self.read)
         after = self.tok.decode(self.ids[self.prefix:], skip_special=self.skip)
-        if len(after) <= len(before) or after.endswith("�"):
+        self._cache = (self.prefix, len(self.ids), after)
+        if len(after) <= len(before) or after.endswith("\ufffd"):
             return ""   # nothing new yet, or an incomplete multi-byte character
         delta = after[len(before):]
         self.read = len(self.ids)
-        self.prefix = max(self.prefix, self.read - _WINDOW)
+        if self.read - self.prefix >= 2 * _WINDOW:
+            self.prefix = self.read - _WINDOW
         self.text += delta
         return delta
 
