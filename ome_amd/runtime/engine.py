@@ -25,6 +25,25 @@ from ome_amd.runtime.tokenizer import get_tokenizer
 log = logging.getLogger("ome_amd.engine")
 
 
+_REASONS = ["stop", "length", "abort", "abort:error", "abort:kv_capacity"]
+_REASON_CODE = {r: i for i, r in enumerate(_REASONS)}
+
+
+def _unpack_updates(v: list[float]):
+    """Inverse of the DP-attention update packing in :meth:`Engine._dp_step`."""
+    n, i, out, heads = int(v[0]), 1, [], []
+    for _ in range(n):
+        h, nt, fin, code = int(v[i]), int(v[i + 1]), bool(v[i + 2]), int(v[i + 3])
+        toks = [int(t) for t in v[i + 4:i + 4 + nt]]
+        i += 4 + nt
+        heads.append((h, toks, fin, _REASONS[code] if 0 <= code < len(_REASONS) else "stop"))
+    for h, toks, fin, reason in heads:   # log-probs follow all headers, in the same order
+        lps = v[i:i + len(toks)]
+        i += len(toks)
+        out.append((h, toks, lps, fin, reason))
+    return out
+
+
 @dataclass
 class EngineArgs:
     model_path: str | None = None
@@ -94,6 +113,8 @@ class Engine:
         self.pstate.tbo = bool(args.enable_two_batch_overlap and self.pstate.ep_size > 1)
         self.dp = self.pstate.dp_size > 1
         self._remote: dict[str, Request] = {}   # DP attention, rank 0: requests served by other ranks
+        self._remote_h: dict[int, Request] = {}  # ... by the integer handle all ranks agree on
+        self._dp_seq = 0
         self._dp_next = 0
         device = args.device
         if device == "cuda" and torch.cuda.is_available():
@@ -207,9 +228,13 @@ class Engine:
             new, aborts = self._broadcast_control(new, aborts)
         kt = self.kv_transfer
         for r in new:
+            if self.dp:   # every rank sees the same new requests in the same order: same handles
+                r.dp_handle = self._dp_seq
+                self._dp_seq += 1
             if self.dp and getattr(r, "dp_rank", 0) != self.pstate.rank:
                 if self.pstate.rank == 0:
                     self._remote[r.rid] = r  # proxy: tokens arrive from the owning rank
+                    self._remote_h[r.dp_handle] = r
                     self.metrics.on_arrival(r)
                 continue
             r.arrival_time = r.arrival_time or time.perf_counter()
@@ -227,6 +252,7 @@ class Engine:
             r = self.scheduler.abort(rid)
             if r is None and rid in self._remote:  # DP proxy: the owning rank aborts its copy
                 r = self._remote.pop(rid)
+                self._remote_h.pop(getattr(r, "dp_handle", -1), None)
                 r.state, r.finish_reason = ReqState.FINISHED, "abort"
             if r is not None and r.on_token:
                 r.on_token(r, [], True)
@@ -379,21 +405,38 @@ class Engine:
             self.runner.idle_decode()
         else:
             self.runner.idle_forward()
-        updates = []
+        # token updates of the followers' requests -> rank 0 (which owns every HTTP stream) as ONE
+        # float64 tensor per rank (no pickling): [n_updates, then per update handle, n_tokens,
+        # finished, reason code, and the tokens; then all log-probs]; sizes first, then a gather
+        packed: list[float] = [0.0]
+        lps_all: list[float] = []
         for r in touched:
             k = getattr(r, "_reported", 0)
-            updates.append((r.rid, r.output_ids[k:], r.output_logprobs[k:], r.state == ReqState.FINISHED,
-                            r.finish_reason))
+            toks = r.output_ids[k:]
+            fin = r.state == ReqState.FINISHED
+            packed += [float(getattr(r, "dp_handle", -1)), float(len(toks)), float(fin),
+                       float(_REASON_CODE.get(r.finish_reason, -1) if fin else -1)]
+            packed += [float(t) for t in toks]
+            lps_all += [float(x) for x in r.output_logprobs[k:]]
             r._reported = len(r.output_ids)
-        gathered = [None] * self.pstate.world_size if self.pstate.rank == 0 else None
-        dist.gather_object(updates, gathered, dst=self.pstate.to_global(0), group=self._cpu_group())
+            packed[0] += 1
+        mine = torch.tensor(packed + lps_all, dtype=torch.float64)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.pstate.world_size)]
+        dist.all_gather(sizes, torch.tensor([mine.numel()], dtype=torch.int64), group=self._cpu_group())
+        cap = max(int(x) for x in sizes)
+        buf = torch.zeros(cap, dtype=torch.float64)
+        buf[:mine.numel()] = mine
+        bufs = [torch.zeros(cap, dtype=torch.float64) for _ in range(self.pstate.world_size)] \
+            if self.pstate.rank == 0 else None
+        dist.gather(buf, bufs, dst=self.pstate.to_global(0), group=self._cpu_group())
         if self.pstate.rank == 0:
             now = time.perf_counter()
-            for rank_updates in gathered[1:]:
-                for rid, toks, lps, fin, reason in rank_updates:
-                    p = self._remote.get(rid)
+            for b in bufs[1:]:
+                for handle, toks, lps, fin, reason in _unpack_updates(b.tolist()):
+                    p = self._remote_h.get(handle)
                     if p is None:
                         continue
+                    rid = p.rid
                     if toks and p.first_token_time is None:
                         p.first_token_time = now
                     p.output_ids.extend(toks)
@@ -402,6 +445,7 @@ class Engine:
                     if fin:
                         p.state, p.finish_reason = ReqState.FINISHED, reason
                         self._remote.pop(rid, None)
+                        self._remote_h.pop(handle, None)
                         done.append(p)
                     if p.on_token is not None and (toks or fin):
                         p.on_token(p, list(toks), fin)
