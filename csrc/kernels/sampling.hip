@@ -62,7 +62,10 @@ __device__ float block_sumf(float v, float* red) {
 // the last bin), the crossing bin is found by a block prefix scan, and level 2 splits that bin
 // into HB sub-bins (z resolution 1.5e-5, finer than a bf16 logit step): three row passes instead
 // of the 26 bisection passes per constraint.  Values in the crossing sub-bin are all kept (the
-// same tie rule as a threshold compare).
+// same tie rule as a threshold compare).  Counts are exact (integer-valued float adds); the
+// top-p mass bins sum in atomic order, so a target within float rounding of a bin edge may pick
+// the neighbouring sub-bin from run to run (a 1.5e-5-wide logit band): seeded draws are
+// reproducible everywhere else.
 constexpr int HB = 2048;
 constexpr float HZ = 64.f;
 
