@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_kernel(
     const float* __restrict__ cos_sin, int rot_dim, bf16* __restrict__ q_out,
     typename KVStore<F>::T* __restrict__ k_cache, typename KVStore<F>::T* __restrict__ v_cache,
     const int* __restrict__ slots, int Hq, int Hkv, int apply_rope, const bf16* __restrict__ q_norm_w,
-    const bf16* __restrict__ k_norm_w, float qk_eps, float k_inv_scale, float v_inv_scale) {
+    const bf16* __restrict__ k_norm_w, float qk_eps, float k_inv_scale, float v_inv_scale, int v_rowmajor) {
   const int t = blockIdx.x;
   const bf16* row = qkv + (int64_t)t * qkv_stride;
   const int pos = positions[t];
@@ -99,15 +99,26 @@ __global__ __launch_bounds__(256) void rope_qkv_cache_kernel(
     }
   }
   // ---- V: transposed scatter into [page][kh][d][off] ----
+  // lanes take CONSECUTIVE dims: one wave store then covers 64 dim rows 2*P bytes apart (2 KB,
+  // 16 cache lines) instead of 64 rows 8 dims apart (64 lines), so the partial writes of a
+  // token's column coalesce per line
   if (slot >= 0) {
     const int64_t page = slot / P, off = slot % P;
     const bf16* vsrc = row + (int64_t)(Hq + Hkv) * D;
-    for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < Hkv * DV; i += gridDim.y * blockDim.x) {
-      const int kh = i / DV, dv = i % DV;
-      bf16x8 x = ld8(vsrc + kh * D + dv * 8);
-      typename KVStore<F>::T* dst = v_cache + ((page * Hkv + kh) * D + dv * 8) * P + off;
+    typename KVStore<F>::T* vbase = v_cache + page * Hkv * D * P + off;
+    if (!v_rowmajor) {
+      for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < Hkv * D; i += gridDim.y * blockDim.x) {
+        const float x = (float)vsrc[i];   // i = kh * D + d
+        kv_st1<F>(vbase + (int64_t)i * P, F == KV_BF16 ? x : x * v_inv_scale);
+      }
+    } else {   // previous mapping (8 dims per lane), kept for A/B (OME_ROPE_VMAP=1)
+      for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < Hkv * DV; i += gridDim.y * blockDim.x) {
+        const int kh = i / DV, dv = i % DV;
+        bf16x8 x = ld8(vsrc + kh * D + dv * 8);
+        typename KVStore<F>::T* dst = v_cache + ((page * Hkv + kh) * D + dv * 8) * P + off;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) kv_st1<F>(dst + j * P, F == KV_BF16 ? (float)x[j] : (float)x[j] * v_inv_scale);
+        for (int j = 0; j < 8; ++j) kv_st1<F>(dst + j * P, F == KV_BF16 ? (float)x[j] : (float)x[j] * v_inv_scale);
+      }
     }
   }
 }
@@ -147,6 +158,11 @@ OME_API int ome_rope_set_split(int ny) {
 }
 
 // kv_fmt: KVFmt of the cache tensors; k_scale / v_scale: dequantisation scales (fp8 only)
+static const int g_rope_vmap = [] {
+  const char* e = getenv("OME_ROPE_VMAP");
+  return e ? atoi(e) : 0;
+}();
+
 OME_API int ome_rope_qkv_cache(const void* qkv, int64_t qkv_stride, const int* positions, const float* cos_sin,
                                int rot_dim, void* q_out, void* k_cache, void* v_cache, const int* slots, int T,
                                int Hq, int Hkv, int D, int P, int apply_rope, const void* q_norm_w,
@@ -168,7 +184,7 @@ OME_API int ome_rope_qkv_cache(const void* qkv, int64_t qkv_stride, const int* p
   rope_qkv_cache_kernel<DD, 16, FF><<<grid, 256, 0, stream>>>(                                                    \
       (const bf16*)qkv, qkv_stride, positions, cos_sin, rot_dim, (bf16*)q_out, (KVStore<FF>::T*)k_cache,       \
       (KVStore<FF>::T*)v_cache, slots, Hq, Hkv, apply_rope, (const bf16*)q_norm_w, (const bf16*)k_norm_w,      \
-      qk_eps, ki, vi)
+      qk_eps, ki, vi, g_rope_vmap)
   if (D == 128) {
     if (kv_fmt == KV_BF16) LAUNCH(128, KV_BF16);
     else if (kv_fmt == KV_E4M3) LAUNCH(128, KV_E4M3);
