@@ -862,6 +862,10 @@ class PrefillPlan:
 
 
 PREFILL_SPLIT_TARGET = int(os.environ.get("OME_PREFILL_SPLIT_ITEMS", "128"))
+# an item must span more than this many keys before a small grid is split.  2048 since the causal
+# fast body (profiles/r03_prefill_split_bench_fast.txt): classic now wins at 700 and 2000 keys
+# (27 vs 34 us, 85 vs 93 us) and split still wins 256 new rows over a 4096-key prefix (53 vs 132 us)
+PREFILL_SPLIT_MIN_KEYS = int(os.environ.get("OME_PREFILL_SPLIT_MIN_KEYS", "2048"))
 
 
 def prefill_plan(q_lens: list[int], kv_lens: list[int], tile: int = 32, target: int | None = None,
@@ -875,7 +879,7 @@ def prefill_plan(q_lens: list[int], kv_lens: list[int], tile: int = 32, target: 
     ``target`` split items exist -- long prompts already have plenty of items and stay unsplit.
     Measured (profiles/r03_prefill_split_bench.txt): splitting pays when the classic grid is
     smaller than the chip (items x kv heads < 256 workgroups) AND some item has a long key range
-    (> 512 keys), e.g. 256 new rows over a 4096-token prefix 243 -> 68 us; at ~900 rows over
+    (> ``PREFILL_SPLIT_MIN_KEYS`` keys), e.g. 256 new rows over a 4096-token prefix 243 -> 68 us; at ~900 rows over
     <= 480 keys the classic grid is already full and splitting costs the partial round trip."""
     target = target or PREFILL_SPLIT_TARGET
     items = prefill_work_items(q_lens, kv_lens, tile)
@@ -885,7 +889,7 @@ def prefill_plan(q_lens: list[int], kv_lens: list[int], tile: int = 32, target: 
         e = (kv_lens[s] - q_lens[s]) + min(r + tile, q_lens[s])
         ends.append(e)
         work += e
-    if not force and (len(items) * kv_heads >= 256 or max(ends, default=0) <= 512):
+    if not force and (len(items) * kv_heads >= 256 or max(ends, default=0) <= PREFILL_SPLIT_MIN_KEYS):
         return items, [], [], 0, 0
     chunk = max(128, -(-(-(-work // max(1, target))) // 64) * 64)
     split, comb, parts = [], [], 0
