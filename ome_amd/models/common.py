@@ -1,6 +1,7 @@
 """Shared runtime structures for model forward passes: attention metadata and the paged KV cache."""
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -121,7 +122,7 @@ class PagedKVCache:
 # the headline (16.06k / 16.06k tok/s off vs 15.86k / 15.84k on, interleaved runs on one box,
 # profiles/r03_mixed_attention_overlap.txt) -- the prefill grid steals CUs the HBM-bound decode
 # kernel needs and the per-layer stream hand-offs add host work to every eager mixed step.
-_MIXED_OVERLAP = __import__("os").environ.get("OME_MIXED_OVERLAP", "0") == "1"
+_MIXED_OVERLAP = os.environ.get("OME_MIXED_OVERLAP", "0") == "1"
 _SIDE: dict = {}
 
 

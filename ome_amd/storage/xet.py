@@ -214,8 +214,12 @@ class XetClient:
         dest = Path(dest)
         dest.parent.mkdir(parents=True, exist_ok=True)
         part = dest.with_name(dest.name + ".xet.part")
-        with open(part, "wb") as f:
-            n = self.reconstruct(rec, f)
+        try:
+            with open(part, "wb") as f:
+                n = self.reconstruct(rec, f)
+        except BaseException:
+            part.unlink(missing_ok=True)   # no half-written part file left behind
+            raise
         if size is not None and n != size:
             os.unlink(part)
             raise XetError(f"{path}: reconstructed {n} bytes, expected {size}")
