@@ -364,6 +364,11 @@ OME_API int ome_comm_all_reduce(void* ctx, const void* in, void* out, int64_t n,
   hipError_t e = hipSuccess;
   // callers that produced the input straight into the IPC buffer skip the staging pass
   const u32x4* src = in != c->data ? (const u32x4*)in : nullptr;
+  // one-shot: peers read every index of this rank's IPC buffer while the kernel writes `out`;
+  // an output inside that buffer could be re-read (already reduced) by a slower peer
+  if (!two_shot && (const char*)out < (const char*)c->data + c->data_bytes &&
+      (const char*)out + bytes > (const char*)c->data)
+    return -4;
   const int64_t n_vec = n / 8;
   const int64_t red_vec = (int64_t)(c->data_bytes / 16);
   dim3 grid(blocks), block(kThreads);

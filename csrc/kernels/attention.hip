@@ -994,14 +994,17 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
 
   // FAST body: one online-softmax update per 32*SUB-key stage (one max reduction, one O
   // rescale) instead of per 32-key subtile.  Subtiles past kv_end are skipped in both MFMA
-  // passes; their keys lie past every row's causal limit, so the diagonal mask covers them.
+  // passes and their scores set to -inf here, so they never enter l whatever the alignment of
+  // kv_lo / the split chunk start (the diagonal mask alone covers them only while stages are
+  // 64-aligned to the causal limit).
   auto compute_fast = [&](int buf, int kb) __attribute__((always_inline)) {
     if (!active) return;
     f32x4 sc[SUB][2][2];
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
+      const float s0 = kb + 32 * u < kv_end ? 0.f : OME_NEG_INF;
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb) sc[u][rb][0] = sc[u][rb][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int rb = 0; rb < 2; ++rb) sc[u][rb][0] = sc[u][rb][1] = f32x4{s0, s0, s0, s0};
       if (kb + 32 * u < kv_end) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {

@@ -1,0 +1,354 @@
+// Stream-K bf16 GEMM for the decoder projections, "NT" layout:
+//   C[M][N] = X[M][K] . W[N][K]^T  (+ bias)          (= F.linear(x, w))
+//
+// Round-4 redesign of the decomposition around the 256-row MFMA tile of gemm.hip.  The tile body
+// (256 x BN output per 512-thread workgroup, BK = 64, v_mfma_f32_16x16x32_bf16, W as the MFMA A
+// operand so every lane owns 4 consecutive output columns, global_load_lds staging into
+// lane-linear LDS with the XOR swizzle on the source address) was measured at ~5 TF/CU; what
+// lost to hipBLASLt was tile-count quantisation (24 output tiles for 256 CUs at decode M = 256)
+// and the split-K fp32 round trip through a second launch (profiles/r03_bf16_gemm_tile_vs_hipblaslt.txt).
+//
+// Decomposition (per XCD, persistent):
+//   * the T output tiles are cut into 8 contiguous ranges, one per XCD group (blocks b with the
+//     same b % 8 share an XCD under round-robin dispatch -- a speed assumption only, nothing
+//     below depends on placement for correctness);
+//   * the nwg / 8 blocks of a group split the group's (tile, k-step) units evenly and walk
+//     them in order: a block computes the end of one tile, whole tiles, and the head of the next;
+//   * a segment that covers a whole tile stores through the fused epilogue directly; a partial
+//     segment writes its fp32 accumulators to a slab in FRAGMENT order (thread-private, 1 KiB
+//     contiguous per wave instruction) and takes a ticket; the tile's last arriver acquires the
+//     slabs and adds them into its own registers element-wise (the slab layout is its own
+//     accumulator layout, so no shuffle) and runs the epilogue.  Nothing ever waits on another
+//     workgroup (no co-residency assumption).  Hand-off = MI355X_MICROARCH.md "Valid forms"
+//     producer / consumer protocol: every storing wave vmcnt(0) -> barrier -> lane-0 agent
+//     release -> vmcnt(0) -> relaxed agent ticket; last arriver: agent acquire -> vmcnt(0) ->
+//     barrier -> plain loads.
+//   * nwg = T (with T % 8 == 0) degenerates to plain data-parallel tiles; nwg = 256 is full
+//     stream-K.  ops.gemm_sk_plan picks per shape from a measured table.
+// Pipeline: NBUF = 2 (BN = 256: 128 KiB LDS) or 3 (BN = 128: 3 x 48 KiB) K-tiles in LDS; with
+// three, the DMA of tile t+2 stays in flight across the barrier that publishes tile t+1
+// (counted vmcnt + raw s_barrier, cdna_hip_programming.md "Pipelining across barriers").
+// Epilogues: bf16 (+bias), SiLU(gate) * up for gate/up weights interleaved in 16-row blocks.
+#include "common.h"
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+namespace {
+
+constexpr int BM = 256, BK = 64, NTHR = 512;
+enum { SK_BF16 = 0, SK_SILU = 2 };
+
+__device__ __forceinline__ int sk_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// ROWS x 64 bf16 rows into lane-linear LDS: one wave instruction = 8 rows x 128 B.  Rows past
+// `rows` re-read the last valid row (their products are never stored).
+template <int ROWS>
+__device__ __forceinline__ void sk_stage(char* lds, const bf16* __restrict__ g, int64_t ld, int row0, int rows, int k0,
+                                         int wave, int lane) {
+  constexpr int PER = ROWS / 64;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int blk = wave * PER + j;
+    const int r = blk * 8 + (lane >> 3);
+    int gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    const bf16* src = g + (int64_t)gr * ld + k0 + sk_swz(r, lane & 7) * 8;
+    __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(lds + blk * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 sk_frag(const char* lds, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(lds + row * 128 + sk_swz(row, chunk) * 16);
+}
+
+typedef unsigned int sk_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float sk_silu(float x) { return x / (1.f + __expf(-x)); }
+
+// first block (local index) whose unit range contains unit u, for B blocks splitting U units
+// with block i covering [i*U/B, (i+1)*U/B)
+__device__ __forceinline__ int sk_block_of(int64_t u, int64_t U, int B) {
+  return (int)(((u + 1) * B + U - 1) / U) - 1;
+}
+
+template <int BN, int NBUF, int EPI>
+__global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict__ X, int64_t ldx,
+                                                          const bf16* __restrict__ W, int64_t ldw,
+                                                          const bf16* __restrict__ bias, bf16* __restrict__ out,
+                                                          int64_t ldo, int M, int N, int K,
+                                                          float* __restrict__ ws, int* __restrict__ cnt) {
+  constexpr int WT = BN * BK * 2, XT = BM * BK * 2, BUF = WT + XT;
+  constexpr int NI = BN / 32;          // 16-row W blocks per wave (a wave covers BN / 2 W rows)
+  constexpr int NH = NI / 2;
+  constexpr int LPT = (BN + BM) / 64;  // global_load_lds per thread per K-tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wn = wave & 1, wm = wave >> 1, fr = lane & 15, fc = lane >> 4;
+
+  const int tiles_m = (M + BM - 1) / BM, T = tiles_m * (N / BN), kt = K / BK;
+  const int grp = blockIdx.x & 7, lb = blockIdx.x >> 3, B = gridDim.x >> 3;
+  const int tile_lo = (int)((int64_t)T * grp / 8), tile_hi = (int)((int64_t)T * (grp + 1) / 8);
+  // whole tiles round-robin over the group's blocks (round r: tiles tile_lo + r*B + 0..B-1, so the
+  // blocks running together share W panels and X row tiles in the XCD's L2), then the remaining
+  // tiles' (tile, k-step) units split evenly: stream-K
+  const int R = (tile_hi - tile_lo) / B;
+  const int sk_lo = tile_lo + R * B;
+  const int64_t U = (int64_t)(tile_hi - sk_lo) * kt;
+  const int64_t u_beg = (int64_t)lb * U / B, u_end = (int64_t)(lb + 1) * U / B;
+
+  auto bw = [&](int b) { return smem + b * BUF; };
+  auto bx = [&](int b) { return smem + b * BUF + WT; };
+
+  f32x4 acc[NI][4];
+  bf16x8 x0[4], x1[4], wa[NH], wb[NH];
+
+  int r = 0;
+  int64_t u = u_beg;
+  while (true) {
+    int tile, t0, t1, tl = 0;
+    if (r < R) {
+      tile = tile_lo + r * B + lb;
+      t0 = 0;
+      t1 = kt;
+      ++r;
+    } else if (u < u_end) {
+      tl = (int)(u / kt);                          // tile index inside the stream-K range
+      tile = sk_lo + tl;
+      t0 = (int)(u - (int64_t)tl * kt);
+      const int64_t te = (int64_t)(tl + 1) * kt;
+      t1 = (int)((u_end < te ? u_end : te) - (int64_t)tl * kt);
+      u += t1 - t0;
+    } else {
+      break;
+    }
+    const int nt = t1 - t0;
+    const int tn = tile / tiles_m, tm = tile - tn * tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto stage = [&](int t, int b) {
+      sk_stage<BN>(bw(b), W, ldw, n0, N, t * BK, wave, lane);
+      sk_stage<BM>(bx(b), X, ldx, m0, M, t * BK, wave, lane);
+    };
+    auto rdx = [&](bf16x8 (&fx)[4], const char* lx, int kk) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fx[j] = sk_frag(lx, wm * 64 + j * 16 + fr, kk * 4 + fc);
+    };
+    auto rdw = [&](bf16x8 (&fw)[NH], const char* lw, int kk, int ih) {
+#pragma unroll
+      for (int i = 0; i < NH; ++i) fw[i] = sk_frag(lw, wn * (BN / 2) + (ih * NH + i) * 16 + fr, kk * 4 + fc);
+    };
+    auto mm = [&](const bf16x8 (&fx)[4], const bf16x8 (&fw)[NH], int ih) {
+#pragma unroll
+      for (int i = 0; i < NH; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[ih * NH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[i], fx[j], acc[ih * NH + i][j], 0, 0, 0);
+    };
+    // schedule of one phase: its MFMAs with the NR fragment reads of the NEXT phase (issued after
+    // them in program order) threaded one per MFMA gap, so the reads land while the MFMAs run and
+    // the next phase's MFMAs find their operands without a wait (T19 sched_group_barrier)
+    auto interleave = [&](auto nr_tag) {
+      constexpr int NR = decltype(nr_tag)::value;
+#pragma unroll
+      for (int k = 0; k < 4 * NH; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // 1 MFMA
+        if (k < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+      }
+    };
+
+    // ---- prologue: NBUF - 1 K-tiles in flight, wait for the first
+    stage(t0, 0);
+    if constexpr (NBUF == 3) {
+      if (nt > 1) {
+        stage(t0 + 1, 1);
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(LPT) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    rdx(x0, bx(0), 0);
+    rdw(wa, bw(0), 0, 0);
+    int cur = 0;
+    for (int i = 0; i < nt; ++i) {
+      // stage K-tile i + NBUF - 1 into the buffer read in iteration i - 1 (all of those reads
+      // were retired by the lgkmcnt(0) ahead of the barrier that ended iteration i - 1)
+      if (i + NBUF - 1 < nt) {
+        int sb = cur + NBUF - 1;
+        sb = sb >= NBUF ? sb - NBUF : sb;
+        stage(t0 + i + NBUF - 1, sb);
+      }
+      const char* lw = bw(cur);
+      const char* lx = bx(cur);
+      // four phases of 4*NH MFMAs (k-half kk, W half ih); each threads the next phase's reads
+      mm(x0, wa, 0);                       // (kk0, ih0)
+      rdw(wb, lw, 0, 1);
+      interleave(std::integral_constant<int, NH>{});
+      mm(x0, wb, 1);                       // (kk0, ih1)
+      rdx(x1, lx, 1);
+      rdw(wa, lw, 1, 0);
+      interleave(std::integral_constant<int, 4 + NH>{});
+      mm(x1, wa, 0);                       // (kk1, ih0)
+      rdw(wb, lw, 1, 1);
+      interleave(std::integral_constant<int, NH>{});
+      // K-tile i + 1 landed for this wave (tile i + 2's DMA may stay in flight), every LDS read
+      // of tile i retired, then the barrier publishes tile i + 1 to all waves
+      if (NBUF == 3 && i + 2 < nt)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(LPT) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      cur = cur + 1 == NBUF ? 0 : cur + 1;
+      mm(x1, wb, 1);                       // (kk1, ih1) + the next tile's first fragments
+      rdx(x0, bx(cur), 0);                 // (read unconditionally: past the last tile they are
+      rdw(wa, bw(cur), 0, 0);              //  unused in-bounds LDS words)
+      interleave(std::integral_constant<int, 4 + NH>{});
+    }
+
+    // ---- partial tile: fp32 slab in fragment order + ticket; the last arriver reduces.
+    // Write-through (sc1) slab stores and sc1 loads, so no release / acquire fence is needed
+    // (MI355X_MICROARCH.md "Valid forms", table row 1: every storing wave vmcnt(0) -> barrier ->
+    // one lane's relaxed agent-scope add; the last adder's workgroup loads every slab with sc1
+    // loads).  A fence here would write back the XCD L2's whole dirty set (~128 KiB per block).
+    if (nt != kt) {
+      const int64_t ts = (int64_t)tl * kt, te = ts + kt;   // the tile's units
+      const int first = sk_block_of(ts, U, B);
+      auto slab = [&](int blk) {   // one slab per (block, head-of-tile?) -> unique per segment
+        const int gb = blk * 8 + grp;
+        return __builtin_amdgcn_make_buffer_rsrc(ws + ((int64_t)gb * 2 + (blk == first ? 1 : 0)) * (int64_t)(BM * BN),
+                                                 (short)0, BM * BN * 4, 0x00020000);
+      };
+      {
+        const auto rs = slab(lb);
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sk_u32x4, acc[i][j]), rs,
+                                                   ((i * 4 + j) * NTHR + tid) * 16, 0, 16 /* sc1 */);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();   // every wave's slab stores are complete; every wave is past its LDS reads
+      int narr = 0;      // arrivals = non-empty blocks whose range meets the tile
+      for (int blk = first;;) {
+        ++narr;
+        const int64_t nu = (int64_t)(blk + 1) * U / B;
+        if (nu >= te) break;
+        blk = sk_block_of(nu, U, B);
+      }
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        const int tk = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = tk == narr - 1;
+        if (tk == narr - 1) __hip_atomic_store(&cnt[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // re-arm
+      }
+      __syncthreads();
+      const bool is_last = flag[0] != 0;
+      __syncthreads();   // flag word read by every wave before the next segment's DMA reuses LDS
+      if (!is_last) continue;
+      for (int blk = first;;) {
+        if (blk != lb) {
+          const auto rs = slab(blk);
+#pragma unroll
+          for (int ih = 0; ih < 2; ++ih) {   // half a slab per pass: 16 (BN 256) / 8 loads in flight
+            f32x4 v[NH][4];
+#pragma unroll
+            for (int i = 0; i < NH; ++i)
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                v[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                        rs, (((ih * NH + i) * 4 + j) * NTHR + tid) * 16, 0, 16));
+#pragma unroll
+            for (int i = 0; i < NH; ++i)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) acc[ih * NH + i][j] += v[i][j];
+          }
+        }
+        const int64_t nu = (int64_t)(blk + 1) * U / B;
+        if (nu >= te) break;
+        blk = sk_block_of(nu, U, B);
+      }
+    }
+
+    // ---- epilogue: lane (fr, fc) of (i, j) holds C[m0 + wm*64 + j*16 + fr][n0 + wn*BN/2 + i*16 + 4fc .. +3]
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + wm * 64 + j * 16 + fr;
+      if (m >= M) continue;
+      if constexpr (EPI == SK_BF16) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int n = n0 + wn * (BN / 2) + i * 16 + 4 * fc;
+          bf16x4 v;
+          if (bias) {
+            const bf16x4 bv = *reinterpret_cast<const bf16x4*>(bias + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (bf16)(acc[i][j][r] + (float)bv[r]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (bf16)acc[i][j][r];
+          }
+          *reinterpret_cast<bf16x4*>(out + (int64_t)m * ldo + n) = v;
+        }
+      } else {
+        // gate / up weight rows interleaved in 16-row blocks: W block 2i = gate, 2i + 1 = up
+#pragma unroll
+        for (int i = 0; i < NI; i += 2) {
+          const int n = ((n0 + wn * (BN / 2) + i * 16) >> 1) + 4 * fc;
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (bf16)(sk_silu(acc[i][j][r]) * acc[i + 1][j][r]);
+          *reinterpret_cast<bf16x4*>(out + (int64_t)m * ldo + n) = v;
+        }
+      }
+    }
+  }
+}
+
+template <int BN, int NBUF, int EPI>
+int launch_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, void* out, int64_t ldo, int M,
+              int N, int K, int nwg, float* ws, int* cnt, hipStream_t stream) {
+  constexpr int LDS = NBUF * (BN + BM) * BK * 2;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_sk_kernel<BN, NBUF, EPI>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  gemm_sk_kernel<BN, NBUF, EPI><<<nwg, NTHR, LDS, stream>>>((const bf16*)X, ldx, (const bf16*)W, ldw,
+                                                           (const bf16*)bias, (bf16*)out, ldo, M, N, K, ws, cnt);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// X [M][K] (row stride ldx), W [N][K] (row stride ldw), out [M][N] (or [M][N/2] for epi = 2).
+// bn in {128, 256}, N % bn == 0, K % 64 == 0, nwg % 8 == 0 (1..4096 blocks, one per CU resident:
+// 128 KiB / 144 KiB of LDS).  ws: >= nwg * 2 * 256 * bn floats; cnt: >= ceil(M/256) * N/bn ints,
+// zero before the first launch (the kernel re-arms them: HIP-graph replayable).  epi 0: bf16
+// (+ optional bias[N]); epi 2: SiLU(gate) * up with gate/up rows interleaved in 16-row blocks.
+OME_API int ome_gemm_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, void* out,
+                        int64_t ldo, int M, int N, int K, int bn, int epi, int nwg, void* ws, void* cnt,
+                        hipStream_t stream) {
+  if (M <= 0) return 0;
+  if ((bn != 128 && bn != 256) || N % bn || K % BK || K <= 0 || nwg < 8 || nwg % 8 || nwg > 4096) return -2;
+  if (ldx % 8 || ldw % 8 || ((uintptr_t)X | (uintptr_t)W) % 16 || ldo % 4 || (uintptr_t)out % 8) return -3;
+  if (epi != SK_BF16 && epi != SK_SILU) return -4;
+  if (epi == SK_SILU && bias) return -4;
+  if (!ws || !cnt) return -5;
+  float* w = (float*)ws;
+  int* c = (int*)cnt;
+#define SK_GO(BNV, NB)                                                                                     \
+  return epi == SK_BF16 ? launch_sk<BNV, NB, SK_BF16>(X, ldx, W, ldw, bias, out, ldo, M, N, K, nwg, w, c, stream) \
+                        : launch_sk<BNV, NB, SK_SILU>(X, ldx, W, ldw, bias, out, ldo, M, N, K, nwg, w, c, stream)
+  if (bn == 256) SK_GO(256, 2);
+  SK_GO(128, 3);
+#undef SK_GO
+}

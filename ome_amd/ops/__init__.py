@@ -845,6 +845,64 @@ def deinterleave_gate_up(y: torch.Tensor, block: int = 16):
     return v[:, :, 0].reshape(M, N // 2), v[:, :, 1].reshape(M, N // 2)
 
 
+# ---------------------------------------------------------------------------------------------
+# Stream-K MFMA GEMM (csrc/kernels/gemm_sk.hip): persistent per-XCD stream-K over 256 x bn
+# output tiles, fp32 partial slabs reduced in-launch by each tile's last arriver.  One workspace
+# per device (GEMMs of one engine run on one stream at a time; graph replays reuse it).
+_SK_MAX_WG = 256
+_SK_CNT = 1 << 16
+_SK_WS: dict = {}
+
+
+def _sk_workspace(device: torch.device):
+    w = _SK_WS.get(device.index)
+    if w is None:
+        ws = torch.empty(_SK_MAX_WG * 2 * 256 * 256, dtype=torch.float32, device=device)
+        cnt = torch.zeros(_SK_CNT, dtype=torch.int32, device=device)   # the kernel re-arms every ticket it takes
+        w = _SK_WS[device.index] = (ws, cnt)
+    return w
+
+
+def gemm_sk_tiles(M: int, N: int, bn: int) -> int:
+    return -(-M // 256) * (N // bn)
+
+
+def gemm_sk_ok(M: int, N: int, K: int, bn: int, nwg: int) -> bool:
+    """Shape / decomposition accepted by ``ome_gemm_sk`` with the shared workspace (blocks left
+    without a unit simply exit)."""
+    if bn not in (128, 256) or N % bn or K % 64 or K <= 0 or nwg % 8 or not 8 <= nwg <= _SK_MAX_WG or M <= 0:
+        return False
+    return gemm_sk_tiles(M, N, bn) <= _SK_CNT
+
+
+def gemm_sk(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
+            epi: int = 0, bn: int = 256, nwg: int = 256) -> torch.Tensor:
+    """out = x @ w.T (+ bias) on the stream-K MFMA kernel.  ``epi=2``: w holds gate/up rows
+    interleaved in 16-row blocks (:func:`interleave_gate_up`) and out = SiLU(gate) * up [M, N/2].
+    ``bn`` 128 | 256 output columns per tile, ``nwg`` workgroups (multiple of 8; = tiles gives
+    plain data-parallel tiles, 256 full stream-K)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not _gpu(x):
+        y = x.float() @ w.float().t()
+        if bias is not None:
+            y = y + bias.float()
+        if epi == 2:
+            g, u = deinterleave_gate_up(y)
+            y = F.silu(g) * u
+        y = y.to(x.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == 2 else N, dtype=x.dtype, device=x.device)
+    ws, cnt = _sk_workspace(x.device)
+    call("ome_gemm_sk", x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ptr(bias), out.data_ptr(),
+         out.stride(0), M, N, K, bn, epi, nwg, ws.data_ptr(), cnt.data_ptr(), stream_ptr())
+    return out
+
+
 class PrefillPlan:
     """Work decomposition of one prefill attention call, built host-side by
     :func:`prefill_plan` and uploaded with the step's other inputs.  ``items`` is the classic

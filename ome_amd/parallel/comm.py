@@ -72,15 +72,24 @@ class CustomAllReduce:
                 n * 2 <= self.max_bytes)
 
     def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """Sum of ``x`` over the group (in place unless ``out`` is given)."""
+        """Sum of ``x`` over the group (in place unless ``out`` is given; callers use the returned
+        tensor).  One-shot never writes into the registered IPC buffer: peers read every index of
+        it while this rank writes, so an in-place result there (``x`` produced straight into
+        :meth:`staging`) could be re-added by a slower peer.  Such calls get a fresh output."""
         out = x if out is None else out
         two = x.numel() * 2 > self.one_shot_max
+        if not two and self._in_buffer(out):
+            out = torch.empty_like(x)
         rc = self._lib.ome_comm_all_reduce(self._ctx, C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()),
                                            x.numel(), int(two), self._grid(x.numel(), two),
                                            C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
         if rc != 0:
             raise _native.NativeError(f"ome_comm_all_reduce failed ({rc})")
         return out
+
+    def _in_buffer(self, t: torch.Tensor) -> bool:
+        p = t.data_ptr()
+        return self._buf_ptr <= p < self._buf_ptr + self.max_bytes
 
     def staging(self, shape, dtype=torch.bfloat16, device=None) -> torch.Tensor | None:
         """A tensor view of this rank's registered IPC input buffer: a producer (the row-parallel

@@ -25,8 +25,14 @@ from ome_amd.runtime.tokenizer import get_tokenizer
 log = logging.getLogger("ome_amd.engine")
 
 
-_REASONS = ["stop", "length", "abort", "abort:error", "abort:kv_capacity"]
+_REASONS = ["stop", "length", "abort", "abort:error", "abort:kv_capacity", "abort:kv_layout_mismatch",
+            "abort:kv_transfer"]
 _REASON_CODE = {r: i for i, r in enumerate(_REASONS)}
+
+
+def _unknown_code(reason) -> int:
+    """Code of a finish reason missing from the table: "abort" for any abort:* (or other) reason."""
+    return _REASON_CODE["stop"] if reason in (None, "stop") else _REASON_CODE["abort"]
 
 
 def _unpack_updates(v: list[float]):
@@ -36,7 +42,8 @@ def _unpack_updates(v: list[float]):
         h, nt, fin, code = int(v[i]), int(v[i + 1]), bool(v[i + 2]), int(v[i + 3])
         toks = [int(t) for t in v[i + 4:i + 4 + nt]]
         i += 4 + nt
-        heads.append((h, toks, fin, _REASONS[code] if 0 <= code < len(_REASONS) else "stop"))
+        # a reason outside the table is still a failure, never a normal completion
+        heads.append((h, toks, fin, _REASONS[code] if 0 <= code < len(_REASONS) else "abort"))
     for h, toks, fin, reason in heads:   # log-probs follow all headers, in the same order
         lps = v[i:i + len(toks)]
         i += len(toks)
@@ -415,7 +422,7 @@ class Engine:
             toks = r.output_ids[k:]
             fin = r.state == ReqState.FINISHED
             packed += [float(getattr(r, "dp_handle", -1)), float(len(toks)), float(fin),
-                       float(_REASON_CODE.get(r.finish_reason, -1) if fin else -1)]
+                       float(_REASON_CODE.get(r.finish_reason, _unknown_code(r.finish_reason)) if fin else -1)]
             packed += [float(t) for t in toks]
             lps_all += [float(x) for x in r.output_logprobs[k:]]
             r._reported = len(r.output_ids)

@@ -54,15 +54,45 @@ class _DecodeBuffers:
         self.bmax = bmax
         n = (len(self.FIELDS_I) + len(self.FIELDS_F) + 2) * bmax
         self.dev = torch.zeros(n, dtype=torch.int32, device=device)
-        self.host = torch.zeros(n, dtype=torch.int32, pin_memory=device.type == "cuda")
-        self.hnp = self.host.numpy()
-        self.hf = self.hnp.view(np.float32)
+        # two pinned host images, alternated per step: with overlapped scheduling the host fills
+        # step n+1's fields while step n's copy kernel (which reads the mapped host pages when it
+        # runs) may still be queued; each image is refilled only after the event of the copy that
+        # last read it
+        self.cuda = device.type == "cuda"
+        self.hosts = [torch.zeros(n, dtype=torch.int32, pin_memory=self.cuda) for _ in range(2)]
+        self.events: list = [None, None]
+        self.k = 0
+        self._bind()
         self.off = {}
         o = 0
         for f in self.FIELDS_I + self.FIELDS_F:
             self.off[f] = o
             o += bmax
         self.off["seeds"] = o  # 2*bmax int32 words, 8-byte aligned (bmax even or o even)
+
+    def _bind(self) -> None:
+        self.host = self.hosts[self.k]
+        self.hnp = self.host.numpy()
+        self.hf = self.hnp.view(np.float32)
+
+    def next_host(self) -> None:
+        """Switch to the other host image, waiting for the copy that last read it."""
+        self.k ^= 1
+        ev = self.events[self.k]
+        if ev is not None:
+            ev.synchronize()
+        self._bind()
+
+    def copied(self) -> None:
+        """Call right after enqueueing the copy of the current image."""
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self.events[self.k] = ev
+
+    def sync_images(self) -> None:
+        """Make the other image equal to the current one (after a full re-initialisation)."""
+        self.hosts[self.k ^ 1].numpy()[:] = self.hnp
 
     def view(self, name: str, bs: int) -> torch.Tensor:
         o = self.off[name]
@@ -298,6 +328,7 @@ class ModelRunner:
         for name, v in (("rep", 1.0), ("top_p", 1.0)):   # neutral sampling params for the warm-up rows
             d.hf[d.off[name]:d.off[name] + d.bmax] = v
         d.hnp[d.off["top_k"]:d.off["top_k"] + d.bmax] = -1
+        d.sync_images()
         d.dev.copy_(d.host)
         torch.cuda.synchronize(self.device)
         stream = torch.cuda.Stream(self.device)
@@ -358,6 +389,7 @@ class ModelRunner:
         replay the smallest decode graph on one padding row (scratch slot, sequence length 0) so
         every MoE exchange has all participants."""
         d, bs = self.dbuf, self.buckets[0]
+        d.next_host()
         h, off = d.hnp, d.off
         for name, v in (("ids", 0), ("slots", -1), ("seq_lens", 0), ("pos", 0), ("src", -1), ("order", 0),
                         ("top_k", -1)):
@@ -366,6 +398,7 @@ class ModelRunner:
         for name, v in (("temp", 0.0), ("top_p", 1.0), ("min_p", 0.0), ("rep", 1.0), ("freq", 0.0), ("pres", 0.0)):
             d.hf[off[name]:off[name] + bs] = v
         copy_h2d(d.dev, d.host) if self.is_cuda else d.dev.copy_(d.host)
+        d.copied()
         if self.use_graph:
             self.graphs[bs].replay()
         else:
@@ -417,6 +450,7 @@ class ModelRunner:
                        graph: bool = True) -> "StepHandle":
         B = len(batch.chunks)
         d = self.dbuf
+        d.next_host()
         h, hf, off = d.hnp, d.hf, d.off
         h[off["ids"]:off["ids"] + bs] = 0
         h[off["slots"]:off["slots"] + bs] = -1
@@ -468,6 +502,7 @@ class ModelRunner:
         self._init_penalty_rows(batch.chunks)
         self._probe_mark("decode")
         copy_h2d(d.dev, d.host) if self.is_cuda else d.dev.copy_(d.host)
+        d.copied()
         if any_pending:
             ops.fill_pending(d.view("ids", bs), d.view("src", bs), prev.ids_dev)
         if self.use_graph and graph:

@@ -95,6 +95,7 @@ class XetClient:
     def __init__(self, hub, workers: int = 8, refresh_margin_s: float = 30.0, timeout: float = 60.0):
         self.hub = hub                      # storage.hfhub.HfHub (endpoint, token, resolve_url)
         self.workers = workers
+        self.prefetch = workers            # xorb ranges fetched / decoded ahead of the write position
         self.margin = refresh_margin_s
         self.timeout = timeout
         self._tokens: dict[str, XetConnection] = {}
@@ -165,11 +166,14 @@ class XetClient:
 
     def reconstruct(self, rec: dict, out) -> int:
         """Write the file described by a reconstruction response into the binary stream ``out``;
-        returns the bytes written."""
+        returns the bytes written.
+
+        Streams in file order: the xorb ranges are fetched + decoded by the worker pool at most
+        ``self.prefetch`` ahead of the term being written, and a decoded range is dropped right
+        after the last term that needs it, so peak memory is a few ranges (a few tens of MB),
+        not the whole file (a 5 GB shard must fit the model-agent's memory limit)."""
         terms = rec.get("terms") or []
         fetch = rec.get("fetch_info") or {}
-        # every (xorb, fetch entry) a term needs, fetched once
-        need: dict[tuple[str, int], dict] = {}
         plan = []
         for t in terms:
             h, cs, ce = t["hash"], t["range"]["start"], t["range"]["end"]
@@ -177,30 +181,53 @@ class XetClient:
                         if f["range"]["start"] <= cs and ce <= f["range"]["end"]), None)
             if ent is None:
                 raise XetError(f"no fetch range covers chunks {cs}-{ce} of xorb {h}")
-            need[(h, ent)] = fetch[h][ent]
             plan.append((h, ent, cs, ce, int(t.get("unpacked_length", -1))))
-        with cf.ThreadPoolExecutor(max(1, min(self.workers, len(need)))) as ex:
-            futs = {k: ex.submit(self._fetch, f["url"], f["url_range"]["start"], f["url_range"]["end"])
-                    for k, f in need.items()}
-            decoded = {}
-            for k, fut in futs.items():
-                data, offs = native.xet_decode(fut.result())
-                decoded[k] = (data, offs, need[k]["range"]["start"])
+        # keys in order of first use, and the index of each key's last use
+        order, last_use = [], {}
+        for i, (h, ent, *_rest) in enumerate(plan):
+            k = (h, ent)
+            if k not in last_use:
+                order.append(k)
+            last_use[k] = i
+
+        def fetch_decode(k):
+            f = fetch[k[0]][k[1]]
+            data, offs = native.xet_decode(self._fetch(f["url"], f["url_range"]["start"], f["url_range"]["end"]))
+            return data, offs, f["range"]["start"]
+
+        window = max(1, int(getattr(self, "prefetch", 0) or self.workers))
         skip = int(rec.get("offset_into_first_range", 0))
         written = 0
-        for h, ent, cs, ce, ulen in plan:
-            data, offs, first = decoded[(h, ent)]
-            a, b = cs - first, ce - first
-            if b >= len(offs):
-                raise XetError(f"xorb {h}: fetched range holds {len(offs) - 1} chunks, term needs {b}")
-            piece = data[offs[a]:offs[b]]
-            if ulen >= 0 and len(piece) != ulen:
-                raise XetError(f"xorb {h} chunks {cs}-{ce}: {len(piece)} bytes, expected {ulen}")
-            if skip:
-                cut = min(skip, len(piece))
-                piece, skip = piece[cut:], skip - cut
-            out.write(piece)
-            written += len(piece)
+        live: dict = {}          # key -> future (submitted, not yet dropped)
+        nxt = 0                  # next key of `order` to submit
+        with cf.ThreadPoolExecutor(max(1, min(self.workers, len(order) or 1))) as ex:
+            try:
+                for i, (h, ent, cs, ce, ulen) in enumerate(plan):
+                    k = (h, ent)
+                    # keep `window` ranges in flight or decoded ahead of the write position
+                    while nxt < len(order) and (len(live) < window or order[nxt] == k):
+                        live[order[nxt]] = ex.submit(fetch_decode, order[nxt])
+                        nxt += 1
+                    with self._lock:
+                        self.stats["peak_live_ranges"] = max(self.stats.get("peak_live_ranges", 0), len(live))
+                    data, offs, first = live[k].result()
+                    a, b = cs - first, ce - first
+                    if b >= len(offs):
+                        raise XetError(f"xorb {h}: fetched range holds {len(offs) - 1} chunks, term needs {b}")
+                    piece = data[offs[a]:offs[b]]
+                    if ulen >= 0 and len(piece) != ulen:
+                        raise XetError(f"xorb {h} chunks {cs}-{ce}: {len(piece)} bytes, expected {ulen}")
+                    if skip:
+                        cut = min(skip, len(piece))
+                        piece, skip = piece[cut:], skip - cut
+                    out.write(piece)
+                    written += len(piece)
+                    del piece, data
+                    if last_use[k] == i:
+                        del live[k]      # the decoded range is no longer referenced
+            finally:
+                for fut in live.values():
+                    fut.cancel()
         return written
 
     def download(self, repo: str, path: str, dest: str | Path, rev: str = "main", size: int | None = None,

@@ -78,6 +78,17 @@ def _worker(rank, world, port, q):
             y_ref = r_ref * torch.rsqrt(r_ref.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float().cpu()
             worst = max(worst, ((res.float().cpu() - r_ref).abs() / (r_ref.abs() + 1)).max().item())
             worst = max(worst, ((y.float().cpu() - y_ref).abs() / (y_ref.abs() + 1)).max().item())
+        # plain all-reduce of an input produced straight into the IPC buffer at one-shot sizes
+        # (dense MLP partials of MoE models, non-last pipeline stages): the result must not be
+        # written over the buffer peers are still reading
+        for it in range(4):
+            for rows, H in ((1, 4096), (16, 4096), (24, 4096)):
+                st = ar.staging((rows, H))
+                st.copy_(_inputs(rank, rows * H, 500 + it + rows).view(rows, H).cuda())
+                y = ar.all_reduce(st)
+                assert not ar._in_buffer(y)
+                want = sum(_inputs(r, rows * H, 500 + it + rows).float() for r in range(world)).view(rows, H)
+                worst = max(worst, ((y.float().cpu() - want).abs() / (want.abs() + 1)).max().item())
         # all-gather along the last dim (vocab-parallel logits)
         for rows, cols in ((1, 512), (7, 1024), (256, 16032)):
             x = _inputs(rank, rows * cols, 400 + rows).view(rows, cols).cuda()

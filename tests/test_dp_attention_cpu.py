@@ -73,3 +73,15 @@ def test_dp_attention_ep_matches_single(tmp_path, kind):
         assert p.exitcode == 0
     assert owners == {0, 1}  # both ranks served requests
     assert got == want
+
+
+def test_dp_relay_unknown_finish_reason_is_an_abort():
+    """The DP-attention token relay packs finish reasons as codes: a reason outside the table
+    (e.g. a PD transfer failure) must reach the client as an abort, never as a normal stop."""
+    from ome_amd.runtime import engine as E
+
+    assert E._unknown_code("abort:something_new") == E._REASON_CODE["abort"]
+    assert E._REASONS[E._REASON_CODE["abort:kv_layout_mismatch"]] == "abort:kv_layout_mismatch"
+    packed = [1.0, 7.0, 1.0, 1.0, 99.0, 42.0, -0.5]   # one update: handle 7, 1 token, finished, code 99
+    (h, toks, lps, fin, reason), = E._unpack_updates(packed)
+    assert (h, toks, fin, reason) == (7, [42], True, "abort")

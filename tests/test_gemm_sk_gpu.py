@@ -1,0 +1,134 @@
+"""csrc/kernels/gemm_sk.hip: per-XCD stream-K MFMA GEMM (fragment-order fp32 slabs, last-arriver
+in-launch reduction, 2- and 3-stage global_load_lds pipelines, bf16+bias and SiLU*mul epilogues)
+against an fp32 PyTorch reference."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ome_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _ref(x, w, b=None):
+    y = x.float() @ w.float().t()
+    return y + b.float() if b is not None else y
+
+
+def _rel(a, b):
+    return ((a.float() - b).abs().max() / (b.abs().max() + 1e-6)).item()
+
+
+def _nwgs(M, N, K, bn):
+    T = ops.gemm_sk_tiles(M, N, bn)
+    cands = {8, 64, 128, 200, 256}
+    if T % 8 == 0 and T <= 256:
+        cands.add(T)
+    return sorted(c for c in cands if ops.gemm_sk_ok(M, N, K, bn, c))
+
+
+@pytest.mark.parametrize("M", [1, 37, 256, 300, 913])
+@pytest.mark.parametrize("N,K", [(256, 64), (512, 4096), (6144, 4096), (4096, 14336)])
+@pytest.mark.parametrize("bn", [128, 256])
+def test_gemm_sk_plain(M, N, K, bn):
+    torch.manual_seed(M + N + K + bn)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
+    ref = _ref(x, w)
+    for nwg in _nwgs(M, N, K, bn):
+        y = ops.gemm_sk(x, w, bn=bn, nwg=nwg)
+        assert y.shape == (M, N)
+        assert _rel(y, ref) < 1e-2, (nwg, _rel(y, ref))
+
+
+def test_gemm_sk_identity_asymmetric():
+    """A = I-like selector with an asymmetric B: catches a transposed / permuted C write, in every
+    decomposition (whole tiles, split tiles, partial slabs of several arrivers)."""
+    M, N, K = 512, 1024, 512
+    x = torch.zeros(M, K, device=DEV, dtype=torch.bfloat16)
+    x[torch.arange(M), torch.arange(M) % K] = 1
+    w = (torch.arange(N, device=DEV).view(N, 1) * 1000 + torch.arange(K, device=DEV).view(1, K)).float()
+    w = (w % 251).to(torch.bfloat16)
+    ref = _ref(x, w)
+    for bn in (128, 256):
+        for nwg in _nwgs(M, N, K, bn):
+            assert torch.equal(ops.gemm_sk(x, w, bn=bn, nwg=nwg).float(), ref), (bn, nwg)
+
+
+@pytest.mark.parametrize("M", [1, 64, 256, 700])
+@pytest.mark.parametrize("bn", [128, 256])
+def test_gemm_sk_silu_mul(M, bn):
+    I, H = 1792, 1024
+    torch.manual_seed(M)
+    x = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(2 * I, H, device=DEV, dtype=torch.bfloat16) / H ** 0.5
+    wi = ops.interleave_gate_up(w)
+    g, u = _ref(x, w[:I]), _ref(x, w[I:])
+    ref = F.silu(g) * u
+    for nwg in _nwgs(M, 2 * I, H, bn):
+        y = ops.gemm_sk(x, wi, epi=2, bn=bn, nwg=nwg)
+        assert y.shape == (M, I)
+        assert _rel(y, ref) < 1e-2, nwg
+
+
+def test_gemm_sk_bias_and_strided():
+    M, N, K = 300, 768, 1024
+    big = torch.randn(M, K + 128, device=DEV, dtype=torch.bfloat16)
+    x = big[:, 64:64 + K]
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    out_big = torch.zeros(M, N + 64, device=DEV, dtype=torch.bfloat16)
+    for bn in (128, 256):
+        for nwg in _nwgs(M, N, K, bn):
+            y = ops.gemm_sk(x, w, b, out=out_big[:, :N], bn=bn, nwg=nwg)
+            assert _rel(y, _ref(x, w, b)) < 1e-2
+    assert out_big[:, N:].abs().max().item() == 0   # nothing written past the output view
+
+
+def test_gemm_sk_repeat_and_graph_replay():
+    """Tickets are re-armed by each tile's last arriver: repeated launches and HIP-graph replays
+    of a split decomposition give the same result."""
+    M, N, K = 256, 6144, 4096
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
+    ref = _ref(x, w)
+    y0 = ops.gemm_sk(x, w, bn=128, nwg=256)
+    for _ in range(5):
+        assert _rel(ops.gemm_sk(x, w, bn=128, nwg=256), ref) < 1e-2
+    out = torch.empty_like(y0)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.gemm_sk(x, w, out=out, bn=128, nwg=256)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.gemm_sk(x, w, out=out, bn=128, nwg=256)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert _rel(out, ref) < 1e-2
+
+
+def test_gemm_sk_rejects_bad_arguments():
+    x = torch.randn(16, 64, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(256, 64, device=DEV, dtype=torch.bfloat16)
+    assert not ops.gemm_sk_ok(16, 256, 64, 256, 12)      # nwg not a multiple of 8
+    assert not ops.gemm_sk_ok(16, 200, 64, 128, 8)       # N not a multiple of bn
+    for bn, nwg in ((256, 12), (64, 8)):
+        with pytest.raises(ops.NativeError):
+            ops.gemm_sk(x, w, bn=bn, nwg=nwg)
+
+
+def test_gemm_sk_more_blocks_than_units():
+    """Tiny K: fewer (tile, k-step) units than blocks in a group -- empty blocks exit and the
+    ticket count only includes blocks that own units."""
+    for M, N, K in ((16, 256, 64), (300, 512, 128), (513, 1024, 192)):
+        x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
+        for bn in (128, 256):
+            for nwg in (16, 64, 256):
+                assert _rel(ops.gemm_sk(x, w, bn=bn, nwg=nwg), _ref(x, w)) < 1e-2, (M, N, K, bn, nwg)

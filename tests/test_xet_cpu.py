@@ -313,3 +313,32 @@ def test_snapshot_download_uses_xet_for_xet_files(hub, tmp_path):
     assert hub.cdn_gets >= 1 and hub.recon_gets == 2   # config.json over HTTP, the rest from CAS
     again = hfhub.snapshot_download("org/x", tmp_path / "snap", token="hf_tok", endpoint=hub.url)
     assert again["xet_files"] == 2 and hub.recon_gets == 2, "present + verified files are kept"
+
+
+def test_reconstruct_streams_with_bounded_window():
+    """A many-xorb file is written in file order with at most ``prefetch`` decoded ranges alive
+    (plus ranges a later term still needs): peak memory does not grow with the file."""
+    n = 48
+    blobs = [os.urandom(1000) + bytes([i]) * 64000 for i in range(n)]
+    xorbs = {f"X{i}": chunk(b, 1 if i % 2 else 0) for i, b in enumerate(blobs)}
+    terms = [{"hash": f"X{i}", "unpacked_length": len(blobs[i]), "range": {"start": 0, "end": 1}} for i in range(n)]
+    terms.append({"hash": "X0", "unpacked_length": len(blobs[0]), "range": {"start": 0, "end": 1}})  # X0 reused last
+    fetch = {h: [{"range": {"start": 0, "end": 1}, "url": h, "url_range": {"start": 0, "end": len(x) - 1}}]
+             for h, x in xorbs.items()}
+    fetched = []
+
+    class Local(xet.XetClient):
+        def _fetch(self, url, start, end):
+            fetched.append(url)
+            return xorbs[url][start:end + 1]
+
+    xc = Local(hub=None, workers=4)
+    xc.prefetch = 3
+    import io
+
+    buf = io.BytesIO()
+    wrote = xc.reconstruct({"terms": terms, "fetch_info": fetch}, buf)
+    want = b"".join(blobs) + blobs[0]
+    assert buf.getvalue() == want and wrote == len(want)
+    assert sorted(fetched) == sorted(xorbs)                      # every range fetched exactly once
+    assert xc.stats["peak_live_ranges"] <= xc.prefetch + 1       # X0 stays alive for its last term
