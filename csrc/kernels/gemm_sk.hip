@@ -58,6 +58,13 @@ __device__ __forceinline__ void sk_stage(char* lds, const bf16* __restrict__ g, 
   }
 }
 
+// LDS-DMA of 16 B per lane: buffer_load_dwordx4 ... lds (a non-template wrapper: the builtin
+// only exists for the device target, and inside the kernel template the host pass dropped the
+// kernel's stub)
+__device__ __forceinline__ void sk_buf_lds(__amdgpu_buffer_rsrc_t rs, char* lds, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 16, voff, soff, 0, 0);
+}
+
 __device__ __forceinline__ bf16x8 sk_frag(const char* lds, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds + row * 128 + sk_swz(row, chunk) * 16);
 }
@@ -131,9 +138,60 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto stage = [&](int t, int b) {
-      sk_stage<BN>(bw(b), W, ldw, n0, N, t * BK, wave, lane);
-      sk_stage<BM>(bx(b), X, ldx, m0, M, t * BK, wave, lane);
+    // One K-tile = LPT DMA pieces per thread (piece q < BN/64: 8 W rows x 128 B per wave
+    // instruction, else 8 X rows).  The pieces of tile T are threaded through the MFMA phases:
+    // S4 of them in phase 4 of iteration T - NBUF (right after the barrier that frees buffer
+    // T % NBUF), S1 in phase 1 and S2 in phase 2 of iteration T - NBUF + 1 -- an LDS-DMA issue
+    // costs 60-185 cycles, and issued as one burst by every wave right after a barrier it left
+    // the MFMA pipe idle (measured: ~25 % of the kernel, profiles/r04_gemm_sk_probe.txt).
+    constexpr int PW = BN / 64;
+    constexpr int S4 = (LPT + 2) / 3, S1 = (LPT + 1) / 3, S2 = LPT - S4 - S1;
+    // buffer_load ... lds: scalar base per segment (the tile's first W / X row), one 32-bit
+    // loop-invariant row offset per piece and the K offset in soffset -- 1 VGPR per piece
+    // instead of a 64-bit address (the 64-bit form spilled at BN = 256)
+    const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (int64_t)n0 * ldw), (short)0, 0x7fffffff,
+                                                       0x00020000);
+    const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (int64_t)m0 * ldx), (short)0, 0x7fffffff,
+                                                       0x00020000);
+    uint32_t vo[LPT];
+#pragma unroll
+    for (int q = 0; q < LPT; ++q) {
+      if (q < PW) {
+        const int r = (wave * PW + q) * 8 + (lane >> 3);
+        vo[q] = (uint32_t)((r * ldw + sk_swz(r, lane & 7) * 8) * 2);
+      } else {
+        const int r = (wave * (BM / 64) + (q - PW)) * 8 + (lane >> 3);
+        const int rr = m0 + r < M ? r : M - 1 - m0;   // rows past M re-read the last row
+        vo[q] = (uint32_t)((rr * ldx + sk_swz(r, lane & 7) * 8) * 2);
+      }
+    }
+    auto piece = [&](int t, int b, auto q_tag) {
+      constexpr int q = decltype(q_tag)::value;
+      if constexpr (q < PW)
+        sk_buf_lds(rsw, bw(b) + (wave * PW + q) * 1024, vo[q], t * BK * 2);
+      else
+        sk_buf_lds(rsx, bx(b) + (wave * (BM / 64) + q - PW) * 1024, vo[q], t * BK * 2);
+    };
+    auto pieces = [&](int T, int b, auto q0_tag, auto q1_tag) {   // pieces [q0, q1) of relative tile T
+      constexpr int q0 = decltype(q0_tag)::value, q1 = decltype(q1_tag)::value;
+      // issued unconditionally (no branch: a branch cuts the scheduling region and the pieces
+      // could not be threaded between MFMAs); past the segment's last K-tile they re-read that
+      // tile into a buffer nothing reads any more -- in bounds, and retired in issue order by the
+      // next vmcnt wait, before any later DMA into the same buffer lands
+      const int t = t0 + (T < nt ? T : nt - 1);
+      if constexpr (q0 < q1) piece(t, b, std::integral_constant<int, q0>{});
+      if constexpr (q0 + 1 < q1) piece(t, b, std::integral_constant<int, q0 + 1>{});
+      if constexpr (q0 + 2 < q1) piece(t, b, std::integral_constant<int, q0 + 2>{});
+      if constexpr (q0 + 3 < q1) piece(t, b, std::integral_constant<int, q0 + 3>{});
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using IS4 = std::integral_constant<int, S4>;
+    using IS41 = std::integral_constant<int, S4 + S1>;
+    using ILPT = std::integral_constant<int, LPT>;
+    auto stage_all = [&](int T, int b) {
+      pieces(T, b, I0{}, IS4{});
+      pieces(T, b, IS4{}, IS41{});
+      pieces(T, b, IS41{}, ILPT{});
     };
     auto rdx = [&](bf16x8 (&fx)[4], const char* lx, int kk) {
 #pragma unroll
@@ -150,65 +208,65 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
         for (int j = 0; j < 4; ++j)
           acc[ih * NH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[i], fx[j], acc[ih * NH + i][j], 0, 0, 0);
     };
-    // schedule of one phase: its MFMAs with the NR fragment reads of the NEXT phase (issued after
-    // them in program order) threaded one per MFMA gap, so the reads land while the MFMAs run and
-    // the next phase's MFMAs find their operands without a wait (T19 sched_group_barrier)
-    auto interleave = [&](auto nr_tag) {
-      constexpr int NR = decltype(nr_tag)::value;
+    // schedule of one phase: its MFMAs with NV DMA pieces and the NR fragment reads of the NEXT
+    // phase (issued after them in program order) threaded one per MFMA gap, so the reads land
+    // while the MFMAs run and the next phase's MFMAs find their operands without a wait (T19)
+    auto interleave = [&](auto nr_tag, auto nv_tag) {
+      constexpr int NR = decltype(nr_tag)::value, NV = decltype(nv_tag)::value;
 #pragma unroll
       for (int k = 0; k < 4 * NH; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);             // 1 MFMA
+        if (k < NV) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);  // 1 LDS-DMA piece
         if (k < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
       }
     };
+    auto bufp = [&](int k) { return k >= NBUF ? k - NBUF : k; };   // k < 2 * NBUF
 
-    // ---- prologue: NBUF - 1 K-tiles in flight, wait for the first
-    stage(t0, 0);
+    // ---- prologue: tiles 0 .. NBUF-2 whole, the phase-4 share of tile NBUF-1, wait for tile 0
+    stage_all(0, 0);
+    if constexpr (NBUF == 3) stage_all(1, 1);
     if constexpr (NBUF == 3) {
-      if (nt > 1) {
-        stage(t0 + 1, 1);
+      if (nt > 1)
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(LPT) : "memory");
-      } else {
+      else
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      }
     } else {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     }
+    pieces(NBUF - 1, NBUF - 1, I0{}, IS4{});
     rdx(x0, bx(0), 0);
     rdw(wa, bw(0), 0, 0);
     int cur = 0;
     for (int i = 0; i < nt; ++i) {
-      // stage K-tile i + NBUF - 1 into the buffer read in iteration i - 1 (all of those reads
-      // were retired by the lgkmcnt(0) ahead of the barrier that ended iteration i - 1)
-      if (i + NBUF - 1 < nt) {
-        int sb = cur + NBUF - 1;
-        sb = sb >= NBUF ? sb - NBUF : sb;
-        stage(t0 + i + NBUF - 1, sb);
-      }
       const char* lw = bw(cur);
       const char* lx = bx(cur);
+      const int nb = bufp(cur + NBUF - 1);   // buffer of tile i + NBUF - 1 (freed in iteration i - 1)
       // four phases of 4*NH MFMAs (k-half kk, W half ih); each threads the next phase's reads
       mm(x0, wa, 0);                       // (kk0, ih0)
       rdw(wb, lw, 0, 1);
-      interleave(std::integral_constant<int, NH>{});
+      pieces(i + NBUF - 1, nb, IS4{}, IS41{});
+      interleave(std::integral_constant<int, NH>{}, std::integral_constant<int, S1>{});
       mm(x0, wb, 1);                       // (kk0, ih1)
       rdx(x1, lx, 1);
       rdw(wa, lw, 1, 0);
-      interleave(std::integral_constant<int, 4 + NH>{});
+      pieces(i + NBUF - 1, nb, IS41{}, ILPT{});
+      interleave(std::integral_constant<int, 4 + NH>{}, std::integral_constant<int, S2>{});
       mm(x1, wa, 0);                       // (kk1, ih0)
       rdw(wb, lw, 1, 1);
-      interleave(std::integral_constant<int, NH>{});
-      // K-tile i + 1 landed for this wave (tile i + 2's DMA may stay in flight), every LDS read
-      // of tile i retired, then the barrier publishes tile i + 1 to all waves
+      interleave(std::integral_constant<int, NH>{}, I0{});
+      // K-tile i + 1 landed for this wave (with three buffers tile i + 2's pieces may stay in
+      // flight), every LDS read of tile i retired, then the barrier publishes tile i + 1
       if (NBUF == 3 && i + 2 < nt)
         asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(LPT) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      const int freed = cur;
       cur = cur + 1 == NBUF ? 0 : cur + 1;
       mm(x1, wb, 1);                       // (kk1, ih1) + the next tile's first fragments
       rdx(x0, bx(cur), 0);                 // (read unconditionally: past the last tile they are
       rdw(wa, bw(cur), 0, 0);              //  unused in-bounds LDS words)
-      interleave(std::integral_constant<int, 4 + NH>{});
+      pieces(i + NBUF, freed, I0{}, IS4{});   // tile i + NBUF into the buffer tile i just left
+      interleave(std::integral_constant<int, 4 + NH>{}, std::integral_constant<int, S4>{});
     }
 
     // ---- partial tile: fp32 slab in fragment order + ticket; the last arriver reduces.

@@ -34,8 +34,11 @@ struct Fd {
   }
 };
 
+std::atomic<uint64_t> g_bytes_read{0};   // bytes pread by this process (loader stats)
+
 // pread the whole [off, off+len) range, retrying short reads.
 bool pread_full(int fd, void* dst, uint64_t len, uint64_t off) {
+  g_bytes_read.fetch_add(len, std::memory_order_relaxed);
   auto* p = static_cast<char*>(dst);
   while (len) {
     ssize_t r = pread(fd, p, std::min<uint64_t>(len, 1ull << 30), static_cast<off_t>(off));
@@ -195,6 +198,86 @@ OMEIO_API int omeio_load_ranges(const char* path, int n, const uint64_t* offs, c
   for (auto& x : th) x.join();
   return err ? fail(err, std::string("device load failed: ") + path) : 0;
 }
+
+// Column shard of a row-major [nrows][*] tensor: nrows slices of row_bytes at
+// file_off + r * file_stride, packed contiguously into dst (the [nrows][row_bytes] shard of a
+// row-parallel TP weight).  Only the slices are read and only they reach HBM: each thread
+// preads a run of rows into its pinned stage (one pread per row) and sends the packed run with
+// ONE hipMemcpyAsync, double-buffered.
+OMEIO_API int omeio_load_strided(const char* path, uint64_t file_off, uint64_t nrows, uint64_t file_stride,
+                                 uint64_t row_bytes, void* dst, void* stream, int nthreads, uint64_t chunk) {
+  if (nrows == 0 || row_bytes == 0) return 0;
+  Fd f(open(path, O_RDONLY | O_CLOEXEC));
+  if (f.fd < 0) return fail(-ENOENT, std::string("open ") + path + ": " + strerror(errno));
+  if (chunk == 0) chunk = 16ull << 20;
+  if (hipStreamSynchronize(static_cast<hipStream_t>(stream)) != hipSuccess) return fail(-EIO, "stream sync failed");
+  const uint64_t rows_per = std::max<uint64_t>(1, chunk / row_bytes);
+  const uint64_t nruns = (nrows + rows_per - 1) / rows_per;
+  const uint64_t stage_bytes = rows_per * row_bytes;
+  nthreads = std::max(1, std::min<int>(nthreads, static_cast<int>(nruns)));
+  std::atomic<int> err{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    th.emplace_back([&, t] {
+      hipStream_t s;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        err = -EIO;
+        return;
+      }
+      void* stage[2] = {nullptr, nullptr};
+      hipEvent_t ev[2];
+      bool used[2] = {false, false};
+      for (int b = 0; b < 2; ++b) {
+        if (hipHostMalloc(&stage[b], stage_bytes, hipHostMallocDefault) != hipSuccess) err = -ENOMEM;
+        hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
+      }
+      const uint64_t lo = nruns * t / nthreads, hi = nruns * (t + 1) / nthreads;
+      int b = 0;
+      for (uint64_t run = lo; run < hi && !err.load(); ++run, b ^= 1) {
+        if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) {
+          err = -EIO;
+          break;
+        }
+        const uint64_t r0 = run * rows_per, nr = std::min(rows_per, nrows - r0);
+        char* st = static_cast<char*>(stage[b]);
+        for (uint64_t r = 0; r < nr; ++r)
+          if (!pread_full(f.fd, st + r * row_bytes, row_bytes, file_off + (r0 + r) * file_stride)) {
+            err = -EIO;
+            break;
+          }
+        if (err.load()) break;
+        if (hipMemcpyAsync(static_cast<char*>(dst) + r0 * row_bytes, st, nr * row_bytes, hipMemcpyHostToDevice, s) !=
+                hipSuccess ||
+            hipEventRecord(ev[b], s) != hipSuccess) {
+          err = -EIO;
+          break;
+        }
+        used[b] = true;
+      }
+      hipStreamSynchronize(s);
+      for (int k = 0; k < 2; ++k) {
+        if (stage[k]) hipHostFree(stage[k]);
+        hipEventDestroy(ev[k]);
+      }
+      hipStreamDestroy(s);
+    });
+  }
+  for (auto& x : th) x.join();
+  return err ? fail(err, std::string("strided device load failed: ") + path) : 0;
+}
+
+// host-memory form of omeio_load_strided (CPU loads and tests)
+OMEIO_API int omeio_read_strided(const char* path, uint64_t file_off, uint64_t nrows, uint64_t file_stride,
+                                 uint64_t row_bytes, void* dst) {
+  Fd f(open(path, O_RDONLY | O_CLOEXEC));
+  if (f.fd < 0) return fail(-ENOENT, std::string("open ") + path + ": " + strerror(errno));
+  for (uint64_t r = 0; r < nrows; ++r)
+    if (!pread_full(f.fd, static_cast<char*>(dst) + r * row_bytes, row_bytes, file_off + r * file_stride))
+      return fail(-EIO, std::string("strided read failed: ") + path);
+  return 0;
+}
+
+OMEIO_API uint64_t omeio_bytes_read() { return g_bytes_read.load(); }
 
 OMEIO_API int omeio_md5_file(const char* path, char* md5_hex) {
   Fd f(open(path, O_RDONLY | O_CLOEXEC));

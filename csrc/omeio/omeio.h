@@ -31,6 +31,16 @@ OMEIO_API int omeio_load_ranges(const char* path, int n, const uint64_t* file_of
 OMEIO_API int omeio_read_ranges(const char* path, int n, const uint64_t* file_offsets, const uint64_t* sizes,
                                 void* const* dst_host, int nthreads);
 
+// Column shard of a row-major tensor: nrows slices of row_bytes starting at file_off with a
+// file_stride between rows, packed contiguously into device memory (TP row-parallel weights:
+// each rank reads and uploads only its 1/TP of every row).  omeio_read_strided: same, to host.
+OMEIO_API int omeio_load_strided(const char* path, uint64_t file_off, uint64_t nrows, uint64_t file_stride,
+                                 uint64_t row_bytes, void* dst_device, void* stream, int nthreads, uint64_t chunk);
+OMEIO_API int omeio_read_strided(const char* path, uint64_t file_off, uint64_t nrows, uint64_t file_stride,
+                                 uint64_t row_bytes, void* dst_host);
+// Bytes pread by this process so far (loader statistics).
+OMEIO_API uint64_t omeio_bytes_read();
+
 // Parallel chunked copy src -> dst (creates/truncates dst).  If md5_hex (33 bytes) is non-null
 // it receives the MD5 of the content.
 OMEIO_API int omeio_copy_file(const char* src, const char* dst, int nthreads, char* md5_hex);

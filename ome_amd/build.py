@@ -77,7 +77,19 @@ def _build_lib(name: str, sources: list[Path], headers: list[Path], compiler: st
         _, rc, out = _compile(cmd)
         if rc != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{out}")
+    _check_loadable(lib)
     return lib
+
+
+def _check_loadable(lib: Path) -> None:
+    """dlopen the fresh library with every symbol resolved: a kernel template whose host stub was
+    silently dropped links fine but fails here (and would fail on the GPU box)."""
+    import ctypes
+
+    try:
+        ctypes.CDLL(str(lib), mode=os.RTLD_NOW | os.RTLD_LOCAL)
+    except OSError as e:
+        raise RuntimeError(f"{lib.name} does not load: {e}") from e
 
 
 def build(force: bool = False, jobs: int | None = None, verbose: bool = True,

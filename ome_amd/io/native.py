@@ -46,6 +46,11 @@ def load():
         "omeio_load_ranges": ([ctypes.c_char_p, ctypes.c_int, u64p, u64p, vpp, ctypes.c_void_p, ctypes.c_int,
                                ctypes.c_uint64], ctypes.c_int),
         "omeio_read_ranges": ([ctypes.c_char_p, ctypes.c_int, u64p, u64p, vpp, ctypes.c_int], ctypes.c_int),
+        "omeio_load_strided": ([ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64], ctypes.c_int),
+        "omeio_read_strided": ([ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                ctypes.c_void_p], ctypes.c_int),
+        "omeio_bytes_read": ([], ctypes.c_uint64),
         "omeio_copy_file": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p], ctypes.c_int),
         "omeio_md5_file": ([ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
         "omeio_aes_gcm_encrypt_file": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
@@ -147,31 +152,106 @@ def aes_gcm_decrypt(blob: bytes, key: bytes) -> bytes:
     return out.raw[:n.value]
 
 
-def iter_tensors_to_device(files, device):
-    """Stream every tensor of ``files`` straight into HBM through the native loader."""
+def bytes_read() -> int:
+    """Bytes this process has pread through libomeio (loader statistics)."""
+    return int(load().omeio_bytes_read())
+
+
+def shard_ranges(shape, itemsize: int, spec):
+    """Byte geometry of a tensor shard inside its tensor's data block.
+
+    ``spec`` None -> the whole tensor; ("rows", start, n) -> rows [start, start+n) of dim 0 (one
+    contiguous range); ("cols", start, n) -> columns [start, start+n) of a 2-D tensor (one
+    strided slice per row).  Returns (shard shape, kind, offset, nrows, row_bytes, stride)."""
+    shape = list(shape)
+    if spec is None:
+        n = itemsize
+        for d in shape:
+            n *= d
+        return shape, "flat", 0, 1, n, n
+    kind, start, cnt = spec
+    inner = itemsize
+    for d in shape[1:]:
+        inner *= d
+    if kind == "rows":
+        return [cnt] + shape[1:], "flat", start * inner, 1, cnt * inner, cnt * inner
+    if kind == "cols":
+        if len(shape) != 2:
+            raise OmeIOError(f"column shard of a {len(shape)}-D tensor")
+        return [shape[0], cnt], "strided", start * itemsize, shape[0], cnt * itemsize, shape[1] * itemsize
+    raise OmeIOError(f"unknown shard kind {kind}")
+
+
+def iter_tensors_to_device(files, device, plan=None):
+    """Stream every tensor of ``files`` straight into HBM through the native loader.
+
+    ``plan(name, shape) -> None | ("rows"|"cols", start, n)``: a tensor-parallel rank's shard of
+    the tensor; only those bytes are read from disk and uploaded (no full-tensor transient)."""
     import torch
 
     from ome_amd.io.safetensors import DTYPES, read_header
 
     dev = torch.device(device)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    lib = load()
     for f in files:
         hdr, data_off = read_header(f)
         items = [(k, v) for k, v in hdr.items() if k != "__metadata__"]
-        tensors, offs, sizes, ptrs = [], [], [], []
+        tensors, offs, sizes, ptrs, strided = [], [], [], [], []
         for name, meta in items:
-            t = torch.empty(meta["shape"], dtype=DTYPES[meta["dtype"]], device=dev)
+            dt = DTYPES[meta["dtype"]]
+            itemsize = torch.empty(0, dtype=dt).element_size()
             b, e = meta["data_offsets"]
-            if e - b != t.numel() * t.element_size():
+            full = 1
+            for d in meta["shape"]:
+                full *= d
+            if e - b != full * itemsize:
                 raise OmeIOError(f"{f}:{name}: byte range {e - b} != shape/dtype size")
+            spec = plan(name, tuple(meta["shape"])) if plan is not None else None
+            shp, kind, off, nrows, row_bytes, stride = shard_ranges(meta["shape"], itemsize, spec)
+            t = torch.empty(shp, dtype=dt, device=dev)
             tensors.append((name, t))
-            if e > b:
-                offs.append(data_off + b)
-                sizes.append(e - b)
+            if t.numel() == 0:
+                continue
+            if kind == "flat":
+                offs.append(data_off + b + off)
+                sizes.append(row_bytes)
                 ptrs.append(t.data_ptr())
+            else:
+                strided.append((data_off + b + off, nrows, stride, row_bytes, t.data_ptr()))
         if offs:
             load_ranges(f, offs, sizes, ptrs, stream=stream, threads=min(16, max(2, len(offs))))
+        for fo, nrows, stride, row_bytes, p in strided:
+            _check(lib.omeio_load_strided(str(f).encode(), fo, nrows, stride, row_bytes, ctypes.c_void_p(p),
+                                          ctypes.c_void_p(stream), 8, 16 << 20))
         yield from tensors
+
+
+def iter_tensors_host(files, plan=None):
+    """CPU form of :func:`iter_tensors_to_device` (the same shard geometry, into host memory)."""
+    import torch
+
+    from ome_amd.io.safetensors import DTYPES, read_header
+
+    lib = load()
+    for f in files:
+        hdr, data_off = read_header(f)
+        for name, meta in hdr.items():
+            if name == "__metadata__":
+                continue
+            dt = DTYPES[meta["dtype"]]
+            itemsize = torch.empty(0, dtype=dt).element_size()
+            b, _ = meta["data_offsets"]
+            spec = plan(name, tuple(meta["shape"])) if plan is not None else None
+            shp, kind, off, nrows, row_bytes, stride = shard_ranges(meta["shape"], itemsize, spec)
+            t = torch.empty(shp, dtype=dt)
+            if t.numel():
+                if kind == "flat":
+                    read_ranges(f, [data_off + b + off], [row_bytes], [t.data_ptr()], threads=1)
+                else:
+                    _check(lib.omeio_read_strided(str(f).encode(), data_off + b + off, nrows, stride, row_bytes,
+                                                  ctypes.c_void_p(t.data_ptr())))
+            yield name, t
 
 
 def xet_decode(data: bytes) -> tuple[bytes, list[int]]:

@@ -184,7 +184,10 @@ def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: i
     elif fmt == "safetensors":
         from ome_amd.models.loader import iter_safetensors
 
-        m.load_hf_weights(iter_safetensors(model_path, device=device))
+        plan = m.shard_plan if hasattr(m, "sharded") and m.sharded() else None
+        if plan is not None:
+            m._presliced = True   # every tensor arrives as this rank's shard
+        m.load_hf_weights(iter_safetensors(model_path, device=device, plan=plan))
     else:
         raise ValueError(f"unknown load_format {load_format}")
     return m

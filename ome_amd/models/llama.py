@@ -146,14 +146,56 @@ class LlamaForCausalLM:
             logging.getLogger("ome_amd.models").warning("fp8: %d projections keep bf16 (shape not 64x128-tileable)",
                                                         kept)
 
+    # ------------------------------------------------------------------ rank-aware loading
+    _presliced = False   # set by build_model when the loader already applied shard_plan
+
+    def sharded(self) -> bool:
+        """Whether this rank reads only its shard of the checkpoint (dense Llama family under
+        TP / PP; fp8 checkpoints keep whole-tensor reads: their scales follow the block grid)."""
+        st = pstate.get()
+        return type(self) is LlamaForCausalLM and not self.fp8 and (self.tp.tp > 1 or st.pp_size > 1)
+
+    def shard_plan(self, name: str, shape) -> tuple[str, int, int] | None:
+        """This rank's slice of checkpoint tensor ``name`` (full ``shape``), mirroring
+        :meth:`load_hf_weights`: column-parallel q/k/v/gate/up and the vocab-parallel embedding
+        / LM head by rows, row-parallel o/down by columns; other pipeline stages' layers are not
+        read at all (("rows", 0, 0))."""
+        tp, D = self.tp, self.D
+        n = name[len("model."):] if name.startswith("model.") else name
+        if n in ("embed_tokens.weight", "lm_head.weight"):
+            return "rows", tp.vocab_start, max(0, min(tp.vocab, shape[0] - tp.vocab_start))
+        parts = n.split(".")
+        if parts[0] != "layers" or len(parts) < 3:
+            return None
+        if int(parts[1]) not in self._layer_set:
+            return "rows", 0, 0
+        rest = ".".join(parts[2:])
+        if rest in ("self_attn.q_proj.weight", "self_attn.q_proj.bias"):
+            return "rows", tp.rank * tp.hq * D, tp.hq * D
+        if rest in ("self_attn.k_proj.weight", "self_attn.k_proj.bias", "self_attn.v_proj.weight",
+                    "self_attn.v_proj.bias"):
+            return "rows", tp.kv_start * D, tp.hkv * D
+        if rest == "self_attn.o_proj.weight":
+            return "cols", tp.rank * tp.hq * D, tp.hq * D
+        if rest in ("mlp.gate_proj.weight", "mlp.up_proj.weight"):
+            return "rows", tp.rank * tp.inter, max(0, min(tp.inter, shape[0] - tp.rank * tp.inter))
+        if rest == "mlp.down_proj.weight":
+            return "cols", tp.rank * tp.inter, max(0, min(tp.inter, shape[1] - tp.rank * tp.inter))
+        return None
+
     def load_hf_weights(self, weights) -> "LlamaForCausalLM":
-        """Load from an iterator of (hf_name, tensor) — shards / fuses for this TP rank."""
+        """Load from an iterator of (hf_name, tensor) — shards / fuses for this TP rank (tensors
+        arrive already sliced when the loader applied :meth:`shard_plan`)."""
         cfg, tp, D = self.cfg, self.tp, self.D
         qkv_parts: dict[int, dict[str, torch.Tensor]] = {}
         gu_parts: dict[int, dict[str, torch.Tensor]] = {}
+        pre = self._presliced
 
         def rows(t, start, n):
-            return t.narrow(0, start, n)
+            return t if pre else t.narrow(0, start, n)
+
+        def cols(t, start, n):
+            return t if pre else t.narrow(1, start, n)
 
         def put(t):
             return t.to(device=self.device, dtype=self.dtype).contiguous()
@@ -185,13 +227,13 @@ class LlamaForCausalLM:
             elif rest in ("self_attn.v_proj.weight", "self_attn.v_proj.bias"):
                 qkv_parts.setdefault(i, {})["v" + rest[-1]] = rows(w, tp.kv_start * D, tp.hkv * D)
             elif rest == "self_attn.o_proj.weight":
-                self.w_o[i] = put(w.narrow(1, tp.rank * tp.hq * D, tp.hq * D))
+                self.w_o[i] = put(cols(w, tp.rank * tp.hq * D, tp.hq * D))
             elif rest == "mlp.gate_proj.weight":
                 gu_parts.setdefault(i, {})["g"] = rows(w, tp.rank * tp.inter, min(tp.inter, w.shape[0] - tp.rank * tp.inter))
             elif rest == "mlp.up_proj.weight":
                 gu_parts.setdefault(i, {})["u"] = rows(w, tp.rank * tp.inter, min(tp.inter, w.shape[0] - tp.rank * tp.inter))
             elif rest == "mlp.down_proj.weight":
-                self.w_d[i] = put(w.narrow(1, tp.rank * tp.inter, min(tp.inter, w.shape[1] - tp.rank * tp.inter)))
+                self.w_d[i] = put(cols(w, tp.rank * tp.inter, min(tp.inter, w.shape[1] - tp.rank * tp.inter)))
             elif rest == "input_layernorm.weight":
                 self.ln1[i] = put(w)
             elif rest == "post_attention_layernorm.weight":
@@ -222,7 +264,7 @@ class LlamaForCausalLM:
 
     def _vocab_shard(self, w: torch.Tensor) -> torch.Tensor:
         tp = self.tp
-        sh = w[tp.vocab_start:tp.vocab_end]
+        sh = w if self._presliced else w[tp.vocab_start:tp.vocab_end]
         if sh.shape[0] < tp.vocab:
             sh = torch.cat([sh, sh.new_zeros(tp.vocab - sh.shape[0], sh.shape[1])], 0)
         return sh

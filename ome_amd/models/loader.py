@@ -23,18 +23,25 @@ def shard_files(model_path: str | Path) -> list[Path]:
     return sorted(p.glob("*.safetensors"))
 
 
-def iter_safetensors(model_path: str | Path, device="cpu") -> Iterator[tuple[str, torch.Tensor]]:
+def iter_safetensors(model_path: str | Path, device="cpu", plan=None) -> Iterator[tuple[str, torch.Tensor]]:
+    """``plan(name, shape) -> None | ("rows"|"cols", start, n)``: read only this tensor-parallel
+    rank's shard of each tensor (``LlamaForCausalLM.shard_plan``); None = whole tensors."""
     files = shard_files(model_path)
     if not files:
         raise FileNotFoundError(f"no safetensors shards under {model_path}")
     try:
         from ome_amd.io import native as nio
 
-        if nio.available() and torch.device(device).type == "cuda":
-            yield from nio.iter_tensors_to_device(files, device)
+        if nio.available():
+            if torch.device(device).type == "cuda":
+                yield from nio.iter_tensors_to_device(files, device, plan)
+            else:
+                yield from nio.iter_tensors_host(files, plan)
             return
     except ImportError:
         pass
+    if plan is not None:
+        raise RuntimeError("sharded checkpoint loading needs libomeio (python -m ome_amd.build)")
     from safetensors import safe_open
 
     for f in files:

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Native loader throughput (libomeio: pread -> pinned staging -> hipMemcpyAsync into HBM).
+
+Writes a synthetic Llama-3-70B-shaped checkpoint slice (``--layers`` decoder layers, bf16), evicts
+it from the page cache (POSIX_FADV_DONTNEED; cold reads come from disk), then loads it
+(1) whole, as TP=1 does, and (2) as every rank of TP=--tp with the rank-aware shard plan, and
+prints GB/s of bytes read and the bytes each TP rank read relative to the whole checkpoint."""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ome_amd.io import native as nio  # noqa: E402
+from ome_amd.io.safetensors import save_file  # noqa: E402
+from ome_amd.models import build_model  # noqa: E402
+from ome_amd.models.config import PRESETS, ModelConfig  # noqa: E402
+from ome_amd.parallel import state as pstate  # noqa: E402
+
+
+def evict(path):
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+        os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+    finally:
+        os.close(fd)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--tp", type=int, default=8)
+    ap.add_argument("--dir", default=None)
+    a = ap.parse_args()
+    hf = dict(PRESETS["llama-3-70b"])
+    hf["num_hidden_layers"] = a.layers
+    cfg = ModelConfig.from_hf(hf)
+    d = a.dir or tempfile.mkdtemp(prefix="ome_loader_")
+    H, D, I, V = cfg.hidden_size, cfg.head_dim, cfg.intermediate_size, cfg.vocab_size
+    t0 = time.time()
+    shards = []
+    w = {"model.embed_tokens.weight": torch.empty(V, H, dtype=torch.bfloat16),
+         "model.norm.weight": torch.ones(H, dtype=torch.bfloat16),
+         "lm_head.weight": torch.empty(V, H, dtype=torch.bfloat16)}
+    save_file(w, os.path.join(d, "model-00000.safetensors"))
+    shards.append(os.path.join(d, "model-00000.safetensors"))
+    for i in range(cfg.num_layers):
+        p = f"model.layers.{i}."
+        w = {p + "self_attn.q_proj.weight": torch.empty(cfg.num_heads * D, H, dtype=torch.bfloat16),
+             p + "self_attn.k_proj.weight": torch.empty(cfg.num_kv_heads * D, H, dtype=torch.bfloat16),
+             p + "self_attn.v_proj.weight": torch.empty(cfg.num_kv_heads * D, H, dtype=torch.bfloat16),
+             p + "self_attn.o_proj.weight": torch.empty(H, cfg.num_heads * D, dtype=torch.bfloat16),
+             p + "mlp.gate_proj.weight": torch.empty(I, H, dtype=torch.bfloat16),
+             p + "mlp.up_proj.weight": torch.empty(I, H, dtype=torch.bfloat16),
+             p + "mlp.down_proj.weight": torch.empty(H, I, dtype=torch.bfloat16),
+             p + "input_layernorm.weight": torch.ones(H, dtype=torch.bfloat16),
+             p + "post_attention_layernorm.weight": torch.ones(H, dtype=torch.bfloat16)}
+        f = os.path.join(d, f"model-{i + 1:05d}.safetensors")
+        save_file(w, f)
+        shards.append(f)
+    (open(os.path.join(d, "config.json"), "w")).write(json.dumps(hf))
+    total = sum(os.path.getsize(f) for f in shards)
+    print(f"# wrote {total / 1e9:.2f} GB ({a.layers} layers of Llama-3-70B) in {time.time() - t0:.1f}s", flush=True)
+    res = {"checkpoint_gb": round(total / 1e9, 3), "layers": a.layers}
+    for tp in (1, a.tp):
+        per = []
+        for r in range(tp):
+            for f in shards:
+                evict(f)
+            pstate.set_state(pstate.ParallelState(tp_size=tp, tp_rank=r, world_size=tp, rank=r))
+            b0 = nio.bytes_read()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            m = build_model(cfg, "cuda", torch.bfloat16, model_path=d, load_format="safetensors")
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t
+            nb = nio.bytes_read() - b0
+            per.append((dt, nb))
+            del m
+            torch.cuda.empty_cache()
+            if tp > 1 and r >= 1:
+                break   # ranks are symmetric; two cold loads are enough
+        dt = sum(x[0] for x in per) / len(per)
+        nb = sum(x[1] for x in per) / len(per)
+        print(f"tp={tp}: {nb / 1e9:.2f} GB read per rank ({100 * nb / total:.1f}% of checkpoint) in {dt:.2f}s = "
+              f"{nb / dt / 1e9:.2f} GB/s", flush=True)
+        res[f"tp{tp}"] = {"bytes_per_rank": int(nb), "fraction": round(nb / total, 4), "seconds": round(dt, 3),
+                          "GBps": round(nb / dt / 1e9, 2)}
+    pstate.set_state(pstate.ParallelState())
+    print(json.dumps(res))
+    if not a.dir:
+        for f in shards:
+            os.unlink(f)
+
+
+if __name__ == "__main__":
+    main()
