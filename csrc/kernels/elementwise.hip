@@ -12,14 +12,18 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 
 template <int ACT>
 __global__ __launch_bounds__(256) void act_and_mul_kernel(const bf16* __restrict__ x, bf16* __restrict__ out,
-                                                          int64_t rows, int I) {
-  // grid (column blocks, rows): no per-element 64-bit division, every lane one 16-B vector
+                                                          int64_t rows, int I, bool il) {
+  // grid (column blocks, rows): no per-element 64-bit division, every lane one 16-B vector.
+  // il: gate / up columns interleaved in 16-column blocks (the layout of a gate_up weight
+  // interleaved for the fused SiLU*mul GEMM epilogue, ops.interleave_gate_up)
   const int nv = I >> 3;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t r = blockIdx.y;
   if (c >= nv) return;
   const bf16* xr = x + r * 2 * I;
-  bf16x8 g = ld8(xr + c * 8), u = ld8(xr + I + c * 8), o;
+  const int gcol = il ? ((c * 8) >> 4) * 32 + ((c * 8) & 15) : c * 8;
+  const int ucol = il ? gcol + 16 : I + c * 8;
+  bf16x8 g = ld8(xr + gcol), u = ld8(xr + ucol), o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float gf = (float)g[j];
@@ -62,20 +66,23 @@ static inline int grid_for(int64_t work, int nt) {
   return (int)g;
 }
 
+// act: 0 SiLU, 1 GELU-tanh, 2 GPT-OSS clamped SwiGLU; | 16: interleaved gate/up (16-col blocks)
 OME_API int ome_act_and_mul(const void* x, void* out, int64_t rows, int I, int act, hipStream_t stream) {
   if (rows <= 0) return 0;
-  if (I % 8) return -2;
+  const bool il = (act & 16) != 0;
+  act &= 15;
+  if (I % 8 || (il && I % 16)) return -2;
   for (int64_t r0 = 0; r0 < rows; r0 += 65535) {  // grid.y limit
     const int64_t n = rows - r0 < 65535 ? rows - r0 : 65535;
     const dim3 g((I / 8 + 255) / 256, (unsigned)n);
     const bf16* xp = (const bf16*)x + r0 * 2 * I;
     bf16* op = (bf16*)out + r0 * I;
     if (act == 0)
-      act_and_mul_kernel<0><<<g, 256, 0, stream>>>(xp, op, n, I);
+      act_and_mul_kernel<0><<<g, 256, 0, stream>>>(xp, op, n, I, il);
     else if (act == 1)
-      act_and_mul_kernel<1><<<g, 256, 0, stream>>>(xp, op, n, I);
+      act_and_mul_kernel<1><<<g, 256, 0, stream>>>(xp, op, n, I, il);
     else
-      act_and_mul_kernel<2><<<g, 256, 0, stream>>>(xp, op, n, I);
+      act_and_mul_kernel<2><<<g, 256, 0, stream>>>(xp, op, n, I, il);
   }
   OME_CHECK_LAUNCH();
   return 0;

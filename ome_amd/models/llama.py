@@ -128,9 +128,19 @@ class LlamaForCausalLM:
         return isinstance(w, torch.Tensor) and w.dim() == 2 and w.numel() > 0 and w.shape[0] % 64 == 0 and \
             w.shape[1] % 128 == 0
 
+    gu_il = False   # gate_up rows interleaved in 16-row blocks (fused SiLU*mul GEMM epilogue)
+
     def _post_load(self) -> None:
         """``quantization: fp8``: the QKV / O / gate-up / down projections become W8A8 (the
-        embedding, LM head and norms stay bf16, as in the reference runtimes)."""
+        embedding, LM head and norms stay bf16, as in the reference runtimes).  bf16 SwiGLU on a
+        GPU: gate_up weights are interleaved in 16-row blocks so the stream-K GEMM can apply
+        SiLU(gate) * up in its epilogue (no act_and_mul pass, no [T, 2I] intermediate)."""
+        if not self.fp8 and type(self) is LlamaForCausalLM and self.act == 0 and self.device.type == "cuda" and \
+                self.dtype == torch.bfloat16 and os.environ.get("OME_GATE_UP_INTERLEAVE", "1") == "1" and \
+                all(isinstance(self.w_gu[i], torch.Tensor) and self.w_gu[i].shape[0] % 32 == 0 for i in self.layers):
+            for i in self.layers:
+                self.w_gu[i] = ops.interleave_gate_up(self.w_gu[i])
+            self.gu_il = True
         if not self.fp8:
             return
         kept = 0
@@ -262,6 +272,15 @@ class LlamaForCausalLM:
         self._post_load()
         return self
 
+    def gate_up_weight(self, i: int) -> torch.Tensor:
+        """Layer i's gate_up weight in checkpoint order ([gate; up] rows), whatever the layout
+        the kernels use."""
+        w = self.w_gu[i]
+        if not self.gu_il:
+            return w
+        g, u = ops.deinterleave_gate_up(w.t())
+        return torch.cat([g.t(), u.t()], 0)
+
     def _vocab_shard(self, w: torch.Tensor) -> torch.Tensor:
         tp = self.tp
         sh = w if self._presliced else w[tp.vocab_start:tp.vocab_end]
@@ -305,8 +324,16 @@ class LlamaForCausalLM:
     def _mlp_partial(self, i: int, x: torch.Tensor) -> torch.Tensor:
         """gate_up -> SiLU*mul -> down: this rank's partial sums (before the TP all-reduce),
         written straight into the all-reduce's staging buffer when there is one."""
-        gu = linear(x, self.w_gu[i])
         wd = self.w_d[i]
+        if self.gu_il:
+            w = self.w_gu[i]
+            plan = ops.gemm_sk_plan(x.shape[0], w.shape[0], w.shape[1], 2) if x.shape[0] > _GEMV_ROWS else None
+            if plan is not None and x.stride(1) == 1 and x.stride(0) % 8 == 0:
+                a = ops.gemm_sk(x, w, epi=2, bn=plan[0], nwg=plan[1])
+            else:
+                a = ops.act_and_mul(linear(x, w), self.act, interleaved=True)
+            return self._row_parallel(a, wd)
+        gu = linear(x, self.w_gu[i])
         if _GEMV_ACT and self.act == 0 and gu.is_cuda and type(wd) is torch.Tensor and gu.dim() == 2 and \
                 gu.shape[0] <= _GEMV_ROWS and gu.dtype == wd.dtype == torch.bfloat16 and gu.stride(1) == 1 and \
                 gu.stride(0) % 8 == 0 and gu.data_ptr() % 16 == 0 and wd.data_ptr() % 16 == 0:

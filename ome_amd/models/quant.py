@@ -125,11 +125,24 @@ def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
 _GEMV_ROWS = int(os.environ.get("OME_GEMV_ROWS", "4"))
 
 
+def _sk_operands_ok(x, w, bias, out) -> bool:
+    return (x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.is_contiguous()
+            and w.data_ptr() % 16 == 0 and (bias is None or bias.dtype == torch.bfloat16)
+            and (out is None or (out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0)))
+
+
 def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Dispatch: plain tensor -> hipBLASLt GEMM; single-row decode -> the GEMV stream kernel
+    """Dispatch: bf16 weight at a row count where the stream-K MFMA kernel was measured faster
+    (``ops.gemm_sk_plan``) -> ``ops.gemm_sk``; single-row decode -> the GEMV stream kernel
     (``ops.gemv``, ``OME_GEMV_ROWS``); the weight-streaming MFMA GEMM for decode shapes where it
-    was measured faster (``ops.decode_gemm_plan``, opt-in); Fp8Weight -> W8A8 MFMA path.
-    ``out``: write the result there (e.g. the TP all-reduce's IPC staging buffer)."""
+    was measured faster (``ops.decode_gemm_plan``, opt-in); other plain tensors -> hipBLASLt;
+    Fp8Weight -> W8A8 MFMA path.  ``out``: write the result there (e.g. the TP all-reduce's IPC
+    staging buffer)."""
+    if (x.dim() == 2 and x.is_cuda and x.shape[0] > _GEMV_ROWS and type(w) is torch.Tensor
+            and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
+        plan = ops.gemm_sk_plan(x.shape[0], w.shape[0], w.shape[1], 0)
+        if plan is not None and _sk_operands_ok(x, w, bias, out):
+            return ops.gemm_sk(x, w, bias, out=out, bn=plan[0], nwg=plan[1])
     if out is not None:
         if x.is_cuda and x.shape[0] <= _GEMV_ROWS and ops.gemv_ok(x, w, bias, out):
             return ops.gemv(x, w, bias, out=out)

@@ -185,14 +185,19 @@ def kv_cache_write(k, v, k_cache, v_cache, slots, k_scale: float = 1.0, v_scale:
          _i32(slots).data_ptr(), T, Hkv, D, P, kv_format(k_cache), float(k_scale), float(v_scale), stream_ptr())
 
 
-def act_and_mul(x: torch.Tensor, act: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
-    """act 0 = SiLU (SwiGLU), 1 = GELU-tanh (GeGLU).  x [.., 2I] -> [.., I]."""
+def act_and_mul(x: torch.Tensor, act: int = 0, out: torch.Tensor | None = None,
+                interleaved: bool = False) -> torch.Tensor:
+    """act 0 = SiLU (SwiGLU), 1 = GELU-tanh (GeGLU).  x [.., 2I] -> [.., I].  ``interleaved``:
+    gate / up columns alternate in 16-column blocks (:func:`interleave_gate_up` weights)."""
     if not _gpu(x):
+        if interleaved:
+            g, u = deinterleave_gate_up(x.reshape(-1, x.shape[-1]))
+            x = torch.cat([g, u], -1).view(*x.shape)
         return ref.act_and_mul(x, act)
     I = x.shape[-1] // 2
     rows = x.numel() // x.shape[-1]
     out = torch.empty(*x.shape[:-1], I, dtype=x.dtype, device=x.device) if out is None else out
-    call("ome_act_and_mul", x.data_ptr(), out.data_ptr(), rows, I, act, stream_ptr())
+    call("ome_act_and_mul", x.data_ptr(), out.data_ptr(), rows, I, act | (16 if interleaved else 0), stream_ptr())
     return out
 
 
@@ -873,6 +878,44 @@ def gemm_sk_ok(M: int, N: int, K: int, bn: int, nwg: int) -> bool:
     if bn not in (128, 256) or N % bn or K % 64 or K <= 0 or nwg % 8 or not 8 <= nwg <= _SK_MAX_WG or M <= 0:
         return False
     return gemm_sk_tiles(M, N, bn) <= _SK_CNT
+
+
+_SK_TABLE: dict | None = None
+_SK_MODE = os.environ.get("OME_GEMM_SK", "table")   # table | 0 (hipBLASLt only)
+_SK_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_tuned",
+                              "gemm_sk_gfx950.json")
+
+
+def _sk_table() -> dict:
+    global _SK_TABLE
+    if _SK_TABLE is None:
+        import json
+
+        try:
+            with open(os.environ.get("OME_GEMM_SK_TABLE", _SK_TABLE_PATH)) as f:
+                raw = json.load(f)
+            _SK_TABLE = {k: sorted((int(m), v) for m, v in d.items()) for k, d in raw.get("shapes", {}).items()}
+        except (OSError, ValueError):
+            _SK_TABLE = {}
+    return _SK_TABLE
+
+
+def gemm_sk_plan(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:
+    """(bn, nwg) when the stream-K kernel was measured faster than hipBLASLt (gate_up: than
+    hipBLASLt + act_and_mul) for this weight shape at the nearest measured row count, else None.
+    Table: ``ome_amd/_tuned/gemm_sk_gfx950.json`` written by ``scripts/gemm_sk_bench.py --table``
+    (cold weights, interleaved same-box timings)."""
+    if _SK_MODE == "0":
+        return None
+    rows = _sk_table().get(f"{N},{K},{epi}")
+    if not rows:
+        return None
+    m_near, e = min(rows, key=lambda r: abs(r[0] - M) / max(r[0], M))
+    if max(m_near, M) > 1.34 * min(m_near, M):   # nothing measured close to this M
+        return None
+    if e["us"] >= 0.97 * e["lib_us"] or not gemm_sk_ok(M, N, K, e["bn"], e["nwg"]):
+        return None
+    return e["bn"], e["nwg"]
 
 
 def gemm_sk(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, out: torch.Tensor | None = None,

@@ -5,7 +5,8 @@ Cold weights: every call uses the next of several weight copies (> 256 MiB Infin
 total), as in a layer stack; activations stay warm.  gate_up is timed as the serving path runs
 it: hipBLASLt GEMM + act_and_mul against the fused SiLU*mul epilogue (interleaved weight).
 Every stream-K configuration is checked against an fp32 reference before it is timed.
-Prints one line per (shape, M) and, with --json PATH, the best configuration per (shape, M).
+Prints one line per (shape, M); --json PATH writes the best configuration per (shape, M), and
+--table PATH the planner table of ``ops.gemm_sk_plan`` (``ome_amd/_tuned/gemm_sk_gfx950.json``).
 """
 import argparse
 import json
@@ -46,13 +47,14 @@ def nwg_cands(M, N, K, bn):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--m", default="256,512,768,1024,1280,1536,2048,2304")
+    ap.add_argument("--m", default="128,192,256,384,512,768,1024,1280,1536,1792,2048,2304")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--json", default=None)
+    ap.add_argument("--table", default=None, help="write the ops.gemm_sk_plan table here")
     ap.add_argument("--iters", type=int, default=30)
     a = ap.parse_args()
     ms = [int(v) for v in a.m.split(",")]
-    table = {}
+    table, plan = {}, {}
     for name in a.shapes.split(","):
         N, K = SHAPES[name]
         epi = 2 if name == "gate_up" else 0
@@ -67,8 +69,8 @@ def main():
             if epi == 2:
                 ref = F.silu(ref[:, :N // 2]) * ref[:, N // 2:]
             fl = 2 * M * N * K
-            if epi == 2:
-                t_lib = bench(lambda i: ops.act_and_mul(F.linear(x, ws[i])), n_w, a.iters)
+            if epi == 2:   # the serving fallback: hipBLASLt on the interleaved weight + interleaved act
+                t_lib = bench(lambda i: ops.act_and_mul(F.linear(x, wi[i]), interleaved=True), n_w, a.iters)
             else:
                 t_lib = bench(lambda i: F.linear(x, ws[i]), n_w, a.iters)
             row = [f"M={M:5d} {name:8s} hipblaslt{'+act' if epi else ''} {t_lib:7.1f}us {fl / t_lib / 1e6:5.0f}TF"]
@@ -92,12 +94,17 @@ def main():
                 row.append(f"BEST {best[0]:6.1f}us {fl / best[0] / 1e6:5.0f}TF x{t_lib / best[0]:.2f}")
                 table.setdefault(name, {})[str(M)] = {"bn": best[1], "nwg": best[2], "us": round(best[0], 1),
                                                       "lib_us": round(t_lib, 1)}
+                plan.setdefault(f"{N},{K},{epi}", {})[str(M)] = table[name][str(M)]
             print("  ".join(row), flush=True)
         del ws, wi
         torch.cuda.empty_cache()
     if a.json:
         with open(a.json, "w") as f:
             json.dump(table, f, indent=1)
+    if a.table:
+        with open(a.table, "w") as f:
+            json.dump({"device": torch.cuda.get_device_name(), "method": "scripts/gemm_sk_bench.py, cold weights",
+                       "shapes": plan}, f, indent=1)
 
 
 if __name__ == "__main__":

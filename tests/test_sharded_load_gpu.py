@@ -33,7 +33,7 @@ def test_gpu_shards_match_cpu(tmp_path, tp, rank):
         pstate.set_state(prev)
     assert gpu._presliced
     for i in range(cfg.num_layers):
-        for a, b in ((cpu.w_qkv[i], gpu.w_qkv[i]), (cpu.w_o[i], gpu.w_o[i]), (cpu.w_gu[i], gpu.w_gu[i]),
+        for a, b in ((cpu.w_qkv[i], gpu.w_qkv[i]), (cpu.w_o[i], gpu.w_o[i]), (cpu.w_gu[i], gpu.gate_up_weight(i)),
                      (cpu.w_d[i], gpu.w_d[i])):
             assert torch.equal(a, b.cpu())
     assert torch.equal(cpu.embed, gpu.embed.cpu()) and torch.equal(cpu.lm_head, gpu.lm_head.cpu())
