@@ -11,6 +11,7 @@ import logging
 import os
 import signal
 import threading
+import time
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 from ome_amd.api import constants as C
@@ -34,6 +35,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--kubeconfig", default=None)
     ap.add_argument("--in-cluster", action="store_true")
     ap.add_argument("--namespace", default=C.OME_NAMESPACE, help="namespace of the per-node ConfigMaps")
+    ap.add_argument("--startup-jitter", type=float, default=30.0,
+                    help="spread agent start-up over [0, N) s by a hash of the node name (0 disables)")
     return ap
 
 
@@ -61,6 +64,19 @@ def make_handler(agent):
     return H
 
 
+def startup_jitter_s(node_name: str, span: float = 30.0) -> float:
+    """Deterministic per-node start-up delay (reference cmd/model-agent/main.go:229-239: hash =
+    hash*31 + c over the node name, delay = hash % 30 s) so a fleet of agents starting together
+    does not hit the HF API at the same moment (429 storms)."""
+    if span <= 0 or not node_name:
+        return 0.0
+    h = 0
+    for c in node_name:   # Go int64 arithmetic: wraps on overflow
+        h = ((h * 31 + ord(c) + (1 << 63)) % (1 << 64)) - (1 << 63)
+    r = abs(h) % int(span) * (1 if h >= 0 else -1)   # Go's % truncates toward zero
+    return float(max(0, r))                           # a negative delay sleeps for no time in Go
+
+
 def main(argv=None) -> int:
     args = build_parser().parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(levelname)s %(message)s")
@@ -71,6 +87,10 @@ def main(argv=None) -> int:
 
     client = kube.KubeClient.in_cluster() if args.in_cluster or not args.kubeconfig else \
         kube.KubeClient.from_kubeconfig(args.kubeconfig)
+    delay = startup_jitter_s(args.node_name, args.startup_jitter)
+    if delay:
+        log.info("start-up jitter %.0f s before initialising the hub clients (rate-limit protection)", delay)
+        time.sleep(delay)
     store = kube.KubeStore(client, AGENT_KINDS)
     agent = ModelAgent(store, args.node_name, args.models_root_dir, workers=args.num_download_worker,
                        download_retry=args.download_retry, heal_interval=args.configmap_heal_interval)

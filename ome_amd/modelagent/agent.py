@@ -324,8 +324,16 @@ class Gopher:
                 break
             except (backends.FetchError, StorageURIError, OSError) as e:
                 err = e
-                M.DOWNLOAD_FAILURES.labels(model=obj["metadata"]["name"]).inc()
-                log.warning("download %s attempt %d failed: %s", key, attempt + 1, e)
+                kind = getattr(e, "kind", "download_error")
+                waits = getattr(e, "rate_limit_waits", [])
+                if kind == "rate_limit_error" or "429" in str(e) or "rate limit" in str(e).lower():
+                    # reference gopher.go:1134-1137: count the 429 and the wait it imposed
+                    M.record_rate_limit(obj, sum(waits) if waits else 30.0)
+                    kind = "rate_limit_error"
+                if kind == "md5_mismatch":
+                    M.record_verification(obj, False)
+                M.record_failed(obj, kind)
+                log.warning("download %s attempt %d failed (%s): %s", key, attempt + 1, kind, e)
                 time.sleep(min(2.0, ag.retry_backoff * (2 ** attempt)))
         if res is None:
             ag.labeler.set(obj, STATUS_FAILED)
@@ -358,10 +366,14 @@ class Gopher:
         cfg["artifact"] = artifact
         ag.cm.set_entry(key, self._entry(obj, STATUS_READY, config=cfg))
         ag.labeler.set(obj, STATUS_READY)
-        M.DOWNLOADS.labels(model=obj["metadata"]["name"]).inc()
-        M.DOWNLOAD_SECONDS.observe(time.time() - t0)
+        M.record_success(obj)
+        M.observe_download(obj, time.time() - t0)
         if res.bytes:
-            M.DOWNLOAD_BYTES.inc(res.bytes)
+            M.record_bytes(obj, res.bytes)
+        for w in (res.extra or {}).get("rate_limit_waits") or []:   # 429s that a retry got past
+            M.record_rate_limit(obj, w)
+        if (res.extra or {}).get("verified"):
+            M.record_verification(obj, True)
 
     def _hf_token(self, obj: dict) -> str | None:
         st = (obj.get("spec") or {}).get("storage") or {}
@@ -407,7 +419,7 @@ class Gopher:
                     ag.cm.set_entry(pk, pe)
         ag.cm.delete_entry(key)
         ag.labeler.set(obj, None)
-        M.DELETES.labels(model=obj["metadata"]["name"]).inc()
+        M.record_delete(obj)
 
 
 class ModelAgent:

@@ -34,7 +34,13 @@ Progress = Callable[[dict], None]
 
 
 class FetchError(RuntimeError):
-    pass
+    """``kind``: the reference's failed-download error type (``rate_limit_error``,
+    ``hf_download_error``, ``md5_mismatch``, ...); ``rate_limit_waits``: seconds waited on 429s."""
+
+    def __init__(self, msg: str, kind: str = "download_error", rate_limit_waits: list[float] | None = None):
+        super().__init__(msg)
+        self.kind = kind
+        self.rate_limit_waits = list(rate_limit_waits or [])
 
 
 @dataclass
@@ -96,7 +102,7 @@ def _copy_tree(src: Path, dest: Path, progress: Progress | None, verify: dict | 
             want = verify[str(rel)]
             if want.get("md5") and _md5(out) != want["md5"]:
                 out.unlink(missing_ok=True)
-                raise FetchError(f"MD5 mismatch for {rel}")
+                raise FetchError(f"MD5 mismatch for {rel}", kind="md5_mismatch")
             if want.get("size") is not None and out.stat().st_size != int(want["size"]):
                 raise FetchError(f"size mismatch for {rel}")
         done_b += p.stat().st_size
@@ -159,13 +165,16 @@ def fetch_hf(uri: str, dest: str, progress: Progress | None = None, token: str |
                                          part_size=int(os.environ.get("OME_DOWNLOAD_PART_SIZE", 64 << 20)),
                                          progress=progress)
             return FetchResult(str(dest), sha=st["sha"], files=st["files"], bytes=st["bytes"],
-                               extra={k: st[k] for k in ("parts", "fetched_parts", "verified")})
+                               extra={k: st[k] for k in ("parts", "fetched_parts", "verified", "rate_limit_waits")})
+        except hfhub.O.RateLimitError as e:
+            raise FetchError(f"Hugging Face download of {repo}@{rev} rate limited: {e}", kind="rate_limit_error",
+                             rate_limit_waits=e.waits) from e
         except hfhub.HfHubError as e:
             if e.status in (401, 403, 404):
-                raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}") from e
-            raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}") from e
+                raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}", kind="hf_download_error") from e
+            raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}", kind="hf_download_error") from e
         except (hfhub.O.ObjectStoreError, OSError) as e:
-            raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}") from e
+            raise FetchError(f"Hugging Face download of {repo}@{rev} failed: {e}", kind="hf_download_error") from e
     try:
         from huggingface_hub import snapshot_download
     except ImportError as e:  # pragma: no cover

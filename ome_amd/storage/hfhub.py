@@ -156,4 +156,5 @@ def snapshot_download(repo: str, local_dir: str | Path, revision: str = "main", 
         stats["fetched_parts"] += r["fetched_parts"]
         stats["verified"] += int(bool(r["md5_verified"]))
     (local / ".ome-hf-commit").write_text(sha)
+    stats["rate_limit_waits"] = list(hub.http.rate_limit_waits)
     return stats

@@ -73,18 +73,52 @@ def _md5_of(etag_or_md5: str | None, b64: bool) -> str | None:
         return None
 
 
-class _Http:
-    """Tiny signed-request helper shared by the clients (retries 5xx / connection errors)."""
+class RateLimitError(ObjectStoreError):
+    """HTTP 429 after the rate-limit retry budget (``waits``: seconds slept on this request)."""
 
-    def __init__(self, creds: A.Credentials | None, retries: int = 3, timeout: float = 60.0):
+    def __init__(self, msg: str, waits: list[float]):
+        super().__init__(msg, 429)
+        self.waits = waits
+
+
+def retry_after_seconds(value: str | None, default: float) -> float:
+    """``Retry-After`` as seconds: delta-seconds or an HTTP-date (RFC 9110 §10.2.3)."""
+    if not value:
+        return default
+    value = value.strip()
+    try:
+        return max(0.0, float(value))
+    except ValueError:
+        pass
+    try:
+        import email.utils
+
+        when = email.utils.parsedate_to_datetime(value)
+        return max(0.0, when.timestamp() - time.time())
+    except (TypeError, ValueError, OverflowError):
+        return default
+
+
+class _Http:
+    """Tiny signed-request helper shared by the clients: retries 5xx / connection errors; HTTP 429
+    honours ``Retry-After`` (capped at ``max_wait`` s) for ``rate_limit_retries`` attempts and
+    records every wait in ``rate_limit_waits`` (the model agent turns them into
+    ``model_agent_rate_limit_*`` metrics; reference ``pkg/modelagent/gopher.go:1134-1136``)."""
+
+    def __init__(self, creds: A.Credentials | None, retries: int = 3, timeout: float = 60.0,
+                 rate_limit_retries: int = 5, max_wait: float = 60.0, default_wait: float = 5.0):
         self.creds, self.retries, self.timeout = creds, retries, timeout
+        self.rate_limit_retries, self.max_wait, self.default_wait = rate_limit_retries, max_wait, default_wait
         self.requests = 0
+        self.rate_limit_waits: list[float] = []
         self._lock = threading.Lock()
 
     def __call__(self, method: str, url: str, headers: dict | None = None, body: bytes = b"",
                  ok=(200, 201, 204, 206)) -> tuple[int, dict, bytes]:
         last = None
-        for attempt in range(self.retries):
+        waits: list[float] = []
+        attempt = 0
+        while attempt < self.retries:
             h = dict(headers or {})
             u = url
             if isinstance(self.creds, A.AzureSas):
@@ -102,12 +136,23 @@ class _Http:
                 data = e.read()
                 if e.code in ok:
                     return e.code, {k.lower(): v for k, v in e.headers.items()}, data
-                if e.code < 500 and e.code != 429:
+                if e.code == 429:
+                    if len(waits) >= self.rate_limit_retries:
+                        raise RateLimitError(f"{method} {url}: HTTP 429 after {len(waits)} rate-limit waits "
+                                             f"({sum(waits):.1f} s)", waits) from e
+                    w = min(self.max_wait, retry_after_seconds(e.headers.get("Retry-After"), self.default_wait))
+                    waits.append(w)
+                    with self._lock:
+                        self.rate_limit_waits.append(w)
+                    time.sleep(w)
+                    continue   # rate-limit waits do not use up the error retries
+                if e.code < 500:
                     raise ObjectStoreError(f"{method} {url}: HTTP {e.code} {data[:200]!r}", e.code) from e
                 last = ObjectStoreError(f"{method} {url}: HTTP {e.code}", e.code)
             except OSError as e:
                 last = ObjectStoreError(f"{method} {url}: {e}")
             time.sleep(min(2.0, 0.1 * 2 ** attempt))
+            attempt += 1
         raise last
 
 
