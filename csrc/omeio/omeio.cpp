@@ -16,6 +16,9 @@
 
 #include <hip/hip_runtime_api.h>
 #include <openssl/evp.h>
+#include <openssl/pem.h>
+#include <openssl/rsa.h>
+#include <openssl/x509.h>
 
 namespace {
 
@@ -426,4 +429,133 @@ OMEIO_API int omeio_aes_gcm_encrypt_file(const char* src, const char* dst, const
 
 OMEIO_API int omeio_aes_gcm_decrypt_file(const char* src, const char* dst, const uint8_t* key) {
   return gcm_file(src, dst, key, nullptr, false);
+}
+
+// ------------------------------------------------------------------------------------------
+// RSA PKCS#1 v1.5 / SHA-256 signatures for the cloud request signers (OCI API keys, GCP service
+// accounts) through OpenSSL: the private-key operation uses OpenSSL's blinded constant-time RSA
+// (CRT), and verification checks the complete DigestInfo encoding.  The key is a PEM (PKCS#1 or
+// PKCS#8 private key; for verification also a public key / SubjectPublicKeyInfo).
+// ------------------------------------------------------------------------------------------
+namespace {
+EVP_PKEY* pem_key(const char* pem, size_t n, bool want_private) {
+  BIO* b = BIO_new_mem_buf(pem, static_cast<int>(n));
+  if (!b) return nullptr;
+  EVP_PKEY* k = PEM_read_bio_PrivateKey(b, nullptr, nullptr, const_cast<char*>(""));
+  if (!k && !want_private) {
+    BIO_reset(b);
+    k = PEM_read_bio_PUBKEY(b, nullptr, nullptr, nullptr);
+  }
+  BIO_free(b);
+  if (k && EVP_PKEY_base_id(k) != EVP_PKEY_RSA) {
+    EVP_PKEY_free(k);
+    return nullptr;
+  }
+  return k;
+}
+}  // namespace
+
+// sig: capacity *sig_len bytes (>= the modulus size); *sig_len receives the signature length
+OMEIO_API int omeio_rsa_sign_sha256(const char* pem, size_t pem_len, const uint8_t* msg, size_t n, uint8_t* sig,
+                                    size_t* sig_len) {
+  EVP_PKEY* k = pem_key(pem, pem_len, true);
+  if (!k) return fail(-EINVAL, "not an RSA private key (or an encrypted one)");
+  EVP_MD_CTX* c = EVP_MD_CTX_new();
+  int rc = -EIO;
+  size_t need = 0;
+  if (c && EVP_DigestSignInit(c, nullptr, EVP_sha256(), nullptr, k) == 1 && EVP_DigestSignUpdate(c, msg, n) == 1 &&
+      EVP_DigestSignFinal(c, nullptr, &need) == 1) {
+    if (need > *sig_len) {
+      rc = fail(-ENOSPC, "signature buffer too small");
+    } else if (EVP_DigestSignFinal(c, sig, sig_len) == 1) {
+      rc = 0;
+    }
+  }
+  if (rc == -EIO) rc = fail(-EIO, "RSA signing failed");
+  EVP_MD_CTX_free(c);
+  EVP_PKEY_free(k);
+  return rc;
+}
+
+// 1 = valid, 0 = invalid signature, < 0 = bad key
+OMEIO_API int omeio_rsa_verify_sha256(const char* pem, size_t pem_len, const uint8_t* msg, size_t n,
+                                      const uint8_t* sig, size_t sig_len) {
+  EVP_PKEY* k = pem_key(pem, pem_len, false);
+  if (!k) return fail(-EINVAL, "not an RSA key");
+  EVP_MD_CTX* c = EVP_MD_CTX_new();
+  int ok = 0;
+  if (c && EVP_DigestVerifyInit(c, nullptr, EVP_sha256(), nullptr, k) == 1 && EVP_DigestVerifyUpdate(c, msg, n) == 1)
+    ok = EVP_DigestVerifyFinal(c, sig, sig_len) == 1 ? 1 : 0;
+  EVP_MD_CTX_free(c);
+  EVP_PKEY_free(k);
+  return ok;
+}
+
+namespace {
+int bio_to(BIO* b, char* out, size_t cap) {
+  char* p = nullptr;
+  const long n = BIO_get_mem_data(b, &p);
+  if (n < 0 || static_cast<size_t>(n) + 1 > cap) return fail(-ENOSPC, "output buffer too small");
+  memcpy(out, p, static_cast<size_t>(n));
+  out[n] = 0;
+  return 0;
+}
+}  // namespace
+
+// Fresh RSA key pair (OCI instance-principal session keys): PKCS#8 private PEM + SPKI public PEM.
+OMEIO_API int omeio_rsa_keygen(int bits, char* priv_pem, size_t priv_cap, char* pub_pem, size_t pub_cap) {
+  EVP_PKEY_CTX* c = EVP_PKEY_CTX_new_id(EVP_PKEY_RSA, nullptr);
+  EVP_PKEY* k = nullptr;
+  int rc = -EIO;
+  if (c && EVP_PKEY_keygen_init(c) == 1 && EVP_PKEY_CTX_set_rsa_keygen_bits(c, bits) == 1 &&
+      EVP_PKEY_keygen(c, &k) == 1) {
+    BIO* a = BIO_new(BIO_s_mem());
+    BIO* b = BIO_new(BIO_s_mem());
+    if (a && b && PEM_write_bio_PrivateKey(a, k, nullptr, nullptr, 0, nullptr, nullptr) == 1 &&
+        PEM_write_bio_PUBKEY(b, k) == 1) {
+      rc = bio_to(a, priv_pem, priv_cap);
+      if (rc == 0) rc = bio_to(b, pub_pem, pub_cap);
+    }
+    BIO_free(a);
+    BIO_free(b);
+  }
+  if (rc == -EIO) rc = fail(-EIO, "RSA key generation failed");
+  EVP_PKEY_free(k);
+  EVP_PKEY_CTX_free(c);
+  return rc;
+}
+
+// X.509 certificate facts for request signing: the one-line RFC 2253 subject, and the SHA-1 /
+// SHA-256 fingerprints of the DER encoding as colon-separated upper-case hex.
+OMEIO_API int omeio_x509_info(const char* pem, size_t n, char* subject, size_t subject_cap, char* sha1_fp,
+                              char* sha256_fp) {
+  BIO* in = BIO_new_mem_buf(pem, static_cast<int>(n));
+  X509* x = in ? PEM_read_bio_X509(in, nullptr, nullptr, nullptr) : nullptr;
+  BIO_free(in);
+  if (!x) return fail(-EINVAL, "not a PEM X.509 certificate");
+  int rc = 0;
+  BIO* b = BIO_new(BIO_s_mem());
+  if (!b || X509_NAME_print_ex(b, X509_get_subject_name(x), 0, XN_FLAG_RFC2253) < 0) rc = fail(-EIO, "subject");
+  if (rc == 0) rc = bio_to(b, subject, subject_cap);
+  BIO_free(b);
+  const EVP_MD* mds[2] = {EVP_sha1(), EVP_sha256()};
+  char* outs[2] = {sha1_fp, sha256_fp};
+  for (int i = 0; i < 2 && rc == 0; ++i) {
+    unsigned char md[EVP_MAX_MD_SIZE];
+    unsigned int len = 0;
+    if (X509_digest(x, mds[i], md, &len) != 1) {
+      rc = fail(-EIO, "certificate digest failed");
+      break;
+    }
+    static const char* hx = "0123456789ABCDEF";
+    char* o = outs[i];
+    for (unsigned int j = 0; j < len; ++j) {
+      if (j) *o++ = ':';
+      *o++ = hx[md[j] >> 4];
+      *o++ = hx[md[j] & 15];
+    }
+    *o = 0;
+  }
+  X509_free(x);
+  return rc;
 }

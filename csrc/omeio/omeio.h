@@ -73,3 +73,14 @@ OMEIO_API int64_t omeio_lz4_block_decode(const uint8_t* src, size_t len, uint8_t
 OMEIO_API int64_t omeio_lz4_frame_decode(const uint8_t* src, size_t len, uint8_t* dst, size_t cap);
 
 int omeio_fail(int code, const char* msg);
+
+// RSA PKCS#1 v1.5 / SHA-256 (OpenSSL: blinded constant-time signing, strict DigestInfo verify).
+OMEIO_API int omeio_rsa_sign_sha256(const char* pem, size_t pem_len, const uint8_t* msg, size_t n, uint8_t* sig,
+                                    size_t* sig_len);
+OMEIO_API int omeio_rsa_verify_sha256(const char* pem, size_t pem_len, const uint8_t* msg, size_t n,
+                                      const uint8_t* sig, size_t sig_len);
+// Fresh RSA key pair: PKCS#8 private PEM + SubjectPublicKeyInfo public PEM.
+OMEIO_API int omeio_rsa_keygen(int bits, char* priv_pem, size_t priv_cap, char* pub_pem, size_t pub_cap);
+// X.509: RFC 2253 subject line and SHA-1 / SHA-256 DER fingerprints ("AA:BB:..."; 60 / 96 bytes).
+OMEIO_API int omeio_x509_info(const char* pem, size_t n, char* subject, size_t subject_cap, char* sha1_fp,
+                              char* sha256_fp);

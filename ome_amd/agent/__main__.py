@@ -109,6 +109,32 @@ def cmd_encrypt(args) -> int:
     return 0
 
 
+def data_key(args, cfg: dict, model_dir: Path) -> bytes:
+    """The model's plaintext DEK (enigma.go prepareDecryptionKey): with a key service configured
+    (``kms_provider`` oci | vault, :func:`ome_amd.storage.kms.from_config`) the master key id comes
+    from the key metadata (``key_metadata``), the wrapped DEK from the vault secret
+    (``secret_name`` / ``vault_id``) or the model's ``.ome-dek``, and the key service unwraps
+    it; otherwise the local MEK (Secret / file) unwraps ``.ome-dek``."""
+    import base64 as _b64
+
+    from ome_amd.io import native
+    from ome_amd.storage import kms
+
+    provider, secrets = kms.from_config(cfg)
+    if provider is None:
+        return native.aes_gcm_decrypt((model_dir / ".ome-dek").read_bytes(), master_key(args, cfg))
+    key_id = provider.master_key_id(cfg.get("key_metadata") or {})
+    secret = _opt(args, cfg, "secret-name", "DECRYPTION_SECRET_NAME")
+    if secrets is not None and secret:
+        wrapped = secrets.get(secret, cfg.get("vault_id"))
+    else:
+        wrapped = (model_dir / ".ome-dek").read_text().strip()
+    dek = provider.decrypt(wrapped, key_id)
+    if len(dek) != 32:
+        dek = _b64.b64decode(dek)   # services that return the key base64-encoded once more
+    return dek
+
+
 def cmd_enigma(args) -> int:
     """Model-init: validate the model store, then decrypt every weight file (``enigma.go:41-174``).
     With ``--temp-path`` the model is first copied there (the reference copies to a temp dir so the
@@ -130,10 +156,9 @@ def cmd_enigma(args) -> int:
     if tmp:
         shutil.copytree(d, tmp, dirs_exist_ok=True)
         d = Path(tmp)
-    mek = master_key(args, cfg)
     try:
-        dek = native.aes_gcm_decrypt((d / ".ome-dek").read_bytes(), mek)
-    except native.OmeIOError as e:
+        dek = data_key(args, cfg, d)
+    except Exception as e:  # noqa: BLE001 -- any key-service failure stops the model-init
         log.error("failed to unwrap the data key with the master key: %s", e)
         return 1
     n = 0
@@ -141,7 +166,7 @@ def cmd_enigma(args) -> int:
         native.aes_gcm_decrypt_file(p, p, dek)
         n += 1
     (d / MARKER).unlink()
-    (d / ".ome-dek").unlink()
+    (d / ".ome-dek").unlink(missing_ok=True)   # absent when the wrapped DEK lives in a vault secret
     log.info("decrypted %d files under %s", n, d)
     return 0
 

@@ -51,6 +51,14 @@ def load():
         "omeio_read_strided": ([ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                 ctypes.c_void_p], ctypes.c_int),
         "omeio_bytes_read": ([], ctypes.c_uint64),
+        "omeio_rsa_sign_sha256": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                   ctypes.c_char_p, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+        "omeio_rsa_keygen": ([ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t],
+                             ctypes.c_int),
+        "omeio_x509_info": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                             ctypes.c_char_p], ctypes.c_int),
+        "omeio_rsa_verify_sha256": ([ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                     ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
         "omeio_copy_file": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p], ctypes.c_int),
         "omeio_md5_file": ([ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
         "omeio_aes_gcm_encrypt_file": ([ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p], ctypes.c_int),
@@ -277,3 +285,33 @@ def lz4_decode(data: bytes, size: int, frame: bool = True) -> bytes:
     if got < 0:
         raise OmeIOError(lib.omeio_last_error().decode())
     return out.raw[:got]
+
+
+def rsa_sign_sha256(pem: bytes, msg: bytes) -> bytes:
+    """RSA PKCS#1 v1.5 / SHA-256 with OpenSSL (blinded, constant-time)."""
+    out = ctypes.create_string_buffer(1024)
+    n = ctypes.c_size_t(1024)
+    _check(load().omeio_rsa_sign_sha256(pem, len(pem), msg, len(msg), out, ctypes.byref(n)))
+    return out.raw[:n.value]
+
+
+def rsa_verify_sha256(pem: bytes, msg: bytes, sig: bytes) -> bool:
+    rc = load().omeio_rsa_verify_sha256(pem, len(pem), msg, len(msg), sig, len(sig))
+    if rc < 0:
+        raise OmeIOError(load().omeio_last_error().decode())
+    return rc == 1
+
+
+def rsa_keygen(bits: int = 2048) -> tuple[str, str]:
+    """(private PKCS#8 PEM, public SPKI PEM) of a fresh RSA key pair (OpenSSL)."""
+    a, b = ctypes.create_string_buffer(8192), ctypes.create_string_buffer(4096)
+    _check(load().omeio_rsa_keygen(bits, a, len(a), b, len(b)))
+    return a.value.decode(), b.value.decode()
+
+
+def x509_info(cert_pem: str | bytes) -> dict:
+    """{"subject": RFC 2253 line, "sha1": "AA:BB:..", "sha256": ".."} of a PEM certificate."""
+    pem = cert_pem.encode() if isinstance(cert_pem, str) else cert_pem
+    subj, f1, f2 = ctypes.create_string_buffer(4096), ctypes.create_string_buffer(64), ctypes.create_string_buffer(100)
+    _check(load().omeio_x509_info(pem, len(pem), subj, len(subj), f1, f2))
+    return {"subject": subj.value.decode(), "sha1": f1.value.decode(), "sha256": f2.value.decode()}

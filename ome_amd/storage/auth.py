@@ -365,9 +365,12 @@ def _der_children(buf: bytes, start: int, end: int) -> list[tuple[int, int, int]
 
 @dataclass
 class RsaKey:
+    """An RSA private key.  Signing and verification go through OpenSSL in libomeio (blinded CRT
+    private operation, strict PKCS#1 v1.5 DigestInfo check); the parsed (n, e) remain available."""
     n: int
     e: int
     d: int
+    pem: bytes = b""
 
     @property
     def size(self) -> int:
@@ -389,21 +392,23 @@ class RsaKey:
         ints = [int.from_bytes(der[s:e], "big") for t, s, e in kids if t == 0x02]
         if len(ints) < 4:
             raise AuthError("not an RSA private key")
-        return cls(n=ints[1], e=ints[2], d=ints[3])
+        return cls(n=ints[1], e=ints[2], d=ints[3], pem=text.encode())
 
     def sign_sha256(self, msg: bytes) -> bytes:
-        prefix = bytes.fromhex("3031300d060960864801650304020105000420")
-        t = prefix + hashlib.sha256(msg).digest()
-        k = self.size
-        if k < len(t) + 11:
-            raise AuthError("RSA key too small")
-        em = b"\x00\x01" + b"\xff" * (k - len(t) - 3) + b"\x00" + t
-        return pow(int.from_bytes(em, "big"), self.d, self.n).to_bytes(k, "big")
+        from ome_amd.io import native
+
+        try:
+            return native.rsa_sign_sha256(self.pem, msg)
+        except native.OmeIOError as e:
+            raise AuthError(f"RSA signing failed: {e}") from e
 
     def verify_sha256(self, msg: bytes, sig: bytes) -> bool:
-        k = self.size
-        em = pow(int.from_bytes(sig, "big"), self.e, self.n).to_bytes(k, "big")
-        return em.endswith(hashlib.sha256(msg).digest()) and em.startswith(b"\x00\x01\xff")
+        """Strict PKCS#1 v1.5 verification (the whole encoded message, not a prefix/suffix match)."""
+        from ome_amd.io import native
+
+        if len(sig) != self.size:
+            return False
+        return native.rsa_verify_sha256(self.pem, msg, sig)
 
 
 # ------------------------------------------------------------------ OCI
@@ -523,6 +528,73 @@ class OciOkeWorkloadIdentity(OciSigner):
                     tok = tok[3:]
                 self._token, self._exp = tok, time.time() + float(d.get("expires_in", 3600))
             return "ST$" + self._token
+
+
+class OciInstancePrincipal(OciSigner):
+    """Instance principal (reference ``pkg/principals/instance_principal.go`` -> the OCI SDK
+    flow): the instance's identity certificate and key from IMDS (:mod:`.imds`) sign an X.509
+    federation request to ``https://auth.<region>.<realm domain>/v1/x509`` (key id
+    ``<tenancy>/fed-x509-sha256/<cert SHA-256 fingerprint>``) that binds a fresh session key
+    pair (generated by OpenSSL in libomeio); requests are then signed with the session key and
+    key id ``ST$<token>``, refreshed before the token's ``exp``."""
+    auth_type = "OCIInstancePrincipal"
+
+    def __init__(self, imds=None, region: str | None = None, auth_endpoint: str | None = None):
+        from ome_amd.io import native
+        from ome_amd.storage.imds import Imds
+
+        self.imds = imds or Imds()
+        priv, self._session_pub = native.rsa_keygen(2048)
+        super().__init__(RsaKey.from_pem(priv), "")
+        self.region = region or os.environ.get("OCI_REGION") or ""
+        self.auth_endpoint = auth_endpoint or os.environ.get("OCI_SDK_AUTH_CLIENT_REGION_URL") or ""
+        self._token, self._exp = "", 0.0
+        self._lock = threading.Lock()
+
+    def _endpoint(self) -> str:
+        if self.auth_endpoint:
+            return self.auth_endpoint.rstrip("/")
+        region = self.region or self.imds.region()
+        return f"https://auth.{region}.{self.imds.realm_domain()}"
+
+    def _federate(self) -> tuple[str, float]:
+        from ome_amd.io import native
+        from ome_amd.storage.imds import pem_body
+
+        cert, key, inter = (self.imds.leaf_certificate(), self.imds.leaf_private_key(),
+                            self.imds.intermediate_certificate())
+        info = native.x509_info(cert)
+        tenancy = self.imds.tenancy_id(cert)
+        body = json.dumps({"certificate": pem_body(cert), "publicKey": pem_body(self._session_pub),
+                           "intermediateCertificates": [pem_body(inter)], "purpose": "DEFAULT",
+                           "fingerprintAlgorithm": "SHA256"}).encode()
+        fed = OciSigner(RsaKey.from_pem(key), f"{tenancy}/fed-x509-sha256/{info['sha256']}")
+        url = self._endpoint() + "/v1/x509"
+        h = fed.sign("POST", url, {"content-type": "application/json"}, body)
+        try:
+            _, _, resp = _http("POST", url, h, body, timeout=30.0)
+        except OSError as e:
+            raise AuthError(f"instance principal federation at {url} failed: {e}") from e
+        tok = json.loads(resp).get("token", "")
+        if not tok:
+            raise AuthError("instance principal federation returned no token")
+        return tok, _jwt_exp(tok)
+
+    def key_id(self) -> str:
+        with self._lock:
+            if not self._token or time.time() > self._exp - 60:
+                self._token, self._exp = self._federate()
+            return "ST$" + self._token
+
+
+def _jwt_exp(token: str, default_s: float = 1200.0) -> float:
+    """``exp`` claim of a JWT (no signature check: the token is opaque to us, the service checks it)."""
+    try:
+        payload = token.split(".")[1]
+        d = json.loads(base64.urlsafe_b64decode(payload + "=" * (-len(payload) % 4)))
+        return float(d["exp"])
+    except (IndexError, ValueError, KeyError, TypeError):
+        return time.time() + default_s
 
 
 def _der_len(n: int) -> bytes:
@@ -662,6 +734,15 @@ class Factory:
 
         self.register(OCI, "OCIUserPrincipal", oci_user)
         self.register(OCI, "OCIResourcePrincipal", lambda c: OciResourcePrincipal(x(c, "rpst"), x(c, "key_pem")))
+        def oci_instance(c):
+            from ome_amd.storage.imds import Imds
+
+            imds = Imds(x(c, "imds_endpoint") or "http://169.254.169.254/opc/v2",
+                        x(c, "imds_fallback_endpoint") or "http://169.254.169.254/opc/v1")
+            return OciInstancePrincipal(imds, x(c, "region"), x(c, "auth_endpoint_override") or x(c, "auth_endpoint"))
+
+        self.register(OCI, "OCIInstancePrincipal", oci_instance)
+        self.register(OCI, "InstancePrincipal", oci_instance)
         self.register(OCI, "OCIOkeWorkloadIdentity", lambda c: OciOkeWorkloadIdentity(
             x(c, "key_pem") or open(x(c, "key_file")).read(), x(c, "endpoint"), x(c, "sa_token_file")))
 

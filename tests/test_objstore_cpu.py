@@ -445,3 +445,29 @@ def test_filesystem_root_still_serves_without_endpoint(tmp_path, monkeypatch):
     monkeypatch.setenv("OME_OBJECT_STORE_ROOT", str(root))
     res = fetch("s3://bk/pre", str(tmp_path / "dst"))
     assert Path(res.path, "f").read_bytes() == b"abc"
+
+
+def test_rsa_verify_rejects_forged_encodings(tmp_path):
+    """verify_sha256 checks the whole PKCS#1 v1.5 encoding: a signature whose decoded block only
+    starts 00 01 ff and ends with the digest (garbage in between, a Bleichenbacher-style shape)
+    is rejected, as are wrong-length and tampered signatures."""
+    key = _openssl_key(tmp_path)
+    k = A.RsaKey.from_pem(key.read_text())
+    msg = b"GET /n/ns/b/bucket/o/name"
+    sig = k.sign_sha256(msg)
+    assert k.verify_sha256(msg, sig)
+    assert not k.verify_sha256(msg + b"x", sig)
+    assert not k.verify_sha256(msg, sig[:-1])
+    bad = bytearray(sig)
+    bad[10] ^= 1
+    assert not k.verify_sha256(msg, bytes(bad))
+    # forge: 00 01 ff <junk> <sha256(msg)> raised to d -- passes a prefix/suffix check, fails strict
+    import hashlib
+
+    size = k.size
+    digest = hashlib.sha256(msg).digest()
+    em = b"\x00\x01\xff" + bytes(range(7, 7 + size - 3 - len(digest))) + digest
+    forged = pow(int.from_bytes(em, "big"), k.d, k.n).to_bytes(size, "big")
+    em_back = pow(int.from_bytes(forged, "big"), k.e, k.n).to_bytes(size, "big")
+    assert em_back.startswith(b"\x00\x01\xff") and em_back.endswith(digest)   # the old check would pass
+    assert not k.verify_sha256(msg, forged)
