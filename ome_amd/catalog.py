@@ -120,6 +120,10 @@ FAMILIES: list[Family] = [
     Family("gemma-2-9b-it", "google", "google/gemma-2-9b-it", "Gemma2ForCausalLM", 9.2, "gemma-2-9b"),
     Family("gemma-3-27b-it", "google", "google/gemma-3-27b-it", "Gemma3ForConditionalGeneration", 27.4,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("gemma-3-1b-it", "google", "google/gemma-3-1b-it", "Gemma3ForCausalLM", 1.0),
+    Family("grok-1", "xai-org", "xai-org/grok-1", "Grok1ModelForCausalLM", 316.0, "grok-1"),
+    Family("grok-2", "xai-org", "xai-org/grok-2", "Grok1ForCausalLM", 314.0, "grok-2"),
+    Family("tele-flm", "cofeai", "CofeAI/Tele-FLM", "TeleFLMModel", 52.0, "tele-flm"),
     Family("phi-3-mini-4k-instruct", "microsoft", "microsoft/Phi-3-mini-4k-instruct", "Phi3ForCausalLM", 3.8),
     Family("phi-3-5-moe-instruct", "microsoft", "microsoft/Phi-3.5-MoE-instruct", "PhiMoEForCausalLM", 41.9),
     Family("starcoder2-7b", "bigcode", "bigcode/starcoder2-7b", "Starcoder2ForCausalLM", 7.2, "starcoder2-7b"),

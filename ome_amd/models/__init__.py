@@ -32,6 +32,14 @@ MOE_ARCHS = {"MixtralForCausalLM", "Qwen2MoeForCausalLM", "Qwen3MoeForCausalLM",
 
 
 def model_class(cfg: ModelConfig):
+    if cfg.architecture in ("Grok1ModelForCausalLM", "Grok1ForCausalLM") or cfg.model_type in ("grok-1", "grok1"):
+        from ome_amd.models.grok import GrokForCausalLM
+
+        return GrokForCausalLM
+    if cfg.architecture in ("TeleFLMModel", "TeleFLMForCausalLM") or cfg.model_type == "teleflm":
+        from ome_amd.models.teleflm import TeleFLMForCausalLM
+
+        return TeleFLMForCausalLM
     if cfg.architecture == "GptOssForCausalLM" or cfg.model_type == "gpt_oss":
         from ome_amd.models.gpt_oss import GptOssForCausalLM
 
@@ -169,7 +177,8 @@ def supported(arch: str) -> bool:
         arch in ("LlavaQwenForCausalLM", "LlavaOnevisionForConditionalGeneration") or \
         arch in ("BailingMoeForCausalLM", "XverseMoeForCausalLM", "Glm4vMoeForConditionalGeneration") or \
         arch == "GptOssForCausalLM" or arch in ("KimiVLForConditionalGeneration", "Kimi_K25ForConditionalGeneration") or \
-        arch in ("Phi4MMForCausalLM", "Phi4MultimodalForCausalLM")
+        arch in ("Phi4MMForCausalLM", "Phi4MultimodalForCausalLM") or \
+        arch in ("Grok1ModelForCausalLM", "Grok1ForCausalLM") or arch in ("TeleFLMModel", "TeleFLMForCausalLM")
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,

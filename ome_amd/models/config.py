@@ -479,6 +479,41 @@ PRESETS: dict[str, dict] = {
                      num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, head_dim=128,
                      intermediate_size=512, moe_intermediate_size=128, num_experts=8, num_experts_per_tok=2,
                      vocab_size=1024, rms_norm_eps=1e-6, rope_theta=10000.0, max_position_embeddings=2048),
+    # xai-org Grok-1 (hpcai-tech/grok-1 config.json) and Grok-2 (xai-org/grok-2, SGLang's keys)
+    "grok-1": dict(architectures=["Grok1ModelForCausalLM"], model_type="grok-1", hidden_size=6144,
+                   num_hidden_layers=64, num_attention_heads=48, num_key_value_heads=8, intermediate_size=32768,
+                   num_experts=8, num_experts_per_tok=2, vocab_size=131072, rms_norm_eps=1e-5, rope_theta=10000.0,
+                   max_position_embeddings=8192, attn_output_multiplier=0.08838834764831845, max_attn_value=30.0,
+                   embedding_multiplier_scale=78.38367176906169, output_multiplier_scale=0.5773502691896257,
+                   tie_word_embeddings=True),
+    "grok-2": dict(architectures=["Grok1ForCausalLM"], model_type="grok-2", hidden_size=8192, num_hidden_layers=64,
+                   num_attention_heads=64, num_key_value_heads=8, head_dim=128, intermediate_size=32768,
+                   moe_intermediate_size=16384, num_local_experts=8, num_experts_per_tok=2, vocab_size=131072,
+                   rms_norm_eps=1e-5, rope_theta=208533496.0, max_position_embeddings=131072, residual_moe=True,
+                   attn_logit_softcapping=30.0, router_logit_softcapping=30.0, final_logit_softcapping=50.0,
+                   embedding_multiplier_scale=90.50966799187809, output_multiplier_scale=0.5,
+                   tie_word_embeddings=False),
+    "tiny-grok1": dict(architectures=["Grok1ModelForCausalLM"], model_type="grok-1", hidden_size=256,
+                       num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, intermediate_size=256,
+                       num_experts=8, num_experts_per_tok=2, vocab_size=1024, rms_norm_eps=1e-5, rope_theta=10000.0,
+                       max_position_embeddings=2048, attn_output_multiplier=0.125, max_attn_value=30.0,
+                       embedding_multiplier_scale=16.0, output_multiplier_scale=0.5773502691896257,
+                       tie_word_embeddings=True),
+    "tiny-grok2": dict(architectures=["Grok1ForCausalLM"], model_type="grok-2", hidden_size=256, num_hidden_layers=2,
+                       num_attention_heads=4, num_key_value_heads=2, head_dim=64, intermediate_size=512,
+                       moe_intermediate_size=128, num_local_experts=8, num_experts_per_tok=2, vocab_size=1024,
+                       rms_norm_eps=1e-5, rope_theta=1000000.0, max_position_embeddings=2048, residual_moe=True,
+                       attn_logit_softcapping=30.0, router_logit_softcapping=30.0, final_logit_softcapping=50.0,
+                       embedding_multiplier_scale=16.0, output_multiplier_scale=0.5, tie_word_embeddings=False),
+    # CofeAI/Tele-FLM (52B, muP multipliers)
+    "tele-flm": dict(architectures=["TeleFLMModel"], model_type="teleflm", hidden_size=8192, num_hidden_layers=64,
+                     num_attention_heads=64, num_key_value_heads=64, intermediate_size=21824, vocab_size=80000,
+                     rms_norm_eps=1e-5, rope_theta=10000.0, max_position_embeddings=4096, use_mup=True,
+                     input_mult=1.0, output_mult=1.0, mup_scale_factor=32.0, tie_word_embeddings=False),
+    "tiny-teleflm": dict(architectures=["TeleFLMModel"], model_type="teleflm", hidden_size=256, num_hidden_layers=2,
+                         num_attention_heads=4, num_key_value_heads=4, intermediate_size=512, vocab_size=1024,
+                         rms_norm_eps=1e-5, rope_theta=10000.0, max_position_embeddings=2048, use_mup=True,
+                         input_mult=3.0, output_mult=2.0, mup_scale_factor=8.0, tie_word_embeddings=False),
     "deepseek-v3": dict(architectures=["DeepseekV3ForCausalLM"], model_type="deepseek_v3", hidden_size=7168,
                         num_hidden_layers=61, num_attention_heads=128, num_key_value_heads=128,
                         intermediate_size=18432, moe_intermediate_size=2048, n_routed_experts=256,

@@ -128,6 +128,12 @@ class LlamaForCausalLM:
         return isinstance(w, torch.Tensor) and w.dim() == 2 and w.numel() > 0 and w.shape[0] % 64 == 0 and \
             w.shape[1] % 128 == 0
 
+    plain_layout = False   # subclass keeps the Llama weight layout, loader and MLP (e.g. TeleFLM)
+
+    def _plain(self) -> bool:
+        return type(self) is LlamaForCausalLM or type(self).__dict__.get("plain_layout", False)
+
+    softcap = 0.0   # attention-logit soft-capping cap * tanh(s / cap) (0: off)
     gu_il = False   # gate_up rows interleaved in 16-row blocks (fused SiLU*mul GEMM epilogue)
 
     def _post_load(self) -> None:
@@ -135,7 +141,7 @@ class LlamaForCausalLM:
         embedding, LM head and norms stay bf16, as in the reference runtimes).  bf16 SwiGLU on a
         GPU: gate_up weights are interleaved in 16-row blocks so the stream-K GEMM can apply
         SiLU(gate) * up in its epilogue (no act_and_mul pass, no [T, 2I] intermediate)."""
-        if not self.fp8 and type(self) is LlamaForCausalLM and self.act == 0 and self.device.type == "cuda" and \
+        if not self.fp8 and self._plain() and self.act == 0 and self.device.type == "cuda" and \
                 self.dtype == torch.bfloat16 and os.environ.get("OME_GATE_UP_INTERLEAVE", "1") == "1" and \
                 all(isinstance(self.w_gu[i], torch.Tensor) and self.w_gu[i].shape[0] % 32 == 0 for i in self.layers):
             for i in self.layers:
@@ -163,7 +169,7 @@ class LlamaForCausalLM:
         """Whether this rank reads only its shard of the checkpoint (dense Llama family under
         TP / PP; fp8 checkpoints keep whole-tensor reads: their scales follow the block grid)."""
         st = pstate.get()
-        return type(self) is LlamaForCausalLM and not self.fp8 and (self.tp.tp > 1 or st.pp_size > 1)
+        return self._plain() and not self.fp8 and (self.tp.tp > 1 or st.pp_size > 1)
 
     def shard_plan(self, name: str, shape) -> tuple[str, int, int] | None:
         """This rank's slice of checkpoint tensor ``name`` (full ``shape``), mirroring
@@ -304,19 +310,21 @@ class LlamaForCausalLM:
     def attention(self, q: torch.Tensor, k_cache, v_cache, meta: AttnMeta, ks: float = 1.0,
                   vs: float = 1.0) -> torch.Tensor:
         """``ks`` / ``vs``: the layer's fp8 KV dequantisation scales (1 for a bf16 cache)."""
+        cap = self.softcap
         if meta.is_decode:
             return ops.paged_decode(q, k_cache, v_cache, meta.block_tables, meta.seq_lens, self.scale,
-                                    meta.decode_ws, self.window, order=meta.order, k_scale=ks, v_scale=vs)
+                                    meta.decode_ws, self.window, order=meta.order, k_scale=ks, v_scale=vs, softcap=cap)
         if meta.mode == "mixed":
             return mixed_attention(
                 q, meta.num_prefill,
                 lambda qp, op: ops.paged_prefill(qp, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens,
-                                                 meta.items, self.scale, self.window, out=op, k_scale=ks, v_scale=vs),
+                                                 meta.items, self.scale, self.window, out=op, k_scale=ks, v_scale=vs,
+                                                 softcap=cap),
                 lambda qd, od: ops.paged_decode(qd, k_cache, v_cache, meta.dec_block_tables, meta.seq_lens,
                                                 self.scale, meta.decode_ws, self.window, out=od, order=meta.order,
-                                                k_scale=ks, v_scale=vs))
+                                                k_scale=ks, v_scale=vs, softcap=cap))
         return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
-                                 self.scale, self.window, k_scale=ks, v_scale=vs)
+                                 self.scale, self.window, k_scale=ks, v_scale=vs, softcap=cap)
 
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
         return pstate.tp_all_reduce(self._mlp_partial(i, x))

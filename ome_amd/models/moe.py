@@ -182,11 +182,17 @@ class MoEForCausalLM(LlamaForCausalLM):
             n += sum(t.nbytes() if hasattr(t, "scale") else t.numel() * t.element_size() for t in lst if t is not None)
         return n
 
+    def router_logits(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        return F.linear(x, self.w_router[i])
+
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
         if i not in self.moe_layers:
             return super().mlp(i, x)
-        logits = F.linear(x, self.w_router[i])
-        tw, tid = ops.moe_route(logits, self.k, self.renorm)
+        return pstate.tp_all_reduce(self._moe_partial(i, x))
+
+    def _moe_partial(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        """Routed experts (+ shared expert): this rank's partial sums, before the TP all-reduce."""
+        tw, tid = ops.moe_route(self.router_logits(i, x), self.k, self.renorm)
         if self.ep > 1:
             from ome_amd.parallel.ep import moe_ep
 
@@ -202,4 +208,4 @@ class MoEForCausalLM(LlamaForCausalLM):
             if self.w_sgate[i] is not None:
                 sh = sh * torch.sigmoid(F.linear(x, self.w_sgate[i]))
             out = out + sh
-        return pstate.tp_all_reduce(out)
+        return out
