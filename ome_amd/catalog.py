@@ -124,6 +124,8 @@ FAMILIES: list[Family] = [
     Family("grok-1", "xai-org", "xai-org/grok-1", "Grok1ModelForCausalLM", 316.0, "grok-1"),
     Family("grok-2", "xai-org", "xai-org/grok-2", "Grok1ForCausalLM", 314.0, "grok-2"),
     Family("tele-flm", "cofeai", "CofeAI/Tele-FLM", "TeleFLMModel", 52.0, "tele-flm"),
+    Family("phi-3-vision-128k-instruct", "microsoft", "microsoft/Phi-3-vision-128k-instruct", "Phi3VForCausalLM", 4.2,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("phi-3-mini-4k-instruct", "microsoft", "microsoft/Phi-3-mini-4k-instruct", "Phi3ForCausalLM", 3.8),
     Family("phi-3-5-moe-instruct", "microsoft", "microsoft/Phi-3.5-MoE-instruct", "PhiMoEForCausalLM", 41.9),
     Family("starcoder2-7b", "bigcode", "bigcode/starcoder2-7b", "Starcoder2ForCausalLM", 7.2, "starcoder2-7b"),

@@ -36,6 +36,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.grok import GrokForCausalLM
 
         return GrokForCausalLM
+    if cfg.architecture == "Phi3VForCausalLM" or cfg.model_type == "phi3_v":
+        from ome_amd.models.phi3v import Phi3VForCausalLM
+
+        return Phi3VForCausalLM
     if cfg.architecture in ("TeleFLMModel", "TeleFLMForCausalLM") or cfg.model_type == "teleflm":
         from ome_amd.models.teleflm import TeleFLMForCausalLM
 

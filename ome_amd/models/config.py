@@ -24,7 +24,7 @@ PADDED_HEAD_ARCHS = {"OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM", "
                      "SmolLM3ForCausalLM", "InternLM2ForCausalLM", "InternLM2ForRewardModel", "Qwen2ForRewardModel",
                      "LlamaForSequenceClassification", "Qwen2ForSequenceClassification",
                      "MistralForSequenceClassification", "MiMoForCausalLM", "QWenLMHeadModel", "BaichuanForCausalLM",
-                     "ExaoneForCausalLM", "OrionForCausalLM", "MiniCPMForCausalLM", "ChatGLMModel",
+                     "ExaoneForCausalLM", "OrionForCausalLM", "MiniCPMForCausalLM", "ChatGLMModel", "Phi3VForCausalLM",
                      "ChatGLMForConditionalGeneration", "OlmoeForCausalLM", "GraniteMoeForCausalLM", "DbrxForCausalLM",
                      "Ernie4_5_MoeForCausalLM", "MiniMaxM2ForCausalLM"}
 # remote-code class names that end in "Model" but are causal LMs (not embedding models)

@@ -188,7 +188,7 @@ def _spec_for(cfg: ModelConfig) -> DecoderSpec:
                                (r"blocks\.(\d+)\.attn\.out_proj\.weight", r"L.\1.o.weight"),
                                (r"blocks\.(\d+)\.ffn\.up_proj\.weight", r"L.\1.fc.weight"),
                                (r"blocks\.(\d+)\.ffn\.down_proj\.weight", r"L.\1.down.weight")])
-    if arch == "Phi3ForCausalLM":
+    if arch in ("Phi3ForCausalLM", "Phi3VForCausalLM"):   # Phi3V: the decoder of models/phi3v.py
         names = list(_LLAMA_NAMES) + [(r"(?:model\.)?layers\.(\d+)\.self_attn\.qkv_proj\.weight", r"L.\1.qkv.weight")]
         return DecoderSpec(qkv_layout="concat", names=names)
     if arch == "GraniteForCausalLM":
