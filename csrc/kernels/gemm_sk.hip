@@ -36,7 +36,7 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 
 namespace {
 
-constexpr int BM = 256, BK = 64, NTHR = 512;
+constexpr int BK = 64, NTHR = 512;
 enum { SK_BF16 = 0, SK_SILU = 2 };
 
 __device__ __forceinline__ int sk_swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
@@ -79,19 +79,24 @@ __device__ __forceinline__ int sk_block_of(int64_t u, int64_t U, int B) {
   return (int)(((u + 1) * B + U - 1) / U) - 1;
 }
 
-template <int BN, int NBUF, int EPI>
+template <int BM, int BN, int NBUF, int EPI>
 __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                           const bf16* __restrict__ W, int64_t ldw,
                                                           const bf16* __restrict__ bias, bf16* __restrict__ out,
                                                           int64_t ldo, int M, int N, int K,
                                                           float* __restrict__ ws, int* __restrict__ cnt) {
   constexpr int WT = BN * BK * 2, XT = BM * BK * 2, BUF = WT + XT;
-  constexpr int NI = BN / 32;          // 16-row W blocks per wave (a wave covers BN / 2 W rows)
+  // 8 waves = (BM / 64) X-row groups x WNS W-row groups; every wave owns 64 X rows x BN / WNS W rows
+  constexpr int WNS = 8 / (BM / 64);
+  constexpr int WR = BN / WNS;         // W rows per wave
+  constexpr int NI = WR / 16;          // 16-row W blocks per wave
   constexpr int NH = NI / 2;
   constexpr int LPT = (BN + BM) / 64;  // global_load_lds per thread per K-tile
+  static_assert(BM == 128 || BM == 256, "BM");
+  static_assert(NH >= 1 && NBUF >= 2 && NBUF <= 4, "tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wn = wave & 1, wm = wave >> 1, fr = lane & 15, fc = lane >> 4;
+  const int wn = wave % WNS, wm = wave / WNS, fr = lane & 15, fc = lane >> 4;
 
   const int tiles_m = (M + BM - 1) / BM, T = tiles_m * (N / BN), kt = K / BK;
   const int grp = blockIdx.x & 7, lb = blockIdx.x >> 3, B = gridDim.x >> 3;
@@ -199,7 +204,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
     };
     auto rdw = [&](bf16x8 (&fw)[NH], const char* lw, int kk, int ih) {
 #pragma unroll
-      for (int i = 0; i < NH; ++i) fw[i] = sk_frag(lw, wn * (BN / 2) + (ih * NH + i) * 16 + fr, kk * 4 + fc);
+      for (int i = 0; i < NH; ++i) fw[i] = sk_frag(lw, wn * WR + (ih * NH + i) * 16 + fr, kk * 4 + fc);
     };
     auto mm = [&](const bf16x8 (&fx)[4], const bf16x8 (&fw)[NH], int ih) {
 #pragma unroll
@@ -223,16 +228,15 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
     auto bufp = [&](int k) { return k >= NBUF ? k - NBUF : k; };   // k < 2 * NBUF
 
     // ---- prologue: tiles 0 .. NBUF-2 whole, the phase-4 share of tile NBUF-1, wait for tile 0
+    // (tiles past the segment's end are clamped re-reads, so the counted wait is exact either way)
     stage_all(0, 0);
-    if constexpr (NBUF == 3) stage_all(1, 1);
-    if constexpr (NBUF == 3) {
-      if (nt > 1)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(LPT) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    } else {
+    if constexpr (NBUF >= 3) stage_all(1, 1);
+    if constexpr (NBUF >= 4) stage_all(2, 2);
+    constexpr int INFL = (NBUF - 2) * LPT;   // pieces younger than the tile being waited for
+    if (INFL > 0 && nt > 1)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(INFL) : "memory");
+    else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    }
     pieces(NBUF - 1, NBUF - 1, I0{}, IS4{});
     rdx(x0, bx(0), 0);
     rdw(wa, bw(0), 0, 0);
@@ -254,10 +258,10 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
       mm(x1, wa, 0);                       // (kk1, ih0)
       rdw(wb, lw, 1, 1);
       interleave(std::integral_constant<int, NH>{}, I0{});
-      // K-tile i + 1 landed for this wave (with three buffers tile i + 2's pieces may stay in
-      // flight), every LDS read of tile i retired, then the barrier publishes tile i + 1
-      if (NBUF == 3 && i + 2 < nt)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(LPT) : "memory");
+      // K-tile i + 1 landed for this wave (tiles i + 2 .. i + NBUF - 1 may stay in flight), every
+      // LDS read of tile i retired, then the barrier publishes tile i + 1
+      if (INFL > 0 && i + 2 < nt)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INFL) : "memory");
       else
         asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       const int freed = cur;
@@ -334,7 +338,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
       }
     }
 
-    // ---- epilogue: lane (fr, fc) of (i, j) holds C[m0 + wm*64 + j*16 + fr][n0 + wn*BN/2 + i*16 + 4fc .. +3]
+    // ---- epilogue: lane (fr, fc) of (i, j) holds C[m0 + wm*64 + j*16 + fr][n0 + wn*WR + i*16 + 4fc .. +3]
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + wm * 64 + j * 16 + fr;
@@ -342,7 +346,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
       if constexpr (EPI == SK_BF16) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
-          const int n = n0 + wn * (BN / 2) + i * 16 + 4 * fc;
+          const int n = n0 + wn * WR + i * 16 + 4 * fc;
           bf16x4 v;
           if (bias) {
             const bf16x4 bv = *reinterpret_cast<const bf16x4*>(bias + n);
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
         // gate / up weight rows interleaved in 16-row blocks: W block 2i = gate, 2i + 1 = up
 #pragma unroll
         for (int i = 0; i < NI; i += 2) {
-          const int n = ((n0 + wn * (BN / 2) + i * 16) >> 1) + 4 * fc;
+          const int n = ((n0 + wn * WR + i * 16) >> 1) + 4 * fc;
           bf16x4 v;
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = (bf16)(sk_silu(acc[i][j][r]) * acc[i + 1][j][r]);
@@ -369,18 +373,18 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
   }
 }
 
-template <int BN, int NBUF, int EPI>
+template <int BM, int BN, int NBUF, int EPI>
 int launch_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, void* out, int64_t ldo, int M,
               int N, int K, int nwg, float* ws, int* cnt, hipStream_t stream) {
   constexpr int LDS = NBUF * (BN + BM) * BK * 2;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_sk_kernel<BN, NBUF, EPI>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_sk_kernel<BM, BN, NBUF, EPI>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  gemm_sk_kernel<BN, NBUF, EPI><<<nwg, NTHR, LDS, stream>>>((const bf16*)X, ldx, (const bf16*)W, ldw,
+  gemm_sk_kernel<BM, BN, NBUF, EPI><<<nwg, NTHR, LDS, stream>>>((const bf16*)X, ldx, (const bf16*)W, ldw,
                                                            (const bf16*)bias, (bf16*)out, ldo, M, N, K, ws, cnt);
   return (int)hipGetLastError();
 }
@@ -388,25 +392,32 @@ int launch_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const void
 }  // namespace
 
 // X [M][K] (row stride ldx), W [N][K] (row stride ldw), out [M][N] (or [M][N/2] for epi = 2).
-// bn in {128, 256}, N % bn == 0, K % 64 == 0, nwg % 8 == 0 (1..4096 blocks, one per CU resident:
-// 128 KiB / 144 KiB of LDS).  ws: >= nwg * 2 * 256 * bn floats; cnt: >= ceil(M/256) * N/bn ints,
-// zero before the first launch (the kernel re-arms them: HIP-graph replayable).  epi 0: bf16
+// Tiles (bm x bn): 256 x 256 (2 LDS buffers, 128 KiB), 256 x 128 (3, 144 KiB), 128 x 256 (3,
+// 144 KiB: twice the W bytes in flight per CU of 256 x 128 -- the decode shapes are HBM-latency
+// bound), 128 x 128 (4, 128 KiB).  N % bn == 0, K % 64 == 0, nwg % 8 == 0 (1..4096 blocks, one
+// per CU resident).  ws: >= nwg * 2 * bm * bn floats; cnt: >= ceil(M/bm) * N/bn ints, zero
+// before the first launch (the kernel re-arms them: HIP-graph replayable).  epi 0: bf16
 // (+ optional bias[N]); epi 2: SiLU(gate) * up with gate/up rows interleaved in 16-row blocks.
 OME_API int ome_gemm_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, void* out,
-                        int64_t ldo, int M, int N, int K, int bn, int epi, int nwg, void* ws, void* cnt,
+                        int64_t ldo, int M, int N, int K, int bm, int bn, int epi, int nwg, void* ws, void* cnt,
                         hipStream_t stream) {
   if (M <= 0) return 0;
-  if ((bn != 128 && bn != 256) || N % bn || K % BK || K <= 0 || nwg < 8 || nwg % 8 || nwg > 4096) return -2;
+  if ((bm != 128 && bm != 256) || (bn != 128 && bn != 256) || N % bn || K % BK || K <= 0 || nwg < 8 ||
+      nwg % 8 || nwg > 4096)
+    return -2;
   if (ldx % 8 || ldw % 8 || ((uintptr_t)X | (uintptr_t)W) % 16 || ldo % 4 || (uintptr_t)out % 8) return -3;
   if (epi != SK_BF16 && epi != SK_SILU) return -4;
   if (epi == SK_SILU && bias) return -4;
   if (!ws || !cnt) return -5;
   float* w = (float*)ws;
   int* c = (int*)cnt;
-#define SK_GO(BNV, NB)                                                                                     \
-  return epi == SK_BF16 ? launch_sk<BNV, NB, SK_BF16>(X, ldx, W, ldw, bias, out, ldo, M, N, K, nwg, w, c, stream) \
-                        : launch_sk<BNV, NB, SK_SILU>(X, ldx, W, ldw, bias, out, ldo, M, N, K, nwg, w, c, stream)
-  if (bn == 256) SK_GO(256, 2);
-  SK_GO(128, 3);
+#define SK_GO(BMV, BNV, NB)                                                                                         \
+  return epi == SK_BF16                                                                                             \
+             ? launch_sk<BMV, BNV, NB, SK_BF16>(X, ldx, W, ldw, bias, out, ldo, M, N, K, nwg, w, c, stream)          \
+             : launch_sk<BMV, BNV, NB, SK_SILU>(X, ldx, W, ldw, bias, out, ldo, M, N, K, nwg, w, c, stream)
+  if (bm == 256 && bn == 256) SK_GO(256, 256, 2);
+  if (bm == 256) SK_GO(256, 128, 3);
+  if (bn == 256) SK_GO(128, 256, 3);
+  SK_GO(128, 128, 4);
 #undef SK_GO
 }

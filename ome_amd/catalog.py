@@ -140,6 +140,8 @@ FAMILIES: list[Family] = [
     Family("nvidia-nemotron-3-nano-30b-a3b-bf16", "nvidia", "nvidia/NVIDIA-Nemotron-3-Nano-30B-A3B-BF16",
            "NemotronHForCausalLM", 31.6, "nemotron-3-nano-30b-a3b",
            args=['--reasoning-parser', 'nano_v3', '--tool-call-parser', 'qwen3_coder']),
+    Family("nvidia-nemotron-nano-12b-v2-vl-bf16", "nvidia", "nvidia/NVIDIA-Nemotron-Nano-12B-v2-VL-BF16",
+           "NemotronVLForConditionalGeneration", 12.6, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("nemotron-h-8b-base", "nvidia", "nvidia/Nemotron-H-8B-Base-8K", "NemotronHForCausalLM", 8.1,
            "nemotron-h-8b"),
     Family("opt-125m", "facebook", "facebook/opt-125m", "OPTForCausalLM", 0.125, "opt-125m"),

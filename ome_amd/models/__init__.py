@@ -36,6 +36,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.grok import GrokForCausalLM
 
         return GrokForCausalLM
+    if cfg.architecture in ("NemotronH_Nano_VL_V2", "NemotronVLForConditionalGeneration"):
+        from ome_amd.models.nemotron_vl import nemotron_vl_class
+
+        return nemotron_vl_class(cfg)
     if cfg.architecture == "Phi3VForCausalLM" or cfg.model_type == "phi3_v":
         from ome_amd.models.phi3v import Phi3VForCausalLM
 
@@ -182,11 +186,14 @@ def supported(arch: str) -> bool:
         arch in ("BailingMoeForCausalLM", "XverseMoeForCausalLM", "Glm4vMoeForConditionalGeneration") or \
         arch == "GptOssForCausalLM" or arch in ("KimiVLForConditionalGeneration", "Kimi_K25ForConditionalGeneration") or \
         arch in ("Phi4MMForCausalLM", "Phi4MultimodalForCausalLM") or \
-        arch in ("Grok1ModelForCausalLM", "Grok1ForCausalLM") or arch in ("TeleFLMModel", "TeleFLMForCausalLM")
+        arch in ("Grok1ModelForCausalLM", "Grok1ForCausalLM") or arch in ("TeleFLMModel", "TeleFLMForCausalLM") or \
+        arch == "Phi3VForCausalLM" or arch in ("NemotronH_Nano_VL_V2", "NemotronVLForConditionalGeneration")
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,
                 model_path: str | None = None, load_format: str = "auto", seed: int = 0):
+    if model_path:   # models that read side files of the checkpoint (tokenizer special-token ids)
+        cfg.extra = {**(cfg.extra or {}), "_model_path": str(model_path)}
     cls = model_class(cfg)
     m = cls(cfg, device=device, dtype=dtype, max_positions=max_positions)
     fmt = load_format

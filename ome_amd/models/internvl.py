@@ -318,7 +318,7 @@ def _text_config(cfg: ModelConfig) -> ModelConfig:
     if arch is None:
         mt = llm.get("model_type", "qwen2")
         arch = {"qwen2": "Qwen2ForCausalLM", "llama": "LlamaForCausalLM", "internlm2": "InternLM2ForCausalLM",
-                "qwen3": "Qwen3ForCausalLM"}.get(mt, "Qwen2ForCausalLM")
+                "qwen3": "Qwen3ForCausalLM", "nemotron_h": "NemotronHForCausalLM"}.get(mt, "Qwen2ForCausalLM")
     return dataclasses.replace(cfg, architecture=arch, model_type=llm.get("model_type", cfg.model_type))
 
 

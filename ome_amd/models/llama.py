@@ -337,7 +337,7 @@ class LlamaForCausalLM:
             w = self.w_gu[i]
             plan = ops.gemm_sk_plan(x.shape[0], w.shape[0], w.shape[1], 2) if x.shape[0] > _GEMV_ROWS else None
             if plan is not None and x.stride(1) == 1 and x.stride(0) % 8 == 0:
-                a = ops.gemm_sk(x, w, epi=2, bn=plan[0], nwg=plan[1])
+                a = ops.gemm_sk(x, w, epi=2, bn=plan[0], nwg=plan[1], bm=plan[2])
             else:
                 a = ops.act_and_mul(linear(x, w), self.act, interleaved=True)
             return self._row_parallel(a, wd)

@@ -142,7 +142,7 @@ def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None, out: torch.Tens
             and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
         plan = ops.gemm_sk_plan(x.shape[0], w.shape[0], w.shape[1], 0)
         if plan is not None and _sk_operands_ok(x, w, bias, out):
-            return ops.gemm_sk(x, w, bias, out=out, bn=plan[0], nwg=plan[1])
+            return ops.gemm_sk(x, w, bias, out=out, bn=plan[0], nwg=plan[1], bm=plan[2])
     if out is not None:
         if x.is_cuda and x.shape[0] <= _GEMV_ROWS and ops.gemv_ok(x, w, bias, out):
             return ops.gemv(x, w, bias, out=out)

@@ -851,7 +851,7 @@ def deinterleave_gate_up(y: torch.Tensor, block: int = 16):
 
 
 # ---------------------------------------------------------------------------------------------
-# Stream-K MFMA GEMM (csrc/kernels/gemm_sk.hip): persistent per-XCD stream-K over 256 x bn
+# Stream-K MFMA GEMM (csrc/kernels/gemm_sk.hip): persistent per-XCD stream-K over bm x bn
 # output tiles, fp32 partial slabs reduced in-launch by each tile's last arriver.  One workspace
 # per device (GEMMs of one engine run on one stream at a time; graph replays reuse it).
 _SK_MAX_WG = 256
@@ -868,16 +868,17 @@ def _sk_workspace(device: torch.device):
     return w
 
 
-def gemm_sk_tiles(M: int, N: int, bn: int) -> int:
-    return -(-M // 256) * (N // bn)
+def gemm_sk_tiles(M: int, N: int, bn: int, bm: int = 256) -> int:
+    return -(-M // bm) * (N // bn)
 
 
-def gemm_sk_ok(M: int, N: int, K: int, bn: int, nwg: int) -> bool:
+def gemm_sk_ok(M: int, N: int, K: int, bn: int, nwg: int, bm: int = 256) -> bool:
     """Shape / decomposition accepted by ``ome_gemm_sk`` with the shared workspace (blocks left
     without a unit simply exit)."""
-    if bn not in (128, 256) or N % bn or K % 64 or K <= 0 or nwg % 8 or not 8 <= nwg <= _SK_MAX_WG or M <= 0:
+    if bn not in (128, 256) or bm not in (128, 256) or N % bn or K % 64 or K <= 0 or nwg % 8 or \
+            not 8 <= nwg <= _SK_MAX_WG or M <= 0:
         return False
-    return gemm_sk_tiles(M, N, bn) <= _SK_CNT
+    return gemm_sk_tiles(M, N, bn, bm) <= _SK_CNT
 
 
 _SK_TABLE: dict | None = None
@@ -900,8 +901,8 @@ def _sk_table() -> dict:
     return _SK_TABLE
 
 
-def gemm_sk_plan(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:
-    """(bn, nwg) when the stream-K kernel was measured faster than hipBLASLt (gate_up: than
+def gemm_sk_plan(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int, int] | None:
+    """(bn, nwg, bm) when the stream-K kernel was measured faster than hipBLASLt (gate_up: than
     hipBLASLt + act_and_mul) for this weight shape at the nearest measured row count, else None.
     Table: ``ome_amd/_tuned/gemm_sk_gfx950.json`` written by ``scripts/gemm_sk_bench.py --table``
     (cold weights, interleaved same-box timings)."""
@@ -913,16 +914,17 @@ def gemm_sk_plan(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None
     m_near, e = min(rows, key=lambda r: abs(r[0] - M) / max(r[0], M))
     if max(m_near, M) > 1.34 * min(m_near, M):   # nothing measured close to this M
         return None
-    if e["us"] >= 0.97 * e["lib_us"] or not gemm_sk_ok(M, N, K, e["bn"], e["nwg"]):
+    bm = int(e.get("bm", 256))
+    if e["us"] >= 0.97 * e["lib_us"] or not gemm_sk_ok(M, N, K, e["bn"], e["nwg"], bm):
         return None
-    return e["bn"], e["nwg"]
+    return e["bn"], e["nwg"], bm
 
 
 def gemm_sk(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
-            epi: int = 0, bn: int = 256, nwg: int = 256) -> torch.Tensor:
+            epi: int = 0, bn: int = 256, nwg: int = 256, bm: int = 256) -> torch.Tensor:
     """out = x @ w.T (+ bias) on the stream-K MFMA kernel.  ``epi=2``: w holds gate/up rows
     interleaved in 16-row blocks (:func:`interleave_gate_up`) and out = SiLU(gate) * up [M, N/2].
-    ``bn`` 128 | 256 output columns per tile, ``nwg`` workgroups (multiple of 8; = tiles gives
+    ``bm`` x ``bn`` (128 | 256 each) output tile, ``nwg`` workgroups (multiple of 8; = tiles gives
     plain data-parallel tiles, 256 full stream-K)."""
     M, K = x.shape
     N = w.shape[0]
@@ -942,7 +944,7 @@ def gemm_sk(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
         out = torch.empty(M, N // 2 if epi == 2 else N, dtype=x.dtype, device=x.device)
     ws, cnt = _sk_workspace(x.device)
     call("ome_gemm_sk", x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ptr(bias), out.data_ptr(),
-         out.stride(0), M, N, K, bn, epi, nwg, ws.data_ptr(), cnt.data_ptr(), stream_ptr())
+         out.stride(0), M, N, K, bm, bn, epi, nwg, ws.data_ptr(), cnt.data_ptr(), stream_ptr())
     return out
 
 

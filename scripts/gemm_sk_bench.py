@@ -36,13 +36,16 @@ def bench(fn, n_w, iters=30):
     return s.elapsed_time(e) * 1000 / iters
 
 
-def nwg_cands(M, N, K, bn):
-    T = ops.gemm_sk_tiles(M, N, bn)
-    c = {256, 248, 240, 224, 192, 128}
+TILES = ((256, 128), (256, 256), (128, 256), (128, 128))   # (bm, bn)
+
+
+def nwg_cands(M, N, K, bn, bm):
+    T = ops.gemm_sk_tiles(M, N, bn, bm)
+    c = {256, 240, 224, 192}
     for k in (1, 2, 3, 4, 6, 8):
         if T % k == 0 and (T // k) % 8 == 0 and T // k <= 256:
             c.add(T // k)
-    return sorted(x for x in c if ops.gemm_sk_ok(M, N, K, bn, x))
+    return sorted(x for x in c if ops.gemm_sk_ok(M, N, K, bn, x, bm))
 
 
 def main():
@@ -76,24 +79,24 @@ def main():
             row = [f"M={M:5d} {name:8s} hipblaslt{'+act' if epi else ''} {t_lib:7.1f}us {fl / t_lib / 1e6:5.0f}TF"]
             best = None
             res = []
-            for bn in (128, 256):
-                out = torch.empty(M, N // 2 if epi else N, device=DEV, dtype=torch.bfloat16)
-                for nwg in nwg_cands(M, N, K, bn):
-                    y = ops.gemm_sk(x, wi[0], out=out, epi=epi, bn=bn, nwg=nwg)
+            out = torch.empty(M, N // 2 if epi else N, device=DEV, dtype=torch.bfloat16)
+            for bm, bn in TILES:
+                for nwg in nwg_cands(M, N, K, bn, bm):
+                    y = ops.gemm_sk(x, wi[0], out=out, epi=epi, bn=bn, nwg=nwg, bm=bm)
                     err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
                     if not err < 2e-2:
-                        row.append(f"bn{bn}/w{nwg} ERR {err:.3g}")
+                        row.append(f"{bm}x{bn}/w{nwg} ERR {err:.3g}")
                         continue
-                    t = bench(lambda i: ops.gemm_sk(x, wi[i], out=out, epi=epi, bn=bn, nwg=nwg), n_w, a.iters)
-                    res.append((t, bn, nwg))
+                    t = bench(lambda i: ops.gemm_sk(x, wi[i], out=out, epi=epi, bn=bn, nwg=nwg, bm=bm), n_w, a.iters)
+                    res.append((t, bm, bn, nwg))
                     if best is None or t < best[0]:
-                        best = (t, bn, nwg)
+                        best = (t, bm, bn, nwg)
             res.sort()
-            row.append(" ".join(f"bn{b}/w{n} {t:6.1f}" for t, b, n in res[:4]))
+            row.append(" ".join(f"{m}x{b}/w{n} {t:6.1f}" for t, m, b, n in res[:4]))
             if best:
                 row.append(f"BEST {best[0]:6.1f}us {fl / best[0] / 1e6:5.0f}TF x{t_lib / best[0]:.2f}")
-                table.setdefault(name, {})[str(M)] = {"bn": best[1], "nwg": best[2], "us": round(best[0], 1),
-                                                      "lib_us": round(t_lib, 1)}
+                table.setdefault(name, {})[str(M)] = {"bm": best[1], "bn": best[2], "nwg": best[3],
+                                                      "us": round(best[0], 1), "lib_us": round(t_lib, 1)}
                 plan.setdefault(f"{N},{K},{epi}", {})[str(M)] = table[name][str(M)]
             print("  ".join(row), flush=True)
         del ws, wi

@@ -1,6 +1,6 @@
 """csrc/kernels/gemm_sk.hip: per-XCD stream-K MFMA GEMM (fragment-order fp32 slabs, last-arriver
-in-launch reduction, 2- and 3-stage global_load_lds pipelines, bf16+bias and SiLU*mul epilogues)
-against an fp32 PyTorch reference."""
+in-launch reduction, 2-, 3- and 4-stage global_load_lds pipelines, 256- and 128-row tiles, bf16+bias
+and SiLU*mul epilogues) against an fp32 PyTorch reference."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -20,24 +20,27 @@ def _rel(a, b):
     return ((a.float() - b).abs().max() / (b.abs().max() + 1e-6)).item()
 
 
-def _nwgs(M, N, K, bn):
-    T = ops.gemm_sk_tiles(M, N, bn)
+TILES = [(256, 128), (256, 256), (128, 256), (128, 128)]   # (bm, bn)
+
+
+def _nwgs(M, N, K, bn, bm=256):
+    T = ops.gemm_sk_tiles(M, N, bn, bm)
     cands = {8, 64, 128, 200, 256}
     if T % 8 == 0 and T <= 256:
         cands.add(T)
-    return sorted(c for c in cands if ops.gemm_sk_ok(M, N, K, bn, c))
+    return sorted(c for c in cands if ops.gemm_sk_ok(M, N, K, bn, c, bm))
 
 
 @pytest.mark.parametrize("M", [1, 37, 256, 300, 913])
 @pytest.mark.parametrize("N,K", [(256, 64), (512, 4096), (6144, 4096), (4096, 14336)])
-@pytest.mark.parametrize("bn", [128, 256])
-def test_gemm_sk_plain(M, N, K, bn):
-    torch.manual_seed(M + N + K + bn)
+@pytest.mark.parametrize("bm,bn", TILES)
+def test_gemm_sk_plain(M, N, K, bm, bn):
+    torch.manual_seed(M + N + K + bn + bm)
     x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
     ref = _ref(x, w)
-    for nwg in _nwgs(M, N, K, bn):
-        y = ops.gemm_sk(x, w, bn=bn, nwg=nwg)
+    for nwg in _nwgs(M, N, K, bn, bm):
+        y = ops.gemm_sk(x, w, bn=bn, nwg=nwg, bm=bm)
         assert y.shape == (M, N)
         assert _rel(y, ref) < 1e-2, (nwg, _rel(y, ref))
 
@@ -51,14 +54,14 @@ def test_gemm_sk_identity_asymmetric():
     w = (torch.arange(N, device=DEV).view(N, 1) * 1000 + torch.arange(K, device=DEV).view(1, K)).float()
     w = (w % 251).to(torch.bfloat16)
     ref = _ref(x, w)
-    for bn in (128, 256):
-        for nwg in _nwgs(M, N, K, bn):
-            assert torch.equal(ops.gemm_sk(x, w, bn=bn, nwg=nwg).float(), ref), (bn, nwg)
+    for bm, bn in TILES:
+        for nwg in _nwgs(M, N, K, bn, bm):
+            assert torch.equal(ops.gemm_sk(x, w, bn=bn, nwg=nwg, bm=bm).float(), ref), (bm, bn, nwg)
 
 
 @pytest.mark.parametrize("M", [1, 64, 256, 700])
-@pytest.mark.parametrize("bn", [128, 256])
-def test_gemm_sk_silu_mul(M, bn):
+@pytest.mark.parametrize("bm,bn", TILES)
+def test_gemm_sk_silu_mul(M, bm, bn):
     I, H = 1792, 1024
     torch.manual_seed(M)
     x = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
@@ -66,8 +69,8 @@ def test_gemm_sk_silu_mul(M, bn):
     wi = ops.interleave_gate_up(w)
     g, u = _ref(x, w[:I]), _ref(x, w[I:])
     ref = F.silu(g) * u
-    for nwg in _nwgs(M, 2 * I, H, bn):
-        y = ops.gemm_sk(x, wi, epi=2, bn=bn, nwg=nwg)
+    for nwg in _nwgs(M, 2 * I, H, bn, bm):
+        y = ops.gemm_sk(x, wi, epi=2, bn=bn, nwg=nwg, bm=bm)
         assert y.shape == (M, I)
         assert _rel(y, ref) < 1e-2, nwg
 
@@ -79,9 +82,9 @@ def test_gemm_sk_bias_and_strided():
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
     b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
     out_big = torch.zeros(M, N + 64, device=DEV, dtype=torch.bfloat16)
-    for bn in (128, 256):
-        for nwg in _nwgs(M, N, K, bn):
-            y = ops.gemm_sk(x, w, b, out=out_big[:, :N], bn=bn, nwg=nwg)
+    for bm, bn in TILES:
+        for nwg in _nwgs(M, N, K, bn, bm):
+            y = ops.gemm_sk(x, w, b, out=out_big[:, :N], bn=bn, nwg=nwg, bm=bm)
             assert _rel(y, _ref(x, w, b)) < 1e-2
     assert out_big[:, N:].abs().max().item() == 0   # nothing written past the output view
 
@@ -129,6 +132,6 @@ def test_gemm_sk_more_blocks_than_units():
     for M, N, K in ((16, 256, 64), (300, 512, 128), (513, 1024, 192)):
         x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
         w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
-        for bn in (128, 256):
+        for bm, bn in TILES:
             for nwg in (16, 64, 256):
-                assert _rel(ops.gemm_sk(x, w, bn=bn, nwg=nwg), _ref(x, w)) < 1e-2, (M, N, K, bn, nwg)
+                assert _rel(ops.gemm_sk(x, w, bn=bn, nwg=nwg, bm=bm), _ref(x, w)) < 1e-2, (M, N, K, bm, bn, nwg)
