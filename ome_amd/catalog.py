@@ -78,6 +78,8 @@ FAMILIES: list[Family] = [
     Family("mistral-small-3-1-24b-instruct-2503", "mistralai", "mistralai/Mistral-Small-3.1-24B-Instruct-2503",
            "Mistral3ForConditionalGeneration", 24.0, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"],
            args=['--tool-call-parser', 'mistral']),
+    Family("minicpm-v-2-6", "openbmb", "openbmb/MiniCPM-V-2_6", "MiniCPMV", 8.1,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("minicpm3-4b", "openbmb", "openbmb/MiniCPM3-4B", "MiniCPM3ForCausalLM", 4.1),
     Family("internvl2-5-8b", "opengvlab", "OpenGVLab/InternVL2_5-8B", "InternVLChatModel", 8.1,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),

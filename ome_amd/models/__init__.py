@@ -40,6 +40,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.nemotron_vl import nemotron_vl_class
 
         return nemotron_vl_class(cfg)
+    if cfg.architecture == "MiniCPMV" or cfg.model_type == "minicpmv":
+        from ome_amd.models.minicpmv import MiniCPMV
+
+        return MiniCPMV
     if cfg.architecture == "Phi3VForCausalLM" or cfg.model_type == "phi3_v":
         from ome_amd.models.phi3v import Phi3VForCausalLM
 
@@ -187,7 +191,8 @@ def supported(arch: str) -> bool:
         arch == "GptOssForCausalLM" or arch in ("KimiVLForConditionalGeneration", "Kimi_K25ForConditionalGeneration") or \
         arch in ("Phi4MMForCausalLM", "Phi4MultimodalForCausalLM") or \
         arch in ("Grok1ModelForCausalLM", "Grok1ForCausalLM") or arch in ("TeleFLMModel", "TeleFLMForCausalLM") or \
-        arch == "Phi3VForCausalLM" or arch in ("NemotronH_Nano_VL_V2", "NemotronVLForConditionalGeneration")
+        arch == "Phi3VForCausalLM" or arch in ("NemotronH_Nano_VL_V2", "NemotronVLForConditionalGeneration") or \
+        arch == "MiniCPMV"
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,

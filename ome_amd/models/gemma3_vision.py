@@ -120,8 +120,13 @@ class SiglipVisionTower:
         x = pixels.to(device=self.device, dtype=self.dtype)
         x = x.reshape(n, self.C, s, ps, s, ps).permute(0, 2, 4, 1, 3, 5).reshape(n * self.n_patch, -1)
         x = (linear(x, w["patch.weight"], w["patch.bias"]).view(n, self.n_patch, E) + w["pos"]).reshape(-1, E)
-        T = x.shape[0]
-        lens = [self.n_patch] * n
+        return self.encode(x, [self.n_patch] * n, n_layers, post_norm).view(n, self.n_patch, E)
+
+    def encode(self, x: torch.Tensor, lens: list[int], n_layers: int | None = None,
+               post_norm: bool = True) -> torch.Tensor:
+        """Encoder layers over packed embeddings x [T, E] of sequences of lengths ``lens``
+        (bidirectional varlen MFMA attention per sequence) -> [T, E]."""
+        w, E, T = self.w, self.E, x.shape[0]
         for b in range(self.depth if n_layers is None else n_layers):
             p = f"layers.{b}."
             h = ops.layernorm(x.contiguous(), w[p + "ln1.weight"], w[p + "ln1.bias"], self.eps)
@@ -133,8 +138,8 @@ class SiglipVisionTower:
             f = ops.act(f, self.act) if self.act is not None else f * torch.sigmoid(1.702 * f)
             x = x + linear(f, w[p + "fc2.weight"], w[p + "fc2.bias"])
         if not post_norm:
-            return x.view(n, self.n_patch, E)
-        return ops.layernorm(x, w["post_ln.weight"], w["post_ln.bias"], self.eps).view(n, self.n_patch, E)
+            return x
+        return ops.layernorm(x, w["post_ln.weight"], w["post_ln.bias"], self.eps)
 
 
 class Gemma3ForConditionalGeneration(GemmaForCausalLM):
