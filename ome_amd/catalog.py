@@ -113,6 +113,8 @@ FAMILIES: list[Family] = [
            "MllamaForConditionalGeneration", 88.6, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("deepseek-v2-lite-chat", "deepseek-ai", "deepseek-ai/DeepSeek-V2-Lite-Chat", "DeepseekV2ForCausalLM",
            15.7, "deepseek-v2-lite"),
+    Family("deepseek-vl2", "deepseek-ai", "deepseek-ai/deepseek-vl2", "DeepseekVLV2ForCausalLM", 27.5,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("deepseek-v3", "deepseek-ai", "deepseek-ai/DeepSeek-V3", "DeepseekV3ForCausalLM", 671.0, None, 1.0,
            args=["--enable-dp-attention", "--dp", "8"], quantization="fp8", multinode=2, min_tp=8, pd=True),
     Family("kimi-k2-instruct", "moonshotai", "moonshotai/Kimi-K2-Instruct", "DeepseekV3ForCausalLM", 1026.0, None,

@@ -138,7 +138,7 @@ class RadioTower:
     def forward(self, pixels: torch.Tensor) -> torch.Tensor:
         """pixels [n, 3, S, S] (normalised) -> patch features [n * side^2, E]."""
         w, E, n, ps, s = self.w, self.E, pixels.shape[0], self.patch, pixels.shape[-1] // self.patch
-        x = pixels.to(device=self.device, dtype=self.dtype)
+        x = pixels[..., :s * ps, :s * ps].to(device=self.device, dtype=self.dtype)   # a stride-ps conv drops the rest
         x = x.reshape(n, 3, s, ps, s, ps).permute(0, 2, 4, 1, 3, 5).reshape(n * s * s, -1)
         x = linear(x, w["patch.weight"], w.get("patch.bias")).view(n, s * s, E) + self.pos_embed(s, s)
         k = self.n_skip

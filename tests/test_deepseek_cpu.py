@@ -68,8 +68,8 @@ def _rms(x, w, eps):
     return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * w
 
 
-def _hf_forward(cfg: ModelConfig, w: dict, ids: list[int]) -> torch.Tensor:
-    """HF modeling_deepseek semantics, fp32, single causal sequence."""
+def _hf_forward(cfg: ModelConfig, w: dict, ids: list[int], h0: torch.Tensor | None = None) -> torch.Tensor:
+    """HF modeling_deepseek semantics, fp32, single causal sequence (``h0``: input embeddings)."""
     T, nh = len(ids), cfg.num_heads
     nope, rope, vd = cfg.qk_nope_head_dim, cfg.qk_rope_head_dim, cfg.v_head_dim
     eps = cfg.rms_norm_eps
@@ -91,7 +91,7 @@ def _hf_forward(cfg: ModelConfig, w: dict, ids: list[int]) -> torch.Tensor:
     if sc.get("mscale_all_dim"):
         m = 0.1 * sc["mscale_all_dim"] * math.log(sc["factor"]) + 1.0
         scale *= m * m
-    h = w["model.embed_tokens.weight"][ids]
+    h = w["model.embed_tokens.weight"][ids] if h0 is None else h0
     mask = torch.full((T, T), float("-inf")).triu(1)
     for i in range(cfg.num_layers):
         p = f"model.layers.{i}."
