@@ -115,6 +115,10 @@ FAMILIES: list[Family] = [
            15.7, "deepseek-v2-lite"),
     Family("deepseek-vl2", "deepseek-ai", "deepseek-ai/deepseek-vl2", "DeepseekVLV2ForCausalLM", 27.5,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("dots-ocr", "rednote-hilab", "rednote-hilab/dots.ocr", "DotsOCRForConditionalGeneration", 3.0,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("dots-vlm1-inst", "rednote-hilab", "rednote-hilab/dots.vlm1.inst", "DotsVLMForConditionalGeneration",
+           672.0, capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], min_tp=8),
     Family("deepseek-v3", "deepseek-ai", "deepseek-ai/DeepSeek-V3", "DeepseekV3ForCausalLM", 671.0, None, 1.0,
            args=["--enable-dp-attention", "--dp", "8"], quantization="fp8", multinode=2, min_tp=8, pd=True),
     Family("kimi-k2-instruct", "moonshotai", "moonshotai/Kimi-K2-Instruct", "DeepseekV3ForCausalLM", 1026.0, None,

@@ -40,6 +40,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.nemotron_vl import nemotron_vl_class
 
         return nemotron_vl_class(cfg)
+    if cfg.architecture in ("DotsOCRForConditionalGeneration", "DotsVLMForConditionalGeneration"):
+        from ome_amd.models.dots import dots_class
+
+        return dots_class(cfg)
     if cfg.architecture == "DeepseekVLV2ForCausalLM":
         from ome_amd.models.deepseek_vl2 import DeepseekVLV2ForCausalLM
 
@@ -196,7 +200,8 @@ def supported(arch: str) -> bool:
         arch in ("Phi4MMForCausalLM", "Phi4MultimodalForCausalLM") or \
         arch in ("Grok1ModelForCausalLM", "Grok1ForCausalLM") or arch in ("TeleFLMModel", "TeleFLMForCausalLM") or \
         arch == "Phi3VForCausalLM" or arch in ("NemotronH_Nano_VL_V2", "NemotronVLForConditionalGeneration") or \
-        arch == "MiniCPMV" or arch == "DeepseekVLV2ForCausalLM"
+        arch == "MiniCPMV" or arch == "DeepseekVLV2ForCausalLM" or \
+        arch in ("DotsOCRForConditionalGeneration", "DotsVLMForConditionalGeneration")
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,
