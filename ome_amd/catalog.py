@@ -41,6 +41,7 @@ class Family:
     multinode: int = 0        # also emit a leader/worker runtime over this many nodes (bf16)
     quantization: str | None = None
     min_tp: int = 1           # e.g. DP attention over a whole node
+    diffusion: str | None = None   # diffusers pipeline class: served by ome_amd.diffusion.server
 
 
 FAMILIES: list[Family] = [
@@ -181,6 +182,12 @@ FAMILIES: list[Family] = [
     Family("ernie-4-5-21b-a3b-pt", "baidu", "baidu/ERNIE-4.5-21B-A3B-PT", "Ernie4_5_MoeForCausalLM", 21.8),
     Family("minimax-m2", "minimax", "MiniMaxAI/MiniMax-M2", "MiniMaxM2ForCausalLM", 229.0, None, 1.0,
            quantization="fp8"),
+    Family("qwen-image", "qwen", "Qwen/Qwen-Image", "QwenImagePipeline", 28.9, "qwen-image",
+           capabilities=["TEXT_TO_IMAGE"], diffusion="QwenImagePipeline"),
+    Family("qwen-image-edit", "qwen", "Qwen/Qwen-Image-Edit", "QwenImageEditPipeline", 28.9, "qwen-image",
+           capabilities=["IMAGE_TEXT_TO_IMAGE"], diffusion="QwenImageEditPipeline"),
+    Family("qwen-image-edit-plus", "qwen", "Qwen/Qwen-Image-Edit-2511", "QwenImageEditPlusPipeline", 28.9, "qwen-image",
+           capabilities=["IMAGE_TEXT_TO_IMAGE"], diffusion="QwenImageEditPlusPipeline"),
     Family("bge-large-en-v1-5", "baai", "BAAI/bge-large-en-v1.5", "BertModel", 0.335,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
     Family("bge-m3", "baai", "BAAI/bge-m3", "XLMRobertaModel", 0.568,
@@ -223,6 +230,9 @@ def _probes() -> dict:
 
 
 def server_args(f: Family, tp: int, extra: list[str] | None = None) -> list[str]:
+    if f.diffusion:
+        return ["--host", "0.0.0.0", "--port", "8080", "--enable-metrics", "--model-path", "$(MODEL_PATH)",
+                "--served-model-name", f.hf, "--pipeline", f.diffusion, "--tp-size", "1"]
     a = ["--host", "0.0.0.0", "--port", "8080", "--enable-metrics", "--model-path", "$(MODEL_PATH)",
          "--tp-size", str(tp), "--mem-frac", "0.9", "--served-model-name", f.hf]
     if f.quantization:
@@ -233,12 +243,25 @@ def server_args(f: Family, tp: int, extra: list[str] | None = None) -> list[str]
 def _container(f: Family, tp: int, args: list[str], name: str = "ome-container") -> dict:
     cpu, mem = 16 * tp, f"{64 * tp}Gi"
     return {"name": name, "image": IMAGE, "ports": [{"containerPort": 8080, "name": "http1", "protocol": "TCP"}],
-            "command": ["python3", "-m", "ome_amd.runtime.server"], "args": args,
+            "command": ["python3", "-m", "ome_amd.diffusion.server" if f.diffusion else "ome_amd.runtime.server"],
+            "args": args,
             "env": [{"name": "HSA_ENABLE_IPC_MODE_LEGACY", "value": "0"}, {"name": "GPU_MAX_HW_QUEUES", "value": "4"}],
             "volumeMounts": [{"mountPath": "/dev/shm", "name": "dshm"}],
             "resources": {"requests": {"cpu": cpu, "memory": mem, "amd.com/gpu": tp},
                           "limits": {"cpu": cpu, "memory": mem, "amd.com/gpu": tp}},
-            **_probes()}
+            **(_diffusion_probes() if f.diffusion else _probes())}
+
+
+def _diffusion_probes() -> dict:
+    def get(path, **kw):
+        return {"httpGet": {"path": path, "port": 8080}, **kw}
+
+    return {"readinessProbe": get("/health", failureThreshold=5, successThreshold=1, periodSeconds=60,
+                                  timeoutSeconds=200),
+            "livenessProbe": get("/health", failureThreshold=5, successThreshold=1, periodSeconds=60,
+                                 timeoutSeconds=200),
+            "startupProbe": get("/health", failureThreshold=150, successThreshold=1, periodSeconds=6,
+                                initialDelaySeconds=10, timeoutSeconds=30)}
 
 
 def _router() -> dict:
@@ -255,6 +278,10 @@ def _router() -> dict:
 
 
 def _formats(f: Family, priority: int = 2) -> list[dict]:
+    if f.diffusion:
+        return [{"modelFramework": {"name": "diffusers", "version": "0.34.0", "operator": "GreaterThanOrEqual"},
+                 "modelFormat": {"name": "diffusers", "version": "0.34.0"}, "modelArchitecture": f.arch,
+                 "autoSelect": True, "priority": priority, "version": "1.0.0"}]
     return [{"modelFramework": {"name": "transformers", "version": "5.0.0", "operator": "GreaterThanOrEqual"},
              "modelFormat": {"name": "safetensors", "version": "1.0.0"}, "modelArchitecture": f.arch,
              "autoSelect": True, "priority": priority, "version": "1.0.0",
@@ -287,7 +314,8 @@ def runtime(f: Family) -> dict:
                                             "prometheus.io/path": "/metrics"},
                             "volumes": [{"name": "dshm", "emptyDir": {"medium": "Memory"}}],
                             "runner": _container(f, tp, server_args(f, tp))}
-    spec["routerConfig"] = _router()
+    if not f.diffusion:
+        spec["routerConfig"] = _router()
     return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterServingRuntime",
             "metadata": {"name": f"ome-amd-{f.name}-tp{tp}"}, "spec": spec}
 
@@ -337,8 +365,10 @@ def base_model(f: Family) -> dict:
     spec = {"vendor": f.vendor, "disabled": False, "version": "1.0.0", "displayName": f"{f.vendor}.{f.name}",
             "modelCapabilities": list(f.capabilities), "modelArchitecture": f.arch,
             "modelParameterSize": size_label(f.params_b),
-            "modelFormat": {"name": "safetensors", "version": "1.0.0"},
-            "modelFramework": {"name": "transformers", "version": "4.46.0"},
+            "modelFormat": {"name": "diffusers", "version": "0.34.0"} if f.diffusion else
+            {"name": "safetensors", "version": "1.0.0"},
+            "modelFramework": {"name": "diffusers", "version": "0.34.0"} if f.diffusion else
+            {"name": "transformers", "version": "4.46.0"},
             "storage": {"storageUri": uri, "path": f"/raid/models/{f.vendor}/{f.name}"}}
     if f.quantization:
         spec["quantization"] = f.quantization

@@ -201,7 +201,8 @@ def supported(arch: str) -> bool:
         arch in ("Grok1ModelForCausalLM", "Grok1ForCausalLM") or arch in ("TeleFLMModel", "TeleFLMForCausalLM") or \
         arch == "Phi3VForCausalLM" or arch in ("NemotronH_Nano_VL_V2", "NemotronVLForConditionalGeneration") or \
         arch == "MiniCPMV" or arch == "DeepseekVLV2ForCausalLM" or \
-        arch in ("DotsOCRForConditionalGeneration", "DotsVLMForConditionalGeneration")
+        arch in ("DotsOCRForConditionalGeneration", "DotsVLMForConditionalGeneration") or \
+        arch in ("QwenImagePipeline", "QwenImageEditPipeline", "QwenImageEditPlusPipeline")   # ome_amd.diffusion
 
 
 def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: int | None = None,

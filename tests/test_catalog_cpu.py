@@ -46,6 +46,12 @@ def test_runtime_entry(rt):
     for c in _containers(rt["spec"]):
         args = [a.replace("$(MODEL_PATH)", "/m").replace("$(LWS_LEADER_ADDRESS)", "10.0.0.1")
                 .replace("$(LWS_WORKER_INDEX)", "1") for a in c["args"]]
+        if "ome_amd.diffusion.server" in c["command"]:
+            from ome_amd.diffusion.server import build_parser as diffusion_parser
+
+            ns = diffusion_parser().parse_args(args)
+            assert ns.tp_size == 1 and c["resources"]["limits"]["amd.com/gpu"] == 1
+            continue
         ns = build_parser().parse_args(args)
         gpus = c["resources"]["limits"]["amd.com/gpu"]
         assert ns.tp_size in (gpus, gpus * getattr(ns, "nnodes", 1))
