@@ -24,7 +24,8 @@ def _worker(rank, world, port, q):
 
         from ome_amd.parallel.comm import CustomAllReduce
 
-        torch.cuda.set_device(0)
+        dev_i = rank % torch.cuda.device_count() if os.environ.get("OME_TEST_SPREAD") == "1" else 0
+        torch.cuda.set_device(dev_i)   # spread: one rank per GPU over xGMI; else all ranks share GPU 0
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         ar = CustomAllReduce(None, max_bytes=8 << 20, one_shot_max=256 << 10, blocks=32)
         worst = 0.0
@@ -133,3 +134,11 @@ def test_custom_all_reduce(world):
         assert tb is None, tb
         assert err == 0, f"rank {rank}: barrier timeout recorded"
         assert worst < 1e-2, f"rank {rank}: max rel err {worst}"
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 GPUs (xGMI peers)")
+def test_custom_all_reduce_across_devices(monkeypatch):
+    """The same protocol with one rank per GPU: IPC handles opened on peer devices, flags and data
+    read over xGMI (one-shot, two-shot, graph replay, fused add + RMSNorm)."""
+    monkeypatch.setenv("OME_TEST_SPREAD", "1")
+    test_custom_all_reduce(min(8, torch.cuda.device_count()))

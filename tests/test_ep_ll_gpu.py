@@ -39,9 +39,10 @@ def _worker(rank, world, port, fp8, q):
         from ome_amd.models.quant import quantize_experts
         from ome_amd.parallel.ep_ll import LowLatencyEP
 
-        torch.cuda.set_device(0)
+        dev_i = rank % torch.cuda.device_count() if os.environ.get("OME_TEST_SPREAD") == "1" else 0
+        torch.cuda.set_device(dev_i)   # spread: one rank per GPU over xGMI; else all ranks share GPU 0
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-        dev = torch.device("cuda", 0)
+        dev = torch.device("cuda", dev_i)
         w13, w2 = (w.to(dev) for w in _weights())
         el = E // world
         loc13, loc2 = w13[rank * el:(rank + 1) * el].contiguous(), w2[rank * el:(rank + 1) * el].contiguous()
@@ -122,3 +123,11 @@ def test_low_latency_ep_matches_single_rank(world, fp8):
         assert tb is None, tb
         assert err == 0, f"rank {rank}: error word {err}"
         assert worst < 2e-2, f"rank {rank}: rel err {worst}"
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs >= 2 GPUs (xGMI peers)")
+@pytest.mark.parametrize("fp8", [False, True])
+def test_low_latency_ep_across_devices(monkeypatch, fp8):
+    """Low-latency EP dispatch / combine with one rank per GPU (peer buffers over xGMI)."""
+    monkeypatch.setenv("OME_TEST_SPREAD", "1")
+    test_low_latency_ep_matches_single_rank(min(4, torch.cuda.device_count()), fp8)
