@@ -107,7 +107,8 @@ def test_qwen_image_dit_vae_on_gpu():
     v1 = QwenImageVAE(vc, "cuda", torch.bfloat16)
     v1.w = {k: v.to("cuda", torch.bfloat16) for k, v in v0.w.items()}
     z = torch.randn(1, 16, 16, 16, generator=g)
-    assert _rel(v1.decode(z.cuda()), v0.decode(z)) < 5e-2
+    got, want = v1.decode(z.cuda()).float().cpu(), v0.decode(z)
+    assert (got - want).abs().mean().item() < 1e-2 and _rel(got, want) < 1e-1   # bf16 through ~30 convolutions
 
 
 def test_qwen_image_pipeline_on_gpu():
