@@ -29,6 +29,16 @@
 // three, the DMA of tile t+2 stays in flight across the barrier that publishes tile t+1
 // (counted vmcnt + raw s_barrier, cdna_hip_programming.md "Pipelining across barriers").
 // Epilogues: bf16 (+bias), SiLU(gate) * up for gate/up weights interleaved in 16-row blocks.
+//
+// FP8 (OCP e4m3) W8A8 on the same decomposition (Q = 1: per-token x per-channel scales, Q = 2:
+// DeepSeek 1 x 128 activation groups x 128 x 128 weight blocks).  A K-tile is 128 bytes of a row
+// in both dtypes, so the DMA pieces, the LDS images and the fragment reads are byte-identical to
+// the bf16 path; the bf16 path's kk = 0 and kk = 1 chunks of a row, side by side, are the 32-byte
+// operand of ONE v_mfma_scale_f32_16x16x128_f8f6f4 (unit MX scales; the same K permutation on both
+// operands, so the sum is exact) -- half the MFMAs at twice the rate per instruction, half the
+// weight bytes per K.  Q = 2 adds one 4-byte DMA piece per wave and K-tile that lands the tile's
+// activation group scales (and the W block scales) in LDS next to the operands, so the scale
+// traffic rides the same counted vmcnt pipeline; each block product is scaled by a VALU FMA.
 #include "common.h"
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -70,6 +80,24 @@ __device__ __forceinline__ bf16x8 sk_frag(const char* lds, int row, int chunk) {
 }
 
 typedef unsigned int sk_u32x4 __attribute__((ext_vector_type(4)));
+typedef int sk_i32x4 __attribute__((ext_vector_type(4)));
+typedef int sk_i32x8 __attribute__((ext_vector_type(8)));
+
+// fp8 operand: chunks fc and 4 + fc of the 128-byte row (the bf16 path's kk = 0 / kk = 1 reads)
+__device__ __forceinline__ sk_i32x8 sk_frag8(const char* lds, int row, int fc) {
+  const sk_i32x4 lo = *reinterpret_cast<const sk_i32x4*>(lds + row * 128 + sk_swz(row, fc) * 16);
+  const sk_i32x4 hi = *reinterpret_cast<const sk_i32x4*>(lds + row * 128 + sk_swz(row, 4 + fc) * 16);
+  return sk_i32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+__device__ __forceinline__ f32x4 sk_mfma8(sk_i32x8 a, sk_i32x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// LDS-DMA of 4 B per lane (the Q = 2 scale piece: 64 floats per wave instruction)
+__device__ __forceinline__ void sk_buf_lds4(__amdgpu_buffer_rsrc_t rs, char* lds, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 4, voff, soff, 0, 0);
+}
 
 __device__ __forceinline__ float sk_silu(float x) { return x / (1.f + __expf(-x)); }
 
@@ -79,26 +107,30 @@ __device__ __forceinline__ int sk_block_of(int64_t u, int64_t U, int B) {
   return (int)(((u + 1) * B + U - 1) / U) - 1;
 }
 
-template <int BM, int BN, int NBUF, int EPI>
-__global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict__ X, int64_t ldx,
-                                                          const bf16* __restrict__ W, int64_t ldw,
+// X, W: byte pointers with byte row strides; kt = K-tiles of 128 bytes (bf16: K / 64, fp8: K / 128)
+template <int BM, int BN, int NBUF, int EPI, int Q>
+__global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const char* __restrict__ X, int64_t ldx,
+                                                          const char* __restrict__ W, int64_t ldw,
+                                                          const float* __restrict__ sa, const float* __restrict__ sw,
                                                           const bf16* __restrict__ bias, bf16* __restrict__ out,
-                                                          int64_t ldo, int M, int N, int K,
+                                                          int64_t ldo, int M, int N, int kt,
                                                           float* __restrict__ ws, int* __restrict__ cnt) {
-  constexpr int WT = BN * BK * 2, XT = BM * BK * 2, BUF = WT + XT;
+  // LDS per buffer: W image, X image, (Q = 2) BM activation scales + 64 W-block scale slots + 64 dummy
+  constexpr int WT = BN * 128, XT = BM * 128, ST = Q == 2 ? BM * 4 + 512 : 0, BUF = WT + XT + ST;
   // 8 waves = (BM / 64) X-row groups x WNS W-row groups; every wave owns 64 X rows x BN / WNS W rows
   constexpr int WNS = 8 / (BM / 64);
   constexpr int WR = BN / WNS;         // W rows per wave
   constexpr int NI = WR / 16;          // 16-row W blocks per wave
   constexpr int NH = NI / 2;
-  constexpr int LPT = (BN + BM) / 64;  // global_load_lds per thread per K-tile
+  constexpr int LPT = (BN + BM) / 64 + (Q == 2);  // LDS-DMA pieces per thread per K-tile
   static_assert(BM == 128 || BM == 256, "BM");
+  static_assert(Q == 0 || NH <= 2, "fp8: 64 accumulator + 2 x 32 X + 2 x 8 NH W fragment registers");
   static_assert(NH >= 1 && NBUF >= 2 && NBUF <= 4, "tile");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wn = wave % WNS, wm = wave / WNS, fr = lane & 15, fc = lane >> 4;
 
-  const int tiles_m = (M + BM - 1) / BM, T = tiles_m * (N / BN), kt = K / BK;
+  const int tiles_m = (M + BM - 1) / BM, T = tiles_m * (N / BN);
   const int grp = blockIdx.x & 7, lb = blockIdx.x >> 3, B = gridDim.x >> 3;
   const int tile_lo = (int)((int64_t)T * grp / 8), tile_hi = (int)((int64_t)T * (grp + 1) / 8);
   // whole tiles round-robin over the group's blocks (round r: tiles tile_lo + r*B + 0..B-1, so the
@@ -111,9 +143,12 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
 
   auto bw = [&](int b) { return smem + b * BUF; };
   auto bx = [&](int b) { return smem + b * BUF + WT; };
+  auto bs = [&](int b) { return smem + b * BUF + WT + XT; };
 
   f32x4 acc[NI][4];
   bf16x8 x0[4], x1[4], wa[NH], wb[NH];
+  sk_i32x8 xa8[4], xb8[4], wa8[NH], wb8[NH];   // fp8 path (dead code for Q = 0)
+  float sc0[5], sc1[5];                          // Q = 2: 4 row scales + the W block scale per K-tile
 
   int r = 0;
   int64_t u = u_beg;
@@ -158,24 +193,38 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
                                                        0x00020000);
     const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (int64_t)m0 * ldx), (short)0, 0x7fffffff,
                                                        0x00020000);
+    // Q = 2 scale piece: waves < BM/64 land 64 activation-row scales each, wave BM/64 the tile's
+    // W block scales (lanes < BN/128), the rest re-read those into a dummy slot (uniform counts)
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    const auto rss = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Q != 2 ? (const float*)X : wv < BM / 64 ? sa + (int64_t)m0 * kt : sw + (int64_t)(n0 >> 7) * kt),
+        (short)0, 0x7fffffff, 0x00020000);
+    const int sdst = wv < BM / 64 ? wv * 256 : wv == BM / 64 ? BM * 4 : BM * 4 + 256;
     uint32_t vo[LPT];
 #pragma unroll
     for (int q = 0; q < LPT; ++q) {
       if (q < PW) {
         const int r = (wave * PW + q) * 8 + (lane >> 3);
-        vo[q] = (uint32_t)((r * ldw + sk_swz(r, lane & 7) * 8) * 2);
-      } else {
+        vo[q] = (uint32_t)(r * ldw + sk_swz(r, lane & 7) * 16);
+      } else if (q < PW + BM / 64) {
         const int r = (wave * (BM / 64) + (q - PW)) * 8 + (lane >> 3);
         const int rr = m0 + r < M ? r : M - 1 - m0;   // rows past M re-read the last row
-        vo[q] = (uint32_t)((rr * ldx + sk_swz(r, lane & 7) * 8) * 2);
+        vo[q] = (uint32_t)(rr * ldx + sk_swz(r, lane & 7) * 16);
+      } else if (wv < BM / 64) {
+        const int r = wv * 64 + lane;
+        vo[q] = (uint32_t)((m0 + r < M ? r : M - 1 - m0) * kt * 4);
+      } else {
+        vo[q] = (uint32_t)((lane < BN / 128 ? lane : 0) * kt * 4);
       }
     }
     auto piece = [&](int t, int b, auto q_tag) {
       constexpr int q = decltype(q_tag)::value;
       if constexpr (q < PW)
-        sk_buf_lds(rsw, bw(b) + (wave * PW + q) * 1024, vo[q], t * BK * 2);
+        sk_buf_lds(rsw, bw(b) + (wave * PW + q) * 1024, vo[q], t * 128);
+      else if constexpr (q < PW + BM / 64)
+        sk_buf_lds(rsx, bx(b) + (wave * (BM / 64) + q - PW) * 1024, vo[q], t * 128);
       else
-        sk_buf_lds(rsx, bx(b) + (wave * (BM / 64) + q - PW) * 1024, vo[q], t * BK * 2);
+        sk_buf_lds4(rss, bs(b) + sdst, vo[q], t * 4);
     };
     auto pieces = [&](int T, int b, auto q0_tag, auto q1_tag) {   // pieces [q0, q1) of relative tile T
       constexpr int q0 = decltype(q0_tag)::value, q1 = decltype(q1_tag)::value;
@@ -238,9 +287,80 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
     pieces(NBUF - 1, NBUF - 1, I0{}, IS4{});
+    int cur = 0;
+    if constexpr (Q != 0) {
+      // ---- fp8: two phases of 4*NH MFMAs per K-tile (W half ih = 0, 1); X fragments double-
+      // buffered across K-tiles (xa8 / xb8: the iteration body is unrolled twice)
+      auto rdx8 = [&](sk_i32x8 (&fx)[4], float (&sc)[5], int b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fx[j] = sk_frag8(bx(b), wm * 64 + j * 16 + fr, fc);
+        if constexpr (Q == 2) {
+          const char* ls = bs(b);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) sc[j] = *reinterpret_cast<const float*>(ls + (wm * 64 + j * 16 + fr) * 4);
+          sc[4] = *reinterpret_cast<const float*>(ls + BM * 4 + ((wn * WR) >> 7) * 4);
+        }
+      };
+      auto rdw8 = [&](sk_i32x8 (&fw)[NH], int b, int ih) {
+#pragma unroll
+        for (int i = 0; i < NH; ++i) fw[i] = sk_frag8(bw(b), wn * WR + (ih * NH + i) * 16 + fr, fc);
+      };
+      auto mm8 = [&](const sk_i32x8 (&fx)[4], const sk_i32x8 (&fw)[NH], int ih, const float (&sc)[5]) {
+#pragma unroll
+        for (int i = 0; i < NH; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if constexpr (Q == 2) {
+              const f32x4 p = sk_mfma8(fw[i], fx[j], f32x4{0.f, 0.f, 0.f, 0.f});
+              acc[ih * NH + i][j] += p * (sc[j] * sc[4]);
+            } else {
+              acc[ih * NH + i][j] = sk_mfma8(fw[i], fx[j], acc[ih * NH + i][j]);
+            }
+          }
+      };
+      // up to 3 fragment reads per MFMA gap (a 16x16x128 fp8 MFMA is twice a bf16 one)
+      auto interleave8 = [&](auto nr_tag, auto nv_tag) {
+        constexpr int NR = decltype(nr_tag)::value, NV = decltype(nv_tag)::value;
+        constexpr int PER = (NR + 4 * NH - 1) / (4 * NH);
+#pragma unroll
+        for (int k = 0; k < 4 * NH; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (k < NV) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+          if (k * PER < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          if (PER > 1 && k * PER + 1 < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          if (PER > 2 && k * PER + 2 < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+      };
+      constexpr int NRX = 8 + (Q == 2 ? 5 : 0);
+      auto it8 = [&](int i, sk_i32x8 (&xc)[4], sk_i32x8 (&xn)[4], float (&sc)[5], float (&sn)[5]) {
+        const int nb = bufp(cur + NBUF - 1);
+        mm8(xc, wa8, 0, sc);
+        rdw8(wb8, cur, 1);
+        pieces(i + NBUF - 1, nb, IS4{}, ILPT{});
+        interleave8(std::integral_constant<int, 2 * NH>{}, std::integral_constant<int, LPT - S4>{});
+        if (INFL > 0 && i + 2 < nt)
+          asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(INFL) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const int freed = cur;
+        cur = cur + 1 == NBUF ? 0 : cur + 1;
+        mm8(xc, wb8, 1, sc);
+        rdx8(xn, sn, cur);
+        rdw8(wa8, cur, 0);
+        pieces(i + NBUF, freed, I0{}, IS4{});
+        interleave8(std::integral_constant<int, NRX + 2 * NH>{}, std::integral_constant<int, S4>{});
+      };
+      rdx8(xa8, sc0, 0);
+      rdw8(wa8, 0, 0);
+      int i = 0;
+      for (; i + 1 < nt; i += 2) {
+        it8(i, xa8, xb8, sc0, sc1);
+        it8(i + 1, xb8, xa8, sc1, sc0);
+      }
+      if (i < nt) it8(i, xa8, xb8, sc0, sc1);
+    } else {
     rdx(x0, bx(0), 0);
     rdw(wa, bw(0), 0, 0);
-    int cur = 0;
     for (int i = 0; i < nt; ++i) {
       const char* lw = bw(cur);
       const char* lx = bx(cur);
@@ -271,6 +391,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
       rdw(wa, bw(cur), 0, 0);              //  unused in-bounds LDS words)
       pieces(i + NBUF, freed, I0{}, IS4{});   // tile i + NBUF into the buffer tile i just left
       interleave(std::integral_constant<int, 4 + NH>{}, std::integral_constant<int, S4>{});
+    }
     }
 
     // ---- partial tile: fp32 slab in fragment order + ticket; the last arriver reduces.
@@ -343,6 +464,14 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
     for (int j = 0; j < 4; ++j) {
       const int m = m0 + wm * 64 + j * 16 + fr;
       if (m >= M) continue;
+      if constexpr (Q == 1) {   // per-token x per-channel (W row) scales
+        const float srow = sa[m];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const f32x4 sv = *reinterpret_cast<const f32x4*>(sw + n0 + wn * WR + i * 16 + 4 * fc);
+          acc[i][j] *= sv * srow;
+        }
+      }
       if constexpr (EPI == SK_BF16) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
@@ -373,19 +502,21 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const bf16* __restrict
   }
 }
 
-template <int BM, int BN, int NBUF, int EPI>
-int launch_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const void* bias, void* out, int64_t ldo, int M,
-              int N, int K, int nwg, float* ws, int* cnt, hipStream_t stream) {
-  constexpr int LDS = NBUF * (BN + BM) * BK * 2;
+template <int BM, int BN, int NBUF, int EPI, int Q>
+int launch_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const float* sa, const float* sw,
+              const void* bias, void* out, int64_t ldo, int M, int N, int kt, int nwg, float* ws, int* cnt,
+              hipStream_t stream) {
+  constexpr int LDS = NBUF * ((BN + BM) * 128 + (Q == 2 ? BM * 4 + 512 : 0));
+  static_assert(LDS <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_sk_kernel<BM, BN, NBUF, EPI>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_sk_kernel<BM, BN, NBUF, EPI, Q>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  gemm_sk_kernel<BM, BN, NBUF, EPI><<<nwg, NTHR, LDS, stream>>>((const bf16*)X, ldx, (const bf16*)W, ldw,
-                                                           (const bf16*)bias, (bf16*)out, ldo, M, N, K, ws, cnt);
+  gemm_sk_kernel<BM, BN, NBUF, EPI, Q><<<nwg, NTHR, LDS, stream>>>((const char*)X, ldx, (const char*)W, ldw, sa, sw,
+                                                              (const bf16*)bias, (bf16*)out, ldo, M, N, kt, ws, cnt);
   return (int)hipGetLastError();
 }
 
@@ -411,13 +542,47 @@ OME_API int ome_gemm_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, 
   if (!ws || !cnt) return -5;
   float* w = (float*)ws;
   int* c = (int*)cnt;
-#define SK_GO(BMV, BNV, NB)                                                                                         \
-  return epi == SK_BF16                                                                                             \
-             ? launch_sk<BMV, BNV, NB, SK_BF16>(X, ldx, W, ldw, bias, out, ldo, M, N, K, nwg, w, c, stream)          \
-             : launch_sk<BMV, BNV, NB, SK_SILU>(X, ldx, W, ldw, bias, out, ldo, M, N, K, nwg, w, c, stream)
+#define SK_GO(BMV, BNV, NB)                                                                                     \
+  return epi == SK_BF16 ? launch_sk<BMV, BNV, NB, SK_BF16, 0>(X, ldx * 2, W, ldw * 2, nullptr, nullptr, bias, out, \
+                                                             ldo, M, N, K / BK, nwg, w, c, stream)                \
+                        : launch_sk<BMV, BNV, NB, SK_SILU, 0>(X, ldx * 2, W, ldw * 2, nullptr, nullptr, bias, out, \
+                                                             ldo, M, N, K / BK, nwg, w, c, stream)
   if (bm == 256 && bn == 256) SK_GO(256, 256, 2);
   if (bm == 256) SK_GO(256, 128, 3);
   if (bn == 256) SK_GO(128, 256, 3);
   SK_GO(128, 128, 4);
 #undef SK_GO
+}
+
+// FP8 W8A8: X [M][K] e4m3 (row stride ldx bytes), W [N][K] e4m3; block 0: sa [M] per token, sw [N]
+// per channel; block 128: sa [M][K/128], sw [N/128][K/128].  Tiles 128 x 128, 128 x 256 (per-channel
+// only) (K % 128 == 0); epi / nwg / ws / cnt as ome_gemm_sk (epi 2 needs sw in the interleaved row order).
+OME_API int ome_gemm_sk_fp8(const void* X, int64_t ldx, const float* sa, const void* W, int64_t ldw, const float* sw,
+                            int block, const void* bias, void* out, int64_t ldo, int M, int N, int K, int bm, int bn,
+                            int epi, int nwg, void* ws, void* cnt, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (bm != 128 || (bn != 128 && bn != 256) || N % bn || K % 128 ||
+      K <= 0 || nwg < 8 || nwg % 8 || nwg > 4096 || (block != 0 && block != 128))
+    return -2;
+  if (ldx % 16 || ldw % 16 || ((uintptr_t)X | (uintptr_t)W) % 16 || ldo % 4 || (uintptr_t)out % 8) return -3;
+  if ((uintptr_t)sw % 16 || !sa || !sw) return -3;
+  if (epi != SK_BF16 && epi != SK_SILU) return -4;
+  if (epi == SK_SILU && bias) return -4;
+  if (!ws || !cnt) return -5;
+  float* w = (float*)ws;
+  int* c = (int*)cnt;
+  const int kt = K / 128;
+#define SK8_Q(BMV, BNV, NB, QV)                                                                                      \
+  return epi == SK_BF16 ? launch_sk<BMV, BNV, NB, SK_BF16, QV>(X, ldx, W, ldw, sa, sw, bias, out, ldo, M, N, kt, nwg, \
+                                                               w, c, stream)                                          \
+                        : launch_sk<BMV, BNV, NB, SK_SILU, QV>(X, ldx, W, ldw, sa, sw, bias, out, ldo, M, N, kt, nwg, \
+                                                               w, c, stream)
+  // 256 x 128 and the block-scaled 128 x 256 spill at 256 VGPRs: not offered
+  if (bn == 256) {
+    if (block) return -2;
+    SK8_Q(128, 256, 3, 1);
+  }
+  if (block) SK8_Q(128, 128, 4, 2);
+  SK8_Q(128, 128, 4, 1);
+#undef SK8_Q
 }

@@ -270,6 +270,9 @@ def fp8_gemm(qa, sa, qw, sw, block: int = 0, bias=None, out: torch.Tensor | None
     assert qw.shape[1] == K and qa.is_contiguous() and qw.is_contiguous()
     if out is None:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=qa.device)
+    if M <= FP8_SK_MAX_ROWS and gemm_sk_fp8_ok(M, N, K, 128):
+        # decode rows: stream-K fp8 (csrc/kernels/gemm_sk.hip, Q = 1 / 2) -- every CU busy at any M
+        return gemm_sk_fp8(qa, sa, qw, sw, block, bias, out)
     if N % 256 == 0 and K % 128 == 0 and M >= FP8_MX_MIN_ROWS and -(-M // 256) * (N // 256) >= FP8_MX_MIN_TILES:
         # 256 x 256 MX-scaled MFMA tile (csrc/kernels/gemm.hip): twice the bf16 MFMA rate
         call("ome_fp8_gemm_mx", qa.data_ptr(), qa.stride(0), sa.data_ptr(), qw.data_ptr(), qw.stride(0),
@@ -280,6 +283,8 @@ def fp8_gemm(qa, sa, qw, sw, block: int = 0, bias=None, out: torch.Tensor | None
     return out
 
 
+# rows up to which the dense fp8 GEMM runs on the stream-K kernel (128 x 128 tiles)
+FP8_SK_MAX_ROWS = int(os.environ.get("OME_FP8_SK_MAX_ROWS", "512"))
 # rows from which the dense fp8 GEMM uses the 256 x 256 MX tile (smaller M: the 64 x 64 kernel)
 FP8_MX_MIN_ROWS = int(os.environ.get("OME_FP8_MX_MIN_ROWS", "65"))
 # ...and from this many 256 x 256 output tiles (profiles/r03_fp8_gemm_bench.txt: below ~128 tiles
@@ -945,6 +950,40 @@ def gemm_sk(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
     ws, cnt = _sk_workspace(x.device)
     call("ome_gemm_sk", x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ptr(bias), out.data_ptr(),
          out.stride(0), M, N, K, bm, bn, epi, nwg, ws.data_ptr(), cnt.data_ptr(), stream_ptr())
+    return out
+
+
+def gemm_sk_fp8_ok(M: int, N: int, K: int, bn: int = 128, nwg: int = 256) -> bool:
+    return bn in (128, 256) and N % bn == 0 and K % 128 == 0 and K > 0 and nwg % 8 == 0 and \
+        8 <= nwg <= _SK_MAX_WG and M > 0 and gemm_sk_tiles(M, N, bn, 128) <= _SK_CNT
+
+
+def gemm_sk_fp8(qa: torch.Tensor, sa: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0,
+                bias: torch.Tensor | None = None, out: torch.Tensor | None = None, epi: int = 0, bn: int = 128,
+                nwg: int = 256) -> torch.Tensor:
+    """W8A8 on the stream-K kernel: qa [M, K] / qw [N, K] e4m3; block 0: sa [M] (or [M, 1]) per token,
+    sw [N] per channel; block 128: sa [M, K/128], sw [N/128, K/128].  128-row tiles, ``bn`` 128 | 256
+    (256: per-channel only); ``epi=2`` as :func:`gemm_sk` (qw / sw rows interleaved)."""
+    M, K = qa.shape
+    N = qw.shape[0]
+    if not _gpu(qa):
+        y = ref.fp8_gemm(qa, sa, qw, sw, block, bias).float()
+        if epi == 2:
+            g, u = deinterleave_gate_up(y)
+            y = F.silu(g) * u
+        y = y.to(torch.bfloat16)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    assert qa.is_contiguous() and qw.stride(1) == 1 and sa.is_contiguous() and sw.is_contiguous()
+    assert sa.dtype == torch.float32 and sw.dtype == torch.float32 and (block == 0 or bn == 128)
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == 2 else N, dtype=torch.bfloat16, device=qa.device)
+    ws, cnt = _sk_workspace(qa.device)
+    call("ome_gemm_sk_fp8", qa.data_ptr(), qa.stride(0), sa.data_ptr(), qw.data_ptr(), qw.stride(0), sw.data_ptr(),
+         block, ptr(bias), out.data_ptr(), out.stride(0), M, N, K, 128, bn, epi, nwg, ws.data_ptr(), cnt.data_ptr(),
+         stream_ptr())
     return out
 
 

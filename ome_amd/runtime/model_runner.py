@@ -336,6 +336,7 @@ class ModelRunner:
         with torch.cuda.stream(stream), ops.decode_gemm_tuning():
             for bs in reversed(self.buckets):
                 self._decode_forward(bs)  # warm-up (allocations, hipBLASLt heuristics / tuning, GEMM routing)
+                log.info("decode warm-up bs=%d done at %.1fs", bs, time.perf_counter() - t0)
         torch.cuda.current_stream(self.device).wait_stream(stream)
         torch.cuda.synchronize(self.device)
         if tuning:

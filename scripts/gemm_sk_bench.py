@@ -20,7 +20,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ome_amd import ops  # noqa: E402
 
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
-          "lm_head": (128256, 4096)}
+          "lm_head": (128256, 4096),
+          # Llama-3-70B at TP = 1 (BASELINE config 3 on one 288 GB MI355X)
+          "qkv70": (10240, 8192), "o70": (8192, 8192), "gate_up70": (57344, 8192), "down70": (8192, 28672),
+          "lm_head70": (128256, 8192)}
 DEV = torch.device("cuda")
 
 
@@ -55,17 +58,18 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--table", default=None, help="write the ops.gemm_sk_plan table here")
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--merge", action="store_true", help="--table: update the existing table's shapes")
     a = ap.parse_args()
     ms = [int(v) for v in a.m.split(",")]
     table, plan = {}, {}
     for name in a.shapes.split(","):
         N, K = SHAPES[name]
-        epi = 2 if name == "gate_up" else 0
+        epi = 2 if name.startswith("gate_up") else 0
         n_w = max(2, -(-(600 << 20) // (N * K * 2)))
         ws = [torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5 for _ in range(n_w)]
         wi = [ops.interleave_gate_up(w) for w in ws] if epi == 2 else ws
         for M in ms:
-            if name == "lm_head" and M > 512:
+            if name.startswith("lm_head") and M > 512:
                 continue
             x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
             ref = F.linear(x, ws[0]).float()
@@ -105,6 +109,12 @@ def main():
         with open(a.json, "w") as f:
             json.dump(table, f, indent=1)
     if a.table:
+        if a.merge and os.path.exists(a.table):
+            with open(a.table) as f:
+                old = json.load(f).get("shapes", {})
+            for k, v in plan.items():
+                old.setdefault(k, {}).update(v)
+            plan = old
         with open(a.table, "w") as f:
             json.dump({"device": torch.cuda.get_device_name(), "method": "scripts/gemm_sk_bench.py, cold weights",
                        "shapes": plan}, f, indent=1)

@@ -135,3 +135,69 @@ def test_gemm_sk_more_blocks_than_units():
         for bm, bn in TILES:
             for nwg in (16, 64, 256):
                 assert _rel(ops.gemm_sk(x, w, bn=bn, nwg=nwg, bm=bm), _ref(x, w)) < 1e-2, (M, N, K, bm, bn, nwg)
+
+
+# ---------------------------------------------------------------- fp8 W8A8 (Q = 1 per-channel, Q = 2 block 128)
+def _fp8_case(M, N, K, block, seed):
+    from ome_amd.models.quant import quantize_weight
+
+    torch.manual_seed(seed)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5
+    qa, sa = ops.fp8_quant(x, block)
+    fw = quantize_weight(w, block)
+    ref = ops.reference.fp8_gemm(qa.cpu(), sa.cpu(), fw.q.cpu(), fw.scale.cpu(), block, out_dtype=torch.float32)
+    return qa, sa, fw.q, fw.scale, ref.to(DEV)
+
+
+@pytest.mark.parametrize("M", [1, 37, 128, 256, 300])
+@pytest.mark.parametrize("N,K", [(256, 128), (1024, 4096), (6144, 4096), (4096, 14336)])
+@pytest.mark.parametrize("block,bn", [(0, 128), (0, 256), (128, 128)])
+def test_gemm_sk_fp8(M, N, K, block, bn):
+    qa, sa, qw, sw, ref = _fp8_case(M, N, K, block, M + N + K + block + bn)
+    for nwg in (8, 64, 256):
+        if not ops.gemm_sk_fp8_ok(M, N, K, bn, nwg):
+            continue
+        y = ops.gemm_sk_fp8(qa, sa, qw, sw, block, bn=bn, nwg=nwg)
+        assert y.shape == (M, N) and y.dtype == torch.bfloat16
+        assert _rel(y, ref) < 1e-2, (nwg, _rel(y, ref))
+
+
+def test_gemm_sk_fp8_identity_block_scales():
+    """Selector activations with distinct per-(row, K-group) and per-(N-block, K-block) scales:
+    a scale applied to the wrong K-tile, row or W block changes exact small-integer results."""
+    M, N, K = 256, 512, 512
+    qa = torch.zeros(M, K, device=DEV)
+    qa[torch.arange(M), (torch.arange(M) * 7) % K] = 1
+    qa = qa.to(torch.float8_e4m3fn)
+    qw = ((torch.arange(N, device=DEV).view(N, 1) + 3 * torch.arange(K, device=DEV).view(1, K)) % 13 - 6).float()
+    qw = qw.to(torch.float8_e4m3fn)
+    sa = (2.0 ** (torch.arange(M * (K // 128), device=DEV) % 3)).float().view(M, K // 128)
+    sw = (2.0 ** -(torch.arange((N // 128) * (K // 128), device=DEV) % 4)).float().view(N // 128, K // 128)
+    ref = ops.reference.fp8_gemm(qa.cpu(), sa.cpu(), qw.cpu(), sw.cpu(), 128, out_dtype=torch.float32).to(DEV)
+    for nwg in (8, 16, 256):
+        assert torch.equal(ops.gemm_sk_fp8(qa, sa, qw, sw, 128, nwg=nwg).float(), ref), nwg
+
+
+@pytest.mark.parametrize("M", [1, 64, 256])
+def test_gemm_sk_fp8_silu_mul(M):
+    from ome_amd.models.quant import quantize_weight
+
+    I, H = 1792, 1024
+    torch.manual_seed(M)
+    x = torch.randn(M, H, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(2 * I, H, device=DEV, dtype=torch.bfloat16) / H ** 0.5
+    qa, sa = ops.fp8_quant(x, 0)
+    fw = quantize_weight(ops.interleave_gate_up(w), 0)
+    y = ops.gemm_sk_fp8(qa, sa, fw.q, fw.scale, 0, epi=2)
+    full = ops.reference.fp8_gemm(qa.cpu(), sa.cpu(), fw.q.cpu(), fw.scale.cpu(), 0, out_dtype=torch.float32)
+    g, u = ops.deinterleave_gate_up(full)
+    ref = (F.silu(g) * u).to(DEV)
+    assert y.shape == (M, I) and _rel(y, ref) < 1e-2
+
+
+def test_fp8_gemm_routes_decode_rows_to_stream_k():
+    """ops.fp8_gemm: decode-sized M goes to the stream-K kernel and matches the library-free reference."""
+    for block in (0, 128):
+        qa, sa, qw, sw, ref = _fp8_case(200, 2048, 1024, block, 5)
+        assert _rel(ops.fp8_gemm(qa, sa, qw, sw, block), ref) < 1e-2
