@@ -122,6 +122,9 @@ class Engine:
         self._remote: dict[str, Request] = {}   # DP attention, rank 0: requests served by other ranks
         self._remote_h: dict[int, Request] = {}  # ... by the integer handle all ranks agree on
         self._dp_seq = 0
+        self._dp_pending: list[float] = []   # this rank's token updates awaiting the next relay
+        # relay capacity: one token (+ header and log-prob) per running request, in float64s
+        self._dp_cap = 8 + 6 * (args.max_running_requests + 1)
         self._dp_next = 0
         device = args.device
         if device == "cuda" and torch.cuda.is_available():
@@ -387,75 +390,69 @@ class Engine:
     def _dp_step(self) -> list[Request]:
         """DP attention: every rank schedules its own requests, all ranks run the forward in
         lockstep (a rank without work runs one dummy token so the MoE all-to-alls are complete),
-        and the followers report their new tokens to rank 0, which owns the HTTP streams."""
+        and the followers report their new tokens to rank 0, which owns the HTTP streams.
+
+        ONE CPU collective per step (besides the leader's control header): a fixed-capacity
+        all-gather of [this step's token count, payload length, the PREVIOUS step's packed token
+        updates].  Every rank learns every batch size (same MoE exchange mode everywhere) and rank
+        0 receives the relayed tokens, one step after they were sampled.  The capacity covers one
+        token per running request; a larger payload (never in steady state) falls back to a
+        sizes all-gather + gather for that step, decided identically on every rank."""
         import torch.distributed as dist
 
         batch = self.scheduler.schedule()
-        mine = torch.tensor([0 if batch is None else sum(c.length for c in batch.chunks)], dtype=torch.int64)
-        allw = [torch.zeros(1, dtype=torch.int64) for _ in range(self.pstate.world_size)]
-        dist.all_gather(allw, mine, group=self._cpu_group())
-        if not any(int(w) for w in allw):
-            return []
+        n_tok = 0 if batch is None else sum(c.length for c in batch.chunks)
+        pend = self._dp_pending
+        self._dp_pending = []
+        cap = self._dp_cap
+        over = len(pend) > cap - 2
+        buf = torch.zeros(cap, dtype=torch.float64)
+        buf[0] = n_tok
+        buf[1] = -1.0 if over else len(pend)
+        if pend and not over:
+            buf[2:2 + len(pend)] = torch.tensor(pend, dtype=torch.float64)
+        bufs = [torch.empty(cap, dtype=torch.float64) for _ in range(self.pstate.world_size)]
+        dist.all_gather(bufs, buf, group=self._cpu_group())
+        allw = [int(b[0]) for b in bufs]
+        done: list[Request] = []
+        if any(int(b[1]) < 0 for b in bufs):   # overflow somewhere: two-phase exchange, all ranks
+            payloads = self._dp_gather_updates(pend if over else [])
+            bufs = [torch.cat([torch.tensor([0.0, float(len(pl))], dtype=torch.float64), pl]) for pl in payloads]
+        if self.pstate.rank == 0:
+            done += self._dp_apply_updates(bufs)
+        if not any(allw):
+            return done
         # every rank sees the same token counts, so all pick the same MoE exchange mode: the
         # device-only low-latency buckets when every rank's batch fits, RCCL all-to-all otherwise
         st = self.pstate
-        st.ep_ll_ok = st.ep_ll is not None and max(int(w) for w in allw) <= st.ep_ll_cap
-        done: list[Request] = []
+        st.ep_ll_ok = st.ep_ll is not None and max(allw) <= st.ep_ll_cap
         touched = []
         if batch is not None:
             t0 = time.perf_counter()
             handle = self.runner.launch(batch, allow_graph=st.ep_ll_ok)
             self.scheduler.launch_commit(batch)
-            done = self._complete(batch, handle, t0)
+            done += self._complete(batch, handle, t0)
             touched = list({id(c.req): c.req for c in batch.chunks}.values())
         elif st.ep_ll_ok:
             self.runner.idle_decode()
         else:
             self.runner.idle_forward()
-        # token updates of the followers' requests -> rank 0 (which owns every HTTP stream) as ONE
-        # float64 tensor per rank (no pickling): [n_updates, then per update handle, n_tokens,
-        # finished, reason code, and the tokens; then all log-probs]; sizes first, then a gather
-        packed: list[float] = [0.0]
-        lps_all: list[float] = []
-        for r in touched:
-            k = getattr(r, "_reported", 0)
-            toks = r.output_ids[k:]
-            fin = r.state == ReqState.FINISHED
-            packed += [float(getattr(r, "dp_handle", -1)), float(len(toks)), float(fin),
-                       float(_REASON_CODE.get(r.finish_reason, _unknown_code(r.finish_reason)) if fin else -1)]
-            packed += [float(t) for t in toks]
-            lps_all += [float(x) for x in r.output_logprobs[k:]]
-            r._reported = len(r.output_ids)
-            packed[0] += 1
-        mine = torch.tensor(packed + lps_all, dtype=torch.float64)
-        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.pstate.world_size)]
-        dist.all_gather(sizes, torch.tensor([mine.numel()], dtype=torch.int64), group=self._cpu_group())
-        cap = max(int(x) for x in sizes)
-        buf = torch.zeros(cap, dtype=torch.float64)
-        buf[:mine.numel()] = mine
-        bufs = [torch.zeros(cap, dtype=torch.float64) for _ in range(self.pstate.world_size)] \
-            if self.pstate.rank == 0 else None
-        dist.gather(buf, bufs, dst=self.pstate.to_global(0), group=self._cpu_group())
-        if self.pstate.rank == 0:
-            now = time.perf_counter()
-            for b in bufs[1:]:
-                for handle, toks, lps, fin, reason in _unpack_updates(b.tolist()):
-                    p = self._remote_h.get(handle)
-                    if p is None:
-                        continue
-                    rid = p.rid
-                    if toks and p.first_token_time is None:
-                        p.first_token_time = now
-                    p.output_ids.extend(toks)
-                    p.output_logprobs.extend(lps)
-                    p.token_times.extend([now] * len(toks))
-                    if fin:
-                        p.state, p.finish_reason = ReqState.FINISHED, reason
-                        self._remote.pop(rid, None)
-                        self._remote_h.pop(handle, None)
-                        done.append(p)
-                    if p.on_token is not None and (toks or fin):
-                        p.on_token(p, list(toks), fin)
+        if self.pstate.rank != 0 and touched:
+            # [n_updates, then per update handle, n_tokens, finished, reason code, and the tokens;
+            # then all log-probs] -- relayed with the next step's all-gather
+            packed: list[float] = [0.0]
+            lps_all: list[float] = []
+            for r in touched:
+                k = getattr(r, "_reported", 0)
+                toks = r.output_ids[k:]
+                fin = r.state == ReqState.FINISHED
+                packed += [float(getattr(r, "dp_handle", -1)), float(len(toks)), float(fin),
+                           float(_REASON_CODE.get(r.finish_reason, _unknown_code(r.finish_reason)) if fin else -1)]
+                packed += [float(t) for t in toks]
+                lps_all += [float(x) for x in r.output_logprobs[k:]]
+                r._reported = len(r.output_ids)
+                packed[0] += 1
+            self._dp_pending = packed + lps_all
         self._dp_steps = getattr(self, "_dp_steps", 0) + 1
         n = self.args.eplb_rebalance_steps
         if n and self._dp_steps % n == 0:  # every rank reaches this point in the same lockstep step
@@ -464,6 +461,50 @@ class Engine:
             imb = rebalance_model(self.runner.model)
             if imb:
                 log.info("EPLB round: max/mean expert load per rank %.3f", max(imb.values()))
+        return done
+
+    def _dp_gather_updates(self, mine_list: list[float]) -> list[torch.Tensor]:
+        """Two-phase fallback of the update relay (sizes all-gather, then a padded gather to rank
+        0); returns every rank's payload on rank 0 (empty tensors elsewhere)."""
+        import torch.distributed as dist
+
+        mine = torch.tensor(mine_list, dtype=torch.float64)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(self.pstate.world_size)]
+        dist.all_gather(sizes, torch.tensor([mine.numel()], dtype=torch.int64), group=self._cpu_group())
+        cap = max(1, max(int(x) for x in sizes))
+        buf = torch.zeros(cap, dtype=torch.float64)
+        buf[:mine.numel()] = mine
+        bufs = [torch.zeros(cap, dtype=torch.float64) for _ in range(self.pstate.world_size)] \
+            if self.pstate.rank == 0 else None
+        dist.gather(buf, bufs, dst=self.pstate.to_global(0), group=self._cpu_group())
+        if self.pstate.rank != 0:
+            return [torch.zeros(0, dtype=torch.float64)] * self.pstate.world_size
+        return [b[:int(n)] for b, n in zip(bufs, sizes)]
+
+    def _dp_apply_updates(self, bufs) -> list[Request]:
+        """Rank 0: apply the followers' relayed token updates to the proxy requests."""
+        done: list[Request] = []
+        now = time.perf_counter()
+        for b in bufs[1:]:
+            n = int(b[1])
+            if n <= 0:
+                continue
+            for handle, toks, lps, fin, reason in _unpack_updates(b[2:2 + n].tolist()):
+                p = self._remote_h.get(handle)
+                if p is None:
+                    continue
+                if toks and p.first_token_time is None:
+                    p.first_token_time = now
+                p.output_ids.extend(toks)
+                p.output_logprobs.extend(lps)
+                p.token_times.extend([now] * len(toks))
+                if fin:
+                    p.state, p.finish_reason = ReqState.FINISHED, reason
+                    self._remote.pop(p.rid, None)
+                    self._remote_h.pop(handle, None)
+                    done.append(p)
+                if p.on_token is not None and (toks or fin):
+                    p.on_token(p, list(toks), fin)
         return done
 
     def flush(self) -> list[Request]:

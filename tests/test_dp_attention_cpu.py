@@ -19,13 +19,15 @@ from tests.test_moe_cpu import _export_hf
 PROMPTS = [[3 + (i * 37 + j) % 1000 for j in range(5 + 7 * i)] for i in range(5)]
 
 
-def _worker(rank, world, port, path, q):
+def _worker(rank, world, port, path, q, relay_cap=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     from ome_amd.runtime.engine import Engine, EngineArgs
     from ome_amd.runtime.request import SamplingParams
 
     eng = Engine(EngineArgs(model_path=path, tp_size=world, dp_size=world, enable_dp_attention=True, device="cpu",
                             max_running_requests=8, context_length=256, dtype="float32"))
+    if relay_cap is not None:   # force the two-phase relay fallback on every step
+        eng._dp_cap = relay_cap
     m = eng.runner.model
     assert m.E_local == m.E // world and m.e0 == rank * m.E_local
     if rank == 0:
@@ -50,8 +52,8 @@ def _checkpoint(tmp_path, kind):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("kind", ["qwen3-moe", "deepseek-v3"])
-def test_dp_attention_ep_matches_single(tmp_path, kind):
+@pytest.mark.parametrize("kind,relay_cap", [("qwen3-moe", None), ("deepseek-v3", None), ("qwen3-moe", 3)])
+def test_dp_attention_ep_matches_single(tmp_path, kind, relay_cap):
     _checkpoint(tmp_path, kind)
     from ome_amd.runtime.engine import Engine, EngineArgs
     from ome_amd.runtime.request import SamplingParams
@@ -64,7 +66,7 @@ def test_dp_attention_ep_matches_single(tmp_path, kind):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q, relay_cap)) for r in range(2)]
     for p in ps:
         p.start()
     got, owners = q.get(timeout=300)
