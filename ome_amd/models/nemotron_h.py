@@ -21,9 +21,15 @@ Recurrent state lives per request slot (the row of the page-table pool, ``Reques
 conv state [slots, conv_dim, K-1] (model dtype) and SSM state [slots, H, P, N] (fp32) per Mamba
 layer; a sequence's first prefill chunk starts from zeros (``reset``), later chunks and decode
 rows continue.  The prefix cache is disabled for this family (a prefix's SSM state is not paged).
-HIP-graph decode captures the same kernels with one-row sequences.  Tensor parallelism is not
-implemented for this family (tp must be 1).  The dt clamp ``time_step_min`` is applied on every
-row (HF clamps in its chunked prefill path only).
+HIP-graph decode captures the same kernels with one-row sequences.  The dt clamp
+``time_step_min`` is applied on every row (HF clamps in its chunked prefill path only).
+
+Tensor parallelism: a Mamba-2 mixer splits by SSM heads in whole B/C groups (rank r owns heads
+[r*H/tp, (r+1)*H/tp) and groups [r*G/tp, ...): its z / x / B / C / dt rows of in_proj, those conv
+channels, A / D / dt_bias, the gated-norm weight slice and out_proj's columns), so the scan needs
+no exchange; attention splits by heads, the ReLU^2 MLP / experts / shared expert by intermediate
+dim (router and latent projections replicated).  Every mixer's output is a row-parallel partial
+sum, all-reduced with the next residual add + RMSNorm.
 """
 from __future__ import annotations
 
@@ -58,22 +64,27 @@ class NemotronHForCausalLM(LlamaForCausalLM):
 
     def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
         super().__init__(cfg, device, dtype, max_positions)
-        if self.tp.tp > 1 or pstate.get().pp_size > 1:
-            raise NotImplementedError("NemotronH runs on one GPU per replica (no TP / PP yet)")
+        if pstate.get().pp_size > 1:
+            raise NotImplementedError("NemotronH: pipeline parallelism (TP is supported)")
         hf = cfg.extra or {}
         self.types = layer_types(hf)
         self.kv_layers = [i for i in self.layers if self.types[i] == "full_attention"]
         self.mamba_layers = [i for i in self.layers if self.types[i] == "linear_attention"]
         self.mi = {i: k for k, i in enumerate(self.mamba_layers)}
-        self.H = int(hf.get("mamba_num_heads", 128))
+        ntp = self.tp.tp
+        self.H_full = int(hf.get("mamba_num_heads", 128))
         self.P = int(hf.get("mamba_head_dim", 64))
         self.N = int(hf.get("ssm_state_size", 128))
-        self.G = int(hf.get("n_groups", 8))
+        self.G_full = int(hf.get("n_groups", 8))
         self.K = int(hf.get("conv_kernel", 4))
+        if self.H_full % ntp or self.G_full % ntp:
+            raise ValueError(f"NemotronH: {self.H_full} SSM heads / {self.G_full} groups do not split over TP={ntp}")
+        self.H, self.G = self.H_full // ntp, self.G_full // ntp   # this rank's heads / groups
         self.I = self.H * self.P
         self.conv_dim = self.I + 2 * self.G * self.N
         self.dt_min = float(hf.get("time_step_min", 0.001) or 0.0)
-        self.inter = int(hf.get("intermediate_size", cfg.intermediate_size))
+        self.inter_full = int(hf.get("intermediate_size", cfg.intermediate_size))
+        self.inter = self._split(self.inter_full, "intermediate_size")
         self.mlp_act = {"relu2": 4, "silu": 0, "gelu": 3}[hf.get("mlp_hidden_act", "relu2")]
         L = cfg.num_layers
         self.w_in: list[torch.Tensor | None] = [None] * L
@@ -89,8 +100,9 @@ class NemotronHForCausalLM(LlamaForCausalLM):
         # MoE blocks
         self.E = int(hf.get("n_routed_experts") or hf.get("num_local_experts") or 0)
         self.topk = int(hf.get("num_experts_per_tok", 2))
-        self.moe_I = int(hf.get("moe_intermediate_size", 0) or 0)
-        self.shared_I = int(hf.get("moe_shared_expert_intermediate_size", 0) or 0)
+        self.moe_I = self._split(int(hf.get("moe_intermediate_size", 0) or 0), "moe_intermediate_size")
+        self.shared_I = self._split(int(hf.get("moe_shared_expert_intermediate_size", 0) or 0),
+                                    "moe_shared_expert_intermediate_size")
         self.latent = int(hf.get("moe_latent_size") or 0)
         self.n_group = int(hf.get("n_group", 1) or 1)
         self.topk_group = int(hf.get("topk_group", 1) or 1)
@@ -104,6 +116,22 @@ class NemotronHForCausalLM(LlamaForCausalLM):
         self.w_sd: list[torch.Tensor | None] = [None] * L
         self.w_l1: list[torch.Tensor | None] = [None] * L          # latent in / out projections
         self.w_l2: list[torch.Tensor | None] = [None] * L
+
+    def _split(self, n: int, what: str) -> int:
+        if n % self.tp.tp:
+            raise ValueError(f"NemotronH: {what}={n} does not split over TP={self.tp.tp}")
+        return n // self.tp.tp
+
+    def _mamba_slices(self):
+        """(in_proj row index, conv channel index, head slice, inner slice) of this rank."""
+        r, I, H, G, N = self.tp.rank, self.I, self.H, self.G, self.N
+        If, GNf = self.H_full * self.P, self.G_full * self.N
+        ar = torch.arange
+        xs = ar(r * I, (r + 1) * I)
+        bs, cs = ar(r * G * N, (r + 1) * G * N), ar(r * G * N, (r + 1) * G * N)
+        conv = torch.cat([xs, If + bs, If + GNf + cs])
+        rows = torch.cat([xs, If + conv, 2 * If + 2 * GNf + ar(r * H, (r + 1) * H)])
+        return rows, conv, slice(r * H, (r + 1) * H), slice(r * I, (r + 1) * I)
 
     def alloc_state(self, slots: int) -> None:
         nm = len(self.mamba_layers)
@@ -155,6 +183,13 @@ class NemotronHForCausalLM(LlamaForCausalLM):
         def put(t, dtype=None):
             return t.to(device=self.device, dtype=dtype or self.dtype).contiguous()
 
+        tp, D = self.tp, self.D
+        rows_in, conv_ch, hs, isl = self._mamba_slices()
+        r = tp.rank
+
+        def part(t, n, dim):   # this rank's n-wide block of dim
+            return t.narrow(dim, r * n, n) if tp.tp > 1 else t
+
         qkv: dict[int, dict[str, torch.Tensor]] = {}
         experts: dict[int, dict[tuple[int, str], torch.Tensor]] = {}
         for name, w in weights:
@@ -180,51 +215,51 @@ class NemotronHForCausalLM(LlamaForCausalLM):
             if sub == "norm.weight":
                 self.ln1[i] = put(w)
             elif sub == "mixer.in_proj.weight":
-                self.w_in[i] = put(w)
+                self.w_in[i] = put(w[rows_in.to(w.device)])
             elif sub == "mixer.conv1d.weight":
-                self.conv_w[i] = put(w.reshape(w.shape[0], -1))
+                self.conv_w[i] = put(w.reshape(w.shape[0], -1)[conv_ch.to(w.device)])
             elif sub == "mixer.conv1d.bias":
-                self.conv_b[i] = put(w)
+                self.conv_b[i] = put(w[conv_ch.to(w.device)])
             elif sub == "mixer.A_log":
-                self.A[i] = -torch.exp(w.float()).to(self.device)
+                self.A[i] = -torch.exp(w[hs].float()).to(self.device)
             elif sub == "mixer.D":
-                self.Dp[i] = put(w, torch.float32)
+                self.Dp[i] = put(w[hs], torch.float32)
             elif sub == "mixer.dt_bias":
-                self.dt_bias[i] = put(w, torch.float32)
+                self.dt_bias[i] = put(w[hs], torch.float32)
             elif sub == "mixer.norm.weight":
-                self.gnorm[i] = put(w)
+                self.gnorm[i] = put(w[isl])
             elif sub == "mixer.out_proj.weight":
-                self.w_out[i] = put(w)
+                self.w_out[i] = put(w[:, isl])
             elif sub in ("mixer.q_proj.weight", "mixer.k_proj.weight", "mixer.v_proj.weight"):
                 qkv.setdefault(i, {})[sub[6]] = w
             elif sub == "mixer.o_proj.weight":
-                self.w_o[i] = put(w)
+                self.w_o[i] = put(part(w, tp.hq * D, 1))
             elif sub == "mixer.up_proj.weight":
-                self.w_gu[i] = put(w)
+                self.w_gu[i] = put(part(w, self.inter, 0))
             elif sub == "mixer.down_proj.weight":
-                self.w_d[i] = put(w)
+                self.w_d[i] = put(part(w, self.inter, 1))
             elif sub == "mixer.gate.weight":
                 self.w_router[i] = put(w, torch.float32)
             elif sub == "mixer.gate.e_score_correction_bias":
                 self.e_bias[i] = put(w, torch.float32)
             elif sub == "mixer.experts.up_proj":             # fused [E, I, H']
-                self.w_eu[i] = put(w)
+                self.w_eu[i] = put(part(w, self.moe_I, 1))
             elif sub == "mixer.experts.down_proj":
-                self.w_ed[i] = put(w)
+                self.w_ed[i] = put(part(w, self.moe_I, 2))
             elif sub.startswith("mixer.experts.") and sub.endswith(".weight"):   # per expert
                 e, kind = int(sub.split(".")[2]), sub.split(".")[3]
                 experts.setdefault(i, {})[(e, kind)] = w
             elif sub == "mixer.shared_experts.up_proj.weight":
-                self.w_su[i] = put(w)
+                self.w_su[i] = put(part(w, self.shared_I, 0))
             elif sub == "mixer.shared_experts.down_proj.weight":
-                self.w_sd[i] = put(w)
+                self.w_sd[i] = put(part(w, self.shared_I, 1))
             elif sub == "mixer.fc1_latent_proj.weight":
                 self.w_l1[i] = put(w)
             elif sub == "mixer.fc2_latent_proj.weight":
                 self.w_l2[i] = put(w)
         for i, d in experts.items():
-            self.w_eu[i] = put(torch.stack([d[(e, "up_proj")] for e in range(self.E)]))
-            self.w_ed[i] = put(torch.stack([d[(e, "down_proj")] for e in range(self.E)]))
+            self.w_eu[i] = put(torch.stack([part(d[(e, "up_proj")], self.moe_I, 0) for e in range(self.E)]))
+            self.w_ed[i] = put(torch.stack([part(d[(e, "down_proj")], self.moe_I, 1) for e in range(self.E)]))
         for i in self.layers:
             if self.types[i] == "moe":
                 if self.e_bias[i] is None:
@@ -232,7 +267,8 @@ class NemotronHForCausalLM(LlamaForCausalLM):
                 if self.w_router[i] is None or self.w_eu[i] is None or self.w_ed[i] is None:
                     raise ValueError(f"layer {i}: incomplete MoE weights")
         for i, d in qkv.items():
-            self.w_qkv[i] = put(torch.cat([d["q"], d["k"], d["v"]], 0))
+            kv = slice(tp.kv_start * D, (tp.kv_start + tp.hkv) * D)
+            self.w_qkv[i] = put(torch.cat([d["q"][r * tp.hq * D:(r + 1) * tp.hq * D], d["k"][kv], d["v"][kv]], 0))
         if self.lm_head is None:
             self.lm_head = self.embed
         return self
@@ -277,8 +313,8 @@ class NemotronHForCausalLM(LlamaForCausalLM):
         seqs = meta.extra["ssm"]
         x, residual = self._stage_input(ids, input_embeds)
         for i in self.layers:
-            if i > 0:
-                ops.fused_add_rmsnorm(x, residual, self.ln1[i], self.eps)
+            if i > 0:   # the previous mixer's partial sums: TP all-reduce + residual add + norm
+                x = self._reduce_add_norm(x, residual, self.ln1[i])
             t = self.types[i]
             if t == "linear_attention":
                 x = self.mamba(i, x, seqs)
@@ -295,4 +331,6 @@ class NemotronHForCausalLM(LlamaForCausalLM):
                 x = self.moe(i, x)
             else:
                 x = linear(ops.act(linear(x, self.w_gu[i]), self.mlp_act), self.w_d[i])
+        if self.layers and tp.tp > 1:
+            x = pstate.tp_all_reduce(x)
         return self._stage_output(x, residual)

@@ -21,8 +21,14 @@ grouped-GEMM experts, a shared expert scaled by ``sigmoid(shared_expert_gate(x))
 Only the attention layers own KV pages (``kv_layers``); recurrent state lives per request slot
 (``alloc_state``: conv [n_lin, slots, conv_dim, K-1] in the model dtype, delta-rule state
 [n_lin, slots, Hv, dv, dk] fp32, transposed -- ~2 MiB per layer-slot at the 80B shape, sized
-before the KV pool).  The prefix cache is off for stateful models.  One GPU per replica: 80B bf16 weights
-(~160 GB) fit one MI355X, so TP / PP are not implemented for this family.
+before the KV pool).  The prefix cache is off for stateful models.
+
+Tensor parallelism: the Gated-DeltaNet layers split by key-head groups (rank r owns k-heads
+[r*Hk/tp, (r+1)*Hk/tp) and the v-heads of those groups -- the q / k / v / z / b / a rows, the
+conv channels, A_log / dt_bias and out_proj's columns), so the recurrence needs no exchange; the
+gated attention splits by query heads as the Llama base does, the MoE by experts' intermediate
+dim (``moe.py``); each mixer's out projection is row-parallel and all-reduced with the residual
+add + RMSNorm.  80B bf16 (~160 GB) also fits one MI355X, where TP=1 is the default.
 """
 from __future__ import annotations
 
@@ -53,18 +59,23 @@ class Qwen3NextForCausalLM(MoEForCausalLM):
 
     def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
         super().__init__(cfg, device, dtype, max_positions)
-        if self.tp.tp > 1 or pstate.get().pp_size > 1:
-            raise NotImplementedError("Qwen3-Next runs on one GPU per replica (no TP / PP yet)")
+        if pstate.get().pp_size > 1:
+            raise NotImplementedError("Qwen3-Next: pipeline parallelism (TP is supported)")
         hf = cfg.extra or {}
         self.types = layer_types(hf, cfg.num_layers)
         self.kv_layers = [i for i in self.layers if self.types[i] == "full_attention"]
         self.lin_layers = [i for i in self.layers if self.types[i] == "linear_attention"]
         self.li = {i: k for k, i in enumerate(self.lin_layers)}
-        self.Hk = int(hf.get("linear_num_key_heads", 16))
-        self.Hv = int(hf.get("linear_num_value_heads", 32))
+        self.Hk_full = int(hf.get("linear_num_key_heads", 16))
+        self.Hv_full = int(hf.get("linear_num_value_heads", 32))
         self.dk = int(hf.get("linear_key_head_dim", 128))
         self.dv = int(hf.get("linear_value_head_dim", 128))
         self.K = int(hf.get("linear_conv_kernel_dim", 4))
+        ntp, r = self.tp.tp, self.tp.rank
+        if self.Hk_full % ntp:
+            raise ValueError(f"Qwen3-Next: {self.Hk_full} linear-attention key heads do not split over TP={ntp}")
+        self.Hk, self.Hv = self.Hk_full // ntp, self.Hv_full // ntp   # this rank's heads
+        self.hk0 = r * self.Hk
         self.kd, self.vd = self.Hk * self.dk, self.Hv * self.dv
         self.conv_dim = 2 * self.kd + self.vd
         step = int(hf.get("decoder_sparse_step", 1) or 1)
@@ -111,16 +122,17 @@ class Qwen3NextForCausalLM(MoEForCausalLM):
         return self
 
     def _qkvz_order(self) -> tuple[torch.Tensor, torch.Tensor]:
-        """Row permutations: HF's per-k-head groups [q k v z] / [b a] -> [all q | all k | all v | all z]
-        and [all b | all a]."""
+        """Row gathers: HF's per-k-head groups [q k v z] / [b a] -> [all q | all k | all v | all z]
+        and [all b | all a], over this rank's k-head groups only."""
         Hk, dk, dv, r = self.Hk, self.dk, self.dv, self.Hv // self.Hk
         g = 2 * dk + 2 * r * dv
-        base = torch.arange(Hk)[:, None] * g
+        heads = self.hk0 + torch.arange(Hk)
+        base = heads[:, None] * g
         q = (base + torch.arange(dk)).reshape(-1)
         k = (base + dk + torch.arange(dk)).reshape(-1)
         v = (base + 2 * dk + torch.arange(r * dv)).reshape(-1)
         z = (base + 2 * dk + r * dv + torch.arange(r * dv)).reshape(-1)
-        gb = torch.arange(Hk)[:, None] * (2 * r)
+        gb = heads[:, None] * (2 * r)
         b = (gb + torch.arange(r)).reshape(-1)
         a = (gb + r + torch.arange(r)).reshape(-1)
         return torch.cat([q, k, v, z]), torch.cat([b, a])
@@ -177,17 +189,24 @@ class Qwen3NextForCausalLM(MoEForCausalLM):
                     raise ValueError(f"layer {i}: missing linear_attn weights {miss}")
                 qkvz, ba = d["in_proj_qkvz.weight"], d["in_proj_ba.weight"]
                 self.w_lin[i] = put(torch.cat([qkvz[pq.to(qkvz.device)], ba[pb.to(ba.device)]], 0))
-                self.conv_w[i] = put(d["conv1d.weight"].reshape(self.conv_dim, -1))
-                self.A_log[i] = put(d["A_log"], torch.float32)
-                self.dt_bias[i] = put(d["dt_bias"], torch.float32)
+                kdf = self.Hk_full * self.dk
+                cw = d["conv1d.weight"].reshape(2 * kdf + self.Hv_full * self.dv, -1)   # [q | k | v] channels
+                k0, v0 = self.hk0 * self.dk, self.hk0 * (self.Hv // self.Hk) * self.dv
+                self.conv_w[i] = put(torch.cat([cw[k0:k0 + self.kd], cw[kdf + k0:kdf + k0 + self.kd],
+                                                cw[2 * kdf + v0:2 * kdf + v0 + self.vd]], 0))
+                h0 = v0 // self.dv
+                self.A_log[i] = put(d["A_log"][h0:h0 + self.Hv], torch.float32)
+                self.dt_bias[i] = put(d["dt_bias"][h0:h0 + self.Hv], torch.float32)
                 self.gnorm[i] = put(d["norm.weight"])
-                self.w_out[i] = put(d["out_proj.weight"])
+                self.w_out[i] = put(d["out_proj.weight"][:, v0:v0 + self.vd])
             else:
                 d = attn.get(i, {})
                 if len(d) != 3:
                     raise ValueError(f"layer {i}: missing attention projections")
-                qg = d["q"].reshape(hq, 2, D, -1)
-                self.w_qkv[i] = put(torch.cat([qg[:, 0].reshape(hq * D, -1), d["k"], d["v"],
+                tp = self.tp
+                qg = d["q"].reshape(-1, 2, D, d["q"].shape[-1])[tp.rank * hq:(tp.rank + 1) * hq]
+                kv = slice(tp.kv_start * D, (tp.kv_start + tp.hkv) * D)
+                self.w_qkv[i] = put(torch.cat([qg[:, 0].reshape(hq * D, -1), d["k"][kv], d["v"][kv],
                                                qg[:, 1].reshape(hq * D, -1)], 0))
         return self
 
@@ -208,7 +227,7 @@ class Qwen3NextForCausalLM(MoEForCausalLM):
                          p[:, cd + vd:cd + vd + Hv], self.A_log[i], self.dt_bias[i], self.rec_state[j], cu, slot,
                          reset, Hv, self.Hk)
         o = ops.gated_rmsnorm(o, p[:, cd:cd + vd], self.gnorm[i], self.dv, self.eps, norm_first=True)
-        return linear(o, self.w_out[i])
+        return self._row_parallel(o, self.w_out[i])   # partial sums under TP
 
     def gated_attention(self, i: int, x: torch.Tensor, meta: AttnMeta, kv: PagedKVCache) -> torch.Tensor:
         tp, D, T = self.tp, self.D, x.shape[0]
@@ -220,7 +239,7 @@ class Qwen3NextForCausalLM(MoEForCausalLM):
                            tp.hq, tp.hkv, D, True, self.qn[i], self.kn[i], self.eps, ks, vs)
         a = self.attention(q, k_cache, v_cache, meta, ks, vs).view(T, tp.hq * D)
         a = a * torch.sigmoid(p[:, (tp.hq + 2 * tp.hkv) * D:])
-        return linear(a, self.w_o[i])
+        return self._row_parallel(a, self.w_o[i])
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: PagedKVCache,
                 input_embeds: torch.Tensor | None = None) -> torch.Tensor:
@@ -233,6 +252,6 @@ class Qwen3NextForCausalLM(MoEForCausalLM):
                 o = self.gated_delta(i, x, seqs)
             else:
                 o = self.gated_attention(i, x, meta, kv)
-            ops.fused_add_rmsnorm(o, residual, self.ln2[i], self.eps)
+            o = self._reduce_add_norm(o, residual, self.ln2[i])   # TP all-reduce + add + norm
             x = self.mlp(i, o)
         return self._stage_output(x, residual)
