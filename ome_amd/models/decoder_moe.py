@@ -10,7 +10,8 @@ selection only, optional renormalisation -- this one kernel covers all five rout
 ``ome_moe_align`` -> grouped MFMA GEMM gate_up -> SiLU*mul -> grouped MFMA GEMM down ->
 ``ome_moe_combine``, plus an optional always-on shared expert (ERNIE).  Experts are tensor-parallel
 over the intermediate dimension, so the block output is one partial sum and the decoder's
-single TP all-reduce per block still applies.
+single TP all-reduce per block still applies; under DP attention they are expert-parallel
+instead (rank r owns experts [r*E/ep, (r+1)*E/ep), tokens by all-to-all, ``parallel/ep.py``).
 
 Checkpoint expert layouts accepted: per expert (``experts.<e>.{gate,up,down}_proj`` / ``w1,w3,w2``),
 fused per layer (``experts.gate_up_proj`` [E, 2I, H] + ``experts.down_proj`` [E, H, I]),
@@ -65,8 +66,11 @@ class DecoderMoEForCausalLM(DecoderForCausalLM):
     def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
         super().__init__(cfg, device, dtype, max_positions)
         st, tp, hf, arch = pstate.get(), self.tp, cfg.extra or {}, cfg.architecture
-        if st.ep_size > 1:
-            raise NotImplementedError(f"expert parallelism for {arch} (experts are tensor-parallel here)")
+        self.ep = st.ep_size
+        if cfg.num_experts % self.ep:
+            raise ValueError(f"{cfg.num_experts} experts do not split over ep={self.ep}")
+        self.E_local = cfg.num_experts // self.ep
+        self.e0 = st.ep_rank * self.E_local if self.ep > 1 else 0
         self.spec.names = list(self.spec.names) + _moe_names(arch)
         self.E, self.k = cfg.num_experts, cfg.num_experts_per_tok
         self.scoring = "sigmoid" if arch == "MiniMaxM2ForCausalLM" else "softmax"
@@ -95,13 +99,13 @@ class DecoderMoEForCausalLM(DecoderForCausalLM):
         super().init_random(seed, std)
         gen = torch.Generator(device=self.device)
         gen.manual_seed(seed + 104729 + 7919 * pstate.get().tp_rank)
-        H, I, E = self.cfg.hidden_size, self.moe_inter, self.E
+        H, I, E = self.cfg.hidden_size, self.moe_inter, self.E_local
         for i in self.moe_layers:
-            self.w_router[i] = self._alloc(E, H, std=std, gen=gen)
+            self.w_router[i] = self._alloc(self.E, H, std=std, gen=gen)
             self.w13[i] = self._alloc(E, 2 * I, H, std=std, gen=gen)
             self.w2[i] = self._alloc(E, H, I, std=std / math.sqrt(2 * self.cfg.num_layers), gen=gen)
             if self.scoring == "sigmoid" or self.cfg.architecture == "Ernie4_5_MoeForCausalLM":
-                self.b_router[i] = torch.zeros(E, dtype=torch.float32, device=self.device)
+                self.b_router[i] = torch.zeros(self.E, dtype=torch.float32, device=self.device)
             if self.shared_inter:
                 self.w_sgu[i] = self._alloc(2 * self.shared_inter, H, std=std, gen=gen)
                 self.w_sd[i] = self._alloc(H, self.shared_inter, std=std / math.sqrt(2 * self.cfg.num_layers), gen=gen)
@@ -111,6 +115,7 @@ class DecoderMoEForCausalLM(DecoderForCausalLM):
         if i not in self.moe_layers:
             return super()._load_mlp(i, p, put)
         tp, E, I, H = self.tp, self.E, self.moe_inter, self.cfg.hidden_size
+        ex = slice(self.e0, self.e0 + self.E_local)   # this rank's experts under EP (all otherwise)
         full = self.cfg.moe_intermediate_size
         self.w_router[i] = put(p["router.weight"])
         if "router.bias" in p:
@@ -122,18 +127,18 @@ class DecoderMoEForCausalLM(DecoderForCausalLM):
         if "experts.gate_up" in p:  # fused per layer: [E, 2I, H] gate rows then up rows, [E, H, I]
             g, u = p["experts.gate_up"].chunk(2, 1)
             dn = p["experts.down"]
-            w13 = torch.cat([g[:, tp.rank * I:(tp.rank + 1) * I], u[:, tp.rank * I:(tp.rank + 1) * I]], 1)
-            w2 = dn[:, :, tp.rank * I:(tp.rank + 1) * I]
+            w13 = torch.cat([g[ex, tp.rank * I:(tp.rank + 1) * I], u[ex, tp.rank * I:(tp.rank + 1) * I]], 1)
+            w2 = dn[ex, :, tp.rank * I:(tp.rank + 1) * I]
         elif "experts.dbrx_w1" in p:  # DBRX: w1 (gate) / v1 (up) / w2 (down, transposed) as [E*I, H]
             g = p["experts.dbrx_w1"].reshape(E, full, H)
             u = p["experts.dbrx_v1"].reshape(E, full, H)
             d = p["experts.dbrx_w2"].reshape(E, full, H)
             sl = slice(tp.rank * I, (tp.rank + 1) * I)
-            w13 = torch.cat([g[:, sl], u[:, sl]], 1)
-            w2 = d[:, sl].transpose(1, 2)
+            w13 = torch.cat([g[ex, sl], u[ex, sl]], 1)
+            w2 = d[ex, sl].transpose(1, 2)
         else:  # per expert
             gs, ds = [], []
-            for e in range(E):
+            for e in range(ex.start, ex.stop):
                 gw = p.get(f"experts.{e}.gate", p.get(f"experts.{e}.w1"))
                 uw = p.get(f"experts.{e}.up", p.get(f"experts.{e}.w3"))
                 dw = p.get(f"experts.{e}.down", p.get(f"experts.{e}.w2"))
@@ -162,7 +167,12 @@ class DecoderMoEForCausalLM(DecoderForCausalLM):
         logits = linear(x, self.w_router[i])
         tw, tid = ops.moe_route(logits, self.k, self.renorm, self.scoring, bias=self.b_router[i],
                                 group_mode=2 if self.b_router[i] is not None else 0)
-        out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act)
+        if self.ep > 1:
+            from ome_amd.parallel.ep import moe_ep
+
+            out = moe_ep(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E)
+        else:
+            out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act)
         if self.w_sgu[i] is not None:
             out = out + linear(ops.act_and_mul(linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
         return out

@@ -18,7 +18,10 @@ What differs from the Llama / MoE paths, and where it runs:
 * MXFP4 expert checkpoints (``*_blocks`` / ``*_scales``, e2m1 pairs + e8m0 exponents) are
   dequantised to bf16 while streaming (``dequant_mxfp4``, checked against transformers'
   ``convert_moe_packed_tensors``).
-Experts are tensor-parallel over the intermediate dimension (like ``moe.py`` TP mode).
+Experts are tensor-parallel over the intermediate dimension (like ``moe.py`` TP mode), or, under
+DP attention, expert-parallel: rank r owns experts [r*E/ep, (r+1)*E/ep) with their biases and the
+tokens travel by all-to-all (``parallel/ep.py``, RCCL path: the expert biases keep the
+low-latency exchange off).
 """
 from __future__ import annotations
 
@@ -53,9 +56,13 @@ class GptOssForCausalLM(LlamaForCausalLM):
         super().__init__(cfg, device, dtype, max_positions)
         hf = cfg.extra or {}
         st = pstate.get()
-        if st.ep_size > 1:
-            raise NotImplementedError("GPT-OSS runs experts tensor-parallel (no DP-attention EP mode yet)")
         self.E, self.k = cfg.num_experts, cfg.num_experts_per_tok
+        self.ep = st.ep_size
+        if self.E % self.ep:
+            raise ValueError(f"{self.E} experts do not split over ep={self.ep}")
+        self.E_local = self.E // self.ep            # expert slots on this rank (all of them without EP)
+        self.e0 = st.ep_rank * self.E_local if self.ep > 1 else 0
+        self.expert_biases = True
         self.I = -(-cfg.moe_intermediate_size // self.tp.tp)
         self.act = 2
         L = cfg.num_layers
@@ -78,17 +85,18 @@ class GptOssForCausalLM(LlamaForCausalLM):
         cfg, tp = self.cfg, self.tp
         gen = torch.Generator(device=self.device)
         gen.manual_seed(seed + 31337 + 7919 * tp.rank)
-        H, I, E = cfg.hidden_size, self.I, self.E
+        H, I, E = cfg.hidden_size, self.I, self.E_local
+        bias_here = tp.rank == 0 or self.ep > 1     # TP: added once by rank 0; EP: by each owner
         for i in self.layers:
             self.w_gu[i] = self.w_d[i] = None
             self.sinks[i] = torch.randn(tp.hq, generator=gen, device=self.device, dtype=torch.float32)
             self.b_o[i] = self._alloc(H, std=std, gen=gen) if tp.rank == 0 else None
-            self.w_router[i] = self._alloc(E, H, std=std, gen=gen)
-            self.b_router[i] = self._alloc(E, std=std, gen=gen)
+            self.w_router[i] = self._alloc(self.E, H, std=std, gen=gen)
+            self.b_router[i] = self._alloc(self.E, std=std, gen=gen)
             self.w13[i] = self._alloc(E, 2 * I, H, std=std, gen=gen)
             self.b13[i] = self._alloc(E, 2 * I, std=std, gen=gen)
             self.w2[i] = self._alloc(E, H, I, std=std / math.sqrt(2 * cfg.num_layers), gen=gen)
-            self.b2[i] = self._alloc(E, H, std=std, gen=gen) if tp.rank == 0 else torch.zeros(
+            self.b2[i] = self._alloc(E, H, std=std, gen=gen) if bias_here else torch.zeros(
                 E, H, dtype=self.dtype, device=self.device)
             if self.b_qkv[i] is None:
                 self.b_qkv[i] = self._alloc((tp.hq + 2 * tp.hkv) * self.D, std=std, gen=gen)
@@ -135,17 +143,18 @@ class GptOssForCausalLM(LlamaForCausalLM):
         super().load_hf_weights(rest())
         for (i, key), d in pending.items():  # MXFP4 experts -> dense [E, in, out] (the bf16 param layout)
             mlp.setdefault(i, {})[key] = dequant_mxfp4(d["_blocks"], d["_scales"]).transpose(1, 2)
+        ex = slice(self.e0, self.e0 + self.E_local)         # this rank's experts (EP), all otherwise
         for i, d in mlp.items():
-            gu = d["experts.gate_up_proj"].float()            # [E, H, 2I] gate/up interleaved
-            gb = d["experts.gate_up_proj_bias"].float()       # [E, 2I]
+            gu = d["experts.gate_up_proj"][ex].float()        # [E, H, 2I] gate/up interleaved
+            gb = d["experts.gate_up_proj_bias"][ex].float()   # [E, 2I]
             g, u = gu[..., 0::2], gu[..., 1::2]               # [E, H, I_full]
             sl = slice(tp.rank * I, tp.rank * I + I)
             self.w13[i] = put(torch.cat([g[..., sl], u[..., sl]], -1).transpose(1, 2))    # [E, 2I, H]
             self.b13[i] = put(torch.cat([gb[:, 0::2][:, sl], gb[:, 1::2][:, sl]], -1))
-            dn = d["experts.down_proj"].float()               # [E, I_full, H]
+            dn = d["experts.down_proj"][ex].float()           # [E, I_full, H]
             self.w2[i] = put(dn[:, sl, :].transpose(1, 2))    # [E, H, I]
-            b2 = d["experts.down_proj_bias"]
-            self.b2[i] = put(b2) if tp.rank == 0 else torch.zeros_like(put(b2))
+            b2 = d["experts.down_proj_bias"][ex]
+            self.b2[i] = put(b2) if tp.rank == 0 or self.ep > 1 else torch.zeros_like(put(b2))
             self.w_router[i] = put(d["router.weight"])
             self.b_router[i] = put(d["router.bias"])
             self.w_gu[i] = self.w_d[i] = None
@@ -201,5 +210,10 @@ class GptOssForCausalLM(LlamaForCausalLM):
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
         logits = F.linear(x, self.w_router[i], self.b_router[i])
         tw, tid = ops.moe_route(logits, self.k, True)
-        out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.b13[i], self.b2[i])
+        if self.ep > 1:
+            from ome_amd.parallel.ep import moe_ep
+
+            out = moe_ep(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E, None, self.b13[i], self.b2[i])
+        else:
+            out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.b13[i], self.b2[i])
         return pstate.tp_all_reduce(out)

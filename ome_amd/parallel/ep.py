@@ -53,12 +53,14 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits: list[int], in_splits:
 
 def moe_ep_forward(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13_local: torch.Tensor,
                    w2_local: torch.Tensor, act: int, scale: float, num_experts: int,
-                   tables: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+                   tables: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None,
+                   b13_local: torch.Tensor | None = None, b2_local: torch.Tensor | None = None) -> torch.Tensor:
     """x [T, H] (this rank's tokens), routing [T, k] over the global (logical) experts; w13/w2
     hold this rank's expert slots.  Without ``tables`` rank r owns experts [r*E/ep, (r+1)*E/ep);
     with EPLB tables (``ome_amd.parallel.eplb``: rep_rank / rep_slot [E, Rmax], n_rep [E]) each
     (token, k-slot) assignment goes to replica ``(t*k + j) mod n_rep[e]`` of its expert, which
-    spreads a replicated hot expert's rows evenly over its copies.  Returns [T, H]."""
+    spreads a replicated hot expert's rows evenly over its copies.  ``b13_local`` / ``b2_local``:
+    per-expert biases of the owner's slots (GPT-OSS).  Returns [T, H]."""
     st = pstate.get()
     group, ep, me = st.ep_group, st.ep_size, st.ep_rank
     T, H = x.shape
@@ -88,7 +90,7 @@ def moe_ep_forward(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor
     _a2a(recv_e, send_e, rc, sc, group)
     if R:
         ones = torch.ones(R, 1, dtype=torch.float32, device=x.device)
-        y = ops.fused_moe(recv_x, ones, recv_e.view(R, 1), w13_local, w2_local, act, 1.0)
+        y = ops.fused_moe(recv_x, ones, recv_e.view(R, 1), w13_local, w2_local, act, 1.0, b13_local, b2_local)
     else:
         y = x.new_empty(0, H)
     back = x.new_empty(T * k, H)
@@ -110,7 +112,8 @@ def _a2a_async(out, inp, out_splits, in_splits, group):
 
 def moe_ep_forward_tbo(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13_local: torch.Tensor,
                        w2_local: torch.Tensor, act: int, scale: float, num_experts: int,
-                       tables: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+                       tables: tuple[torch.Tensor, torch.Tensor, torch.Tensor] | None = None,
+                       b13_local: torch.Tensor | None = None, b2_local: torch.Tensor | None = None) -> torch.Tensor:
     """Two-batch overlap of the expert-parallel MoE block (SGLang ``--enable-two-batch-overlap``,
     reference deepseek-rdma-pd-rt.yaml:89): the token rows are split into two micro-batches;
     their dispatches are issued back to back, then micro-batch A's experts run while B's
@@ -169,7 +172,8 @@ def moe_ep_forward_tbo(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Te
         R = mb["rx"].shape[0]
         if R:
             ones = torch.ones(R, 1, dtype=torch.float32, device=x.device)
-            y = ops.fused_moe(mb["rx"], ones, mb["re"].view(R, 1), w13_local, w2_local, act, 1.0)
+            y = ops.fused_moe(mb["rx"], ones, mb["re"].view(R, 1), w13_local, w2_local, act, 1.0, b13_local,
+                              b2_local)
         else:
             y = x.new_empty(0, H)
         mb["y"] = y
@@ -185,19 +189,20 @@ def moe_ep_forward_tbo(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Te
 
 
 def moe_ep(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13_local, w2_local, act: int,
-           scale: float, num_experts: int, tables=None) -> torch.Tensor:
+           scale: float, num_experts: int, tables=None, b13_local=None, b2_local=None) -> torch.Tensor:
     """Expert-parallel MoE block: the device-only low-latency exchange
     (:mod:`ome_amd.parallel.ep_ll`) when this lockstep step allows it (``state.ep_ll_ok``: every
     rank's batch fits the fixed buckets; set per step by the engine, so all ranks pick the same
     mode), the RCCL all-to-all (normal / two-batch-overlap) otherwise.  EPLB replica tables are
-    honoured by both."""
+    honoured by both.  Expert biases (GPT-OSS) take the RCCL path (the low-latency exchange is
+    not attached for such models)."""
     st = pstate.get()
     ll = getattr(st, "ep_ll", None)
-    if ll is not None and x.is_cuda and st.ep_ll_ok:
+    if ll is not None and x.is_cuda and st.ep_ll_ok and b13_local is None and b2_local is None:
         e_local = w13_local.shape[0]   # expert slots per rank (redundant replicas included)
         return ll.forward(x, topk_w, topk_ids, w13_local, w2_local, act, scale, e_local, tables)
     fwd = moe_ep_forward_tbo if st.tbo else moe_ep_forward
-    return fwd(x, topk_w, topk_ids, w13_local, w2_local, act, scale, num_experts, tables)
+    return fwd(x, topk_w, topk_ids, w13_local, w2_local, act, scale, num_experts, tables, b13_local, b2_local)
 
 
 def attach_low_latency(model, max_tokens: int) -> bool:
@@ -210,7 +215,7 @@ def attach_low_latency(model, max_tokens: int) -> bool:
     if st.ep_size <= 1 or not torch.cuda.is_available() or os.environ.get("OME_EP_LL", "1") == "0":
         return False
     k = getattr(model, "k", 0)
-    if not k or getattr(model, "E", 0) % st.ep_size:
+    if not k or getattr(model, "E", 0) % st.ep_size or getattr(model, "expert_biases", False):
         return False
     from ome_amd.parallel.ep_ll import LowLatencyEP
 

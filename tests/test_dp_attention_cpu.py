@@ -40,6 +40,16 @@ def _worker(rank, world, port, path, q, relay_cap=None):
 
 
 def _checkpoint(tmp_path, kind):
+    if kind == "gpt-oss":   # biased experts, sinks, sliding windows
+        from tests.test_gpt_oss_cpu import _hf_model
+
+        _hf_model(tmp_path)
+        return
+    if kind in ("olmoe", "dbrx", "minimax_m2"):   # spec-driven decoder MoE families
+        from tests.test_decoder_families_cpu import _hf_model
+
+        _hf_model(kind, tmp_path)
+        return
     if kind == "qwen3-moe":
         hf = dict(PRESETS["tiny-moe"])
         m = build_model(ModelConfig.from_hf(hf), "cpu", torch.float32, load_format="dummy", seed=5)
@@ -52,7 +62,8 @@ def _checkpoint(tmp_path, kind):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("kind,relay_cap", [("qwen3-moe", None), ("deepseek-v3", None), ("qwen3-moe", 3)])
+@pytest.mark.parametrize("kind,relay_cap", [("qwen3-moe", None), ("deepseek-v3", None), ("qwen3-moe", 3),
+                                            ("gpt-oss", None), ("olmoe", None), ("dbrx", None), ("minimax_m2", None)])
 def test_dp_attention_ep_matches_single(tmp_path, kind, relay_cap):
     _checkpoint(tmp_path, kind)
     from ome_amd.runtime.engine import Engine, EngineArgs
