@@ -10,7 +10,9 @@ A Llama decoder whose blocks were searched per layer (``block_configs``):
   or ``replace_with_linear``.
 Residual adds are chained through the fused add + RMSNorm kernel (the pending block output is
 added when the next norm runs).  Tensor parallelism splits heads / FFN width per layer; linear
-replacements are replicated (no collective).  Only real attention layers own KV pages.
+replacements are replicated (no collective).  Only real attention layers own KV pages.  Pipeline
+stages hand over (pending block output, residual stream) -- a zero block output when the
+boundary layer ended on a no-op.
 The remote-code model is not importable here: tests compose transformers' Llama modules per the
 block config (parity with the remote code itself unpinned).
 """
@@ -52,8 +54,6 @@ class DeciLMForCausalLM(LlamaForCausalLM):
     def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, max_positions: int | None = None):
         super().__init__(cfg, device, dtype, max_positions)
         st = pstate.get()
-        if st.pp_size > 1:
-            raise NotImplementedError("pipeline parallelism for DeciLM")
         self.blocks = block_kinds(cfg)
         tp, nh = st.tp_size, cfg.num_heads
         self.hkv: dict[int, int] = {}
@@ -158,9 +158,14 @@ class DeciLMForCausalLM(LlamaForCausalLM):
                 input_embeds: torch.Tensor | None = None) -> torch.Tensor:
         cfg, tp, D = self.cfg, self.tp, self.D
         T = ids.shape[0]
-        h = input_embeds if input_embeds is not None else \
-            pstate.tp_all_reduce(ops.embedding(ids, self.embed, tp.vocab_start, tp.vocab_end))
+        st = pstate.get()
         pend = None   # block output still to be added to the residual stream h
+        if st.pp_size > 1 and not st.is_first_pp:
+            spec = ((T, cfg.hidden_size), self.dtype, ids.device)
+            pend, h = pstate.pp_recv(spec, spec)
+        else:
+            h = input_embeds if input_embeds is not None else \
+                pstate.tp_all_reduce(ops.embedding(ids, self.embed, tp.vocab_start, tp.vocab_end))
 
         def norm(w):
             nonlocal pend
@@ -189,4 +194,7 @@ class DeciLMForCausalLM(LlamaForCausalLM):
                 pend = self.mlp(i, norm(self.ln2[i]))
             elif b["ffn"] == "linear":
                 pend = linear(norm(self.ln2[i]), self.w_lin_mlp[i])
+        if st.pp_size > 1 and not st.is_last_pp:
+            pstate.pp_send(pend if pend is not None else torch.zeros_like(h), h)
+            return None
         return norm(self.norm)

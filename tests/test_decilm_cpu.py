@@ -119,3 +119,47 @@ def test_decilm_matches_block_semantics(tmp_path):
     for _ in range(6):
         seq.append(int(_ref_logits(w, seq)[-1].argmax()))
     assert out == seq[len(ids):]
+
+
+def _pp_worker(rank, world, port, path, q):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    eng = Engine(EngineArgs(model_path=path, pp_size=world, device="cpu", max_running_requests=4,
+                            context_length=256, dtype="float32"))
+    if rank == 0:
+        out = [r.output_ids for r in eng.generate(PP_PROMPTS, SamplingParams(max_new_tokens=6, ignore_eos=True))]
+        eng.stop_group()
+        q.put(out)
+    else:
+        eng.run_forever()
+
+
+PP_PROMPTS = [[(7 * i + 3 * j) % 290 + 5 for j in range(6 + 5 * i)] for i in range(3)]
+
+
+@pytest.mark.timeout(300)
+def test_decilm_pp2_matches_single(tmp_path):
+    """PP=2 over the heterogeneous block stack: stage 0 ends on an attention-only block (no-op
+    FFN), so the hand-off carries a pending block output; per-stage per-layer KV heads."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    _checkpoint(tmp_path)
+    single = Engine(EngineArgs(model_path=str(tmp_path), device="cpu", dtype="float32", max_running_requests=4,
+                               context_length=256))
+    want = [r.output_ids for r in single.generate(PP_PROMPTS, SamplingParams(max_new_tokens=6, ignore_eos=True))]
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_pp_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=240)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == want
