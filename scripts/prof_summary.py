@@ -100,6 +100,7 @@ def main(d: str, last_steps: int = 0) -> None:
     inter = {"decode": 0, "mixed": 0}
     intra = {"decode": collections.Counter(), "mixed": collections.Counter()}
     step_rows, prev_end, pending_inter = [], None, 0
+    pairs, pair_n, prev_name = collections.Counter(), collections.Counter(), None
     for r in rows:
         st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         if prev_end is not None:
@@ -108,6 +109,11 @@ def main(d: str, last_steps: int = 0) -> None:
                 pending_inter = gap
             elif gap > 2000:
                 step_rows.append(("gap", cat_of(r["Kernel_Name"]), gap))
+            if gap > 2000:
+                key = f"{short(prev_name, 48)}` -> `{short(r['Kernel_Name'], 48)}"
+                pairs[key] += gap
+                pair_n[key] += 1
+        prev_name = r["Kernel_Name"]
         step_rows.append(("k", r["Kernel_Name"], 0))
         prev_end = en if prev_end is None else max(prev_end, en)
         if "sample_kernel" in r["Kernel_Name"]:
@@ -123,6 +129,10 @@ def main(d: str, last_steps: int = 0) -> None:
     for c in sorted(set(intra["decode"]) | set(intra["mixed"]), key=lambda c: -(intra["decode"][c] + intra["mixed"][c])):
         print(f"| inside, before a {c} kernel (gaps > 2 us) | {intra['decode'][c] / 1e3 / max(1, nk['decode']):.0f} | "
               f"{intra['mixed'][c] / 1e3 / max(1, nk['mixed']):.0f} |")
+    print("\n## Largest idle gaps by (kernel before -> kernel after), gaps > 2 us\n")
+    print("| total ms | count | avg us | previous kernel -> next kernel |\n|---:|---:|---:|---|")
+    for k, v in pairs.most_common(12):
+        print(f"| {v / 1e6:.2f} | {pair_n[k]} | {v / pair_n[k] / 1e3:.1f} | `{k}` |")
     print("\n## GEMMs by kernel+grid\n\n| total ms | calls | avg us | kernel / grid |\n|---:|---:|---:|---|")
     for n, v in grids.most_common(20):
         print(f"| {v / 1e6:.2f} | {gcnt[n]} | {v / gcnt[n] / 1e3:.1f} | `{n}` |")
