@@ -73,6 +73,15 @@ def _worker(rank, world, port, q):
             x = torch.randn(n, device=dev).to(torch.bfloat16)
             t = _graph_time(lambda: ar.all_reduce(x), dist)
             rows.append(f"all_reduce        {kib:6d} KiB  {t:8.1f} us  {2 * (world - 1) / world * kib / 1024 / t * 1e6 / 1024:6.2f} GB/s busbw")
+        if os.environ.get("OME_AR_GRID_SWEEP") == "1":   # one-shot grid sizing: vectors per lane
+            for vpt in (1, 2, 4):
+                ar.vpt = vpt
+                for kib in (8, 16, 24, 32, 48, 64, 96, 128, 256, 512):
+                    n = kib * 1024 // 2
+                    x = torch.randn(n, device=dev).to(torch.bfloat16)
+                    t = _graph_time(lambda: ar.all_reduce(x), dist)
+                    rows.append(f"one-shot vpt={vpt} grid={ar._grid(n, False):3d} {kib:5d} KiB  {t:8.1f} us")
+            ar.vpt = 4
         for r in (1, 16, 32, 64):
             H = 4096
             st = ar.staging((r, H))
