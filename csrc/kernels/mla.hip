@@ -249,3 +249,70 @@ OME_API int ome_mla_attn(const void* q, int64_t q_stride_t, const void* cache, c
   OME_CHECK_LAUNCH();
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------
+// MLA pre-attention glue as ONE launch per layer (it was ~25 PyTorch elementwise / cat /
+// index_select / index_copy kernels per layer: profiles/r03_deepseek_v3_fp8_reduced.md "other").
+// One workgroup per token t:
+//   cache[slot_t][0 : lat]          = RMSNorm(a[t, qlr : qlr + lat]) * w       (kv_a_layernorm)
+//   cache[slot_t][lat : lat + rope] = RoPE_pos(a[t, qlr + lat : qlr + lat + rope])
+//   qf[t, h, lat : lat + rope]      = RoPE_pos(q[t, h, nope : nope + rope])   for every head h
+// RoPE in NeoX halves (the checkpoint's interleaved rows are permuted at load), table cs[pos] =
+// [cos | sin] fp32; fp32 math, bf16 stores (the reference op's order: x * rs * w, rounded once).
+// Padding rows (slot < 0) write row 0 of the scratch page, as the eager path did.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void mla_prep_kernel(const bf16* __restrict__ a, int64_t lda, int qlr, int lat,
+                                                       int rope, const bf16* __restrict__ w, float eps,
+                                                       const int* __restrict__ pos, const float* __restrict__ cs,
+                                                       const int* __restrict__ slots, bf16* __restrict__ cache,
+                                                       int64_t cache_row, const bf16* __restrict__ q, int64_t q_tok,
+                                                       int64_t q_head, int nope, int H, bf16* __restrict__ qf,
+                                                       int64_t qf_tok, int64_t qf_head) {
+  __shared__ float red[4];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const bf16* ar = a + (int64_t)t * lda + qlr;
+  int slot = slots[t];
+  slot = slot < 0 ? 0 : slot;
+  bf16* crow = cache + (int64_t)slot * cache_row;
+  float ss = 0.f;
+  for (int i = tid; i < lat; i += 256) {
+    const float v = (float)ar[i];
+    ss += v * v;
+  }
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  const float rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)lat + eps);
+  for (int i = tid; i < lat; i += 256) crow[i] = (bf16)((float)ar[i] * rs * (float)w[i]);
+  const int half = rope >> 1;
+  const float* c = cs + (int64_t)pos[t] * rope;
+  // k_pe: pairs (j, j + half)
+  for (int j = tid; j < half; j += 256) {
+    const float x1 = (float)ar[lat + j], x2 = (float)ar[lat + half + j];
+    const float co = c[j], si = c[half + j];
+    crow[lat + j] = (bf16)(x1 * co - x2 * si);
+    crow[lat + half + j] = (bf16)(x2 * co + x1 * si);
+  }
+  // q_pe of every head
+  for (int k = tid; k < H * half; k += 256) {
+    const int h = k / half, j = k - h * half;
+    const bf16* qr = q + (int64_t)t * q_tok + (int64_t)h * q_head + nope;
+    const float x1 = (float)qr[j], x2 = (float)qr[half + j];
+    const float co = c[j], si = c[half + j];
+    bf16* o = qf + (int64_t)t * qf_tok + (int64_t)h * qf_head + lat;
+    o[j] = (bf16)(x1 * co - x2 * si);
+    o[half + j] = (bf16)(x2 * co + x1 * si);
+  }
+}
+
+OME_API int ome_mla_prep(const void* a, int64_t lda, int qlr, int lat, int rope, const void* w, float eps,
+                         const int* pos, const float* cs, const int* slots, void* cache, int64_t cache_row,
+                         const void* q, int64_t q_tok, int64_t q_head, int nope, int H, void* qf, int64_t qf_tok,
+                         int64_t qf_head, int T, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (rope % 2 || lat <= 0 || H <= 0) return -2;
+  mla_prep_kernel<<<T, 256, 0, stream>>>((const bf16*)a, lda, qlr, lat, rope, (const bf16*)w, eps, pos, cs, slots,
+                                         (bf16*)cache, cache_row, (const bf16*)q, q_tok, q_head, nope, H, (bf16*)qf,
+                                         qf_tok, qf_head);
+  return (int)hipGetLastError();
+}

@@ -296,15 +296,6 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         return n
 
     # ------------------------------------------------------------------ forward
-    def _rope(self, x: torch.Tensor, positions: torch.Tensor) -> torch.Tensor:
-        cs = self.cos_sin.index_select(0, positions.long())
-        half = self.rope // 2
-        cos, sin = cs[:, :half], cs[:, half:]
-        if x.dim() == 3:
-            cos, sin = cos[:, None, :], sin[:, None, :]
-        x1, x2 = x[..., :half].float(), x[..., half:].float()
-        return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], -1).to(x.dtype)
-
     def _token_rows(self, meta: AttnMeta, T: int):
         """(tok_row, kv_lens) per query token, plus the block table they index."""
         if self._arange is None or self._arange.numel() < T:
@@ -327,23 +318,21 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         Hl = self.Hl
         a = linear(x, self.w_qa[i])
         if self.qlr:
-            qa = ops.rmsnorm(a[:, : self.qlr].contiguous(), self.qa_ln[i], self.eps)
+            qa = ops.rmsnorm(a[:, : self.qlr], self.qa_ln[i], self.eps)   # row-strided view, no copy
             q = linear(qa, self.w_qb[i])
         else:
             q = linear(x, self.w_qb[i])
-        ckv = a[:, self.qlr:]
         lat = self.lat
-        c = ops.rmsnorm(ckv[:, :lat].contiguous(), self.kva_ln[i], self.eps)
         q = q.view(T, Hl, self.qk_dim)
-        q_pe = self._rope(q[..., self.nope:], meta.positions)
-        k_pe = self._rope(ckv[:, lat:], meta.positions)
         cache = kv.k[i]
         flat = cache.view(-1, lat + self.rope)
-        # padding rows carry slot -1: park them in the scratch page 0
-        flat.index_copy_(0, meta.slots.long().clamp_min(0), torch.cat([c, k_pe], -1))
+        q_full = torch.empty(T, Hl, lat + self.rope, dtype=x.dtype, device=x.device)   # [q_nope . W_UK | q_pe]
+        # kv_a_layernorm + RoPE(k_pe) -> latent cache row, RoPE(q_pe) -> q_full: one kernel
+        # (padding rows carry slot -1: parked in the scratch page 0)
+        ops.mla_prep(a, self.qlr, lat, self.rope, self.kva_ln[i], self.eps, meta.positions, self.cos_sin, meta.slots,
+                     flat, q, self.nope, q_full)
         q_nope = q[..., : self.nope].transpose(0, 1).contiguous()         # [Hl, T, nope]
-        q_lat = torch.bmm(q_nope, self.w_uk[i])                           # [Hl, T, lat]
-        q_full = torch.cat([q_lat.transpose(0, 1), q_pe], -1).contiguous()  # [T, Hl, lat + rope]
+        q_full[:, :, :lat].copy_(torch.bmm(q_nope, self.w_uk[i]).transpose(0, 1))
         o_lat = torch.empty(T, Hl, lat, dtype=x.dtype, device=x.device)
         if x.is_cuda and self._ws is None:
             self._ws = ops.MLAWorkspace(x.device)

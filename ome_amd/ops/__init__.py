@@ -953,6 +953,35 @@ def gemm_sk(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
     return out
 
 
+def mla_prep(a: torch.Tensor, qlr: int, lat: int, rope: int, w: torch.Tensor, eps: float, positions: torch.Tensor,
+             cos_sin: torch.Tensor, slots: torch.Tensor, cache_flat: torch.Tensor, q: torch.Tensor, nope: int,
+             q_full: torch.Tensor) -> None:
+    """MLA pre-attention glue in one kernel (csrc/kernels/mla.hip ``ome_mla_prep``): from the fused
+    q_a / kv_a projection output ``a`` [T, qlr + lat + rope] write the token's latent cache row
+    ``cache_flat[slot] = [RMSNorm(c_kv) * w | RoPE(k_pe)]`` (slot < 0 -> row 0, the scratch page)
+    and the roped q_pe of every head into ``q_full[:, :, lat:]`` (q [T, H, nope + rope])."""
+    T, H = q.shape[0], q.shape[1]
+    if not _gpu(a):
+        ckv = a[:, qlr:qlr + lat + rope]
+        c = ref.rmsnorm(ckv[:, :lat], w, eps)
+        cs = cos_sin.index_select(0, positions.long())
+        half = rope // 2
+
+        def rot(x, cos, sin):
+            x1, x2 = x[..., :half].float(), x[..., half:].float()
+            return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], -1).to(x.dtype)
+
+        k_pe = rot(ckv[:, lat:], cs[:, :half], cs[:, half:])
+        cache_flat.index_copy_(0, slots.long().clamp_min(0), torch.cat([c, k_pe], -1))
+        q_full[:, :, lat:] = rot(q[..., nope:], cs[:, None, :half], cs[:, None, half:])
+        return
+    assert a.stride(1) == 1 and q.stride(2) == 1 and q_full.stride(2) == 1 and cache_flat.is_contiguous()
+    assert cos_sin.dtype == torch.float32 and cos_sin.shape[1] == rope and cos_sin.is_contiguous()
+    call("ome_mla_prep", a.data_ptr(), a.stride(0), qlr, lat, rope, w.data_ptr(), float(eps), _i32(positions).data_ptr(),
+         cos_sin.data_ptr(), _i32(slots).data_ptr(), cache_flat.data_ptr(), cache_flat.stride(0), q.data_ptr(),
+         q.stride(0), q.stride(1), nope, H, q_full.data_ptr(), q_full.stride(0), q_full.stride(1), T, stream_ptr())
+
+
 def gemm_sk_fp8_ok(M: int, N: int, K: int, bn: int = 128, nwg: int = 256) -> bool:
     return bn in (128, 256) and N % bn == 0 and K % 128 == 0 and K > 0 and nwg % 8 == 0 and \
         8 <= nwg <= _SK_MAX_WG and M > 0 and gemm_sk_tiles(M, N, bn, 128) <= _SK_CNT

@@ -124,3 +124,30 @@ def test_deepseek_gpu_vs_cpu_logits():
     lb = b.compute_logits(b.forward(torch.tensor(ids, dtype=torch.int32, device=DEV), meta, kvb)).float().cpu()
     cos = torch.nn.functional.cosine_similarity(la, lb, dim=-1)
     assert cos.min().item() > 0.99, cos.min()
+
+
+@pytest.mark.parametrize("qlr,lat,rope,H,nope", [(1536, 512, 64, 16, 128), (768, 256, 32, 8, 64), (0, 512, 64, 4, 128)])
+def test_mla_prep_matches_reference(qlr, lat, rope, H, nope):
+    """Fused kv_a_layernorm + RoPE(k_pe) cache write + RoPE(q_pe) (``ome_mla_prep``) against the
+    eager fp32 reference path, including a padding row (slot -1 -> scratch row 0)."""
+    torch.manual_seed(qlr + lat)
+    T, npos = 37, 4096
+    a = torch.randn(T, qlr + lat + rope, dtype=torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(lat)).to(torch.bfloat16)
+    q = torch.randn(T, H, nope + rope, dtype=torch.bfloat16)
+    pos = torch.randint(0, npos, (T,), dtype=torch.int32)
+    ang = torch.arange(npos)[:, None].float() * (1.0 / 10000 ** (torch.arange(0, rope, 2).float() / rope))[None]
+    cs = torch.cat([ang.cos(), ang.sin()], -1).contiguous()
+    slots = torch.randperm(200)[:T].to(torch.int32) + 1
+    slots[5] = -1
+    outs = []
+    for dev in ("cpu", "cuda"):
+        flat = torch.zeros(256, lat + rope, dtype=torch.bfloat16, device=dev)
+        qf = torch.zeros(T, H, lat + rope, dtype=torch.bfloat16, device=dev)
+        ops.mla_prep(a.to(dev), qlr, lat, rope, w.to(dev), 1e-6, pos.to(dev), cs.to(dev), slots.to(dev), flat,
+                     q.to(dev), nope, qf)
+        outs.append((flat.float().cpu(), qf.float().cpu()))
+    (f0, q0), (f1, q1) = outs
+    assert (f1 - f0).abs().max().item() <= 2e-2 * max(1.0, f0.abs().max().item())
+    assert (q1[:, :, lat:] - q0[:, :, lat:]).abs().max().item() <= 2e-2 * max(1.0, q0.abs().max().item())
+    assert f1[0].abs().sum() > 0   # the padding row landed in the scratch row
