@@ -6,7 +6,8 @@ import csv
 import sys
 from pathlib import Path
 
-CATS = [("gemm", ("Cijk_", "Custom_Cijk", "gemm", "Gemm")), ("attn_decode", ("paged_decode",)),
+CATS = [("attn_mla", ("mla_attn", "mla_reduce")), ("mla_prep", ("mla_prep",)), ("moe", ("moe_",)),
+        ("gemm", ("Cijk_", "Custom_Cijk", "gemm", "Gemm")), ("attn_decode", ("paged_decode",)),
         ("attn_prefill", ("paged_prefill",)), ("rope_kv", ("rope_qkv", "kv_cache_write")),
         ("norm", ("rmsnorm",)), ("act", ("act_and_mul",)), ("sample", ("sample_kernel",)),
         ("embed", ("embedding_kernel",)), ("copy", ("copyBuffer", "fill_pending", "Fill", "index")),
@@ -133,6 +134,23 @@ def main(d: str, last_steps: int = 0) -> None:
     print("| total ms | count | avg us | previous kernel -> next kernel |\n|---:|---:|---:|---|")
     for k, v in pairs.most_common(12):
         print(f"| {v / 1e6:.2f} | {pair_n[k]} | {v / pair_n[k] / 1e3:.1f} | `{k}` |")
+    dump = int(__import__("os").environ.get("PROF_DUMP_GAPS", "0"))
+    if dump:   # kernel sequences around the first few gaps > 300 us (timestamps relative, us)
+        print("\n## Kernel sequences around large gaps\n")
+        shown, prev_end = 0, None
+        for j, r in enumerate(rows):
+            st = int(r["Start_Timestamp"])
+            if prev_end is not None and st - prev_end > 300_000 and j > 8:
+                base = int(rows[j - 8]["Start_Timestamp"])
+                print("```")
+                for q in rows[j - 8:j + 6]:
+                    print(f"{(int(q['Start_Timestamp']) - base) / 1e3:9.1f} {(int(q['End_Timestamp']) - base) / 1e3:9.1f} "
+                          f"{short(q['Kernel_Name'], 70)}")
+                print("```")
+                shown += 1
+                if shown >= dump:
+                    break
+            prev_end = int(r["End_Timestamp"]) if prev_end is None else max(prev_end, int(r["End_Timestamp"]))
     print("\n## GEMMs by kernel+grid\n\n| total ms | calls | avg us | kernel / grid |\n|---:|---:|---:|---|")
     for n, v in grids.most_common(20):
         print(f"| {v / 1e6:.2f} | {gcnt[n]} | {v / gcnt[n] / 1e3:.1f} | `{n}` |")
