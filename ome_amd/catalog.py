@@ -42,6 +42,7 @@ class Family:
     quantization: str | None = None
     min_tp: int = 1           # e.g. DP attention over a whole node
     diffusion: str | None = None   # diffusers pipeline class: served by ome_amd.diffusion.server
+    runtime: bool | None = None    # emit a runtime; None = only if no earlier family's runtime covers it
 
 
 FAMILIES: list[Family] = [
@@ -205,6 +206,139 @@ FAMILIES: list[Family] = [
 ]
 
 
+# More checkpoints of supported architectures (the rest of the reference's model catalog,
+# ``config/models/**``): base models whose runtime is an earlier family's when one of the same
+# architecture / quantisation already covers the size, otherwise a runtime of their own.
+_C, _I, _V = ["TEXT_TO_TEXT"], ["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], ["IMAGE_TO_TEXT"]
+_L, _Q2, _Q3 = "LlamaForCausalLM", "Qwen2ForCausalLM", "Qwen3ForCausalLM"
+_MORE = [
+    ("deepseek-coder-7b-instruct-v1-5", "deepseek", "deepseek-ai/deepseek-coder-7b-instruct-v1.5", _L, 6.9),
+    ("deepseek-llm-7b-chat", "deepseek", "deepseek-ai/deepseek-llm-7b-chat", _L, 6.9),
+    ("deepseek-r1-distill-llama-8b", "deepseek", "deepseek-ai/DeepSeek-R1-Distill-Llama-8B", _L, 8.0),
+    ("deepseek-r1-distill-llama-70b", "deepseek", "deepseek-ai/DeepSeek-R1-Distill-Llama-70B", _L, 70.6),
+    ("deepseek-r1-distill-qwen-1-5b", "deepseek", "deepseek-ai/DeepSeek-R1-Distill-Qwen-1.5B", _Q2, 1.8),
+    ("deepseek-r1-distill-qwen-7b", "deepseek", "deepseek-ai/DeepSeek-R1-Distill-Qwen-7B", _Q2, 7.6),
+    ("deepseek-r1-distill-qwen-14b", "deepseek", "deepseek-ai/DeepSeek-R1-Distill-Qwen-14B", _Q2, 14.8),
+    ("deepseek-r1-distill-qwen-32b", "deepseek", "deepseek-ai/DeepSeek-R1-Distill-Qwen-32B", _Q2, 32.8),
+    ("deepseek-v2", "deepseek", "deepseek-ai/DeepSeek-V2", "DeepseekV2ForCausalLM", 236.0),
+    ("deepseek-v2-5", "deepseek", "deepseek-ai/DeepSeek-V2.5", "DeepseekV2ForCausalLM", 236.0),
+    ("dolly-v2-12b", "databricks", "databricks/dolly-v2-12b", "GPTNeoXForCausalLM", 12.0),
+    ("stablelm-tuned-alpha-7b", "stabilityai", "stabilityai/stablelm-tuned-alpha-7b", "GPTNeoXForCausalLM", 7.9),
+    ("falcon3-10b-instruct", "tiiuae", "tiiuae/Falcon3-10B-Instruct", _L, 10.3),
+    ("gemma-2b", "google", "google/gemma-2b", "GemmaForCausalLM", 2.5),
+    ("gemma-7b", "google", "google/gemma-7b", "GemmaForCausalLM", 8.5),
+    ("gemma-2-2b", "google", "google/gemma-2-2b", "Gemma2ForCausalLM", 2.6),
+    ("gemma-2-2b-it", "google", "google/gemma-2-2b-it", "Gemma2ForCausalLM", 2.6),
+    ("gemma-2-9b", "google", "google/gemma-2-9b", "Gemma2ForCausalLM", 9.2),
+    ("gemma-2-27b", "google", "google/gemma-2-27b", "Gemma2ForCausalLM", 27.2),
+    ("gemma-2-27b-it", "google", "google/gemma-2-27b-it", "Gemma2ForCausalLM", 27.2),
+    ("gemma-3-4b-it", "google", "google/gemma-3-4b-it", "Gemma3ForConditionalGeneration", 4.3, _I),
+    ("gemma-3-12b-it", "google", "google/gemma-3-12b-it", "Gemma3ForConditionalGeneration", 12.2, _I),
+    ("granite-3-0-2b-instruct", "ibm", "ibm-granite/granite-3.0-2b-instruct", "GraniteForCausalLM", 2.6),
+    ("granite-3-1-2b-instruct", "ibm", "ibm-granite/granite-3.1-2b-instruct", "GraniteForCausalLM", 2.5),
+    ("granite-3-0-8b-instruct", "ibm", "ibm-granite/granite-3.0-8b-instruct", "GraniteForCausalLM", 8.2),
+    ("hermes-2-pro-llama-3-8b", "nousresearch", "NousResearch/Hermes-2-Pro-Llama-3-8B", _L, 8.0),
+    ("internlm2-7b", "internlm", "internlm/internlm2-7b", "InternLM2ForCausalLM", 7.7),
+    ("internlm2-20b", "internlm", "internlm/internlm2-20b", "InternLM2ForCausalLM", 19.9),
+    ("llama-2-7b", "meta", "meta-llama/Llama-2-7b-hf", _L, 6.7),
+    ("llama-2-7b-chat-hf", "meta", "meta-llama/Llama-2-7b-chat-hf", _L, 6.7),
+    ("llama-2-13b-hf", "meta", "meta-llama/Llama-2-13b-hf", _L, 13.0),
+    ("llama-2-13b-chat-hf", "meta", "meta-llama/Llama-2-13b-chat-hf", _L, 13.0),
+    ("llama-2-70b-hf", "meta", "meta-llama/Llama-2-70b-hf", _L, 69.0),
+    ("llama-2-70b-chat-hf", "meta", "meta-llama/Llama-2-70b-chat-hf", _L, 69.0),
+    ("llama-3-1-70b-instruct", "meta", "meta-llama/Meta-Llama-3.1-70B-Instruct", _L, 70.6),
+    ("llama-3-3-70b-instruct", "meta", "meta-llama/Llama-3.3-70B-Instruct", _L, 70.6),
+    ("llama-3-1-nemotron-70b-instruct-hf", "nvidia", "nvidia/Llama-3.1-Nemotron-70B-Instruct-HF", _L, 70.6),
+    ("llama-3-1-nemotron-nano-8b-v1", "nvidia", "nvidia/Llama-3.1-Nemotron-Nano-8B-v1", _L, 8.0),
+    ("llama-3-2-1b-instruct", "meta", "meta-llama/Llama-3.2-1B-Instruct", _L, 1.2),
+    ("llama-3-2-3b-instruct", "meta", "meta-llama/Llama-3.2-3B-Instruct", _L, 3.2),
+    ("llama-guard-3-8b", "meta", "meta-llama/Llama-Guard-3-8B", _L, 8.0),
+    ("llama-4-maverick-17b-128e-instruct", "meta", "meta-llama/Llama-4-Maverick-17B-128E-Instruct",
+     "Llama4ForConditionalGeneration", 402.0, _I),
+    ("unsloth-llama-3-2-11b-vision-instruct", "unsloth", "unsloth/Llama-3.2-11B-Vision-Instruct",
+     "MllamaForConditionalGeneration", 10.7, _I),
+    ("llava-v1-5-7b", "llava", "liuhaotian/llava-v1.5-7b", "LlavaLlamaForCausalLM", 7.1, _V),
+    ("mistral-7b-instruct-v0-2", "mistralai", "mistralai/Mistral-7B-Instruct-v0.2", "MistralForCausalLM", 7.2),
+    ("mistral-7b-instruct-v0-3", "mistral", "mistralai/Mistral-7B-Instruct-v0.3", "MistralForCausalLM", 7.2),
+    ("mistral-7b-v0-1", "mistral", "mistralai/Mistral-7B-v0.1", "MistralForCausalLM", 7.2),
+    ("mistral-nemo-instruct-2407", "mistral", "mistralai/Mistral-Nemo-Instruct-2407", "MistralForCausalLM", 12.2),
+    ("mixtral-8x7b-instruct-v0-1", "mistral", "mistralai/Mixtral-8x7B-Instruct-v0.1", "MixtralForCausalLM", 46.7),
+    ("mixtral-8x7b-v0-1", "mistral", "mistralai/Mixtral-8x7B-v0.1", "MixtralForCausalLM", 46.7),
+    ("mixtral-8x22b-v0-1", "mistral", "mistralai/Mixtral-8x22B-v0.1", "MixtralForCausalLM", 141.0),
+    ("nvidia-nemotron-3-nano-30b-a3b-base-bf16", "nvidia", "nvidia/NVIDIA-Nemotron-3-Nano-30B-A3B-Base-BF16",
+     "NemotronHForCausalLM", 31.6),
+    ("phi-1-5", "microsoft", "microsoft/phi-1_5", "PhiForCausalLM", 1.4),
+    ("phi-3-mini-128k-instruct", "microsoft", "microsoft/Phi-3-mini-128k-instruct", "Phi3ForCausalLM", 3.8),
+    ("phi-3-5-mini-instruct", "microsoft", "microsoft/Phi-3.5-mini-instruct", "Phi3ForCausalLM", 3.8),
+    ("phi-4-mini-instruct", "microsoft", "microsoft/Phi-4-mini-instruct", "Phi3ForCausalLM", 3.8),
+    ("phi-3-medium-4k-instruct", "microsoft", "microsoft/Phi-3-medium-4k-instruct", "Phi3ForCausalLM", 14.0),
+    ("phi-4", "microsoft", "microsoft/phi-4", "Phi3ForCausalLM", 14.7),
+    ("qwen1-5-7b-chat", "qwen", "Qwen/Qwen1.5-7B-Chat", _Q2, 7.7),
+    ("qwen1-5-32b-chat", "qwen", "Qwen/Qwen1.5-32B-Chat", _Q2, 32.5),
+    ("qwen1-5-72b-chat", "qwen", "Qwen/Qwen1.5-72B-Chat", _Q2, 72.3),
+    ("qwen1-5-110b-chat", "qwen", "Qwen/Qwen1.5-110B-Chat", _Q2, 111.0),
+    ("qwen2-7b-instruct", "qwen", "Qwen/Qwen2-7B-Instruct", _Q2, 7.6),
+    ("qwen2-72b-instruct", "qwen", "Qwen/Qwen2-72B-Instruct", _Q2, 72.7),
+    ("qwen2-5-0-5b", "qwen", "Qwen/Qwen2.5-0.5B", _Q2, 0.5),
+    ("qwen2-5-1-5b", "qwen", "Qwen/Qwen2.5-1.5B", _Q2, 1.5),
+    ("qwen2-5-3b", "qwen", "Qwen/Qwen2.5-3B", _Q2, 3.1),
+    ("qwen2-5-3b-instruct", "qwen", "Qwen/Qwen2.5-3B-Instruct", _Q2, 3.1),
+    ("qwen2-5-7b", "qwen", "Qwen/Qwen2.5-7B", _Q2, 7.6),
+    ("qwen2-5-14b", "qwen", "Qwen/Qwen2.5-14B", _Q2, 14.8),
+    ("qwen2-5-14b-instruct", "qwen", "Qwen/Qwen2.5-14B-Instruct", _Q2, 14.8),
+    ("qwen2-5-32b", "qwen", "Qwen/Qwen2.5-32B", _Q2, 32.8),
+    ("qwen2-5-32b-instruct", "qwen", "Qwen/Qwen2.5-32B-Instruct", _Q2, 32.8),
+    ("qwen2-5-72b", "qwen", "Qwen/Qwen2.5-72B", _Q2, 72.7),
+    ("qwen2-5-coder-7b-instruct", "qwen", "Qwen/Qwen2.5-Coder-7B-Instruct", _Q2, 7.6),
+    ("qwen2-5-coder-32b-instruct", "qwen", "Qwen/Qwen2.5-Coder-32B-Instruct", _Q2, 32.8),
+    ("skywork-or1-7b-preview", "skywork", "Skywork/Skywork-OR1-7B-Preview", _Q2, 7.6),
+    ("qwen2-vl-2b-instruct", "qwen", "Qwen/Qwen2-VL-2B-Instruct", "Qwen2VLForConditionalGeneration", 2.2, _I),
+    ("qwen2-vl-72b-instruct", "qwen", "Qwen/Qwen2-VL-72B-Instruct", "Qwen2VLForConditionalGeneration", 73.4, _I),
+    ("qwen3-0-6b", "qwen", "Qwen/Qwen3-0.6B", _Q3, 0.75),
+    ("qwen3-1-7b", "qwen", "Qwen/Qwen3-1.7B", _Q3, 2.0),
+    ("qwen3-4b", "qwen", "Qwen/Qwen3-4B", _Q3, 4.0),
+    ("qwen3-14b", "qwen", "Qwen/Qwen3-14B", _Q3, 14.8),
+    ("qwen3-32b", "qwen", "Qwen/Qwen3-32B", _Q3, 32.8),
+    ("smollm-135m", "huggingface", "HuggingFaceTB/SmolLM-135M", _L, 0.135),
+    ("smollm-360m", "huggingface", "HuggingFaceTB/SmolLM-360M", _L, 0.36),
+    ("smollm-1-7b", "huggingfacetb", "HuggingFaceTB/SmolLM-1.7B", _L, 1.7),
+    ("smollm2-1-7b-instruct", "huggingfacetb", "HuggingFaceTB/SmolLM2-1.7B-Instruct", _L, 1.7),
+    ("solar-10-7b-instruct-v1-0", "upstage", "upstage/SOLAR-10.7B-Instruct-v1.0", _L, 10.7),
+    ("starcoder2-3b", "bigcode", "bigcode/starcoder2-3b", "Starcoder2ForCausalLM", 3.0),
+    ("starcoder2-15b", "bigcode", "bigcode/starcoder2-15b", "Starcoder2ForCausalLM", 16.0),
+    ("vicuna-7b-v1-5", "lmsys", "lmsys/vicuna-7b-v1.5", _L, 6.7),
+    ("vicuna-13b-v1-5", "lmsys", "lmsys/vicuna-13b-v1.5", _L, 13.0),
+    ("xgen-7b-8k-inst", "salesforce", "Salesforce/xgen-7b-8k-inst", _L, 6.7),
+]
+_FP8 = [   # the reference's DeepSeek-V3-architecture fp8 checkpoints, served like deepseek-v3
+    ("deepseek-v3-0324", "deepseek-ai/DeepSeek-V3-0324"), ("deepseek-r1", "deepseek-ai/DeepSeek-R1"),
+    ("deepseek-r1-zero", "deepseek-ai/DeepSeek-R1-Zero"),
+]
+
+
+def _covers(g: Family, f: Family) -> bool:
+    return (g.arch == f.arch and g.quantization == f.quantization and g.diffusion == f.diffusion
+            and g.params_b * 0.85 <= f.params_b <= g.params_b * 1.15)
+
+
+def _extend() -> None:
+    for f in FAMILIES:   # the hand-picked families above all carry their own runtimes
+        if f.runtime is None:
+            f.runtime = True
+    for row in _MORE:
+        name, vendor, hf, arch, b = row[:5]
+        FAMILIES.append(Family(name, vendor, hf, arch, b, capabilities=list(row[5]) if len(row) > 5 else list(_C)))
+    for name, hf in _FP8:
+        FAMILIES.append(Family(name, "deepseek-ai", hf, "DeepseekV3ForCausalLM", 671.0, None, 1.0,
+                               args=["--enable-dp-attention", "--dp", "8"], quantization="fp8", min_tp=8))
+    for i, f in enumerate(FAMILIES):
+        if f.runtime is None:
+            f.runtime = not any(g.runtime and _covers(g, f) for g in FAMILIES[:i])
+
+
+_extend()
+
+
 def tp_for(f: Family) -> int:
     gb = f.params_b * f.bytes_per_param
     tp = f.min_tp
@@ -296,7 +430,7 @@ def _priority(f: Family) -> int:
         return (g.arch, g.quantization, size_label(g.params_b * 0.85), size_label(g.params_b * 1.15))
 
     k = key(f)
-    same = [g.name for g in FAMILIES if key(g) == k]
+    same = [g.name for g in FAMILIES if g.runtime and key(g) == k]
     return 2 + same.index(f.name) if f.name in same else 2
 
 
@@ -437,13 +571,15 @@ def generate() -> tuple[dict[str, list[dict]], dict[str, list[dict]]]:
     rts: dict[str, list[dict]] = {}
     models: dict[str, list[dict]] = {}
     for f in FAMILIES:
+        models.setdefault(f.vendor, []).append(base_model(f))
+        if not f.runtime:   # served by an earlier family's runtime (same architecture and size class)
+            continue
         docs = [runtime(f)]
         if f.pd:
             docs.append(pd_runtime(f))
         if f.multinode:
             docs.append(multinode_runtime(f))
         rts[f.name] = docs
-        models.setdefault(f.vendor, []).append(base_model(f))
     return rts, models
 
 
@@ -462,6 +598,8 @@ def write(out: Path) -> list[Path]:
         p.write_text(hdr + yaml.safe_dump_all(docs, sort_keys=False))
         paths.append(p)
     for f in FAMILIES:
+        if not f.runtime:
+            continue
         for stem, doc in isvc_samples(f).items():
             p = out / "samples" / "isvc" / f.vendor / f"{stem}.yaml"
             p.parent.mkdir(parents=True, exist_ok=True)
