@@ -186,6 +186,10 @@ class ModelRunner:
         if self.is_cuda:
             free, total = torch.cuda.mem_get_info(self.device)
             used_by_others = total - free
+            if os.environ.get("OME_KV_BUDGET_OWN") == "1":
+                # several engines share this device (1-GPU rehearsals of multi-rank runs): each
+                # sizes its KV from its own allocations, the fraction being its share of the device
+                used_by_others = torch.cuda.memory_reserved(self.device)
             budget = total * mem_fraction_static - used_by_others - 2 * (1 << 30)
             num_pages = int(max(budget, 0) // page_bytes)
         else:
