@@ -37,8 +37,9 @@ class CustomAllReduce:
         if self.world not in (2, 4, 8):
             raise ValueError(f"custom all-reduce supports 2/4/8 ranks, got {self.world}")
         self.max_bytes, self.one_shot_max, self.blocks = max_bytes, one_shot_max, blocks
-        # one-shot: 16-B vectors per lane before another workgroup is added (grid sizing)
-        self.vpt = int(os.environ.get("OME_AR_VPT", "4"))
+        # one-shot: 16-B vectors per lane before another workgroup is added (grid sizing);
+        # 0 = the measured per-size rule in _grid
+        self.vpt = int(os.environ.get("OME_AR_VPT", "0"))
         lib = _native.load("ome_comm")
         hs = lib.ome_comm_handle_size()
         sig_h, dat_h = (C.c_char * hs)(), (C.c_char * hs)()
@@ -66,7 +67,11 @@ class CustomAllReduce:
         (profiles/r03_comm_latency.txt: 1 row 6.6 us, 64 rows 28.8 us), so small messages use
         few of them -- at least 4 16-B vectors per lane (2 per lane and rank's chunk in two-shot)."""
         vec = n // 8
-        per = 512 * (2 * self.world if two_shot else self.vpt)
+        vpt = self.vpt
+        if vpt <= 0:   # measured per size (profiles/r04_comm_latency.txt: one-shot grid sweep)
+            nb = n * 2
+            vpt = 1 if nb <= 64 << 10 else 2 if nb <= 128 << 10 else 4
+        per = 512 * (2 * self.world if two_shot else vpt)
         return max(1, min(self.blocks, -(-vec // per)))
 
     def usable(self, x: torch.Tensor) -> bool:
