@@ -815,8 +815,10 @@ constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
 // only diagonal stages (key <= qpos also bounds kv_len), folds the scale into the exp2 FMA,
 // keeps per-lane partial row sums (reduced across the row's 4 lanes once, at the end) and
 // rescales O / l lazily (only when some row's max grew by more than 2^8).
-template <int SUB, int F, bool SPLIT, bool FAST = false>
-__global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
+// NW = waves per workgroup: 4 (one 32-row block per head of the kv group) or 8 (two row blocks:
+// 64-row items, every K/V stage staged once for twice the query rows, one chunk per thread).
+template <int SUB, int F, bool SPLIT, bool FAST = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ kv_lens, const int2* __restrict__ items,
@@ -841,7 +843,10 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   const int kv_len = kv_lens[s];
   const int prefix = kv_len - q_len;
   const int G = Hq / Hkv;
-  const int rows_per_item = 32 * (4 / G);
+  static_assert(NW == 4 || NW == 8, "NW");
+  static_assert(!SPLIT || NW == 4, "split partials are laid out for 4 waves");
+  constexpr int PT = 2 * 4 / NW;   // K (and V) chunks of 8 elements per thread per 32-key subtile
+  const int rows_per_item = 32 * (NW / G);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n = lane & 15, g = lane >> 4;
   const int hl = wave % G, rblk = wave / G;
@@ -880,8 +885,8 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
   // Two register stages (A, B) in flight: a tile's global loads are issued two compute phases
   // before its LDS write, so each load has ~2 x (64 MFMA + softmax) per wave to land.  With one
   // stage the loop was latency-bound at ~3.9 us per 64-key step (profiles/r03_prefill_*).
-  Raw8 rkA[SUB][2], rvA[SUB][2], rkB[SUB][2], rvB[SUB][2];
-  auto load_tile = [&](Raw8 (&rk)[SUB][2], Raw8 (&rv)[SUB][2], int kb0) {
+  Raw8 rkA[SUB][PT], rvA[SUB][PT], rkB[SUB][PT], rvB[SUB][PT];
+  auto load_tile = [&](Raw8 (&rk)[SUB][PT], Raw8 (&rv)[SUB][PT], int kb0) {
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       const int kb = kb0 + 32 * u;
@@ -889,8 +894,8 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
       const int pA = (kb < kv_len) ? bt[pi] : bt[0];  // out-of-range subtiles: any valid page (masked)
       const int pB = (kb + P < kv_len) ? bt[pi + 1] : pA;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int c = tid + 256 * i;
+      for (int i = 0; i < PT; ++i) {
+        const int c = tid + 64 * NW * i;
         const int key = c >> 4, dc = c & 15;
         const typename KVStore<F>::T* kp = k_cache + (key < 16 ? pA : pB) * kpage + (int64_t)kvh * P * D;
         rk[u][i] = k8_load<F>(kp + (key & 15) * D + dc * 8);
@@ -900,12 +905,12 @@ __global__ __launch_bounds__(256, 2) void paged_prefill_v2_kernel(
       }
     }
   };
-  auto store_tile = [&](const Raw8 (&rk)[SUB][2], const Raw8 (&rv)[SUB][2], int buf) {
+  auto store_tile = [&](const Raw8 (&rk)[SUB][PT], const Raw8 (&rv)[SUB][PT], int buf) {
 #pragma unroll
     for (int u = 0; u < SUB; ++u)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int c = tid + 256 * i;
+      for (int i = 0; i < PT; ++i) {
+        const int c = tid + 64 * NW * i;
         const int key = c >> 4, dc = c & 15;
         *reinterpret_cast<bf16x8*>(&sK[buf][u][key * PF_KLD + dc * 8]) = k8_bf16<F>(rk[u][i]);
         const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
@@ -1208,7 +1213,7 @@ static bool prefill_fast(const Scaler& scl, int window, const int* row_hi) {
 }
 
 template <int D, int F>
-static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, const void* q, int64_t q_stride,
+static void launch_prefill(int variant, int rows, int G, dim3 grid, hipStream_t stream, const void* q, int64_t q_stride,
                            const void* k_cache, const void* v_cache, const int* block_tables, int bt_stride,
                            const int* cu_q, const int* kv_lens, const int* items, void* out, int64_t out_stride,
                            int Hq, int Hkv, Scaler scl, int window, float v_scale, const float* sinks,
@@ -1216,12 +1221,17 @@ static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, co
   typedef typename KVStore<F>::T T;
   if constexpr (D == 128) {
     if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
-#define OME_PF2(FAST)                                                                                             \
-  paged_prefill_v2_kernel<2, F, false, FAST><<<grid, 256, 0, stream>>>(                                           \
+#define OME_PF2(FAST, NW)                                                                                         \
+  paged_prefill_v2_kernel<2, F, false, FAST, NW><<<grid, 64 * NW, 0, stream>>>(                                   \
       (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,      \
       (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi, 0, nullptr, nullptr)
-      if (prefill_fast(scl, window, row_hi)) OME_PF2(true);
-      else OME_PF2(false);
+      if (rows == 64) {   // 8 waves over 64-row items
+        if (prefill_fast(scl, window, row_hi)) OME_PF2(true, 8);
+        else OME_PF2(false, 8);
+      } else {
+        if (prefill_fast(scl, window, row_hi)) OME_PF2(true, 4);
+        else OME_PF2(false, 4);
+      }
 #undef OME_PF2
       return;
     }
@@ -1233,14 +1243,14 @@ static void launch_prefill(int variant, int G, dim3 grid, hipStream_t stream, co
 }
 
 template <int D>
-static void prefill_dispatch(int kv_fmt, int variant, int G, dim3 grid, hipStream_t stream, const void* q,
+static void prefill_dispatch(int kv_fmt, int variant, int rows, int G, dim3 grid, hipStream_t stream, const void* q,
                              int64_t q_stride, const void* k_cache, const void* v_cache, const int* block_tables,
                              int bt_stride, const int* cu_q, const int* kv_lens, const int* items, void* out,
                              int64_t out_stride, int Hq, int Hkv, Scaler scl, int window, float v_scale,
                              const float* sinks, const int* row_hi) {
 #define ARGS                                                                                                   \
-  variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, out, \
-      out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi
+  variant, rows, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, \
+      out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi
   if (kv_fmt == KV_BF16) launch_prefill<D, KV_BF16>(ARGS);
   else if (kv_fmt == KV_E4M3) launch_prefill<D, KV_E4M3>(ARGS);
   else launch_prefill<D, KV_E5M2>(ARGS);
@@ -1252,8 +1262,9 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
                               const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
                               int P, float scale, int window, int kv_fmt, float k_scale, float v_scale,
                               float softcap, const float* sinks, const float* alibi, const int* row_hi,
-                              hipStream_t stream) {
+                              int rows, hipStream_t stream) {
   if (n_items <= 0) return 0;
+  if (rows != 32 && rows != 64) return -2;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0) return -3;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
@@ -1263,8 +1274,8 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
   const char* ve = getenv("OME_PREFILL_ATTN");
   const int variant = ve ? atoi(ve) : 2;
 #define ARGS                                                                                                     \
-  kv_fmt, variant, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens, items, \
-      out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi
+  kv_fmt, variant, rows, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens,  \
+      items, out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi
   if (D == 64) prefill_dispatch<64>(ARGS);
   else if (D == 256) prefill_dispatch<256>(ARGS);
   else prefill_dispatch<128>(ARGS);

@@ -1022,10 +1022,11 @@ class PrefillPlan:
     [n, 2] (seq, row0) list; ``split`` [n4, 4] (seq, row0, chunk start, part) and ``comb``
     [nc, 4] (seq, row0, first part, parts) are the split-KV form (empty when nothing splits)."""
 
-    __slots__ = ("items", "split", "comb", "chunk", "parts")
+    __slots__ = ("items", "split", "comb", "chunk", "parts", "rows")
 
-    def __init__(self, items, split, comb, chunk: int, parts: int):
+    def __init__(self, items, split, comb, chunk: int, parts: int, rows: int = 32):
         self.items, self.split, self.comb, self.chunk, self.parts = items, split, comb, chunk, parts
+        self.rows = rows   # query rows per classic item (64: the 8-wave GQA-4 kernel)
 
     @property
     def shape(self):
@@ -1033,6 +1034,15 @@ class PrefillPlan:
 
 
 PREFILL_SPLIT_TARGET = int(os.environ.get("OME_PREFILL_SPLIT_ITEMS", "128"))
+# query rows per classic prefill item for the GQA-4 / D=128 kernel: 32 (4 waves) or 64 (8 waves,
+# every K/V stage shared by twice the rows)
+PREFILL_ROWS = int(os.environ.get("OME_PREFILL_ROWS", "32"))
+
+
+def prefill_rows(Hq: int, Hkv: int, D: int, page: int = 16) -> int:
+    """Rows per classic prefill work item for this attention shape (see PREFILL_ROWS)."""
+    ok = D == 128 and page == 16 and Hq == 4 * Hkv and os.environ.get("OME_PREFILL_ATTN", "2") == "2"
+    return PREFILL_ROWS if ok and PREFILL_ROWS in (32, 64) else 32
 # an item must span more than this many keys before a small grid is split.  2048 since the causal
 # fast body (profiles/r03_prefill_split_bench_fast.txt): classic now wins at 700 and 2000 keys
 # (27 vs 34 us, 85 vs 93 us) and split still wins 256 new rows over a 4096-key prefix (53 vs 132 us)
@@ -1054,17 +1064,19 @@ def prefill_plan(q_lens: list[int], kv_lens: list[int], tile: int = 32, target: 
     <= 480 keys the classic grid is already full and splitting costs the partial round trip."""
     target = target or PREFILL_SPLIT_TARGET
     items = prefill_work_items(q_lens, kv_lens, tile)
+    # the split decision and the split items use 32-row items (the split kernel's partial layout)
+    items32 = items if tile == 32 else prefill_work_items(q_lens, kv_lens, 32)
     work = 0
     ends = []
-    for s, r in items:
-        e = (kv_lens[s] - q_lens[s]) + min(r + tile, q_lens[s])
+    for s, r in items32:
+        e = (kv_lens[s] - q_lens[s]) + min(r + 32, q_lens[s])
         ends.append(e)
         work += e
-    if not force and (len(items) * kv_heads >= 256 or max(ends, default=0) <= PREFILL_SPLIT_MIN_KEYS):
+    if not force and (len(items32) * kv_heads >= 256 or max(ends, default=0) <= PREFILL_SPLIT_MIN_KEYS):
         return items, [], [], 0, 0
     chunk = max(128, -(-(-(-work // max(1, target))) // 64) * 64)
     split, comb, parts = [], [], 0
-    for (s, r), e in zip(items, ends):
+    for (s, r), e in zip(items32, ends):
         n = -(-e // chunk)
         if n <= 1:
             split.append((s, r, 0, -1))
@@ -1095,8 +1107,10 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     Tq, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     out = torch.empty_like(q) if out is None else out
+    rows = 32
     if isinstance(items, PrefillPlan):
         plan, items = items, items.items
+        rows = plan.rows
         if (plan.parts and D == 128 and P == 16 and Hq == 4 * Hkv and row_hi is None and
                 os.environ.get("OME_PREFILL_ATTN", "2") == "2"):
             po = torch.empty(plan.parts * Hkv * 4 * 32 * 128, dtype=torch.float32, device=q.device)
@@ -1112,7 +1126,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
          _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),
          int(window), kv_format(k_cache), float(k_scale), float(v_scale), float(softcap), _sinks(sinks),
-         _sinks(alibi), None if row_hi is None else _i32(row_hi).data_ptr(), stream_ptr())
+         _sinks(alibi), None if row_hi is None else _i32(row_hi).data_ptr(), rows, stream_ptr())
     return out
 
 

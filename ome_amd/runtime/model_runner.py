@@ -581,7 +581,10 @@ class ModelRunner:
                 ids[t0 + n - 1] = 0
                 any_pending = True
             last_row[i] = len(ids) - 1
-        items, split, comb, chunk, parts = ops.prefill_plan(q_lens, kv_lens, kv_heads=self.model.tp.hkv) if q_lens else ([], [], [], 0, 0)
+        tp_ = self.model.tp
+        rows = ops.prefill_rows(tp_.hq, tp_.hkv, self.cfg.head_dim, P)
+        items, split, comb, chunk, parts = ops.prefill_plan(q_lens, kv_lens, tile=rows, kv_heads=tp_.hkv) if q_lens \
+            else ([], [], [], 0, 0)
         T, S, n_it, nd, B = len(ids), len(q_lens), len(items), len(dec_lens), len(chunks)
         n_sp, n_cb = len(split), len(comb)
         cu = np.zeros(S + 1, dtype=np.int32)
@@ -627,7 +630,9 @@ class ModelRunner:
         t_items = take(2 * n_it).view(n_it, 2)
         if n_sp:   # split-KV prefill attention (ops.prefill_plan)
             t_items = ops.PrefillPlan(t_items, take(4 * n_sp).view(n_sp, 4), take(4 * n_cb).view(n_cb, 4), chunk,
-                                      parts)
+                                      parts, rows)
+        elif rows != 32 and n_it:   # 64-row classic items (the 8-wave kernel)
+            t_items = ops.PrefillPlan(t_items, t_items[:0], t_items[:0], 0, 0, rows)
         if any_pending:
             ops.fill_pending(t_ids, t_src, prev.ids_dev)
         ws = None

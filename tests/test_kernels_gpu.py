@@ -451,3 +451,21 @@ def test_paged_decode_dynamic_partitions(parts, window):
     for sk in (None, sinks):
         out = ops.paged_decode(q, kc, vc, bt, sl, D ** -0.5, ws, window=window, sinks=sk)
         _close(out, ref.paged_decode(q, kc, vc, bt, sl, D ** -0.5, window, 1.0, 1.0, 0.0, sk), atol=2e-2)
+
+
+@pytest.mark.parametrize("q_lens,kv_lens", [([5], [5]), ([37, 64, 1, 100], [37, 80, 300, 100]),
+                                            ([300], [1000]), ([1000], [1000]), ([100, 64], [164, 64])])
+@pytest.mark.parametrize("window", [-1, 100])
+def test_paged_prefill_64_row_items(q_lens, kv_lens, window):
+    """8-wave GQA-4 prefill over 64-row items (ops.PrefillPlan rows=64) == the fp32 reference."""
+    D, P, Hq, Hkv = 128, 16, 32, 8
+    npages = sum(-(-L // P) for L in kv_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    bt = _block_tables(kv_lens, P, npages)
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    items = torch.tensor(ops.prefill_work_items(q_lens, kv_lens, 64), dtype=torch.int32, device=DEV)
+    plan = ops.PrefillPlan(items, items[:0], items[:0], 0, 0, 64)
+    q = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    out = ops.paged_prefill(q, kc, vc, bt, cu, kl, plan, 0.0884, window=window)
+    _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884, window), atol=2e-2)
