@@ -60,6 +60,9 @@ COMMAND_ALIASES = [
     (re.compile(_NB + r"genai-bench\b"), f"{_PYS} -m ome_amd.bench.loadgen"),
     (re.compile(_NB + r"multinode-prober\b"), f"{_PYS} -m ome_amd.prober"),
     (re.compile(_NB + r"ome-agent\b"), f"{_PYS} -m ome_amd.agent"),
+    # Ray contract (MultiNodeRayVLLM): the rendezvous agent in place of a Ray cluster
+    (re.compile(_NB + r"ray\s+(start|stop)\b"), f"{_PYS} -m ome_amd.raylet \\1"),
+    (re.compile(r"(?:\S*/)?ray_init\.sh\b"), f"{_PYS} -m ome_amd.raylet init"),
     (re.compile(_NB + r"python3?(?=\s|$)"), _PYS),
 ]
 IMAGE_ENTRYPOINTS = {  # image (substring) -> default argv when the container has no command

@@ -20,6 +20,7 @@ from __future__ import annotations
 import copy
 import hashlib
 import json
+import sys
 
 from ome_amd.api import constants as C
 from ome_amd.controllers.runtime import Controller, Result
@@ -294,6 +295,9 @@ class KnativeController(DeploymentController):
 
 
 # ------------------------------------------------------------------ RayCluster
+RAY_PORT_ANNOTATION = "ome.io/ray-head-port"
+
+
 class RayClusterController:
     api, kind = "ray.io/v1", "RayCluster"
 
@@ -308,17 +312,33 @@ class RayClusterController:
         pods = _owned_pods(self.store, rc)
         have = {p["metadata"]["name"] for p in pods}
         head = f"{name}-head"
+        # the head's rendezvous store (ome_amd.raylet, Ray's GCS port): one port per cluster on
+        # this node, kept in an annotation so restarted pods find the same head
+        ann = rc["metadata"].get("annotations") or {}
+        port = ann.get(RAY_PORT_ANNOTATION)
+        if port is None:
+            import socket
+
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = str(sk.getsockname()[1])
+            self.store.patch(self.api, self.kind, name, {"metadata": {"annotations": {**ann, RAY_PORT_ANNOTATION: port}}},
+                             ns)
+        addr = f"127.0.0.1:{port}"
+        py = f"{sys.executable} -m ome_amd.raylet"
         if head not in have:
             self.store.create(make_pod(rc, head, rc["spec"]["headGroupSpec"]["template"],
                                        {"ray.io/cluster": name, C.RAY_NODE_TYPE_LABEL: "head"},
-                                       {"KUBERAY_GEN_RAY_START_CMD": "ray start --head"}))
+                                       {"KUBERAY_GEN_RAY_START_CMD": f"{py} start --head --port={port}",
+                                        "RAY_ADDRESS": addr, "OME_RAY_ADDRESS": addr}))
         for wg in rc["spec"].get("workerGroupSpecs") or []:
             for i in range(int(wg.get("replicas", 1))):
                 wn = f"{name}-{wg.get('groupName', 'worker')}-{i}"
                 if wn not in have:
                     self.store.create(make_pod(rc, wn, wg["template"], {"ray.io/cluster": name,
                                                                         C.RAY_NODE_TYPE_LABEL: "worker"},
-                                               {"KUBERAY_GEN_RAY_START_CMD": f"ray start --address={head}:6379"}))
+                                               {"KUBERAY_GEN_RAY_START_CMD": f"{py} start --address={addr} --block",
+                                                "RAY_ADDRESS": addr, "OME_RAY_ADDRESS": addr}))
         pods = _owned_pods(self.store, rc)
         ok = bool(pods) and all(pod_ready(p) for p in pods)
         st = {**(rc.get("status") or {}), "state": "ready" if ok else "unhealthy" if any(pod_failed(p) for p in pods) else "pending"}

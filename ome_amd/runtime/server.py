@@ -79,6 +79,8 @@ def build_parser() -> argparse.ArgumentParser:
     a("--device", default="cuda")
     a("--dist-init-addr", "--nccl-init", dest="dist_init_addr", default=None)
     a("--nnodes", type=int, default=1)
+    a("--distributed-executor-backend", dest="distributed_executor_backend", default=None,
+      help="vLLM spelling; 'ray': the group spans the nodes of a RayCluster (ome_amd.raylet)")
     a("--node-rank", type=int, default=0)
     a("--disaggregation-mode", default="null", choices=["null", "prefill", "decode"])
     a("--disaggregation-bootstrap-port", type=int, default=8998)
@@ -684,6 +686,44 @@ def _worker_main(rank: int, world: int, ns_dict: dict, addr: str, local_rank: in
     eng.run_forever()
 
 
+_RAY_STORE = None   # the head's rendezvous store client / host, alive as long as the server
+
+
+def _ray_group(ns, argv: list[str], world: int) -> None:
+    """``--distributed-executor-backend ray`` (MultiNodeRayVLLM): the TP x PP group spans the
+    RayCluster's nodes -- publish this launch for the workers' ``ome_amd.raylet`` agents and run
+    as node 0 (``ome_amd.raylet`` module doc)."""
+    global _RAY_STORE
+    from ome_amd import raylet
+
+    gpn = int(os.environ.get("OME_RAY_GPUS_PER_NODE") or 0)
+    if gpn <= 0:
+        import torch
+
+        gpn = torch.cuda.device_count() or 8   # does not initialise the GPU on this stack
+    nnodes = max(1, -(-world // gpn))
+    if nnodes == 1:
+        return
+    addr = raylet.head_address()
+    _RAY_STORE = raylet.connect_or_host(addr)
+    drop = {"--distributed-executor-backend"}
+    wargv, skip = [], False
+    for a in argv:
+        if skip:
+            skip = False
+            continue
+        if a in drop:
+            skip = True
+            continue
+        if a.split("=", 1)[0] in drop:
+            continue
+        wargv.append(a)
+    port = raylet.publish_launch(_RAY_STORE, wargv, nnodes)
+    ns.nnodes, ns.node_rank = nnodes, 0
+    ns.dist_init_addr = f"{addr.rpartition(':')[0] or '127.0.0.1'}:{port}"
+    log.info("ray backend: %d nodes x %d ranks, rendezvous %s", nnodes, world // nnodes, ns.dist_init_addr)
+
+
 def main(argv=None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     # the engine thread shares the GIL with the asyncio HTTP loop: a shorter switch interval than
@@ -699,6 +739,8 @@ def main(argv=None) -> int:
     if unknown:
         log.warning("ignoring unsupported flags: %s", " ".join(unknown))
     world = (ns.dp_size if ns.enable_dp_attention and ns.tp_size == 1 else ns.tp_size) * ns.pp_size
+    if ns.distributed_executor_backend == "ray" and world > 1 and ns.nnodes == 1:
+        _ray_group(ns, argv if argv is not None else sys.argv[1:], world)
     per_node = max(1, world // max(1, ns.nnodes))
     base_rank = ns.node_rank * per_node
     procs = []
