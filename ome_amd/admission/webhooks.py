@@ -115,6 +115,9 @@ def validate_isvc(op, obj, old, store: Store):
     cls = ann.get(C.AUTOSCALER_CLASS)
     if cls is not None and cls not in C.AUTOSCALER_CLASSES:
         raise Invalid(f"[{cls}] is not a supported autoscaler class type")
+    if cls == C.AUTOSCALER_HPA and C.AUTOSCALER_METRICS in ann and \
+            ann[C.AUTOSCALER_METRICS] not in C.AUTOSCALER_METRICS_ALLOWED:
+        raise Invalid(f"[{ann[C.AUTOSCALER_METRICS]}] is not a supported metric")
     if C.TARGET_UTILIZATION in ann:
         try:
             t = int(ann[C.TARGET_UTILIZATION])
