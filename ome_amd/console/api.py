@@ -20,6 +20,7 @@ import asyncio
 import json
 import os
 import queue
+import re
 import threading
 import time
 from pathlib import Path
@@ -77,22 +78,62 @@ class EventBroadcaster:
         self.store.unwatch(self._entry)
 
 
+_GITHUB = re.compile(r"^https?://(?:github\.com/[^/]+/[^/]+/(?:blob|raw)/[^/]+|raw\.githubusercontent\.com/[^/]+/[^/]+/[^/]+)/(.*)$")
+
+
+def _candidates(p: str, roots: list[Path]):
+    """Where a fetch-yaml argument may live: an absolute path, or -- for a catalog-relative path
+    or a GitHub blob URL of a repository laid out like the catalog (``config/runtimes/...``) --
+    that path under each root, with and without a leading ``config/``."""
+    m = _GITHUB.match(p.strip())
+    rel = m.group(1) if m else p.strip()
+    if not m and Path(rel).is_absolute():
+        yield Path(rel)
+        return
+    parts = Path(rel).parts
+    tails = [Path(*parts)] + ([Path(*parts[1:])] if len(parts) > 1 and parts[0] == "config" else [])
+    for r in roots:
+        for t in tails:
+            yield r / t
+            yield r / "runtimes" / t
+
+
 def _sanitize_yaml_path(p: str, roots: list[Path]) -> Path | None:
     """fetch-yaml only reads YAML files under the configured catalog roots (the reference
-    restricts the URL host to github.com, runtimes.go:222-326; here there is no egress)."""
-    try:
-        rp = Path(p).resolve()
-    except (OSError, RuntimeError):
-        return None
-    if rp.suffix not in (".yaml", ".yml") or not rp.is_file():
-        return None
-    for r in roots:
+    restricts the URL host to github.com, runtimes.go:222-326; here there is no egress, so a
+    GitHub URL is mapped onto the local catalog and anything outside the roots is refused)."""
+    for cand in _candidates(p, roots):
         try:
-            rp.relative_to(r.resolve())
-            return rp
-        except ValueError:
+            rp = cand.resolve()
+        except (OSError, RuntimeError):
             continue
+        if rp.suffix not in (".yaml", ".yml") or not rp.is_file():
+            continue
+        for r in roots:
+            try:
+                rp.relative_to(r.resolve())
+                return rp
+            except ValueError:
+                continue
     return None
+
+
+def _catalog(roots: list[Path], installed: set[str]) -> list[dict]:
+    """Runtime YAMLs under the catalog roots (the import page's picker)."""
+    out = []
+    for r in roots:
+        base = r / "runtimes" if (r / "runtimes").is_dir() else r
+        for f in sorted(base.rglob("*.yaml")):
+            try:
+                docs = [d for d in yaml.safe_load_all(f.read_text()) if isinstance(d, dict)]
+            except (OSError, yaml.YAMLError):
+                continue
+            rts = [d for d in docs if d.get("kind") in ("ClusterServingRuntime", "ServingRuntime")]
+            if rts:
+                name = (rts[0].get("metadata") or {}).get("name")
+                out.append({"path": str(f.relative_to(r)), "name": name, "kind": rts[0]["kind"],
+                            "installed": name in installed})
+    return out
 
 
 def create_router(store, catalog_roots: list[str] | None = None, models_root: str | None = None):
@@ -264,6 +305,12 @@ def create_router(store, catalog_roots: list[str] | None = None, models_root: st
     @r.get("/runtimes")
     def list_runtimes():
         return items("ClusterServingRuntime")
+
+    @r.get("/runtimes/catalog")
+    def runtime_catalog():
+        have = {o["metadata"]["name"] for o in store.list(API, "ClusterServingRuntime")}
+        files = _catalog(roots, have)
+        return {"files": files, "total": len(files)}
 
     @r.get("/runtimes/fetch-yaml")
     def fetch_yaml(path: str):
