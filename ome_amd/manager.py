@@ -314,6 +314,13 @@ def create_api(cluster: Cluster):
         except Exception as e:  # noqa: BLE001
             return err(e)
 
+    @app.get("/openapi/v2")
+    def openapi_v2():
+        """Swagger 2.0 of the ome.io/v1beta1 API (the SDK's source document)."""
+        from ome_amd.api.openapi import swagger
+
+        return swagger()
+
     @app.get("/healthz")
     def healthz():
         return {"status": "ok"}
