@@ -44,6 +44,9 @@ class ParallelState:
     ep_ll: object | None = None # ome_amd.parallel.ep_ll.LowLatencyEP (DP attention on one node)
     ep_ll_ok: bool = False      # this lockstep step may use it (every rank's batch fits the buckets)
     ep_ll_cap: int = 0          # tokens per rank the low-latency buckets hold
+    pp_prev: object | None = None   # CustomAllReduce over (previous stage, this stage): IPC hand-off
+    pp_next: object | None = None   # CustomAllReduce over (this stage, next stage)
+    pp_bcast: object | None = None  # CustomAllReduce over the pipeline group: sampled tokens from the last stage
 
     def to_global(self, r: int) -> int:
         return self.base + r
@@ -113,6 +116,7 @@ def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_in
                     kw["device_id"] = torch.device("cuda", lr)
             dist.init_process_group(backend=backend, init_method=init_method, rank=grk, world_size=world, **kw)
         tp_cpu = None
+        pp_groups: dict = {}
         # new_group is collective over the whole job: every rank creates every replica's groups
         for rep in range(replicas):
             b = rep * gsize
@@ -128,12 +132,22 @@ def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_in
                 gc = dist.new_group(ranks, backend="gloo") if tp_size > 1 else None
                 if mine and p == st.pp_rank:
                     st.tp_group, tp_cpu = g, gc
+            pp_cpu = {}
             for t in range(tp_size):
                 ranks = [b + p * tp_size + t for p in range(pp_size)]
                 g = dist.new_group(ranks) if pp_size > 1 else None
                 if mine and t == st.tp_rank:
                     st.pp_group = g
+                if pp_size > 1 and torch.cuda.is_available():   # gloo groups for the IPC hand-off handles
+                    pp_cpu[(t, "all")] = dist.new_group(ranks, backend="gloo")
+                    for p in range(pp_size - 1):
+                        pp_cpu[(t, p)] = dist.new_group(ranks[p:p + 2], backend="gloo")
+            if mine:
+                pp_groups = pp_cpu
         single_node = int(os.environ.get("LOCAL_WORLD_SIZE", world)) >= world
+        if torch.cuda.is_available() and pp_size > 1 and single_node and pp_size in (2, 4, 8) and \
+                os.environ.get("OME_PP_IPC", "1") != "0" and os.environ.get("OME_CUSTOM_AR", "1") != "0":
+            _pp_ipc_init(st, pp_groups)
         if torch.cuda.is_available() and tp_size in (2, 4, 8) and single_node and \
                 os.environ.get("OME_CUSTOM_AR", "1") != "0":
             from ome_amd.parallel.comm import TPCommunicator
@@ -198,9 +212,74 @@ def _pp_peer(stage: int) -> int:
     return st.base + stage * st.tp_size + st.tp_rank
 
 
-def pp_send(*tensors: torch.Tensor) -> None:
-    """Activations to the next pipeline stage (same TP rank): RCCL p2p on GPU, gloo on CPU."""
+# ------------------------------------------------------------------ pipeline hand-offs
+# On one node every stage pair has a direct xGMI link, so the stage-to-stage activations and the
+# last stage's sampled tokens move through the IPC peer kernels of ome_amd.parallel.comm (a
+# 2-rank gather per adjacent stage pair, a pp-wide gather for the tokens) instead of RCCL p2p:
+# stream-ordered device-side hand-offs with no host round trip, which is what lets a pipeline
+# stage's decode step -- receive, layers, send, token broadcast -- be ONE captured HIP graph.
+# RCCL p2p / broadcast remain for multi-node pipelines and CPU (gloo) runs.
+PP_IPC_BYTES = 64 << 20
+
+
+def _pp_ipc_init(st: ParallelState, groups: dict) -> None:
+    from ome_amd.parallel.comm import CustomAllReduce
+
+    t, p = st.tp_rank, st.pp_rank
+    try:
+        # every rank builds its comms in stage order, so each pair's two members meet in the
+        # same collective (handle exchange over that pair's gloo group)
+        for q in range(st.pp_size - 1):
+            if q == p - 1:
+                st.pp_prev = CustomAllReduce(groups[(t, q)], max_bytes=PP_IPC_BYTES, cpu_group=groups[(t, q)])
+            elif q == p:
+                st.pp_next = CustomAllReduce(groups[(t, q)], max_bytes=PP_IPC_BYTES, cpu_group=groups[(t, q)])
+        st.pp_bcast = CustomAllReduce(groups[(t, "all")], max_bytes=4 << 20, cpu_group=groups[(t, "all")])
+    except Exception as e:  # noqa: BLE001 -- e.g. peers not IPC-reachable: RCCL p2p, loudly
+        import logging
+
+        logging.getLogger("ome_amd.parallel").warning("pipeline IPC hand-off unavailable (%s); using RCCL p2p", e)
+        st.pp_prev = st.pp_next = st.pp_bcast = None
+
+
+def pp_graph_ok() -> bool:
+    """Every hand-off of a decode step is a device-side IPC kernel (HIP-graph capturable)."""
     st = _STATE
+    return st.pp_size > 1 and st.pp_bcast is not None and (st.is_first_pp or st.pp_prev is not None) and \
+        (st.is_last_pp or st.pp_next is not None)
+
+
+def _pp_ipc_cols(comm, rows: int, shapes, dtype) -> int | None:
+    """Columns of the packed [rows, cols] hand-off, or None when the IPC path does not apply
+    (sender and receiver evaluate this on the same shapes, so they always agree)."""
+    if comm is None or dtype != torch.bfloat16 or rows <= 0:
+        return None
+    cols = 0
+    for shp in shapes:
+        if len(shp) < 1 or shp[0] != rows:
+            return None
+        n = 1
+        for d in shp[1:]:
+            n *= int(d)
+        cols += n
+    if (cols * 2) % 16 or rows * cols * 2 > comm.max_bytes:
+        return None
+    return cols
+
+
+def pp_send(*tensors: torch.Tensor) -> None:
+    """Activations to the next pipeline stage (same TP rank): the IPC pair gather on one node,
+    RCCL p2p across nodes, gloo on CPU."""
+    st = _STATE
+    comm = st.pp_next if tensors and tensors[0].is_cuda else None
+    rows = tensors[0].shape[0] if tensors else 0
+    dts = {t.dtype for t in tensors}
+    cols = _pp_ipc_cols(comm, rows, [tuple(t.shape) for t in tensors], dts.pop() if len(dts) == 1 else None)
+    if cols is not None:
+        packed = torch.cat([t.reshape(rows, -1) for t in tensors], dim=1) if len(tensors) > 1 else \
+            tensors[0].reshape(rows, -1).contiguous()
+        comm.all_gather_last(packed)   # the receiver takes the sender's (first) half
+        return
     dst = _pp_peer(st.pp_rank + 1)
     for t in tensors:
         dist.send(t.contiguous(), dst=dst)
@@ -208,6 +287,22 @@ def pp_send(*tensors: torch.Tensor) -> None:
 
 def pp_recv(*like: tuple[tuple, torch.dtype, torch.device]) -> list[torch.Tensor]:
     st = _STATE
+    dev = torch.device(like[0][2]) if like else torch.device("cpu")
+    comm = st.pp_prev if dev.type == "cuda" else None
+    rows = like[0][0][0] if like and like[0][0] else 0
+    dts = {dt for _, dt, _ in like}
+    cols = _pp_ipc_cols(comm, rows, [tuple(s) for s, _, _ in like], dts.pop() if len(dts) == 1 else None)
+    if cols is not None:
+        dummy = torch.empty(rows, cols, dtype=torch.bfloat16, device=dev)
+        got = comm.all_gather_last(dummy)[:, :cols]
+        out, c0 = [], 0
+        for shape, _dt, _d in like:
+            n = 1
+            for d in shape[1:]:
+                n *= int(d)
+            out.append(got[:, c0:c0 + n].contiguous().view(*shape))
+            c0 += n
+        return out
     src = _pp_peer(st.pp_rank - 1)
     out = []
     for shape, dtype, device in like:
@@ -223,6 +318,26 @@ def pp_broadcast_from_last(t: torch.Tensor) -> torch.Tensor:
     if st.pp_size > 1:
         dist.broadcast(t, src=_pp_peer(st.pp_size - 1), group=st.pp_group)
     return t
+
+
+def pp_broadcast_tokens(ids: torch.Tensor, logprobs: torch.Tensor) -> None:
+    """Sampled ids (int32) and log-probs (fp32) of the last stage -> every stage, in place.  On
+    the IPC path both ride one pp-wide gather of 16-B rows (id, logprob bits, 2 pad words)."""
+    st = _STATE
+    if st.pp_size == 1:
+        return
+    n = ids.shape[0]
+    if st.pp_bcast is not None and ids.is_cuda and n and n * 16 <= st.pp_bcast.max_bytes:
+        row = torch.zeros(n, 4, dtype=torch.int32, device=ids.device)
+        row[:, 0] = ids
+        row[:, 1] = logprobs.float().view(torch.int32)
+        g = st.pp_bcast.all_gather_last(row.view(torch.bfloat16)).view(torch.int32)   # [n, 4 * pp]
+        last = g[:, 4 * (st.pp_size - 1):4 * (st.pp_size - 1) + 2]
+        ids.copy_(last[:, 0])
+        logprobs.copy_(last[:, 1].contiguous().view(torch.float32))
+        return
+    pp_broadcast_from_last(ids)
+    pp_broadcast_from_last(logprobs)
 
 
 def destroy() -> None:

@@ -175,6 +175,9 @@ class Engine:
         self.metrics.host_times = self.host_times
         ov = self.runner.is_cuda if args.overlap_schedule is None else bool(args.overlap_schedule)
         self.overlap = ov and not self.cfg.is_embedding and self.pstate.pp_size == 1 and not self.dp
+        # DP attention overlaps too: step k+1 (this rank's part of the lockstep forward) is enqueued
+        # before step k's tokens are read back; the relay then carries step k's tokens
+        self.dp_overlap = ov and self.dp and not self.cfg.is_embedding
 
     # ------------------------------------------------------------------ API
     def make_request(self, prompt_ids: list[int], params: SamplingParams | None = None, **kw) -> Request:
@@ -420,39 +423,37 @@ class Engine:
             bufs = [torch.cat([torch.tensor([0.0, float(len(pl))], dtype=torch.float64), pl]) for pl in payloads]
         if self.pstate.rank == 0:
             done += self._dp_apply_updates(bufs)
+        prev = self._inflight if self.dp_overlap else None
+        completed = None
         if not any(allw):
+            if prev is not None:   # nothing new anywhere: drain the step still in flight
+                done += self._complete(*prev)
+                completed, self._inflight = prev[0], None
+            self._dp_relay(completed)
             return done
         # every rank sees the same token counts, so all pick the same MoE exchange mode: the
         # device-only low-latency buckets when every rank's batch fits, RCCL all-to-all otherwise
         st = self.pstate
         st.ep_ll_ok = st.ep_ll is not None and max(allw) <= st.ep_ll_cap
-        touched = []
+        launched = None
         if batch is not None:
             t0 = time.perf_counter()
-            handle = self.runner.launch(batch, allow_graph=st.ep_ll_ok)
+            handle = self.runner.launch(batch, prev[1] if prev is not None else None, allow_graph=st.ep_ll_ok)
             self.scheduler.launch_commit(batch)
-            done += self._complete(batch, handle, t0)
-            touched = list({id(c.req): c.req for c in batch.chunks}.values())
+            launched = (batch, handle, t0)
         elif st.ep_ll_ok:
             self.runner.idle_decode()
         else:
             self.runner.idle_forward()
-        if self.pstate.rank != 0 and touched:
-            # [n_updates, then per update handle, n_tokens, finished, reason code, and the tokens;
-            # then all log-probs] -- relayed with the next step's all-gather
-            packed: list[float] = [0.0]
-            lps_all: list[float] = []
-            for r in touched:
-                k = getattr(r, "_reported", 0)
-                toks = r.output_ids[k:]
-                fin = r.state == ReqState.FINISHED
-                packed += [float(getattr(r, "dp_handle", -1)), float(len(toks)), float(fin),
-                           float(_REASON_CODE.get(r.finish_reason, _unknown_code(r.finish_reason)) if fin else -1)]
-                packed += [float(t) for t in toks]
-                lps_all += [float(x) for x in r.output_logprobs[k:]]
-                r._reported = len(r.output_ids)
-                packed[0] += 1
-            self._dp_pending = packed + lps_all
+        if self.dp_overlap:
+            if prev is not None:
+                done += self._complete(*prev)
+                completed = prev[0]
+            self._inflight = launched
+        elif launched is not None:
+            done += self._complete(*launched)
+            completed = batch
+        self._dp_relay(completed)
         self._dp_steps = getattr(self, "_dp_steps", 0) + 1
         n = self.args.eplb_rebalance_steps
         if n and self._dp_steps % n == 0:  # every rank reaches this point in the same lockstep step
@@ -462,6 +463,35 @@ class Engine:
             if imb:
                 log.info("EPLB round: max/mean expert load per rank %.3f", max(imb.values()))
         return done
+
+    def _dp_relay(self, completed) -> None:
+        """Follower: pack the tokens ``completed`` (the step whose ids just reached the host)
+        gave this rank's requests, for the next step's all-gather: [n_updates, then per update
+        handle, n_tokens, finished, reason code, and the tokens; then all log-probs].  Only
+        resolved tokens travel -- under overlap the rows of the step in flight are PENDING."""
+        if self.pstate.rank == 0 or completed is None:
+            return
+        touched = list({id(c.req): c.req for c in completed.chunks}.values())
+        if not touched:
+            return
+        packed: list[float] = [0.0]
+        lps_all: list[float] = []
+        for r in touched:
+            k = getattr(r, "_reported", 0)
+            end = len(r.output_ids) - r.n_pending
+            toks = r.output_ids[k:end]
+            fin = r.state == ReqState.FINISHED
+            if (not toks and not fin) or getattr(r, "_fin_reported", False):
+                continue   # (a finished request can sit in the next in-flight step as a dead row)
+            r._fin_reported = fin
+            packed += [float(getattr(r, "dp_handle", -1)), float(len(toks)), float(fin),
+                       float(_REASON_CODE.get(r.finish_reason, _unknown_code(r.finish_reason)) if fin else -1)]
+            packed += [float(t) for t in toks]
+            lps_all += [float(x) for x in r.output_logprobs[k:end]]
+            r._reported = end
+            packed[0] += 1
+        if packed[0]:
+            self._dp_pending = packed + lps_all
 
     def _dp_gather_updates(self, mine_list: list[float]) -> list[torch.Tensor]:
         """Two-phase fallback of the update relay (sizes all-gather, then a padded gather to rank

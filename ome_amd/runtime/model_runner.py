@@ -233,10 +233,13 @@ class ModelRunner:
         self.counts = torch.zeros(max_running + 1, cfg.vocab_size, dtype=torch.int32, device=self.device)
         self.graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_pool = None
-        # pipeline stages run eagerly: the stage hand-off is a blocking p2p exchange; DP attention
-        # replays graphs only with the low-latency EP exchange (cuda_graph=None: "if possible")
+        # pipeline stages capture their decode step when every hand-off is an IPC peer kernel
+        # (pstate.pp_graph_ok: one node); across nodes they run eagerly over RCCL p2p.  DP
+        # attention replays graphs only with the low-latency EP exchange (cuda_graph=None: "if possible")
         dp_ok = pstate.get().ep_size <= 1 or self.ep_ll
-        self.use_graph = bool(cuda_graph) and self.is_cuda and not self.pp and dp_ok and \
+        pp_ok = not self.pp or (pstate.pp_graph_ok() and os.environ.get("OME_PP_GRAPHS", "1") == "1"
+                                and not self.stateful)
+        self.use_graph = bool(cuda_graph) and self.is_cuda and pp_ok and dp_ok and \
             not getattr(self.model, "encoder_only", False)
         if self.use_graph:
             self.capture_graphs()
@@ -269,12 +272,15 @@ class ModelRunner:
         if self.stateful:  # one-row sequences continuing each request slot's state
             meta.extra["ssm"] = (self._ssm_cu[:bs + 1], d.view("req_idx", bs), self._ssm_zero[:bs])
         hidden = self.model.forward(d.view("ids", bs), meta, self.kv)
-        logits = self.model.compute_logits(hidden)
-        pen = (d.view("rep", bs), d.view("freq", bs), d.view("pres", bs))
-        ops.apply_penalties(logits, self.counts, d.view("req_idx", bs), *pen)
-        ops.sample(logits, d.view("temp", bs), d.view("top_k", bs), d.view("top_p", bs), d.view("min_p", bs),
-                   d.view("seeds", bs), 0, out_ids=self.out_ids[:bs], out_logprob=self.out_lp[:bs])
-        ops.update_counts(self.counts, d.view("req_idx", bs), self.out_ids[:bs], *pen)
+        if hidden is not None:   # (an earlier pipeline stage returns None: it samples nothing)
+            logits = self.model.compute_logits(hidden)
+            pen = (d.view("rep", bs), d.view("freq", bs), d.view("pres", bs))
+            ops.apply_penalties(logits, self.counts, d.view("req_idx", bs), *pen)
+            ops.sample(logits, d.view("temp", bs), d.view("top_k", bs), d.view("top_p", bs), d.view("min_p", bs),
+                       d.view("seeds", bs), 0, out_ids=self.out_ids[:bs], out_logprob=self.out_lp[:bs])
+            ops.update_counts(self.counts, d.view("req_idx", bs), self.out_ids[:bs], *pen)
+        if self.pp:   # the last stage's tokens -> every stage, inside the same graph (IPC gather)
+            pstate.pp_broadcast_tokens(self.out_ids[:bs], self.out_lp[:bs])
 
     # ------------------------------------------------------------------ GEMM tuning
     TUNED_DIR = Path(__file__).resolve().parent.parent / "_tuned"
@@ -376,7 +382,7 @@ class ModelRunner:
         if self.probe_log is not None:
             self.probe = (time.perf_counter(), prev.event if prev is not None else None)
         self.slots.flush()
-        if batch.mode == "decode" and not self.pp and all(c.length == 1 for c in batch.chunks):
+        if batch.mode == "decode" and (not self.pp or self.use_graph) and all(c.length == 1 for c in batch.chunks):
             bs = next((b for b in self.buckets if b >= len(batch.chunks)), None)
             if bs is not None:
                 return self._launch_decode(batch, bs, prev, graph=allow_graph)
@@ -537,8 +543,7 @@ class ModelRunner:
         else:
             out_ids, out_lp = self._eager_forward(chunks, prev, batch.mode)
         if self.pp:
-            pstate.pp_broadcast_from_last(out_ids)
-            pstate.pp_broadcast_from_last(out_lp)
+            pstate.pp_broadcast_tokens(out_ids, out_lp)
         return self._finish_launch(out_ids, out_lp, len(chunks))
 
     def _eager_forward(self, chunks, prev: "StepHandle | None", mode: str) -> tuple[torch.Tensor, torch.Tensor]:

@@ -19,13 +19,14 @@ from tests.test_moe_cpu import _export_hf
 PROMPTS = [[3 + (i * 37 + j) % 1000 for j in range(5 + 7 * i)] for i in range(5)]
 
 
-def _worker(rank, world, port, path, q, relay_cap=None):
+def _worker(rank, world, port, path, q, relay_cap=None, overlap=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     from ome_amd.runtime.engine import Engine, EngineArgs
     from ome_amd.runtime.request import SamplingParams
 
     eng = Engine(EngineArgs(model_path=path, tp_size=world, dp_size=world, enable_dp_attention=True, device="cpu",
-                            max_running_requests=8, context_length=256, dtype="float32"))
+                            max_running_requests=8, context_length=256, dtype="float32", overlap_schedule=overlap))
+    assert eng.dp_overlap == bool(overlap)
     if relay_cap is not None:   # force the two-phase relay fallback on every step
         eng._dp_cap = relay_cap
     m = eng.runner.model
@@ -62,9 +63,12 @@ def _checkpoint(tmp_path, kind):
 
 
 @pytest.mark.timeout(400)
-@pytest.mark.parametrize("kind,relay_cap", [("qwen3-moe", None), ("deepseek-v3", None), ("qwen3-moe", 3),
-                                            ("gpt-oss", None), ("olmoe", None), ("dbrx", None), ("minimax_m2", None)])
-def test_dp_attention_ep_matches_single(tmp_path, kind, relay_cap):
+@pytest.mark.parametrize("kind,relay_cap,overlap", [
+    ("qwen3-moe", None, None), ("deepseek-v3", None, None), ("qwen3-moe", 3, None), ("gpt-oss", None, None),
+    ("olmoe", None, None), ("dbrx", None, None), ("minimax_m2", None, None),
+    # overlapped DP steps (the GPU default): step k+1 enqueued before step k's tokens are read back
+    ("qwen3-moe", None, True), ("deepseek-v3", None, True), ("qwen3-moe", 3, True)])
+def test_dp_attention_ep_matches_single(tmp_path, kind, relay_cap, overlap):
     _checkpoint(tmp_path, kind)
     from ome_amd.runtime.engine import Engine, EngineArgs
     from ome_amd.runtime.request import SamplingParams
@@ -77,7 +81,7 @@ def test_dp_attention_ep_matches_single(tmp_path, kind, relay_cap):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q, relay_cap)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q, relay_cap, overlap)) for r in range(2)]
     for p in ps:
         p.start()
     got, owners = q.get(timeout=300)
