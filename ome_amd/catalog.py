@@ -316,6 +316,9 @@ _FP8 = [   # the reference's DeepSeek-V3-architecture fp8 checkpoints, served li
 ]
 
 
+_PD_MORE = {"llama-3-1-70b-instruct", "llama-3-3-70b-instruct", "llama-3-2-1b-instruct", "llama-3-2-3b-instruct"}
+
+
 def _covers(g: Family, f: Family) -> bool:
     return (g.arch == f.arch and g.quantization == f.quantization and g.diffusion == f.diffusion
             and g.params_b * 0.85 <= f.params_b <= g.params_b * 1.15)
@@ -331,9 +334,14 @@ def _extend() -> None:
     for name, hf in _FP8:
         FAMILIES.append(Family(name, "deepseek-ai", hf, "DeepseekV3ForCausalLM", 671.0, None, 1.0,
                                args=["--enable-dp-attention", "--dp", "8"], quantization="fp8", min_tp=8))
-    for i, f in enumerate(FAMILIES):
+    for f in FAMILIES:
+        # every catalog model carries its own runtime, as in the reference catalog (look-alikes of
+        # one size class are opt-in by name, see _lookalike); the reference's PD
+        # runtimes exist for these too
         if f.runtime is None:
-            f.runtime = not any(g.runtime and _covers(g, f) for g in FAMILIES[:i])
+            f.runtime = True
+        if f.name in _PD_MORE:
+            f.pd = True
 
 
 _extend()
@@ -422,21 +430,27 @@ def _formats(f: Family, priority: int = 2) -> list[dict]:
              **({"quantization": f.quantization} if f.quantization else {})}]
 
 
-def _priority(f: Family) -> int:
-    """Runtimes that auto-select for the same format / architecture / size range must carry
-    distinct priorities (the ServingRuntime admission rule, ``servingruntime_webhook.go:202``):
-    the first family keeps 2, later look-alikes (e.g. Llama-3 8B vs 3.1 8B) step up by one."""
+def _lookalike(f: Family) -> int:
+    """Position of ``f`` among the runtime families of its format / architecture / size range.
+    Two auto-selecting runtimes of one such class would need distinct priorities (the
+    ServingRuntime admission rule, ``servingruntime_webhook.go:202``), and the higher one would
+    then win for every model of the class.  So the first family of a class auto-selects and its
+    look-alikes (e.g. Llama-3.1 8B next to Llama-3 8B, Vicuna next to Llama-2 13B) are opt-in by
+    runtime name -- every model still lands on a runtime of its own size class."""
     def key(g: Family):
         return (g.arch, g.quantization, size_label(g.params_b * 0.85), size_label(g.params_b * 1.15))
 
     k = key(f)
     same = [g.name for g in FAMILIES if g.runtime and key(g) == k]
-    return 2 + same.index(f.name) if f.name in same else 2
+    return same.index(f.name) if f.name in same else 0
 
 
 def _spec_base(f: Family) -> dict:
     lo, hi = f.params_b * 0.85, f.params_b * 1.15
-    return {"disabled": False, "supportedModelFormats": _formats(f, _priority(f)), "protocolVersions": ["openAI"],
+    fmts = _formats(f, 2)
+    if _lookalike(f):
+        fmts[0]["autoSelect"] = False
+    return {"disabled": False, "supportedModelFormats": fmts, "protocolVersions": ["openAI"],
             "modelSizeRange": {"min": size_label(lo), "max": size_label(hi)},
             "acceleratorRequirements": {"acceleratorClasses": ["amd-mi355x", "amd-mi300x"]}}
 
