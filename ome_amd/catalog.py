@@ -203,6 +203,26 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_EMBEDDINGS", "EMBEDDING"], args=["--is-embedding"]),
     Family("e5-mistral-7b-instruct", "intfloat", "intfloat/e5-mistral-7b-instruct", "MistralModel", 7.1,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    # embedding / reward checkpoints of generative architectures (pooled or scored, --is-embedding)
+    Family("qwen3-embedding-0-6b", "qwen", "Qwen/Qwen3-Embedding-0.6B", "Qwen3ForCausalLM", 0.6,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("qwen3-embedding-4b", "qwen", "Qwen/Qwen3-Embedding-4B", "Qwen3ForCausalLM", 4.0,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("qwen3-embedding-8b", "qwen", "Qwen/Qwen3-Embedding-8B", "Qwen3ForCausalLM", 7.6,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("gte-qwen2-7b-instruct", "alibaba-nlp", "Alibaba-NLP/gte-Qwen2-7B-instruct", "Qwen2ForCausalLM", 7.6,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("skywork-reward-llama-3-1-8b-v0-2", "skywork", "Skywork/Skywork-Reward-Llama-3.1-8B-v0.2",
+           "LlamaForSequenceClassification", 7.5, capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("qwen2-5-math-rm-72b", "qwen", "Qwen/Qwen2.5-Math-RM-72B", "Qwen2ForRewardModel", 72.7,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("qwen2-5-1-5b-apeach", "jason9693", "jason9693/Qwen2.5-1.5B-apeach", "Qwen2ForSequenceClassification", 1.5,
+           capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    # fp8 checkpoints of served architectures (dequantised per 128x128 block at load, fp8 GEMMs)
+    Family("llama-3-3-70b-instruct-fp8-dynamic", "redhatai", "RedHatAI/Llama-3.3-70B-Instruct-FP8-dynamic",
+           "LlamaForCausalLM", 70.6, None, 1.0, quantization="fp8"),
+    Family("nvidia-nemotron-3-nano-30b-a3b-fp8", "nvidia", "nvidia/NVIDIA-Nemotron-3-Nano-30B-A3B-FP8",
+           "NemotronHForCausalLM", 31.6, None, 1.0, quantization="fp8"),
 ]
 
 
@@ -441,14 +461,22 @@ def _lookalike(f: Family) -> int:
         return (g.arch, g.quantization, size_label(g.params_b * 0.85), size_label(g.params_b * 1.15))
 
     k = key(f)
-    same = [g.name for g in FAMILIES if g.runtime and key(g) == k]
+    same = [g.name for g in FAMILIES if g.runtime and key(g) == k and not _pooled_twin(g)]
     return same.index(f.name) if f.name in same else 0
+
+
+def _pooled_twin(f: Family) -> bool:
+    """An embedding / reward checkpoint of an architecture that also has generative runtimes:
+    runtime selection does not look at capabilities, so its (pooling) runtime is opt-in by name
+    and never captures the generative models of its size class."""
+    return "--is-embedding" in f.args and any(g.arch == f.arch and "--is-embedding" not in g.args
+                                              for g in FAMILIES if g.runtime)
 
 
 def _spec_base(f: Family) -> dict:
     lo, hi = f.params_b * 0.85, f.params_b * 1.15
     fmts = _formats(f, 2)
-    if _lookalike(f):
+    if _lookalike(f) or _pooled_twin(f):
         fmts[0]["autoSelect"] = False
     return {"disabled": False, "supportedModelFormats": fmts, "protocolVersions": ["openAI"],
             "modelSizeRange": {"min": size_label(lo), "max": size_label(hi)},

@@ -74,8 +74,15 @@ def test_selector_picks_catalog_runtime_for_each_base_model():
     for docs in models.values():
         for m in docs:
             spec = V.BaseModelSpec.model_validate(m["spec"])
-            got = sel.select(spec, None, "default").name
             f = next(f for f in catalog.FAMILIES if f.name == m["metadata"]["name"])
+            if catalog._pooled_twin(f):
+                # embedding / reward checkpoint of a generative architecture: its pooling runtime is
+                # opt-in (validated for the model by name), and the catalog's ISVC sample names it
+                own = f"ome-amd-{f.name}-tp{catalog.tp_for(f)}"
+                assert catalog.isvc_samples(f)[f.name]["spec"]["runtime"]["name"] == own
+                sel.validate(own, spec, None, "default")
+                continue
+            got = sel.select(spec, None, "default").name
             if not f.runtime:
                 # model-only entry: served by a runtime family of the same architecture / quantisation
                 # whose size class covers it
