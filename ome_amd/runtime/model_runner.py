@@ -222,6 +222,10 @@ class ModelRunner:
         self.dbuf = _DecodeBuffers(self.bmax, self.device)
         self.out_ids = torch.zeros(self.bmax, dtype=torch.int32, device=self.device)
         self.out_lp = torch.zeros(self.bmax, dtype=torch.float32, device=self.device)
+        # pipeline stages decode in micro-batches (stage s works on micro-batch i while stage s+1
+        # works on i-1); each micro-batch slot has its own input / output buffers and graphs
+        self.dbufs = [self.dbuf]
+        self.mb_out = [(self.out_ids, self.out_lp)]
         # pinned landing zone for sampled ids / logprobs, double-buffered so step k+1 can be
         # enqueued while the host still reads step k (overlapped scheduling)
         nout = max(self.bmax, max_running + 8)
@@ -237,10 +241,20 @@ class ModelRunner:
         # (pstate.pp_graph_ok: one node); across nodes they run eagerly over RCCL p2p.  DP
         # attention replays graphs only with the low-latency EP exchange (cuda_graph=None: "if possible")
         dp_ok = pstate.get().ep_size <= 1 or self.ep_ll
-        pp_ok = not self.pp or (pstate.pp_graph_ok() and os.environ.get("OME_PP_GRAPHS", "1") == "1"
+        # opt-in (OME_PP_GRAPHS=1): on the one-GPU rehearsal (both stages sharing GPU 0) the eager
+        # micro-batched steps measured faster (profiles/r04_pp2_rehearsal.txt); distinct-GPU
+        # pipelines are unmeasured
+        pp_ok = not self.pp or (pstate.pp_graph_ok() and os.environ.get("OME_PP_GRAPHS", "0") == "1"
                                 and not self.stateful)
         self.use_graph = bool(cuda_graph) and self.is_cuda and pp_ok and dp_ok and \
             not getattr(self.model, "encoder_only", False)
+        self.mb_graphs: list[dict[int, torch.cuda.CUDAGraph]] = [self.graphs]
+        if self.use_graph and self.pp:
+            for _ in range(pstate.get().pp_size - 1):
+                self.dbufs.append(_DecodeBuffers(self.bmax, self.device))
+                self.mb_out.append((torch.zeros(self.bmax, dtype=torch.int32, device=self.device),
+                                    torch.zeros(self.bmax, dtype=torch.float32, device=self.device)))
+                self.mb_graphs.append({})
         if self.use_graph:
             self.capture_graphs()
 
@@ -264,8 +278,9 @@ class ModelRunner:
             self._ws_cache[bs] = ws
         return ws
 
-    def _decode_forward(self, bs: int) -> None:
-        d = self.dbuf
+    def _decode_forward(self, bs: int, m: int = 0) -> None:
+        d = self.dbufs[m]
+        out_ids, out_lp = self.mb_out[m]
         bt = self.slots.table.index_select(0, d.view("req_idx", bs))
         meta = AttnMeta("decode", d.view("pos", bs), d.view("slots", bs), bt, seq_lens=d.view("seq_lens", bs),
                         decode_ws=self.decode_ws(bs), order=d.view("order", bs))
@@ -277,10 +292,11 @@ class ModelRunner:
             pen = (d.view("rep", bs), d.view("freq", bs), d.view("pres", bs))
             ops.apply_penalties(logits, self.counts, d.view("req_idx", bs), *pen)
             ops.sample(logits, d.view("temp", bs), d.view("top_k", bs), d.view("top_p", bs), d.view("min_p", bs),
-                       d.view("seeds", bs), 0, out_ids=self.out_ids[:bs], out_logprob=self.out_lp[:bs])
-            ops.update_counts(self.counts, d.view("req_idx", bs), self.out_ids[:bs], *pen)
-        if self.pp:   # the last stage's tokens -> every stage, inside the same graph (IPC gather)
-            pstate.pp_broadcast_tokens(self.out_ids[:bs], self.out_lp[:bs])
+                       d.view("seeds", bs), 0, out_ids=out_ids[:bs], out_logprob=out_lp[:bs])
+            ops.update_counts(self.counts, d.view("req_idx", bs), out_ids[:bs], *pen)
+        # (pipeline stages: the last stage's tokens reach every stage in ONE broadcast after all
+        # micro-batches, _launch_decode -- a per-micro-batch broadcast would hold stage 0 inside
+        # micro-batch i until the last stage had sampled it, serialising the pipeline)
 
     # ------------------------------------------------------------------ GEMM tuning
     TUNED_DIR = Path(__file__).resolve().parent.parent / "_tuned"
@@ -332,14 +348,14 @@ class ModelRunner:
     def capture_graphs(self) -> None:
         t0 = time.perf_counter()
         tuning = self._tuning_begin()
-        d = self.dbuf
-        d.hnp[:] = 0
-        d.hnp[d.off["slots"]:d.off["slots"] + d.bmax] = -1
-        for name, v in (("rep", 1.0), ("top_p", 1.0)):   # neutral sampling params for the warm-up rows
-            d.hf[d.off[name]:d.off[name] + d.bmax] = v
-        d.hnp[d.off["top_k"]:d.off["top_k"] + d.bmax] = -1
-        d.sync_images()
-        d.dev.copy_(d.host)
+        for d in self.dbufs:
+            d.hnp[:] = 0
+            d.hnp[d.off["slots"]:d.off["slots"] + d.bmax] = -1
+            for name, v in (("rep", 1.0), ("top_p", 1.0)):   # neutral sampling params for the warm-up rows
+                d.hf[d.off[name]:d.off[name] + d.bmax] = v
+            d.hnp[d.off["top_k"]:d.off["top_k"] + d.bmax] = -1
+            d.sync_images()
+            d.dev.copy_(d.host)
         torch.cuda.synchronize(self.device)
         stream = torch.cuda.Stream(self.device)
         stream.wait_stream(torch.cuda.current_stream(self.device))
@@ -352,15 +368,16 @@ class ModelRunner:
         if tuning:
             self._tuning_end()
             log.info("GEMM tuning pass done in %.1fs", time.perf_counter() - t0)
-        for bs in reversed(self.buckets):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=self.graph_pool):
-                self._decode_forward(bs)
-            if self.graph_pool is None:
-                self.graph_pool = g.pool()
-            self.graphs[bs] = g
+        for m, graphs in enumerate(self.mb_graphs):   # (one slot unless this is a pipeline stage)
+            for bs in reversed(self.buckets):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.graph_pool):
+                    self._decode_forward(bs, m)
+                if self.graph_pool is None:
+                    self.graph_pool = g.pool()
+                graphs[bs] = g
         torch.cuda.synchronize(self.device)
-        log.info("captured %d decode graphs in %.1fs", len(self.graphs), time.perf_counter() - t0)
+        log.info("captured %d decode graphs in %.1fs", sum(len(g) for g in self.mb_graphs), time.perf_counter() - t0)
 
     @staticmethod
     def _seed(req, pos: int) -> int:
@@ -460,7 +477,32 @@ class ModelRunner:
     def _launch_decode(self, batch: StepBatch, bs: int, prev: "StepHandle | None",
                        graph: bool = True) -> "StepHandle":
         B = len(batch.chunks)
-        d = self.dbuf
+        n_mb = min(self.pp_microbatches or len(self.mb_graphs), len(self.mb_graphs), B) if self.pp else 1
+        if n_mb > 1 and self.use_graph and graph:
+            # pipeline stage: micro-batch i's graph (receive, layers, send, token broadcast) runs
+            # while the next stage still works on micro-batch i-1
+            ids, lps = [], []
+            for m, part in enumerate(_split_balanced(batch.chunks, n_mb)):
+                bs_m = next(b for b in self.buckets if b >= len(part))
+                self._fill_decode(self.dbufs[m], part, bs_m, prev)
+                self.mb_graphs[m][bs_m].replay()
+                ids.append(self.mb_out[m][0][:len(part)])
+                lps.append(self.mb_out[m][1][:len(part)])
+            out_ids, out_lp = torch.cat(ids), torch.cat(lps)
+            pstate.pp_broadcast_tokens(out_ids, out_lp)
+            return self._finish_launch(out_ids, out_lp, B)
+        self._fill_decode(self.dbuf, batch.chunks, bs, prev)
+        if self.use_graph and graph:
+            self.graphs[bs].replay()
+        else:
+            self._decode_forward(bs)
+        if self.pp:
+            pstate.pp_broadcast_tokens(self.out_ids[:B], self.out_lp[:B])
+        return self._finish_launch(self.out_ids, self.out_lp, B)
+
+    def _fill_decode(self, d: "_DecodeBuffers", chunks, bs: int, prev: "StepHandle | None") -> None:
+        """Host-side fields of a decode (micro-)batch -> ``d``'s pinned image -> one H2D copy."""
+        B = len(chunks)
         d.next_host()
         h, hf, off = d.hnp, d.hf, d.off
         h[off["ids"]:off["ids"] + bs] = 0
@@ -474,7 +516,7 @@ class ModelRunner:
         P = self.P
         toks, poss, slots, lens, rsl, srcs, sds = [], [], [], [], [], [], []
         tk, tmp, tp, mp, rep, frq, prs = [], [], [], [], [], [], []
-        for c in batch.chunks:  # python lists, one numpy store per field (not per element)
+        for c in chunks:  # python lists, one numpy store per field (not per element)
             r = c.req
             pos = c.start
             src = self._src_row(r, pos, prev)
@@ -510,17 +552,12 @@ class ModelRunner:
             h[off["top_k"] + B:off["top_k"] + bs] = -1
         # attention visits sequences longest-first (padding rows, seq_len 0, last)
         h[off["order"]:off["order"] + bs] = np.argsort(-h[off["seq_lens"]:off["seq_lens"] + bs], kind="stable")
-        self._init_penalty_rows(batch.chunks)
+        self._init_penalty_rows(chunks)
         self._probe_mark("decode")
         copy_h2d(d.dev, d.host) if self.is_cuda else d.dev.copy_(d.host)
         d.copied()
         if any_pending:
             ops.fill_pending(d.view("ids", bs), d.view("src", bs), prev.ids_dev)
-        if self.use_graph and graph:
-            self.graphs[bs].replay()
-        else:
-            self._decode_forward(bs)
-        return self._finish_launch(self.out_ids, self.out_lp, B)
 
     pp_microbatches = 0   # pipeline parallel: micro-batches per step (0 = one per stage)
 
