@@ -278,6 +278,10 @@ _MORE = [
     ("unsloth-llama-3-2-11b-vision-instruct", "unsloth", "unsloth/Llama-3.2-11B-Vision-Instruct",
      "MllamaForConditionalGeneration", 10.7, _I),
     ("llava-v1-5-7b", "llava", "liuhaotian/llava-v1.5-7b", "LlavaLlamaForCausalLM", 7.1, _V),
+    # LLaVA-1.6 / NeXT (anyres): same original layout, the model class follows the checkpoint config
+    ("llava-v1-6-vicuna-7b", "liuhaotian", "liuhaotian/llava-v1.6-vicuna-7b", "LlavaLlamaForCausalLM", 7.1, _V),
+    ("llava-v1-6-vicuna-13b", "liuhaotian", "liuhaotian/llava-v1.6-vicuna-13b", "LlavaLlamaForCausalLM", 13.4, _V),
+    ("llava-next-8b", "lmms-lab", "lmms-lab/llava-next-8b", "LlavaLlamaForCausalLM", 8.4, _V),
     ("mistral-7b-instruct-v0-2", "mistralai", "mistralai/Mistral-7B-Instruct-v0.2", "MistralForCausalLM", 7.2),
     ("mistral-7b-instruct-v0-3", "mistral", "mistralai/Mistral-7B-Instruct-v0.3", "MistralForCausalLM", 7.2),
     ("mistral-7b-v0-1", "mistral", "mistralai/Mistral-7B-v0.1", "MistralForCausalLM", 7.2),

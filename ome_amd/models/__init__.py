@@ -136,6 +136,11 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.clip import CLIPModel
 
         return CLIPModel
+    if cfg.architecture == "LlavaNextForConditionalGeneration" or \
+            (cfg.architecture == "LlavaLlamaForCausalLM" and "anyres" in str((cfg.extra or {}).get("image_aspect_ratio", ""))):
+        from ome_amd.models.llava_next import LlavaNextForConditionalGeneration
+
+        return LlavaNextForConditionalGeneration
     if cfg.architecture in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM"):
         from ome_amd.models.llava import LlavaForConditionalGeneration
 
@@ -190,6 +195,7 @@ def supported(arch: str) -> bool:
     return arch in DENSE_ARCHS or arch in MOE_ARCHS or arch in GEMMA_ARCHS or arch in LAYERNORM_ARCHS or arch in LLAMA4_ARCHS or arch in QWEN2_VL_ARCHS or arch in NEMOTRON_H_ARCHS or \
         arch in DECODER_ARCHS or arch in ENCODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
         arch == "DeciLMForCausalLM" or arch in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM") or \
+        arch == "LlavaNextForConditionalGeneration" or \
         arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or \
         arch == "Mistral3ForConditionalGeneration" or arch == "MiniCPM3ForCausalLM" or \
         arch in ("InternVLChatModel", "InternVLForConditionalGeneration") or \

@@ -209,10 +209,15 @@ class LlavaOnevisionForConditionalGeneration(LlamaForCausalLM):
         ids += prompt_ids[last:]
         return ids, MMInput(torch.cat(pvs, 0), grids, spans)
 
-    def encode_images(self, pixel_values: torch.Tensor, grids) -> torch.Tensor:
+    def _tile_features(self, pixel_values: torch.Tensor) -> torch.Tensor:
+        """[n_tiles, side * side, hidden]: tower -> GEMM -> GELU -> GEMM per tile."""
         p, s = self.proj, self.side
         f = self.visual.forward(pixel_values, self.n_layers, post_norm=False).reshape(-1, self.visual.E)
-        f = linear(ops.act(linear(f, p["w1"], p["b1"]), 3), p["w2"], p["b2"]).view(pixel_values.shape[0], s * s, -1)
+        return linear(ops.act(linear(f, p["w1"], p["b1"]), 3), p["w2"], p["b2"]).view(pixel_values.shape[0], s * s, -1)
+
+    def encode_images(self, pixel_values: torch.Tensor, grids) -> torch.Tensor:
+        s = self.side
+        f = self._tile_features(pixel_values)
         out, off = [], 0
         nl = self.newline
         for n, h, w in grids:
