@@ -404,9 +404,11 @@ def url_path(isvc: dict, ic: IngressConfig) -> str:
 
 
 def entrypoint_component(isvc_spec: dict) -> str:
-    if isvc_spec.get("router"):
+    # a component present with an empty spec (``router: {}``) still exists (the reference tests
+    # ``Spec.Router != nil``)
+    if isvc_spec.get("router") is not None:
         return C.ROUTER
-    if isvc_spec.get("decoder"):
+    if isvc_spec.get("decoder") is not None:
         return C.DECODER
     return C.ENGINE
 
