@@ -1273,6 +1273,9 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
   dim3 grid(n_items, Hkv);
   const char* ve = getenv("OME_PREFILL_ATTN");
   const int variant = ve ? atoi(ve) : 2;
+  // 64-row items exist only for the 8-wave GQA-4 / D = 128 kernel; every other kernel would
+  // treat them as 32-row items and silently skip rows 32..63
+  if (rows == 64 && !(D == 128 && variant == 2 && G == 4)) return -2;
 #define ARGS                                                                                                     \
   kv_fmt, variant, rows, G, grid, stream, q, q_stride, k_cache, v_cache, block_tables, bt_stride, cu_q, kv_lens,  \
       items, out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi

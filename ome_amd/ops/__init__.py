@@ -270,7 +270,7 @@ def fp8_gemm(qa, sa, qw, sw, block: int = 0, bias=None, out: torch.Tensor | None
     assert qw.shape[1] == K and qa.is_contiguous() and qw.is_contiguous()
     if out is None:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=qa.device)
-    if M <= FP8_SK_MAX_ROWS and gemm_sk_fp8_ok(M, N, K, 128):
+    if M <= FP8_SK_MAX_ROWS and gemm_sk_fp8_ok(M, N, K, 128) and _sk_fp8_operands_ok(sa, sw, qw):
         # decode rows: stream-K fp8 (csrc/kernels/gemm_sk.hip, Q = 1 / 2) -- every CU busy at any M
         return gemm_sk_fp8(qa, sa, qw, sw, block, bias, out)
     if N % 256 == 0 and K % 128 == 0 and M >= FP8_MX_MIN_ROWS and -(-M // 256) * (N // 256) >= FP8_MX_MIN_TILES:
@@ -858,18 +858,22 @@ def deinterleave_gate_up(y: torch.Tensor, block: int = 16):
 # ---------------------------------------------------------------------------------------------
 # Stream-K MFMA GEMM (csrc/kernels/gemm_sk.hip): persistent per-XCD stream-K over bm x bn
 # output tiles, fp32 partial slabs reduced in-launch by each tile's last arriver.  One workspace
-# per device (GEMMs of one engine run on one stream at a time; graph replays reuse it).
+# (slabs + tickets) per (device, stream): launches on one stream are ordered, so they may share
+# slabs and tickets; two streams running GEMMs concurrently (a side-stream overlap, TBO halves,
+# a vision tower) each get their own, so their partial sums and tickets never alias.  Graph
+# replays reuse the workspace of the stream they were captured on.
 _SK_MAX_WG = 256
 _SK_CNT = 1 << 16
 _SK_WS: dict = {}
 
 
 def _sk_workspace(device: torch.device):
-    w = _SK_WS.get(device.index)
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    w = _SK_WS.get(key)
     if w is None:
         ws = torch.empty(_SK_MAX_WG * 2 * 256 * 256, dtype=torch.float32, device=device)
         cnt = torch.zeros(_SK_CNT, dtype=torch.int32, device=device)   # the kernel re-arms every ticket it takes
-        w = _SK_WS[device.index] = (ws, cnt)
+        w = _SK_WS[key] = (ws, cnt)
     return w
 
 
@@ -953,6 +957,41 @@ def gemm_sk(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
     return out
 
 
+def gemm_pp_ok(M: int, N: int, K: int) -> bool:
+    """Shapes accepted by the ping-pong 256 x 256 GEMM (csrc/kernels/gemm_pp.hip)."""
+    return M > 0 and N > 0 and N % 256 == 0 and K > 0 and K % 64 == 0
+
+
+def gemm_pp(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
+            epi: int = 0, res: torch.Tensor | None = None) -> torch.Tensor:
+    """out = x @ w.T (+ bias) on the ping-pong MFMA GEMM (256 x 256 tiles, one per workgroup).
+    ``epi=1``: out = x @ w.T (+ bias) + ``res`` (may be ``out`` itself: the residual stream updated
+    in place); ``epi=2``: w holds gate/up rows interleaved in 16-row blocks and out = SiLU(gate) * up."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not _gpu(x):
+        y = x.float() @ w.float().t()
+        if bias is not None:
+            y = y + bias.float()
+        if epi == 1:
+            y = y + res.float()
+        if epi == 2:
+            g, u = deinterleave_gate_up(y)
+            y = F.silu(g) * u
+        y = y.to(x.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    assert x.stride(1) == 1 and w.stride(1) == 1 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == 2 else N, dtype=x.dtype, device=x.device)
+    call("ome_gemm_pp", x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ptr(bias),
+         ptr(res) if epi == 1 else None, res.stride(0) if epi == 1 else 0, out.data_ptr(), out.stride(0), M, N, K,
+         epi, stream_ptr())
+    return out
+
+
 def mla_prep(a: torch.Tensor, qlr: int, lat: int, rope: int, w: torch.Tensor, eps: float, positions: torch.Tensor,
              cos_sin: torch.Tensor, slots: torch.Tensor, cache_flat: torch.Tensor, q: torch.Tensor, nope: int,
              q_full: torch.Tensor) -> None:
@@ -985,6 +1024,14 @@ def mla_prep(a: torch.Tensor, qlr: int, lat: int, rope: int, w: torch.Tensor, ep
 def gemm_sk_fp8_ok(M: int, N: int, K: int, bn: int = 128, nwg: int = 256) -> bool:
     return bn in (128, 256) and N % bn == 0 and K % 128 == 0 and K > 0 and nwg % 8 == 0 and \
         8 <= nwg <= _SK_MAX_WG and M > 0 and gemm_sk_tiles(M, N, bn, 128) <= _SK_CNT
+
+
+def _sk_fp8_operands_ok(sa: torch.Tensor, sw: torch.Tensor, qw: torch.Tensor) -> bool:
+    """Operand conditions of ``ome_gemm_sk_fp8`` beyond the shape (fp32 contiguous scales, 16-B
+    aligned per-channel scales, unit-stride weight rows): callers that fail them take the other
+    fp8 kernels instead of an assertion."""
+    return sa.dtype == torch.float32 and sw.dtype == torch.float32 and sa.is_contiguous() and \
+        sw.is_contiguous() and sw.data_ptr() % 16 == 0 and qw.stride(1) == 1 and qw.stride(0) % 16 == 0
 
 
 def gemm_sk_fp8(qa: torch.Tensor, sa: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0,
@@ -1111,6 +1158,9 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     if isinstance(items, PrefillPlan):
         plan, items = items, items.items
         rows = plan.rows
+        if rows != 32 and prefill_rows(Hq, Hkv, D, P) != rows:
+            raise ValueError(f"paged_prefill: {rows}-row items need the GQA-4 / D=128 kernel, got Hq={Hq} "
+                             f"Hkv={Hkv} D={D} page={P} (build the plan with prefill_rows of this layer)")
         if (plan.parts and D == 128 and P == 16 and Hq == 4 * Hkv and row_hi is None and
                 os.environ.get("OME_PREFILL_ATTN", "2") == "2"):
             po = torch.empty(plan.parts * Hkv * 4 * 32 * 128, dtype=torch.float32, device=q.device)

@@ -223,9 +223,15 @@ PP_IPC_BYTES = 64 << 20
 
 
 def _pp_ipc_init(st: ParallelState, groups: dict) -> None:
+    """Build the pipeline's IPC hand-off comms, then AGREE on the outcome over the engine group:
+    IPC is kept only if every rank built every comm it needs.  A rank that fell back on its own
+    would run RCCL ``send``/``recv`` against a peer still in ``all_gather_last`` -- both hang."""
+    import logging
+
     from ome_amd.parallel.comm import CustomAllReduce
 
     t, p = st.tp_rank, st.pp_rank
+    err = None
     try:
         # every rank builds its comms in stage order, so each pair's two members meet in the
         # same collective (handle exchange over that pair's gloo group)
@@ -235,11 +241,28 @@ def _pp_ipc_init(st: ParallelState, groups: dict) -> None:
             elif q == p:
                 st.pp_next = CustomAllReduce(groups[(t, q)], max_bytes=PP_IPC_BYTES, cpu_group=groups[(t, q)])
         st.pp_bcast = CustomAllReduce(groups[(t, "all")], max_bytes=4 << 20, cpu_group=groups[(t, "all")])
-    except Exception as e:  # noqa: BLE001 -- e.g. peers not IPC-reachable: RCCL p2p, loudly
-        import logging
-
-        logging.getLogger("ome_amd.parallel").warning("pipeline IPC hand-off unavailable (%s); using RCCL p2p", e)
+    except Exception as e:  # noqa: BLE001 -- e.g. peers not IPC-reachable
+        err = e
+    if not _all_ranks_ok(err is None, st.cpu_group):
+        logging.getLogger("ome_amd.parallel").warning(
+            "pipeline IPC hand-off unavailable (%s); every rank uses RCCL p2p",
+            err if err is not None else "failed on another rank")
+        for c in (st.pp_prev, st.pp_next, st.pp_bcast):
+            if c is not None:
+                try:
+                    c.close()
+                except Exception:  # noqa: BLE001 -- best effort: the fallback does not use it
+                    pass
         st.pp_prev = st.pp_next = st.pp_bcast = None
+
+
+def _all_ranks_ok(ok: bool, group) -> bool:
+    """MIN-reduce of a per-rank success flag over a (gloo) group: True only if every rank is ok."""
+    if group is None:
+        return ok
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    return bool(flag.item())
 
 
 def pp_graph_ok() -> bool:

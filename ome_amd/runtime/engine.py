@@ -419,7 +419,9 @@ class Engine:
         allw = [int(b[0]) for b in bufs]
         done: list[Request] = []
         if any(int(b[1]) < 0 for b in bufs):   # overflow somewhere: two-phase exchange, all ranks
-            payloads = self._dp_gather_updates(pend if over else [])
+            # every rank re-sends its update: a rank that fit the capacity has already taken it
+            # out of _dp_pending, so the fixed-capacity copy above is discarded with `bufs`
+            payloads = self._dp_gather_updates(pend)
             bufs = [torch.cat([torch.tensor([0.0, float(len(pl))], dtype=torch.float64), pl]) for pl in payloads]
         if self.pstate.rank == 0:
             done += self._dp_apply_updates(bufs)

@@ -371,7 +371,9 @@ class ModelRunner:
         for m, graphs in enumerate(self.mb_graphs):   # (one slot unless this is a pipeline stage)
             for bs in reversed(self.buckets):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=self.graph_pool):
+                # captured on the warm-up stream: per-stream state made there (the stream-K GEMM
+                # workspace) already exists, so nothing is allocated or zeroed inside the capture
+                with torch.cuda.graph(g, pool=self.graph_pool, stream=stream):
                     self._decode_forward(bs, m)
                 if self.graph_pool is None:
                     self.graph_pool = g.pool()
@@ -624,7 +626,10 @@ class ModelRunner:
                 any_pending = True
             last_row[i] = len(ids) - 1
         tp_ = self.model.tp
-        rows = ops.prefill_rows(tp_.hq, tp_.hkv, self.cfg.head_dim, P)
+        # 64-row items only when EVERY attention layer has the qualifying shape (DeciLM varies
+        # its kv heads per layer; the plan is shared by all layers)
+        hkvs = set(getattr(self.model, "kv_heads_per_layer", {}).values()) | {tp_.hkv}
+        rows = ops.prefill_rows(tp_.hq, tp_.hkv, self.cfg.head_dim, P) if len(hkvs) == 1 else 32
         items, split, comb, chunk, parts = ops.prefill_plan(q_lens, kv_lens, tile=rows, kv_heads=tp_.hkv) if q_lens \
             else ([], [], [], 0, 0)
         T, S, n_it, nd, B = len(ids), len(q_lens), len(items), len(dec_lens), len(chunks)

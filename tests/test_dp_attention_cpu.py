@@ -19,7 +19,7 @@ from tests.test_moe_cpu import _export_hf
 PROMPTS = [[3 + (i * 37 + j) % 1000 for j in range(5 + 7 * i)] for i in range(5)]
 
 
-def _worker(rank, world, port, path, q, relay_cap=None, overlap=None):
+def _worker(rank, world, port, path, q, relay_cap=None, overlap=None, prompts=PROMPTS):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     from ome_amd.runtime.engine import Engine, EngineArgs
     from ome_amd.runtime.request import SamplingParams
@@ -32,7 +32,7 @@ def _worker(rank, world, port, path, q, relay_cap=None, overlap=None):
     m = eng.runner.model
     assert m.E_local == m.E // world and m.e0 == rank * m.E_local
     if rank == 0:
-        reqs = eng.generate(PROMPTS, SamplingParams(max_new_tokens=8, ignore_eos=True))
+        reqs = eng.generate(prompts, SamplingParams(max_new_tokens=8, ignore_eos=True))
         owners = {r.dp_rank for r in reqs}
         eng.stop_group()
         q.put(([r.output_ids for r in reqs], owners))
@@ -68,28 +68,40 @@ def _checkpoint(tmp_path, kind):
     ("olmoe", None, None), ("dbrx", None, None), ("minimax_m2", None, None),
     # overlapped DP steps (the GPU default): step k+1 enqueued before step k's tokens are read back
     ("qwen3-moe", None, True), ("deepseek-v3", None, True), ("qwen3-moe", 3, True)])
-def test_dp_attention_ep_matches_single(tmp_path, kind, relay_cap, overlap):
+def test_dp_attention_ep_matches_single(tmp_path, kind, relay_cap, overlap, world=2, prompts=PROMPTS):
     _checkpoint(tmp_path, kind)
     from ome_amd.runtime.engine import Engine, EngineArgs
     from ome_amd.runtime.request import SamplingParams
 
     single = Engine(EngineArgs(model_path=str(tmp_path), device="cpu", max_running_requests=8, context_length=256,
                                dtype="float32"))
-    want = [r.output_ids for r in single.generate(PROMPTS, SamplingParams(max_new_tokens=8, ignore_eos=True))]
+    want = [r.output_ids for r in single.generate(prompts, SamplingParams(max_new_tokens=8, ignore_eos=True))]
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), q, relay_cap, overlap)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), q, relay_cap, overlap, prompts))
+          for r in range(world)]
     for p in ps:
         p.start()
     got, owners = q.get(timeout=300)
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert owners == {0, 1}  # both ranks served requests
+    assert owners == set(range(world))  # every rank served requests
     assert got == want
+
+
+@pytest.mark.timeout(400)
+def test_dp_relay_mixed_overflow_keeps_every_rank(tmp_path):
+    """4 ranks (2 of the 8 experts each), 6 prompts -> ranks own {0, 4}, {1, 5}, {2}, {3}; relay
+    capacity 12 floats: follower 1's two-request update overflows (13 floats) while followers 2
+    and 3 fit theirs (7 floats).  The two-phase fallback must carry EVERY follower's update --
+    the non-overflowing ranks already took theirs out of the pending list, so dropping them
+    would leave their proxy requests hanging on rank 0."""
+    prompts = [[3 + (i * 37 + j) % 1000 for j in range(5 + 3 * i)] for i in range(6)]
+    test_dp_attention_ep_matches_single(tmp_path, "qwen3-moe", 12, None, world=4, prompts=prompts)
 
 
 def test_dp_relay_unknown_finish_reason_is_an_abort():

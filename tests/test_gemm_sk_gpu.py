@@ -116,6 +116,30 @@ def test_gemm_sk_repeat_and_graph_replay():
         assert _rel(out, ref) < 1e-2
 
 
+def test_gemm_sk_two_streams_concurrently():
+    """Stream-K GEMMs on two streams at once (side-stream overlap, TBO halves) must not share
+    partial slabs or tickets: each stream gets its own workspace (ops._sk_workspace)."""
+    M, N, K = 256, 6144, 4096
+    torch.manual_seed(1)
+    xs = [torch.randn(M, K, device=DEV, dtype=torch.bfloat16) for _ in range(2)]
+    ws = [torch.randn(N, K, device=DEV, dtype=torch.bfloat16) / K ** 0.5 for _ in range(2)]
+    refs = [_ref(x, w) for x, w in zip(xs, ws)]
+    outs = [[torch.empty(M, N, device=DEV, dtype=torch.bfloat16) for _ in range(8)] for _ in range(2)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream())
+    for i in range(8):   # interleaved issue: the two streams' launches overlap on the device
+        for k, s in enumerate(streams):
+            with torch.cuda.stream(s):
+                ops.gemm_sk(xs[k], ws[k], out=outs[k][i], bn=128, nwg=256)
+    torch.cuda.synchronize()
+    for k in range(2):
+        for o in outs[k]:
+            assert _rel(o, refs[k]) < 1e-2
+    keys = {key for key in ops._SK_WS if key[1] in (streams[0].cuda_stream, streams[1].cuda_stream)}
+    assert len(keys) == 2
+
+
 def test_gemm_sk_rejects_bad_arguments():
     x = torch.randn(16, 64, device=DEV, dtype=torch.bfloat16)
     w = torch.randn(256, 64, device=DEV, dtype=torch.bfloat16)
