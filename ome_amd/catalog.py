@@ -214,6 +214,8 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
     Family("skywork-reward-llama-3-1-8b-v0-2", "skywork", "Skywork/Skywork-Reward-Llama-3.1-8B-v0.2",
            "LlamaForSequenceClassification", 7.5, capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("skywork-reward-gemma-2-27b-v0-2", "skywork", "Skywork/Skywork-Reward-Gemma-2-27B-v0.2",
+           "Gemma2ForSequenceClassification", 27.2, capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
     Family("qwen2-5-math-rm-72b", "qwen", "Qwen/Qwen2.5-Math-RM-72B", "Qwen2ForRewardModel", 72.7,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
     Family("qwen2-5-1-5b-apeach", "jason9693", "jason9693/Qwen2.5-1.5B-apeach", "Qwen2ForSequenceClassification", 1.5,
@@ -223,6 +225,13 @@ FAMILIES: list[Family] = [
            "LlamaForCausalLM", 70.6, None, 1.0, quantization="fp8"),
     Family("nvidia-nemotron-3-nano-30b-a3b-fp8", "nvidia", "nvidia/NVIDIA-Nemotron-3-Nano-30B-A3B-FP8",
            "NemotronHForCausalLM", 31.6, None, 1.0, quantization="fp8"),
+    # compressed-tensors (RedHatAI FP8-dynamic) and NVIDIA ModelOpt FP8 vision-language checkpoints
+    Family("llama-3-2-90b-vision-instruct-fp8", "meta", "RedHatAI/Llama-3.2-90B-Vision-Instruct-FP8-dynamic",
+           "MllamaForConditionalGeneration", 88.6, None, 1.0, quantization="fp8",
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("nvidia-nemotron-nano-12b-v2-vl-fp8", "nvidia", "nvidia/NVIDIA-Nemotron-Nano-12B-v2-VL-FP8",
+           "NemotronH_Nano_VL_V2", 12.6, None, 1.0, quantization="fp8",
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
 ]
 
 

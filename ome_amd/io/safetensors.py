@@ -88,7 +88,7 @@ def save_file(tensors: dict[str, torch.Tensor], path: str | os.PathLike, metadat
     hdr, off, blobs = {}, 0, []
     for name, t in tensors.items():
         t = t.detach().contiguous().cpu()
-        b = t.view(torch.uint8).numpy().tobytes() if t.numel() else b""
+        b = t.reshape(-1).view(torch.uint8).numpy().tobytes() if t.numel() else b""
         hdr[name] = {"dtype": rev[t.dtype], "shape": list(t.shape), "data_offsets": [off, off + len(b)]}
         off += len(b)
         blobs.append(b)

@@ -17,7 +17,8 @@ DENSE_ARCHS = {
     "LlamaForCausalLM", "MistralForCausalLM", "Qwen2ForCausalLM", "Qwen3ForCausalLM",
     "LlamaModel", "MistralModel", "Qwen2Model", "Qwen3Model",
 }
-GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
+GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration",
+               "Gemma2ForSequenceClassification"}
 LAYERNORM_ARCHS = {"Starcoder2ForCausalLM", "GPTNeoXForCausalLM", "PhiForCausalLM"}
 LLAMA4_ARCHS = {"Llama4ForCausalLM", "Llama4ForConditionalGeneration"}
 QWEN2_VL_ARCHS = {"Qwen2VLForConditionalGeneration", "Qwen2_5_VLForConditionalGeneration",

@@ -123,6 +123,27 @@ def _standard_keys(c: dict[str, Any]) -> dict[str, Any]:
     return out
 
 
+
+def _is_fp8_checkpoint(q: dict) -> bool:
+    """FP8 weight checkpoints in any of the formats the reference catalog ships, all served as
+    W8A8 with dynamic per-token activation scales (``models/quant.py``):
+    ``quant_method: fp8`` / ``fbgemm_fp8`` (DeepSeek block scales, Meta per-row scales),
+    ``compressed-tensors`` with 8-bit float weights (RedHatAI ``*-FP8-dynamic``: per-channel
+    ``weight_scale``), and NVIDIA ModelOpt ``quant_algo: FP8`` (per-tensor ``weight_scale``)."""
+    m = str(q.get("quant_method") or q.get("quant_type") or "").lower()
+    if m in ("fp8", "fbgemm_fp8"):
+        return True
+    if m == "compressed-tensors":
+        for grp in (q.get("config_groups") or {}).values():
+            w = (grp or {}).get("weights") or {}
+            if int(w.get("num_bits") or 0) == 8 and str(w.get("type", "")).lower() == "float":
+                return True
+        return False
+    if m == "modelopt":
+        algo = q.get("quant_algo") or (q.get("quantization") or {}).get("quant_algo")
+        return str(algo or "").upper() == "FP8"
+    return False
+
 @dataclass
 class ModelConfig:
     architecture: str = "LlamaForCausalLM"
@@ -278,7 +299,7 @@ class ModelConfig:
             c.v_head_dim = text.get("v_head_dim", 128)
         q = cfg.get("quantization_config")
         if q:
-            c.quantization = q.get("quant_method") or q.get("quant_type")
+            c.quantization = "fp8" if _is_fp8_checkpoint(q) else (q.get("quant_method") or q.get("quant_type"))
         c.is_embedding = ("Embedding" in arch) or arch.endswith(("ForSequenceClassification", "RewardModel")) or \
             (arch.endswith("Model") and "ForCausalLM" not in arch and arch not in CAUSAL_MODEL_CLASSES)
         if mt in ("roberta", "xlm-roberta") and c.max_position_embeddings > 2:

@@ -18,6 +18,11 @@ kernels:
 * per-layer sliding windows (``layer_types``; Gemma 2 alternates local/global, Gemma 3 has one
   global layer in six) and, for Gemma 3, a separate RoPE table for the local layers
   (``rope_local_base_freq``).
+
+``Gemma2ForSequenceClassification`` (reward models such as Skywork-Reward-Gemma-2-27B-v0.2,
+reference ``config/models/Skywork/Skywork-Reward-Gemma-2-27B-v0.2.yaml``): the same decoder, the
+final norm's last-token row through the ``score`` Linear (no bias, no logit soft-capping), served as
+an embedding-style model (``pool``).
 """
 from __future__ import annotations
 
@@ -30,7 +35,8 @@ from ome_amd.models.llama import LlamaForCausalLM
 from ome_amd.models.quant import linear
 from ome_amd.parallel import state as pstate
 
-GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration"}
+GEMMA_ARCHS = {"GemmaForCausalLM", "Gemma2ForCausalLM", "Gemma3ForCausalLM", "Gemma3ForConditionalGeneration",
+               "Gemma2ForSequenceClassification"}
 
 
 def _hf(cfg: ModelConfig) -> dict:
@@ -72,6 +78,9 @@ class GemmaForCausalLM(LlamaForCausalLM):
             lc = ModelConfig(**{**cfg.__dict__, "rope_theta": float(local_theta), "rope_scaling": None})
             self.cos_sin_local = rope_cos_sin(lc, mp, device=self.device)
         self.normalizer = torch.tensor(cfg.hidden_size ** 0.5, dtype=dtype).item()
+        self.is_cls = cfg.architecture.endswith("ForSequenceClassification")
+        self.num_labels = int(hf.get("num_labels") or len(hf.get("id2label") or {}) or 1)
+        self.score: torch.Tensor | None = None   # [num_labels, H] sequence-classification head
 
     # ------------------------------------------------------------------ weights
     def init_random(self, seed: int = 0, std: float = 0.02) -> "GemmaForCausalLM":
@@ -84,6 +93,10 @@ class GemmaForCausalLM(LlamaForCausalLM):
             if self.gen == 3 and self.qn[i] is None:
                 self.qn[i] = self._alloc(self.D, std=None, gen=None)
                 self.kn[i] = self._alloc(self.D, std=None, gen=None)
+        if self.is_cls:
+            g = torch.Generator(device="cpu").manual_seed(seed + 7)
+            self.score = (torch.randn(self.num_labels, self.cfg.hidden_size, generator=g) * std).to(
+                device=self.device, dtype=self.dtype)
         return self
 
     def load_hf_weights(self, weights) -> "GemmaForCausalLM":
@@ -113,6 +126,9 @@ class GemmaForCausalLM(LlamaForCausalLM):
                 parts = n.split(".")
                 if parts[0] == "layers" and len(parts) >= 4 and parts[2] in ("gemma_post_attn", "gemma_post_ff"):
                     extra[(int(parts[1]), parts[2])] = w
+                    continue
+                if name == "score.weight":
+                    self.score = w.to(device=self.device, dtype=self.dtype).contiguous()
                     continue
                 yield name, w
 
@@ -186,6 +202,14 @@ class GemmaForCausalLM(LlamaForCausalLM):
         return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
                                  self.scale, w, k_scale=ks, v_scale=vs, softcap=cap, row_hi=hi)
 
+    def pool(self, hidden: torch.Tensor, cu: torch.Tensor) -> torch.Tensor:
+        """Per sequence (rows ``cu[s]:cu[s+1]``): the classification head's raw scores of the last
+        token (``Gemma2ForSequenceClassification``), else last-token pooling + L2 norm."""
+        if self.score is None:
+            return ops.pool(hidden, cu, 0, True)
+        last = hidden.index_select(0, (cu[1:] - 1).long())
+        return linear(last, self.score).float()
+
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         logits = super().compute_logits(hidden)
         if self.final_softcap > 0:
@@ -195,6 +219,8 @@ class GemmaForCausalLM(LlamaForCausalLM):
 
     def weight_bytes(self) -> int:
         n = super().weight_bytes()
+        if self.score is not None:
+            n += self.score.numel() * self.score.element_size()
         for lst in (self.post_attn, self.post_ff):
             n += sum(t.numel() * t.element_size() for t in lst if t is not None)
         return n

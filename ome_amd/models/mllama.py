@@ -38,7 +38,7 @@ from ome_amd import ops
 from ome_amd.models.common import AttnMeta, PagedKVCache
 from ome_amd.models.config import ModelConfig
 from ome_amd.models.llama import LlamaForCausalLM
-from ome_amd.models.quant import linear
+from ome_amd.models.quant import dequant_fp8_stream, linear
 from ome_amd.parallel import state as pstate
 
 MLLAMA_ARCHS = {"MllamaForConditionalGeneration"}
@@ -249,6 +249,8 @@ class MllamaForConditionalGeneration(LlamaForCausalLM):
 
     def load_hf_weights(self, weights) -> "MllamaForConditionalGeneration":
         tp, D = self.tp, self.D
+        if self.fp8:   # e.g. RedHatAI Llama-3.2-90B-Vision-Instruct-FP8-dynamic: per-channel weight_scale
+            weights = dequant_fp8_stream(weights, self.fp8_block, self.dtype)
         xparts: dict[int, dict[str, torch.Tensor]] = {}
         rest = []
         embed_full = None

@@ -41,7 +41,7 @@ from ome_amd import ops
 from ome_amd.models.common import AttnMeta, PagedKVCache
 from ome_amd.models.config import ModelConfig
 from ome_amd.models.llama import LlamaForCausalLM
-from ome_amd.models.quant import linear
+from ome_amd.models.quant import dequant_fp8_stream, linear
 from ome_amd.parallel import state as pstate
 
 NEMOTRON_H_ARCHS = {"NemotronHForCausalLM"}
@@ -180,6 +180,9 @@ class NemotronHForCausalLM(LlamaForCausalLM):
         return self
 
     def load_hf_weights(self, weights) -> "NemotronHForCausalLM":
+        if self.fp8:   # FP8 checkpoints (ModelOpt / compressed-tensors / block-scaled): dequantised to bf16
+            weights = dequant_fp8_stream(weights, self.fp8_block, self.dtype)
+
         def put(t, dtype=None):
             return t.to(device=self.device, dtype=dtype or self.dtype).contiguous()
 

@@ -75,3 +75,34 @@ def test_gemma_prefill_logits_match_hf(tmp_path, kind):
         ref = hf.generate(torch.tensor([ids]), max_new_tokens=6, do_sample=False)[0, len(ids):].tolist()
     r = eng.generate([ids], SamplingParams(max_new_tokens=6, ignore_eos=True))[0]
     assert r.output_ids == ref
+
+
+def test_gemma2_sequence_classification_matches_hf(tmp_path):
+    """Gemma2ForSequenceClassification (Skywork-Reward-Gemma-2 style reward model): the score of the
+    last token of each prompt matches HF's pooled logits."""
+    from tests.test_decoder_remote_families_cpu import _scores
+
+    torch.manual_seed(0)
+    cfg = transformers.Gemma2Config(vocab_size=512, hidden_size=128, intermediate_size=256, num_hidden_layers=4,
+                                    num_attention_heads=4, num_key_value_heads=2, head_dim=64,
+                                    max_position_embeddings=512, rms_norm_eps=1e-6, sliding_window=16,
+                                    query_pre_attn_scalar=64, attn_logit_softcapping=50.0,
+                                    final_logit_softcapping=30.0, pad_token_id=0, num_labels=1)
+    hf = transformers.Gemma2ForSequenceClassification(cfg)
+    with torch.no_grad():
+        for n, p in hf.named_parameters():
+            if "norm" in n:
+                p.normal_(0.0, 0.2)
+            elif p.dim() == 2:
+                p.normal_(0.0, 0.08)
+    hf = hf.float().eval()
+    hf.config._attn_implementation = "eager"
+    hf.save_pretrained(tmp_path, safe_serialization=True)
+    prompts = [[(7 * i + 3) % 500 + 3 for i in range(40)], [(5 * i + 1) % 500 + 3 for i in range(11)]]
+    with torch.no_grad():
+        want = torch.cat([hf(torch.tensor([p])).logits for p in prompts]).float()
+    eng = Engine(EngineArgs(model_path=str(tmp_path), device="cpu", dtype="float32", max_running_requests=4,
+                            context_length=256))
+    assert eng.cfg.is_embedding
+    got = _scores(eng, prompts)
+    assert got.shape == (2, 1) and torch.allclose(got, want, atol=2e-3, rtol=2e-3), (got, want)
