@@ -212,6 +212,9 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
     Family("gte-qwen2-7b-instruct", "alibaba-nlp", "Alibaba-NLP/gte-Qwen2-7B-instruct", "Qwen2ForCausalLM", 7.6,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
+    Family("gme-qwen2-vl-2b-instruct", "alibaba-nlp", "Alibaba-NLP/gme-Qwen2-VL-2B-Instruct",
+           "Qwen2VLForConditionalGeneration", 2.2, capabilities=["TEXT_EMBEDDINGS", "EMBEDDING"],
+           args=["--is-embedding"]),
     Family("skywork-reward-llama-3-1-8b-v0-2", "skywork", "Skywork/Skywork-Reward-Llama-3.1-8B-v0.2",
            "LlamaForSequenceClassification", 7.5, capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
     Family("skywork-reward-gemma-2-27b-v0-2", "skywork", "Skywork/Skywork-Reward-Gemma-2-27B-v0.2",

@@ -67,6 +67,7 @@ _SIGNATURES = {
         "ome_gemm": [vp, i64, vp, i64, vp, i64, i32, i32, i32, i32, i32, vp, vp],
         "ome_gemm_set_variant": [i32],
         "ome_gemm_sk": [vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+        "ome_gemm_pp": [vp, i64, vp, i64, vp, vp, i64, vp, i64, i32, i32, i32, i32, vp],
         "ome_mla_prep": [vp, i64, i32, i32, i32, vp, f32, vp, vp, vp, vp, i64, vp, i64, i64, i32, i32, vp, i64, i64,
                          i32, vp],
         "ome_gemm_sk_fp8": [vp, i64, vp, vp, i64, vp, i32, vp, vp, i64, i32, i32, i32, i32, i32, i32, i32, vp, vp,

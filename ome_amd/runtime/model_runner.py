@@ -849,7 +849,16 @@ class ModelRunner:
         meta = AttnMeta("prefill", t(pos), t(slots), bt, cu_q=t(cu), kv_lens=t(q_lens),
                         items=t(items).view(-1, 2) if items else torch.zeros(0, 2, dtype=torch.int32, device=dv))
         meta.extra["lengths"] = q_lens  # host copy (encoders' varlen attention work items)
-        hidden = self.model.forward(t(ids), meta, self.kv)
+        t_ids = t(ids)
+        embeds = None
+        if getattr(m, "is_multimodal", False) and not getattr(m, "mm_cross", False) and \
+                any(c.req.mm is not None for c in batch.chunks):
+            # VLM embedders (GME-Qwen2-VL): image features + M-RoPE positions of whole prompts
+            from types import SimpleNamespace
+
+            whole = [SimpleNamespace(req=c.req, start=0, length=len(c.req.prompt_ids)) for c in batch.chunks]
+            embeds = self._mm_prepare(whole, list(range(len(whole))), len(ids), t_ids, meta)
+        hidden = self.model.forward(t_ids, meta, self.kv, embeds)
         pool = getattr(self.model, "pool", None)  # classification / reward heads (models/decoder.py)
         out = pool(hidden, t(cu)) if pool is not None else ops.pool(hidden, t(cu), 0, True)
         return out.cpu().tolist()

@@ -620,9 +620,20 @@ def create_app(engine, ns=None):
         from ome_amd.runtime.request import SamplingParams
 
         for i, x in enumerate(items):
-            if isinstance(x, dict) and ("image" in x or "image_url" in x):   # CLIP-style image embedding
+            if isinstance(x, dict) and ("image" in x or "image_url" in x):
                 im = x.get("image") or (x.get("image_url") or {}).get("url")
-                emb = await _embed_ids([], images=[im])
+                m = engine.runner.model
+                if hasattr(m, "image_prompt_ids") or hasattr(m, "image_token_id"):
+                    # VLM embedder (GME-Qwen2-VL style): the image (+ text) as one user turn of the
+                    # chat template, last-token pooling over the language model
+                    content = [{"type": "image_url", "image_url": {"url": im}}]
+                    if x.get("text"):
+                        content.append({"type": "text", "text": str(x["text"])})
+                    ids, ims = _encode({"messages": [{"role": "user", "content": content}]}, True)
+                    total += len(ids)
+                    emb = await _embed_ids(ids, images=ims)
+                else:   # CLIP-style image tower embedding
+                    emb = await _embed_ids([], images=[im])
             else:
                 if isinstance(x, dict):
                     x = x.get("text", "")

@@ -115,3 +115,28 @@ def test_text_only_prompt_on_vl_model(tmp_path):
     with torch.no_grad():
         ref = hf.generate(torch.tensor([ids]), max_new_tokens=5, do_sample=False)[0, len(ids):].tolist()
     assert eng.generate([ids], SamplingParams(max_new_tokens=5, ignore_eos=True))[0].output_ids == ref
+
+
+def test_gme_style_image_text_embedding_matches_hf(tmp_path):
+    """GME-Qwen2-VL (reference ``config/models/Alibaba-NLP/gme-Qwen2-VL-2B-Instruct.yaml``): a
+    Qwen2-VL checkpoint served with --is-embedding; an image + text prompt is embedded as the
+    L2-normalised final hidden state of its last token (GME's pooling)."""
+    hf = _hf_model(tmp_path)
+    img = _image()
+    pv, grid = preprocess_image(img)
+    eng = Engine(EngineArgs(model_path=str(tmp_path), device="cpu", dtype="float32", max_running_requests=4,
+                            context_length=512, is_embedding=True))
+    prompt = [5, 9, VS, IMG, VE, 33, 41, 12, 7]
+    req = eng.make_mm_request(prompt, [img], SamplingParams(max_new_tokens=0))
+    req.is_embedding = True
+    eng.add_request(req)
+    while not req.finished:
+        eng.step()
+    ex, _ = expand_image_tokens(prompt, IMG, [grid], 2)
+    t = torch.tensor([ex])
+    with torch.no_grad():
+        h = hf.model(input_ids=t, pixel_values=torch.from_numpy(pv), image_grid_thw=torch.tensor([grid]),
+                     mm_token_type_ids=(t == IMG).int()).last_hidden_state[0, -1]
+    want = torch.nn.functional.normalize(h.float(), dim=-1)
+    got = torch.tensor(req.embedding)
+    assert (got - want).abs().max().item() < 1e-3
