@@ -48,8 +48,18 @@ struct Scaler {
                        // logit gains slope * (key_pos - query_pos), i.e. alibi_l2(head) * (k - q)
   const int* row_lo;   // decode only: per-row first visible key (nullptr = 0) -- Mllama cross
                        // attention reads one [lo, seq_len) range of a request's vision-token cache
+  // Block-sparse causal attention (Phi-3-small): keys and queries in blocks of 1 << bs_shift
+  // tokens; query block qb sees key block kb <= qb when qb - kb < bs_local (the local band) or
+  // (kb + bs_h0 + head * bs_step + 1) % bs_vert == 0 (per-head vertical stripes).  bs_shift == 0:
+  // dense.  Applied as a -inf mask on the scores of the generic (non-FAST) kernel bodies.
+  int bs_shift, bs_local, bs_vert, bs_step, bs_h0;
   __device__ __forceinline__ float alibi_l2(int head) const {
     return alibi != nullptr ? alibi[head] * 1.4426950408889634f : 0.f;
+  }
+  __device__ __forceinline__ bool bs_visible(int qpos, int key, int head) const {
+    if (bs_shift == 0) return true;
+    const int qb = qpos >> bs_shift, kb = key >> bs_shift;
+    return qb - kb < bs_local || (kb + bs_h0 + head * bs_step + 1) % bs_vert == 0;
   }
   __device__ __forceinline__ float operator()(float s) const {
     if (cap_inv > 0.f) {
@@ -60,11 +70,23 @@ struct Scaler {
   }
 };
 
-static inline Scaler make_scaler(float scale, float softcap, const float* alibi = nullptr) {
+// packed block-sparse parameters (ops.blocksparse_pack): [0:4) log2 block, [4:20) local blocks,
+// [20:32) vertical stride, [32:40) head step, [40:52) global index of this rank's first head
+static inline void set_blocksparse(Scaler& r, int64_t bs) {
+  r.bs_shift = (int)(bs & 15);
+  r.bs_local = (int)((bs >> 4) & 0xffff);
+  r.bs_vert = (int)((bs >> 20) & 0xfff);
+  r.bs_step = (int)((bs >> 32) & 0xff);
+  r.bs_h0 = (int)((bs >> 40) & 0xfff);
+  if (r.bs_vert <= 0) r.bs_shift = 0;
+}
+
+static inline Scaler make_scaler(float scale, float softcap, const float* alibi = nullptr, int64_t bs = 0) {
   const float l2e = 1.4426950408889634f;
   Scaler r;
   r.alibi = alibi;
   r.row_lo = nullptr;
+  set_blocksparse(r, bs);
   r.mul = scale * l2e;
   r.cap_inv = softcap > 0.f ? scale / softcap : 0.f;
   r.cap_l2 = softcap > 0.f ? softcap * l2e : 0.f;
@@ -322,7 +344,7 @@ __device__ __forceinline__ void kv_tile_load(KVTile<D, F>& t, const typename KVS
 template <int D, int F, bool AL = false>
 __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf16x8 (&qf)[D / 32],
                                                 f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
-                                                int lo, Scaler scl, int g, float al, int qpos) {
+                                                int lo, Scaler scl, int g, float al, int qpos, int head = 0) {
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
@@ -333,8 +355,11 @@ __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf1
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k0 = kb + 4 * g + i, k1 = k0 + 16;
-    s0[i] = (k0 < p_end && k0 >= lo) ? (AL ? scl(s0[i]) + al * (float)(k0 - qpos) : scl(s0[i])) : OME_NEG_INF;
-    s1[i] = (k1 < p_end && k1 >= lo) ? (AL ? scl(s1[i]) + al * (float)(k1 - qpos) : scl(s1[i])) : OME_NEG_INF;
+    // AL instantiation: ALiBi bias and / or the block-sparse mask (both per query head)
+    const bool v0 = k0 < p_end && k0 >= lo && (!AL || scl.bs_visible(qpos, k0, head));
+    const bool v1 = k1 < p_end && k1 >= lo && (!AL || scl.bs_visible(qpos, k1, head));
+    s0[i] = v0 ? (AL ? scl(s0[i]) + al * (float)(k0 - qpos) : scl(s0[i])) : OME_NEG_INF;
+    s1[i] = v1 ? (AL ? scl(s1[i]) + al * (float)(k1 - qpos) : scl(s1[i])) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
   mt = fmaxf(mt, __shfl_xor(mt, 16));
@@ -395,7 +420,7 @@ __device__ __forceinline__ void kv_tilep_load(KVTileP<D, F>& t, const typename K
 template <int D, int F, bool AL = false>
 __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const bf16x8 (&qf)[D / 32],
                                                  f32x4 (&o)[D / 16], float& m_i, float& l_i, int kb, int p_end,
-                                                 int lo, Scaler scl, int g, float al, int qpos) {
+                                                 int lo, Scaler scl, int g, float al, int qpos, int head = 0) {
   f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < D / 32; ++ks) {
@@ -407,8 +432,11 @@ __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const b
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k0 = base + i, k1 = k0 + 4;
-    s0[i] = (k0 < p_end && k0 >= lo) ? (AL ? scl(s0[i]) + al * (float)(k0 - qpos) : scl(s0[i])) : OME_NEG_INF;
-    s1[i] = (k1 < p_end && k1 >= lo) ? (AL ? scl(s1[i]) + al * (float)(k1 - qpos) : scl(s1[i])) : OME_NEG_INF;
+    // AL instantiation: ALiBi bias and / or the block-sparse mask (both per query head)
+    const bool v0 = k0 < p_end && k0 >= lo && (!AL || scl.bs_visible(qpos, k0, head));
+    const bool v1 = k1 < p_end && k1 >= lo && (!AL || scl.bs_visible(qpos, k1, head));
+    s0[i] = v0 ? (AL ? scl(s0[i]) + al * (float)(k0 - qpos) : scl(s0[i])) : OME_NEG_INF;
+    s1[i] = v1 ? (AL ? scl(s1[i]) + al * (float)(k1 - qpos) : scl(s1[i])) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
   mt = fmaxf(mt, __shfl_xor(mt, 16));
@@ -486,13 +514,13 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     for (; kb < p_end; kb += 128) {
       KVTileP<D, F> t;
       kv_tilep_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tilep_compute<D, F, AL>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
+      kv_tilep_compute<D, F, AL>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos, kvh * G + n);
     }
   } else if (MODE == 0) {
     for (; kb < p_end; kb += 128) {
       KVTile<D, F> t;
       kv_tile_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F, AL>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
+      kv_tile_compute<D, F, AL>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos, kvh * G + n);
     }
   } else if (kb < p_end) {
     KVTile<D, F> t0, t1;
@@ -501,12 +529,12 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
       const int kn = kb + 128;
       const bool more = kn < p_end;
       if (more) kv_tile_load<D, P, F>(t1, k_cache, v_cache, bt, kn, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F, AL>(t0, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos);
+      kv_tile_compute<D, F, AL>(t0, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos, kvh * G + n);
       if (!more) break;
       const int kn2 = kn + 128;
       const bool more2 = kn2 < p_end;
       if (more2) kv_tile_load<D, P, F>(t0, k_cache, v_cache, bt, kn2, seq_len, kpage, kvh, n, g);
-      kv_tile_compute<D, F, AL>(t1, qf, o, m_i, l_i, kn, p_end, lo, scl, g, al, qpos);
+      kv_tile_compute<D, F, AL>(t1, qf, o, m_i, l_i, kn, p_end, lo, scl, g, al, qpos, kvh * G + n);
       if (!more2) break;
       kb = kn2;
     }
@@ -562,7 +590,7 @@ static void launch_decode_v2(int variant, dim3 grid, size_t smem, hipStream_t st
                              int window, const int* order, float v_scale, const float* sinks) {
   // ALiBi (Bloom / MPT) runs the key-permuted variant only, compiled with the bias term; the
   // other instantiations carry no trace of it
-  auto kern = scl.alibi != nullptr ? paged_decode_v2_kernel<D, 16, 2, F, true>
+  auto kern = (scl.alibi != nullptr || scl.bs_shift != 0) ? paged_decode_v2_kernel<D, 16, 2, F, true>
               : variant == 2       ? paged_decode_v2_kernel<D, 16, 1, F>
               : variant == 4       ? paged_decode_v2_kernel<D, 16, 2, F>
                                    : paged_decode_v2_kernel<D, 16, 0, F>;
@@ -604,20 +632,21 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
                              int64_t out_stride, void* part_o, void* part_ml, int B, int Hq, int Hkv, int D, int P,
                              int part_size, int max_parts, float scale, int window, const int* order, int kv_fmt,
                              float k_scale, float v_scale, float softcap, const float* sinks, const float* alibi,
-                             const int* row_lo, hipStream_t stream) {
+                             const int* row_lo, int64_t bsparse, hipStream_t stream) {
   if (B <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
   if (part_size < 0 || part_size % 128 != 0 || max_parts <= 0) return -4;   // 0: per-sequence span
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
-  Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
+  Scaler scl = make_scaler(scale * k_scale, softcap, alibi, bsparse);
   scl.row_lo = row_lo;
   dim3 grid(max_parts, Hkv, B);
   // A/B switch for benchmarking: 1 = v1, 2 = v2 (register ring), 3 = v2 without ring, 4 = v3 with
   // key-permuted tiles (16-B V loads; default: 5.38 vs 5.24 TB/s on the bench's context mix)
   const char* ve = getenv("OME_DECODE_ATTN");
   int variant = ve ? atoi(ve) : 4;
-  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks || alibi || row_lo || part_size == 0))
+  if (variant == 1 && (kv_fmt != KV_BF16 || D != 128 || softcap > 0.f || sinks || alibi || row_lo || part_size == 0 ||
+                       scl.bs_shift != 0))
     variant = 4;  // v1: plain bf16 D=128, fixed partitions
   if (variant == 1) {
     const size_t smem = (128 + 4 * 16 * D) * sizeof(float);
@@ -714,7 +743,8 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
           sc[rb][1] = mfma16(a1, qf[rb][ks], sc[rb][1]);
         }
       }
-      const bool need_mask = (kb + 32 > prefix + r0 + 1) || (kb + 32 > kv_len) || (window > 0 || window < -1);
+      const bool need_mask = (kb + 32 > prefix + r0 + 1) || (kb + 32 > kv_len) || (window > 0 || window < -1) ||
+                             scl.bs_shift != 0;
       bf16x8 pb[2];
       float alpha[2];
 #pragma unroll
@@ -730,7 +760,8 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
             const int key = kb + 16 * X + 4 * g + i;
             if (al != 0.f) v += al * (float)(key - qpos);
             if (need_mask) {
-              const bool ok = key <= qlim && key < kv_len && key >= attn_lo(qpos, window);
+              const bool ok = key <= qlim && key < kv_len && key >= attn_lo(qpos, window) &&
+                               scl.bs_visible(qpos, key, head);
               v = ok ? v : OME_NEG_INF;
             }
             sc[rb][X][i] = v;
@@ -946,7 +977,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
         bf16x8 pb[2];
         float alpha[2];
         const bool need_mask =
-            (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0 || window < -1);
+            (kbu + 32 > prefix + r0 + 1) || (kbu + 32 > kv_len) || (window > 0 || window < -1) ||
+            scl.bs_shift != 0;
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
           const int qpos = prefix + r0 + 16 * rb + n;
@@ -960,7 +992,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
               const int key = kbu + 16 * X + 4 * g + i;
               if (al != 0.f) v += al * (float)(key - qpos);
               if (need_mask) {
-                const bool ok = key <= qlim && key < kv_len && key >= attn_lo(qpos, window);
+                const bool ok = key <= qlim && key < kv_len && key >= attn_lo(qpos, window) &&
+                               scl.bs_visible(qpos, key, head);
                 v = ok ? v : OME_NEG_INF;
               }
               sc[rb][X][i] = v;
@@ -1209,7 +1242,8 @@ static bool prefill_fast(const Scaler& scl, int window, const int* row_hi) {
     const char* e = getenv("OME_PREFILL_FAST");
     return e && atoi(e) == 0;
   }();
-  return !off && scl.cap_inv == 0.f && scl.alibi == nullptr && row_hi == nullptr && (window == -1 || window == 0);
+  return !off && scl.cap_inv == 0.f && scl.alibi == nullptr && scl.bs_shift == 0 && row_hi == nullptr &&
+         (window == -1 || window == 0);
 }
 
 template <int D, int F>
@@ -1262,14 +1296,14 @@ OME_API int ome_paged_prefill(const void* q, int64_t q_stride, const void* k_cac
                               const int* items, int n_items, void* out, int64_t out_stride, int Hq, int Hkv, int D,
                               int P, float scale, int window, int kv_fmt, float k_scale, float v_scale,
                               float softcap, const float* sinks, const float* alibi, const int* row_hi,
-                              int rows, hipStream_t stream) {
+                              int rows, int64_t bsparse, hipStream_t stream) {
   if (n_items <= 0) return 0;
   if (rows != 32 && rows != 64) return -2;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0) return -3;
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
   const int G = Hq / Hkv;
-  const Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
+  const Scaler scl = make_scaler(scale * k_scale, softcap, alibi, bsparse);
   dim3 grid(n_items, Hkv);
   const char* ve = getenv("OME_PREFILL_ATTN");
   const int variant = ve ? atoi(ve) : 2;
@@ -1294,10 +1328,10 @@ OME_API int ome_paged_prefill_split(const void* q, int64_t q_stride, const void*
                                     const int* items4, int n_items, const int* comb, int n_comb, int chunk,
                                     void* part_o, void* part_ml, void* out, int64_t out_stride, int Hq, int Hkv,
                                     float scale, int window, int kv_fmt, float k_scale, float v_scale, float softcap,
-                                    const float* sinks, const float* alibi, hipStream_t stream) {
+                                    const float* sinks, const float* alibi, int64_t bsparse, hipStream_t stream) {
   if (n_items <= 0) return 0;
   if (Hq != 4 * Hkv || chunk % 64 || kv_fmt < 0 || kv_fmt > 2) return -2;
-  const Scaler scl = make_scaler(scale * k_scale, softcap, alibi);
+  const Scaler scl = make_scaler(scale * k_scale, softcap, alibi, bsparse);
   dim3 grid(n_items, Hkv);
 #define OME_PFS(F, FAST)                                                                                       \
   paged_prefill_v2_kernel<2, F, true, FAST><<<grid, 256, 0, stream>>>(                                         \

@@ -27,10 +27,12 @@ __global__ __launch_bounds__(256) void act_and_mul_kernel(const bf16* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float gf = (float)g[j];
-    if constexpr (ACT == 2) {
-      // GPT-OSS clamped SwiGLU: (clamp(u, -7, 7) + 1) * g' * sigmoid(1.702 g'), g' = min(g, 7)
-      const float g2 = fminf(gf, 7.f);
-      const float u2 = fminf(fmaxf((float)u[j], -7.f), 7.f);
+    if constexpr (ACT == 2 || ACT == 3) {
+      // clamped SwiGLU / GeGELU: (clamp(u, -L, L) + 1) * g' * sigmoid(1.702 g'), g' = min(g, L);
+      // L = 7 (GPT-OSS), 20 (Phi-3-small gegelu_limit)
+      constexpr float L = ACT == 2 ? 7.f : 20.f;
+      const float g2 = fminf(gf, L);
+      const float u2 = fminf(fmaxf((float)u[j], -L), L);
       o[j] = (bf16)((u2 + 1.f) * g2 / (1.f + __expf(-1.702f * g2)));
     } else {
       const float a = ACT == 0 ? silu(gf) : gelu_tanh(gf);
@@ -66,7 +68,8 @@ static inline int grid_for(int64_t work, int nt) {
   return (int)g;
 }
 
-// act: 0 SiLU, 1 GELU-tanh, 2 GPT-OSS clamped SwiGLU; | 16: interleaved gate/up (16-col blocks)
+// act: 0 SiLU, 1 GELU-tanh, 2 GPT-OSS clamped SwiGLU (limit 7), 3 Phi-3-small GeGELU (limit 20);
+// | 16: interleaved gate/up (16-col blocks)
 OME_API int ome_act_and_mul(const void* x, void* out, int64_t rows, int I, int act, hipStream_t stream) {
   if (rows <= 0) return 0;
   const bool il = (act & 16) != 0;
@@ -81,8 +84,10 @@ OME_API int ome_act_and_mul(const void* x, void* out, int64_t rows, int I, int a
       act_and_mul_kernel<0><<<g, 256, 0, stream>>>(xp, op, n, I, il);
     else if (act == 1)
       act_and_mul_kernel<1><<<g, 256, 0, stream>>>(xp, op, n, I, il);
-    else
+    else if (act == 2)
       act_and_mul_kernel<2><<<g, 256, 0, stream>>>(xp, op, n, I, il);
+    else
+      act_and_mul_kernel<3><<<g, 256, 0, stream>>>(xp, op, n, I, il);
   }
   OME_CHECK_LAUNCH();
   return 0;

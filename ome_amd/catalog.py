@@ -137,6 +137,7 @@ FAMILIES: list[Family] = [
     Family("phi-3-vision-128k-instruct", "microsoft", "microsoft/Phi-3-vision-128k-instruct", "Phi3VForCausalLM", 4.2,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("phi-3-mini-4k-instruct", "microsoft", "microsoft/Phi-3-mini-4k-instruct", "Phi3ForCausalLM", 3.8),
+    Family("phi-3-small-8k-instruct", "microsoft", "microsoft/Phi-3-small-8k-instruct", "Phi3SmallForCausalLM", 7.4),
     Family("phi-3-5-moe-instruct", "microsoft", "microsoft/Phi-3.5-MoE-instruct", "PhiMoEForCausalLM", 41.9),
     Family("starcoder2-7b", "bigcode", "bigcode/starcoder2-7b", "Starcoder2ForCausalLM", 7.2, "starcoder2-7b"),
     Family("pythia-1-4b", "eleutherai", "EleutherAI/pythia-1.4b", "GPTNeoXForCausalLM", 1.4, "pythia-1.4b"),

@@ -17,7 +17,7 @@ import torch
 
 
 # dense families of ``models/decoder.py`` (zero-padded head dims are handled there)
-PADDED_HEAD_ARCHS = {"OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM", "RWForCausalLM",
+PADDED_HEAD_ARCHS = {"Phi3SmallForCausalLM", "OPTForCausalLM", "GPTJForCausalLM", "FalconForCausalLM", "RWForCausalLM",
                      "StableLmForCausalLM", "PersimmonForCausalLM", "CohereForCausalLM", "GlmForCausalLM",
                      "Glm4ForCausalLM", "Olmo2ForCausalLM", "OlmoForCausalLM", "ArceeForCausalLM",
                      "BloomForCausalLM", "MptForCausalLM", "MPTForCausalLM", "Phi3ForCausalLM", "GraniteForCausalLM",
@@ -113,6 +113,9 @@ def _standard_keys(c: dict[str, Any]) -> dict[str, Any]:
         a = dict(attention_bias=c.get("use_qkv_bias", False))
     elif mt == "persimmon":
         a = dict(attention_bias=True, hidden_act=c.get("hidden_act", "relu2"))
+    elif mt == "phi3small":   # microsoft/Phi-3-small (remote code)
+        a = dict(intermediate_size=c.get("ff_intermediate_size"), rope_theta=c.get("rope_embedding_base", 1e6),
+                 layer_norm_eps=c.get("layer_norm_epsilon", 1e-5), attention_bias=True, tie_word_embeddings=False)
     elif mt in ("cohere", "olmo"):
         a = dict(layer_norm_eps=c.get("layer_norm_eps") or 1e-5, tie_word_embeddings=c.get("tie_word_embeddings",
                                                                                          mt == "cohere"))

@@ -52,7 +52,8 @@ from ome_amd.parallel import state as pstate
 # kernel activation codes (csrc/kernels/elementwise.hip): plain ``ops.act`` and gated ``ops.act_and_mul``
 ACT_PLAIN = {"silu": 0, "swish": 0, "gelu_pytorch_tanh": 1, "gelu_new": 1, "gelu_fast": 1, "gelu": 3,
              "relu2": 4, "relu": 5}
-ACT_GATED = {"silu": 0, "swish": 0, "gelu_pytorch_tanh": 1, "gelu_new": 1, "gelu_fast": 1}
+ACT_GATED = {"silu": 0, "swish": 0, "gelu_pytorch_tanh": 1, "gelu_new": 1, "gelu_fast": 1,
+             "gegelu": 3}   # gegelu: Phi-3-small (ops.act_and_mul act 3, gate / up de-interleaved at load)
 
 _LLAMA_NAMES = [
     (r"(?:model\.)?embed_tokens\.weight", "embed"),
@@ -215,6 +216,22 @@ def _spec_for(cfg: ModelConfig) -> DecoderSpec:
         names = list(_LLAMA_NAMES) + [(r"score\.(\d+)\.(weight|bias)", r"head.\1.\2"),
                                       (r"score\.(weight|bias)", r"head.0.\1")]
         return DecoderSpec(head="reward_mlp" if arch == "Qwen2ForRewardModel" else "score", names=names)
+    if arch == "Phi3SmallForCausalLM":   # models/phi3small.py: grouped biased QKV, LayerNorm, muP scalings
+        hd = cfg.attn_head_dim or cfg.head_dim   # the checkpoint's head dim (before kernel padding)
+        mup = bool(hf.get("mup_use_scaling", True))
+        return DecoderSpec(norm="ln", qkv_layout="groups",
+                           embed_scale=float(hf.get("mup_embedding_multiplier") or 1.0),
+                           attn_scale=float(hf.get("mup_attn_multiplier", 1.0)) / hd if mup else None,
+                           logit_mult=1.0 / float(hf.get("mup_width_multiplier") or 1.0),
+                           prefixes=("model.",), names=[
+                               (r"embed_tokens\.weight", "embed"), (r"final_layernorm\.(weight|bias)", r"norm.\1"),
+                               (r"lm_head\.weight", "lm_head.weight"),
+                               (r"layers\.(\d+)\.self_attn\.query_key_value\.(weight|bias)", r"L.\1.qkv.\2"),
+                               (r"layers\.(\d+)\.self_attn\.dense\.(weight|bias)", r"L.\1.o.\2"),
+                               (r"layers\.(\d+)\.mlp\.gate_up_il\.(weight|bias)", r"L.\1.gate_up.\2"),
+                               (r"layers\.(\d+)\.mlp\.down_proj\.(weight|bias)", r"L.\1.down.\2"),
+                               (r"layers\.(\d+)\.input_layernorm\.(weight|bias)", r"L.\1.ln1.\2"),
+                               (r"layers\.(\d+)\.post_attention_layernorm\.(weight|bias)", r"L.\1.ln2.\2")])
     if arch == "MiMoForCausalLM":  # Qwen2 layout; the multi-token-prediction layers (mtp_layers.*) are unused
         return DecoderSpec()
     if arch == "QWenLMHeadModel":  # Qwen (v1): fused biased c_attn, SwiGLU as c_proj(w1(x) * silu(w2(x)))

@@ -187,7 +187,8 @@ def kv_cache_write(k, v, k_cache, v_cache, slots, k_scale: float = 1.0, v_scale:
 
 def act_and_mul(x: torch.Tensor, act: int = 0, out: torch.Tensor | None = None,
                 interleaved: bool = False) -> torch.Tensor:
-    """act 0 = SiLU (SwiGLU), 1 = GELU-tanh (GeGLU).  x [.., 2I] -> [.., I].  ``interleaved``:
+    """act 0 = SiLU (SwiGLU), 1 = GELU-tanh (GeGLU), 2 = GPT-OSS clamped SwiGLU, 3 = Phi-3-small
+    GeGELU (quick-GELU gate, limit 20, ``up + 1``).  x [.., 2I] -> [.., I].  ``interleaved``:
     gate / up columns alternate in 16-column blocks (:func:`interleave_gate_up` weights)."""
     if not _gpu(x):
         if interleaved:
@@ -471,18 +472,33 @@ class DecodeWorkspace:
         self.part_ml = torch.empty(max_batch * Hq * self.max_parts * 2, dtype=torch.float32, device=device)
 
 
+def blocksparse_pack(bs) -> int:
+    """(block, local_blocks, vert_stride, head_step, head0) -> the packed int64 of the attention
+    kernels (attention.hip ``set_blocksparse``); None -> 0 (dense)."""
+    if bs is None:
+        return 0
+    block, local, vert, step, h0 = (int(v) for v in bs)
+    shift = block.bit_length() - 1
+    if block != 1 << shift or not 0 < shift < 16 or not 0 < local < 1 << 16 or not 0 < vert < 1 << 12 or \
+            not 0 <= step < 256 or not 0 <= h0 < 4096:
+        raise ValueError(f"unsupported block-sparse parameters {bs}")
+    return shift | local << 4 | vert << 20 | step << 32 | h0 << 40
+
+
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeWorkspace | None = None,
                  window: int = -1, out=None, order: torch.Tensor | None = None, k_scale: float = 1.0,
                  v_scale: float = 1.0, softcap: float = 0.0, sinks: torch.Tensor | None = None,
-                 alibi: torch.Tensor | None = None, row_lo: torch.Tensor | None = None) -> torch.Tensor:
+                 alibi: torch.Tensor | None = None, row_lo: torch.Tensor | None = None,
+                 blocksparse: tuple | None = None) -> torch.Tensor:
     """q [B, Hq, D] -> [B, Hq, D].  ``alibi``: fp32 [Hq] ALiBi slopes (logit += slope * (key - query
     position)), or None.  ``row_lo``: int32 [B], row b attends keys [row_lo[b], seq_lens[b]) only
     (Mllama cross attention over a range of a request's vision-token cache).  ``order`` (int32 [B], optional): sequence visit order for the
     workgroup dispatcher (longest first balances the tail).  The cache may be bf16 or fp8
-    (``k_scale`` / ``v_scale`` dequantise it)."""
+    (``k_scale`` / ``v_scale`` dequantise it).  ``blocksparse``: (block, local_blocks, vert_stride,
+    head_step, head0) block-sparse causal mask (Phi-3-small), None = dense."""
     if not _gpu(q):
         r = ref.paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window, k_scale, v_scale, softcap,
-                             sinks, alibi, row_lo)
+                             sinks, alibi, row_lo, blocksparse)
         if out is not None:
             out.copy_(r)
             return out
@@ -497,7 +513,7 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, ws: DecodeW
          out.stride(0), ws.part_o.data_ptr(), ws.part_ml.data_ptr(), B, Hq, Hkv, D, P, ws.part_size, ws.max_parts,
          float(scale), int(window), _i32(order).data_ptr() if order is not None else None, kv_format(k_cache),
          float(k_scale), float(v_scale), float(softcap), _sinks(sinks), _sinks(alibi),
-         _i32(row_lo).data_ptr() if row_lo is not None else None, stream_ptr())
+         _i32(row_lo).data_ptr() if row_lo is not None else None, blocksparse_pack(blocksparse), stream_ptr())
     return out
 
 
@@ -1139,14 +1155,14 @@ def prefill_plan(q_lens: list[int], kv_lens: list[int], tile: int = 32, target: 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale, window: int = -1,
                   out=None, k_scale: float = 1.0, v_scale: float = 1.0, softcap: float = 0.0,
                   sinks: torch.Tensor | None = None, alibi: torch.Tensor | None = None,
-                  row_hi: torch.Tensor | None = None) -> torch.Tensor:
+                  row_hi: torch.Tensor | None = None, blocksparse: tuple | None = None) -> torch.Tensor:
     """q [Tq, Hq, D]; items int32 [n, 2] from :func:`prefill_work_items`.  ``softcap`` > 0:
     attention-logit soft-capping ``cap * tanh(score / cap)`` (Gemma-2); ``alibi``: fp32 [Hq]
     ALiBi slopes; ``row_hi``: int32 [Tq], per query row the last key position it may see
     beyond the causal one (-1: causal) -- Gemma 3's bidirectional image blocks."""
     if not _gpu(q):
         r = ref.paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window, k_scale, v_scale,
-                              softcap, sinks, alibi, row_hi)
+                              softcap, sinks, alibi, row_hi, blocksparse)
         if out is not None:
             out.copy_(r)
             return out
@@ -1170,13 +1186,14 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
                  _i32(kv_lens).data_ptr(), plan.split.data_ptr(), plan.split.shape[0], plan.comb.data_ptr(),
                  plan.comb.shape[0], int(plan.chunk), po.data_ptr(), pml.data_ptr(), out.data_ptr(), out.stride(0),
                  Hq, Hkv, float(scale), int(window), kv_format(k_cache), float(k_scale), float(v_scale),
-                 float(softcap), _sinks(sinks), _sinks(alibi), stream_ptr())
+                 float(softcap), _sinks(sinks), _sinks(alibi), blocksparse_pack(blocksparse), stream_ptr())
             return out
     call("ome_paged_prefill", q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
          _i32(block_tables).data_ptr(), block_tables.stride(0), _i32(cu_q).data_ptr(), _i32(kv_lens).data_ptr(),
          _i32(items).data_ptr(), items.shape[0], out.data_ptr(), out.stride(0), Hq, Hkv, D, P, float(scale),
          int(window), kv_format(k_cache), float(k_scale), float(v_scale), float(softcap), _sinks(sinks),
-         _sinks(alibi), None if row_hi is None else _i32(row_hi).data_ptr(), rows, stream_ptr())
+         _sinks(alibi), None if row_hi is None else _i32(row_hi).data_ptr(), rows, blocksparse_pack(blocksparse),
+         stream_ptr())
     return out
 
 

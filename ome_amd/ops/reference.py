@@ -189,9 +189,10 @@ def kv_cache_write(k, v, k_cache, v_cache, slots, P, k_scale=1.0, v_scale=1.0) -
 def act_and_mul(x: torch.Tensor, act: int = 0) -> torch.Tensor:
     I = x.shape[-1] // 2
     g, u = x[..., :I].float(), x[..., I:].float()
-    if act == 2:  # GPT-OSS clamped SwiGLU
-        g = g.clamp(max=7.0)
-        u = u.clamp(-7.0, 7.0)
+    if act in (2, 3):  # clamped SwiGLU / GeGELU: GPT-OSS (limit 7), Phi-3-small (limit 20)
+        lim = 7.0 if act == 2 else 20.0
+        g = g.clamp(max=lim)
+        u = u.clamp(-lim, lim)
         return ((u + 1) * g * torch.sigmoid(1.702 * g)).to(x.dtype)
     a = torch.nn.functional.silu(g) if act == 0 else torch.nn.functional.gelu(g, approximate="tanh")
     return (a * u).to(x.dtype)
@@ -238,8 +239,17 @@ def attn_lo(qpos, window: int):
     return qpos * 0
 
 
+def blocksparse_visible(qpos: torch.Tensor, kpos: torch.Tensor, heads: torch.Tensor, bs) -> torch.Tensor:
+    """Block-sparse causal visibility (attention.hip ``Scaler::bs_visible``; Phi-3-small):
+    ``bs`` = (block, local_blocks, vert_stride, head_step, head0); broadcasts qpos / kpos / heads.
+    The causal limit itself is applied by the caller."""
+    block, local, vert, step, h0 = bs
+    qb, kb = torch.div(qpos, block, rounding_mode="floor"), torch.div(kpos, block, rounding_mode="floor")
+    return ((qb - kb) < local) | (((kb + h0 + heads * step + 1) % vert) == 0)
+
+
 def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, k_scale=1.0,
-                 v_scale=1.0, softcap=0.0, sinks=None, alibi=None, row_lo=None) -> torch.Tensor:
+                 v_scale=1.0, softcap=0.0, sinks=None, alibi=None, row_lo=None, blocksparse=None) -> torch.Tensor:
     B, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -259,13 +269,18 @@ def paged_decode(q, k_cache, v_cache, block_tables, seq_lens, scale, window=-1, 
             if alibi is not None:  # slope * (key - query position)
                 kp = torch.arange(lo, L, device=q.device, dtype=torch.float32) - (L - 1)
                 s = s + alibi[h * G:(h + 1) * G].float().view(G, 1).to(s.device) * kp[None]
+            if blocksparse is not None:
+                kp = torch.arange(lo, L, device=q.device)[None]
+                hs = torch.arange(h * G, (h + 1) * G, device=q.device)[:, None]
+                s = s.masked_fill(~blocksparse_visible(torch.tensor(L - 1, device=q.device), kp, hs, blocksparse),
+                                  float("-inf"))
             sk = None if sinks is None else sinks[h * G:(h + 1) * G].float().view(G, 1)
             out[b, h * G:(h + 1) * G] = (_softmax_sink(s, sk) @ v).to(q.dtype)
     return out
 
 
 def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, window=-1, k_scale=1.0,
-                  v_scale=1.0, softcap=0.0, sinks=None, alibi=None, row_hi=None) -> torch.Tensor:
+                  v_scale=1.0, softcap=0.0, sinks=None, alibi=None, row_hi=None, blocksparse=None) -> torch.Tensor:
     Tq, Hq, D = q.shape
     Hkv, P = k_cache.shape[1], k_cache.shape[2]
     G = Hq // Hkv
@@ -288,7 +303,11 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, scale, windo
             if alibi is not None:
                 sl = alibi[h * G:(h + 1) * G].float().view(G, 1, 1).to(sc.device)
                 sc = sc + sl * (kpos - qpos).float()[None]
-            sc = sc.masked_fill(~mask[None], float("-inf"))
+            m = mask[None]
+            if blocksparse is not None:
+                hs = torch.arange(h * G, (h + 1) * G, device=q.device).view(G, 1, 1)
+                m = m & blocksparse_visible(qpos[None], kpos[None], hs, blocksparse)
+            sc = sc.masked_fill(~m, float("-inf"))
             sk = None if sinks is None else sinks[h * G:(h + 1) * G].float().view(G, 1, 1).expand(G, sc.shape[1], 1)
             o = _softmax_sink(sc, sk) @ v
             out[q0:q1, h * G:(h + 1) * G] = o.transpose(0, 1).to(q.dtype)

@@ -469,3 +469,29 @@ def test_paged_prefill_64_row_items(q_lens, kv_lens, window):
     q = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
     out = ops.paged_prefill(q, kc, vc, bt, cu, kl, plan, 0.0884, window=window)
     _close(out, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884, window), atol=2e-2)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])   # GQA-4 (the v2 prefill kernel) and G = 8 (generic)
+@pytest.mark.parametrize("bs", [(64, 16, 8, 1, 0), (64, 4, 8, 1, 32), (16, 2, 3, 0, 0)])
+def test_blocksparse_prefill_decode(Hq, Hkv, bs):
+    """Phi-3-small block-sparse causal attention (local band + per-head vertical stripes) in the
+    paged prefill (classic and split-KV plans) and decode kernels == the fp32 reference."""
+    D, P = 128, 16
+    q_lens, kv_lens = [1500, 37, 300], [1500, 1200, 2100]
+    npages = sum(-(-L // P) for L in kv_lens) + 8
+    kc, vc = _cache(npages, Hkv, D)
+    bt = _block_tables(kv_lens, P, npages)
+    cu = torch.tensor([0] + list(torch.tensor(q_lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    kl = torch.tensor(kv_lens, dtype=torch.int32, device=DEV)
+    q = torch.randn(sum(q_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    want = ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884, blocksparse=bs)
+    items = torch.tensor(ops.prefill_work_items(q_lens, kv_lens), dtype=torch.int32, device=DEV)
+    _close(ops.paged_prefill(q, kc, vc, bt, cu, kl, items, 0.0884, blocksparse=bs), want, atol=2e-2)
+    if Hq == 4 * Hkv:
+        _close(ops.paged_prefill(q, kc, vc, bt, cu, kl, _plan(q_lens, kv_lens, 128), 0.0884, blocksparse=bs), want,
+               atol=2e-2)
+    assert not torch.allclose(want, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884), atol=1e-2)   # mask bites
+    qd = torch.randn(len(kv_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
+    ws = ops.DecodeWorkspace(len(kv_lens), Hq, D, 4096, 256, DEV)
+    _close(ops.paged_decode(qd, kc, vc, bt, kl, 0.0884, ws, blocksparse=bs),
+           ref.paged_decode(qd, kc, vc, bt, kl, 0.0884, blocksparse=bs), atol=2e-2)
