@@ -169,6 +169,10 @@ FAMILIES: list[Family] = [
     Family("internlm2-7b-reward", "internlm", "internlm/internlm2-7b-reward", "InternLM2ForRewardModel", 7.7,
            capabilities=["TEXT_EMBEDDINGS"], args=["--is-embedding"]),
     Family("qwen-7b-chat", "qwen", "Qwen/Qwen-7B-Chat", "QWenLMHeadModel", 7.7),
+    Family("qwen-vl-chat", "qwen", "Qwen/Qwen-VL-Chat", "QWenLMHeadModel", 9.6,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], runtime=True),
+    Family("qwen-vl", "qwen", "Qwen/Qwen-VL", "QWenLMHeadModel", 9.6,
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("baichuan2-7b-chat", "baichuan-inc", "baichuan-inc/Baichuan2-7B-Chat", "BaichuanForCausalLM", 7.5),
     Family("baichuan2-13b-chat", "baichuan-inc", "baichuan-inc/Baichuan2-13B-Chat", "BaichuanForCausalLM", 13.9),
     Family("exaone-3-5-7-8b-instruct", "lgai-exaone", "LGAI-EXAONE/EXAONE-3.5-7.8B-Instruct", "ExaoneForCausalLM",

@@ -159,6 +159,10 @@ def model_class(cfg: ModelConfig):
 
         if cfg.architecture in DECODER_MOE_ARCHS:
             return DecoderMoEForCausalLM
+        if cfg.architecture == "QWenLMHeadModel" and (cfg.extra or {}).get("visual"):
+            from ome_amd.models.qwen_vl import QwenVLForCausalLM
+
+            return QwenVLForCausalLM
         if cfg.architecture == "Phi3SmallForCausalLM":
             from ome_amd.models.phi3small import Phi3SmallForCausalLM
 
