@@ -2,6 +2,7 @@
 #include "omeio.h"
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -70,6 +71,38 @@ bool pwrite_full(int fd, const void* src, uint64_t len, uint64_t off) {
     len -= static_cast<uint64_t>(r);
   }
   return true;
+}
+
+// Read-only mapping of a file range for strided slice gathers.  A TP rank's slice of a
+// row-parallel weight is a short piece (K / tp elements) of every row: one pread per row costs a
+// syscall + page-cache lookup per few KB (2.6 GB/s measured for TP = 8, profiles/r04_llama70b_tp1.md),
+// while a memcpy out of the mapping streams the same bytes at memory speed once the pages are
+// resident (MADV_WILLNEED starts readahead of the whole range up front; ranks of one node share
+// the page cache, so the file is read from storage once for all of them).
+struct Mapping {
+  void* base = MAP_FAILED;
+  size_t len = 0;
+  const char* at = nullptr;   // byte file_off of the request
+  Mapping(int fd, uint64_t file_off, uint64_t span) {
+    const uint64_t pg = static_cast<uint64_t>(sysconf(_SC_PAGESIZE));
+    const uint64_t a = file_off / pg * pg;
+    len = static_cast<size_t>(file_off - a + span);
+    base = mmap(nullptr, len, PROT_READ, MAP_SHARED | MAP_POPULATE, fd, static_cast<off_t>(a));
+    if (base != MAP_FAILED) {
+      madvise(base, len, MADV_WILLNEED);
+      at = static_cast<const char*>(base) + (file_off - a);
+    }
+  }
+  bool ok() const { return base != MAP_FAILED; }
+  ~Mapping() {
+    if (base != MAP_FAILED) munmap(base, len);
+  }
+};
+
+// rows [r0, r0 + nr) of a strided slice from the mapping into a compact buffer
+void gather_rows(const Mapping& m, uint64_t r0, uint64_t nr, uint64_t stride, uint64_t row_bytes, char* dst) {
+  for (uint64_t r = 0; r < nr; ++r) memcpy(dst + r * row_bytes, m.at + (r0 + r) * stride, row_bytes);
+  g_bytes_read.fetch_add(nr * row_bytes, std::memory_order_relaxed);
 }
 
 struct Piece {
@@ -217,6 +250,7 @@ OMEIO_API int omeio_load_strided(const char* path, uint64_t file_off, uint64_t n
   const uint64_t rows_per = std::max<uint64_t>(1, chunk / row_bytes);
   const uint64_t nruns = (nrows + rows_per - 1) / rows_per;
   const uint64_t stage_bytes = rows_per * row_bytes;
+  const Mapping map(f.fd, file_off, (nrows - 1) * file_stride + row_bytes);   // pread per row if it fails
   nthreads = std::max(1, std::min<int>(nthreads, static_cast<int>(nruns)));
   std::atomic<int> err{0};
   std::vector<std::thread> th;
@@ -243,11 +277,15 @@ OMEIO_API int omeio_load_strided(const char* path, uint64_t file_off, uint64_t n
         }
         const uint64_t r0 = run * rows_per, nr = std::min(rows_per, nrows - r0);
         char* st = static_cast<char*>(stage[b]);
-        for (uint64_t r = 0; r < nr; ++r)
-          if (!pread_full(f.fd, st + r * row_bytes, row_bytes, file_off + (r0 + r) * file_stride)) {
-            err = -EIO;
-            break;
-          }
+        if (map.ok()) {
+          gather_rows(map, r0, nr, file_stride, row_bytes, st);
+        } else {
+          for (uint64_t r = 0; r < nr; ++r)
+            if (!pread_full(f.fd, st + r * row_bytes, row_bytes, file_off + (r0 + r) * file_stride)) {
+              err = -EIO;
+              break;
+            }
+        }
         if (err.load()) break;
         if (hipMemcpyAsync(static_cast<char*>(dst) + r0 * row_bytes, st, nr * row_bytes, hipMemcpyHostToDevice, s) !=
                 hipSuccess ||
@@ -274,6 +312,19 @@ OMEIO_API int omeio_read_strided(const char* path, uint64_t file_off, uint64_t n
                                  uint64_t row_bytes, void* dst) {
   Fd f(open(path, O_RDONLY | O_CLOEXEC));
   if (f.fd < 0) return fail(-ENOENT, std::string("open ") + path + ": " + strerror(errno));
+  if (nrows == 0 || row_bytes == 0) return 0;
+  const Mapping map(f.fd, file_off, (nrows - 1) * file_stride + row_bytes);
+  if (map.ok()) {   // gather from the mapping, a few threads over row ranges
+    const int nt = static_cast<int>(std::min<uint64_t>(8, std::max<uint64_t>(1, nrows * row_bytes >> 20)));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([&, t] {
+        const uint64_t lo = nrows * t / nt, hi = nrows * (t + 1) / nt;
+        gather_rows(map, lo, hi - lo, file_stride, row_bytes, static_cast<char*>(dst) + lo * row_bytes);
+      });
+    for (auto& x : th) x.join();
+    return 0;
+  }
   for (uint64_t r = 0; r < nrows; ++r)
     if (!pread_full(f.fd, static_cast<char*>(dst) + r * row_bytes, row_bytes, file_off + r * file_stride))
       return fail(-EIO, std::string("strided read failed: ") + path);
