@@ -20,6 +20,8 @@
 // spreads both the row reads and the transposed reads over the banks.
 #include "common.h"
 
+#include <cstdlib>
+
 #ifndef OME_NEG_INF
 #define OME_NEG_INF (-__builtin_inff())
 #endif
@@ -188,25 +190,196 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
   }
 }
 
-// merge split-K partitions: one workgroup per (token, head), DV / 4 threads x 4 dims
+// ------------------------------------------------------------------------------------------
+// All-heads variant: one workgroup of NW waves owns 16 * NW heads of a token and one split-K
+// partition, so each latent key tile is streamed from HBM and staged in LDS ONCE for all of them
+// (the 16-head kernel above re-reads every token's latent KV H / 16 times -- 8x for DeepSeek-V3's
+// 128 heads -- and its four waves each recompute the same S^T).  Wave w owns heads 16 w .. 16 w + 15
+// and ALL DV value dims:
+//   S^T [32 keys x 16 heads] = K . Q^T   (2 x DK/32 MFMAs, Q^T resident in 72 VGPRs)
+//   O^T [DV x 16] += V^T . P^T           (DV/16 MFMAs, V^T by hardware-transposed LDS reads)
+// Key tiles arrive by LDS DMA (buffer_load ... lds) into a double-buffered image: the DMA of tile
+// n+1 is issued before tile n is computed and retired (vmcnt(0) + barrier) after it.
+// ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void mla_lds_t;
+
+template <int DK, int DV, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
+    const bf16* __restrict__ q, int64_t q_stride_t, const bf16* __restrict__ cache,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ tok_row,
+    const int* __restrict__ kv_lens, int H, float scale_log2, int parts, bf16* __restrict__ out,
+    int64_t out_stride_t, float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+  static_assert(DK == 576 && lds_chunks<DK>() == DK / 8, "LDS DMA image assumes unpadded 72-chunk rows");
+  constexpr int CH = DK / 8, NI = KT * CH / 64, NB = DV / 16;
+  constexpr int IMG = KT * CH * 8;   // bf16 elements per K-tile image
+  __shared__ __attribute__((aligned(16))) bf16 sK[2 * IMG];
+  const int t = blockIdx.x, part = blockIdx.z;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int col = lane & 15, g = lane >> 4;
+  const int head = blockIdx.y * 16 * NW + wave * 16 + col;   // this lane's head (S^T / O^T column)
+  const int L = kv_lens[t];
+  const int n_pages = (L + 15) >> 4;
+  const int pairs = (n_pages + 1) >> 1;
+  const int per_part = (pairs + parts - 1) / parts;
+  const int pair_begin = part * per_part, pair_end = min(pairs, pair_begin + per_part);
+  const int* bt = block_tables + (int64_t)tok_row[t] * bt_stride;
+
+  // K tile pair -> LDS image: instruction i writes chunks [64 i, 64 i + 64) lane-linearly, each
+  // lane fetching the source chunk the row's XOR swizzle puts there.  A page is 16 rows x 72 chunks
+  // = 18 instructions, so each instruction reads one page: its descriptor is based at that page.
+  auto dma_pair = [&](int pr, bf16* img) {
+#pragma unroll
+    for (int j = 0; j < (NI + NW - 1) / NW; ++j) {
+      const int i = wave + NW * j;
+      if (i >= NI) break;
+      const int c = 64 * i + lane, row = c / CH, xl = c - row * CH;
+      const int pg = 2 * pr + (i >= NI / 2);
+      const int page = bt[pg < n_pages ? pg : 0];
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(cache + (int64_t)page * 16 * DK), (short)0,
+                                                        16 * DK * 2, 0x00020000);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (mla_lds_t*)(img + 64 * 8 * i), 16,
+                                               (uint32_t)(((row & 15) * CH + (xl ^ (row & 7))) * 16), 0, 0, 0);
+    }
+  };
+  if (pair_begin < pair_end) dma_pair(pair_begin, sK);
+
+  bf16x8 qf[DK / 32];
+  const bf16* qp = q + (int64_t)t * q_stride_t + (int64_t)head * DK + 8 * g;
+#pragma unroll
+  for (int s = 0; s < DK / 32; ++s) qf[s] = ld8(qp + 32 * s);
+
+  f32x4 o[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = OME_NEG_INF, lsum = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // The XOR swizzle makes every LDS offset lane-dependent; split it so the compiler sees a lane
+  // base plus an immediate: (8k + c) ^ z = 8k + (c ^ z) for c, z < 8.  S^T reads chunk 4 s + g of
+  // row col (2 bases by s parity); V^T reads chunk 2 nb + pcol/2 of row 4 g + qrow (4 bases by
+  // nb mod 4).  Rows 16..31 sit 16 * CH chunks further on with the same (row & 7).
+  const int qrow = (lane & 15) >> 2, pcol = lane & 3;
+  int sofs[2], vofs[4];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) sofs[e] = (col * CH + ((4 * e + g) ^ (col & 7))) * 16;
+  const int rv = 4 * g + qrow;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) vofs[e] = (rv * CH + ((2 * e + (pcol >> 1)) ^ (rv & 7))) * 16 + (pcol & 1) * 8;
+  int buf = 0;
+  for (int pr = pair_begin; pr < pair_end; ++pr) {
+    const bf16* img = sK + buf * IMG;
+    // the other image's last readers passed the barrier that ended the previous tile
+    if (pr + 1 < pair_end) dma_pair(pr + 1, sK + (buf ^ 1) * IMG);
+    // ---- S^T [32 keys x 16 heads] ----
+    const char* ib = reinterpret_cast<const char*>(img);
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < DK / 32; ++s) {
+      const int off = sofs[s & 1] + (s >> 1) * 128;   // swz(col, 4 s + g): lane base + immediate
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(ib + off);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(ib + off + 16 * CH * 16);
+      s0 = mfma16x32(a0, qf[s], s0);
+      s1 = mfma16x32(a1, qf[s], s1);
+    }
+    const int kbase = pr * KT;
+    float mx = OME_NEG_INF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s0[i] = (kbase + 4 * g + i < L) ? s0[i] * scale_log2 : OME_NEG_INF;
+      s1[i] = (kbase + 16 + 4 * g + i < L) ? s1[i] * scale_log2 : OME_NEG_INF;
+      mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = (m_new == OME_NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - m_new);
+    bf16x8 pb;
+    float ps = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float p0 = (m_new == OME_NEG_INF) ? 0.f : __builtin_amdgcn_exp2f(s0[i] - m_new);
+      const float p1 = (m_new == OME_NEG_INF) ? 0.f : __builtin_amdgcn_exp2f(s1[i] - m_new);
+      ps += p0 + p1;
+      pb[i] = (bf16)p0;
+      pb[4 + i] = (bf16)p1;
+    }
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    lsum = lsum * alpha + ps;
+    m = m_new;
+    // ---- O^T [DV x 16 heads] += V^T . P^T (keys permuted as in pb: 4g + i, 16 + 4g + i) ----
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int off = vofs[nb & 3] + (nb >> 2) * 128;   // swz(4g + qrow, 2 nb + pcol/2) + 8 (pcol & 1)
+      const bf16x4 va = tr_read(img, off);
+      const bf16x4 vb = tr_read(img, off + 16 * CH * 16);
+      bf16x8 a;
+      a[0] = va[0]; a[1] = va[1]; a[2] = va[2]; a[3] = va[3];
+      a[4] = vb[0]; a[5] = vb[1]; a[6] = vb[2]; a[7] = vb[3];
+      o[nb] *= alpha;
+      o[nb] = mfma16x32(a, pb, o[nb]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA has landed
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // ---- epilogue: O^T lane map dim = 16 nb + 4 g + i, head = col ----
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  if (parts == 1) {
+    bf16* op = out + (int64_t)t * out_stride_t + (int64_t)head * DV + 4 * g;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      bf16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = (bf16)(o[nb][i] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * nb) = v;
+    }
+  } else {
+    const int64_t ws_row = ((int64_t)t * H + head) * parts + part;
+    float* wp = ws_o + ws_row * DV + 4 * g;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+      *reinterpret_cast<f32x4*>(wp + 16 * nb) = f32x4{o[nb][0] * inv, o[nb][1] * inv, o[nb][2] * inv,
+                                                       o[nb][3] * inv};
+    if (g == 0) {
+      ws_ml[2 * ws_row] = m;
+      ws_ml[2 * ws_row + 1] = lsum;
+    }
+  }
+}
+
+// merge split-K partitions: one workgroup per (token, head), DV / 4 threads x 4 dims.  Partitions
+// are consumed 8 at a time with all their loads issued up front (online max rescaling), so up to
+// 64 partitions cost ~8 memory latencies rather than one each.
 template <int DV>
 __global__ __launch_bounds__(128) void mla_reduce_kernel(const float* __restrict__ ws_o,
                                                          const float* __restrict__ ws_ml, int H, int parts,
                                                          bf16* __restrict__ out, int64_t out_stride_t) {
   const int t = blockIdx.x, h = blockIdx.y;
   const int64_t row0 = ((int64_t)t * H + h) * parts;
-  float M = OME_NEG_INF;
-  for (int p = 0; p < parts; ++p)
-    if (ws_ml[2 * (row0 + p) + 1] > 0.f) M = fmaxf(M, ws_ml[2 * (row0 + p)]);
+  float M = OME_NEG_INF, den = 0.f;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  float den = 0.f;
-  for (int p = 0; p < parts; ++p) {
-    const float l = ws_ml[2 * (row0 + p) + 1];
-    if (!(l > 0.f)) continue;
-    const float w = l * __builtin_amdgcn_exp2f(ws_ml[2 * (row0 + p)] - M);
-    const f32x4 v = *reinterpret_cast<const f32x4*>(ws_o + (row0 + p) * DV + 4 * threadIdx.x);
-    acc += w * v;
-    den += w;
+  for (int p0 = 0; p0 < parts; p0 += 8) {
+    float mm[8], ll[8];
+    f32x4 vv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t r = row0 + min(p0 + j, parts - 1);
+      mm[j] = ws_ml[2 * r];
+      ll[j] = p0 + j < parts ? ws_ml[2 * r + 1] : 0.f;
+      vv[j] = *reinterpret_cast<const f32x4*>(ws_o + r * DV + 4 * threadIdx.x);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (!(ll[j] > 0.f)) continue;
+      const float mn = fmaxf(M, mm[j]);
+      const float a = __builtin_amdgcn_exp2f(M - mn), w = ll[j] * __builtin_amdgcn_exp2f(mm[j] - mn);
+      acc = acc * a + w * vv[j];
+      den = den * a + w;
+      M = mn;
+    }
   }
   const float inv = den > 0.f ? 1.f / den : 0.f;
   bf16x4 r;
@@ -223,10 +396,28 @@ template <int DK, int DV>
 static void mla_launch(const void* q, int64_t q_stride_t, const void* cache, const int* block_tables, int bt_stride,
                        const int* tok_row, const int* kv_lens, int T, int H, float scale_log2, int parts, void* out,
                        int64_t out_stride_t, float* ws_o, float* ws_ml, hipStream_t stream) {
-  dim3 grid(T, (H + 15) / 16, parts);
-  mla_attn_kernel<DK, DV><<<grid, 256, 0, stream>>>((const bf16*)q, q_stride_t, (const bf16*)cache, block_tables,
-                                                    bt_stride, tok_row, kv_lens, H, scale_log2, parts, (bf16*)out,
-                                                    out_stride_t, ws_o, ws_ml);
+  // all-heads kernel when the heads tile into groups of 128 (DeepSeek-V3 / Kimi-K2 at TP 1) or 64
+  // (TP 2): one latent stream per token and partition; else the 16-head kernel.  OME_MLA_ALL=0
+  // forces the 16-head kernel (A/B timing).
+  static const bool all_ok = !getenv("OME_MLA_ALL") || atoi(getenv("OME_MLA_ALL")) != 0;
+  bool done = false;
+  if constexpr (DK == 576) {
+    if (all_ok && H % 128 == 0) {
+      mla_attn_all_kernel<DK, DV, 8><<<dim3(T, H / 128, parts), 512, 0, stream>>>(
+          (const bf16*)q, q_stride_t, (const bf16*)cache, block_tables, bt_stride, tok_row, kv_lens, H, scale_log2,
+          parts, (bf16*)out, out_stride_t, ws_o, ws_ml);
+      done = true;
+    } else if (all_ok && H % 64 == 0) {
+      mla_attn_all_kernel<DK, DV, 4><<<dim3(T, H / 64, parts), 256, 0, stream>>>(
+          (const bf16*)q, q_stride_t, (const bf16*)cache, block_tables, bt_stride, tok_row, kv_lens, H, scale_log2,
+          parts, (bf16*)out, out_stride_t, ws_o, ws_ml);
+      done = true;
+    }
+  }
+  if (!done)
+    mla_attn_kernel<DK, DV><<<dim3(T, (H + 15) / 16, parts), 256, 0, stream>>>(
+        (const bf16*)q, q_stride_t, (const bf16*)cache, block_tables, bt_stride, tok_row, kv_lens, H, scale_log2,
+        parts, (bf16*)out, out_stride_t, ws_o, ws_ml);
   if (parts > 1)
     mla_reduce_kernel<DV><<<dim3(T, H), DV / 4, 0, stream>>>(ws_o, ws_ml, H, parts, (bf16*)out, out_stride_t);
 }

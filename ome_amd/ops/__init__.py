@@ -526,21 +526,38 @@ def _sinks(s: torch.Tensor | None):
 
 
 class MLAWorkspace:
-    """Split-K partials for :func:`mla_attn`: partitions are only used while (tokens x head
-    groups) is below ~1024 workgroups, so the buffers are bounded by 1024*16 rows."""
+    """Split-K partials for :func:`mla_attn` (``ws_o`` [rows, 512] f32, ``ws_ml`` [rows, 2]; rows =
+    tokens x heads x partitions, bounded by ``ROWS``).
+
+    Two kernels (``mla.hip``): the all-heads kernel (DK 576 with 64 | H: one workgroup streams a
+    token's latent KV once for 64 / 128 heads, one workgroup per CU) and the 16-head kernel (MiniCPM3
+    shapes, TP-sharded head counts).  Partitions lift the grid towards ~1 workgroup per CU (all-heads)
+    or ~1024 workgroups (16-head), and never beyond what the f32 partials' HBM round trip repays:
+    large decode batches (T x H / 128 >= 256) run unsplit."""
 
     TARGET_WGS = 1024
+    TARGET_WGS_ALL = 256
     MAX_PARTS = 16
+    MAX_PARTS_ALL = 64
+    ROWS = 1 << 15
 
     def __init__(self, device="cuda"):
-        rows = self.TARGET_WGS * 16
-        self.ws_o = torch.empty(rows * 512, dtype=torch.float32, device=device)
-        self.ws_ml = torch.empty(rows * 2, dtype=torch.float32, device=device)
+        self.ws_o = torch.empty(self.ROWS * 512, dtype=torch.float32, device=device)
+        self.ws_ml = torch.empty(self.ROWS * 2, dtype=torch.float32, device=device)
+
+    @staticmethod
+    def all_heads(H: int, DK: int = 576) -> bool:
+        return DK == 576 and H % 64 == 0 and os.environ.get("OME_MLA_ALL", "1") != "0"
 
     @classmethod
-    def parts(cls, T: int, H: int) -> int:
-        wgs = T * -(-H // 16)
-        return 1 if wgs >= cls.TARGET_WGS else max(1, min(cls.MAX_PARTS, cls.TARGET_WGS // max(wgs, 1)))
+    def parts(cls, T: int, H: int, DK: int = 576) -> int:
+        if cls.all_heads(H, DK):
+            wgs = T * (H // (128 if H % 128 == 0 else 64))
+            p = max(1, min(cls.MAX_PARTS_ALL, cls.TARGET_WGS_ALL // max(wgs, 1)))
+        else:
+            wgs = T * -(-H // 16)
+            p = 1 if wgs >= cls.TARGET_WGS else max(1, min(cls.MAX_PARTS, cls.TARGET_WGS // max(wgs, 1)))
+        return max(1, min(p, cls.ROWS // max(T * H, 1)))
 
 
 def mla_attn(q, cache, block_tables, tok_row, kv_lens, scale: float, ws: MLAWorkspace | None = None,
@@ -560,7 +577,7 @@ def mla_attn(q, cache, block_tables, tok_row, kv_lens, scale: float, ws: MLAWork
     assert q.stride(2) == 1 and q.stride(1) == DK and cache.shape[-1] == DK
     if out is None:
         out = torch.empty(T, H, dv, dtype=q.dtype, device=q.device)
-    parts = MLAWorkspace.parts(T, H)
+    parts = MLAWorkspace.parts(T, H, DK)
     if parts > 1 and ws is None:
         ws = MLAWorkspace(q.device)
     call("ome_mla_attn", q.data_ptr(), q.stride(0), cache.data_ptr(), _i32(block_tables).data_ptr(),

@@ -858,7 +858,8 @@ class ModelRunner:
 
             whole = [SimpleNamespace(req=c.req, start=0, length=len(c.req.prompt_ids)) for c in batch.chunks]
             embeds = self._mm_prepare(whole, list(range(len(whole))), len(ids), t_ids, meta)
-        hidden = self.model.forward(t_ids, meta, self.kv, embeds)
+        hidden = self.model.forward(t_ids, meta, self.kv, embeds) if embeds is not None else \
+            self.model.forward(t_ids, meta, self.kv)
         pool = getattr(self.model, "pool", None)  # classification / reward heads (models/decoder.py)
         out = pool(hidden, t(cu)) if pool is not None else ops.pool(hidden, t(cu), 0, True)
         return out.cpu().tolist()
