@@ -77,8 +77,23 @@ class PromptFactory:
             except Exception:  # noqa: BLE001 — fall back to the word-count approximation
                 self.tok = None
 
-    def make(self, n_tokens: int) -> str:
-        words = [self.rng.choice(WORDS) for _ in range(max(1, n_tokens))]
+        # without a local tokenizer: server tokens ~= a * words + b, fitted by calibrate()
+        self.tok_per_word, self.overhead = 1.0, 0.0
+
+    def calibrate(self, counts: list[tuple[int, int]]) -> None:
+        """Fit the server's prompt tokens per word from (words, prompt_tokens) probes, so an
+        N(480, 240) scenario sends ~480-token prompts whatever the server's tokenizer (a byte-level
+        fallback turns one word into ~4.6 tokens)."""
+        (w0, t0), (w1, t1) = counts[0], counts[-1]
+        if w1 != w0 and t1 > t0:
+            self.tok_per_word = (t1 - t0) / (w1 - w0)
+            self.overhead = max(0.0, t0 - self.tok_per_word * w0)
+
+    def make(self, n_tokens: int, rng: random.Random | None = None) -> str:
+        rng = rng or self.rng
+        n_words = n_tokens if self.tok is not None else \
+            int(round((n_tokens - self.overhead) / self.tok_per_word))
+        words = [rng.choice(WORDS) for _ in range(max(1, n_words))]
         if self.tok is None:
             return " ".join(words)
         ids = self.tok(" ".join(words), add_special_tokens=False)["input_ids"][:n_tokens]
@@ -119,7 +134,7 @@ async def _one_request(session, args, base: str, scen: Scenario, pf: PromptFacto
     headers = {"Authorization": f"Bearer {args.api_key}"} if args.api_key else {}
     try:
         if args.task in ("text-to-embeddings", "text-to-rerank"):
-            body = {"model": args.api_model_name, "input": pf.make(n_in), **extra}
+            body = {"model": args.api_model_name, "input": pf.make(n_in, rng), **extra}
             async with session.post(f"{base}/v1/embeddings", json=body, headers=headers) as r:
                 data = await r.json()
                 if r.status != 200:
@@ -127,7 +142,7 @@ async def _one_request(session, args, base: str, scen: Scenario, pf: PromptFacto
                 e2e = time.perf_counter() - t0
                 itok = int((data.get("usage") or {}).get("prompt_tokens", n_in))
                 return Sample(True, itok, 0, ttft=e2e, e2e=e2e, start=t0)
-        body = {"model": args.api_model_name, "messages": [{"role": "user", "content": pf.make(n_in)}],
+        body = {"model": args.api_model_name, "messages": [{"role": "user", "content": pf.make(n_in, rng)}],
                 "max_tokens": n_out, "stream": True, "ignore_eos": True, "temperature": 0.0,
                 "stream_options": {"include_usage": True}, **extra}
         ttft, usage, n_chunks = None, None, 0
@@ -162,6 +177,27 @@ async def _one_request(session, args, base: str, scen: Scenario, pf: PromptFacto
         return Sample(False, n_in, 0, start=t0, error=f"{type(e).__name__}: {e}"[:200])
 
 
+async def _calibrate(session, args, base: str, pf: PromptFactory) -> None:
+    """Two 1-token chat requests (50 and 400 words) -> server prompt tokens per word."""
+    headers = {"Authorization": f"Bearer {args.api_key}"} if args.api_key else {}
+    counts = []
+    rng = random.Random(12345)
+    for n in (50, 400):
+        body = {"model": args.api_model_name, "max_tokens": 1, "temperature": 0.0,
+                "messages": [{"role": "user", "content": " ".join(rng.choice(WORDS) for _ in range(n))}]}
+        try:
+            async with session.post(f"{base}/v1/chat/completions", json=body, headers=headers) as r:
+                if r.status != 200:
+                    return
+                usage = (await r.json()).get("usage") or {}
+        except Exception:  # noqa: BLE001 — keep the 1 token / word approximation
+            return
+        if "prompt_tokens" not in usage:
+            return
+        counts.append((n, int(usage["prompt_tokens"])))
+    pf.calibrate(counts)
+
+
 async def run_one(args, scen_text: str, conc: int, seed: int) -> RunResult:
     import aiohttp
 
@@ -183,8 +219,13 @@ async def run_one(args, scen_text: str, conc: int, seed: int) -> RunResult:
 
     async with aiohttp.ClientSession(timeout=timeout,
                                      connector=aiohttp.TCPConnector(limit=max(conc, 1) * 2)) as session:
+        if pf.tok is None and args.task not in ("text-to-embeddings", "text-to-rerank"):
+            await _calibrate(session, args, base, pf)
+
         async def worker(wid: int):
-            rng = random.Random(seed * 1000003 + wid)
+            # per (run seed, concurrency, worker) streams: a sweep's levels do not replay each
+            # other's prompts (the server's prefix cache would turn later levels into cache hits)
+            rng = random.Random((seed * 1000003 + conc) * 1000003 + wid)
             while time.perf_counter() < deadline and budget["left"] > 0:
                 budget["left"] -= 1
                 samples.append(await _one_request(session, args, base, scen, pf, rng, extra))

@@ -90,6 +90,50 @@ def test_decode_batch_drops_requests_preempted_while_scheduling():
     assert all(len(c.req.pages) * 16 >= c.req.seq_len for c in bt.chunks)
 
 
+def test_sjf_admission_with_aging(monkeypatch):
+    """A burst is admitted shortest-prompt first within the chunk budget; a request older than the
+    aging bound (or preempted) goes first regardless of length."""
+    import time as _time
+
+    pages, slots = PagePool(200), ReqSlotPool(17, 64)
+    s = Scheduler(pages, slots, 16, max_running=16, chunked_prefill_size=100, max_context=1000)
+    assert s.policy == "sjf"
+    lens = [90, 10, 60, 20, 30]
+    reqs = [Request(prompt_ids=list(range(n)), params=SamplingParams(max_new_tokens=4)) for n in lens]
+    for r in reqs:
+        s.add(r)
+    b = s.schedule()
+    # budget 100: 10 + 20 + 30 whole, then the first 40 tokens of the 60-token prompt
+    assert [len(c.req.prompt_ids) for c in b.chunks] == [10, 20, 30, 60] and b.chunks[-1].length == 40
+    # aging: the 90-token head has waited past the bound -> admitted before the 60-token one
+    s2 = Scheduler(PagePool(200), ReqSlotPool(17, 64), 16, max_running=16, chunked_prefill_size=100,
+                   max_context=1000)
+    old = Request(prompt_ids=list(range(90)), params=SamplingParams(max_new_tokens=4))
+    old.arrival_time = _time.perf_counter() - 10.0
+    young = Request(prompt_ids=list(range(60)), params=SamplingParams(max_new_tokens=4))
+    s2.add(old)
+    s2.add(young)
+    assert [len(c.req.prompt_ids) for c in s2.schedule().chunks][0] == 90
+    # fifo policy keeps arrival order
+    monkeypatch.setenv("OME_SCHED_POLICY", "fifo")
+    s3 = Scheduler(PagePool(200), ReqSlotPool(17, 64), 16, max_running=16, chunked_prefill_size=100,
+                   max_context=1000)
+    for n in (50, 10):
+        s3.add(Request(prompt_ids=list(range(n)), params=SamplingParams(max_new_tokens=4)))
+    assert [len(c.req.prompt_ids) for c in s3.schedule().chunks] == [50, 10]
+
+
+def test_loadgen_calibrated_prompt_length():
+    from ome_amd.bench.loadgen import PromptFactory
+
+    pf = PromptFactory(None, 0)
+    pf.calibrate([(50, 50 * 4.6 + 12), (400, 400 * 4.6 + 12)])   # byte-level server tokenizer
+    text = pf.make(480, random.Random(1))
+    assert abs(len(text.split()) * 4.6 + 12 - 480) < 6
+    a, b = pf.make(100, random.Random(1)), pf.make(100, random.Random(2))
+    assert a != b
+
+
 def test_stop_conditions():
     pages, slots = PagePool(100), ReqSlotPool(9, 64)
     s = Scheduler(pages, slots, 16, max_running=8, chunked_prefill_size=1000, max_context=1000)
