@@ -169,6 +169,8 @@ __device__ __forceinline__ float row_allreduce(float v) {   // sum over aligned 
     v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
   if constexpr (L >= 16)  // row_mirror
     v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  if constexpr (L >= 32)  // across the two DPP rows of a half-wave (dk = 256)
+    v += __shfl_xor(v, 16);
   return v;
 }
 
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(256) void gdn_scan_v3_kernel(
 
 // q / k / v: row-major views (shared row stride qkv_stride, in elements) of the conv output,
 // q and k [T, Hk * dk], v [T, Hv * dv]; a / b: [T, Hv] views (row stride ab_stride); state fp32
-// [slots, Hv, dv, dk] (transposed); out [T, Hv * dv].  dk in {64, 128}, dv <= 128.  ws: fp32 workspace of
+// [slots, Hv, dv, dk] (transposed); out [T, Hv * dv].  dk in {64, 128, 256} (v1: 64 / 128, dv <= 128).  ws: fp32 workspace of
 // T * (2 * Hk * dk + Hk + 2 * Hv) floats for v3 (null -> the v1 kernel: one lane per state
 // column, q / k staged through LDS; kept as the numerics cross-check and for comparison).
 OME_API int ome_gdn_scan(const void* q, const void* k, const void* v, int64_t qkv_stride, const void* a,
@@ -273,17 +275,21 @@ OME_API int ome_gdn_scan(const void* q, const void* k, const void* v, int64_t qk
                          void* out, int64_t out_stride, const int* cu, const int* slot, const int* reset, int S,
                          int T, int Hv, int Hk, int dk, int dv, float* ws, hipStream_t stream) {
   if (S <= 0) return 0;
-  if (dv <= 0 || dv > 128 || Hk <= 0 || Hv % Hk != 0) return -2;
+  if (dv <= 0 || Hk <= 0 || Hv % Hk != 0) return -2;
   static const int nc_env = getenv("OME_GDN_NC") ? atoi(getenv("OME_GDN_NC")) : 0;   // bench override
-  if (ws) {   // v3: prep (parallel over rows) + scan
-    if (dk != 128 && dk != 64) return -3;
+  if (ws) {   // v3: prep (parallel over rows) + scan; any dv (grid z tiles the state columns)
+    if (dk != 256 && dk != 128 && dk != 64) return -3;
     float* qn = ws;
     float* kn = qn + (int64_t)T * Hk * dk;
     float* qk = kn + (int64_t)T * Hk * dk;
     float* gb = qk + (int64_t)T * Hk;
     const int waves = T * Hk;
     if (waves > 0) {
-      if (dk == 128)
+      if (dk == 256)
+        gdn_prep_kernel<256><<<(waves + 3) / 4, 256, 0, stream>>>((const bf16*)q, (const bf16*)k, qkv_stride,
+                                                                  (const bf16*)a, (const bf16*)b, ab_stride, A_log,
+                                                                  dt_bias, qn, kn, qk, gb, T, Hk, Hv);
+      else if (dk == 128)
         gdn_prep_kernel<128><<<(waves + 3) / 4, 256, 0, stream>>>((const bf16*)q, (const bf16*)k, qkv_stride,
                                                                   (const bf16*)a, (const bf16*)b, ab_stride, A_log,
                                                                   dt_bias, qn, kn, qk, gb, T, Hk, Hv);
@@ -302,7 +308,11 @@ OME_API int ome_gdn_scan(const void* q, const void* k, const void* v, int64_t qk
 #define GDN3(DKV, NCV)                                                                                      \
   gdn_scan_v3_kernel<DKV, NCV><<<grid3, 256, 0, stream>>>(qn, kn, qk, gb, (const bf16*)v, qkv_stride, state, \
                                                            (bf16*)out, out_stride, cu, slot, reset, Hv, Hk, dv)
-    if (dk == 128) {
+    if (dk == 256) {
+      if (nc == 1) GDN3(256, 1);
+      else if (nc == 2) GDN3(256, 2);
+      else GDN3(256, 4);
+    } else if (dk == 128) {
       if (nc == 1) GDN3(128, 1);
       else if (nc == 2) GDN3(128, 2);
       else GDN3(128, 4);
@@ -315,6 +325,7 @@ OME_API int ome_gdn_scan(const void* q, const void* k, const void* v, int64_t qk
     OME_CHECK_LAUNCH();
     return 0;
   }
+  if (dv > 128) return -2;   // v1: one 128-thread workgroup per (sequence, head)
   dim3 grid(S, Hv);
 #define GDN_ARGS                                                                                                \
   (const bf16*)q, (const bf16*)k, (const bf16*)v, qkv_stride, (const bf16*)a, (const bf16*)b, ab_stride, A_log, \

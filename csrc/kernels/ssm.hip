@@ -3,6 +3,7 @@
 //
 //   ome_ssm_conv1d       : causal depthwise conv (kernel K <= 8) + SiLU over a varlen batch of
 //                          sequences, continuing from / updating each sequence's conv state
+//   ome_dyn_conv1d       : the same with per-row (input-generated) taps (Jet-Nemotron JetBlock)
 //   ome_ssm_scan         : the selective scan  h <- exp(dt*A) h + dt * B x,  y = C.h + D x
 //                          (dt = softplus(dt + dt_bias) clamped below), recurrent over the rows of
 //                          each sequence, state in fp32 per (slot, head, p, n)
@@ -55,6 +56,43 @@ __global__ __launch_bounds__(256) void ssm_conv1d_kernel(const bf16* __restrict_
     float acc = b + wt[K - 1] * v;
 #pragma unroll
     for (int j = 0; j < K - 1; ++j) acc += wt[j] * win[j];
+#pragma unroll
+    for (int j = 0; j < K - 2; ++j) win[j] = win[j + 1];
+    win[K - 2] = v;
+    out[(int64_t)r * out_stride + c] = (bf16)silu_f(acc);
+  }
+#pragma unroll
+  for (int j = 0; j < K - 1; ++j) st[j] = (bf16)win[j];
+}
+
+// Dynamic (input-conditioned) causal depthwise conv + SiLU (Jet-Nemotron's JetBlock value path):
+// every row r brings its own taps kern[r][(c / cpk) * K + j] (cpk channels share a kernel: 1 =
+// per-channel, head_v_dim = per-head), tap K-1 on the current row.  Same varlen / state contract
+// as ssm_conv1d_kernel.
+template <int K>
+__global__ __launch_bounds__(256) void dyn_conv1d_kernel(const bf16* __restrict__ x, int64_t x_stride,
+                                                         const bf16* __restrict__ kern, int64_t k_stride, int cpk,
+                                                         bf16* __restrict__ out, int64_t out_stride,
+                                                         bf16* __restrict__ state, const int* __restrict__ cu,
+                                                         const int* __restrict__ slot, const int* __restrict__ reset,
+                                                         int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int s = blockIdx.y;
+  if (c >= C) return;
+  const int r0 = cu[s], r1 = cu[s + 1];
+  if (r1 <= r0) return;
+  bf16* st = state + ((int64_t)slot[s] * C + c) * (K - 1);
+  float win[K - 1];
+  const bool fresh = reset[s] != 0;
+#pragma unroll
+  for (int j = 0; j < K - 1; ++j) win[j] = fresh ? 0.f : (float)st[j];
+  const int64_t kc = (int64_t)(c / cpk) * K;
+  for (int r = r0; r < r1; ++r) {
+    const float v = (float)x[(int64_t)r * x_stride + c];
+    const bf16* kr = kern + (int64_t)r * k_stride + kc;
+    float acc = (float)kr[K - 1] * v;
+#pragma unroll
+    for (int j = 0; j < K - 1; ++j) acc += (float)kr[j] * win[j];
 #pragma unroll
     for (int j = 0; j < K - 2; ++j) win[j] = win[j + 1];
     win[K - 2] = v;
@@ -190,6 +228,31 @@ OME_API int ome_ssm_conv1d(const void* x, int64_t x_stride, const void* w, const
       return -2;
   }
 #undef CONV_CASE
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+OME_API int ome_dyn_conv1d(const void* x, int64_t x_stride, const void* kern, int64_t k_stride, int cpk, void* out,
+                           int64_t out_stride, void* state, const int* cu, const int* slot, const int* reset, int S,
+                           int C, int K, hipStream_t stream) {
+  if (S <= 0 || C <= 0) return 0;
+  if (cpk <= 0 || C % cpk) return -3;
+  dim3 grid((C + 255) / 256, S);
+#define DCONV_CASE(KK)                                                                                         \
+  case KK:                                                                                                      \
+    dyn_conv1d_kernel<KK><<<grid, 256, 0, stream>>>((const bf16*)x, x_stride, (const bf16*)kern, k_stride, cpk, \
+                                                    (bf16*)out, out_stride, (bf16*)state, cu, slot, reset, C);   \
+    break;
+  switch (K) {
+    DCONV_CASE(2)
+    DCONV_CASE(3)
+    DCONV_CASE(4)
+    DCONV_CASE(5)
+    DCONV_CASE(6)
+    default:
+      return -2;
+  }
+#undef DCONV_CASE
   OME_CHECK_LAUNCH();
   return 0;
 }

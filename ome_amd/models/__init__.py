@@ -77,6 +77,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.nemotron_h import NemotronHForCausalLM
 
         return NemotronHForCausalLM
+    if cfg.architecture == "JetNemotronForCausalLM" or cfg.model_type == "jet_nemotron":
+        from ome_amd.models.jet_nemotron import JetNemotronForCausalLM
+
+        return JetNemotronForCausalLM
     if cfg.architecture == "Qwen3NextForCausalLM" or cfg.model_type == "qwen3_next":
         from ome_amd.models.qwen3_next import Qwen3NextForCausalLM
 
@@ -205,7 +209,7 @@ def supported(arch: str) -> bool:
         arch in DECODER_ARCHS or arch in ENCODER_ARCHS or arch == "MllamaForConditionalGeneration" or \
         arch == "DeciLMForCausalLM" or arch in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM") or \
         arch == "LlavaNextForConditionalGeneration" or \
-        arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or \
+        arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or arch == "JetNemotronForCausalLM" or \
         arch == "Mistral3ForConditionalGeneration" or arch == "MiniCPM3ForCausalLM" or \
         arch in ("InternVLChatModel", "InternVLForConditionalGeneration") or \
         arch in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM") or \

@@ -475,6 +475,23 @@ PRESETS: dict[str, dict] = {
                                 n_routed_experts=16, num_experts_per_tok=4, moe_intermediate_size=128,
                                 moe_shared_expert_intermediate_size=256, n_group=4, topk_group=2,
                                 routed_scaling_factor=2.5, norm_topk_prob=True),
+    # Jet-Nemotron-2B shape (Qwen2.5-1.5B backbone, 28 layers: JetBlocks + full attention at 15 / 20 and
+    # sliding window at 21 / 22; JetBlock shape as published -- the remote config is not available offline)
+    "jet-nemotron-2b": dict(architectures=["JetNemotronForCausalLM"], model_type="jet_nemotron", hidden_size=1536,
+                            num_hidden_layers=28, num_attention_heads=12, num_key_value_heads=2,
+                            intermediate_size=8960, vocab_size=151936, rms_norm_eps=1e-6, rope_theta=1000000.0,
+                            max_position_embeddings=65536, tie_word_embeddings=True,
+                            efficient_attention_config={"jet": dict(num_heads=6, head_dim=256, expand_v=2.0,
+                                                                    conv_size=4, dconv_generator_reduction=8,
+                                                                    norm_eps=1e-6),
+                                                        "swa": {"window_size": 1152}}),
+    "tiny-jet-nemotron": dict(architectures=["JetNemotronForCausalLM"], model_type="jet_nemotron", hidden_size=256,
+                              num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2,
+                              intermediate_size=512, vocab_size=1024, rms_norm_eps=1e-6, rope_theta=10000.0,
+                              max_position_embeddings=4096, layer_types=["jet", "attn", "jet", "swa"],
+                              efficient_attention_config={"jet": dict(num_heads=2, head_dim=128, expand_v=2.0,
+                                                                      conv_size=4, dconv_generator_reduction=8),
+                                                          "swa": {"window_size": 64}}),
     # Qwen3-Next-80B-A3B shape (48 layers: 3 Gated-DeltaNet + 1 gated attention, 512 experts top-10)
     "qwen3-next-80b-a3b": dict(architectures=["Qwen3NextForCausalLM"], model_type="qwen3_next", hidden_size=2048,
                                num_hidden_layers=48, num_attention_heads=16, num_key_value_heads=2, head_dim=256,

@@ -99,6 +99,24 @@ def ssm_conv1d(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, stat
     return out
 
 
+def dyn_conv1d(x: torch.Tensor, kern: torch.Tensor, state: torch.Tensor, cu, slot, reset, cpk: int = 1,
+               out: torch.Tensor | None = None) -> torch.Tensor:
+    """Causal depthwise conv + SiLU with per-row taps (Jet-Nemotron's dynamic convolution):
+    x [T, C], kern [T, (C / cpk) * K] (row r's taps; ``cpk`` channels share one kernel), state
+    [slots, C, K-1] continued / updated per sequence as in :func:`ssm_conv1d`."""
+    T, C = x.shape
+    K = state.shape[-1] + 1
+    out = torch.empty(T, C, dtype=x.dtype, device=x.device) if out is None else out
+    if not _gpu(x):
+        return ref.dyn_conv1d(x, kern, state, cu, slot, reset, cpk, out)
+    assert x.stride(1) == 1 and out.stride(1) == 1 and kern.stride(1) == 1 and state.is_contiguous()
+    assert kern.shape[1] == (C // cpk) * K and C % cpk == 0
+    call("ome_dyn_conv1d", x.data_ptr(), x.stride(0), kern.data_ptr(), kern.stride(0), cpk, out.data_ptr(),
+         out.stride(0), state.data_ptr(), _i32(cu).data_ptr(), _i32(slot).data_ptr(), _i32(reset).data_ptr(),
+         slot.shape[0], C, K, stream_ptr())
+    return out
+
+
 def ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min: float, state, cu, slot, reset, H: int, P: int, N: int, G: int,
              out: torch.Tensor | None = None) -> torch.Tensor:
     """Mamba-2 selective scan, recurrent over each sequence's rows: x [T, H*P], dt [T, H], B/C

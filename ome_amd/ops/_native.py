@@ -36,6 +36,7 @@ _SIGNATURES = {
         "ome_act_and_mul": [vp, vp, i64, i32, i32, vp],
         "ome_act": [vp, i64, i32, vp],
         "ome_ssm_conv1d": [vp, i64, vp, vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp],
+        "ome_dyn_conv1d": [vp, i64, vp, i64, i32, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp],
         "ome_ssm_scan": [vp, i64, vp, i64, vp, vp, i64, vp, vp, vp, f32, vp, vp, i64, vp, vp, vp, i32, i32, i32,
                          i32, i32, vp],
         "ome_gdn_scan": [vp, vp, vp, i64, vp, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32,

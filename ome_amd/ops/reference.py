@@ -70,6 +70,24 @@ def ssm_conv1d(x, w, bias, state, cu, slot, reset, out):
     return out
 
 
+def dyn_conv1d(x, kern, state, cu, slot, reset, cpk, out):
+    """Per-row-tap causal depthwise conv + SiLU; tap K-1 multiplies the current row."""
+    C = x.shape[1]
+    K = state.shape[-1] + 1
+    for s in range(len(slot)):
+        r0, r1 = int(cu[s]), int(cu[s + 1])
+        if r1 <= r0:
+            continue
+        st = state[int(slot[s])]
+        prev = torch.zeros_like(st) if int(reset[s]) else st
+        seq = torch.cat([prev.float().t(), x[r0:r1].float()], 0)          # [K-1+L, C]
+        taps = kern[r0:r1].float().view(r1 - r0, C // cpk, 1, K).expand(-1, -1, cpk, -1).reshape(r1 - r0, C, K)
+        win = seq.unfold(0, K, 1)                                         # [L, C, K]
+        out[r0:r1] = torch.nn.functional.silu((win * taps).sum(-1)).to(out.dtype)
+        st.copy_(seq[-(K - 1):].t().to(st.dtype))
+    return out
+
+
 def ssm_scan(x, dt, B, C, A, D, dt_bias, dt_min, state, cu, slot, reset, H, P, N, G, out):
     """Selective scan (Mamba-2), recurrent per sequence; ``state`` [slots, H, P, N] fp32."""
     rep = H // G
