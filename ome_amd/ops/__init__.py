@@ -1209,7 +1209,7 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     if isinstance(items, PrefillPlan):
         plan, items = items, items.items
         rows = plan.rows
-        if rows != 32 and prefill_rows(Hq, Hkv, D, P) != rows:
+        if rows != 32 and not (rows == 64 and D == 128 and P == 16 and Hq == 4 * Hkv):
             raise ValueError(f"paged_prefill: {rows}-row items need the GQA-4 / D=128 kernel, got Hq={Hq} "
                              f"Hkv={Hkv} D={D} page={P} (build the plan with prefill_rows of this layer)")
         if (plan.parts and D == 128 and P == 16 and Hq == 4 * Hkv and row_hi is None and

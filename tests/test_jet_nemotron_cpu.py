@@ -17,8 +17,8 @@ from ome_amd.runtime.engine import Engine, EngineArgs
 from ome_amd.runtime.request import SamplingParams
 
 JET = dict(num_heads=2, head_dim=64, expand_v=1.5, conv_size=4, dconv_generator_reduction=4, norm_eps=1e-5)
-CFG = dict(architectures=["JetNemotronForCausalLM"], model_type="jet_nemotron", vocab_size=256, hidden_size=64,
-           intermediate_size=96, num_hidden_layers=4, num_attention_heads=4, num_key_value_heads=2,
+CFG = dict(architectures=["JetNemotronForCausalLM"], model_type="jet_nemotron", vocab_size=256, hidden_size=128,
+           intermediate_size=96, num_hidden_layers=4, num_attention_heads=2, num_key_value_heads=1,
            rms_norm_eps=1e-6, rope_theta=10000.0, max_position_embeddings=512, tie_word_embeddings=False,
            layer_types=["jet", "attn", "jet", "swa"],
            efficient_attention_config={"jet": JET, "swa": {"window_size": 8}}, bos_token_id=1, eos_token_id=2)
