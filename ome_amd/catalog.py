@@ -73,6 +73,8 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
     Family("mimo-vl-7b-rl", "xiaomimimo", "XiaomiMiMo/MiMo-VL-7B-RL", "Qwen2_5_VLForConditionalGeneration", 8.3,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
+    Family("nvila-8b", "Efficient-Large-Model", "Efficient-Large-Model/NVILA-8B", "LlavaLlamaModel", 8.0, "nvila-8b",
+           capabilities=["IMAGE_TEXT_TO_TEXT", "VIDEO_TEXT_TO_TEXT"]),
     Family("jet-nemotron-2b", "jet-ai", "jet-ai/Jet-Nemotron-2B", "JetNemotronForCausalLM", 2.0, "jet-nemotron-2b"),
     Family("qwen3-next-80b-a3b-instruct", "qwen", "Qwen/Qwen3-Next-80B-A3B-Instruct", "Qwen3NextForCausalLM", 81.3,
            "qwen3-next-80b-a3b", args=['--tool-call-parser', 'hermes']),

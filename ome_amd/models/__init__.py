@@ -121,6 +121,10 @@ def model_class(cfg: ModelConfig):
         from ome_amd.models.bailing import BailingMoeForCausalLM
 
         return BailingMoeForCausalLM
+    if cfg.architecture == "LlavaLlamaModel":
+        from ome_amd.models.nvila import NVILAForCausalLM
+
+        return NVILAForCausalLM
     if cfg.architecture in ("LlavaQwenForCausalLM", "LlavaOnevisionForConditionalGeneration"):
         from ome_amd.models.llava_onevision import LlavaOnevisionForConditionalGeneration
 
@@ -210,6 +214,7 @@ def supported(arch: str) -> bool:
         arch == "DeciLMForCausalLM" or arch in ("LlavaForConditionalGeneration", "LlavaLlamaForCausalLM") or \
         arch == "LlavaNextForConditionalGeneration" or \
         arch == "CLIPModel" or arch == "Qwen3NextForCausalLM" or arch == "JetNemotronForCausalLM" or \
+        arch == "LlavaLlamaModel" or \
         arch == "Mistral3ForConditionalGeneration" or arch == "MiniCPM3ForCausalLM" or \
         arch in ("InternVLChatModel", "InternVLForConditionalGeneration") or \
         arch in ("JanusForConditionalGeneration", "MultiModalityCausalLM", "JanusMultiModalityCausalLM") or \
@@ -232,7 +237,9 @@ def build_model(cfg: ModelConfig, device, dtype=torch.bfloat16, max_positions: i
     m = cls(cfg, device=device, dtype=dtype, max_positions=max_positions)
     fmt = load_format
     if fmt == "auto":
-        fmt = "safetensors" if model_path and any(Path(model_path).glob("*.safetensors")) else "dummy"
+        from ome_amd.models.loader import has_checkpoint
+
+        fmt = "safetensors" if model_path and has_checkpoint(model_path) else "dummy"
     if fmt == "dummy":
         m.init_random(seed)
     elif fmt == "safetensors":

@@ -28,7 +28,10 @@ PADDED_HEAD_ARCHS = {"Phi3SmallForCausalLM", "OPTForCausalLM", "GPTJForCausalLM"
                      "ChatGLMForConditionalGeneration", "OlmoeForCausalLM", "GraniteMoeForCausalLM", "DbrxForCausalLM",
                      "Ernie4_5_MoeForCausalLM", "MiniMaxM2ForCausalLM"}
 # remote-code class names that end in "Model" but are causal LMs (not embedding models)
-CAUSAL_MODEL_CLASSES = {"ChatGLMModel", "QWenLMHeadModel", "TeleFLMModel", "InternVLChatModel"}
+CAUSAL_MODEL_CLASSES = {"ChatGLMModel", "QWenLMHeadModel", "TeleFLMModel", "InternVLChatModel", "LlavaLlamaModel"}
+#: VILA / NVILA checkpoints: one sub-directory (own config.json + safetensors) per component;
+#: tensors are read with the directory name as a prefix (``llm.model.layers.0...``)
+NESTED_COMPONENTS = ("llm", "vision_tower", "mm_projector")
 
 
 def _standard_keys(c: dict[str, Any]) -> dict[str, Any]:
@@ -223,9 +226,12 @@ class ModelConfig:
 
     @classmethod
     def from_hf(cls, cfg: dict[str, Any]) -> "ModelConfig":
-        if cfg.get("text_config") or cfg.get("llm_config") or cfg.get("language_config"):
-            # llm_config: InternVLChatModel; language_config: Janus / DeepSeek-VL2 originals
-            text = _standard_keys(cfg.get("text_config") or cfg.get("llm_config") or cfg["language_config"])
+        llm_cfg = cfg.get("llm_cfg") if isinstance(cfg.get("llm_cfg"), dict) else None
+        if cfg.get("text_config") or cfg.get("llm_config") or cfg.get("language_config") or llm_cfg:
+            # llm_config: InternVLChatModel; language_config: Janus / DeepSeek-VL2 originals;
+            # llm_cfg: VILA / NVILA (LlavaLlamaModel)
+            text = _standard_keys(cfg.get("text_config") or cfg.get("llm_config") or cfg.get("language_config")
+                                  or llm_cfg)
         else:  # flat configs: keep the original keys (extra) next to the standard aliases
             cfg = text = _standard_keys(cfg)
         arch = (cfg.get("architectures") or ["LlamaForCausalLM"])[0]
@@ -318,7 +324,12 @@ class ModelConfig:
         p = Path(path)
         if p.is_dir():
             p = p / "config.json"
-        return cls.from_hf(json.loads(p.read_text()))
+        cfg = json.loads(p.read_text())
+        for comp in NESTED_COMPONENTS:   # VILA layout: component configs in sub-directories
+            sub = p.parent / comp / "config.json"
+            if not isinstance(cfg.get(comp + "_cfg"), dict) and sub.exists():
+                cfg[comp + "_cfg"] = json.loads(sub.read_text())
+        return cls.from_hf(cfg)
 
     def shrink(self, num_layers: int | None = None, **kw) -> "ModelConfig":
         import dataclasses
@@ -475,6 +486,27 @@ PRESETS: dict[str, dict] = {
                                 n_routed_experts=16, num_experts_per_tok=4, moe_intermediate_size=128,
                                 moe_shared_expert_intermediate_size=256, n_group=4, topk_group=2,
                                 routed_scaling_factor=2.5, norm_topk_prob=True),
+    # NVILA-8B shape (VILA LlavaLlamaModel: Qwen2-7B LM, SigLIP-SO400M 448 px tower, Dynamic-S2 scales
+    # 448 / 896 / 1344, mlp_downsample_3x3_fix projector)
+    "nvila-8b": dict(architectures=["LlavaLlamaModel"], model_type="llava_llama",
+                     llm_cfg=dict(architectures=["Qwen2ForCausalLM"], model_type="qwen2", hidden_size=3584,
+                                  intermediate_size=18944, num_hidden_layers=28, num_attention_heads=28,
+                                  num_key_value_heads=4, vocab_size=151648, rms_norm_eps=1e-6,
+                                  rope_theta=1000000.0, max_position_embeddings=32768),
+                     vision_tower_cfg=dict(hidden_size=1152, intermediate_size=4304, num_hidden_layers=27,
+                                           num_attention_heads=16, image_size=448, patch_size=14),
+                     mm_projector_cfg=dict(mm_projector_type="mlp_downsample_3x3_fix"), mm_vision_select_layer=-2,
+                     image_aspect_ratio="dynamic_s2", s2_scales="448,896,1344", s2_max_split_size=448,
+                     image_token_id=151649),
+    "tiny-nvila": dict(architectures=["LlavaLlamaModel"], model_type="llava_llama",
+                       llm_cfg=dict(model_type="qwen2", hidden_size=256, intermediate_size=512, num_hidden_layers=2,
+                                    num_attention_heads=4, num_key_value_heads=2, vocab_size=1024,
+                                    max_position_embeddings=4096),
+                       vision_tower_cfg=dict(hidden_size=64, intermediate_size=128, num_hidden_layers=2,
+                                             num_attention_heads=4, image_size=84, patch_size=14),
+                       mm_projector_cfg=dict(mm_projector_type="mlp_downsample_3x3_fix"),
+                       image_aspect_ratio="dynamic_s2", s2_scales="84,168,252", s2_max_split_size=84,
+                       image_token_id=1000),
     # Jet-Nemotron-2B shape (Qwen2.5-1.5B backbone, 28 layers: JetBlocks + full attention at 15 / 20 and
     # sliding window at 21 / 22; JetBlock shape as published -- the remote config is not available offline)
     "jet-nemotron-2b": dict(architectures=["JetNemotronForCausalLM"], model_type="jet_nemotron", hidden_size=1536,

@@ -23,9 +23,32 @@ def shard_files(model_path: str | Path) -> list[Path]:
     return sorted(p.glob("*.safetensors"))
 
 
+def nested_components(model_path: str | Path) -> list[str]:
+    """VILA / NVILA layout: component sub-directories holding safetensors (none at the top)."""
+    from ome_amd.models.config import NESTED_COMPONENTS
+
+    p = Path(model_path)
+    if shard_files(p):
+        return []
+    return [c for c in NESTED_COMPONENTS if shard_files(p / c)]
+
+
+def has_checkpoint(model_path: str | Path) -> bool:
+    return bool(shard_files(model_path)) or bool(nested_components(model_path))
+
+
 def iter_safetensors(model_path: str | Path, device="cpu", plan=None) -> Iterator[tuple[str, torch.Tensor]]:
     """``plan(name, shape) -> None | ("rows"|"cols", start, n)``: read only this tensor-parallel
-    rank's shard of each tensor (``LlamaForCausalLM.shard_plan``); None = whole tensors."""
+    rank's shard of each tensor (``LlamaForCausalLM.shard_plan``); None = whole tensors.
+    Component sub-directories (``nested_components``) are read in turn, names prefixed with the
+    directory (``llm.``, ``vision_tower.``, ``mm_projector.``)."""
+    comps = nested_components(model_path)
+    if comps:
+        for c in comps:
+            sub = None if plan is None else (lambda name, shape, c=c: plan(f"{c}.{name}", shape))
+            for name, t in iter_safetensors(Path(model_path) / c, device, sub):
+                yield f"{c}.{name}", t
+        return
     files = shard_files(model_path)
     if not files:
         raise FileNotFoundError(f"no safetensors shards under {model_path}")
