@@ -229,3 +229,88 @@ OME_API int ome_layernorm(void* x, int64_t x_stride, void* res, int64_t res_stri
   OME_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Per-head RMSNorm + complex-pair RoPE + row scatter (Qwen-Image MMDiT q / k; v with no norm and
+// no rotation): one wave per (row, head).  x row r, head h = x[r * xs + h * HD .. +HD); w [HD] (null:
+// no norm); cs [T][HD/2][2] fp32 (cos, sin) (null: no rotation); the result goes to row
+// dst[r] (null: r) of out (row stride os) -- the joint [text; image] sequence is assembled by
+// the writes themselves, no gather pass.  Rounding as the eager path: normed value rounded to
+// bf16 before the fp32 rotation.
+template <int HD>
+__global__ __launch_bounds__(256) void qk_norm_rope_kernel(const bf16* __restrict__ x, int64_t xs,
+                                                           const bf16* __restrict__ w, const float* __restrict__ cs,
+                                                           int T, int H, float eps, bf16* __restrict__ out,
+                                                           int64_t os, const int* __restrict__ dst) {
+  constexpr int NP = HD / 2, PPL = (NP + 63) / 64;   // complex pairs, pairs per lane
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= (int64_t)T * H) return;   // whole wave
+  const int r = (int)(wid / H), h = (int)(wid - (int64_t)r * H);
+  const bf16* xp = x + (int64_t)r * xs + (int64_t)h * HD;
+  float v0[PPL], v1[PPL], ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int p = lane + 64 * j;
+    v0[j] = v1[j] = 0.f;
+    if (p < NP) {
+      const bf16x2 t = *reinterpret_cast<const bf16x2*>(xp + 2 * p);
+      v0[j] = (float)t[0];
+      v1[j] = (float)t[1];
+      ss += v0[j] * v0[j] + v1[j] * v1[j];
+    }
+  }
+  if (w != nullptr) {
+    const float inv = rsqrtf(wave_sum(ss) / HD + eps);
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int p = lane + 64 * j;
+      if (p < NP) {
+        v0[j] = (float)(bf16)((float)(bf16)(v0[j] * inv) * (float)w[2 * p]);
+        v1[j] = (float)(bf16)((float)(bf16)(v1[j] * inv) * (float)w[2 * p + 1]);
+      }
+    }
+  }
+  bf16* op = out + (int64_t)(dst != nullptr ? dst[r] : r) * os + (int64_t)h * HD;
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int p = lane + 64 * j;
+    if (p >= NP) continue;
+    float a = v0[j], b = v1[j];
+    if (cs != nullptr) {
+      const float2 c = *reinterpret_cast<const float2*>(cs + ((int64_t)r * NP + p) * 2);
+      a = v0[j] * c.x - v1[j] * c.y;
+      b = v0[j] * c.y + v1[j] * c.x;
+    }
+    bf16x2 o;
+    o[0] = (bf16)a;
+    o[1] = (bf16)b;
+    *reinterpret_cast<bf16x2*>(op + 2 * p) = o;
+  }
+}
+
+OME_API int ome_qk_norm_rope(const void* x, int64_t xs, const void* w, const float* cs, int T, int H, int hd,
+                             float eps, void* out, int64_t os, const int* dst, hipStream_t stream) {
+  if (T <= 0 || H <= 0) return 0;
+  if ((xs | os) & 1) return -3;
+  const int64_t waves = (int64_t)T * H;
+  dim3 grid((unsigned)((waves + 3) / 4));
+  switch (hd) {
+    case 64:
+      qk_norm_rope_kernel<64><<<grid, 256, 0, stream>>>((const bf16*)x, xs, (const bf16*)w, cs, T, H, eps, (bf16*)out,
+                                                        os, dst);
+      break;
+    case 128:
+      qk_norm_rope_kernel<128><<<grid, 256, 0, stream>>>((const bf16*)x, xs, (const bf16*)w, cs, T, H, eps,
+                                                         (bf16*)out, os, dst);
+      break;
+    case 256:
+      qk_norm_rope_kernel<256><<<grid, 256, 0, stream>>>((const bf16*)x, xs, (const bf16*)w, cs, T, H, eps,
+                                                         (bf16*)out, os, dst);
+      break;
+    default:
+      return -2;
+  }
+  OME_CHECK_LAUNCH();
+  return 0;
+}

@@ -34,8 +34,9 @@ __device__ __forceinline__ int va_slot(int kk) { return 8 * ((kk & 15) >> 2) + (
 template <int DP>
 __global__ __launch_bounds__(256) void varlen_attn_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k, int64_t k_stride,
-    const bf16* __restrict__ v, int64_t v_stride, const int* __restrict__ cu, const int2* __restrict__ items,
-    bf16* __restrict__ out, int64_t o_stride, int Hq, int Hkv, int D, float scale_log2, int causal) {
+    const bf16* __restrict__ v, int64_t v_stride, const int* __restrict__ cu, const int* __restrict__ cuk,
+    const int2* __restrict__ items, bf16* __restrict__ out, int64_t o_stride, int Hq, int Hkv, int D,
+    float scale_log2, int causal) {
   constexpr int KS = DP / 32, NB = DP / 16, KLD = DP + 8, VLD = 32 + 8, CPR = DP / 8;
   constexpr int KCH = 32 * CPR;                       // 16-B K chunks per 32-key subtile
   constexpr int NCH = (KCH + 255) / 256;              // K chunks per thread per subtile
@@ -51,10 +52,12 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
   const int s = it.x, r0_item = it.y;
   const int head = blockIdx.y, kvh = head / (Hq / Hkv);
   const int t0 = cu[s], L = cu[s + 1] - t0;
+  // cross attention (cuk != null): sequence s's keys are rows cuk[s] .. cuk[s+1] of k / v
+  const int tk0 = cuk != nullptr ? cuk[s] : t0, Lk = cuk != nullptr ? cuk[s + 1] - tk0 : L;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int n = lane & 15, g = lane >> 4;
   const int r0 = r0_item + 32 * wave;
-  const int kv_end = causal ? min(L, r0_item + 128) : L;
+  const int kv_end = causal ? min(Lk, r0_item + 128) : Lk;
 
   // ---- this wave's query fragments (rows r0..r0+31), zero past L and past D ----
   bf16x8 qf[2][KS];
@@ -86,8 +89,8 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
       for (int i = 0; i < NCH; ++i) {
         const int c = tid + 256 * i;
         const int key = c / CPR, d0 = (c % CPR) * 8;
-        const bool ok = c < KCH && kb + key < L && d0 < D;
-        rk[u][i] = ok ? ld8(k + (int64_t)(t0 + kb + key) * k_stride + (int64_t)kvh * D + d0) : bf16x8{};
+        const bool ok = c < KCH && kb + key < Lk && d0 < D;
+        rk[u][i] = ok ? ld8(k + (int64_t)(tk0 + kb + key) * k_stride + (int64_t)kvh * D + d0) : bf16x8{};
       }
 #pragma unroll
       for (int i = 0; i < NVG; ++i) {
@@ -96,8 +99,8 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int key = 4 * kq + j;
-          const bool ok = c < VG && kb + key < L && d0 < D;
-          rv[u][i][j] = ok ? ld8(v + (int64_t)(t0 + kb + key) * v_stride + (int64_t)kvh * D + d0) : bf16x8{};
+          const bool ok = c < VG && kb + key < Lk && d0 < D;
+          rv[u][i][j] = ok ? ld8(v + (int64_t)(tk0 + kb + key) * v_stride + (int64_t)kvh * D + d0) : bf16x8{};
         }
       }
     }
@@ -157,7 +160,7 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
           sc[rb][1] = va_mfma(a1, qf[rb][ks], sc[rb][1]);
         }
       }
-      const bool need_mask = kb + 32 > L || (causal && kb + 32 > r0 + 1);
+      const bool need_mask = kb + 32 > Lk || (causal && kb + 32 > r0 + 1);
       bf16x8 pb[2];
       float alpha[2];
 #pragma unroll
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
             float val = sc[rb][X][i] * scale_log2;
             if (need_mask) {
               const int key = kb + 16 * X + 4 * g + i;
-              const bool ok = key < L && (!causal || key <= qpos);
+              const bool ok = key < Lk && (!causal || key <= qpos);
               val = ok ? val : VA_NEG_INF;
             }
             sc[rb][X][i] = val;
@@ -233,13 +236,16 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
 }  // namespace
 
 // items: int2 (sequence, first row) per 128-row work item, n_items of them (host-built).
+// cuk: null (self attention: keys are the query rows) or the key row ranges of each sequence
+// (cross attention: queries cu[s] .. cu[s+1] attend to keys cuk[s] .. cuk[s+1]; not causal).
 // Strides are in elements per token; head h of a token starts at h * D.  D % 8 == 0, D <= 128;
 // every pointer and stride 16-B aligned.
 OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k, int64_t k_stride, const void* v,
-                                 int64_t v_stride, const int* cu, const int* items, int n_items, void* out,
-                                 int64_t o_stride, int Hq, int Hkv, int D, float scale, int causal,
+                                 int64_t v_stride, const int* cu, const int* cuk, const int* items, int n_items,
+                                 void* out, int64_t o_stride, int Hq, int Hkv, int D, float scale, int causal,
                                  hipStream_t stream) {
   if (n_items <= 0) return 0;
+  if (cuk != nullptr && causal) return -6;   // cross attention is bidirectional
   if (D <= 0 || D > 128 || D % 8 != 0) return -2;
   if (Hkv <= 0 || Hq % Hkv != 0) return -3;
   if ((q_stride | k_stride | v_stride | o_stride) % 8 != 0) return -4;
@@ -247,7 +253,7 @@ OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k,
   const float sl2 = scale * 1.4426950408889634f;
   dim3 grid(n_items, Hq);
 #define ARGS                                                                                                  \
-  (const bf16*)q, q_stride, (const bf16*)k, k_stride, (const bf16*)v, v_stride, cu, (const int2*)items,       \
+  (const bf16*)q, q_stride, (const bf16*)k, k_stride, (const bf16*)v, v_stride, cu, cuk, (const int2*)items,  \
       (bf16*)out, o_stride, Hq, Hkv, D, sl2, causal
   if (D <= 64) varlen_attn_kernel<64><<<grid, 256, 0, stream>>>(ARGS);
   else if (D <= 96) varlen_attn_kernel<96><<<grid, 256, 0, stream>>>(ARGS);

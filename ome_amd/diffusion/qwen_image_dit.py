@@ -6,12 +6,16 @@ Reference catalog: ``config/runtimes/srt/Qwen/Qwen-Image-rt.yaml:15`` (``QwenIma
 
 Per block, for the image stream (packed 2x2 latent patches) and the text stream (Qwen2.5-VL
 hidden states) separately: AdaLN modulation from the timestep embedding (SiLU -> GEMM -> shift /
-scale / gate x 2), affine-free LayerNorm, q / k / v GEMMs, per-head RMSNorm on q / k, 3-axis
-complex RoPE (frame, height, width; centred for images, text after the largest image index);
-then ONE joint attention over [text; image] of each sample -- the classifier-free-guidance pair
-(prompt, negative prompt) rides in the same launch as two packed varlen sequences
-(``ops.varlen_attention``: bidirectional MFMA flash attention, no padding) -- out projections,
-gated residuals, and the GELU-tanh MLPs.  Weights keep the diffusers names.
+scale / gate x 2) applied as the affine of the LayerNorm kernel itself (weight 1 + scale, bias
+shift: one launch per sample), ONE fused q|k|v GEMM per stream (the three diffusers projections
+concatenated at load), then ``ome_qk_norm_rope``: per-head RMSNorm + 3-axis complex RoPE (frame,
+height, width; centred for images, text after the largest image index) written straight into the
+joint [text; image] sequence of each sample (v copied there by the same kernel) -- no per-block
+gathers; ONE joint attention over all samples -- the classifier-free-guidance pair (prompt,
+negative prompt) rides in the same launch as two packed varlen sequences
+(``ops.varlen_attention``: bidirectional MFMA flash attention, no padding) -- out projections on
+row gathers of the attention output, gated residuals (in-place addcmul per sample), and the
+GELU-tanh MLPs.  Weights keep the diffusers names (q / k / v fused at load).
 """
 from __future__ import annotations
 
@@ -40,8 +44,6 @@ class QwenImageDiT:
             raise ValueError(f"axes_dims_rope {self.axes} must sum to the head dim {self.hd}")
         self.eps = 1e-6
         self.w: dict[str, torch.Tensor] = {}
-        self._ones = torch.ones(self.D, dtype=dtype, device=self.device)
-        self._zeros = torch.zeros(self.D, dtype=dtype, device=self.device)
         self._freq_cache: dict = {}
 
     # ------------------------------------------------------------------ weights
@@ -79,7 +81,32 @@ class QwenImageDiT:
             else:
                 t.normal_(0.0, std, generator=g)
             self.w[k] = t
+        self._fuse()
         return self
+
+    _QKV = {"img": ("to_q", "to_k", "to_v"), "txt": ("add_q_proj", "add_k_proj", "add_v_proj")}
+
+    def _fuse(self) -> None:
+        """[q; k; v] of each stream -> one GEMM weight (the three originals are dropped)."""
+        for i in range(self.L):
+            p = f"transformer_blocks.{i}.attn."
+            for st, names in self._QKV.items():
+                if p + names[0] + ".weight" not in self.w:
+                    continue
+                for kind in ("weight", "bias"):
+                    self.w[p + f"{st}_qkv.{kind}"] = torch.cat([self.w.pop(p + f"{n}.{kind}") for n in names], 0)
+
+    def state_dict(self) -> dict[str, torch.Tensor]:
+        """Weights under their diffusers names (fused q|k|v split back into views)."""
+        out = {}
+        for k, t in self.w.items():
+            if k.endswith(("img_qkv.weight", "img_qkv.bias", "txt_qkv.weight", "txt_qkv.bias")):
+                pre, st, kind = k[:k.rindex(".", 0, k.rindex("."))], k.split(".")[-2][:3], k.split(".")[-1]
+                for n, part in zip(self._QKV[st], t.chunk(3, 0)):
+                    out[f"{pre}.{n}.{kind}"] = part
+            else:
+                out[k] = t
+        return out
 
     def load(self, weights) -> "QwenImageDiT":
         want = self.shapes()
@@ -91,6 +118,7 @@ class QwenImageDiT:
         missing = [k for k in want if k not in self.w]
         if missing:
             raise ValueError(f"transformer checkpoint incomplete: {missing[:4]}")
+        self._fuse()
         return self
 
     def weight_bytes(self) -> int:
@@ -135,26 +163,25 @@ class QwenImageDiT:
         self._freq_cache[key] = got
         return got
 
-    @staticmethod
-    def _rope(x: torch.Tensor, ang: torch.Tensor) -> torch.Tensor:
-        """x [T, H, hd] with (even, odd) pairs as complex numbers, rotated by ang [T, hd/2]."""
-        xf = x.float().view(*x.shape[:-1], -1, 2)
-        c, s = ang.cos()[:, None, :], ang.sin()[:, None, :]
-        re, im = xf[..., 0], xf[..., 1]
-        return torch.stack([re * c - im * s, re * s + im * c], -1).flatten(-2).to(x.dtype)
-
     # ------------------------------------------------------------------ forward
     def _mod_norm(self, x: torch.Tensor, shift: torch.Tensor, scale: torch.Tensor, rows: list[int]) -> torch.Tensor:
-        """affine-free LayerNorm, then x * (1 + scale_b) + shift_b per sample (rows per sample)."""
-        h = ops.layernorm(x.contiguous(), self._ones, self._zeros, self.eps)
-        if len(rows) == 1:
-            return h * (1 + scale[0]) + shift[0]
-        sc = torch.repeat_interleave(1 + scale, torch.tensor(rows, device=x.device), 0)
-        sh = torch.repeat_interleave(shift, torch.tensor(rows, device=x.device), 0)
-        return h * sc + sh
+        """LayerNorm(x) * (1 + scale_b) + shift_b per sample: the modulation IS the LayerNorm's affine
+        (weight 1 + scale_b, bias shift_b), one launch per sample's rows."""
+        out = torch.empty_like(x)
+        r0 = 0
+        for bb, n in enumerate(rows):
+            ops.layernorm(x[r0:r0 + n], (1 + scale[bb]).contiguous(), shift[bb].contiguous(), self.eps,
+                          out=out[r0:r0 + n])
+            r0 += n
+        return out
 
-    def _gate(self, g: torch.Tensor, rows: list[int]) -> torch.Tensor:
-        return g[0] if len(rows) == 1 else torch.repeat_interleave(g, torch.tensor(rows, device=g.device), 0)
+    @staticmethod
+    def _gated_add(x: torch.Tensor, g: torch.Tensor, y: torch.Tensor, rows: list[int]) -> None:
+        """x += g_b * y over each sample's rows (in place)."""
+        r0 = 0
+        for bb, n in enumerate(rows):
+            x[r0:r0 + n].addcmul_(y[r0:r0 + n], g[bb])
+            r0 += n
 
     def forward(self, img: torch.Tensor, txt: list[torch.Tensor], t: torch.Tensor,
                 img_shapes: list[tuple[int, int, int]]) -> torch.Tensor:
@@ -171,54 +198,44 @@ class QwenImageDiT:
         temb_act = ops.act(temb.clone(), 0)    # SiLU(temb), shared by every modulation GEMM
         img_ang, txt_ang_full = self.rope_angles(img_shapes, max(lt))
         txt_ang = torch.cat([txt_ang_full[:n] for n in lt], 0)
-        img_ang_b = img_ang.repeat(B, 1)
+        # (cos, sin) tables once per forward, fp32 [rows, hd/2, 2]
+        cs_img = torch.stack([img_ang.cos(), img_ang.sin()], -1).repeat(B, 1, 1).contiguous()
+        cs_txt = torch.stack([txt_ang.cos(), txt_ang.sin()], -1).contiguous()
         lens = [n + N for n in lt]
         nr, tr = [N] * B, lt
-        toff = [0]
-        for n in lt:
-            toff.append(toff[-1] + n)
+        total = sum(lens)
+        # joint packed sequence per sample = [text_b; image_b]: destination rows of both streams
+        starts = [sum(lens[:bb]) for bb in range(B)]
+        dst_img = torch.cat([torch.arange(st + lt[bb], st + lens[bb]) for bb, st in enumerate(starts)])
+        dst_txt = torch.cat([torch.arange(st, st + lt[bb]) for bb, st in enumerate(starts)])
+        dst_img, dst_txt = dst_img.to(self.device), dst_txt.to(self.device)
+        di32, dt32 = dst_img.to(torch.int32), dst_txt.to(torch.int32)
         for i in range(self.L):
             p = f"transformer_blocks.{i}."
+            a = p + "attn."
             im = linear(temb_act, w[p + "img_mod.1.weight"], w[p + "img_mod.1.bias"]).view(B, 6, D)
             tm = linear(temb_act, w[p + "txt_mod.1.weight"], w[p + "txt_mod.1.bias"]).view(B, 6, D)
-            xi = self._mod_norm(x, im[:, 0], im[:, 1], nr)
-            xt = self._mod_norm(c, tm[:, 0], tm[:, 1], tr)
-
-            def qkv(h, pre, names):
-                q = linear(h, w[pre + names[0] + ".weight"], w[pre + names[0] + ".bias"]).view(-1, H, hd)
-                k = linear(h, w[pre + names[1] + ".weight"], w[pre + names[1] + ".bias"]).view(-1, H, hd)
-                v = linear(h, w[pre + names[2] + ".weight"], w[pre + names[2] + ".bias"]).view(-1, H, hd)
-                return q, k, v
-
-            qi, ki, vi = qkv(xi, p + "attn.", ("to_q", "to_k", "to_v"))
-            qt, kt, vt = qkv(xt, p + "attn.", ("add_q_proj", "add_k_proj", "add_v_proj"))
-            qi = self._rope(ops.rmsnorm(qi.reshape(-1, hd), w[p + "attn.norm_q.weight"], self.eps).view(-1, H, hd),
-                            img_ang_b)
-            ki = self._rope(ops.rmsnorm(ki.reshape(-1, hd), w[p + "attn.norm_k.weight"], self.eps).view(-1, H, hd),
-                            img_ang_b)
-            qt = self._rope(ops.rmsnorm(qt.reshape(-1, hd), w[p + "attn.norm_added_q.weight"], self.eps)
-                            .view(-1, H, hd), txt_ang)
-            kt = self._rope(ops.rmsnorm(kt.reshape(-1, hd), w[p + "attn.norm_added_k.weight"], self.eps)
-                            .view(-1, H, hd), txt_ang)
-            # joint [text_b; image_b] sequences, packed
-            js = lambda a, b: torch.cat([z for bb in range(B) for z in (a[toff[bb]:toff[bb + 1]],  # noqa: E731
-                                                                          b[bb * N:(bb + 1) * N])], 0)
-            o = ops.varlen_attention(js(qt, qi), js(kt, ki), js(vt, vi), lens, hd ** -0.5).reshape(-1, D)
-            oi = torch.cat([o[sum(lens[:bb]) + lt[bb]:sum(lens[:bb + 1])] for bb in range(B)], 0)
-            ot = torch.cat([o[sum(lens[:bb]):sum(lens[:bb]) + lt[bb]] for bb in range(B)], 0)
-            x = x + self._gate(im[:, 2], nr) * linear(oi.contiguous(), w[p + "attn.to_out.0.weight"],
-                                                      w[p + "attn.to_out.0.bias"])
-            c = c + self._gate(tm[:, 2], tr) * linear(ot.contiguous(), w[p + "attn.to_add_out.weight"],
-                                                      w[p + "attn.to_add_out.bias"])
+            pi = linear(self._mod_norm(x, im[:, 0], im[:, 1], nr), w[a + "img_qkv.weight"], w[a + "img_qkv.bias"])
+            pt = linear(self._mod_norm(c, tm[:, 0], tm[:, 1], tr), w[a + "txt_qkv.weight"], w[a + "txt_qkv.bias"])
+            q = torch.empty(total, H, hd, dtype=self.dtype, device=self.device)
+            k, v = torch.empty_like(q), torch.empty_like(q)
+            # per-head RMSNorm + 3-axis RoPE written straight into the joint sequences
+            for src, cs, dst, nq, nk in ((pi, cs_img, di32, "norm_q", "norm_k"),
+                                         (pt, cs_txt, dt32, "norm_added_q", "norm_added_k")):
+                ops.qk_norm_rope(src[:, :D], H, hd, w[a + nq + ".weight"], cs, self.eps, q, dst)
+                ops.qk_norm_rope(src[:, D:2 * D], H, hd, w[a + nk + ".weight"], cs, self.eps, k, dst)
+                ops.qk_norm_rope(src[:, 2 * D:], H, hd, None, None, self.eps, v, dst)
+            o = ops.varlen_attention(q, k, v, lens, hd ** -0.5).reshape(total, D)
+            self._gated_add(x, im[:, 2], linear(o.index_select(0, dst_img), w[a + "to_out.0.weight"],
+                                                w[a + "to_out.0.bias"]), nr)
+            self._gated_add(c, tm[:, 2], linear(o.index_select(0, dst_txt), w[a + "to_add_out.weight"],
+                                                w[a + "to_add_out.bias"]), tr)
             for st, mod, rows in (("img", im, nr), ("txt", tm, tr)):
                 src = x if st == "img" else c
                 hn = self._mod_norm(src, mod[:, 3], mod[:, 4], rows)
                 f = ops.act(linear(hn, w[p + f"{st}_mlp.net.0.proj.weight"], w[p + f"{st}_mlp.net.0.proj.bias"]), 1)
-                y = linear(f, w[p + f"{st}_mlp.net.2.weight"], w[p + f"{st}_mlp.net.2.bias"])
-                if st == "img":
-                    x = x + self._gate(mod[:, 5], rows) * y
-                else:
-                    c = c + self._gate(mod[:, 5], rows) * y
+                self._gated_add(src, mod[:, 5], linear(f, w[p + f"{st}_mlp.net.2.weight"],
+                                                       w[p + f"{st}_mlp.net.2.bias"]), rows)
         e = linear(temb_act, w["norm_out.linear.weight"], w["norm_out.linear.bias"]).view(B, 2, D)
         x = self._mod_norm(x, e[:, 1], e[:, 0], nr)   # AdaLayerNormContinuous: (scale, shift) order
         return linear(x, w["proj_out.weight"], w["proj_out.bias"]).view(B, N, -1)

@@ -32,7 +32,6 @@ from pathlib import Path
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 from ome_amd import ops
 from ome_amd.models.config import ModelConfig
@@ -309,15 +308,16 @@ class MiniCPMV(LlamaForCausalLM):
         q = ops.layernorm(r["query"], r["ln_q.weight"], r["ln_q.bias"], 1e-6)
         wq, wk, wv = r["in.weight"].split(H, 0)
         bq, bk, bv = r["in.bias"].split(H, 0)
-        qh = linear(q, wq, bq).view(self.nq, nh, d).transpose(0, 1)
-        outs, off = [], 0
-        for h, w in grids:
-            x = kv[off:off + h * w]
-            off += h * w
-            k = linear((x + self._pos(h, w)).contiguous(), wk, bk).view(-1, nh, d).transpose(0, 1)
-            v = linear(x, wv, bv).view(-1, nh, d).transpose(0, 1)
-            outs.append(F.scaled_dot_product_attention(qh[None], k[None], v[None])[0].transpose(0, 1).reshape(self.nq, H))
-        o = linear(torch.cat(outs, 0), r["out.weight"], r["out.bias"])
+        qh = linear(q, wq, bq).view(self.nq, nh, d)
+        n_kv = [h * w for h, w in grids]
+        x = kv[:sum(n_kv)]
+        pos = torch.cat([self._pos(h, w) for h, w in grids], 0)
+        k = linear((x + pos).contiguous(), wk, bk).view(-1, nh, d)
+        v = linear(x.contiguous(), wv, bv).view(-1, nh, d)
+        # every slice's 64 queries cross-attend over that slice's tokens: ONE varlen launch
+        o = ops.varlen_attention(qh.repeat(len(grids), 1, 1), k, v, [self.nq] * len(grids), d ** -0.5,
+                                 k_lengths=n_kv).reshape(len(grids) * self.nq, H)
+        o = linear(o, r["out.weight"], r["out.bias"])
         o = ops.layernorm(o, r["ln_post.weight"], r["ln_post.bias"], 1e-6)
         return o @ r["proj"]
 

@@ -147,13 +147,23 @@ class MllamaVision:
     def _ln(self, x, k):
         return ops.layernorm(x.contiguous(), self.w[k + ".w"], self.w[k + ".b"], self.eps)
 
-    def _layer(self, p: str, x: torch.Tensor, bias: torch.Tensor, gated: bool) -> torch.Tensor:
+    def _layer(self, p: str, x: torch.Tensor, mask, gated: bool) -> torch.Tensor:
+        """``mask`` = (pad_rows, real_rows, pad counts, real counts): a (query, key) pair is masked
+        only when both are padding, i.e. real queries see every key of their image and padding
+        queries see the image's real keys -- two varlen launches (self, then cross lengths for
+        the padding rows) instead of a dense [S, S] bias."""
         n, S, C = x.shape
         w, h = self.w, self.heads
-        qkv = linear(self._ln(x, p + "ln1").view(n * S, C), w[p + "qkv"]).view(n, S, 3, h, C // h)
-        q, k, v = (qkv[:, :, j].transpose(1, 2) for j in range(3))
-        a = F.scaled_dot_product_attention(q, k, v, attn_mask=bias).transpose(1, 2).reshape(n * S, C)
-        a = linear(a, w[p + "o"]).view(n, S, C)
+        D = C // h
+        qkv = linear(self._ln(x, p + "ln1").view(n * S, C), w[p + "qkv"]).view(n * S, 3, h, D)
+        a = ops.varlen_attention(qkv[:, 0], qkv[:, 1], qkv[:, 2], [S] * n, D ** -0.5)
+        pad_rows, real_rows, n_pad, n_real = mask
+        if pad_rows.numel():
+            q = qkv[:, 0].index_select(0, pad_rows)
+            kv = qkv[:, 1:].index_select(0, real_rows)
+            a.index_copy_(0, pad_rows, ops.varlen_attention(q, kv[:, 0], kv[:, 1], n_pad, D ** -0.5,
+                                                            k_lengths=n_real))
+        a = linear(a.reshape(n * S, C), w[p + "o"]).view(n, S, C)
         x = x + (torch.tanh(w[p + "gate_attn"]).to(x.dtype) * a if gated else a)
         m = linear(self._ln(x, p + "ln2").view(n * S, C), w[p + "fc1.w"], w[p + "fc1.b"])
         m = ops.act(m.contiguous(), self.act) if self.act != 6 else m * torch.sigmoid(1.702 * m)
@@ -177,9 +187,10 @@ class MllamaVision:
         # a (query, key) pair is masked only when both are padding (padded patch or padded tile)
         pad = torch.ones(n, T, Pp, dtype=torch.bool, device=x.device)
         pad[:, :, :P] = ~ar_mask.bool()[:, :, None]
-        pad = pad.view(n, T * Pp)
-        bias = torch.zeros(n, 1, T * Pp, T * Pp, dtype=x.dtype, device=x.device)
-        bias.masked_fill_((pad[:, :, None] & pad[:, None, :])[:, None], torch.finfo(x.dtype).min)
+        pad = pad.view(n * T * Pp)
+        rows = torch.arange(n * T * Pp, device=x.device)
+        n_pad = pad.view(n, T * Pp).sum(1).tolist()
+        bias = (rows[pad], rows[~pad], n_pad, [T * Pp - c for c in n_pad])   # see _layer
         x = x.view(n, T * Pp, C)
         inter = []
         for i in range(self.L):

@@ -147,17 +147,9 @@ class Phi4MMVisionTower(SiglipVisionTower):
             qkv = linear(h, w[p + "qkv.weight"], w[p + "qkv.bias"]).view(T, 3, self.heads, self.D)
             a = torch.empty(T, self.heads, self.D, dtype=x.dtype, device=dev)
             ops.varlen_attention(qkv[:Nv, 0], qkv[:Nv, 1], qkv[:Nv, 2], nv, self.D ** -0.5, out=a[:Nv])
-            vo, po = 0, Nv
-            for c in range(n):
-                if npd[c]:
-                    if nv[c]:
-                        q = qkv[po:po + npd[c], 0].transpose(0, 1)[None]
-                        k = qkv[vo:vo + nv[c], 1].transpose(0, 1)[None]
-                        v = qkv[vo:vo + nv[c], 2].transpose(0, 1)[None]
-                        a[po:po + npd[c]] = F.scaled_dot_product_attention(q, k, v, scale=self.D ** -0.5)[0].transpose(0, 1)
-                    else:
-                        a[po:po + npd[c]] = 0
-                vo, po = vo + nv[c], po + npd[c]
+            if T > Nv:   # padding queries of each crop attend to that crop's valid tokens (cross lengths)
+                ops.varlen_attention(qkv[Nv:, 0], qkv[:Nv, 1], qkv[:Nv, 2], list(npd), self.D ** -0.5,
+                                     out=a[Nv:], k_lengths=list(nv))
             x = x + linear(a.reshape(T, E), w[p + "o.weight"], w[p + "o.bias"])
             h = ops.layernorm(x, w[p + "ln2.weight"], w[p + "ln2.bias"], self.eps)
             f = ops.act(linear(h, w[p + "fc1.weight"], w[p + "fc1.bias"]), self.act)

@@ -48,17 +48,44 @@ def fused_add_rmsnorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, eps: 
          x2.shape[0], H, float(eps), stream_ptr())
 
 
-def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, eps: float) -> torch.Tensor:
-    """LayerNorm with optional bias (Starcoder2 / GPT-NeoX)."""
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None, eps: float,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """LayerNorm with optional bias (Starcoder2 / GPT-NeoX); ``out``: a row-strided [rows, H]
+    destination (e.g. one sample's rows of a packed batch)."""
     if not _gpu(x):
-        return ref.layernorm(x, w, b, eps)
+        r = ref.layernorm(x, w, b, eps)
+        if out is not None:
+            out.copy_(r.view(out.shape))
+            return out
+        return r
     H = x.shape[-1]
     x2 = x.reshape(-1, H)
     assert x2.stride(-1) == 1 and x.dtype == torch.bfloat16
+    if out is not None:
+        assert out.stride(-1) == 1 and out.shape[-1] == H
+        call("ome_layernorm", x2.data_ptr(), x2.stride(0), None, 0, w.data_ptr(), ptr(b), out.data_ptr(),
+             out.stride(0), x2.shape[0], H, float(eps), stream_ptr())
+        return out
     out = torch.empty_like(x2)
     call("ome_layernorm", x2.data_ptr(), x2.stride(0), None, 0, w.data_ptr(), ptr(b), out.data_ptr(), out.stride(0),
          x2.shape[0], H, float(eps), stream_ptr())
     return out.view(x.shape)
+
+
+def qk_norm_rope(x: torch.Tensor, H: int, hd: int, w: torch.Tensor | None, cs: torch.Tensor | None, eps: float,
+                 out: torch.Tensor, dst: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-head RMSNorm (``w`` [hd], None: none) + complex-pair RoPE (``cs`` fp32 [T, hd/2, 2] =
+    (cos, sin), None: none) of x [T, >= H*hd] (row-strided), written to rows ``dst`` [T] int32
+    (None: 0..T-1) of ``out`` [rows, H*hd] (Qwen-Image joint attention operands)."""
+    T = x.shape[0]
+    if not _gpu(x):
+        return ref.qk_norm_rope(x, H, hd, w, cs, eps, out, dst)
+    assert x.stride(1) == 1 and out.stride(-1) == 1 and x.dtype == out.dtype == torch.bfloat16
+    assert cs is None or (cs.dtype == torch.float32 and cs.is_contiguous() and cs.shape[0] == T)
+    o2 = out.view(out.shape[0], -1)
+    call("ome_qk_norm_rope", x.data_ptr(), x.stride(0), ptr(w), ptr(cs), T, H, hd, float(eps), o2.data_ptr(),
+         o2.stride(0), None if dst is None else _i32(dst).data_ptr(), stream_ptr())
+    return out
 
 
 def fused_add_layernorm(x: torch.Tensor, res: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None,
@@ -1233,15 +1260,20 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
 
 
 def varlen_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lengths: list[int], scale: float,
-                     causal: bool = False, out: torch.Tensor | None = None) -> torch.Tensor:
+                     causal: bool = False, out: torch.Tensor | None = None,
+                     k_lengths: list[int] | None = None) -> torch.Tensor:
     """Attention over packed variable-length sequences with contiguous (non-paged) K/V: encoder
-    models and vision towers.  q [T, Hq, D], k / v [T, Hkv, D] -- any per-token stride (views of a
+    models and vision towers.  q [T, Hq, D], k / v [Tk, Hkv, D] -- any per-token stride (views of a
     fused QKV projection are read in place), head dim contiguous; ``lengths``: the host-side
-    sequence lengths (sum == T).  Bidirectional unless ``causal``."""
+    sequence lengths (sum == T).  Bidirectional unless ``causal``.  ``k_lengths``: cross
+    attention -- sequence s's queries attend to ITS OWN packed key rows (``k_lengths[s]`` of them,
+    possibly 0: a zero output); None = self attention (k / v rows are the query rows)."""
     T, Hq, D = q.shape
     Hkv = k.shape[1]
+    if k_lengths is not None:
+        assert not causal and len(k_lengths) == len(lengths) and sum(k_lengths) == k.shape[0]
     if not _gpu(q):
-        r = ref.varlen_attention(q, k, v, lengths, scale, causal)
+        r = ref.varlen_attention(q, k, v, lengths, scale, causal, k_lengths)
         if out is not None:
             out.copy_(r)
             return out
@@ -1256,11 +1288,16 @@ def varlen_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lengths:
         items.extend((s, r) for r in range(0, n, 128))
     if not items:
         return out
-    # items (int2, 8-B aligned) first, then cu_seqlens
-    meta = torch.tensor([x for it in items for x in it] + cu, dtype=torch.int32).to(q.device, non_blocking=True)
+    cuk = [0]
+    for n in k_lengths or []:
+        cuk.append(cuk[-1] + n)
+    # items (int2, 8-B aligned) first, then cu_seqlens (then the key ranges)
+    meta = torch.tensor([x for it in items for x in it] + cu + (cuk if k_lengths is not None else []),
+                        dtype=torch.int32).to(q.device, non_blocking=True)
+    ni = 2 * len(items)
     call("ome_varlen_attention", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
-         meta[2 * len(items):].data_ptr(), meta.data_ptr(), len(items), out.data_ptr(), out.stride(0), Hq, Hkv, D,
-         float(scale), int(bool(causal)), stream_ptr())
+         meta[ni:].data_ptr(), meta[ni + len(cu):].data_ptr() if k_lengths is not None else None, meta.data_ptr(),
+         len(items), out.data_ptr(), out.stride(0), Hq, Hkv, D, float(scale), int(bool(causal)), stream_ptr())
     return out
 
 

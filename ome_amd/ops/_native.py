@@ -37,6 +37,7 @@ _SIGNATURES = {
         "ome_act": [vp, i64, i32, vp],
         "ome_ssm_conv1d": [vp, i64, vp, vp, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp],
         "ome_dyn_conv1d": [vp, i64, vp, i64, i32, vp, i64, vp, vp, vp, vp, i32, i32, i32, vp],
+        "ome_qk_norm_rope": [vp, i64, vp, vp, i32, i32, i32, f32, vp, i64, vp, vp],
         "ome_ssm_scan": [vp, i64, vp, i64, vp, vp, i64, vp, vp, vp, f32, vp, vp, i64, vp, vp, vp, i32, i32, i32,
                          i32, i32, vp],
         "ome_gdn_scan": [vp, vp, vp, i64, vp, vp, i64, vp, vp, vp, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32,
@@ -60,7 +61,7 @@ _SIGNATURES = {
                               i32, f32, f32, f32, vp, vp, vp, i32, i64, vp],
         "ome_paged_prefill_split": [vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, vp, i32, i32, vp, vp, vp, i64, i32,
                                     i32, f32, i32, i32, f32, f32, f32, vp, vp, i64, vp],
-        "ome_varlen_attention": [vp, i64, vp, i64, vp, i64, vp, vp, i32, vp, i64, i32, i32, i32, f32, i32, vp],
+        "ome_varlen_attention": [vp, i64, vp, i64, vp, i64, vp, vp, vp, i32, vp, i64, i32, i32, i32, f32, i32, vp],
         "ome_skinny_gemm": [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp, vp],
         "ome_stream_gemm": [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp],
         "ome_gemv": [vp, i64, vp, vp, vp, i64, i32, i32, i32, vp],

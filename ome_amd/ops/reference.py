@@ -70,6 +70,22 @@ def ssm_conv1d(x, w, bias, state, cu, slot, reset, out):
     return out
 
 
+def qk_norm_rope(x, H, hd, w, cs, eps, out, dst):
+    T = x.shape[0]
+    v = x[:, :H * hd].float().view(T, H, hd)
+    if w is not None:
+        v = (v * torch.rsqrt(v.pow(2).mean(-1, keepdim=True) + eps)).to(x.dtype).float() * w.float()
+        v = v.to(x.dtype).float()
+    if cs is not None:
+        c, s = cs[:, None, :, 0], cs[:, None, :, 1]
+        re, im = v[..., 0::2], v[..., 1::2]
+        v = torch.stack([re * c - im * s, re * s + im * c], -1).flatten(-2)
+    o2 = out.view(out.shape[0], H * hd)
+    rows = torch.arange(T) if dst is None else dst.long().cpu()
+    o2[rows.to(o2.device)] = v.reshape(T, H * hd).to(out.dtype)
+    return out
+
+
 def dyn_conv1d(x, kern, state, cu, slot, reset, cpk, out):
     """Per-row-tap causal depthwise conv + SiLU; tap K-1 multiplies the current row."""
     C = x.shape[1]
@@ -377,20 +393,26 @@ def sample(logits, temperature=None, top_k=None, top_p=None, min_p=None, generat
     return ids, lps
 
 
-def varlen_attention(q, k, v, lengths, scale, causal=False) -> torch.Tensor:
+def varlen_attention(q, k, v, lengths, scale, causal=False, k_lengths=None) -> torch.Tensor:
     T, Hq, D = q.shape
     G = Hq // k.shape[1]
     out = torch.empty(T, Hq, D, dtype=q.dtype, device=q.device)
-    t0 = 0
-    for n in lengths:
+    t0 = k0 = 0
+    for i, n in enumerate(lengths):
+        nk = n if k_lengths is None else k_lengths[i]
+        if nk == 0:
+            out[t0:t0 + n] = 0
+            t0 += n
+            continue
         qs = q[t0:t0 + n].float().transpose(0, 1)
-        ks = k[t0:t0 + n].float().repeat_interleave(G, 1).transpose(0, 1)
-        vs = v[t0:t0 + n].float().repeat_interleave(G, 1).transpose(0, 1)
+        ks = k[k0:k0 + nk].float().repeat_interleave(G, 1).transpose(0, 1)
+        vs = v[k0:k0 + nk].float().repeat_interleave(G, 1).transpose(0, 1)
         s = (qs @ ks.transpose(1, 2)) * scale
         if causal:
             s = s.masked_fill(torch.ones(n, n, dtype=torch.bool, device=q.device).triu(1), float("-inf"))
         out[t0:t0 + n] = (s.softmax(-1) @ vs).transpose(0, 1).to(q.dtype)
         t0 += n
+        k0 += nk
     return out
 
 

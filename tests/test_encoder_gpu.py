@@ -25,6 +25,21 @@ def test_varlen_attention_kernel(D, causal):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("D", [64, 72, 128])
+def test_varlen_cross_attention_kernel(D):
+    """Cross lengths (MiniCPM-V resampler, Phi-4-MM padding queries, Mllama padding rows): query
+    sequence s attends to its own packed key rows; an empty key set gives zeros."""
+    torch.manual_seed(D)
+    lq, lk = [64, 0, 5, 129, 64], [300, 7, 0, 1, 37]
+    Hq, Hkv = 4, 2
+    q = torch.randn(sum(lq), Hq, D, device="cuda").bfloat16()
+    kv = torch.randn(sum(lk), 2, Hkv, D, device="cuda").bfloat16()
+    got = ops.varlen_attention(q, kv[:, 0], kv[:, 1], lq, D ** -0.5, k_lengths=lk).float()
+    want = ref.varlen_attention(q.float(), kv[:, 0].float(), kv[:, 1].float(), lq, D ** -0.5, k_lengths=lk)
+    assert (got - want).abs().max().item() < 2e-2
+    assert got[64 + 0 + 5:64 + 5 + 129].abs().max().item() > 0 and got[64:69].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("kind", ["bert", "xlmr_cls"])
 def test_encoder_on_gpu(tmp_path, kind):
     from ome_amd.runtime.engine import Engine, EngineArgs

@@ -130,7 +130,7 @@ def test_dit_matches_reference():
     txts = [torch.randn(7, 96, generator=g), torch.randn(4, 96, generator=g)]
     t = torch.tensor([0.7, 0.7])
     got = dit.forward(img, txts, t, shapes)
-    want = _ref_dit(dit.w, CFG, img, txts, t, shapes)
+    want = _ref_dit(dit.state_dict(), CFG, img, txts, t, shapes)
     assert got.shape == want.shape == (2, N, 64)
     assert (got - want).abs().max().item() < 2e-3 * want.abs().max().item(), (got - want).abs().max()
 
