@@ -127,7 +127,11 @@ class QwenImagePipeline:
         p = PRESETS[preset]
         dit = QwenImageDiT(p["transformer"], device, dtype).init_random(seed)
         vae = QwenImageVAE(p["vae"], device, dtype).init_random(seed + 1)
-        te_cfg = LM_PRESETS.get(p["text_encoder"]) or _tiny_text_encoder_cfg()
+        te_cfg = LM_PRESETS.get(p["text_encoder"])
+        if te_cfg is None:
+            if not p["text_encoder"].startswith("tiny-"):
+                raise KeyError(f"text encoder preset {p['text_encoder']!r} missing")
+            te_cfg = _tiny_text_encoder_cfg()
         te = build_model(ModelConfig.from_hf(te_cfg), device, dtype, load_format="dummy", seed=seed + 2)
         from ome_amd.runtime.tokenizer import ByteTokenizer
 

@@ -449,6 +449,17 @@ PRESETS: dict[str, dict] = {
                         vision_config=dict(depth=32, embed_dim=1280, hidden_size=3584, num_heads=16, mlp_ratio=4,
                                            patch_size=14, spatial_merge_size=2, temporal_patch_size=2,
                                            in_channels=3, hidden_act="quick_gelu")),
+    # Qwen2.5-VL-7B-Instruct (also Qwen-Image's text encoder)
+    "qwen2.5-vl-7b": dict(architectures=["Qwen2_5_VLForConditionalGeneration"], model_type="qwen2_5_vl",
+                          hidden_size=3584, num_hidden_layers=28, num_attention_heads=28, num_key_value_heads=4,
+                          intermediate_size=18944, vocab_size=152064, rms_norm_eps=1e-6, rope_theta=1000000.0,
+                          max_position_embeddings=128000,
+                          rope_scaling={"type": "mrope", "mrope_section": [16, 24, 24]}, image_token_id=151655,
+                          video_token_id=151656, vision_start_token_id=151652, vision_end_token_id=151653,
+                          vision_config=dict(depth=32, hidden_size=1280, num_heads=16, intermediate_size=3420,
+                                             patch_size=14, spatial_merge_size=2, temporal_patch_size=2,
+                                             in_channels=3, window_size=112, fullatt_block_indexes=[7, 15, 23, 31],
+                                             out_hidden_size=3584, hidden_act="silu")),
     "tiny-qwen2-vl": dict(architectures=["Qwen2VLForConditionalGeneration"], model_type="qwen2_vl", hidden_size=256,
                           num_hidden_layers=2, num_attention_heads=4, num_key_value_heads=2, intermediate_size=512,
                           vocab_size=1024, rms_norm_eps=1e-6, rope_theta=1000000.0, max_position_embeddings=4096,
