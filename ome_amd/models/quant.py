@@ -33,16 +33,35 @@ class Fp8Weight:
     q: torch.Tensor        # [N, K] float8_e4m3fn
     scale: torch.Tensor    # [N] (block 0) or [ceil(N/128), K/128] (block 128), float32
     block: int = 0
+    # bf16 copy for the row counts where W8A8 was measured slower than bf16 (small N x K
+    # projections at decode sizes: activation quant + a few output tiles cost more than the halved
+    # weight bytes save -- profiles/r04_fp8_sk_bench.txt); None = always fp8
+    bf16: torch.Tensor | None = None
+    bf16_max_m: int = 0
 
     @property
     def shape(self):
         return self.q.shape
 
     def nbytes(self) -> int:
-        return self.q.numel() + self.scale.numel() * 4
+        n = self.q.numel() + self.scale.numel() * 4
+        return n + (self.bf16.numel() * 2 if self.bf16 is not None else 0)
 
     def dequant(self, dtype=torch.bfloat16) -> torch.Tensor:
         return ref.fp8_dequant_weight(self.q, self.scale, self.block).to(dtype)
+
+
+def fp8_bf16_max_m(N: int, K: int) -> int:
+    """Rows up to which an fp8 [N, K] projection runs on its bf16 copy (0: never), from the
+    measured fp8 / bf16 table (profiles/r04_fp8_sk_bench.txt, r05 re-measure).  Per shape: N <= 2048 (q_a / kv_a) or N <= 6144 with K <= 4096 (Llama-8B qkv / o)
+    lose up to 256 rows; other <= 32M-element weights (DeepSeek shared gate_up) up to 32 rows;
+    <= 64M (Llama-8B down) on the GEMV rows only; anything larger always wins in fp8."""
+    if os.environ.get("OME_FP8_BF16_FALLBACK", "1") == "0":
+        return 0
+    n = N * K
+    if N <= 2048 or (N <= 6144 and K <= 4096):
+        return 256
+    return 32 if n <= (32 << 20) else 4 if n <= (64 << 20) else 0
 
 
 @dataclass
@@ -114,11 +133,17 @@ def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
         s = torch.where(amax > 0, amax / ref.FP8_MAX, torch.ones_like(amax))
         q = (blocks / s[:, None, :, None]).clamp(-ref.FP8_MAX, ref.FP8_MAX).to(torch.float8_e4m3fn)
         q = q.reshape(nb * block, K)[:N].contiguous()
-        return Fp8Weight(q, s.contiguous(), block)
-    amax = wf.abs().amax(-1)
-    s = torch.where(amax > 0, amax / ref.FP8_MAX, torch.ones_like(amax))
-    q = (wf / s[:, None]).clamp(-ref.FP8_MAX, ref.FP8_MAX).to(torch.float8_e4m3fn).contiguous()
-    return Fp8Weight(q, s.contiguous(), 0)
+        out = Fp8Weight(q, s.contiguous(), block)
+    else:
+        amax = wf.abs().amax(-1)
+        s = torch.where(amax > 0, amax / ref.FP8_MAX, torch.ones_like(amax))
+        q = (wf / s[:, None]).clamp(-ref.FP8_MAX, ref.FP8_MAX).to(torch.float8_e4m3fn).contiguous()
+        out = Fp8Weight(q, s.contiguous(), 0)
+    m = fp8_bf16_max_m(N, K) if w.is_cuda else 0
+    if m:
+        # the fp8 weights' own values (dequantised), so both paths compute the same projection
+        out.bf16, out.bf16_max_m = out.dequant(torch.bfloat16).contiguous(), m
+    return out
 
 
 # rows up to which plain bf16 projections run on the GEMV stream kernel (0 disables)
@@ -153,6 +178,8 @@ def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None, out: torch.Tens
         out.copy_(linear(x, w, bias))
         return out
     if isinstance(w, Fp8Weight):
+        if w.bf16 is not None and x.dim() == 2 and x.shape[0] <= w.bf16_max_m and x.dtype == torch.bfloat16:
+            return linear(x, w.bf16, bias)
         return ops.fp8_linear(x, w.q, w.scale, w.block, bias)
     if x.dim() == 2 and x.shape[0] <= 256 and x.is_cuda:
         if x.shape[0] <= _GEMV_ROWS and ops.gemv_ok(x, w, bias):

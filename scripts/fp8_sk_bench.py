@@ -13,7 +13,7 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ome_amd import ops  # noqa: E402
-from ome_amd.models.quant import quantize_weight  # noqa: E402
+from ome_amd.models.quant import linear, quantize_weight  # noqa: E402
 
 SHAPES = {
     "llama8b": [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336)],
@@ -84,6 +84,15 @@ def main():
                     ops.FP8_SK_MAX_ROWS = 512
                     r[f"fp8_{tag}_sk"] = best[0]
                     r[f"fp8_{tag}_sk_cfg"] = best[1:]
+                # what the model actually runs: quant.linear on the bf16 weight vs on the Fp8Weight
+                # (which takes its bf16 copy below fp8_bf16_max_m rows)
+                r["bf16_routed"] = timed(lambda i: linear(x, ws[i % c]))
+                r["fp8_pc_routed"] = timed(lambda i: linear(x, q0[i % c]))
+                r["fp8_blk_routed"] = timed(lambda i: linear(x, q1[i % c]))
+                print(f"  routed: bf16 {r['bf16_routed']:7.1f}us  fp8 pc {r['fp8_pc_routed']:7.1f}us "
+                      f"({r['bf16_routed'] / r['fp8_pc_routed']:4.2f}x)  fp8 blk {r['fp8_blk_routed']:7.1f}us "
+                      f"({r['bf16_routed'] / r['fp8_blk_routed']:4.2f}x)  bf16-copy rows <= {q0[0].bf16_max_m}",
+                      flush=True)
                 bf = min(r["bf16_lib"], r.get("bf16_sk", 1e9))
                 print(f"{model:8s} {name:9s} M={M:4d} bf16 {bf:7.1f}us | fp8 pc: sk {r['fp8_pc_sk']:7.1f} "
                       f"old {r['fp8_pc_old']:7.1f} ({N * K / r['fp8_pc_sk'] / 1e6:4.2f} TB/s, "
