@@ -61,7 +61,7 @@ def fp8_bf16_max_m(N: int, K: int) -> int:
     n = N * K
     if N <= 2048 or (N <= 6144 and K <= 4096):
         return 256
-    return 32 if n <= (32 << 20) else 4 if n <= (64 << 20) else 0
+    return 32 if n <= (32 << 20) else 4 if n < (64 << 20) else 0
 
 
 @dataclass
