@@ -15,6 +15,7 @@
 // reached the epoch.  A bounded spin that expires records an error word instead of hanging the
 // GPU.  Accumulation is in fp32.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -304,6 +305,12 @@ struct Ctx {
 }  // namespace
 
 // allocate this rank's signal + data buffers; returns the two IPC handles (64 bytes each)
+// OME_COMM_FINEGRAINED=1: IPC-shared data buffers allocated fine-grained (docs/COHERENCE.md)
+static bool comm_finegrained() {
+  static const bool f = getenv("OME_COMM_FINEGRAINED") && atoi(getenv("OME_COMM_FINEGRAINED")) != 0;
+  return f;
+}
+
 OME_API int ome_comm_create(int rank, int world, size_t data_bytes, void** ctx_out, void* sig_handle,
                             void* data_handle) {
   if (world < 2 || world > kMaxRanks || rank < 0 || rank >= world) return -2;
@@ -318,7 +325,10 @@ OME_API int ome_comm_create(int rank, int world, size_t data_bytes, void** ctx_o
   if (e != hipSuccess) return (int)e;
   data_bytes = (data_bytes + 15) & ~(size_t)15;
   c->data_bytes = data_bytes;
-  e = hipMalloc((void**)&c->data, 2 * data_bytes);  // input half + reduced-chunk half at +data_bytes
+  // input half + reduced-chunk half at +data_bytes; OME_COMM_FINEGRAINED=1: fine-grained (coherent
+  // peer access without relying on the system-scope write-back / invalidate, docs/COHERENCE.md)
+  e = comm_finegrained() ? hipExtMallocWithFlags((void**)&c->data, 2 * data_bytes, hipDeviceMallocFinegrained)
+                         : hipMalloc((void**)&c->data, 2 * data_bytes);
   if (e != hipSuccess) return (int)e;
   e = hipIpcGetMemHandle((hipIpcMemHandle_t*)sig_handle, c->sig);
   if (e != hipSuccess) return (int)e;

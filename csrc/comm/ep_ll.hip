@@ -20,6 +20,7 @@
 // Bounded spins record an error word instead of hanging the GPU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #define OME_API extern "C" __attribute__((visibility("default")))
@@ -35,6 +36,8 @@ struct EpSig {
   uint32_t ready[2][kMaxRanks];  // [dispatch / combine][peer] = last epoch that peer published
   uint32_t epoch;
   uint32_t error;
+  uint32_t done[2];              // fused kernels: finished workgroups of the current send / comb_send
+  int scnt[kMaxRanks];           // fused send: rows bucketed per owner so far (reset by the last block)
 };
 
 struct EpPeers {
@@ -236,6 +239,196 @@ __global__ __launch_bounds__(256) void ep_comb_pull_kernel(EpPeers P, int me, in
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Fused path (default): 4 launches per MoE layer instead of 10.
+//   send      (grid = assignments): plan + pack in one pass -- each workgroup buckets its
+//             assignment with an atomic on MY per-owner counter, packs the row into S[p][dst][slot],
+//             releases; the LAST workgroup (done counter) publishes the counts, resets the
+//             counters, advances the epoch and raises my dispatch flag on every peer.
+//   recv      (grid G x W): per source, wait for its flag, then copy only the rows it actually
+//             sent (slot loop bounded by its count, not the capacity) and mark the rest empty.
+//   comb_send (grid G x W): expert outputs of the received rows -> MY C[p][src][slot]; the last
+//             workgroup raises my combine flag on every peer.
+//   comb_recv (grid = tokens): wait for every owner's combine flag, weighted sum (fp32).
+// The counters / done words live in the uncached signal page; the data buffers keep the
+// owner-writes / peers-read protocol of the unfused kernels above.
+// ------------------------------------------------------------------------------------------
+constexpr int kRecvBlocks = 32;
+
+__device__ __forceinline__ bool last_block(uint32_t* done) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();   // this block's stores are visible system-wide before it counts
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = atomicAdd(done, 1u) == gridDim.x * gridDim.y - 1;
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+__device__ __forceinline__ void spin_flag(EpSig* self, int which, int src, uint32_t e) {
+  uint64_t spins = 0;
+  while (ld_acquire_sys(&self->ready[which][src]) < e) {
+    if (++spins > kSpinLimit) {
+      atomicOr(&self->error, 1u);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__global__ __launch_bounds__(256) void ep_send_kernel(EpPeers P, int me, int W, const bf16* __restrict__ x,
+                                                      int64_t ldx, int H, int k, const int* __restrict__ topk_ids,
+                                                      int n, int e_local, int n_experts, int cap,
+                                                      int* __restrict__ a_dst, int* __restrict__ a_slot,
+                                                      int* __restrict__ a_local, const int64_t* __restrict__ rep_rank,
+                                                      const int64_t* __restrict__ rep_slot,
+                                                      const int64_t* __restrict__ n_rep, int rmax, EpSig* self,
+                                                      char* mybuf, Layout L) {
+  const uint32_t cur = self->epoch + 1;
+  const int par = cur & 1;
+  const int a = blockIdx.x;
+  __shared__ int s_dst, s_slot, s_loc;
+  if (a < n && threadIdx.x == 0) {
+    int id = topk_ids[a];
+    id = id < 0 ? 0 : (id < n_experts ? id : n_experts - 1);
+    int dst, loc;
+    if (rep_rank != nullptr) {
+      const int nr = (int)n_rep[id];
+      const int j = nr > 0 ? a % nr : 0;
+      dst = (int)rep_rank[(int64_t)id * rmax + j];
+      loc = (int)rep_slot[(int64_t)id * rmax + j];
+    } else {
+      dst = id / e_local;
+      loc = id - dst * e_local;
+    }
+    dst = dst < 0 ? 0 : (dst < W ? dst : W - 1);
+    loc = loc < 0 ? 0 : (loc < e_local ? loc : e_local - 1);
+    const int slot = atomicAdd(&self->scnt[dst], 1);
+    a_dst[a] = dst;
+    a_local[a] = loc;
+    a_slot[a] = slot < cap ? slot : -1;
+    s_dst = dst;
+    s_slot = slot < cap ? slot : -1;
+    s_loc = loc;
+  }
+  __syncthreads();
+  if (a < n && s_slot >= 0) {
+    char* base = mybuf + par * L.per_parity;
+    const u32x4* src = reinterpret_cast<const u32x4*>(x + (int64_t)(a / k) * ldx);
+    u32x4* dstp = reinterpret_cast<u32x4*>(base + ((int64_t)s_dst * cap + s_slot) * H * 2);
+    for (int v = threadIdx.x; v < H / 8; v += blockDim.x) dstp[v] = src[v];
+    if (threadIdx.x == 0) reinterpret_cast<int*>(base + L.rows)[s_dst * cap + s_slot] = s_loc;
+  }
+  if (!last_block(&self->done[0])) return;
+  // last workgroup: every row of this epoch is packed and released
+  int* counts = (int*)(mybuf + par * L.per_parity + L.rows + L.ids);
+  if ((int)threadIdx.x < W) {
+    const int c = atomicExch(&self->scnt[threadIdx.x], 0);
+    counts[threadIdx.x] = c < cap ? c : cap;
+    if (c > cap) atomicOr(&self->error, 2u);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    self->done[0] = 0;
+    self->epoch = cur;
+    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < W) st_release_sys(&P.sig[threadIdx.x]->ready[0][me], cur);
+}
+
+// grid (kRecvBlocks, W): rows source `src` sent me, R [W][cap][H]; rids past the count = e_local
+__global__ __launch_bounds__(256) void ep_recv_kernel(EpPeers P, int me, int H, int cap, int e_local, Layout L,
+                                                      EpSig* self, bf16* __restrict__ R, int* __restrict__ rids,
+                                                      int* __restrict__ rcount) {
+  const int g = blockIdx.x, src = blockIdx.y;
+  const uint32_t cur = self->epoch;
+  if (threadIdx.x == 0) spin_flag(self, 0, src, cur);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const int par = cur & 1;
+  const char* base = P.buf[src] + par * L.per_parity;
+  const int count = reinterpret_cast<const int*>(base + L.rows + L.ids)[me];
+  if (g == 0 && threadIdx.x == 0) rcount[src] = count;
+  for (int slot = g; slot < cap; slot += gridDim.x) {
+    if (slot >= count) {   // empty slots: ids only (the grouped GEMM skips the null expert)
+      for (int s2 = slot + (int)threadIdx.x * gridDim.x; s2 < cap; s2 += blockDim.x * gridDim.x)
+        rids[src * cap + s2] = e_local;
+      break;
+    }
+    const u32x4* s = reinterpret_cast<const u32x4*>(base + ((int64_t)me * cap + slot) * H * 2);
+    u32x4* d = reinterpret_cast<u32x4*>(R + ((int64_t)src * cap + slot) * H);
+    for (int v = threadIdx.x; v < H / 8; v += blockDim.x) d[v] = s[v];
+    if (threadIdx.x == 0) rids[src * cap + slot] = reinterpret_cast<const int*>(base + L.rows)[me * cap + slot];
+  }
+}
+
+// grid (kRecvBlocks, W): expert outputs of the rows src sent me -> MY C[p][src][slot]; the last
+// workgroup raises my combine flag on every peer
+__global__ __launch_bounds__(256) void ep_comb_send_kernel(EpPeers P, int me, int W, const bf16* __restrict__ y_sorted,
+                                                           const int* __restrict__ inv,
+                                                           const int* __restrict__ rcount, int H, int cap, Layout L,
+                                                           EpSig* self, char* mybuf) {
+  const int g = blockIdx.x, src = blockIdx.y;
+  const uint32_t cur = self->epoch;
+  const int par = cur & 1;
+  char* base = mybuf + par * L.per_parity + L.rows + L.ids + L.counts;
+  const int count = rcount[src];
+  for (int slot = g; slot < count; slot += gridDim.x) {
+    const u32x4* s = reinterpret_cast<const u32x4*>(y_sorted + (int64_t)inv[src * cap + slot] * H);
+    u32x4* d = reinterpret_cast<u32x4*>(base + ((int64_t)src * cap + slot) * H * 2);
+    for (int v = threadIdx.x; v < H / 8; v += blockDim.x) d[v] = s[v];
+  }
+  if (!last_block(&self->done[1])) return;
+  if (threadIdx.x == 0) {
+    self->done[1] = 0;
+    __threadfence_system();
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < W) st_release_sys(&P.sig[threadIdx.x]->ready[1][me], cur);
+}
+
+// grid = tokens: wait for every owner's combine flag, then the weighted sum of ep_comb_pull_kernel
+__global__ __launch_bounds__(256) void ep_comb_recv_kernel(EpPeers P, int me, int W, int H, int k, int cap, Layout L,
+                                                           EpSig* self, const float* __restrict__ topk_w,
+                                                           const int* __restrict__ a_dst,
+                                                           const int* __restrict__ a_slot, float scale,
+                                                           bf16* __restrict__ out, int64_t ldo) {
+  const uint32_t cur = self->epoch;
+  if ((int)threadIdx.x < W) spin_flag(self, 1, threadIdx.x, cur);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const int t = blockIdx.x;
+  const int par = cur & 1;
+  for (int v = threadIdx.x; v < H / 8; v += blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < k; ++j) {
+      const int a = t * k + j, slot = a_slot[a];
+      if (slot < 0) continue;
+      const char* base = P.buf[a_dst[a]] + par * L.per_parity + L.rows + L.ids + L.counts;
+      add8(acc, reinterpret_cast<const u32x4*>(base + ((int64_t)me * cap + slot) * H * 2)[v], topk_w[a]);
+    }
+    u32x4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bf16 lo = (bf16)(acc[2 * i] * scale), hi = (bf16)(acc[2 * i + 1] * scale);
+      r[i] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+    }
+    reinterpret_cast<u32x4*>(out + (int64_t)t * ldo)[v] = r;
+  }
+}
+
+// OME_EP_LL_FUSED=0 selects the 10-launch kernels (A/B timing)
+static bool fused() {
+  static const bool f = !getenv("OME_EP_LL_FUSED") || atoi(getenv("OME_EP_LL_FUSED")) != 0;
+  return f;
+}
+
 struct EpCtx {
   int rank, world, cap, H;
   EpSig* sig;
@@ -247,13 +440,21 @@ struct EpCtx {
 
 }  // namespace
 
+// OME_COMM_FINEGRAINED=1: IPC-shared data buffers allocated fine-grained (docs/COHERENCE.md)
+static bool comm_finegrained() {
+  static const bool f = getenv("OME_COMM_FINEGRAINED") && atoi(getenv("OME_COMM_FINEGRAINED")) != 0;
+  return f;
+}
+
 OME_API int ome_ep_create(int rank, int world, int cap, int H, void** ctx_out, void* sig_handle, void* buf_handle) {
   if (world < 2 || world > kMaxRanks || rank < 0 || rank >= world || H % 8 || cap <= 0) return -2;
   EpCtx* c = new EpCtx{rank, world, cap, H, nullptr, nullptr, Layout(world, cap, H), {}, {}};
   hipError_t e = hipExtMallocWithFlags((void**)&c->sig, sizeof(EpSig), hipDeviceMallocUncached);
   if (e != hipSuccess) return (int)e;
   if ((e = hipMemset(c->sig, 0, sizeof(EpSig))) != hipSuccess) return (int)e;
-  if ((e = hipMalloc((void**)&c->buf, 2 * c->L.per_parity)) != hipSuccess) return (int)e;
+  e = comm_finegrained() ? hipExtMallocWithFlags((void**)&c->buf, 2 * c->L.per_parity, hipDeviceMallocFinegrained)
+                         : hipMalloc((void**)&c->buf, 2 * c->L.per_parity);   // docs/COHERENCE.md
+  if (e != hipSuccess) return (int)e;
   if ((e = hipMemset(c->buf, 0, 2 * c->L.per_parity)) != hipSuccess) return (int)e;
   if ((e = hipIpcGetMemHandle((hipIpcMemHandle_t*)sig_handle, c->sig)) != hipSuccess) return (int)e;
   if ((e = hipIpcGetMemHandle((hipIpcMemHandle_t*)buf_handle, c->buf)) != hipSuccess) return (int)e;
@@ -292,6 +493,14 @@ OME_API int ome_ep_dispatch(void* ctx, const void* x, int64_t ldx, const int* to
   EpCtx* c = (EpCtx*)ctx;
   const int n = T * k;
   if (e_local <= 0 || n_experts <= 0) return -2;
+  if (fused()) {
+    ep_send_kernel<<<n > 0 ? n : 1, 256, 0, stream>>>(c->peers, c->rank, c->world, (const bf16*)x, ldx, c->H, k,
+                                                      topk_ids, n, e_local, n_experts, c->cap, a_dst, a_slot, a_local,
+                                                      rep_rank, rep_slot, n_rep, rmax, c->sig, c->buf, c->L);
+    ep_recv_kernel<<<dim3(kRecvBlocks, c->world), 256, 0, stream>>>(c->peers, c->rank, c->H, c->cap, e_local, c->L,
+                                                                   c->sig, (bf16*)R, rids, rcount);
+    return (int)hipGetLastError();
+  }
   ep_begin_kernel<<<1, 64, 0, stream>>>(c->sig);
   ep_plan_kernel<<<1, 1024, 0, stream>>>(topk_ids, n, e_local, c->world, n_experts, c->cap, a_dst, a_slot, a_local,
                                          rep_rank,
@@ -312,6 +521,14 @@ OME_API int ome_ep_combine(void* ctx, const void* y_sorted, const int* inv, cons
                            const int* a_dst, const int* a_slot, int T, int k, float scale, void* out, int64_t ldo,
                            hipStream_t stream) {
   EpCtx* c = (EpCtx*)ctx;
+  if (fused()) {
+    ep_comb_send_kernel<<<dim3(kRecvBlocks, c->world), 256, 0, stream>>>(
+        c->peers, c->rank, c->world, (const bf16*)y_sorted, inv, rcount, c->H, c->cap, c->L, c->sig, c->buf);
+    if (T > 0)
+      ep_comb_recv_kernel<<<T, 256, 0, stream>>>(c->peers, c->rank, c->world, c->H, k, c->cap, c->L, c->sig, topk_w,
+                                                 a_dst, a_slot, scale, (bf16*)out, ldo);
+    return (int)hipGetLastError();
+  }
   ep_comb_pack_kernel<<<dim3(c->cap, c->world), 256, 0, stream>>>((const bf16*)y_sorted, inv, rcount, c->H, c->cap,
                                                                  c->L, c->sig, c->buf);
   ep_signal_kernel<<<1, 64, 0, stream>>>(c->peers, c->rank, c->world, 1, c->sig);
