@@ -31,11 +31,62 @@ def evict(path):
         os.close(fd)
 
 
+def _rank_load(r, tp, d, cfg_hf, start, q, ready):
+    """One TP rank in its own process: wait for the common start, load its shard onto cuda:0."""
+    try:
+        cfg = ModelConfig.from_hf(cfg_hf)
+        pstate.set_state(pstate.ParallelState(tp_size=tp, tp_rank=r, world_size=tp, rank=r))
+        torch.cuda.init()
+        torch.empty(1, device="cuda")
+        ready.put(r)
+        start.wait()
+        b0 = nio.bytes_read()
+        t = time.perf_counter()
+        m = build_model(cfg, "cuda", torch.bfloat16, model_path=d, load_format="safetensors")
+        torch.cuda.synchronize()
+        q.put((r, time.perf_counter() - t, nio.bytes_read() - b0, None))
+        del m
+    except Exception as e:  # noqa: BLE001
+        q.put((r, 0.0, 0, repr(e)))
+
+
+def concurrent(tp, d, hf, shards, total):
+    """All tp ranks loading their slices at once (one process each, all on GPU 0 here; one per
+    GPU on a node) from a cold page cache: per-rank and aggregate GB/s."""
+    import multiprocessing as mp
+
+    for f in shards:
+        evict(f)
+    ctx = mp.get_context("spawn")
+    start, q, ready = ctx.Event(), ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_rank_load, args=(r, tp, d, hf, start, q, ready)) for r in range(tp)]
+    for p in ps:
+        p.start()
+    for _ in ps:   # every process imported torch and initialised the GPU before the common start
+        ready.get(timeout=600)
+    t0 = time.perf_counter()
+    start.set()
+    got = [q.get(timeout=600) for _ in ps]
+    wall = time.perf_counter() - t0
+    for p in ps:
+        p.join(timeout=60)
+    errs = [g for g in got if g[3]]
+    if errs:
+        raise RuntimeError(errs)
+    nb = sum(g[2] for g in got)
+    per = [g[2] / g[1] / 1e9 for g in got]
+    print(f"concurrent tp={tp}: {nb / 1e9:.2f} GB read by {tp} ranks in {wall:.2f}s wall = {nb / wall / 1e9:.2f} GB/s "
+          f"aggregate; per rank {min(per):.2f}-{max(per):.2f} GB/s (mean {sum(per) / len(per):.2f})", flush=True)
+    return {"ranks": tp, "wall_s": round(wall, 3), "aggregate_GBps": round(nb / wall / 1e9, 2),
+            "per_rank_GBps": [round(x, 2) for x in per], "bytes_total": int(nb), "checkpoint_bytes": int(total)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--tp", type=int, default=8)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--concurrent", action="store_true", help="also load all TP ranks at once, one process each")
     a = ap.parse_args()
     hf = dict(PRESETS["llama-3-70b"])
     hf["num_hidden_layers"] = a.layers
@@ -92,6 +143,8 @@ def main():
         res[f"tp{tp}"] = {"bytes_per_rank": int(nb), "fraction": round(nb / total, 4), "seconds": round(dt, 3),
                           "GBps": round(nb / dt / 1e9, 2)}
     pstate.set_state(pstate.ParallelState())
+    if a.concurrent:
+        res[f"concurrent_tp{a.tp}"] = concurrent(a.tp, d, hf, shards, total)
     print(json.dumps(res))
     if not a.dir:
         for f in shards:
