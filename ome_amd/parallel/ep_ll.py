@@ -82,7 +82,10 @@ class LowLatencyEP:
                                        C.c_void_p(rcount.data_ptr()), C.c_void_p(s))
         if rc != 0:
             raise _native.NativeError(f"ome_ep_dispatch failed ({rc})")
-        y, inv = ops.moe_experts_sorted(R, rids, w13, w2, act, e_local)
+        if w13 is None:   # exchange only (latency benchmarks): every received row comes back as is
+            y, inv = R, torch.arange(R.shape[0], dtype=torch.int32, device=dev)
+        else:
+            y, inv = ops.moe_experts_sorted(R, rids, w13, w2, act, e_local)
         out = torch.empty(T, H, dtype=x.dtype, device=dev)
         w = topk_w.float().contiguous()
         rc = self._lib.ome_ep_combine(self._ctx, C.c_void_p(y.data_ptr()), C.c_void_p(inv.data_ptr()),

@@ -102,6 +102,12 @@ def _worker(rank, world, port, q):
             tw, tid = ops.moe_route(logits, K)
             t = _graph_time(lambda: ep.forward(x, tw, tid, w13, w2, 0, 1.0, el), dist)
             rows.append(f"ep_ll layer       T={T:4d} top{K}/{E} H{H}  {t:8.1f} us (dispatch + experts + combine)")
+            t = _graph_time(lambda: ep.forward(x, tw, tid, None, None, 0, 1.0, el), dist)
+            rows.append(f"ep_ll exchange    T={T:4d} top{K}/{E} H{H}  {t:8.1f} us (dispatch + combine, no experts)")
+            rt = torch.randn(T * K, H, device=dev).to(torch.bfloat16)
+            rid = torch.randint(0, el, (T * K,), device=dev, dtype=torch.int32)
+            t = _graph_time(lambda: ops.moe_experts_sorted(rt, rid, w13, w2, 0, el), dist)
+            rows.append(f"experts only      T={T:4d} top{K}/{E} H{H}  {t:8.1f} us (align + 2 grouped GEMMs + act)")
             dist.barrier()
             ep.close()
         q.put((rank, rows, None))
