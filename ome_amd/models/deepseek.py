@@ -334,11 +334,17 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         q_nope = q[..., : self.nope].transpose(0, 1).contiguous()         # [Hl, T, nope]
         q_full[:, :, :lat].copy_(torch.bmm(q_nope, self.w_uk[i]).transpose(0, 1))
         o_lat = torch.empty(T, Hl, lat, dtype=x.dtype, device=x.device)
-        if x.is_cuda and self._ws is None:
-            self._ws = ops.MLAWorkspace(x.device)
+        ws = None
+        if x.is_cuda:   # one split-K workspace per stream (two-batch overlap runs two at once)
+            if self._ws is None:
+                self._ws = {}
+            sid = torch.cuda.current_stream(x.device).cuda_stream
+            ws = self._ws.get(sid)
+            if ws is None:
+                ws = self._ws[sid] = ops.MLAWorkspace(x.device)
         cache3 = cache.view(cache.shape[0], -1, lat + self.rope)
         for s, e, bt, rows, lens in self._token_rows(meta, T):
-            ops.mla_attn(q_full[s:e], cache3, bt, rows, lens, self.scale, self._ws, out=o_lat[s:e], dv=lat)
+            ops.mla_attn(q_full[s:e], cache3, bt, rows, lens, self.scale, ws, out=o_lat[s:e], dv=lat)
         o = torch.bmm(o_lat.transpose(0, 1).contiguous(), self.w_uv[i])   # [Hl, T, vd]
         o = o.transpose(0, 1).reshape(T, Hl * self.vd)
         return pstate.tp_all_reduce(linear(o, self.w_o[i]))

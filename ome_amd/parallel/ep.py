@@ -197,7 +197,7 @@ def moe_ep(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13_lo
     honoured by both.  Expert biases (GPT-OSS) take the RCCL path (the low-latency exchange is
     not attached for such models)."""
     st = pstate.get()
-    ll = getattr(st, "ep_ll", None)
+    ll = getattr(st, "ep_ll_cur", None) or getattr(st, "ep_ll", None)
     if ll is not None and x.is_cuda and st.ep_ll_ok and b13_local is None and b2_local is None:
         e_local = w13_local.shape[0]   # expert slots per rank (redundant replicas included)
         return ll.forward(x, topk_w, topk_ids, w13_local, w2_local, act, scale, e_local, tables)
@@ -220,6 +220,28 @@ def attach_low_latency(model, max_tokens: int) -> bool:
     from ome_amd.parallel.ep_ll import LowLatencyEP
 
     st.ep_ll = LowLatencyEP(st.ep_group, model.cfg.hidden_size, max_tokens, k, cpu_group=st.cpu_group)
+    if st.tbo:   # two-batch overlap: micro-batch B exchanges through its own buffers and epochs
+        st.ep_ll_b = LowLatencyEP(st.ep_group, model.cfg.hidden_size, max_tokens, k, cpu_group=st.cpu_group)
     st.ep_ll_cap = max_tokens
     st.ep_ll_ok = True
     return True
+
+
+def ep_idle_layers(model, ll) -> None:
+    """This rank's part of one forward's worth of exchanges on ``ll`` with NO local tokens: every
+    MoE layer in order dispatches nothing and computes the experts for the rows its peers send.
+    Two-batch overlap: a rank whose step is not a split decode (prefill / mixed) still runs
+    micro-batch B's exchanges, so every exchange keeps all participants."""
+    H = model.cfg.hidden_size
+    dev = model.device
+    x = torch.empty(0, H, dtype=model.dtype, device=dev)
+    k = model.k
+    tw = torch.empty(0, k, dtype=torch.float32, device=dev)
+    tid = torch.empty(0, k, dtype=torch.int32, device=dev)
+    for i in model.layers:
+        if i not in model.moe_layers:
+            continue
+        tables = model.eplb.tables[i] if getattr(model, "eplb", None) is not None else None
+        w13 = model.w13[i]
+        ll.forward(x, tw, tid, w13, model.w2[i], model.act, getattr(model, "routed_scale", 1.0), w13.shape[0],
+                   tables)

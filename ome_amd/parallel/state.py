@@ -44,6 +44,8 @@ class ParallelState:
     ep_ll: object | None = None # ome_amd.parallel.ep_ll.LowLatencyEP (DP attention on one node)
     ep_ll_ok: bool = False      # this lockstep step may use it (every rank's batch fits the buckets)
     ep_ll_cap: int = 0          # tokens per rank the low-latency buckets hold
+    ep_ll_b: object | None = None   # two-batch overlap: micro-batch B's own exchange (buffers + epochs)
+    ep_ll_cur: object | None = None  # the exchange the MoE layers use right now (None: ep_ll)
     pp_prev: object | None = None   # CustomAllReduce over (previous stage, this stage): IPC hand-off
     pp_next: object | None = None   # CustomAllReduce over (this stage, next stage)
     pp_bcast: object | None = None  # CustomAllReduce over the pipeline group: sampled tokens from the last stage

@@ -8,6 +8,8 @@ sampled ids.  Prefill / mixed steps run eagerly (their GPU time dwarfs launch ov
 """
 from __future__ import annotations
 
+import contextlib
+
 import logging
 import math
 import os
@@ -161,6 +163,12 @@ class ModelRunner:
             from ome_amd.parallel.ep import attach_low_latency
 
             self.ep_ll = attach_low_latency(self.model, max(max_running, 8))
+        # two-batch overlap (--enable-two-batch-overlap) on the low-latency exchange: a decode step
+        # runs as two half batches on two streams, each through its own exchange, so one half's
+        # dispatch / combine waits overlap the other half's attention and expert GEMMs
+        self.tbo = bool(self.ep_ll and pstate.get().tbo and pstate.get().ep_ll_b is not None)
+        self._tbo_stream = torch.cuda.Stream(self.device) if self.tbo else None
+        self._tbo_keep: dict = {}
         self.stateful = bool(getattr(self.model, "stateful", False))
         if self.stateful:  # recurrent (SSM) state per request slot, the padding slot included; before
             # the KV sizing below so the page budget sees it
@@ -219,6 +227,8 @@ class ModelRunner:
         self.buckets = default_buckets(self.bmax)
         if self.buckets[-1] < self.bmax:
             self.buckets.append(self.bmax)
+        if self.tbo:   # every graph splits into two non-empty halves
+            self.buckets = [b for b in self.buckets if b >= 2 and b % 2 == 0]
         self.dbuf = _DecodeBuffers(self.bmax, self.device)
         self.out_ids = torch.zeros(self.bmax, dtype=torch.int32, device=self.device)
         self.out_lp = torch.zeros(self.bmax, dtype=torch.float32, device=self.device)
@@ -259,11 +269,13 @@ class ModelRunner:
             self.capture_graphs()
 
     # ------------------------------------------------------------------ helpers
-    def decode_ws(self, bs: int) -> ops.DecodeWorkspace | None:
-        """Split-K partitioning chosen so a decode launch has >= ~1024 active workgroups."""
+    def decode_ws(self, bs: int, half: int = 0) -> ops.DecodeWorkspace | None:
+        """Split-K partitioning chosen so a decode launch has >= ~1024 active workgroups.
+        ``half``: the two-batch-overlap halves run concurrently, so each owns a workspace."""
         if getattr(self.model, "kv_layout", None) is not None:
             return None  # MLA models carry their own workspace
-        ws = self._ws_cache.get(bs)
+        key = bs if not half else (bs, half)
+        ws = self._ws_cache.get(key)
         if ws is None:
             hkv = self.model.tp.hkv
             parts = max(1, math.ceil(1024 / max(1, bs * hkv)))
@@ -275,18 +287,54 @@ class ModelRunner:
                 part = max(256, -(-span // parts))
                 part = -(-part // 128) * 128
                 ws = ops.DecodeWorkspace(bs, self.model.tp.hq, self.cfg.head_dim, span, part, self.device)
-            self._ws_cache[bs] = ws
+            self._ws_cache[key] = ws
         return ws
+
+    def _tbo_forward(self, d: "_DecodeBuffers", bs: int, bt: torch.Tensor) -> torch.Tensor:
+        """Two-batch overlap of a decode step (SGLang ``--enable-two-batch-overlap``, reference
+        deepseek-rdma-pd-rt.yaml:89): rows [0, h) run on the current stream through exchange A,
+        rows [h, bs) on a side stream through exchange B -- attention, routing, dispatch, experts
+        and combine of every layer for each half.  The halves share nothing but the (disjoint) KV
+        rows they write, so whatever one half waits on (a peer's dispatch / combine flag) the
+        other half's kernels fill.  In a captured graph both chains are replayed concurrently.
+        Every rank runs both exchanges in every step (``ep_idle_layers`` for eager steps)."""
+        st = pstate.get()
+        h = bs // 2
+        main = torch.cuda.current_stream(self.device)
+        side = self._tbo_stream
+        outs = []
+        for half, (a, b) in enumerate(((0, h), (h, bs))):
+            ctx = torch.cuda.stream(side) if half else contextlib.nullcontext()
+            if half:
+                side.wait_stream(main)
+            with ctx:
+                meta = AttnMeta("decode", d.view("pos", bs)[a:b], d.view("slots", bs)[a:b], bt[a:b],
+                                seq_lens=d.view("seq_lens", bs)[a:b], decode_ws=self.decode_ws(b - a, half),
+                                order=None)
+                st.ep_ll_cur = st.ep_ll_b if half else st.ep_ll
+                try:
+                    outs.append(self.model.forward(d.view("ids", bs)[a:b], meta, self.kv))
+                finally:
+                    st.ep_ll_cur = None
+        main.wait_stream(side)
+        if torch.cuda.is_current_stream_capturing():
+            self._tbo_keep[bs] = outs   # graph-pool memory: kept for the graph's lifetime
+        else:
+            outs[1].record_stream(main)
+        return torch.cat(outs, 0)
 
     def _decode_forward(self, bs: int, m: int = 0) -> None:
         d = self.dbufs[m]
         out_ids, out_lp = self.mb_out[m]
         bt = self.slots.table.index_select(0, d.view("req_idx", bs))
-        meta = AttnMeta("decode", d.view("pos", bs), d.view("slots", bs), bt, seq_lens=d.view("seq_lens", bs),
-                        decode_ws=self.decode_ws(bs), order=d.view("order", bs))
-        if self.stateful:  # one-row sequences continuing each request slot's state
-            meta.extra["ssm"] = (self._ssm_cu[:bs + 1], d.view("req_idx", bs), self._ssm_zero[:bs])
-        hidden = self.model.forward(d.view("ids", bs), meta, self.kv)
+        if self.tbo and bs >= 2 and not self.stateful and pstate.get().ep_ll_ok:
+            hidden = self._tbo_forward(d, bs, bt)
+        else:
+            meta = AttnMeta("decode", d.view("pos", bs), d.view("slots", bs), bt, seq_lens=d.view("seq_lens", bs),
+                            decode_ws=self.decode_ws(bs), order=d.view("order", bs))
+            if self.stateful:  # one-row sequences continuing each request slot's state
+                meta.extra["ssm"] = (self._ssm_cu[:bs + 1], d.view("req_idx", bs), self._ssm_zero[:bs])
+            hidden = self.model.forward(d.view("ids", bs), meta, self.kv)
         if hidden is not None:   # (an earlier pipeline stage returns None: it samples nothing)
             logits = self.model.compute_logits(hidden)
             pen = (d.view("rep", bs), d.view("freq", bs), d.view("pres", bs))
@@ -713,6 +761,7 @@ class ModelRunner:
                 any(chunks[i].req.mm is not None for i in pre + dec):
             embeds = self._mm_prepare(chunks, pre + dec, T, t_ids, meta)
         hidden = self.model.forward(t_ids, meta, self.kv, embeds)
+        self._tbo_idle()
         if hidden is None:  # an earlier pipeline stage: tokens arrive from the last stage
             return (torch.empty(len(chunks), dtype=torch.int32, device=self.device),
                     torch.empty(len(chunks), dtype=torch.float32, device=self.device))
@@ -812,6 +861,17 @@ class ModelRunner:
             meta.extra["ssm"] = (self._ssm_cu[:2], torch.full((1,), pad, dtype=torch.int32, device=dv),
                                  torch.ones(1, dtype=torch.int32, device=dv))
         self.model.forward(z, meta, self.kv)
+        self._tbo_idle()
+
+    def _tbo_idle(self) -> None:
+        """Two-batch overlap, eager (prefill / mixed / idle) step on the low-latency exchange: the
+        peers that decode split their rows over exchanges A and B, so this rank takes part in B's
+        exchanges too (no tokens of its own; it still computes the experts for rows sent to it)."""
+        st = pstate.get()
+        if self.tbo and st.ep_ll_ok:
+            from ome_amd.parallel.ep import ep_idle_layers
+
+            ep_idle_layers(self.model, st.ep_ll_b)
 
     def embed(self, batch: StepBatch) -> list[list[float]]:
         """Embedding models (``--is-embedding``): last-token pooling + L2 norm over full prompts

@@ -21,40 +21,46 @@ PROMPTS = [[3 + (i * 37 + j) % 1000 for j in range(5 + 7 * i)] for i in range(6)
 NEW = 10
 
 
-def _engine(path, world, quant):
+def _engine(path, world, quant, tbo=False):
     from ome_amd.runtime.engine import Engine, EngineArgs
 
-    kw = dict(tp_size=world, dp_size=world, enable_dp_attention=True) if world > 1 else {}
+    kw = dict(tp_size=world, dp_size=world, enable_dp_attention=True, enable_two_batch_overlap=tbo) \
+        if world > 1 else {}
     return Engine(EngineArgs(model_path=path, device="cuda", max_running_requests=8, context_length=256,
                              max_total_tokens=4096, mem_fraction_static=0.3, cuda_graph=True, cuda_graph_max_bs=8,
                              quantization=quant, **kw))
 
 
-def _worker(rank, world, port, path, quant, q):
+def _worker(rank, world, port, path, quant, q, tbo=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                           LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(world), OME_DIST_BACKEND="gloo", OME_TUNE_GEMM="0")
         torch.cuda.set_device(0)
         from ome_amd.runtime.request import SamplingParams
 
-        eng = _engine(path, world, quant)
+        eng = _engine(path, world, quant, tbo)
         st = eng.pstate
         assert st.ep_ll is not None and eng.runner.use_graph and eng.runner.graphs
+        assert eng.runner.tbo == tbo and (st.ep_ll_b is not None) == tbo
         if rank == 0:
             reqs = eng.generate(PROMPTS, SamplingParams(max_new_tokens=NEW, ignore_eos=True))
             owners = {r.dp_rank for r in reqs}
             eng.stop_group()
-            q.put((rank, [r.output_ids for r in reqs], owners, st.ep_ll.error(), None))
+            err = st.ep_ll.error() | (st.ep_ll_b.error() if st.ep_ll_b is not None else 0)
+            q.put((rank, [r.output_ids for r in reqs], owners, err, None))
         else:
             eng.run_forever()
-            q.put((rank, None, None, st.ep_ll.error(), None))
+            err = st.ep_ll.error() | (st.ep_ll_b.error() if st.ep_ll_b is not None else 0)
+            q.put((rank, None, None, err, None))
     except Exception:  # noqa: BLE001
         q.put((rank, None, None, None, traceback.format_exc()))
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("quant", [None, "fp8"])
-def test_dp_attention_low_latency_ep_graphs(tmp_path, quant):
+@pytest.mark.parametrize("quant,tbo", [(None, False), ("fp8", False), (None, True)])
+def test_dp_attention_low_latency_ep_graphs(tmp_path, quant, tbo):
+    """tbo: two-batch overlap -- each decode step as two half batches on two streams through two
+    exchanges (captured in the graphs), prefill / idle steps joining B's exchanges; same tokens."""
     from tests.test_moe_cpu import _export_hf
 
     hf = dict(PRESETS["tiny-moe"])
@@ -75,7 +81,7 @@ def test_dp_attention_low_latency_ep_graphs(tmp_path, quant):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     env_keep = dict(os.environ)
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), quant, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, str(tmp_path), quant, q, tbo)) for r in range(2)]
     for p in ps:
         p.start()
     res = {}
