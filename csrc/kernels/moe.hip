@@ -627,22 +627,35 @@ __global__ __launch_bounds__(256) void moe_gemm_fp8_kernel(const uint8_t* __rest
   for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the K block's fp32 scales are prefetched one step ahead (they ride the step's vmcnt(0) wait
+  // instead of adding a dependent global-load round trip to every step)
+  const float* sar[MJ];
+  float san[MJ];
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) {
+    sar[j] = sa + (int64_t)srow[j] * KB;
+    san[j] = sar[j][0];
+  }
+  float swn = swe[0];
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
-    if (t + 1 < nt) stage(cur ^ 1, t + 1);
-    const char* la = smem + cur * (ABYTES + WBYTES);
-    const char* lw = la + ABYTES;
-    const float swv = swe[t];
-    mi32x8 xa[MJ];
     float s[MJ];
 #pragma unroll
-    for (int j = 0; j < MJ; ++j) {
-      xa[j] = mfrag32(la, wm * (BMF / 2) + j * 16 + fr, fc);
-      s[j] = sa[(int64_t)srow[j] * KB + t] * swv;
+    for (int j = 0; j < MJ; ++j) s[j] = san[j] * swn;
+    if (t + 1 < nt) {
+      stage(cur ^ 1, t + 1);
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) san[j] = sar[j][t + 1];
+      swn = swe[t + 1];
     }
+    const char* la = smem + cur * (ABYTES + WBYTES);
+    const char* lw = la + ABYTES;
+    mi32x8 xa[MJ];
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) xa[j] = mfrag32(la, wm * (BMF / 2) + j * 16 + fr, fc);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const mi32x8 wf = mfrag32(lw, wn * (BNF / 2) + i * 16 + fr, fc);
@@ -675,16 +688,33 @@ __global__ __launch_bounds__(256) void moe_gemm_fp8_kernel(const uint8_t* __rest
 
 // A [rows][K] e4m3 (gathered through sorted_ids / gather_div when gather_div > 0), sa [rows][K/128];
 // W [E][N][K] e4m3, sw [E][N/128][K/128]; out [n_assign][N] bf16 in sorted order.  N % 128 == 0,
-// K % 128 == 0.  max_m_tiles: static upper bound of 64-row tiles (n_assign / 64 + E).
-OME_API int ome_moe_gemm_fp8(const void* A, int64_t lda, const float* sa, const int* sorted_ids, int gather_div,
-                             const void* W, const float* sw, const int* offsets, int E, int N, int K,
-                             int max_m_tiles, void* out, int64_t ldo, hipStream_t stream) {
+// K % 128 == 0.
+// bm = 64: 64 x 128 tiles (decode: a few rows per expert, more workgroups per weight byte);
+// bm = 128: 128 x 128 tiles, 64 x 64 per wave (prefill: twice the MFMAs per staged K block and the
+// expert's weights read once per 128 gathered rows; 64 KB of LDS, 2 workgroups per CU).
+// max_m_tiles: static upper bound of bm-row tiles (n_assign / bm + E).
+OME_API int ome_moe_gemm_fp8_tile(const void* A, int64_t lda, const float* sa, const int* sorted_ids, int gather_div,
+                                  const void* W, const float* sw, const int* offsets, int E, int N, int K,
+                                  int max_m_tiles, int bm, void* out, int64_t ldo, hipStream_t stream) {
   if (max_m_tiles <= 0) return 0;
   if (N % 128 || K % 128 || lda % 16 || ((uintptr_t)A | (uintptr_t)W) % 16) return -2;
   if (max_m_tiles > 65535) return -3;
-  dim3 grid(N / 128, max_m_tiles);
-  moe_gemm_fp8_kernel<64, 128><<<grid, 256, 0, stream>>>((const uint8_t*)A, lda, sa, sorted_ids, gather_div,
-                                                         (const uint8_t*)W, sw, offsets, E, N, K, (bf16*)out, ldo);
+  if (bm == 128) {
+    moe_gemm_fp8_kernel<128, 128><<<dim3(N / 128, max_m_tiles), 256, 0, stream>>>(
+        (const uint8_t*)A, lda, sa, sorted_ids, gather_div, (const uint8_t*)W, sw, offsets, E, N, K, (bf16*)out, ldo);
+  } else if (bm == 64) {
+    moe_gemm_fp8_kernel<64, 128><<<dim3(N / 128, max_m_tiles), 256, 0, stream>>>(
+        (const uint8_t*)A, lda, sa, sorted_ids, gather_div, (const uint8_t*)W, sw, offsets, E, N, K, (bf16*)out, ldo);
+  } else {
+    return -4;
+  }
   OME_CHECK_LAUNCH();
   return 0;
+}
+
+OME_API int ome_moe_gemm_fp8(const void* A, int64_t lda, const float* sa, const int* sorted_ids, int gather_div,
+                             const void* W, const float* sw, const int* offsets, int E, int N, int K,
+                             int max_m_tiles, void* out, int64_t ldo, hipStream_t stream) {
+  return ome_moe_gemm_fp8_tile(A, lda, sa, sorted_ids, gather_div, W, sw, offsets, E, N, K, max_m_tiles, 64, out, ldo,
+                               stream);
 }

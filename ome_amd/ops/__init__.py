@@ -387,6 +387,17 @@ def moe_tile_m(rows: int, E: int, N: int) -> int:
     return 64
 
 
+def moe_fp8_tile_m(rows: int, E: int) -> int:
+    """Row tile of the fp8 grouped GEMM: 128 (128x128 tiles) once experts average >= 192 rows, else
+    64 (64x128).  Measured (``scripts/fp8_moe_tile_bench.py``, profiles/r05_fp8_moe_tiles.md): the
+    64-row tile wins 1.3x at decode and by 4 % at 64-128 rows / expert, 128 wins 2 % at 256.
+    ``OME_MOE_FP8_TILE`` overrides."""
+    env = os.environ.get("OME_MOE_FP8_TILE")
+    if env:
+        return int(env)
+    return 128 if rows >= 192 * max(1, E) else 64
+
+
 def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
               act: int = 0, scale: float = 1.0, b13: torch.Tensor | None = None,
               b2: torch.Tensor | None = None, gated: bool = True) -> torch.Tensor:
@@ -443,15 +454,17 @@ def fused_moe_fp8(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor,
     call("ome_moe_align", topk_ids.data_ptr(), n, E, offsets.data_ptr(), sorted_ids.data_ptr(), inv.data_ptr(),
          stream_ptr())
     qx, sx = fp8_quant(x, 128)
-    tiles = -(-n // 64) + E
+    tm = moe_fp8_tile_m(n, E)
+    tiles = -(-n // tm) + E
     gu = torch.empty(n, I2, dtype=x.dtype, device=dev)
-    call("ome_moe_gemm_fp8", qx.data_ptr(), qx.stride(0), sx.data_ptr(), sorted_ids.data_ptr(), k, w13.q.data_ptr(),
-         w13.scale.data_ptr(), offsets.data_ptr(), E, I2, H, tiles, gu.data_ptr(), gu.stride(0), stream_ptr())
+    call("ome_moe_gemm_fp8_tile", qx.data_ptr(), qx.stride(0), sx.data_ptr(), sorted_ids.data_ptr(), k,
+         w13.q.data_ptr(), w13.scale.data_ptr(), offsets.data_ptr(), E, I2, H, tiles, tm, gu.data_ptr(), gu.stride(0),
+         stream_ptr())
     h = act_and_mul(gu, act)
     qh, sh = fp8_quant(h, 128)
     y = torch.empty(n, H, dtype=x.dtype, device=dev)
-    call("ome_moe_gemm_fp8", qh.data_ptr(), qh.stride(0), sh.data_ptr(), None, 0, w2.q.data_ptr(),
-         w2.scale.data_ptr(), offsets.data_ptr(), E, H, I, tiles, y.data_ptr(), y.stride(0), stream_ptr())
+    call("ome_moe_gemm_fp8_tile", qh.data_ptr(), qh.stride(0), sh.data_ptr(), None, 0, w2.q.data_ptr(),
+         w2.scale.data_ptr(), offsets.data_ptr(), E, H, I, tiles, tm, y.data_ptr(), y.stride(0), stream_ptr())
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     call("ome_moe_combine", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), float(scale),
          stream_ptr())
@@ -474,16 +487,17 @@ def moe_experts_sorted(rows: torch.Tensor, ids: torch.Tensor, w13, w2, act: int,
     y = torch.empty(n, H, dtype=rows.dtype, device=dev)
     if hasattr(w13, "scale") and hasattr(w13, "q"):
         I2 = w13.q.shape[1]
-        tiles = -(-n // 64) + n_experts
+        tm = moe_fp8_tile_m(n, n_experts)
+        tiles = -(-n // tm) + n_experts
         qx, sx = fp8_quant(rows, 128)
         gu = torch.empty(n, I2, dtype=rows.dtype, device=dev)
-        call("ome_moe_gemm_fp8", qx.data_ptr(), qx.stride(0), sx.data_ptr(), sorted_ids.data_ptr(), 1,
-             w13.q.data_ptr(), w13.scale.data_ptr(), offsets.data_ptr(), n_experts, I2, H, tiles, gu.data_ptr(),
+        call("ome_moe_gemm_fp8_tile", qx.data_ptr(), qx.stride(0), sx.data_ptr(), sorted_ids.data_ptr(), 1,
+             w13.q.data_ptr(), w13.scale.data_ptr(), offsets.data_ptr(), n_experts, I2, H, tiles, tm, gu.data_ptr(),
              gu.stride(0), stream_ptr())
         h = act_and_mul(gu, act)
         qh, sh = fp8_quant(h, 128)
-        call("ome_moe_gemm_fp8", qh.data_ptr(), qh.stride(0), sh.data_ptr(), None, 0, w2.q.data_ptr(),
-             w2.scale.data_ptr(), offsets.data_ptr(), n_experts, H, I2 // 2, tiles, y.data_ptr(), y.stride(0),
+        call("ome_moe_gemm_fp8_tile", qh.data_ptr(), qh.stride(0), sh.data_ptr(), None, 0, w2.q.data_ptr(),
+             w2.scale.data_ptr(), offsets.data_ptr(), n_experts, H, I2 // 2, tiles, tm, y.data_ptr(), y.stride(0),
              stream_ptr())
         return y, inv
     I2 = w13.shape[1]

@@ -14,7 +14,10 @@ DEV = torch.device("cuda")
 
 @pytest.mark.parametrize("T,E,k,H,I", [(1, 8, 2, 256, 128), (37, 16, 4, 1024, 512), (256, 64, 8, 1024, 256),
                                        (600, 8, 2, 512, 384)])
-def test_fused_moe_fp8_matches_emulation(T, E, k, H, I):
+@pytest.mark.parametrize("tile", ["auto", "64", "128"])
+def test_fused_moe_fp8_matches_emulation(T, E, k, H, I, tile, monkeypatch):
+    if tile != "auto":   # both row tiles of ome_moe_gemm_fp8_tile, whatever the heuristic picks
+        monkeypatch.setenv("OME_MOE_FP8_TILE", tile)
     torch.manual_seed(T + E)
     x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
     w13 = (torch.randn(E, 2 * I, H, device=DEV) * H ** -0.5).to(torch.bfloat16)
