@@ -251,10 +251,10 @@ class ModelRunner:
         # (pstate.pp_graph_ok: one node); across nodes they run eagerly over RCCL p2p.  DP
         # attention replays graphs only with the low-latency EP exchange (cuda_graph=None: "if possible")
         dp_ok = pstate.get().ep_size <= 1 or self.ep_ll
-        # opt-in (OME_PP_GRAPHS=1): on the one-GPU rehearsal (both stages sharing GPU 0) the eager
-        # micro-batched steps measured faster (profiles/r04_pp2_rehearsal.txt); distinct-GPU
-        # pipelines are unmeasured
-        pp_ok = not self.pp or (pstate.pp_graph_ok() and os.environ.get("OME_PP_GRAPHS", "0") == "1"
+        # on by default since round 5 (OME_PP_GRAPHS=0: eager micro-batched steps): the r04
+        # rehearsal's 25 % graph regression is gone -- graphs 10.24k vs eager 10.17k tok/s,
+        # decode steps 15.9 vs 16.9 ms, interleaved on one GPU (profiles/r05_pp_graphs.md)
+        pp_ok = not self.pp or (pstate.pp_graph_ok() and os.environ.get("OME_PP_GRAPHS", "1") == "1"
                                 and not self.stateful)
         self.use_graph = bool(cuda_graph) and self.is_cuda and pp_ok and dp_ok and \
             not getattr(self.model, "encoder_only", False)
