@@ -48,6 +48,22 @@ __device__ __forceinline__ bf16x8 pp_frag(const char* img, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(img + row * 128 + pp_swz(row, chunk) * 16);
 }
 
+// id -> (m tile, n tile).  gm = 0: m fastest over the whole M extent.  gm > 0: groups of gm m-tiles,
+// m fastest inside a group, so the ~32 tiles an XCD runs at once span gm m-panels x 32 / gm
+// n-panels (12 distinct panels at gm = 8 instead of 1 W + 32 X panels at M = 8192): fewer L2
+// misses per K step.
+__device__ __forceinline__ void pp_tile(int id, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  if (gm <= 0 || gm >= tiles_m) {
+    tn = id / tiles_m;
+    tm = id - tn * tiles_m;
+    return;
+  }
+  const int per = gm * tiles_n, g = id / per, first = g * gm, r = id - g * per;
+  const int h = min(tiles_m - first, gm);
+  tm = first + r % h;
+  tn = r / h;
+}
+
 __device__ __forceinline__ float pp_silu(float x) { return x / (1.f + __expf(-x)); }
 
 // s_waitcnt lgkmcnt(0) (vmcnt / expcnt left at their maxima), then the barrier; the compiler
@@ -68,7 +84,8 @@ __global__ __launch_bounds__(PP_NT, 1) void gemm_pp_kernel(const bf16* __restric
                                                            const bf16* __restrict__ W, int64_t ldw,
                                                            const bf16* __restrict__ bias,
                                                            const bf16* __restrict__ res, int64_t ldr,
-                                                           bf16* __restrict__ out, int64_t ldo, int M, int N, int kt) {
+                                                           bf16* __restrict__ out, int64_t ldo, int M, int N, int kt,
+                                                           int gm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -79,7 +96,8 @@ __global__ __launch_bounds__(PP_NT, 1) void gemm_pp_kernel(const bf16* __restric
   const int tiles_m = (M + 255) >> 8, T = tiles_m * (N >> 8);
   const int b = blockIdx.x, xcd = b & 7, q8 = T >> 3, r8 = T & 7;
   const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int tn = id / tiles_m, tm = id - tn * tiles_m;
+  int tm, tn;
+  pp_tile(id, tiles_m, N >> 8, gm, tm, tn);
   const int m0 = tm << 8, n0 = tn << 8;
 
   // ---- staging: group 0 -> W image, group 1 -> X image, 8 pieces of 8 rows x 128 B per wave and
@@ -283,7 +301,8 @@ __global__ __launch_bounds__(PP_NT, 1) void gemm_pp32_kernel(const bf16* __restr
                                                              const bf16* __restrict__ W, int64_t ldw,
                                                              const bf16* __restrict__ bias,
                                                              const bf16* __restrict__ res, int64_t ldr,
-                                                             bf16* __restrict__ out, int64_t ldo, int M, int N, int kt) {
+                                                             bf16* __restrict__ out, int64_t ldo, int M, int N, int kt,
+                                                             int gm) {
   constexpr int IMG = 256 * 64, STG = 2 * IMG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -294,7 +313,8 @@ __global__ __launch_bounds__(PP_NT, 1) void gemm_pp32_kernel(const bf16* __restr
   const int tiles_m = (M + 255) >> 8, T = tiles_m * (N >> 8);
   const int b = blockIdx.x, xcd = b & 7, q8 = T >> 3, r8 = T & 7;
   const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
-  const int tn = id / tiles_m, tm = id - tn * tiles_m;
+  int tm, tn;
+  pp_tile(id, tiles_m, N >> 8, gm, tm, tn);
   const int m0 = tm << 8, n0 = tn << 8;
 
   // staging: group 0 -> W image, group 1 -> X image; piece p of wave wi = image rows
@@ -411,6 +431,12 @@ __global__ __launch_bounds__(PP_NT, 1) void gemm_pp32_kernel(const bf16* __restr
   if (g == 0) pp_bar();
 }
 
+// tile-group height (OME_PP_GM, default 4; 0 = m fastest over all of M)
+static int pp_gm() {
+  static const int gm = getenv("OME_PP_GM") ? atoi(getenv("OME_PP_GM")) : 4;
+  return gm;
+}
+
 template <int EPI, bool BIAS, int NB, int PROBE = 0>
 int launch_pp32(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw, const bf16* bias, const bf16* res,
                 int64_t ldr, bf16* out, int64_t ldo, int M, int N, int K, hipStream_t stream) {
@@ -425,7 +451,7 @@ int launch_pp32(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw, const bf
   }
   const int T = ((M + 255) / 256) * (N / 256);
   gemm_pp32_kernel<EPI, BIAS, NB, PROBE><<<T, PP_NT, LDS, stream>>>(X, ldx, W, ldw, bias, res, ldr, out, ldo, M, N,
-                                                                     K / 32);
+                                                                     K / 32, pp_gm());
   return (int)hipGetLastError();
 }
 
@@ -441,7 +467,7 @@ int launch_pp(const bf16* X, int64_t ldx, const bf16* W, int64_t ldw, const bf16
     attr = true;
   }
   const int T = ((M + 255) / 256) * (N / 256);
-  gemm_pp_kernel<EPI, BIAS, PROBE><<<T, PP_NT, LDS, stream>>>(X, ldx, W, ldw, bias, res, ldr, out, ldo, M, N, K / 64);
+  gemm_pp_kernel<EPI, BIAS, PROBE><<<T, PP_NT, LDS, stream>>>(X, ldx, W, ldw, bias, res, ldr, out, ldo, M, N, K / 64, pp_gm());
   return (int)hipGetLastError();
 }
 
