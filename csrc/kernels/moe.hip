@@ -540,15 +540,24 @@ __device__ __forceinline__ mi32x8 mfrag32(const char* lds, int row, int c) {
   return mi32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-template <int BMF, int BNF>
+// NST LDS stages: 2 = one K block in flight during compute, waited with vmcnt(0) at the next
+// step; 3 = the block two steps ahead in flight across the barrier (counted vmcnt + raw s_barrier,
+// cdna_hip_programming.md "Pipelining across barriers"), at 1.5x the LDS.  All LDS is one array
+// (the tile descriptor at its end): a second __shared__ object can make hipcc drain vmcnt before
+// every K step's first LDS read.
+template <int BMF, int BNF, int NST = 2>
 __global__ __launch_bounds__(256) void moe_gemm_fp8_kernel(const uint8_t* __restrict__ A, int64_t lda,
                                                            const float* __restrict__ sa, const int* __restrict__ sorted_ids,
                                                            int gather_div, const uint8_t* __restrict__ W,
                                                            const float* __restrict__ sw, const int* __restrict__ offsets,
                                                            int E, int N, int K, bf16* __restrict__ out, int64_t ldo) {
   constexpr int ABYTES = BMF * 128, WBYTES = BNF * 128;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (ABYTES + WBYTES)];
-  __shared__ int s_tile[3];
+  static_assert(NST == 2 || NST == 3, "NST");
+  // NST == 3 stages also carry the K block's A-row scales (4 x 256 B, one 4-byte DMA per wave):
+  // an ordinary VGPR load beside the DMA makes hipcc wait vmcnt(0) and drain the ring
+  constexpr int SCB = NST == 3 ? 1024 : 0, STG = ABYTES + WBYTES + SCB;
+  __shared__ __attribute__((aligned(16))) char smem[NST * STG + 16];
+  int* s_tile = reinterpret_cast<int*>(smem + NST * STG);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (tid == 0) s_tile[0] = -1;
   __syncthreads();
@@ -600,9 +609,18 @@ __global__ __launch_bounds__(256) void moe_gemm_fp8_kernel(const uint8_t* __rest
     const int n = min(n0 + r, N - 1);
     wsrc[j] = We + (int64_t)n * K + mswz(r, lane & 7) * 16;
   }
+  const float* scsrc = sa;   // NST == 3: this lane's A-row scale source (row wave*BMF/4 + lane, clamped)
+  if constexpr (NST == 3) {
+    const int r = wave * (BMF / 4) + min(lane, BMF / 4 - 1);
+    int p = m0 + r;
+    p = p < m_end ? p : m_end - 1;
+    scsrc = sa + (int64_t)(gather_div > 0 ? sorted_ids[p] / gather_div : p) * (K / 128);
+  }
   auto stage = [&](int buf, int kt) {
-    char* la = smem + buf * (ABYTES + WBYTES);
+    char* la = smem + buf * STG;
     char* lw = la + ABYTES;
+    if constexpr (NST == 3)
+      __builtin_amdgcn_global_load_lds((moe_glb_t*)(scsrc + kt), (moe_lds_t*)(lw + WBYTES + wave * 256), 4, 0, 0);
 #pragma unroll
     for (int j = 0; j < AI; ++j)
       __builtin_amdgcn_global_load_lds((moe_glb_t*)(asrc[j] + kt * 128), (moe_lds_t*)(la + (wave * AI + j) * 1024), 16,
@@ -631,27 +649,57 @@ __global__ __launch_bounds__(256) void moe_gemm_fp8_kernel(const uint8_t* __rest
   // instead of adding a dependent global-load round trip to every step)
   const float* sar[MJ];
   float san[MJ];
+  float swn = 0.f;
+  if constexpr (NST == 2) {
 #pragma unroll
-  for (int j = 0; j < MJ; ++j) {
-    sar[j] = sa + (int64_t)srow[j] * KB;
-    san[j] = sar[j][0];
-  }
-  float swn = swe[0];
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    float s[MJ];
-#pragma unroll
-    for (int j = 0; j < MJ; ++j) s[j] = san[j] * swn;
-    if (t + 1 < nt) {
-      stage(cur ^ 1, t + 1);
-#pragma unroll
-      for (int j = 0; j < MJ; ++j) san[j] = sar[j][t + 1];
-      swn = swe[t + 1];
+    for (int j = 0; j < MJ; ++j) {
+      sar[j] = sa + (int64_t)srow[j] * KB;
+      san[j] = sar[j][0];
     }
-    const char* la = smem + cur * (ABYTES + WBYTES);
+    swn = swe[0];
+  }
+  constexpr int NL = AI + WI + (NST == 3);   // LDS-DMA instructions per thread per K block
+  if constexpr (NST == 2) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    // blocks 0 and 1 in flight; the top of step t waits for block t with block t + 1 still out
+    stage(0, 0);
+    stage(1, min(1, nt - 1));
+  }
+  for (int t = 0; t < nt; ++t) {
+    const int cur = NST == 2 ? (t & 1) : t % 3;
+    if constexpr (NST == 3) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NL) : "memory");   // block t + 1 (maybe a clamped copy) stays out
+      __builtin_amdgcn_s_barrier();   // every wave's block t landed; every wave done reading block t - 1
+    }
+    float s[MJ];
+    if constexpr (NST == 3) {
+      const char* lsc = smem + cur * STG + ABYTES + WBYTES;
+      const float swv = swe[t];
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        const int r = wm * (BMF / 2) + j * 16 + fr;
+        s[j] = *reinterpret_cast<const float*>(lsc + (r / (BMF / 4)) * 256 + (r % (BMF / 4)) * 4) * swv;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) s[j] = san[j] * swn;
+    }
+    if constexpr (NST == 2) {
+      if (t + 1 < nt) {
+#pragma unroll
+        for (int j = 0; j < MJ; ++j) san[j] = sar[j][t + 1];
+        swn = swe[t + 1];
+        stage(cur ^ 1, t + 1);
+      }
+    } else {
+      // branch-free: the DMA of block t + 2 (into the buffer block t - 1 left) is issued every
+      // step, clamped to the last block past the end, so the counted wait above stays exact
+      stage((t + 2) % 3, min(t + 2, nt - 1));
+    }
+    const char* la = smem + cur * STG;
     const char* lw = la + ABYTES;
     mi32x8 xa[MJ];
 #pragma unroll
@@ -666,9 +714,12 @@ __global__ __launch_bounds__(256) void moe_gemm_fp8_kernel(const uint8_t* __rest
         acc[i][j] += p * s[j];
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (NST == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
+  if constexpr (NST == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // clamped tail DMA retires before exit
   // lane (fr, fc) of block (i, j): row p = m0 + wm*BMF/2 + j*16 + fr, cols n = n0 + wn*BNF/2 + i*16 + 4fc .. +3
 #pragma unroll
   for (int j = 0; j < MJ; ++j) {
@@ -699,15 +750,22 @@ OME_API int ome_moe_gemm_fp8_tile(const void* A, int64_t lda, const float* sa, c
   if (max_m_tiles <= 0) return 0;
   if (N % 128 || K % 128 || lda % 16 || ((uintptr_t)A | (uintptr_t)W) % 16) return -2;
   if (max_m_tiles > 65535) return -3;
+  // LDS stages (OME_MOE_FP8_NST): 3 for the 64-row tile (2 workgroups / CU, 2-5 % faster at
+  // prefill sizes), 2 for the 128-row tile (3 stages = 96 KB would leave one workgroup per CU);
+  // profiles/r05_fp8_moe_tiles.md
+  static const int nst_env = getenv("OME_MOE_FP8_NST") ? atoi(getenv("OME_MOE_FP8_NST")) : 0;
+  const int nst = nst_env ? nst_env : (bm == 64 ? 3 : 2);
+#define MOE_FP8(BM, NS)                                                                                          \
+  moe_gemm_fp8_kernel<BM, 128, NS><<<dim3(N / 128, max_m_tiles), 256, 0, stream>>>(                               \
+      (const uint8_t*)A, lda, sa, sorted_ids, gather_div, (const uint8_t*)W, sw, offsets, E, N, K, (bf16*)out, ldo)
   if (bm == 128) {
-    moe_gemm_fp8_kernel<128, 128><<<dim3(N / 128, max_m_tiles), 256, 0, stream>>>(
-        (const uint8_t*)A, lda, sa, sorted_ids, gather_div, (const uint8_t*)W, sw, offsets, E, N, K, (bf16*)out, ldo);
+    if (nst == 3) MOE_FP8(128, 3); else MOE_FP8(128, 2);
   } else if (bm == 64) {
-    moe_gemm_fp8_kernel<64, 128><<<dim3(N / 128, max_m_tiles), 256, 0, stream>>>(
-        (const uint8_t*)A, lda, sa, sorted_ids, gather_div, (const uint8_t*)W, sw, offsets, E, N, K, (bf16*)out, ldo);
+    if (nst == 3) MOE_FP8(64, 3); else MOE_FP8(64, 2);
   } else {
     return -4;
   }
+#undef MOE_FP8
   OME_CHECK_LAUNCH();
   return 0;
 }

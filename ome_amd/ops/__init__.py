@@ -388,14 +388,14 @@ def moe_tile_m(rows: int, E: int, N: int) -> int:
 
 
 def moe_fp8_tile_m(rows: int, E: int) -> int:
-    """Row tile of the fp8 grouped GEMM: 128 (128x128 tiles) once experts average >= 192 rows, else
-    64 (64x128).  Measured (``scripts/fp8_moe_tile_bench.py``, profiles/r05_fp8_moe_tiles.md): the
-    64-row tile wins 1.3x at decode and by 4 % at 64-128 rows / expert, 128 wins 2 % at 256.
-    ``OME_MOE_FP8_TILE`` overrides."""
+    """Row tile of the fp8 grouped GEMM: 64 (64x128 tiles, 3-stage LDS ring) at every size, or
+    128 (128x128, 2 stages) via ``OME_MOE_FP8_TILE=128``.  Measured (``scripts/fp8_moe_tile_bench.py``,
+    profiles/r05_fp8_moe_tiles.md): the 64-row tile wins 1.25-1.5x at decode and ties or wins at
+    prefill (256 rows / expert: 6.90 vs 6.97 ms)."""
     env = os.environ.get("OME_MOE_FP8_TILE")
     if env:
         return int(env)
-    return 128 if rows >= 192 * max(1, E) else 64
+    return 64
 
 
 def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
