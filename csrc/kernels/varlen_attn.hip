@@ -31,8 +31,12 @@ __device__ __forceinline__ float va_exp2(float x) { return __builtin_amdgcn_exp2
 // and 16+4g..16+4g+3 (X = 1) as slots 8g..8g+7
 __device__ __forceinline__ int va_slot(int kk) { return 8 * ((kk & 15) >> 2) + (kk & 3) + ((kk >> 4) << 2); }
 
-template <int DP>
-__global__ __launch_bounds__(256) void varlen_attn_kernel(
+// FAST (bidirectional, DP == 128: the long joint sequences of the Qwen-Image MMDiT, ViT-bigG):
+// the paged prefill's fast softmax (attention.hip) -- only the last tile masks (a wave-uniform
+// branch), the scale folds into the exp2 FMA, per-lane partial row sums (reduced once at the
+// end), and O / l are rescaled lazily, only when some row's running max grew by more than 2^8.
+template <int DP, bool FAST = false, int SUB = 1>
+__global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k, int64_t k_stride,
     const bf16* __restrict__ v, int64_t v_stride, const int* __restrict__ cu, const int* __restrict__ cuk,
     const int2* __restrict__ items, bf16* __restrict__ out, int64_t o_stride, int Hq, int Hkv, int D,
@@ -42,7 +46,8 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
   constexpr int NCH = (KCH + 255) / 256;              // K chunks per thread per subtile
   constexpr int VG = 8 * CPR;                         // V groups (4 keys x 8 dims) per subtile
   constexpr int NVG = (VG + 255) / 256;
-  constexpr int SUB = 1;                              // 32-key subtiles per pipeline stage (2: -20 % at D 128, occupancy)
+  // SUB: 32-key subtiles per pipeline stage (one barrier per stage); 2 measured -20 % on the
+  // generic body at D 128, the FAST body is re-measured in profiles/r05_varlen_attn.md
   constexpr int KT = 32 * KLD, VT = DP * VLD;         // elements per subtile image
   __shared__ __attribute__((aligned(16))) bf16 smem[2 * SUB * (KT + VT)];
   bf16* sK = smem;                      // [2][SUB][32 * KLD]
@@ -160,6 +165,62 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
           sc[rb][1] = va_mfma(a1, qf[rb][ks], sc[rb][1]);
         }
       }
+      if constexpr (FAST) {
+        if (kb + 32 > Lk) {   // the sequence's last tile (wave-uniform)
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int X = 0; X < 2; ++X)
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                if (kb + 16 * X + 4 * g + i >= Lk) sc[rb][X][i] = VA_NEG_INF;
+        }
+        float mt[2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          float v = VA_NEG_INF;
+#pragma unroll
+          for (int X = 0; X < 2; ++X)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v = fmaxf(v, sc[rb][X][i]);
+          v = fmaxf(v, __shfl_xor(v, 16));
+          mt[rb] = fmaxf(v, __shfl_xor(v, 32)) * scale_log2;
+        }
+        if (__ballot(mt[0] > m_i[0] + 8.f || mt[1] > m_i[1] + 8.f) != 0) {
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            const float m_new = fmaxf(m_i[rb], mt[rb]);
+            const float alpha = va_exp2(m_i[rb] - m_new);   // m_new is finite: key 0 of the first tile is real
+            l_i[rb] *= alpha;
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) o[rb][nb] = o[rb][nb] * alpha;
+            m_i[rb] = m_new;
+          }
+        }
+        bf16x8 pb[2];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) {
+          float rs = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float p0 = va_exp2(__builtin_fmaf(sc[rb][0][i], scale_log2, -m_i[rb]));
+            const float p1 = va_exp2(__builtin_fmaf(sc[rb][1][i], scale_log2, -m_i[rb]));
+            pb[rb][i] = (bf16)p0;
+            pb[rb][4 + i] = (bf16)p1;
+            rs += p0 + p1;
+          }
+          l_i[rb] += rs;   // this lane's partial row sum
+        }
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&Vt[(16 * nb + n) * VLD + 8 * g]);
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) o[rb][nb] = va_mfma(a, pb[rb], o[rb][nb]);
+        }
+        continue;
+      }
       const bool need_mask = kb + 32 > Lk || (causal && kb + 32 > r0 + 1);
       bf16x8 pb[2];
       float alpha[2];
@@ -213,6 +274,13 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
     buf ^= 1;
   }
   if (!active) return;
+  if constexpr (FAST) {   // the row's 4 lanes' partial sums
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      l_i[rb] += __shfl_xor(l_i[rb], 16);
+      l_i[rb] += __shfl_xor(l_i[rb], 32);
+    }
+  }
   // ---- epilogue: O^T accumulators hold O[row n][dims 16nb + 4g .. +3] ----
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb) {
@@ -231,6 +299,11 @@ __global__ __launch_bounds__(256) void varlen_attn_kernel(
       }
     }
   }
+}
+
+int getenv_int(const char* name, int dflt) {
+  static const char* v = getenv(name);   // read once: one variable per call site here
+  return v ? atoi(v) : dflt;
 }
 
 }  // namespace
@@ -255,9 +328,22 @@ OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k,
 #define ARGS                                                                                                  \
   (const bf16*)q, q_stride, (const bf16*)k, k_stride, (const bf16*)v, v_stride, cu, cuk, (const int2*)items,  \
       (bf16*)out, o_stride, Hq, Hkv, D, sl2, causal
-  if (D <= 64) varlen_attn_kernel<64><<<grid, 256, 0, stream>>>(ARGS);
-  else if (D <= 96) varlen_attn_kernel<96><<<grid, 256, 0, stream>>>(ARGS);
-  else varlen_attn_kernel<128><<<grid, 256, 0, stream>>>(ARGS);
+  // bidirectional calls take the FAST body (OME_VARLEN_FAST=0: generic); D 128 with 64-key
+  // stages (OME_VARLEN_SUB=1: 32) -- profiles/r05_varlen_attn.md
+  const bool fast = !causal && getenv_int("OME_VARLEN_FAST", 1);
+  static const int sub = getenv("OME_VARLEN_SUB") ? atoi(getenv("OME_VARLEN_SUB")) : 2;
+  if (D <= 64) {
+    if (fast) varlen_attn_kernel<64, true><<<grid, 256, 0, stream>>>(ARGS);
+    else varlen_attn_kernel<64><<<grid, 256, 0, stream>>>(ARGS);
+  } else if (D <= 96) {
+    if (fast) varlen_attn_kernel<96, true><<<grid, 256, 0, stream>>>(ARGS);
+    else varlen_attn_kernel<96><<<grid, 256, 0, stream>>>(ARGS);
+  } else if (fast) {
+    if (sub == 2) varlen_attn_kernel<128, true, 2><<<grid, 256, 0, stream>>>(ARGS);
+    else varlen_attn_kernel<128, true, 1><<<grid, 256, 0, stream>>>(ARGS);
+  } else {
+    varlen_attn_kernel<128><<<grid, 256, 0, stream>>>(ARGS);
+  }
 #undef ARGS
   OME_CHECK_LAUNCH();
   return 0;

@@ -33,7 +33,7 @@ def sdpa(q, k, v, lens, scale):
 
 CASES = [("bert-large b32x512", [512] * 32, 16, 64), ("bert mixed lens", [37, 512, 128, 300, 9, 480] * 8, 16, 64),
          ("vit 4 images 1024p D80", [1024] * 4, 16, 80), ("vit 1 image 4096p D80", [4096], 16, 80),
-         ("long 8k D128", [8192], 32, 128)]
+         ("long 8k D128", [8192], 32, 128), ("qwen-image joint 2x4200 D128", [4200, 4200], 24, 128)]
 for name, lens, H, D in CASES:
     T = sum(lens)
     torch.manual_seed(0)
