@@ -488,9 +488,11 @@ OME_API int ome_moe_gemm(const void* A, int64_t lda, const int* sorted_ids, int 
 // ------------------------------------------------------------------------------------------
 // combine
 // ------------------------------------------------------------------------------------------
+// add (optional, may alias out): out = add + scale * sum -- an always-on shared expert's output
+// folded into the combine instead of a separate elementwise add
 __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict__ Y, const float* __restrict__ w,
                                                           const int* __restrict__ inv, int k, int H,
-                                                          bf16* __restrict__ out, float scale) {
+                                                          bf16* out, const bf16* add, float scale) {
   const int t = blockIdx.x;
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -501,19 +503,30 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(const bf16* __restrict
       for (int q = 0; q < 8; ++q) acc[q] += wj * (float)y[q];
     }
     bf16x8 o;
+    if (add != nullptr) {
+      const bf16x8 a = ld8(add + (int64_t)t * H + c * 8);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] = (bf16)(acc[q] * scale);
+      for (int q = 0; q < 8; ++q) o[q] = (bf16)((float)a[q] + acc[q] * scale);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = (bf16)(acc[q] * scale);
+    }
     st8(out + (int64_t)t * H + c * 8, o);
   }
 }
 
-OME_API int ome_moe_combine(const void* Y, const float* w, const int* inv, int n_tok, int k, int H, void* out,
-                            float scale, hipStream_t stream) {
+OME_API int ome_moe_combine_add(const void* Y, const float* w, const int* inv, int n_tok, int k, int H, void* out,
+                                const void* add, float scale, hipStream_t stream) {
   if (n_tok <= 0) return 0;
   if (H % 8) return -2;
-  moe_combine_kernel<<<n_tok, 256, 0, stream>>>((const bf16*)Y, w, inv, k, H, (bf16*)out, scale);
+  moe_combine_kernel<<<n_tok, 256, 0, stream>>>((const bf16*)Y, w, inv, k, H, (bf16*)out, (const bf16*)add, scale);
   OME_CHECK_LAUNCH();
   return 0;
+}
+
+OME_API int ome_moe_combine(const void* Y, const float* w, const int* inv, int n_tok, int k, int H, void* out,
+                            float scale, hipStream_t stream) {
+  return ome_moe_combine_add(Y, w, inv, n_tok, k, H, out, nullptr, scale, stream);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -171,8 +171,10 @@ class DecoderMoEForCausalLM(DecoderForCausalLM):
             from ome_amd.parallel.ep import moe_ep
 
             out = moe_ep(x, tw, tid, self.w13[i], self.w2[i], self.act, 1.0, self.E)
-        else:
-            out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act)
-        if self.w_sgu[i] is not None:
-            out = out + linear(ops.act_and_mul(linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
-        return out
+            if self.w_sgu[i] is not None:
+                out = out + linear(ops.act_and_mul(linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
+            return out
+        sh = None
+        if self.w_sgu[i] is not None:   # the routed sum lands on the shared expert's output in the combine
+            sh = linear(ops.act_and_mul(linear(x, self.w_sgu[i]), self.act), self.w_sd[i]).contiguous()
+        return ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, add=sh)

@@ -331,7 +331,8 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         # (padding rows carry slot -1: parked in the scratch page 0)
         ops.mla_prep(a, self.qlr, lat, self.rope, self.kva_ln[i], self.eps, meta.positions, self.cos_sin, meta.slots,
                      flat, q, self.nope, q_full)
-        q_nope = q[..., : self.nope].transpose(0, 1).contiguous()         # [Hl, T, nope]
+        # strided batched GEMMs read the head-major views in place (no transpose copies)
+        q_nope = q[..., : self.nope].transpose(0, 1)                       # [Hl, T, nope] view
         q_full[:, :, :lat].copy_(torch.bmm(q_nope, self.w_uk[i]).transpose(0, 1))
         o_lat = torch.empty(T, Hl, lat, dtype=x.dtype, device=x.device)
         ws = None
@@ -345,7 +346,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         cache3 = cache.view(cache.shape[0], -1, lat + self.rope)
         for s, e, bt, rows, lens in self._token_rows(meta, T):
             ops.mla_attn(q_full[s:e], cache3, bt, rows, lens, self.scale, ws, out=o_lat[s:e], dv=lat)
-        o = torch.bmm(o_lat.transpose(0, 1).contiguous(), self.w_uv[i])   # [Hl, T, vd]
+        o = torch.bmm(o_lat.transpose(0, 1), self.w_uv[i])   # [Hl, T, vd]
         o = o.transpose(0, 1).reshape(T, Hl * self.vd)
         return pstate.tp_all_reduce(linear(o, self.w_o[i]))
 
@@ -365,10 +366,13 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                 self.eplb.record(i, tid)
                 tables = self.eplb.tables[i]
             out = moe_ep(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale, self.E, tables)
+            if self.w_sgu[i] is not None:
+                out = out + linear(ops.act_and_mul(linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
+        elif self.w_sgu[i] is not None:   # shared experts first; the routed sum lands on them in the combine
+            sh = linear(ops.act_and_mul(linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
+            out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale, add=sh.contiguous())
         else:
             out = ops.fused_moe(x, tw, tid, self.w13[i], self.w2[i], self.act, self.routed_scale)
-        if self.w_sgu[i] is not None:
-            out = out + linear(ops.act_and_mul(linear(x, self.w_sgu[i]), self.act), self.w_sd[i])
         return pstate.tp_all_reduce(out)
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: PagedKVCache,

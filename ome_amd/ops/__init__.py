@@ -400,15 +400,18 @@ def moe_fp8_tile_m(rows: int, E: int) -> int:
 
 def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
               act: int = 0, scale: float = 1.0, b13: torch.Tensor | None = None,
-              b2: torch.Tensor | None = None, gated: bool = True) -> torch.Tensor:
+              b2: torch.Tensor | None = None, gated: bool = True, add: torch.Tensor | None = None) -> torch.Tensor:
     """Sparse MoE MLP on MFMA: align (counting sort by expert, on device) -> grouped GEMM gate_up
     with gathered A rows -> SiLU*mul -> grouped GEMM down -> weighted combine.  Shapes are
     static given T (graph-capturable); per-expert counts never leave the GPU.  ``gated=False``:
-    w13 holds only up rows [E, I, H] and the activation is applied in place (NemotronH ReLU^2)."""
+    w13 holds only up rows [E, I, H] and the activation is applied in place (NemotronH ReLU^2).
+    ``add`` [T, H] (an always-on shared expert's output): returned as add + MoE, summed inside
+    the combine kernel (written into ``add`` itself)."""
     if hasattr(w13, "scale") and hasattr(w13, "q"):   # Fp8Experts (models/quant.py)
-        return fused_moe_fp8(x, topk_w, topk_ids, w13, w2, act, scale)
+        return fused_moe_fp8(x, topk_w, topk_ids, w13, w2, act, scale, add=add)
     if not _gpu(x):
-        return ref.fused_moe(x, topk_w, topk_ids, w13, w2, act, scale, b13, b2, gated)
+        y = ref.fused_moe(x, topk_w, topk_ids, w13, w2, act, scale, b13, b2, gated)
+        return y if add is None else add.copy_((add.float() + y.float()).to(add.dtype))
     T, H = x.shape
     E, I2, _ = w13.shape
     I = I2 // 2 if gated else I2
@@ -429,19 +432,26 @@ def fused_moe(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13
     tm = moe_tile_m(n, E, H)
     call("ome_moe_gemm", h.data_ptr(), h.stride(0), None, 0, w2.data_ptr(), offsets.data_ptr(), E, H, I,
          -(-n // tm) + E, y.data_ptr(), y.stride(0), ptr(b2), tm, stream_ptr())
-    out = torch.empty(T, H, dtype=x.dtype, device=dev)
-    call("ome_moe_combine", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), float(scale),
-         stream_ptr())
+    return _combine(y, topk_w, inv, T, k, H, scale, add)
+
+
+def _combine(y, topk_w, inv, T, k, H, scale, add):
+    if add is not None:
+        assert add.shape == (T, H) and add.is_contiguous() and add.dtype == y.dtype
+    out = add if add is not None else torch.empty(T, H, dtype=y.dtype, device=y.device)
+    call("ome_moe_combine_add", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), ptr(add),
+         float(scale), stream_ptr())
     return out
 
 
 def fused_moe_fp8(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13, w2, act: int = 0,
-                  scale: float = 1.0) -> torch.Tensor:
+                  scale: float = 1.0, add: torch.Tensor | None = None) -> torch.Tensor:
     """FP8 experts (``Fp8Experts``: e4m3 + 128x128 block scales): the token rows are quantised once
     (1x128 groups) and gathered by the grouped GEMM, the SiLU*mul output re-quantised for the down
     projection; both grouped GEMMs are ``ome_moe_gemm_fp8`` (experts never leave fp8)."""
     if not _gpu(x):
-        return ref.fused_moe_fp8(x, topk_w, topk_ids, w13.q, w13.scale, w2.q, w2.scale, act, scale, w13.block)
+        y = ref.fused_moe_fp8(x, topk_w, topk_ids, w13.q, w13.scale, w2.q, w2.scale, act, scale, w13.block)
+        return y if add is None else add.copy_((add.float() + y.float()).to(add.dtype))
     T, H = x.shape
     E, I2, _ = w13.q.shape
     I = I2 // 2
@@ -465,10 +475,7 @@ def fused_moe_fp8(x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor,
     y = torch.empty(n, H, dtype=x.dtype, device=dev)
     call("ome_moe_gemm_fp8_tile", qh.data_ptr(), qh.stride(0), sh.data_ptr(), None, 0, w2.q.data_ptr(),
          w2.scale.data_ptr(), offsets.data_ptr(), E, H, I, tiles, tm, y.data_ptr(), y.stride(0), stream_ptr())
-    out = torch.empty(T, H, dtype=x.dtype, device=dev)
-    call("ome_moe_combine", y.data_ptr(), topk_w.data_ptr(), inv.data_ptr(), T, k, H, out.data_ptr(), float(scale),
-         stream_ptr())
-    return out
+    return _combine(y, topk_w, inv, T, k, H, scale, add)
 
 
 def moe_experts_sorted(rows: torch.Tensor, ids: torch.Tensor, w13, w2, act: int, n_experts: int):

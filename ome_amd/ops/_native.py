@@ -56,6 +56,7 @@ _SIGNATURES = {
         "ome_moe_gemm_fp8": [vp, i64, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp, i64, vp],
         "ome_moe_gemm_fp8_tile": [vp, i64, vp, vp, i32, vp, vp, vp, i32, i32, i32, i32, i32, vp, i64, vp],
         "ome_moe_combine": [vp, vp, vp, i32, i32, i32, vp, f32, vp],
+        "ome_moe_combine_add": [vp, vp, vp, i32, i32, i32, vp, vp, f32, vp],
         "ome_paged_decode": [vp, i64, vp, vp, vp, i32, vp, vp, i64, vp, vp, i32, i32, i32, i32, i32, i32, i32, f32,
                              i32, vp, i32, f32, f32, f32, vp, vp, vp, i64, vp],
         "ome_paged_prefill": [vp, i64, vp, vp, vp, i32, vp, vp, vp, i32, vp, i64, i32, i32, i32, i32, f32, i32,

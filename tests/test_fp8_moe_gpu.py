@@ -44,3 +44,23 @@ def test_fp8_experts_stay_fp8_in_model():
     m = build_model(cfg, DEV, torch.bfloat16, load_format="dummy", seed=1)
     assert all(isinstance(m.w13[i], Fp8Experts) and isinstance(m.w2[i], Fp8Experts) for i in m.moe_layers)
     assert m.w13[sorted(m.moe_layers)[0]].q.dtype == torch.float8_e4m3fn
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_fused_moe_combine_adds_shared_output(fp8):
+    """``add=``: the shared expert's output summed inside the combine kernel, in place."""
+    torch.manual_seed(3)
+    T, E, k, H, I = 45, 16, 4, 512, 256
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    w13 = (torch.randn(E, 2 * I, H, device=DEV) * H ** -0.5).to(torch.bfloat16)
+    w2 = (torch.randn(E, H, I, device=DEV) * I ** -0.5).to(torch.bfloat16)
+    tw, tid = ops.moe_route(torch.randn(T, E, device=DEV), k)
+    if fp8:
+        w13, w2 = quantize_experts(w13), quantize_experts(w2)
+    sh = torch.randn(T, H, device=DEV, dtype=torch.bfloat16)
+    plain = ops.fused_moe(x, tw, tid, w13, w2, 0, 2.5)
+    acc = sh.clone()
+    got = ops.fused_moe(x, tw, tid, w13, w2, 0, 2.5, add=acc)
+    assert got.data_ptr() == acc.data_ptr()
+    want = sh.float() + plain.float()
+    assert (got.float() - want).abs().max().item() <= 2e-2 * want.abs().max().item()
