@@ -35,7 +35,7 @@ __device__ __forceinline__ int va_slot(int kk) { return 8 * ((kk & 15) >> 2) + (
 // the paged prefill's fast softmax (attention.hip) -- only the last tile masks (a wave-uniform
 // branch), the scale folds into the exp2 FMA, per-lane partial row sums (reduced once at the
 // end), and O / l are rescaled lazily, only when some row's running max grew by more than 2^8.
-template <int DP, bool FAST = false, int SUB = 1>
+template <int DP, bool FAST = false, int SUB = 1, int PROBE = 0>
 __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const bf16* __restrict__ k, int64_t k_stride,
     const bf16* __restrict__ v, int64_t v_stride, const int* __restrict__ cu, const int* __restrict__ cuk,
@@ -84,9 +84,25 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
     for (int nb = 0; nb < NB; ++nb) o[rb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // K: one 16-B chunk (8 dims of one key) per slot; V: groups of 4 consecutive keys x 8 dims, so
-  // the transposed V image is written 4 keys (8 B) at a time
-  bf16x8 rk[SUB][NCH], rv[SUB][NVG][4];
+  // the transposed V image is written 4 keys (8 B) at a time.  V staging note: lane c takes key
+  // group c & 7 and dims 8 (c >> 3): a 16-lane ds_write_b64 group then spans all 8 key-group
+  // columns of two image rows (2-way on the (a/4) mod 32 store banks); with the dims across the
+  // lanes (r04) all 16 lanes hit one bank pair -- 16-way, ~30 % of the kernel
+  // (profiles/r05_varlen_attn.md, OME_VARLEN_PROBE=1).  Global reads stay 128 B per key row.
+  bf16x8 rk[SUB][NCH] = {}, rv[SUB][NVG][4] = {};
   auto load_tile = [&](int kb0) {
+    if constexpr (PROBE == 2) {   // timing probe only: no global loads (stale registers staged)
+#pragma unroll
+      for (int u = 0; u < SUB; ++u) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) asm volatile("" : "+v"(rk[u][i]));
+#pragma unroll
+        for (int i = 0; i < NVG; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(rv[u][i][j]));
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       const int kb = kb0 + 32 * u;
@@ -100,7 +116,7 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
 #pragma unroll
       for (int i = 0; i < NVG; ++i) {
         const int c = tid + 256 * i;
-        const int kq = c / CPR, d0 = (c % CPR) * 8;
+        const int kq = c & 7, d0 = (c >> 3) * 8;   // 8 key groups across lanes: see V staging note
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int key = 4 * kq + j;
@@ -123,8 +139,12 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
 #pragma unroll
       for (int i = 0; i < NVG; ++i) {
         const int c = tid + 256 * i;
+        if (PROBE == 1) {   // timing probe only (wrong results): V image writes skipped
+          asm volatile("" ::"v"(rv[u][i][0]), "v"(rv[u][i][1]), "v"(rv[u][i][2]), "v"(rv[u][i][3]));
+          continue;
+        }
         if (c < VG) {
-          const int kq = c / CPR, d0 = (c % CPR) * 8;
+          const int kq = c & 7, d0 = (c >> 3) * 8;   // 8 key groups across lanes: see V staging note
           bf16* vt = &Vs[d0 * VLD + va_slot(4 * kq)];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -339,7 +359,10 @@ OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k,
     if (fast) varlen_attn_kernel<96, true><<<grid, 256, 0, stream>>>(ARGS);
     else varlen_attn_kernel<96><<<grid, 256, 0, stream>>>(ARGS);
   } else if (fast) {
-    if (sub == 2) varlen_attn_kernel<128, true, 2><<<grid, 256, 0, stream>>>(ARGS);
+    static const int probe = getenv("OME_VARLEN_PROBE") ? atoi(getenv("OME_VARLEN_PROBE")) : 0;
+    if (probe == 1) varlen_attn_kernel<128, true, 2, 1><<<grid, 256, 0, stream>>>(ARGS);
+    else if (probe == 2) varlen_attn_kernel<128, true, 2, 2><<<grid, 256, 0, stream>>>(ARGS);
+    else if (sub == 2) varlen_attn_kernel<128, true, 2><<<grid, 256, 0, stream>>>(ARGS);
     else varlen_attn_kernel<128, true, 1><<<grid, 256, 0, stream>>>(ARGS);
   } else {
     varlen_attn_kernel<128><<<grid, 256, 0, stream>>>(ARGS);
