@@ -89,18 +89,26 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
   // columns of two image rows (2-way on the (a/4) mod 32 store banks); with the dims across the
   // lanes (r04) all 16 lanes hit one bank pair -- 16-way, ~30 % of the kernel
   // (profiles/r05_varlen_attn.md, OME_VARLEN_PROBE=1).  Global reads stay 128 B per key row.
-  bf16x8 rk[SUB][NCH] = {}, rv[SUB][NVG][4] = {};
+  // VSPLIT (D 128, 64-key stages): the two subtiles' 128 V groups each go to one half of the
+  // workgroup (threads 0-127 subtile 0, 128-255 subtile 1) instead of both to threads 0-127, so
+  // every wave issues the same loads and stores (and holds half the V registers)
+  constexpr bool VSPLIT = SUB == 2 && VG == 128;
+  constexpr int RVS = VSPLIT ? 1 : SUB;
+  bf16x8 rk[SUB][NCH] = {}, rv[RVS][NVG][4] = {};
+  const int vu = VSPLIT ? (tid >> 7) : 0, vc = VSPLIT ? (tid & 127) : tid;
   auto load_tile = [&](int kb0) {
     if constexpr (PROBE == 2) {   // timing probe only: no global loads (stale registers staged)
 #pragma unroll
       for (int u = 0; u < SUB; ++u) {
 #pragma unroll
         for (int i = 0; i < NCH; ++i) asm volatile("" : "+v"(rk[u][i]));
+      }
+#pragma unroll
+      for (int u = 0; u < RVS; ++u)
 #pragma unroll
         for (int i = 0; i < NVG; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(rv[u][i][j]));
-      }
       return;
     }
 #pragma unroll
@@ -113,9 +121,13 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
         const bool ok = c < KCH && kb + key < Lk && d0 < D;
         rk[u][i] = ok ? ld8(k + (int64_t)(tk0 + kb + key) * k_stride + (int64_t)kvh * D + d0) : bf16x8{};
       }
+    }
+#pragma unroll
+    for (int u = 0; u < RVS; ++u) {
+      const int kb = kb0 + 32 * (VSPLIT ? vu : u);
 #pragma unroll
       for (int i = 0; i < NVG; ++i) {
-        const int c = tid + 256 * i;
+        const int c = vc + 256 * i;
         const int kq = c & 7, d0 = (c >> 3) * 8;   // 8 key groups across lanes: see V staging note
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -130,15 +142,18 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       bf16* Ks = sK + (buf * SUB + u) * KT;
-      bf16* Vs = sV + (buf * SUB + u) * VT;
 #pragma unroll
       for (int i = 0; i < NCH; ++i) {
         const int c = tid + 256 * i;
         if (c < KCH) *reinterpret_cast<bf16x8*>(&Ks[(c / CPR) * KLD + (c % CPR) * 8]) = rk[u][i];
       }
+    }
+#pragma unroll
+    for (int u = 0; u < RVS; ++u) {
+      bf16* Vs = sV + (buf * SUB + (VSPLIT ? vu : u)) * VT;
 #pragma unroll
       for (int i = 0; i < NVG; ++i) {
-        const int c = tid + 256 * i;
+        const int c = vc + 256 * i;
         if (PROBE == 1) {   // timing probe only (wrong results): V image writes skipped
           asm volatile("" ::"v"(rv[u][i][0]), "v"(rv[u][i][1]), "v"(rv[u][i][2]), "v"(rv[u][i][3]));
           continue;
