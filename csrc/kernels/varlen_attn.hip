@@ -94,9 +94,13 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
   // every wave issues the same loads and stores (and holds half the V registers)
   constexpr bool VSPLIT = SUB == 2 && VG == 128;
   constexpr int RVS = VSPLIT ? 1 : SUB;
+  // RING (fast body, D 128): two register sets, a stage's global loads issued two compute
+  // phases before its LDS store (the paged prefill's A / B ring); otherwise one set, one phase
+  constexpr bool RING = FAST && VSPLIT;
   bf16x8 rk[SUB][NCH] = {}, rv[RVS][NVG][4] = {};
+  bf16x8 rk2[RING ? SUB : 1][NCH] = {}, rv2[RING ? RVS : 1][NVG][4] = {};
   const int vu = VSPLIT ? (tid >> 7) : 0, vc = VSPLIT ? (tid & 127) : tid;
-  auto load_tile = [&](int kb0) {
+  auto load_regs = [&](auto& rk, auto& rv, int kb0) {
     if constexpr (PROBE == 2) {   // timing probe only: no global loads (stale registers staged)
 #pragma unroll
       for (int u = 0; u < SUB; ++u) {
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
       }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_regs = [&](const auto& rk, const auto& rv, int buf) {
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       bf16* Ks = sK + (buf * SUB + u) * KT;
@@ -172,15 +176,7 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
   };
 
   const bool active = r0 < L;
-  int buf = 0;
-  if (kv_end > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
-  for (int kb0 = 0; kb0 < kv_end; kb0 += 32 * SUB) {
-    const bool more = kb0 + 32 * SUB < kv_end;
-    if (more) load_tile(kb0 + 32 * SUB);  // in flight while this stage is consumed from LDS
+  auto compute_stage = [&](int kb0, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       const int kb = kb0 + 32 * u;
@@ -304,9 +300,45 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
         }
       }
     }
-    if (more) store_tile(buf ^ 1);  // the other buffer was last read before the previous barrier
+  };
+  constexpr int STEP = 32 * SUB;
+  if constexpr (RING) {
+    // invariant at the top: LDS buf 0 = stage kb, registers B (rk2 / rv2) = kb + STEP, A = kb + 2 STEP
+    int kb = 0;
+    if (kv_end > 0) {
+      load_regs(rk, rv, 0);
+      if (STEP < kv_end) load_regs(rk2, rv2, STEP);
+      store_regs(rk, rv, 0);
+    }
     __syncthreads();
-    buf ^= 1;
+    if (2 * STEP < kv_end) load_regs(rk, rv, 2 * STEP);
+    for (; kb < kv_end; kb += 2 * STEP) {
+      compute_stage(kb, 0);
+      if (kb + STEP >= kv_end) break;
+      store_regs(rk2, rv2, 1);   // buf 1 was last read before the previous barrier
+      __syncthreads();
+      if (kb + 3 * STEP < kv_end) load_regs(rk2, rv2, kb + 3 * STEP);
+      compute_stage(kb + STEP, 1);
+      if (kb + 2 * STEP >= kv_end) break;
+      store_regs(rk, rv, 0);
+      __syncthreads();
+      if (kb + 4 * STEP < kv_end) load_regs(rk, rv, kb + 4 * STEP);
+    }
+  } else {
+    int buf = 0;
+    if (kv_end > 0) {
+      load_regs(rk, rv, 0);
+      store_regs(rk, rv, 0);
+    }
+    __syncthreads();
+    for (int kb0 = 0; kb0 < kv_end; kb0 += STEP) {
+      const bool more = kb0 + STEP < kv_end;
+      if (more) load_regs(rk, rv, kb0 + STEP);  // in flight while this stage is consumed from LDS
+      compute_stage(kb0, buf);
+      if (more) store_regs(rk, rv, buf ^ 1);  // the other buffer was last read before the previous barrier
+      __syncthreads();
+      buf ^= 1;
+    }
   }
   if (!active) return;
   if constexpr (FAST) {   // the row's 4 lanes' partial sums
