@@ -848,7 +848,9 @@ constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
 // rescales O / l lazily (only when some row's max grew by more than 2^8).
 // NW = waves per workgroup: 4 (one 32-row block per head of the kv group) or 8 (two row blocks:
 // 64-row items, every K/V stage staged once for twice the query rows, one chunk per thread).
-template <int SUB, int F, bool SPLIT, bool FAST = false, int NW = 4>
+// PROBE (timing diagnostics, wrong results by design; OME_PREFILL_PROBE): 1 = no V image stores,
+// 2 = no K/V global loads, 3 = identity pages (no block-table loads before the K/V loads).
+template <int SUB, int F, bool SPLIT, bool FAST = false, int NW = 4, int PROBE = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -918,12 +920,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
   // stage the loop was latency-bound at ~3.9 us per 64-key step (profiles/r03_prefill_*).
   Raw8 rkA[SUB][PT], rvA[SUB][PT], rkB[SUB][PT], rvB[SUB][PT];
   auto load_tile = [&](Raw8 (&rk)[SUB][PT], Raw8 (&rv)[SUB][PT], int kb0) {
+    if constexpr (PROBE == 2) {
+#pragma unroll
+      for (int u = 0; u < SUB; ++u)
+#pragma unroll
+        for (int i = 0; i < PT; ++i) asm volatile("" : "+v"(rk[u][i]), "+v"(rv[u][i]));
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < SUB; ++u) {
       const int kb = kb0 + 32 * u;
       const int pi = kb / P;
-      const int pA = (kb < kv_len) ? bt[pi] : bt[0];  // out-of-range subtiles: any valid page (masked)
-      const int pB = (kb + P < kv_len) ? bt[pi + 1] : pA;
+      const int pA = PROBE == 3 ? pi : (kb < kv_len) ? bt[pi] : bt[0];  // out-of-range subtiles: any valid page (masked)
+      const int pB = PROBE == 3 ? pi + 1 : (kb + P < kv_len) ? bt[pi + 1] : pA;
 #pragma unroll
       for (int i = 0; i < PT; ++i) {
         const int c = tid + 64 * NW * i;
@@ -944,6 +953,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
         const int c = tid + 64 * NW * i;
         const int key = c >> 4, dc = c & 15;
         *reinterpret_cast<bf16x8*>(&sK[buf][u][key * PF_KLD + dc * 8]) = k8_bf16<F>(rk[u][i]);
+        if constexpr (PROBE == 1) {
+          asm volatile("" ::"v"(rv[u][i]));
+          continue;
+        }
         const int page = c >> 8, dim = (c & 255) >> 1, half = c & 1;
         bf16* vrow = &sV[buf][u][dim * PF_VLD];
         const bf16x8 vv = k8_bf16<F>(rv[u][i]);
@@ -1263,8 +1276,20 @@ static void launch_prefill(int variant, int rows, int G, dim3 grid, hipStream_t 
         if (prefill_fast(scl, window, row_hi)) OME_PF2(true, 8);
         else OME_PF2(false, 8);
       } else {
-        if (prefill_fast(scl, window, row_hi)) OME_PF2(true, 4);
-        else OME_PF2(false, 4);
+        static const int probe = getenv("OME_PREFILL_PROBE") ? atoi(getenv("OME_PREFILL_PROBE")) : 0;
+        if (prefill_fast(scl, window, row_hi)) {
+#define OME_PF2P(PR)                                                                                              \
+  paged_prefill_v2_kernel<2, F, false, true, 4, PR><<<grid, 256, 0, stream>>>(                                    \
+      (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,      \
+      (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi, 0, nullptr, nullptr)
+          if (F == KV_BF16 && probe == 1) OME_PF2P(1);
+          else if (F == KV_BF16 && probe == 2) OME_PF2P(2);
+          else if (F == KV_BF16 && probe == 3) OME_PF2P(3);
+          else OME_PF2(true, 4);
+#undef OME_PF2P
+        } else {
+          OME_PF2(false, 4);
+        }
       }
 #undef OME_PF2
       return;
