@@ -25,6 +25,28 @@ def test_varlen_attention_kernel(D, causal):
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("D", [80, 128])
+def test_varlen_attention_fast_rescale_paths(D):
+    """Fast bidirectional body: long sequences (the two-register-stage ring runs many stages), key
+    norms that grow along the sequence (the lazy O / l rescale fires mid-sequence, > 2^8 growth),
+    and a tail that is not a multiple of 32 or 64 keys."""
+    torch.manual_seed(7 + D)
+    lens = [1000, 333, 64, 65]
+    T, Hq, Hkv = sum(lens), 4, 2
+    q = torch.randn(T, Hq, D, device="cuda")
+    k = torch.randn(T, Hkv, D, device="cuda")
+    v = torch.randn(T, Hkv, D, device="cuda")
+    s0 = 0
+    for n in lens:   # key scale ramps 0.2 -> 3: row maxima keep growing by several powers of two
+        k[s0:s0 + n] *= torch.linspace(0.2, 3.0, n, device="cuda")[:, None, None]
+        s0 += n
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    got = ops.varlen_attention(q, k, v, lens, D ** -0.5).float()
+    want = ref.varlen_attention(q.float(), k.float(), v.float(), lens, D ** -0.5)
+    err = (got - want).abs().max().item()
+    assert err < 2e-2, err
+
+
 @pytest.mark.parametrize("D", [64, 72, 128])
 def test_varlen_cross_attention_kernel(D):
     """Cross lengths (MiniCPM-V resampler, Phi-4-MM padding queries, Mllama padding rows): query
