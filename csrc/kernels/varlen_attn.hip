@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
   // VSPLIT (D 128, 64-key stages): the two subtiles' 128 V groups each go to one half of the
   // workgroup (threads 0-127 subtile 0, 128-255 subtile 1) instead of both to threads 0-127, so
   // every wave issues the same loads and stores (and holds half the V registers)
-  constexpr bool VSPLIT = SUB == 2 && VG == 128;
+  constexpr bool VSPLIT = SUB == 2 && VG <= 128;
   constexpr int RVS = VSPLIT ? 1 : SUB;
   // RING (fast body, D 128): two register sets, a stage's global loads issued two compute
   // phases before its LDS store (the paged prefill's A / B ring); otherwise one set, one phase
@@ -399,11 +399,14 @@ OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k,
   // stages (OME_VARLEN_SUB=1: 32) -- profiles/r05_varlen_attn.md
   const bool fast = !causal && getenv_int("OME_VARLEN_FAST", 1);
   static const int sub = getenv("OME_VARLEN_SUB") ? atoi(getenv("OME_VARLEN_SUB")) : 2;
+  static const int sub_small = getenv("OME_VARLEN_SUB_SMALL") ? atoi(getenv("OME_VARLEN_SUB_SMALL")) : 2;
   if (D <= 64) {
-    if (fast) varlen_attn_kernel<64, true><<<grid, 256, 0, stream>>>(ARGS);
+    if (fast && sub_small == 2) varlen_attn_kernel<64, true, 2><<<grid, 256, 0, stream>>>(ARGS);
+    else if (fast) varlen_attn_kernel<64, true><<<grid, 256, 0, stream>>>(ARGS);
     else varlen_attn_kernel<64><<<grid, 256, 0, stream>>>(ARGS);
   } else if (D <= 96) {
-    if (fast) varlen_attn_kernel<96, true><<<grid, 256, 0, stream>>>(ARGS);
+    if (fast && sub_small == 2) varlen_attn_kernel<96, true, 2><<<grid, 256, 0, stream>>>(ARGS);
+    else if (fast) varlen_attn_kernel<96, true><<<grid, 256, 0, stream>>>(ARGS);
     else varlen_attn_kernel<96><<<grid, 256, 0, stream>>>(ARGS);
   } else if (fast) {
     static const int probe = getenv("OME_VARLEN_PROBE") ? atoi(getenv("OME_VARLEN_PROBE")) : 0;
