@@ -1282,10 +1282,14 @@ static void launch_prefill(int variant, int rows, int G, dim3 grid, hipStream_t 
   paged_prefill_v2_kernel<2, F, false, true, 4, PR><<<grid, 256, 0, stream>>>(                                    \
       (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,      \
       (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi, 0, nullptr, nullptr)
-          if (F == KV_BF16 && probe == 1) OME_PF2P(1);
-          else if (F == KV_BF16 && probe == 2) OME_PF2P(2);
-          else if (F == KV_BF16 && probe == 3) OME_PF2P(3);
-          else OME_PF2(true, 4);
+          bool done = false;
+          if constexpr (F == KV_BF16) {   // diagnostic instantiations for the bf16 cache only
+            done = probe >= 1 && probe <= 3;
+            if (probe == 1) OME_PF2P(1);
+            else if (probe == 2) OME_PF2P(2);
+            else if (probe == 3) OME_PF2P(3);
+          }
+          if (!done) OME_PF2(true, 4);
 #undef OME_PF2P
         } else {
           OME_PF2(false, 4);
