@@ -333,7 +333,9 @@ class DeepseekForCausalLM(LlamaForCausalLM):
                      flat, q, self.nope, q_full)
         # strided batched GEMMs read the head-major views in place (no transpose copies)
         q_nope = q[..., : self.nope].transpose(0, 1)                       # [Hl, T, nope] view
-        q_full[:, :, :lat].copy_(torch.bmm(q_nope, self.w_uk[i]).transpose(0, 1))
+        # written straight into q_full's latent columns (a [Hl, T, lat] view with unit inner
+        # stride: the batched GEMM takes it as its output layout, no copy pass)
+        torch.bmm(q_nope, self.w_uk[i], out=q_full[:, :, :lat].transpose(0, 1))
         o_lat = torch.empty(T, Hl, lat, dtype=x.dtype, device=x.device)
         ws = None
         if x.is_cuda:   # one split-K workspace per stream (two-batch overlap runs two at once)
@@ -346,8 +348,8 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         cache3 = cache.view(cache.shape[0], -1, lat + self.rope)
         for s, e, bt, rows, lens in self._token_rows(meta, T):
             ops.mla_attn(q_full[s:e], cache3, bt, rows, lens, self.scale, ws, out=o_lat[s:e], dv=lat)
-        o = torch.bmm(o_lat.transpose(0, 1), self.w_uv[i])   # [Hl, T, vd]
-        o = o.transpose(0, 1).reshape(T, Hl * self.vd)
+        o = torch.empty(T, Hl * self.vd, dtype=x.dtype, device=x.device)
+        torch.bmm(o_lat.transpose(0, 1), self.w_uv[i], out=o.view(T, Hl, self.vd).transpose(0, 1))   # token-major
         return pstate.tp_all_reduce(linear(o, self.w_o[i]))
 
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
