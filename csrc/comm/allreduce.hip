@@ -26,7 +26,7 @@ namespace {
 constexpr int kMaxRanks = 8;
 constexpr int kMaxBlocks = 128;
 constexpr int kThreads = 512;
-constexpr uint64_t kSpinLimit = 1ull << 26;
+constexpr uint64_t kSpinLimitDefault = 1ull << 26;
 
 struct Signal {
   uint32_t start[kMaxBlocks][kMaxRanks];
@@ -38,6 +38,15 @@ struct Signal {
 struct Peers {
   Signal* sig[kMaxRanks];
   char* data[kMaxRanks];
+  // fault handling (kernel arguments, so the normal path pays one scalar compare):
+  //   spin_limit  bounded flag waits (OME_COMM_SPIN_LIMIT, s_sleep(1) iterations);
+  //   host_err    host-mapped word that an expired wait also sets, so a host watchdog sees the
+  //               failure without a HIP call (a blocking copy could queue behind the hung work);
+  //   fault       host-mapped {stall iterations} word, non-null only when OME_COMM_FAULT is set:
+  //               the flag lanes sleep that long before publishing (a stalled rank)
+  uint64_t spin_limit;
+  uint32_t* host_err;
+  const uint32_t* fault;
 };
 
 typedef __bf16 bf16;
@@ -59,6 +68,10 @@ __device__ __forceinline__ void block_barrier(const Peers& P, int rank, int worl
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < world) {
+    if (P.fault) {   // fault injection: stall before the publish
+      const uint32_t n = __hip_atomic_load(P.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (uint32_t i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+    }
     __threadfence_system();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     Signal* peer = P.sig[threadIdx.x];
@@ -67,8 +80,9 @@ __device__ __forceinline__ void block_barrier(const Peers& P, int rank, int worl
     uint32_t* f = which ? &self->end[blockIdx.x][threadIdx.x] : &self->start[blockIdx.x][threadIdx.x];
     uint64_t spins = 0;
     while (ld_acquire(f) < epoch) {
-      if (++spins > kSpinLimit) {
+      if (++spins > P.spin_limit) {
         atomicOr(&self->error, 1u);
+        if (P.host_err) __hip_atomic_store(P.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -300,6 +314,7 @@ struct Ctx {
   char* data;
   Peers peers;
   bool opened[kMaxRanks];
+  uint32_t* host_ctl;   // host-mapped: [0] error mirror, [1] fault stall iterations
 };
 
 }  // namespace
@@ -336,7 +351,33 @@ OME_API int ome_comm_create(int rank, int world, size_t data_bytes, void** ctx_o
   if (e != hipSuccess) return (int)e;
   c->peers.sig[rank] = c->sig;
   c->peers.data[rank] = c->data;
+  const char* sl = getenv("OME_COMM_SPIN_LIMIT");
+  c->peers.spin_limit = sl && atoll(sl) > 0 ? (uint64_t)atoll(sl) : kSpinLimitDefault;
+  e = hipHostMalloc((void**)&c->host_ctl, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return (int)e;
+  memset(c->host_ctl, 0, 64);
+  uint32_t* dctl = nullptr;
+  e = hipHostGetDevicePointer((void**)&dctl, c->host_ctl, 0);
+  if (e != hipSuccess) return (int)e;
+  c->peers.host_err = dctl;
+  c->peers.fault = getenv("OME_COMM_FAULT") ? dctl + 1 : nullptr;
   *ctx_out = c;
+  return 0;
+}
+
+// host-side error word (set by the kernels when a bounded wait expires): no HIP call, safe to poll
+// from a watchdog thread while the GPU is busy
+OME_API int ome_comm_host_error(void* ctx) {
+  Ctx* c = (Ctx*)ctx;
+  return (int)__atomic_load_n(&c->host_ctl[0], __ATOMIC_ACQUIRE);
+}
+
+// fault injection (OME_COMM_FAULT set at create time): the flag lanes of every following barrier
+// sleep `stall` x s_sleep(127) before publishing (0 = off); -1 when injection is not enabled
+OME_API int ome_comm_set_fault(void* ctx, uint32_t stall) {
+  Ctx* c = (Ctx*)ctx;
+  if (!c->peers.fault) return -1;
+  __atomic_store_n(&c->host_ctl[1], stall, __ATOMIC_RELEASE);
   return 0;
 }
 
@@ -462,6 +503,7 @@ OME_API int ome_comm_error(void* ctx) {
 OME_API void ome_comm_destroy(void* ctx) {
   Ctx* c = (Ctx*)ctx;
   if (!c) return;
+  if (c->host_ctl) (void)hipHostFree(c->host_ctl);
   for (int r = 0; r < c->world; ++r) {
     if (c->opened[r]) {
       (void)hipIpcCloseMemHandle(c->peers.sig[r]);

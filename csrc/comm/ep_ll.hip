@@ -28,7 +28,7 @@
 namespace {
 
 constexpr int kMaxRanks = 8;
-constexpr uint64_t kSpinLimit = 1ull << 26;
+constexpr uint64_t kSpinLimitDefault = 1ull << 26;
 typedef __bf16 bf16;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -43,7 +43,19 @@ struct EpSig {
 struct EpPeers {
   EpSig* sig[kMaxRanks];
   char* buf[kMaxRanks];  // each rank's shared buffer (layout below)
+  // fault handling, as in allreduce.hip: bounded waits (OME_COMM_SPIN_LIMIT), host-mapped error
+  // mirror, optional stall-before-publish word (OME_COMM_FAULT)
+  uint64_t spin_limit;
+  uint32_t* host_err;
+  const uint32_t* fault;
 };
+
+__device__ __forceinline__ void ep_fault_stall(const EpPeers& P) {
+  if (P.fault) {
+    const uint32_t n = __hip_atomic_load(P.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+}
 
 // shared buffer layout (bytes), per parity p:  S rows [W][cap][H] bf16 | S ids [W][cap] i32 |
 // S counts [W] i32 (padded to 256 B) | C rows [W][cap][H] bf16
@@ -145,19 +157,21 @@ __global__ __launch_bounds__(256) void ep_pack_kernel(const bf16* __restrict__ x
 __global__ void ep_signal_kernel(EpPeers P, int me, int W, int which, EpSig* self) {
   const uint32_t e = self->epoch;
   if ((int)threadIdx.x < W) {
+    ep_fault_stall(P);
     __threadfence_system();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     st_release_sys(&P.sig[threadIdx.x]->ready[which][me], e);
   }
 }
 
-__global__ void ep_wait_kernel(EpSig* self, int W, int which) {
+__global__ void ep_wait_kernel(EpPeers P, EpSig* self, int W, int which) {
   const uint32_t e = self->epoch;
   if ((int)threadIdx.x < W) {
     uint64_t spins = 0;
     while (ld_acquire_sys(&self->ready[which][threadIdx.x]) < e) {
-      if (++spins > kSpinLimit) {
+      if (++spins > P.spin_limit) {
         atomicOr(&self->error, 1u);
+        if (P.host_err) __hip_atomic_store(P.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -268,11 +282,12 @@ __device__ __forceinline__ bool last_block(uint32_t* done) {
   return last != 0;
 }
 
-__device__ __forceinline__ void spin_flag(EpSig* self, int which, int src, uint32_t e) {
+__device__ __forceinline__ void spin_flag(const EpPeers& P, EpSig* self, int which, int src, uint32_t e) {
   uint64_t spins = 0;
   while (ld_acquire_sys(&self->ready[which][src]) < e) {
-    if (++spins > kSpinLimit) {
+    if (++spins > P.spin_limit) {
       atomicOr(&self->error, 1u);
+      if (P.host_err) __hip_atomic_store(P.host_err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -339,7 +354,10 @@ __global__ __launch_bounds__(256) void ep_send_kernel(EpPeers P, int me, int W, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  if ((int)threadIdx.x < W) st_release_sys(&P.sig[threadIdx.x]->ready[0][me], cur);
+  if ((int)threadIdx.x < W) {
+    ep_fault_stall(P);
+    st_release_sys(&P.sig[threadIdx.x]->ready[0][me], cur);
+  }
 }
 
 // grid (kRecvBlocks, W): rows source `src` sent me, R [W][cap][H]; rids past the count = e_local
@@ -348,7 +366,7 @@ __global__ __launch_bounds__(256) void ep_recv_kernel(EpPeers P, int me, int H, 
                                                       int* __restrict__ rcount) {
   const int g = blockIdx.x, src = blockIdx.y;
   const uint32_t cur = self->epoch;
-  if (threadIdx.x == 0) spin_flag(self, 0, src, cur);
+  if (threadIdx.x == 0) spin_flag(P, self, 0, src, cur);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const int par = cur & 1;
@@ -390,7 +408,10 @@ __global__ __launch_bounds__(256) void ep_comb_send_kernel(EpPeers P, int me, in
     __threadfence_system();
   }
   __syncthreads();
-  if ((int)threadIdx.x < W) st_release_sys(&P.sig[threadIdx.x]->ready[1][me], cur);
+  if ((int)threadIdx.x < W) {
+    ep_fault_stall(P);
+    st_release_sys(&P.sig[threadIdx.x]->ready[1][me], cur);
+  }
 }
 
 // grid = tokens: wait for every owner's combine flag, then the weighted sum of ep_comb_pull_kernel
@@ -400,7 +421,7 @@ __global__ __launch_bounds__(256) void ep_comb_recv_kernel(EpPeers P, int me, in
                                                            const int* __restrict__ a_slot, float scale,
                                                            bf16* __restrict__ out, int64_t ldo) {
   const uint32_t cur = self->epoch;
-  if ((int)threadIdx.x < W) spin_flag(self, 1, threadIdx.x, cur);
+  if ((int)threadIdx.x < W) spin_flag(P, self, 1, threadIdx.x, cur);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const int t = blockIdx.x;
@@ -436,6 +457,7 @@ struct EpCtx {
   Layout L;
   EpPeers peers;
   bool opened[kMaxRanks];
+  uint32_t* host_ctl;   // host-mapped: [0] error mirror, [1] fault stall iterations
 };
 
 }  // namespace
@@ -448,7 +470,7 @@ static bool comm_finegrained() {
 
 OME_API int ome_ep_create(int rank, int world, int cap, int H, void** ctx_out, void* sig_handle, void* buf_handle) {
   if (world < 2 || world > kMaxRanks || rank < 0 || rank >= world || H % 8 || cap <= 0) return -2;
-  EpCtx* c = new EpCtx{rank, world, cap, H, nullptr, nullptr, Layout(world, cap, H), {}, {}};
+  EpCtx* c = new EpCtx{rank, world, cap, H, nullptr, nullptr, Layout(world, cap, H), {}, {}, nullptr};
   hipError_t e = hipExtMallocWithFlags((void**)&c->sig, sizeof(EpSig), hipDeviceMallocUncached);
   if (e != hipSuccess) return (int)e;
   if ((e = hipMemset(c->sig, 0, sizeof(EpSig))) != hipSuccess) return (int)e;
@@ -460,7 +482,28 @@ OME_API int ome_ep_create(int rank, int world, int cap, int H, void** ctx_out, v
   if ((e = hipIpcGetMemHandle((hipIpcMemHandle_t*)buf_handle, c->buf)) != hipSuccess) return (int)e;
   c->peers.sig[rank] = c->sig;
   c->peers.buf[rank] = c->buf;
+  const char* sl = getenv("OME_COMM_SPIN_LIMIT");
+  c->peers.spin_limit = sl && atoll(sl) > 0 ? (uint64_t)atoll(sl) : kSpinLimitDefault;
+  if ((e = hipHostMalloc((void**)&c->host_ctl, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    return (int)e;
+  memset(c->host_ctl, 0, 64);
+  uint32_t* dctl = nullptr;
+  if ((e = hipHostGetDevicePointer((void**)&dctl, c->host_ctl, 0)) != hipSuccess) return (int)e;
+  c->peers.host_err = dctl;
+  c->peers.fault = getenv("OME_COMM_FAULT") ? dctl + 1 : nullptr;
   *ctx_out = c;
+  return 0;
+}
+
+OME_API int ome_ep_host_error(void* ctx) {
+  EpCtx* c = (EpCtx*)ctx;
+  return (int)__atomic_load_n(&c->host_ctl[0], __ATOMIC_ACQUIRE);
+}
+
+OME_API int ome_ep_set_fault(void* ctx, uint32_t stall) {
+  EpCtx* c = (EpCtx*)ctx;
+  if (!c->peers.fault) return -1;
+  __atomic_store_n(&c->host_ctl[1], stall, __ATOMIC_RELEASE);
   return 0;
 }
 
@@ -509,7 +552,7 @@ OME_API int ome_ep_dispatch(void* ctx, const void* x, int64_t ldx, const int* to
     ep_pack_kernel<<<n, 256, 0, stream>>>((const bf16*)x, ldx, c->H, k, a_local, a_dst, a_slot, c->cap, c->sig,
                                           c->buf, c->L);
   ep_signal_kernel<<<1, 64, 0, stream>>>(c->peers, c->rank, c->world, 0, c->sig);
-  ep_wait_kernel<<<1, 64, 0, stream>>>(c->sig, c->world, 0);
+  ep_wait_kernel<<<1, 64, 0, stream>>>(c->peers, c->sig, c->world, 0);
   ep_pull_kernel<<<dim3(c->cap, c->world), 256, 0, stream>>>(c->peers, c->rank, c->H, c->cap, e_local, c->L, c->sig,
                                                             (bf16*)R, rids, rcount);
   return (int)hipGetLastError();
@@ -532,7 +575,7 @@ OME_API int ome_ep_combine(void* ctx, const void* y_sorted, const int* inv, cons
   ep_comb_pack_kernel<<<dim3(c->cap, c->world), 256, 0, stream>>>((const bf16*)y_sorted, inv, rcount, c->H, c->cap,
                                                                  c->L, c->sig, c->buf);
   ep_signal_kernel<<<1, 64, 0, stream>>>(c->peers, c->rank, c->world, 1, c->sig);
-  ep_wait_kernel<<<1, 64, 0, stream>>>(c->sig, c->world, 1);
+  ep_wait_kernel<<<1, 64, 0, stream>>>(c->peers, c->sig, c->world, 1);
   if (T > 0)
     ep_comb_pull_kernel<<<T, 256, 0, stream>>>(c->peers, c->rank, c->H, k, c->cap, c->L, c->sig, topk_w, a_dst,
                                                a_slot, scale, (bf16*)out, ldo);
@@ -549,6 +592,7 @@ OME_API int ome_ep_error(void* ctx) {
 OME_API void ome_ep_destroy(void* ctx) {
   EpCtx* c = (EpCtx*)ctx;
   if (!c) return;
+  if (c->host_ctl) (void)hipHostFree(c->host_ctl);
   for (int r = 0; r < c->world; ++r)
     if (c->opened[r]) {
       (void)hipIpcCloseMemHandle(c->peers.sig[r]);

@@ -74,6 +74,9 @@ __device__ __forceinline__ void sk_stage(char* lds, const bf16* __restrict__ g, 
 __device__ __forceinline__ void sk_buf_lds(__amdgpu_buffer_rsrc_t rs, char* lds, uint32_t voff, uint32_t soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 16, voff, soff, 0, 0);
 }
+__device__ __forceinline__ void sk_buf_lds_nt(__amdgpu_buffer_rsrc_t rs, char* lds, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)lds, 16, voff, soff, 0, 2);
+}
 
 __device__ __forceinline__ bf16x8 sk_frag(const char* lds, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds + row * 128 + sk_swz(row, chunk) * 16);
@@ -108,8 +111,11 @@ __device__ __forceinline__ int sk_block_of(int64_t u, int64_t U, int B) {
 }
 
 // X, W: byte pointers with byte row strides; kt = K-tiles of 128 bytes (bf16: K / 64, fp8: K / 128)
-template <int BM, int BN, int NBUF, int EPI, int Q>
-__global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const char* __restrict__ X, int64_t ldx,
+// OCC = 2: two workgroups per CU (128 VGPRs, NBUF = 2 x 32 KiB LDS) -- the decode-GEMM diagnosis
+// (profiles/r05_decode_gemm_diagnosis.md) found one workgroup per CU idle on its own DMA round trip.
+// NTW = 1: the W pieces stream with the non-temporal policy (MI355X_MICROARCH.md nt-weights).
+template <int BM, int BN, int NBUF, int EPI, int Q, int OCC = 1, int NTW = 0>
+__global__ __launch_bounds__(NTHR, OCC == 2 ? 4 : 1) void gemm_sk_kernel(const char* __restrict__ X, int64_t ldx,
                                                           const char* __restrict__ W, int64_t ldw,
                                                           const float* __restrict__ sa, const float* __restrict__ sw,
                                                           const bf16* __restrict__ bias, bf16* __restrict__ out,
@@ -219,7 +225,9 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const char* __restrict
     }
     auto piece = [&](int t, int b, auto q_tag) {
       constexpr int q = decltype(q_tag)::value;
-      if constexpr (q < PW)
+      if constexpr (q < PW && NTW)
+        sk_buf_lds_nt(rsw, bw(b) + (wave * PW + q) * 1024, vo[q], t * 128);
+      else if constexpr (q < PW)
         sk_buf_lds(rsw, bw(b) + (wave * PW + q) * 1024, vo[q], t * 128);
       else if constexpr (q < PW + BM / 64)
         sk_buf_lds(rsx, bx(b) + (wave * (BM / 64) + q - PW) * 1024, vo[q], t * 128);
@@ -502,7 +510,7 @@ __global__ __launch_bounds__(NTHR, 1) void gemm_sk_kernel(const char* __restrict
   }
 }
 
-template <int BM, int BN, int NBUF, int EPI, int Q>
+template <int BM, int BN, int NBUF, int EPI, int Q, int OCC = 1, int NTW = 0>
 int launch_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const float* sa, const float* sw,
               const void* bias, void* out, int64_t ldo, int M, int N, int kt, int nwg, float* ws, int* cnt,
               hipStream_t stream) {
@@ -510,12 +518,12 @@ int launch_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, const floa
   static_assert(LDS <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)gemm_sk_kernel<BM, BN, NBUF, EPI, Q>,
+    hipError_t e = hipFuncSetAttribute((const void*)gemm_sk_kernel<BM, BN, NBUF, EPI, Q, OCC, NTW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  gemm_sk_kernel<BM, BN, NBUF, EPI, Q><<<nwg, NTHR, LDS, stream>>>((const char*)X, ldx, (const char*)W, ldw, sa, sw,
+  gemm_sk_kernel<BM, BN, NBUF, EPI, Q, OCC, NTW><<<nwg, NTHR, LDS, stream>>>((const char*)X, ldx, (const char*)W, ldw, sa, sw,
                                                               (const bf16*)bias, (bf16*)out, ldo, M, N, kt, ws, cnt);
   return (int)hipGetLastError();
 }
@@ -547,6 +555,22 @@ OME_API int ome_gemm_sk(const void* X, int64_t ldx, const void* W, int64_t ldw, 
                                                              ldo, M, N, K / BK, nwg, w, c, stream)                \
                         : launch_sk<BMV, BNV, NB, SK_SILU, 0>(X, ldx * 2, W, ldw * 2, nullptr, nullptr, bias, out, \
                                                              ldo, M, N, K / BK, nwg, w, c, stream)
+  // decode-GEMM variants (OME_SK_VARIANT, 128 x 128 only): 1 = two workgroups per CU, 2 = nt W
+  // stream, 3 = both
+  static const int var = getenv("OME_SK_VARIANT") ? atoi(getenv("OME_SK_VARIANT")) : 0;
+  if (bm == 128 && bn == 128 && var) {
+#define SK_V(NB, OC, NT)                                                                                          \
+  return epi == SK_BF16 ? launch_sk<128, 128, NB, SK_BF16, 0, OC, NT>(X, ldx * 2, W, ldw * 2, nullptr, nullptr,   \
+                                                                      bias, out, ldo, M, N, K / BK, nwg, w, c,   \
+                                                                      stream)                                    \
+                        : launch_sk<128, 128, NB, SK_SILU, 0, OC, NT>(X, ldx * 2, W, ldw * 2, nullptr, nullptr,   \
+                                                                      bias, out, ldo, M, N, K / BK, nwg, w, c,   \
+                                                                      stream)
+    if (var == 1) SK_V(2, 2, 0);
+    if (var == 2) SK_V(4, 1, 1);
+    SK_V(2, 2, 1);
+#undef SK_V
+  }
   if (bm == 256 && bn == 256) SK_GO(256, 256, 2);
   if (bm == 256) SK_GO(256, 128, 3);
   if (bn == 256) SK_GO(128, 256, 3);

@@ -56,6 +56,8 @@ COMMAND_ALIASES = [
     (re.compile(_NB + r"python3?\s+-m\s+sglang\.launch_server\b"), f"{_PYS} -m ome_amd.runtime.server"),
     (re.compile(_NB + r"python3?\s+-m\s+vllm\.entrypoints\.openai\.api_server\b"), f"{_PYS} -m ome_amd.runtime.server"),
     (re.compile(_NB + r"vllm\s+serve\b"), f"{_PYS} -m ome_amd.runtime.server --model-path"),
+    # SGLang diffusion CLI (the Qwen-Image runtimes): the diffusion server
+    (re.compile(_NB + r"sglang\s+serve\b"), f"{_PYS} -m ome_amd.diffusion.server"),
     (re.compile(_NB + r"python3?\s+-m\s+sglang_router\.launch_router\b"), f"{_PYS} -m ome_amd.router"),
     (re.compile(_NB + r"genai-bench\b"), f"{_PYS} -m ome_amd.bench.loadgen"),
     (re.compile(_NB + r"multinode-prober\b"), f"{_PYS} -m ome_amd.prober"),
@@ -65,6 +67,7 @@ COMMAND_ALIASES = [
     (re.compile(r"(?:\S*/)?ray_init\.sh\b"), f"{_PYS} -m ome_amd.raylet init"),
     (re.compile(_NB + r"python3?(?=\s|$)"), _PYS),
 ]
+_PEER_PORT_FLAGS = {"--service-discovery-port"}
 IMAGE_ENTRYPOINTS = {  # image (substring) -> default argv when the container has no command
     "sglang": [PY, "-m", "ome_amd.runtime.server"],
     "vllm": [PY, "-m", "ome_amd.runtime.server"],
@@ -404,7 +407,10 @@ class Kubelet:
             argv = shlex.split(translate_command(shlex.join(argv)))
         for i, a in enumerate(argv[:-1]):  # exec-form "--port", "8080" / "--addr", ":8080" pairs
             nxt = argv[i + 1]
-            if (a == "--port" or a.endswith("-port")) and nxt.isdigit() and int(nxt) in ports:
+            # (--service-discovery-port names the DISCOVERED pods' container port, not one this pod
+            # listens on: the router maps it through each worker pod's own host-port annotation)
+            if (a == "--port" or a.endswith("-port")) and a not in _PEER_PORT_FLAGS and nxt.isdigit() and \
+                    int(nxt) in ports:
                 argv[i + 1] = str(ports[int(nxt)])
             elif a in ("--addr", "--listen", "--metrics-addr") and nxt.rpartition(":")[2].isdigit():
                 hp, _, pt = nxt.rpartition(":")
@@ -526,8 +532,13 @@ class Kubelet:
                 argv = [translate_command(a) for a in probe["exec"].get("command") or []]
                 return subprocess.run(argv, env=cr.env, cwd=cr.cwd, timeout=timeout, capture_output=True).returncode == 0
             if probe.get("grpc"):
-                with socket.create_connection(("127.0.0.1", port_of(probe["grpc"]["port"])), timeout=timeout):
-                    return True
+                # a real grpc.health.v1.Health/Check of the probe's service (kubelet semantics:
+                # only SERVING passes; the engine's --grpc-mode server answers it)
+                from ome_amd.runtime.grpc_server import SERVING, health_check_sync
+
+                g = probe["grpc"]
+                return health_check_sync(f"127.0.0.1:{port_of(g['port'])}", g.get("service") or "",
+                                         timeout=timeout) == SERVING
         except Exception:  # noqa: BLE001 — any failure is a probe failure
             return False
         return True

@@ -157,7 +157,7 @@ class DeepseekForCausalLM(LlamaForCausalLM):
         for lst in (self.w_qa, self.w_qb, self.w_o, self.w_gu, self.w_d, self.w_sgu, self.w_sd):
             for i in self.layers:
                 if self._quantizable(lst[i]):
-                    lst[i] = quantize_weight(lst[i], self.fp8_block)
+                    lst[i] = quantize_weight(lst[i], self.fp8_block, tp=self.tp.tp)
         quantize_moe_experts(self)   # routed experts stay fp8 (block-scaled grouped GEMM)
 
     def _deinterleave_rows(self, w: torch.Tensor, head_dim: int, n_heads: int) -> torch.Tensor:

@@ -153,14 +153,19 @@ class LlamaForCausalLM:
         for lst in (self.w_qkv, self.w_o, self.w_gu, self.w_d):
             for i in self.layers:
                 if self._quantizable(lst[i]):
-                    lst[i] = quantize_weight(lst[i], self.fp8_block)
+                    lst[i] = quantize_weight(lst[i], self.fp8_block, tp=self.tp.tp)
                 elif isinstance(lst[i], torch.Tensor) and lst[i].numel():
                     kept += 1
-        if kept:
-            import logging
+        import logging
 
-            logging.getLogger("ome_amd.models").warning("fp8: %d projections keep bf16 (shape not 64x128-tileable)",
-                                                        kept)
+        from ome_amd.models.quant import fp8_bf16_copy_bytes
+
+        log = logging.getLogger("ome_amd.models")
+        if kept:
+            log.warning("fp8: %d projections keep bf16 (shape not 64x128-tileable)", kept)
+        if fp8_bf16_copy_bytes():
+            log.info("fp8: bf16 copies of the small projections: %.1f MiB in this process",
+                     fp8_bf16_copy_bytes() / 2 ** 20)
 
     # ------------------------------------------------------------------ rank-aware loading
     _presliced = False   # set by build_model when the loader already applied shard_plan

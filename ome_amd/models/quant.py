@@ -51,17 +51,31 @@ class Fp8Weight:
         return ref.fp8_dequant_weight(self.q, self.scale, self.block).to(dtype)
 
 
-def fp8_bf16_max_m(N: int, K: int) -> int:
-    """Rows up to which an fp8 [N, K] projection runs on its bf16 copy (0: never), from the
-    measured fp8 / bf16 table (profiles/r04_fp8_sk_bench.txt, r05 re-measure).  Per shape: N <= 2048 (q_a / kv_a) or N <= 6144 with K <= 4096 (Llama-8B qkv / o)
-    lose up to 256 rows; other <= 32M-element weights (DeepSeek shared gate_up) up to 32 rows;
-    <= 64M (Llama-8B down) on the GEMV rows only; anything larger always wins in fp8."""
-    if os.environ.get("OME_FP8_BF16_FALLBACK", "1") == "0":
+# bytes of bf16 copies kept next to fp8 weights in this process (logged once at the end of a
+# model's quantisation pass, bounded by OME_FP8_BF16_BUDGET_MB)
+_BF16_COPY_BYTES = 0
+
+
+def fp8_bf16_max_m(N: int, K: int, tp: int = 1) -> int:
+    """Rows up to which an fp8 [N, K] projection also runs on a bf16 copy of its own dequantised
+    values (0: never).  Only the SMALL projections keep a copy: N <= 2048 with N * K <= 16M
+    elements (DeepSeek q_a / kv_a, ~15-22 MB per layer), where activation quantisation plus a few
+    output tiles cost more than the halved weight bytes save at decode sizes (r05
+    profiles/r05_fp8_routed_bench.txt).  The Llama-size projections (qkv / o / down / gate_up) stay
+    fp8-only: a copy there nearly doubled the fp8 footprint.  Under TP the shapes are
+    per-rank shards, which were never measured, so no copies are kept; the total is bounded by
+    ``OME_FP8_BF16_BUDGET_MB`` (default 2048 MiB) and ``OME_FP8_BF16_FALLBACK=0`` disables it."""
+    if os.environ.get("OME_FP8_BF16_FALLBACK", "1") == "0" or tp > 1:
         return 0
-    n = N * K
-    if N <= 2048 or (N <= 6144 and K <= 4096):
-        return 256
-    return 32 if n <= (32 << 20) else 4 if n < (64 << 20) else 0
+    if N <= 2048 and N * K <= (16 << 20):
+        budget = int(os.environ.get("OME_FP8_BF16_BUDGET_MB", "2048")) << 20
+        if _BF16_COPY_BYTES + N * K * 2 <= budget:
+            return 256
+    return 0
+
+
+def fp8_bf16_copy_bytes() -> int:
+    return _BF16_COPY_BYTES
 
 
 @dataclass
@@ -120,8 +134,10 @@ def quantize_moe_experts(model) -> int:
     return kept
 
 
-def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
-    """bf16/fp32 [N, K] -> Fp8Weight (amax/448 scales per row, or per 128x128 block)."""
+def quantize_weight(w: torch.Tensor, block: int = 0, tp: int = 1) -> Fp8Weight:
+    """bf16/fp32 [N, K] -> Fp8Weight (amax/448 scales per row, or per 128x128 block); ``tp``: the
+    tensor-parallel degree the shard belongs to (no bf16 copies under TP)."""
+    global _BF16_COPY_BYTES
     N, K = w.shape
     wf = w.float()
     if block:
@@ -139,10 +155,11 @@ def quantize_weight(w: torch.Tensor, block: int = 0) -> Fp8Weight:
         s = torch.where(amax > 0, amax / ref.FP8_MAX, torch.ones_like(amax))
         q = (wf / s[:, None]).clamp(-ref.FP8_MAX, ref.FP8_MAX).to(torch.float8_e4m3fn).contiguous()
         out = Fp8Weight(q, s.contiguous(), 0)
-    m = fp8_bf16_max_m(N, K) if w.is_cuda else 0
+    m = fp8_bf16_max_m(N, K, tp) if w.is_cuda else 0
     if m:
         # the fp8 weights' own values (dequantised), so both paths compute the same projection
         out.bf16, out.bf16_max_m = out.dequant(torch.bfloat16).contiguous(), m
+        _BF16_COPY_BYTES += out.bf16.numel() * 2
     return out
 
 

@@ -1056,6 +1056,31 @@ def gemm_sk(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
     return out
 
 
+def gemm_xl_ok(M: int, N: int, K: int, bn: int = 256, nwg: int = 256) -> bool:
+    """Shapes / decompositions accepted by ``ome_gemm_xl`` with the shared stream-K workspace."""
+    return bn in (128, 256) and M > 0 and N % bn == 0 and K % 32 == 0 and K > 0 and nwg % 8 == 0 and \
+        8 <= nwg <= _SK_MAX_WG and gemm_sk_tiles(M, N, bn, 256) <= _SK_CNT
+
+
+def gemm_xl(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, out: torch.Tensor | None = None,
+            epi: int = 0, bn: int = 256, nwg: int = 256, probe: int = 0) -> torch.Tensor:
+    """out = x @ w.T (+ bias) on the large-tile stream-K MFMA GEMM (csrc/kernels/gemm_xl.hip: 256 x
+    ``bn`` tiles, one wave per SIMD with 128 x bn/2 accumulators of 32x32x16 MFMAs, BK = 32 LDS-DMA
+    stages).  ``epi=2``: w holds gate/up rows interleaved in 16-row blocks and out = SiLU(gate) * up.
+    ``probe`` 1 / 2: diagnostic skeleton builds (no DMA / no DMA and no LDS reads; wrong results)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not _gpu(x):
+        return gemm_sk(x, w, bias, out, epi)
+    assert x.stride(1) == 1 and w.stride(1) == 1 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == 2 else N, dtype=x.dtype, device=x.device)
+    ws, cnt = _sk_workspace(x.device)
+    call("ome_gemm_xl", x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), ptr(bias), out.data_ptr(),
+         out.stride(0), M, N, K, bn, epi, nwg, ws.data_ptr(), cnt.data_ptr(), probe, stream_ptr())
+    return out
+
+
 def gemm_pp_ok(M: int, N: int, K: int) -> bool:
     """Shapes accepted by the ping-pong 256 x 256 GEMM (csrc/kernels/gemm_pp.hip)."""
     return M > 0 and N > 0 and N % 256 == 0 and K > 0 and K % 64 == 0

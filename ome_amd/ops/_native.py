@@ -72,6 +72,7 @@ _SIGNATURES = {
         "ome_gemm_set_variant": [i32],
         "ome_gemm_sk": [vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
         "ome_gemm_pp": [vp, i64, vp, i64, vp, vp, i64, vp, i64, i32, i32, i32, i32, vp],
+        "ome_gemm_xl": [vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32, vp, vp, i32, vp],
         "ome_mla_prep": [vp, i64, i32, i32, i32, vp, f32, vp, vp, vp, vp, i64, vp, i64, i64, i32, i32, vp, i64, i64,
                          i32, vp],
         "ome_gemm_sk_fp8": [vp, i64, vp, vp, i64, vp, i32, vp, vp, i64, i32, i32, i32, i32, i32, i32, i32, vp, vp,
@@ -89,12 +90,16 @@ _SIGNATURES = {
         "ome_comm_all_reduce_add_rmsnorm": [vp, vp, vp, vp, vp, i32, i32, f32, i32, vp],
         "ome_comm_all_gather": [vp, vp, vp, i64, i64, i32, vp],
         "ome_comm_error": [vp],
+        "ome_comm_host_error": [vp],
+        "ome_comm_set_fault": [vp, C.c_uint32],
         "ome_comm_destroy": [vp],
         "ome_ep_create": [i32, i32, i32, i32, C.POINTER(vp), vp, vp],
         "ome_ep_open": [vp, vp, vp],
         "ome_ep_dispatch": [vp, vp, i64, vp, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp],
         "ome_ep_combine": [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, vp, i64, vp],
         "ome_ep_error": [vp],
+        "ome_ep_host_error": [vp],
+        "ome_ep_set_fault": [vp, C.c_uint32],
         "ome_ep_destroy": [vp],
         "ome_kvlink_export": [vp, vp, C.POINTER(i64)],
         "ome_kvlink_handle_size": [],

@@ -60,6 +60,10 @@ class CustomAllReduce:
         rc = lib.ome_comm_open(ctx, sig_all, dat_all)
         if rc != 0:
             raise _native.NativeError(f"ome_comm_open failed ({rc}): peers not reachable over xGMI/IPC")
+        # bounded-wait expiries land in a host-mapped word the engine watchdog polls (no HIP call)
+        from ome_amd.runtime import watchdog
+
+        watchdog.register_comm(f"allreduce(rank {self.rank}/{self.world})", self.host_error, self.set_fault)
 
     def _grid(self, n: int, two_shot: bool) -> int:
         """Workgroups for an n-element reduction: each one costs a flag hand-off with every peer
@@ -154,6 +158,15 @@ class CustomAllReduce:
 
     def error(self) -> int:
         return self._lib.ome_comm_error(self._ctx)
+
+    def host_error(self) -> int:
+        """The error word the kernels mirror into host memory: no HIP call, safe while the GPU is busy."""
+        return self._lib.ome_comm_host_error(self._ctx) if self._ctx else 0
+
+    def set_fault(self, stall: int) -> int:
+        """Fault injection (OME_COMM_FAULT set before creation): stall the flag publish of every
+        following barrier by ``stall`` x s_sleep(127); -1 when injection was not enabled."""
+        return self._lib.ome_comm_set_fault(self._ctx, int(stall)) if self._ctx else -1
 
     def close(self) -> None:
         if self._ctx:

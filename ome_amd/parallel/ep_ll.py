@@ -48,6 +48,9 @@ class LowLatencyEP:
         rc = lib.ome_ep_open(ctx, b"".join(h[0] for h in allh), b"".join(h[1] for h in allh))
         if rc != 0:
             raise _native.NativeError(f"ome_ep_open failed ({rc}): peers not reachable over xGMI/IPC")
+        from ome_amd.runtime import watchdog
+
+        watchdog.register_comm(f"ep_ll(rank {self.rank}/{self.world})", self.host_error, self.set_fault)
 
     def forward(self, x: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor, w13, w2, act: int,
                 scale: float, e_local: int, tables=None) -> torch.Tensor:
@@ -98,6 +101,12 @@ class LowLatencyEP:
 
     def error(self) -> int:
         return self._lib.ome_ep_error(self._ctx)
+
+    def host_error(self) -> int:
+        return self._lib.ome_ep_host_error(self._ctx) if self._ctx else 0
+
+    def set_fault(self, stall: int) -> int:
+        return self._lib.ome_ep_set_fault(self._ctx, int(stall)) if self._ctx else -1
 
     def close(self) -> None:
         if self._ctx:

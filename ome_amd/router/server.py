@@ -34,10 +34,17 @@ class Worker:
     errors: int = 0
     bootstrap_port: int | None = None
     info: dict = field(default_factory=dict)
+    added_at: float = field(default_factory=time.monotonic)
+    ever_ok: bool = False          # has any health probe succeeded (--worker-startup-timeout-secs)
 
     @property
     def host(self) -> str:
         return urlsplit(self.url).hostname or "127.0.0.1"
+
+    @property
+    def grpc(self) -> bool:
+        """A gRPC-mode engine (``--grpc-mode``: runtime/grpc_server.py), reached as grpc://host:port."""
+        return self.url.startswith("grpc://")
 
 
 def _selector_arg(parts: list[str] | None) -> str | None:
@@ -53,8 +60,13 @@ def _selector_arg(parts: list[str] | None) -> str | None:
 class Router:
     def __init__(self, policy: str = "cache_aware", pd: bool = False, health_interval: float = 5.0,
                  health_failures: int = 3, retries: int = 2, request_timeout: float = 3600.0,
-                 discovery: dict | None = None, pd_policy: str | None = None):
+                 discovery: dict | None = None, pd_policy: str | None = None, health_path: str = "/health",
+                 startup_timeout: float = 0.0, model_path: str | None = None):
         self.workers: dict[str, Worker] = {}
+        self.health_path = health_path if health_path.startswith("/") else "/" + health_path
+        self.startup_timeout = float(startup_timeout or 0.0)   # 0: never drop a slow-starting worker
+        self.model_path = model_path
+        self._grpc: dict = {}   # worker url -> grpc_server.SchedulerClient
         self.policy: Policy = make_policy(policy)
         self.prefill_policy: Policy = make_policy(pd_policy or policy)
         self.decode_policy: Policy = make_policy(pd_policy or policy)
@@ -77,8 +89,22 @@ class Router:
             log.info("added %s worker %s", role, url)
         return w
 
+    def _client(self, w: Worker):
+        c = self._grpc.get(w.url)
+        if c is None:
+            from ome_amd.runtime.grpc_server import SchedulerClient
+
+            c = self._grpc[w.url] = SchedulerClient(resolve_url(w.url.replace("grpc://", "http://")).split("://", 1)[1])
+        return c
+
     def remove_worker(self, url: str) -> None:
         url = url.rstrip("/")
+        c = self._grpc.pop(url, None)
+        if c is not None:
+            try:
+                asyncio.get_running_loop().create_task(c.close())
+            except RuntimeError:   # no loop (admin call from a plain thread): the channel is dropped
+                pass
         if self.workers.pop(url, None) is not None:
             for p in (self.policy, self.prefill_policy, self.decode_policy):
                 tree = getattr(p, "tree", None)
@@ -93,20 +119,38 @@ class Router:
 
     async def _probe(self, w: Worker) -> None:
         try:
-            async with self.session.get(resolve_url(w.url) + "/health", timeout=ClientTimeout(total=5)) as r:
-                ok = r.status == 200
-            if ok and w.role == "decode" and w.bootstrap_port is None:
-                async with self.session.get(resolve_url(w.url) + "/server_info", timeout=ClientTimeout(total=5)) as r:
-                    w.info = await r.json()
+            if w.grpc:
+                from ome_amd.runtime.grpc_server import SERVING
+
+                c = self._client(w)
+                if self.health_path.strip("/") == "HealthCheck":   # a one-token generation
+                    ok = bool((await c.call("HealthCheck", timeout=60)).get("healthy"))
+                else:
+                    ok = await c.health(timeout=5) == SERVING
+                if ok and w.role == "decode" and w.bootstrap_port is None:
+                    w.info = await c.call("GetServerInfo", timeout=5)
                     w.bootstrap_port = int(w.info.get("disaggregation_bootstrap_port") or 0) or None
+            else:
+                async with self.session.get(resolve_url(w.url) + self.health_path, timeout=ClientTimeout(total=5)) as r:
+                    ok = r.status == 200
+                if ok and w.role == "decode" and w.bootstrap_port is None:
+                    async with self.session.get(resolve_url(w.url) + "/server_info",
+                                                timeout=ClientTimeout(total=5)) as r:
+                        w.info = await r.json()
+                        w.bootstrap_port = int(w.info.get("disaggregation_bootstrap_port") or 0) or None
         except Exception:  # noqa: BLE001
             ok = False
         if ok:
-            w.fails, w.healthy = 0, True
+            w.fails, w.healthy, w.ever_ok = 0, True, True
         else:
             w.fails += 1
             if w.fails >= self.health_failures:
                 w.healthy = False
+            if not w.ever_ok and self.startup_timeout > 0 and \
+                    time.monotonic() - w.added_at > self.startup_timeout:
+                log.warning("worker %s not healthy %.0f s after it was added (--worker-startup-timeout-secs): "
+                            "dropped", w.url, self.startup_timeout)
+                self.remove_worker(w.url)
 
     async def _health_loop(self) -> None:
         while True:
@@ -134,9 +178,15 @@ class Router:
                 if not any(c.get("type") == "Ready" and c.get("status") == "True" for c in st.get("conditions") or []):
                     continue
                 port = d["port"]
+                # a container port named grpc* serves the gRPC-mode engine (the reference's grpc1)
+                scheme = "http"
+                for c in (p.get("spec") or {}).get("containers") or []:
+                    for cp in c.get("ports") or []:
+                        if int(cp.get("containerPort", -1)) == int(port) and str(cp.get("name", "")).startswith("grpc"):
+                            scheme = "grpc"
                 hp = json.loads((p["metadata"].get("annotations") or {}).get("ome.io/host-ports") or "{}")
                 port = hp.get(str(port), port)
-                u = f"http://{st.get('podIP') or '127.0.0.1'}:{port}"
+                u = f"{scheme}://{st.get('podIP') or '127.0.0.1'}:{port}"
                 seen.add(u)
                 self.add_worker(u, role)
         for u in [u for u in self.workers if u not in seen]:
@@ -159,6 +209,9 @@ class Router:
     async def stop(self, app=None) -> None:
         for t in self._tasks:
             t.cancel()
+        for c in list(self._grpc.values()):
+            await c.close()
+        self._grpc.clear()
         if self.session:
             await self.session.close()
 
@@ -170,7 +223,39 @@ class Router:
         p = body.get("prompt", body.get("text", body.get("input", "")))
         return p if isinstance(p, str) else json.dumps(p)[:4096]
 
+    async def _forward_grpc(self, request: web.Request, w: Worker, body: dict, stream: bool) -> web.StreamResponse:
+        """Same response as the HTTP path, carried over the worker's gRPC Generate stream."""
+        auth = {k: v for k, v in request.headers.items() if k.lower() == "authorization"}
+        resp = None
+        status, ctype, buf = 200, "application/json", []
+        async for kind, val in self._client(w).generate(request.path, body, headers=auth):
+            if kind == "start":
+                status, ctype = val
+                if stream and status == 200:
+                    resp = web.StreamResponse(status=200, headers={"Content-Type": ctype or "text/event-stream",
+                                                                   "Cache-Control": "no-cache"})
+                    await resp.prepare(request)
+            elif resp is not None:
+                await resp.write(val)
+            else:
+                buf.append(val)
+        if resp is not None:
+            await resp.write_eof()
+            return resp
+        return web.Response(body=b"".join(buf), status=status, content_type=(ctype or "application/json").split(";")[0])
+
     async def _forward(self, request: web.Request, w: Worker, body: dict, stream: bool) -> web.StreamResponse:
+        if w.grpc:
+            import grpc
+
+            w.inflight += 1
+            try:
+                return await self._forward_grpc(request, w, body, stream)
+            except grpc.aio.AioRpcError as e:   # transport failure: retried on another worker
+                raise ConnectionError(f"gRPC worker {w.url}: {e.code()}") from e
+            finally:
+                w.inflight -= 1
+                w.served += 1
         url = resolve_url(w.url) + request.path
         w.inflight += 1
         try:
@@ -240,6 +325,11 @@ class Router:
         async def run_prefill():
             p.inflight += 1
             try:
+                if p.grpc:
+                    async for kind, val in self._client(p).generate(request.path, pbody):
+                        if kind == "start" and val[0] != 200:
+                            log.warning("prefill worker %s returned %d", p.url, val[0])
+                    return
                 async with self.session.post(resolve_url(p.url) + request.path, json=pbody) as r:
                     await r.read()
                     if r.status != 200:
@@ -259,13 +349,22 @@ class Router:
     # ------------------------------------------------------------------ admin / info
     async def models(self, request):
         for w in self.workers.values():
+            if w.healthy and w.role in ("regular", "decode") and w.grpc:
+                try:
+                    info = await self._client(w).call("GetModelInfo", timeout=10)
+                    return web.json_response({"object": "list", "data": [
+                        {"id": info.get("served_model_name"), "object": "model", "owned_by": "ome_amd",
+                         "max_model_len": info.get("context_length")}]})
+                except Exception:  # noqa: BLE001
+                    continue
             if w.healthy and w.role in ("regular", "decode"):
                 try:
                     async with self.session.get(resolve_url(w.url) + "/v1/models") as r:
                         return web.json_response(await r.json(), status=r.status)
                 except Exception:  # noqa: BLE001
                     continue
-        return web.json_response({"object": "list", "data": []})
+        data = [{"id": self.model_path, "object": "model", "owned_by": "ome_amd"}] if self.model_path else []
+        return web.json_response({"object": "list", "data": data})
 
     async def readiness(self, request):
         ok = (self.healthy("prefill") and self.healthy("decode")) if self.pd else bool(self.healthy("regular"))
@@ -301,8 +400,9 @@ class Router:
         return web.Response(text="\n".join(lines) + "\n", content_type="text/plain")
 
 
-def create_app(router: Router) -> web.Application:
-    app = web.Application(client_max_size=64 << 20)
+def create_app(router: Router, max_payload: int = 256 << 20) -> web.Application:
+    # --max-payload-size: larger request bodies are refused with HTTP 413
+    app = web.Application(client_max_size=max_payload)
     for p in PROXIED:
         app.router.add_post(p, router.handle)
     app.router.add_get("/v1/models", router.models)
@@ -337,14 +437,25 @@ def build_parser() -> argparse.ArgumentParser:
     a("--health-check-interval-secs", type=float, default=5.0)
     a("--request-timeout-secs", type=float, default=3600.0)
     a("--cache-threshold", type=float, default=0.5)
+    a("--model-path", default=None, help="model id reported when no worker answers /v1/models")
+    a("--log-level", default="info")
+    a("--health-check-endpoint", default="/health", help="worker health path (HTTP) / gRPC method")
+    a("--max-payload-size", type=int, default=256 << 20, help="largest request body in bytes (413 above)")
+    a("--worker-startup-timeout-secs", type=float, default=0.0,
+      help="drop a worker that is not healthy this long after it was added (0: never)")
     return ap
 
 
 def main(argv=None) -> int:
-    args, unknown = build_parser().parse_known_args(argv)
-    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(name)s %(levelname)s %(message)s")
-    if unknown:
-        log.info("ignoring unsupported router flags: %s", unknown)
+    ap = build_parser()
+    args, unknown = ap.parse_known_args(argv)
+    logging.basicConfig(level=getattr(logging, str(args.log_level).upper(), logging.INFO),
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    if unknown:   # every reference router flag is handled (ome_amd/runtime/flags.py)
+        if os.environ.get("OME_ALLOW_UNKNOWN_FLAGS", "0") == "1":
+            log.warning("ignoring unsupported router flags: %s", unknown)
+        else:
+            ap.error(f"unsupported router flags: {' '.join(unknown)} (OME_ALLOW_UNKNOWN_FLAGS=1 to ignore)")
     disc = None
     if args.service_discovery:
         sels = ({"prefill": _selector_arg(args.prefill_selector), "decode": _selector_arg(args.decode_selector)}
@@ -352,12 +463,13 @@ def main(argv=None) -> int:
         disc = {"namespace": args.service_discovery_namespace, "port": args.service_discovery_port,
                 "selectors": sels, "interval": 5.0}
     r = Router(args.policy, pd=args.pd_disaggregation, health_interval=args.health_check_interval_secs,
-               request_timeout=args.request_timeout_secs, discovery=disc)
+               request_timeout=args.request_timeout_secs, discovery=disc, health_path=args.health_check_endpoint,
+               startup_timeout=args.worker_startup_timeout_secs, model_path=args.model_path)
     for u in args.worker_urls:
         r.add_worker(u)
     for p in args.prefill:
         r.add_worker(p[0], "prefill")
     for d in args.decode:
         r.add_worker(d, "decode")
-    web.run_app(create_app(r), host=args.host, port=args.port, print=None)
+    web.run_app(create_app(r, args.max_payload_size), host=args.host, port=args.port, print=None)
     return 0

@@ -86,6 +86,13 @@ class EngineArgs:
     eplb_rebalance_steps: int = 0          # EPLB: re-place experts from recorded loads every N lockstep steps
     enable_two_batch_overlap: bool = False # EP MoE: two micro-batches, all-to-alls overlapped with experts
     overlap_schedule: bool | None = None   # enqueue step k+1 before step k's tokens reach the host
+    watchdog_timeout: float = 300.0        # --watchdog-timeout: a loop phase older than this ends the
+                                           # process non-zero (0 disables; runtime/watchdog.py)
+    cuda_graph_bs: list | None = None      # --cuda-graph-bs: exact decode batch sizes to capture
+    tokenizer_path: str | None = None      # --tokenizer-path
+    dp_balance: str = "shortest_queue"     # --load-balance-method / --prefill-round-robin-balance
+    deepep_mode: str = "auto"              # --deepep-mode: normal = RCCL all_to_all only
+    decode_log_interval: int = 0           # --decode-log-interval: log decode throughput every N steps
                                            # (None = on for GPU engines)
     num_layers_override: int | None = None
     extra: dict = field(default_factory=dict)
@@ -114,6 +121,8 @@ class Engine:
         self.args = args
         self.cfg = args.model_config()
         dp = args.dp_size if args.enable_dp_attention else 1
+        if args.deepep_mode == "normal":   # RCCL all_to_all for every MoE exchange
+            os.environ["OME_EP_LL"] = "0"
         if args.tp_size > 1 or args.pp_size > 1 or dp > 1:
             pstate.init(args.tp_size, args.pp_size, dist_init_addr=args.dist_init_addr, dp_size=dp)
         self.pstate = pstate.get()
@@ -141,6 +150,7 @@ class Engine:
                                   max_total_tokens=args.max_total_tokens, max_running=args.max_running_requests,
                                   max_context=self.max_context, cuda_graph=args.cuda_graph,
                                   cuda_graph_max_bs=args.cuda_graph_max_bs, seed=args.seed,
+                                  cuda_graph_bs=args.cuda_graph_bs,
                                   kv_cache_dtype_name=args.kv_cache_dtype)
         self.runner.pp_microbatches = args.pp_microbatches
         prefix = None
@@ -151,7 +161,9 @@ class Engine:
             prefix = PrefixCache(self.runner.pages, args.page_size)
         self.scheduler = Scheduler(self.runner.pages, self.runner.slots, args.page_size, args.max_running_requests,
                                    args.chunked_prefill_size, self.max_context, args.enable_mixed_chunk, prefix)
-        self.tokenizer = get_tokenizer(args.model_path, self.cfg.vocab_size)
+        # TP / PP ranks schedule in lockstep on broadcast requests: no wall-clock decisions
+        self.scheduler.lockstep = self.pstate.world_size > 1 and not self.dp
+        self.tokenizer = get_tokenizer(args.tokenizer_path or args.model_path, self.cfg.vocab_size)
         eos = getattr(self.tokenizer, "eos_token_id", None)
         self.eos_ids = {eos} if eos is not None else set()
         self.metrics = EngineMetrics()
@@ -166,6 +178,12 @@ class Engine:
         self.kv_transfer = None  # PD disaggregation hook (ome_amd.runtime.disagg)
         # what a failed lockstep step does to a multi-rank group (tests replace it)
         self.on_fatal = lambda: os._exit(70)
+        # engine watchdog (--watchdog-timeout) + collective expiry / fault-injection hooks
+        from ome_amd.runtime import watchdog as _wd
+
+        self._wd_mod = _wd
+        self.watchdog = _wd.Watchdog(args.watchdog_timeout, self.pstate.rank) if args.watchdog_timeout > 0 else None
+        self._fault = _wd.parse_fault()
         # overlapped scheduling: (batch, handle, launch time) of the step whose tokens are in flight
         self._inflight = None
         # host-side time split of the serving loop (seconds, cumulative): schedule / launch
@@ -304,13 +322,41 @@ class Engine:
             reqs.append(r)
         return reqs, obj[0][1]
 
-    def _dp_assign(self) -> int:
-        """Rank 0: the DP rank with the fewest outstanding requests (round-robin on ties)."""
+    def _log_decode(self, rows: int, now: float) -> None:
+        """--decode-log-interval: one SGLang-style throughput line every N decode steps."""
+        st = self.__dict__.setdefault("_dlog", {"n": 0, "tok": 0, "t": now})
+        st["n"] += 1
+        st["tok"] += rows
+        if st["n"] < self.args.decode_log_interval:
+            return
+        dt = max(now - st["t"], 1e-9)
+        log.info("Decode batch. #running-req: %d, #token: %d, token usage: %.2f, gen throughput (token/s): %.2f, "
+                 "#queue-req: %d", self.scheduler.num_running,
+                 (self.runner.pages.num_pages - 1 - self.runner.pages.num_free) * self.args.page_size,
+                 self.runner.pages.usage(), st["tok"] / dt, self.scheduler.num_waiting)
+        st.update(n=0, tok=0, t=now)
+
+    def _dp_assign(self, req=None) -> int:
+        """Rank 0: the DP rank that serves a new request (``--load-balance-method``):
+        shortest_queue (default) = fewest outstanding requests, minimum_tokens = fewest outstanding
+        prompt + output tokens, round_robin (also ``--prefill-round-robin-balance``) = strict
+        rotation.  Ties rotate."""
         n = self.pstate.dp_size
+        how = self.args.dp_balance
+        if how == "round_robin":
+            best = self._dp_next
+            self._dp_next = (best + 1) % n
+            return best
         load = [0] * n
-        load[0] = len(self.scheduler.running) + len(self.scheduler.waiting)
-        for r in self._remote.values():
-            load[r.dp_rank] += 1
+        mine = list(self.scheduler.running) + list(self.scheduler.waiting)
+        if how == "minimum_tokens":
+            load[0] = sum(r.seq_len + r.params.max_new_tokens for r in mine)
+            for r in self._remote.values():
+                load[r.dp_rank] += len(r.prompt_ids) + r.params.max_new_tokens
+        else:
+            load[0] = len(mine)
+            for r in self._remote.values():
+                load[r.dp_rank] += 1
         best = min(range(n), key=lambda i: (load[i], (i - self._dp_next) % n))
         self._dp_next = (best + 1) % n
         return best
@@ -336,9 +382,23 @@ class Engine:
         device output (``ModelRunner.launch(prev=...)``) — so host-side scheduling, input packing
         and detokenisation hide behind the GPU.  Returned requests are those finished by step k.
         """
+        wd = self.watchdog
+        if wd is not None:
+            wd.enter("control")
+        if self._fault is not None:
+            self._wd_mod.maybe_inject(self.pstate.rank, self.step_count, self._fault)
+        try:
+            return self._step(wd)
+        finally:
+            if wd is not None:
+                wd.idle()
+
+    def _step(self, wd) -> list[Request]:
         self._drain_inbox()
         if self._stop and self.pstate.world_size > 1:
             return []   # the leader's stop broadcast: it runs no further lockstep step
+        if wd is not None:
+            wd.enter("schedule")
         if self.kv_transfer is not None and self.kv_transfer.mode == "decode":
             self.kv_transfer.poll()
         if self.cfg.is_embedding:
@@ -355,6 +415,8 @@ class Engine:
         launched = None
         if batch is not None:
             t0 = time.perf_counter()
+            if wd is not None:
+                wd.enter("launch")
             handle = self.runner.launch(batch, prev[1] if prev else None)
             self.scheduler.launch_commit(batch)
             launched = (batch, handle, t0)
@@ -378,11 +440,22 @@ class Engine:
     def _complete(self, batch, handle, t0) -> list[Request]:
         ht = self.host_times
         tw = time.perf_counter()
+        wd = self.watchdog
+        if wd is not None:
+            wd.enter(f"wait ({batch.mode}, {len(batch.chunks)} rows)")
         ids, lps = handle.result()
+        if self.pstate.world_size > 1:
+            # a bounded collective wait that expired leaves the step's output garbage: fail loudly
+            # (run_forever turns this into a non-zero exit of the whole lockstep group)
+            self._wd_mod.check_comms()
+        if wd is not None:
+            wd.enter("commit")
         now = time.perf_counter()
         done = self.scheduler.final_commit(batch, ids, lps, now, self.eos_ids)
         self.step_count += 1
         self.metrics.on_step(batch, now - t0, done, self.scheduler, self.runner.pages)
+        if self.args.decode_log_interval > 0 and batch.mode == "decode":
+            self._log_decode(len(batch.chunks), now)
         ht["wait"] += now - tw
         if self.host_trace is not None:
             self.host_trace.append(("wait", 0, now - tw, time.perf_counter() - now))
@@ -605,6 +678,8 @@ class Engine:
         return t
 
     def shutdown(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.stop()
         if self.pstate.world_size > 1 and self.pstate.rank == 0:
             self._stop_pending = True  # the loop broadcasts it on its next step, then exits
         else:

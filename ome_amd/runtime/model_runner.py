@@ -144,7 +144,7 @@ class ModelRunner:
                  model_path: str | None = None, load_format: str = "auto", page_size: int = 16,
                  mem_fraction_static: float = 0.9, max_total_tokens: int | None = None, max_running: int = 256,
                  max_context: int = 8192, cuda_graph: bool = True, cuda_graph_max_bs: int | None = None,
-                 seed: int = 0, kv_cache_dtype_name: str = "auto"):
+                 seed: int = 0, kv_cache_dtype_name: str = "auto", cuda_graph_bs: list | None = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -222,9 +222,14 @@ class ModelRunner:
         log.info("KV cache: %d pages x %d tokens (%.1f GiB), weights %.1f GiB", num_pages, page_size,
                  num_pages * page_bytes / 2**30, self.model.weight_bytes() / 2**30)
         # ---- decode graphs ----
-        self.bmax = max(2, cuda_graph_max_bs or max_running)
-        self.bmax += self.bmax % 2
-        self.buckets = default_buckets(self.bmax)
+        if cuda_graph_bs:   # --cuda-graph-bs: exactly these decode batch sizes get graphs
+            self.bmax = max(2, min(max(cuda_graph_bs), max_running))
+            self.bmax += self.bmax % 2
+            self.buckets = sorted({min(int(b), self.bmax) for b in cuda_graph_bs})
+        else:
+            self.bmax = max(2, cuda_graph_max_bs or max_running)
+            self.bmax += self.bmax % 2
+            self.buckets = default_buckets(self.bmax)
         if self.buckets[-1] < self.bmax:
             self.buckets.append(self.bmax)
         if self.tbo:   # every graph splits into two non-empty halves

@@ -77,11 +77,29 @@ class Scheduler:
         # (and any preempted one) goes first, so long prompts cannot starve.  "fifo" = arrival order.
         self.policy = os.environ.get("OME_SCHED_POLICY", "sjf")
         self.sjf_age_s = float(os.environ.get("OME_SJF_AGE_MS", "500")) / 1000.0
+        # Lockstep mode (TP / PP: every rank runs its own copy of this scheduler on the requests
+        # rank 0 broadcasts, and all ranks must pick the SAME batch): every time-based decision
+        # (SJF aging, prefill batching hold) counts schedule() calls since the request was
+        # enqueued instead of reading the wall clock -- followers rebuild a request later than the
+        # leader and read their clocks at different moments, so a time test can flip between ranks
+        # and desynchronise the collectives.  ~30 steps ~ the 500 ms default at 16 ms per step.
+        self.lockstep = False
+        self.n_sched = 0
+        self.sjf_age_steps = int(os.environ.get("OME_SJF_AGE_STEPS", "32"))
+        self.prefill_max_wait_steps = int(os.environ.get("OME_PREFILL_MAX_WAIT_STEPS", "3"))
 
     # ------------------------------------------------------------------ queue ops
     def add(self, req: Request) -> None:
         req.state = ReqState.WAITING
+        req.enq_step = self.n_sched
         self.waiting.append(req)
+
+    def _waited(self, req: Request, seconds: float, steps: int) -> bool:
+        """Has ``req`` waited longer than the bound?  Step-counted in lockstep mode (identical on
+        every rank), wall clock otherwise."""
+        if self.lockstep:
+            return self.n_sched - getattr(req, "enq_step", self.n_sched) > steps
+        return time.perf_counter() - req.arrival_time > seconds
 
     def abort(self, rid: str) -> Request | None:
         for q in (self.waiting, self.running):
@@ -170,6 +188,7 @@ class Scheduler:
 
     # ------------------------------------------------------------------ schedule
     def schedule(self) -> StepBatch | None:
+        self.n_sched += 1
         batch = self._schedule_prefill()
         if batch is not None:
             if self.mixed:
@@ -194,7 +213,7 @@ class Scheduler:
     def _next_waiting(self) -> Request:
         head = self.waiting[0]
         if self.policy != "sjf" or len(self.waiting) == 1 or head.preempted or \
-                time.perf_counter() - head.arrival_time > self.sjf_age_s:
+                self._waited(head, self.sjf_age_s, self.sjf_age_steps):
             return head
         return min(self.waiting, key=lambda r: (not r.preempted, r.seq_len - r.num_cached))
 
@@ -215,7 +234,7 @@ class Scheduler:
         if self.prefill_batch_tokens and not chunks and self.running and self.waiting:
             pending = sum(r.seq_len - r.num_cached for r in self.waiting)
             if pending < min(self.prefill_batch_tokens, budget) and \
-                    time.perf_counter() - self.waiting[0].arrival_time < self.prefill_max_wait_s:
+                    not self._waited(self.waiting[0], self.prefill_max_wait_s, self.prefill_max_wait_steps):
                 return None
         while self.waiting and budget > 0 and len(self.running) < self.max_running:
             r = self._next_waiting()

@@ -91,7 +91,92 @@ def build_parser() -> argparse.ArgumentParser:
     a("--reasoning-parser", default=None, help="deepseek-r1 | qwen3 | nano_v3 | gpt-oss")
     a("--enable-auto-tool-choice", action="store_true", help="accepted (tool_choice=auto is the default)")
     a("--chat-template", default=None, help="path of a Jinja chat template replacing the tokenizer's")
+    # ---- the rest of the reference runtimes' flags (ome_amd/runtime/flags.py has the table)
+    a("--tokenizer-path", default=None, help="tokenizer directory / file (default: the model's)")
+    a("--grpc-mode", action="store_true",
+      help="serve sglang.grpc.scheduler.SglangScheduler + grpc.health.v1 over gRPC on --port (no HTTP)")
+    a("--watchdog-timeout", type=float, default=300.0,
+      help="seconds an engine phase may take before the process exits non-zero (0 disables)")
+    a("--log-requests-level", type=int, default=0, choices=[0, 1, 2, 3])
+    a("--max-log-len", type=int, default=None, help="truncate logged request text to this many characters")
+    a("--log-level", default="info")
+    a("--middleware", action="append", default=[], help="vllm...middleware.log_opc_header only")
+    a("--cuda-graph-bs", nargs="+", type=int, default=None, help="decode batch sizes captured as HIP graphs")
+    a("--cuda-graph-sizes", nargs="+", type=int, default=None, help="vLLM spelling of --cuda-graph-bs")
+    a("--enforce-eager", action="store_true", help="vLLM spelling of --disable-cuda-graph")
+    a("--enable-dp-lm-head", action="store_true", help="requires --enable-dp-attention (per-rank LM head)")
+    a("--moe-dense-tp-size", type=int, default=None, help="only 1, with --enable-dp-attention")
+    a("--load-balance-method", default="shortest_queue", choices=["round_robin", "shortest_queue", "minimum_tokens"])
+    a("--prefill-round-robin-balance", action="store_true")
+    a("--preemption-mode", default="recompute", choices=["recompute", "swap"])
+    a("--limit-mm-per-prompt", default=None, help="image=N (or JSON {\"image\": N})")
+    a("--deepep-mode", default="auto", choices=["auto", "normal", "low_latency"])
+    a("--enable-deepep-moe", action="store_true", help="older spelling of --moe-a2a-backend deepep")
+    a("--decode-log-interval", type=int, default=0, help="log decode throughput every N decode steps (0: off)")
+    # accepted with no effect on purpose (reasons: ome_amd/runtime/flags.py)
+    a("--trust-remote-code", action="store_true")
+    a("--skip-server-warmup", action="store_true")
+    a("--enable-chunked-prefill", action="store_true")
+    a("--enable-multimodal", action="store_true")
+    a("--disable-fast-image-processor", action="store_true")
+    a("--attention-backend", default=None)
+    a("--mm-attention-backend", default=None)
+    a("--enable-torch-compile", action="store_true")
+    a("--torch-compile-max-bs", type=int, default=None)
+    a("--disable-shared-experts-fusion", action="store_true")
+    a("--disaggregation-ib-device", default=None)
     return ap
+
+
+def validate_args(ns, ap: argparse.ArgumentParser | None = None) -> None:
+    """Reject reference flag values this framework cannot honour (instead of silently serving
+    something else); normalise aliases.  ``ap.error`` exits 2 like any argparse error."""
+    def bad(msg):
+        if ap is not None:
+            ap.error(msg)
+        raise ValueError(msg)
+
+    if ns.enable_dp_lm_head and not ns.enable_dp_attention:
+        bad("--enable-dp-lm-head requires --enable-dp-attention")
+    if ns.moe_dense_tp_size not in (None, 1):
+        bad(f"--moe-dense-tp-size {ns.moe_dense_tp_size}: only 1 is supported (dense MLPs data-parallel)")
+    if ns.moe_dense_tp_size == 1 and not ns.enable_dp_attention and ns.tp_size > 1:
+        bad("--moe-dense-tp-size 1 requires --enable-dp-attention (dense layers are tensor-parallel otherwise)")
+    for m in ns.middleware:
+        if not m.endswith("log_opc_header"):
+            bad(f"--middleware {m}: only the opc-request-id logging middleware is available")
+    if ns.enable_deepep_moe:
+        ns.moe_a2a_backend = "deepep"
+    if ns.enforce_eager:
+        ns.disable_cuda_graph = True
+    if ns.cuda_graph_bs is None and ns.cuda_graph_sizes:
+        ns.cuda_graph_bs = ns.cuda_graph_sizes
+    if ns.cuda_graph_bs and min(ns.cuda_graph_bs) <= 0:
+        bad("--cuda-graph-bs: batch sizes must be positive")
+    if ns.limit_mm_per_prompt is not None:
+        ns.mm_limit = parse_mm_limit(ns.limit_mm_per_prompt)
+        if ns.mm_limit is None:
+            bad(f"--limit-mm-per-prompt {ns.limit_mm_per_prompt!r}: expected image=N or JSON")
+    else:
+        ns.mm_limit = None
+    if ns.preemption_mode == "swap":
+        log.info("--preemption-mode swap: preempted requests recompute (KV swap to host is not implemented; "
+                 "288 GB of HBM keeps preemption rare)")
+
+
+def parse_mm_limit(v: str) -> int | None:
+    """``image=4`` / ``{"image": 4}`` -> 4 (max images per prompt)."""
+    v = v.strip()
+    try:
+        if v.startswith("{"):
+            d = json.loads(v)
+            return int(d.get("image", d.get("images")))
+        k, _, n = v.partition("=")
+        if k.strip() in ("image", "images"):
+            return int(n)
+    except (ValueError, TypeError, json.JSONDecodeError):
+        return None
+    return None
 
 
 def engine_args_from(ns, rank_tp: int | None = None):
@@ -122,7 +207,14 @@ def engine_args_from(ns, rank_tp: int | None = None):
                       dist_init_addr=ns.dist_init_addr, nnodes=ns.nnodes,
                       node_rank=ns.node_rank, disaggregation_mode=ns.disaggregation_mode,
                       num_layers_override=ns.num_layers,
-                      overlap_schedule=False if ns.disable_overlap_schedule else None)
+                      overlap_schedule=False if ns.disable_overlap_schedule else None,
+                      watchdog_timeout=getattr(ns, "watchdog_timeout", 300.0),
+                      cuda_graph_bs=getattr(ns, "cuda_graph_bs", None),
+                      tokenizer_path=getattr(ns, "tokenizer_path", None),
+                      dp_balance=("round_robin" if getattr(ns, "prefill_round_robin_balance", False)
+                                  else getattr(ns, "load_balance_method", "shortest_queue")),
+                      deepep_mode=getattr(ns, "deepep_mode", "auto"),
+                      decode_log_interval=getattr(ns, "decode_log_interval", 0))
 
 
 # ------------------------------------------------------------------ request plumbing
@@ -227,6 +319,42 @@ def create_app(engine, ns=None):
     created = int(time.time())
     default_max = 128
     app.state.engine = engine
+    # --log-requests (+ --log-requests-level / --max-log-len), --limit-mm-per-prompt, --middleware
+    log_req = bool(getattr(ns, "log_requests", False)) if ns is not None else False
+    log_level = int(getattr(ns, "log_requests_level", 0) or 0) if ns is not None else 0
+    log_len = getattr(ns, "max_log_len", None) if ns is not None else None
+    mm_limit = getattr(ns, "mm_limit", None) if ns is not None else None
+    rlog = logging.getLogger("ome_amd.requests")
+
+    def _clip(text: str) -> str:
+        return text if log_len is None or len(text) <= log_len else text[:log_len] + f"...(+{len(text) - log_len})"
+
+    def _log_in(req) -> None:
+        msg = f"request {req.rid}: prompt_tokens={len(req.prompt_ids)} max_new_tokens={req.params.max_new_tokens}"
+        if log_level >= 1:
+            msg += f" params={req.params}"
+        if log_level >= 2:
+            msg += f" prompt={_clip(tok.decode(req.prompt_ids))!r}"
+        rlog.info(msg)
+
+    def _log_out(req) -> None:
+        msg = (f"finished {req.rid}: output_tokens={len(req.output_ids)} reason={req.finish_reason} "
+               f"ttft={req.ttft}")
+        if log_level >= 2:
+            msg += f" output={_clip(tok.decode(req.output_ids))!r}"
+        rlog.info(msg)
+
+    for mw in (getattr(ns, "middleware", None) or []) if ns is not None else []:
+        if mw.endswith("log_opc_header"):   # vLLM's OCI middleware: log the opc-request-id header
+            @app.middleware("http")
+            async def _opc(request, call_next):
+                oid = request.headers.get("opc-request-id")
+                if oid:
+                    rlog.info("opc-request-id %s %s %s", oid, request.method, request.url.path)
+                resp = await call_next(request)
+                if oid:
+                    resp.headers["opc-request-id"] = oid
+                return resp
 
     def err(code: int, msg: str, typ: str = "invalid_request_error"):
         return JSONResponse({"error": {"message": msg, "type": typ, "code": code}}, status_code=code)
@@ -236,10 +364,22 @@ def create_app(engine, ns=None):
         stream = _Stream(loop)
         if bootstrap and bootstrap.get("disagg_role") == "prefill":
             params.max_new_tokens = 1  # the prefill engine only produces the first token + KV
+        if images and mm_limit is not None and len(images) > mm_limit:
+            raise ValueError(f"{len(images)} images in the prompt; this server accepts at most {mm_limit} "
+                             f"(--limit-mm-per-prompt)")
         if images:
             req = engine.make_mm_request(prompt_ids, images, params, on_token=stream, bootstrap=bootstrap)
         else:
             req = engine.make_request(prompt_ids, params, on_token=stream, bootstrap=bootstrap)
+        if log_req:
+            _log_in(req)
+            inner = req.on_token
+
+            def on_token(r, toks, fin, _inner=inner):
+                if fin:
+                    _log_out(r)
+                return _inner(r, toks, fin)
+            req.on_token = on_token
         engine.add_request(req)
         return req, stream
 
@@ -250,6 +390,7 @@ def create_app(engine, ns=None):
                                          "bootstrap_prefill")} | {"room": int(body["bootstrap_room"])}
 
     @app.get("/health")
+    @app.get("/HealthCheck")   # the reference routers' --health-check-endpoint spelling
     async def health():
         return {"status": "ok", **engine.health()}
 
@@ -748,7 +889,14 @@ def main(argv=None) -> int:
     ap = build_parser()
     ns, unknown = ap.parse_known_args(argv)
     if unknown:
-        log.warning("ignoring unsupported flags: %s", " ".join(unknown))
+        # every flag of the reference runtimes is either implemented or an explicit no-op
+        # (ome_amd/runtime/flags.py); anything else would silently change what was asked for
+        if os.environ.get("OME_ALLOW_UNKNOWN_FLAGS", "0") == "1":
+            log.warning("ignoring unsupported flags: %s", " ".join(unknown))
+        else:
+            ap.error(f"unsupported flags: {' '.join(unknown)} (OME_ALLOW_UNKNOWN_FLAGS=1 to ignore)")
+    validate_args(ns, ap)
+    logging.getLogger().setLevel(getattr(logging, str(ns.log_level).upper(), logging.INFO))
     world = (ns.dp_size if ns.enable_dp_attention and ns.tp_size == 1 else ns.tp_size) * ns.pp_size
     if ns.distributed_executor_backend == "ray" and world > 1 and ns.nnodes == 1:
         _ray_group(ns, argv if argv is not None else sys.argv[1:], world)
@@ -781,6 +929,11 @@ def main(argv=None) -> int:
         async def h():
             return {"status": "ok", "rank": base_rank}
 
+        if ns.grpc_mode:   # worker pods of a gRPC runtime answer the same grpc.health.v1 probes
+            from ome_amd.runtime import grpc_server
+
+            asyncio.run(grpc_server.serve(app, eng, ns.host, ns.port))
+            return 0
         uvicorn.run(app, host=ns.host, port=ns.port, log_level="warning")
         return 0
     eng = Engine(engine_args_from(ns))
@@ -790,10 +943,19 @@ def main(argv=None) -> int:
         attach_kv_transfer(eng, ns.disaggregation_mode, ns.disaggregation_bootstrap_port)
     eng.start()
     app = create_app(eng, ns)
-    import uvicorn
+    if ns.grpc_mode:
+        from ome_amd.runtime import grpc_server
 
-    log.info("serving %s on %s:%d (tp=%d)", eng.served_model_name, ns.host, ns.port, ns.tp_size)
-    uvicorn.run(app, host=ns.host, port=ns.port, log_level="warning")
+        log.info("serving %s over gRPC on %s:%d (tp=%d)", eng.served_model_name, ns.host, ns.port, ns.tp_size)
+        try:
+            asyncio.run(grpc_server.serve(app, eng, ns.host, ns.port))
+        except KeyboardInterrupt:
+            pass
+    else:
+        import uvicorn
+
+        log.info("serving %s on %s:%d (tp=%d)", eng.served_model_name, ns.host, ns.port, ns.tp_size)
+        uvicorn.run(app, host=ns.host, port=ns.port, log_level="warning")
     eng.shutdown()
     for p in procs:
         p.terminate()
