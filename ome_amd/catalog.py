@@ -43,13 +43,14 @@ class Family:
     min_tp: int = 1           # e.g. DP attention over a whole node
     diffusion: str | None = None   # diffusers pipeline class: served by ome_amd.diffusion.server
     runtime: bool | None = None    # emit a runtime; None = only if no earlier family's runtime covers it
+    grpc: bool = False        # also emit a gRPC-mode runtime (engine --grpc-mode, grpc.health.v1 probes)
 
 
 FAMILIES: list[Family] = [
     Family("llama-3-8b-instruct", "meta", "meta-llama/Meta-Llama-3-8B-Instruct", "LlamaForCausalLM", 8.0,
            "llama-3-8b", pd=True),
     Family("llama-3-1-8b-instruct", "meta", "meta-llama/Llama-3.1-8B-Instruct", "LlamaForCausalLM", 8.0,
-           "llama-3.1-8b", args=['--tool-call-parser', 'llama3_json'], pd=True),
+           "llama-3.1-8b", args=['--tool-call-parser', 'llama3_json'], pd=True, grpc=True),
     Family("llama-3-70b-instruct", "meta", "meta-llama/Meta-Llama-3-70B-Instruct", "LlamaForCausalLM", 70.6,
            "llama-3-70b", pd=True),
     Family("llama-3-1-405b-instruct-fp8", "meta", "meta-llama/Llama-3.1-405B-Instruct-FP8", "LlamaForCausalLM",
@@ -59,7 +60,8 @@ FAMILIES: list[Family] = [
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], args=['--tool-call-parser', 'pythonic'], pd=True),
     Family("llama-4-maverick-17b-128e-instruct-fp8", "meta", "meta-llama/Llama-4-Maverick-17B-128E-Instruct-FP8",
            "Llama4ForConditionalGeneration", 402.0, None, 1.0, quantization="fp8",
-           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], args=['--tool-call-parser', 'pythonic'], pd=True),
+           capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"], args=['--tool-call-parser', 'pythonic'], pd=True,
+           grpc=True),
     Family("mistral-7b-instruct", "mistralai", "mistralai/Mistral-7B-Instruct-v0.3", "MistralForCausalLM", 7.2, pd=True),
     Family("mixtral-8x7b-instruct", "mistralai", "mistralai/Mixtral-8x7B-Instruct-v0.1", "MixtralForCausalLM",
            46.7, "mixtral-8x7b", pd=True),
@@ -128,8 +130,8 @@ FAMILIES: list[Family] = [
            args=["--enable-dp-attention", "--dp", "8"], quantization="fp8", multinode=2, min_tp=8, pd=True),
     Family("kimi-k2-instruct", "moonshotai", "moonshotai/Kimi-K2-Instruct", "DeepseekV3ForCausalLM", 1026.0, None,
            1.0, quantization="fp8", pd=True, multinode=2),
-    Family("gpt-oss-20b", "openai", "openai/gpt-oss-20b", "GptOssForCausalLM", 20.9, "gpt-oss-20b", args=['--tool-call-parser', 'gpt-oss', '--reasoning-parser', 'gpt-oss']),
-    Family("gpt-oss-120b", "openai", "openai/gpt-oss-120b", "GptOssForCausalLM", 117.0, args=['--tool-call-parser', 'gpt-oss', '--reasoning-parser', 'gpt-oss']),
+    Family("gpt-oss-20b", "openai", "openai/gpt-oss-20b", "GptOssForCausalLM", 20.9, "gpt-oss-20b", args=['--tool-call-parser', 'gpt-oss', '--reasoning-parser', 'gpt-oss'], grpc=True),
+    Family("gpt-oss-120b", "openai", "openai/gpt-oss-120b", "GptOssForCausalLM", 117.0, args=['--tool-call-parser', 'gpt-oss', '--reasoning-parser', 'gpt-oss'], grpc=True),
     Family("gemma-2-9b-it", "google", "google/gemma-2-9b-it", "Gemma2ForCausalLM", 9.2, "gemma-2-9b"),
     Family("gemma-3-27b-it", "google", "google/gemma-3-27b-it", "Gemma3ForConditionalGeneration", 27.4,
            capabilities=["TEXT_TO_TEXT", "IMAGE_TEXT_TO_TEXT"]),
@@ -538,6 +540,61 @@ def pd_runtime(f: Family) -> dict:
             "metadata": {"name": f"ome-amd-{f.name}-pd-tp{tp}"}, "spec": spec}
 
 
+GRPC_SERVICE = "sglang.grpc.scheduler.SglangScheduler"
+
+
+def _grpc_container(f: Family, tp: int, args: list[str]) -> dict:
+    """The engine container of a gRPC-mode runtime (reference ``srt/gpt-oss-120b-rt.yaml:61-130``):
+    port ``grpc1``; grpc.health.v1 probes -- service "" for liveness / startup, the scheduler
+    service for readiness (runtime/grpc_server.py)."""
+    c = _container(f, tp, args + ["--grpc-mode"])
+    c["ports"] = [{"containerPort": 8080, "name": "grpc1", "protocol": "TCP"}]
+
+    def g(service, **kw):
+        return {"grpc": {"port": 8080, "service": service}, **kw}
+
+    c["livenessProbe"] = g("", failureThreshold=5, successThreshold=1, periodSeconds=60, timeoutSeconds=60)
+    c["readinessProbe"] = g(GRPC_SERVICE, initialDelaySeconds=60, failureThreshold=3, successThreshold=1,
+                            periodSeconds=60, timeoutSeconds=200)
+    c["startupProbe"] = g("", failureThreshold=150, successThreshold=1, periodSeconds=6, initialDelaySeconds=60,
+                          timeoutSeconds=30)
+    return c
+
+
+def _grpc_router(pd: bool = False) -> dict:
+    r = _router()
+    r["runner"]["command"] += ["--health-check-endpoint", "/HealthCheck"] + (["--pd-disaggregation"] if pd else [])
+    return r
+
+
+def grpc_runtime(f: Family) -> dict:
+    """Engine behind gRPC (``--grpc-mode``), reached by the router over gRPC (opt-in by name)."""
+    tp = tp_for(f)
+    spec = _spec_base(f)
+    spec["supportedModelFormats"][0]["autoSelect"] = False
+    spec["engineConfig"] = {"volumes": [{"name": "dshm", "emptyDir": {"medium": "Memory"}}],
+                            "runner": _grpc_container(f, tp, server_args(f, tp))}
+    spec["routerConfig"] = _grpc_router()
+    return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterServingRuntime",
+            "metadata": {"name": f"ome-amd-{f.name}-grpc-tp{tp}"}, "spec": spec}
+
+
+def pd_grpc_runtime(f: Family) -> dict:
+    """PD disaggregation with both roles behind gRPC (reference ``...-fp8-pd-grpc-rt.yaml``)."""
+    tp = tp_for(f)
+    spec = _spec_base(f)
+    spec["supportedModelFormats"][0]["priority"] = 1
+    spec["supportedModelFormats"][0]["autoSelect"] = False
+    vol = [{"name": "dshm", "emptyDir": {"medium": "Memory"}}]
+    spec["engineConfig"] = {"volumes": vol, "runner": _grpc_container(
+        f, tp, server_args(f, tp, ["--disaggregation-mode", "prefill", "--disaggregation-bootstrap-port", "8998"]))}
+    spec["decoderConfig"] = {"volumes": vol, "runner": _grpc_container(
+        f, tp, server_args(f, tp, ["--disaggregation-mode", "decode"]))}
+    spec["routerConfig"] = _grpc_router(pd=True)
+    return {"apiVersion": "ome.io/v1beta1", "kind": "ClusterServingRuntime",
+            "metadata": {"name": f"ome-amd-{f.name}-pd-grpc-tp{tp}"}, "spec": spec}
+
+
 def multinode_runtime(f: Family) -> dict:
     """Leader/worker (LeaderWorkerSet) serving over ``f.multinode`` nodes of 8 GPUs (TP across the
     nodes, the checkpoint's own precision: the family's model must admit to it)."""
@@ -645,6 +702,10 @@ def generate() -> tuple[dict[str, list[dict]], dict[str, list[dict]]]:
             docs.append(pd_runtime(f))
         if f.multinode:
             docs.append(multinode_runtime(f))
+        if f.grpc:
+            docs.append(grpc_runtime(f))
+            if f.pd:
+                docs.append(pd_grpc_runtime(f))
         rts[f.name] = docs
     return rts, models
 

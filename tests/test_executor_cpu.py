@@ -103,3 +103,35 @@ def test_promql_subset_and_keda_math():
     assert PromQL("sum(rate(vllm:request_success_total[1m]) > bool 0.50) * 2").eval(h, now=1060) == 2.0
     assert desired_from_keda(30.0, 10.0, 1) == 3
     assert parse_prom_text('a{x="1"} 2\na{x="2"} 3\n# c\nb 1e3\n') == {"a": 5.0, "b": 1000.0}
+
+
+def test_lws_group_restart_when_a_rank_watchdog_exits(cluster, tmp_path):
+    """A rank that detects a collective expiry exits with EXIT_COLLECTIVE on its own (the engine
+    watchdog, runtime/watchdog.py); the LWS RecreateGroupOnPodRestart path then rebuilds the whole
+    group, exactly as for a killed rank."""
+    from ome_amd.runtime.watchdog import EXIT_COLLECTIVE
+
+    marker = tmp_path / "fired-once"
+    code = ("import os, time\n"
+            f"m = {str(marker)!r}\n"
+            "if os.environ.get('LWS_WORKER_INDEX', '0') != '0' and not os.path.exists(m):\n"
+            "    open(m, 'w').close()\n"
+            "    from ome_amd.runtime import watchdog as W\n"
+            "    W.register_comm('allreduce(rank 1/2)', lambda: 1)\n"
+            "    W.Watchdog(60.0, rank=1, poll_s=0.05)\n"
+            "time.sleep(600)\n")
+    c = {"name": "c", "image": "busybox", "command": [PY, "-c", code]}
+    tmpl = {"metadata": {"labels": {"app": "w"}}, "spec": {"containers": [c]}}
+    cluster.apply([{"apiVersion": "leaderworkerset.x-k8s.io/v1", "kind": "LeaderWorkerSet",
+                    "metadata": {"name": "wd", "namespace": "default"},
+                    "spec": {"replicas": 1, "leaderWorkerTemplate": {
+                        "size": 2, "restartPolicy": "RecreateGroupOnPodRestart",
+                        "leaderTemplate": tmpl, "workerTemplate": tmpl}}}])
+    pods = lambda: {p["metadata"]["name"]: p for p in cluster.store.list("v1", "Pod", "default")}  # noqa: E731
+    assert _wait(cluster, lambda: len(pods()) == 2 and marker.exists(), timeout=40)
+    first = {n: p["metadata"]["uid"] for n, p in pods().items()}
+    # the worker exited 75 (its container restart is recorded) and the group was recreated
+    assert _wait(cluster, lambda: len(pods()) == 2 and all(p["metadata"]["uid"] != first.get(n)
+                                                             for n, p in pods().items())
+                 and all(_ready(p) for p in pods().values()), timeout=60)
+    assert EXIT_COLLECTIVE == 75

@@ -199,3 +199,32 @@ def test_executor_grpc_probe_is_a_health_check(grpc_engine):
             ports = {8080: s.getsockname()[1]}
 
         assert not k._probe_once({"grpc": {"port": 8080}, "timeoutSeconds": 1}, _Run2(), _CR())
+
+
+def test_catalog_has_grpc_counterparts_of_the_reference_grpc_runtimes():
+    """The reference's gRPC runtimes (gpt-oss-20b / -120b, Llama-3.1-8B, Llama-4-Maverick FP8 and its
+    PD variant) each have a generated counterpart: engine --grpc-mode on port grpc1 with
+    grpc.health.v1 probes, router with --health-check-endpoint /HealthCheck; every one of them
+    passes the runtime admission webhook."""
+    from ome_amd import catalog
+
+    rts, _ = catalog.generate()
+    docs = {d["metadata"]["name"]: d for ds in rts.values() for d in ds}
+    want = {"gpt-oss-20b": False, "gpt-oss-120b": False, "llama-3-1-8b-instruct": False,
+            "llama-4-maverick-17b-128e-instruct-fp8": True}
+    for fam, pd in want.items():
+        names = [n for n in docs if n.startswith(f"ome-amd-{fam}-grpc-") or
+                 (pd and n.startswith(f"ome-amd-{fam}-pd-grpc-"))]
+        assert len(names) == (2 if pd else 1), (fam, names)
+        for n in names:
+            spec = docs[n]["spec"]
+            for comp in ("engineConfig", "decoderConfig"):
+                r = (spec.get(comp) or {}).get("runner")
+                if r is None:
+                    continue
+                assert "--grpc-mode" in r["args"] and r["ports"][0]["name"] == "grpc1"
+                assert r["readinessProbe"]["grpc"]["service"] == G.SERVICE
+                assert r["livenessProbe"]["grpc"]["service"] == ""
+            cmd = spec["routerConfig"]["runner"]["command"]
+            assert cmd[cmd.index("--health-check-endpoint") + 1] == "/HealthCheck"
+            assert not spec["supportedModelFormats"][0]["autoSelect"]   # opt-in by runtime name
