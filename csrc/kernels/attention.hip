@@ -51,15 +51,43 @@ struct Scaler {
   // Block-sparse causal attention (Phi-3-small): keys and queries in blocks of 1 << bs_shift
   // tokens; query block qb sees key block kb <= qb when qb - kb < bs_local (the local band) or
   // (kb + bs_h0 + head * bs_step + 1) % bs_vert == 0 (per-head vertical stripes).  bs_shift == 0:
-  // dense.  Applied as a -inf mask on the scores of the generic (non-FAST) kernel bodies.
+  // dense.  Applied as a -inf mask on the scores; the v2 prefill kernel also skips key stages no
+  // head of its kv group sees (bs_stage_needed) before loading them.
   int bs_shift, bs_local, bs_vert, bs_step, bs_h0;
+  int bs_skip;   // prefill skips invisible stages (OME_BS_SKIP=0: mask only, the r05 behaviour)
   __device__ __forceinline__ float alibi_l2(int head) const {
     return alibi != nullptr ? alibi[head] * 1.4426950408889634f : 0.f;
   }
   __device__ __forceinline__ bool bs_visible(int qpos, int key, int head) const {
     if (bs_shift == 0) return true;
     const int qb = qpos >> bs_shift, kb = key >> bs_shift;
-    return qb - kb < bs_local || (kb + bs_h0 + head * bs_step + 1) % bs_vert == 0;
+    return qb - kb < bs_local || bs_stripe(kb, head);
+  }
+  // block kb is a vertical stripe of `head`
+  __device__ __forceinline__ bool bs_stripe(int kb, int head) const {
+    return (kb + bs_h0 + head * bs_step + 1) % bs_vert == 0;
+  }
+  // Does any (query, head) of query blocks <= qb_hi and heads h0 .. h0 + nh - 1 see a key of
+  // [k0, k0 + n)?  Block-sparse prefill skips stages nobody sees (before loading them).
+  __device__ __forceinline__ bool bs_stage_needed(int k0, int n, int qb_hi, int h0, int nh) const {
+    if (bs_shift == 0) return true;
+    const int b0 = k0 >> bs_shift, b1 = (k0 + n - 1) >> bs_shift;
+    if (qb_hi - b1 < bs_local) return true;   // the last block is in every head's local band
+    for (int b = b0; b <= b1; ++b) {
+      if (qb_hi - b < bs_local) return true;
+      for (int h = 0; h < nh; ++h)
+        if (bs_stripe(b, h0 + h)) return true;
+    }
+    return false;
+  }
+  // Every query block in [qb_lo, qb_hi] of `head` sees every key of [k0, k0 + n)?
+  __device__ __forceinline__ bool bs_stage_full(int k0, int n, int qb_hi, int head) const {
+    if (bs_shift == 0) return true;
+    const int b0 = k0 >> bs_shift, b1 = (k0 + n - 1) >> bs_shift;
+    if (qb_hi - b0 < bs_local) return true;
+    for (int b = b0; b <= b1; ++b)
+      if (qb_hi - b >= bs_local && !bs_stripe(b, head)) return false;
+    return true;
   }
   __device__ __forceinline__ float operator()(float s) const {
     if (cap_inv > 0.f) {
@@ -79,6 +107,8 @@ static inline void set_blocksparse(Scaler& r, int64_t bs) {
   r.bs_step = (int)((bs >> 32) & 0xff);
   r.bs_h0 = (int)((bs >> 40) & 0xfff);
   if (r.bs_vert <= 0) r.bs_shift = 0;
+  static const int skip = getenv("OME_BS_SKIP") ? atoi(getenv("OME_BS_SKIP")) : 1;
+  r.bs_skip = skip;
 }
 
 static inline Scaler make_scaler(float scale, float softcap, const float* alibi = nullptr, int64_t bs = 0) {
@@ -850,7 +880,9 @@ constexpr int PF_KLD = 128 + 8, PF_VLD = 32 + 8;
 // 64-row items, every K/V stage staged once for twice the query rows, one chunk per thread).
 // PROBE (timing diagnostics, wrong results by design; OME_PREFILL_PROBE): 1 = no V image stores,
 // 2 = no K/V global loads, 3 = identity pages (no block-table loads before the K/V loads).
-template <int SUB, int F, bool SPLIT, bool FAST = false, int NW = 4, int PROBE = 0>
+// BS (FAST only): block-sparse layer -- skip the key stages no head of the kv group sees and mask
+// this head's invisible keys (a separate instantiation: the dense kernels keep their registers).
+template <int SUB, int F, bool SPLIT, bool FAST = false, int NW = 4, int PROBE = 0, bool BS = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
     const bf16* __restrict__ q, int64_t q_stride, const typename KVStore<F>::T* __restrict__ k_cache,
     const typename KVStore<F>::T* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -1069,6 +1101,29 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
         }
       }
     }
+    if (BS && !scl.bs_stage_full(kb, 32 * SUB, (prefix + r0 + 31) >> scl.bs_shift, head)) {
+      // block-sparse: this head's invisible keys of the stage.  Blocks are >= 32 * SUB keys (host
+      // check), so the stage spans blocks b0 and at most b1 = b0 + 1, split at key offset `cut`;
+      // visibility is per (row, block): local band or this head's stripe
+      asm volatile("" ::: "memory");
+      const int b0 = kb >> scl.bs_shift, b1 = (kb + 32 * SUB - 1) >> scl.bs_shift;
+      const int cut = (b1 << scl.bs_shift) - kb;   // first key offset in b1 (b1 == b0: >= stage)
+      const bool st0 = scl.bs_stripe(b0, head), st1 = scl.bs_stripe(b1, head);
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int qb = (prefix + r0 + 16 * rb + n) >> scl.bs_shift;
+        const bool v0 = st0 || qb - b0 < scl.bs_local, v1 = st1 || qb - b1 < scl.bs_local;
+#pragma unroll
+        for (int u = 0; u < SUB; ++u)
+#pragma unroll
+          for (int X = 0; X < 2; ++X)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int off = 32 * u + 16 * X + 4 * g + i;
+              if (!((off < cut || b1 == b0) ? v0 : v1)) sc[u][rb][X][i] = OME_NEG_INF;
+            }
+      }
+    }
     const bool diag = kb + 32 * SUB > prefix + r0 + 1;   // wave-uniform
     if (diag) {   // only the diagonal stage masks (a real branch: the asm keeps it from being speculated)
       asm volatile("" ::: "memory");
@@ -1149,25 +1204,44 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
   };
 
   constexpr int STEP = 32 * SUB;
-  int kb = kv_lo;
+  // the stages this workgroup runs: every STEP-key stage from kv_lo, except (block-sparse) stages
+  // that no query row of the item and no head of the kv group sees -- skipped before their loads,
+  // so a sparse layer costs its visible tiles only.  Dense: nxt(k) == k.
+  auto nxt = [&](int k) __attribute__((always_inline)) {
+    if constexpr (BS) {
+      const int qb_hi = (prefix + item_hi - 1) >> scl.bs_shift;
+      if (scl.bs_skip)
+        while (k < kv_end && !scl.bs_stage_needed(k, STEP, qb_hi, kvh * G, G)) k += STEP;
+    }
+    return k;
+  };
+  int kb = nxt(kv_lo);
+  int kB = kb < kv_end ? nxt(kb + STEP) : kv_end;
   if (kb < kv_end) {
     load_tile(rkA, rvA, kb);
-    if (kb + STEP < kv_end) load_tile(rkB, rvB, kb + STEP);
+    if (kB < kv_end) load_tile(rkB, rvB, kB);
     store_tile(rkA, rvA, 0);
   }
   __syncthreads();
-  if (kb + 2 * STEP < kv_end) load_tile(rkA, rvA, kb + 2 * STEP);
-  // invariant at the top: LDS buf 0 = tile kb, registers B = tile kb + STEP, A = tile kb + 2 STEP
-  for (; kb < kv_end; kb += 2 * STEP) {
+  int kC = kB < kv_end ? nxt(kB + STEP) : kv_end;
+  if (kC < kv_end) load_tile(rkA, rvA, kC);
+  // invariant at the top: LDS buf 0 = stage kb, registers B = stage kB, A = stage kC (the next
+  // needed stages in order; dense: kb + STEP, kb + 2 STEP)
+  while (kb < kv_end) {
     step(0, kb);
-    if (kb + STEP < kv_end) store_tile(rkB, rvB, 1);
+    if (kB < kv_end) store_tile(rkB, rvB, 1);
     __syncthreads();
-    if (kb + STEP >= kv_end) break;
-    if (kb + 3 * STEP < kv_end) load_tile(rkB, rvB, kb + 3 * STEP);
-    step(1, kb + STEP);
-    if (kb + 2 * STEP < kv_end) store_tile(rkA, rvA, 0);
+    if (kB >= kv_end) break;
+    const int kD = kC < kv_end ? nxt(kC + STEP) : kv_end;
+    if (kD < kv_end) load_tile(rkB, rvB, kD);
+    step(1, kB);
+    if (kC < kv_end) store_tile(rkA, rvA, 0);
     __syncthreads();
-    if (kb + 4 * STEP < kv_end) load_tile(rkA, rvA, kb + 4 * STEP);
+    const int kE = kD < kv_end ? nxt(kD + STEP) : kv_end;
+    if (kE < kv_end) load_tile(rkA, rvA, kE);
+    kb = kC;
+    kB = kD;
+    kC = kE;
   }
   if (!active) return;
   if constexpr (FAST) {   // per-lane partial row sums -> the row's total (its 4 lane groups)
@@ -1248,14 +1322,15 @@ __global__ __launch_bounds__(256) void prefill_combine_kernel(const int4* __rest
   *reinterpret_cast<bf16x4*>(out + (int64_t)(q0 + row) * out_stride + (int64_t)head * D + 4 * quad) = v;
 }
 
-// the FAST body of paged_prefill_v2_kernel applies: causal only (OME_PREFILL_FAST=0 forces the
-// generic body, for A/B runs)
+// the FAST body of paged_prefill_v2_kernel applies: causal (block-sparse included: its per-head
+// mask runs on the stages a head does not fully see) -- OME_PREFILL_FAST=0 forces the generic
+// body, for A/B runs
 static bool prefill_fast(const Scaler& scl, int window, const int* row_hi) {
   static const bool off = [] {
     const char* e = getenv("OME_PREFILL_FAST");
     return e && atoi(e) == 0;
   }();
-  return !off && scl.cap_inv == 0.f && scl.alibi == nullptr && scl.bs_shift == 0 && row_hi == nullptr &&
+  return !off && scl.cap_inv == 0.f && scl.alibi == nullptr && row_hi == nullptr &&
          (window == -1 || window == 0);
 }
 
@@ -1268,16 +1343,22 @@ static void launch_prefill(int variant, int rows, int G, dim3 grid, hipStream_t 
   typedef typename KVStore<F>::T T;
   if constexpr (D == 128) {
     if (variant == 2 && G == 4) {  // one head per wave over 32-row items (GQA-4: Llama-3, Qwen3, Mixtral)
-#define OME_PF2(FAST, NW)                                                                                         \
-  paged_prefill_v2_kernel<2, F, false, FAST, NW><<<grid, 64 * NW, 0, stream>>>(                                   \
+#define OME_PF2B(FAST, NW, BS)                                                                                    \
+  paged_prefill_v2_kernel<2, F, false, FAST, NW, 0, BS><<<grid, 64 * NW, 0, stream>>>(                            \
       (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,      \
       (const int2*)items, (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, row_hi, 0, nullptr, nullptr)
+#define OME_PF2(FAST, NW) OME_PF2B(FAST, NW, false)
+      const bool bs = scl.bs_shift != 0;   // BS kernels need blocks >= 64 keys (else: generic body, mask only)
+      const bool bs_fast = bs && scl.bs_shift >= 6 && prefill_fast(scl, window, row_hi);
       if (rows == 64) {   // 8 waves over 64-row items
-        if (prefill_fast(scl, window, row_hi)) OME_PF2(true, 8);
+        if (bs_fast) OME_PF2B(true, 8, true);
+        else if (!bs && prefill_fast(scl, window, row_hi)) OME_PF2(true, 8);
         else OME_PF2(false, 8);
+      } else if (bs_fast) {
+        OME_PF2B(true, 4, true);
       } else {
         static const int probe = getenv("OME_PREFILL_PROBE") ? atoi(getenv("OME_PREFILL_PROBE")) : 0;
-        if (prefill_fast(scl, window, row_hi)) {
+        if (!bs && prefill_fast(scl, window, row_hi)) {
 #define OME_PF2P(PR)                                                                                              \
   paged_prefill_v2_kernel<2, F, false, true, 4, PR><<<grid, 256, 0, stream>>>(                                    \
       (const bf16*)q, q_stride, (const T*)k_cache, (const T*)v_cache, block_tables, bt_stride, cu_q, kv_lens,      \
@@ -1296,6 +1377,7 @@ static void launch_prefill(int variant, int rows, int G, dim3 grid, hipStream_t 
         }
       }
 #undef OME_PF2
+#undef OME_PF2B
       return;
     }
   }
@@ -1363,11 +1445,19 @@ OME_API int ome_paged_prefill_split(const void* q, int64_t q_stride, const void*
   const Scaler scl = make_scaler(scale * k_scale, softcap, alibi, bsparse);
   dim3 grid(n_items, Hkv);
 #define OME_PFS(F, FAST)                                                                                       \
+  if (FAST && scl.bs_shift >= 6)                                                                               \
+    paged_prefill_v2_kernel<2, F, true, FAST, 4, 0, FAST><<<grid, 256, 0, stream>>>(                           \
+        (const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache,                                      \
+        (const typename KVStore<F>::T*)v_cache, block_tables, bt_stride, cu_q, kv_lens, (const int2*)items4,   \
+        (bf16*)out, out_stride, Hq, Hkv, scl, window, v_scale, sinks, nullptr, chunk, (float*)part_o,          \
+        (float*)part_ml);                                                                                      \
+  else                                                                                                         \
   paged_prefill_v2_kernel<2, F, true, FAST><<<grid, 256, 0, stream>>>(                                         \
       (const bf16*)q, q_stride, (const typename KVStore<F>::T*)k_cache, (const typename KVStore<F>::T*)v_cache, \
       block_tables, bt_stride, cu_q, kv_lens, (const int2*)items4, (bf16*)out, out_stride, Hq, Hkv, scl, window,  \
       v_scale, sinks, nullptr, chunk, (float*)part_o, (float*)part_ml)
-  const bool fast = prefill_fast(scl, window, nullptr);
+  // block-sparse with blocks < 64 keys: generic body (mask only)
+  const bool fast = prefill_fast(scl, window, nullptr) && (scl.bs_shift == 0 || scl.bs_shift >= 6);
   if (kv_fmt == KV_BF16) {
     if (fast) OME_PFS(KV_BF16, true);
     else OME_PFS(KV_BF16, false);

@@ -385,6 +385,10 @@ OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k,
                                  void* out, int64_t o_stride, int Hq, int Hkv, int D, float scale, int causal,
                                  hipStream_t stream) {
   if (n_items <= 0) return 0;
+  // bit 1 of `causal`: force the generic body for a bidirectional call (ops.varlen_generic(), the
+  // fast-vs-generic equivalence tests); bit 0: causal
+  const bool force_generic = (causal & 2) != 0;
+  causal &= 1;
   if (cuk != nullptr && causal) return -6;   // cross attention is bidirectional
   if (D <= 0 || D > 128 || D % 8 != 0) return -2;
   if (Hkv <= 0 || Hq % Hkv != 0) return -3;
@@ -397,7 +401,7 @@ OME_API int ome_varlen_attention(const void* q, int64_t q_stride, const void* k,
       (bf16*)out, o_stride, Hq, Hkv, D, sl2, causal
   // bidirectional calls take the FAST body (OME_VARLEN_FAST=0: generic); D 128 with 64-key
   // stages (OME_VARLEN_SUB=1: 32) -- profiles/r05_varlen_attn.md
-  const bool fast = !causal && getenv_int("OME_VARLEN_FAST", 1);
+  const bool fast = !causal && !force_generic && getenv_int("OME_VARLEN_FAST", 1);
   static const int sub = getenv("OME_VARLEN_SUB") ? atoi(getenv("OME_VARLEN_SUB")) : 2;
   static const int sub_small = getenv("OME_VARLEN_SUB_SMALL") ? atoi(getenv("OME_VARLEN_SUB_SMALL")) : 2;
   if (D <= 64) {

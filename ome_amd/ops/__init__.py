@@ -4,6 +4,7 @@ native library is missing on a GPU the call raises.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -612,12 +613,15 @@ class MLAWorkspace:
         self.ws_ml = torch.empty(self.ROWS * 2, dtype=torch.float32, device=device)
 
     @staticmethod
-    def all_heads(H: int, DK: int = 576) -> bool:
-        return DK == 576 and H % 64 == 0 and os.environ.get("OME_MLA_ALL", "1") != "0"
+    def all_heads(H: int, DK: int = 576, T: int = 1 << 30) -> bool:
+        """Mirror of mla.hip's kernel choice (same env knobs): all-heads only above
+        ``OME_MLA_ALL_MIN_T`` (default 4) tokens -- tiny batches keep the 16-head kernel."""
+        return (DK == 576 and H % 64 == 0 and os.environ.get("OME_MLA_ALL", "1") != "0"
+                and T > int(os.environ.get("OME_MLA_ALL_MIN_T", "4")))
 
     @classmethod
     def parts(cls, T: int, H: int, DK: int = 576) -> int:
-        if cls.all_heads(H, DK):
+        if cls.all_heads(H, DK, T):
             wgs = T * (H // (128 if H % 128 == 0 else 64))
             p = max(1, min(cls.MAX_PARTS_ALL, cls.TARGET_WGS_ALL // max(wgs, 1)))
         else:
@@ -710,8 +714,13 @@ def skinny_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = No
     return out
 
 
-_stream_ws: dict = {}
-_stream_cnt: dict = {}   # per-device tile arrival counters of the single-launch split-K
+_stream_ws: dict = {}    # split-K partial sums per (device, stream): TBO halves never alias
+_stream_cnt: dict = {}   # tile arrival counters of the single-launch split-K, per (device, stream)
+
+
+def _ws_key(device) -> tuple:
+    device = torch.device(device)
+    return (device.index, torch.cuda.current_stream(device).cuda_stream)
 
 
 def stream_gemm_plan(M: int, N: int, K: int) -> tuple[int, int]:
@@ -738,13 +747,14 @@ _stream_ws_retired: list = []
 def stream_gemm_reserve(device, floats: int) -> None:
     """Pre-size the split-K workspace (call before HIP-graph capture so capture never allocates).
     Growing it later keeps the old buffer alive: graphs captured earlier replay into it."""
-    ws = _stream_ws.get(device)
+    key = _ws_key(device)
+    ws = _stream_ws.get(key)
     if ws is None or ws.numel() < floats:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError(f"split-K workspace must be reserved before capture ({floats} floats needed)")
         if ws is not None:
             _stream_ws_retired.append(ws)
-        _stream_ws[device] = torch.empty(floats, dtype=torch.float32, device=device)
+        _stream_ws[key] = torch.empty(floats, dtype=torch.float32, device=device)
 
 
 def stream_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
@@ -768,11 +778,11 @@ def stream_gemm(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = No
     ws = cnt = None
     if s > 1:
         stream_gemm_reserve(x.device, s * M * N)
-        ws = _stream_ws[x.device]
+        ws = _stream_ws[_ws_key(x.device)]
         if os.environ.get("OME_STREAM_INKERNEL", "0") == "1":   # opt-in single launch: last split combines (measured slower)
-            cnt = _stream_cnt.get(x.device)
+            cnt = _stream_cnt.get(_ws_key(x.device))
             if cnt is None:
-                cnt = _stream_cnt[x.device] = torch.zeros(1 << 13, dtype=torch.int32, device=x.device)
+                cnt = _stream_cnt[_ws_key(x.device)] = torch.zeros(1 << 13, dtype=torch.int32, device=x.device)
             assert N // (128 * nf) <= cnt.numel()
     call("ome_stream_gemm", x.data_ptr(), x.stride(0), w.data_ptr(), ptr(bias), out.data_ptr(), out.stride(0), M, N,
          K, nf, s, ptr(ws), ptr(cnt), stream_ptr())
@@ -974,6 +984,28 @@ def _sk_workspace(device: torch.device):
         cnt = torch.zeros(_SK_CNT, dtype=torch.int32, device=device)   # the kernel re-arms every ticket it takes
         w = _SK_WS[key] = (ws, cnt)
     return w
+
+
+def sk_workspace_bytes() -> int:
+    return _SK_MAX_WG * 2 * 256 * 256 * 4 + _SK_CNT * 4
+
+
+def reserve_stream_workspaces(device, streams) -> int:
+    """Allocate the stream-K workspace of every stream that will run GEMMs (the current stream,
+    a TBO side stream, ...) up front, i.e. before the KV cache is sized from free memory, so a
+    lazily created per-stream workspace never eats into memory the KV budget already promised.
+    Returns the bytes newly allocated."""
+    device = torch.device(device)
+    if device.type != "cuda":
+        return 0
+    n0 = len(_SK_WS)
+    for s in streams:
+        if s is None:
+            _sk_workspace(device)
+        else:
+            with torch.cuda.stream(s):
+                _sk_workspace(device)
+    return (len(_SK_WS) - n0) * sk_workspace_bytes()
 
 
 def gemm_sk_tiles(M: int, N: int, bn: int, bm: int = 256) -> int:
@@ -1305,6 +1337,21 @@ def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, kv_lens, items, scale
     return out
 
 
+_VARLEN_GENERIC = [0]
+
+
+@contextlib.contextmanager
+def varlen_generic():
+    """Inside this block bidirectional :func:`varlen_attention` calls run the generic kernel body
+    instead of the fast one (equivalence tests of the two bodies inside one process; the
+    ``OME_VARLEN_FAST`` environment switch is read once per process)."""
+    _VARLEN_GENERIC[0] += 1
+    try:
+        yield
+    finally:
+        _VARLEN_GENERIC[0] -= 1
+
+
 def varlen_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lengths: list[int], scale: float,
                      causal: bool = False, out: torch.Tensor | None = None,
                      k_lengths: list[int] | None = None) -> torch.Tensor:
@@ -1343,7 +1390,8 @@ def varlen_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, lengths:
     ni = 2 * len(items)
     call("ome_varlen_attention", q.data_ptr(), q.stride(0), k.data_ptr(), k.stride(0), v.data_ptr(), v.stride(0),
          meta[ni:].data_ptr(), meta[ni + len(cu):].data_ptr() if k_lengths is not None else None, meta.data_ptr(),
-         len(items), out.data_ptr(), out.stride(0), Hq, Hkv, D, float(scale), int(bool(causal)), stream_ptr())
+         len(items), out.data_ptr(), out.stride(0), Hq, Hkv, D, float(scale),
+         int(bool(causal)) | (2 if _VARLEN_GENERIC[0] else 0), stream_ptr())
     return out
 
 

@@ -192,6 +192,9 @@ class ModelRunner:
         # encoders own no KV at all (page bookkeeping only)
         page_bytes = max(1, PagedKVCache.bytes_per_page(n_local, kv_heads, k_dim, page_size, kv_dtype, v_dim))
         if self.is_cuda:
+            # per-stream GEMM workspaces exist before the budget is read (a lazily
+            # created TBO-stream workspace used to come out of the KV headroom)
+            ops.reserve_stream_workspaces(self.device, [None, self._tbo_stream])
             free, total = torch.cuda.mem_get_info(self.device)
             used_by_others = total - free
             if os.environ.get("OME_KV_BUDGET_OWN") == "1":
@@ -258,7 +261,9 @@ class ModelRunner:
         dp_ok = pstate.get().ep_size <= 1 or self.ep_ll
         # on by default since round 5 (OME_PP_GRAPHS=0: eager micro-batched steps): the r04
         # rehearsal's 25 % graph regression is gone -- graphs 10.24k vs eager 10.17k tok/s,
-        # decode steps 15.9 vs 16.9 ms, interleaved on one GPU (profiles/r05_pp_graphs.md)
+        # decode steps 15.9 vs 16.9 ms, interleaved on one GPU (profiles/r05_pp_graphs.md).
+        # UNVERIFIED on distinct GPUs: no 2-GPU PP graphs-vs-eager run has been recorded (only the
+        # 1-GPU interleaved rehearsal); OME_PP_GRAPHS=0 is the fallback if a real node disagrees
         pp_ok = not self.pp or (pstate.pp_graph_ok() and os.environ.get("OME_PP_GRAPHS", "1") == "1"
                                 and not self.stateful)
         self.use_graph = bool(cuda_graph) and self.is_cuda and pp_ok and dp_ok and \

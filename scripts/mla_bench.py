@@ -4,6 +4,7 @@ with microseconds per call and the effective latent-KV read bandwidth (every seq
 
     python scripts/mla_bench.py                 # all-heads kernel
     OME_MLA_ALL=0 python scripts/mla_bench.py   # 16-head kernel (A/B)
+    OME_MLA_ALL_MIN_T=0 python scripts/mla_bench.py   # all-heads even at T <= 4 (A/B of the cutover)
 """
 import json
 import os
@@ -39,9 +40,9 @@ def run(T, L, H=128, iters=50):
     flops = 2 * T * H * L * (576 + 512)
     return {"T": T, "L": L, "H": H, "parts": ops.MLAWorkspace.parts(T, H), "us": round(us, 1),
             "kv_GBps": round(kv / us / 1e3, 1), "TFLOPs": round(flops / us / 1e6, 1),
-            "kernel": "all-heads" if ops.MLAWorkspace.all_heads(H) else "16-head"}
+            "kernel": "all-heads" if ops.MLAWorkspace.all_heads(H, 576, T) else "16-head"}
 
 
 if __name__ == "__main__":
-    for T, L in [(1, 4096), (8, 2048), (32, 1024), (64, 1024), (128, 1024), (128, 4096), (256, 2048)]:
+    for T, L in [(1, 4096), (2, 4096), (4, 4096), (6, 2048), (8, 2048), (32, 1024), (64, 1024), (128, 1024), (128, 4096), (256, 2048)]:
         print(json.dumps(run(T, L)), flush=True)

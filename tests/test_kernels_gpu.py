@@ -472,10 +472,11 @@ def test_paged_prefill_64_row_items(q_lens, kv_lens, window):
 
 
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (8, 1)])   # GQA-4 (the v2 prefill kernel) and G = 8 (generic)
-@pytest.mark.parametrize("bs", [(64, 16, 8, 1, 0), (64, 4, 8, 1, 32), (16, 2, 3, 0, 0)])
+@pytest.mark.parametrize("bs", [(64, 16, 8, 1, 0), (64, 4, 8, 1, 32), (16, 2, 3, 0, 0), (128, 3, 4, 1, 5)])
 def test_blocksparse_prefill_decode(Hq, Hkv, bs):
     """Phi-3-small block-sparse causal attention (local band + per-head vertical stripes) in the
-    paged prefill (classic and split-KV plans) and decode kernels == the fp32 reference."""
+    paged prefill (classic, 64-row and split-KV plans: the FAST body skipping invisible stages for
+    blocks >= 64 keys, the generic masked body below) and decode kernels == the fp32 reference."""
     D, P = 128, 16
     q_lens, kv_lens = [1500, 37, 300], [1500, 1200, 2100]
     npages = sum(-(-L // P) for L in kv_lens) + 8
@@ -490,6 +491,9 @@ def test_blocksparse_prefill_decode(Hq, Hkv, bs):
     if Hq == 4 * Hkv:
         _close(ops.paged_prefill(q, kc, vc, bt, cu, kl, _plan(q_lens, kv_lens, 128), 0.0884, blocksparse=bs), want,
                atol=2e-2)
+        it64 = torch.tensor(ops.prefill_work_items(q_lens, kv_lens, 64), dtype=torch.int32, device=DEV)
+        plan64 = ops.PrefillPlan(it64, it64[:0], it64[:0], 0, 0, 64)
+        _close(ops.paged_prefill(q, kc, vc, bt, cu, kl, plan64, 0.0884, blocksparse=bs), want, atol=2e-2)
     assert not torch.allclose(want, ref.paged_prefill(q, kc, vc, bt, cu, kl, 0.0884), atol=1e-2)   # mask bites
     qd = torch.randn(len(kv_lens), Hq, D, device=DEV, dtype=torch.bfloat16)
     ws = ops.DecodeWorkspace(len(kv_lens), Hq, D, 4096, 256, DEV)
