@@ -67,14 +67,15 @@ struct Scaler {
   __device__ __forceinline__ bool bs_stripe(int kb, int head) const {
     return (kb + bs_h0 + head * bs_step + 1) % bs_vert == 0;
   }
-  // Does any (query, head) of query blocks <= qb_hi and heads h0 .. h0 + nh - 1 see a key of
-  // [k0, k0 + n)?  Block-sparse prefill skips stages nobody sees (before loading them).
-  __device__ __forceinline__ bool bs_stage_needed(int k0, int n, int qb_hi, int h0, int nh) const {
+  // Does any (query, head) of query blocks >= qb_lo (up to the causal limit) and heads h0 ..
+  // h0 + nh - 1 see a key of [k0, k0 + n)?  The local band is widest for the EARLIEST query
+  // block, so qb_lo decides it.  Block-sparse kernels skip stages nobody sees, before loading.
+  __device__ __forceinline__ bool bs_stage_needed(int k0, int n, int qb_lo, int h0, int nh) const {
     if (bs_shift == 0) return true;
     const int b0 = k0 >> bs_shift, b1 = (k0 + n - 1) >> bs_shift;
-    if (qb_hi - b1 < bs_local) return true;   // the last block is in every head's local band
+    if (qb_lo - b1 < bs_local) return true;   // the last block is in the first row's local band
     for (int b = b0; b <= b1; ++b) {
-      if (qb_hi - b < bs_local) return true;
+      if (qb_lo - b < bs_local) return true;
       for (int h = 0; h < nh; ++h)
         if (bs_stripe(b, h0 + h)) return true;
     }
@@ -541,7 +542,10 @@ __global__ __launch_bounds__(256) void paged_decode_v2_kernel(
     while (kb + 32 <= lo && kb < p_end) kb += 128;
   }
   if (MODE == 2) {
+    const int qb = AL && scl.bs_shift ? qpos >> scl.bs_shift : 0;
     for (; kb < p_end; kb += 128) {
+      // block-sparse: a 32-key tile no head of the group sees is not loaded at all
+      if (AL && scl.bs_shift && scl.bs_skip && !scl.bs_stage_needed(kb, 32, qb, kvh * G, G)) continue;
       KVTileP<D, F> t;
       kv_tilep_load<D, P, F>(t, k_cache, v_cache, bt, kb, seq_len, kpage, kvh, n, g);
       kv_tilep_compute<D, F, AL>(t, qf, o, m_i, l_i, kb, p_end, lo, scl, g, al, qpos, kvh * G + n);
@@ -1209,9 +1213,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
   // so a sparse layer costs its visible tiles only.  Dense: nxt(k) == k.
   auto nxt = [&](int k) __attribute__((always_inline)) {
     if constexpr (BS) {
-      const int qb_hi = (prefix + item_hi - 1) >> scl.bs_shift;
+      const int qb_lo = (prefix + r0_item) >> scl.bs_shift;   // the item's first query row
       if (scl.bs_skip)
-        while (k < kv_end && !scl.bs_stage_needed(k, STEP, qb_hi, kvh * G, G)) k += STEP;
+        while (k < kv_end && !scl.bs_stage_needed(k, STEP, qb_lo, kvh * G, G)) k += STEP;
     }
     return k;
   };

@@ -399,10 +399,11 @@ static void mla_launch(const void* q, int64_t q_stride_t, const void* cache, con
   // all-heads kernel when the heads tile into groups of 128 (DeepSeek-V3 / Kimi-K2 at TP 1) or 64
   // (TP 2): one latent stream per token and partition; else the 16-head kernel.  OME_MLA_ALL=0
   // forces the 16-head kernel (A/B timing).  Batches of at most OME_MLA_ALL_MIN_T tokens (default
-  // 4) also take the 16-head kernel: the all-heads kernel's fixed cost (Q load, first DMA, fp32
-  // partials + reduce) loses at T = 1 (41.1 vs 37.4 us, profiles/r05_mla_moe_roofline.md:24).
+  // 2) also take the 16-head kernel: the all-heads kernel's fixed cost (Q load, first DMA, fp32
+  // partials + reduce) loses at T = 1 / 2 (41.0 / 40.1 vs 35.2 / 36.0 us) and wins from T = 4
+  // (43.1 vs 61.4 us) -- profiles/r06_mla_cutover.txt.
   static const bool all_env = !getenv("OME_MLA_ALL") || atoi(getenv("OME_MLA_ALL")) != 0;
-  static const int min_t = getenv("OME_MLA_ALL_MIN_T") ? atoi(getenv("OME_MLA_ALL_MIN_T")) : 4;
+  static const int min_t = getenv("OME_MLA_ALL_MIN_T") ? atoi(getenv("OME_MLA_ALL_MIN_T")) : 2;
   const bool all_ok = all_env && T > min_t;
   bool done = false;
   if constexpr (DK == 576) {

@@ -56,10 +56,11 @@ def iter_safetensors(model_path: str | Path, device="cpu", plan=None) -> Iterato
         from ome_amd.io import native as nio
 
         if nio.available():
+            ex = nio.ShardExchange.for_state(device) if plan is not None else None
             if torch.device(device).type == "cuda":
-                yield from nio.iter_tensors_to_device(files, device, plan)
+                yield from nio.iter_tensors_to_device(files, device, plan, ex)
             else:
-                yield from nio.iter_tensors_host(files, plan)
+                yield from nio.iter_tensors_host(files, plan, ex)
             return
     except ImportError:
         pass

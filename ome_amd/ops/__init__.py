@@ -615,9 +615,9 @@ class MLAWorkspace:
     @staticmethod
     def all_heads(H: int, DK: int = 576, T: int = 1 << 30) -> bool:
         """Mirror of mla.hip's kernel choice (same env knobs): all-heads only above
-        ``OME_MLA_ALL_MIN_T`` (default 4) tokens -- tiny batches keep the 16-head kernel."""
+        ``OME_MLA_ALL_MIN_T`` (default 2) tokens -- T = 1 / 2 keep the 16-head kernel."""
         return (DK == 576 and H % 64 == 0 and os.environ.get("OME_MLA_ALL", "1") != "0"
-                and T > int(os.environ.get("OME_MLA_ALL_MIN_T", "4")))
+                and T > int(os.environ.get("OME_MLA_ALL_MIN_T", "2")))
 
     @classmethod
     def parts(cls, T: int, H: int, DK: int = 576) -> int:

@@ -37,6 +37,7 @@ class ParallelState:
     comm: object | None = None  # ome_amd.parallel.comm.TPCommunicator
     tbo: bool = False           # two-batch overlap of the EP MoE all-to-alls (parallel/ep.py)
     cpu_group: object | None = None  # gloo group of this engine group (control-plane broadcasts)
+    tp_cpu_group: object | None = None  # gloo group of this rank's TP group (host-side exchanges)
     global_rank: int = 0        # rank in the whole job (several engine replicas per job)
     replica: int = 0
     replicas: int = 1
@@ -155,6 +156,7 @@ def init(tp_size: int = 1, pp_size: int = 1, ep_size: int | None = None, dist_in
             from ome_amd.parallel.comm import TPCommunicator
 
             st.comm = TPCommunicator(st.tp_group, cpu_group=tp_cpu)
+        st.tp_cpu_group = tp_cpu
     _STATE = st
     return st
 

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--len", type=int, default=8192)
     ap.add_argument("--dense", action="store_true")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--decode-batch", type=int, default=32)
     a = ap.parse_args()
     Hq, Hkv, D, P, L = 32, 8, 128, 16, a.len
     dev = "cuda"
@@ -53,10 +54,31 @@ def main():
     torch.cuda.synchronize()
     ms = e[0].elapsed_time(e[1]) / a.iters
     dense_flops = 4 * Hq * D * L * (L + 1) / 2
-    mode = "dense" if a.dense else ("mask-only generic (r05)" if os.environ.get("OME_BS_SKIP") == "0" else
-                                    "skip + fast body")
-    print(json.dumps({"mode": mode, "len": L, "rows": rows, "split_parts": parts, "ms": round(ms, 3),
-                      "dense_equiv_TFs": round(dense_flops / ms / 1e9, 1)}), flush=True)
+    mode = "dense" if a.dense else ("mask-only" if os.environ.get("OME_BS_SKIP") == "0" else "skip") + \
+        ("" if a.dense else (", generic body" if os.environ.get("OME_PREFILL_FAST") == "0" else ", fast body"))
+    print(json.dumps({"op": "prefill", "mode": mode, "len": L, "rows": rows, "split_parts": parts,
+                      "ms": round(ms, 3), "dense_equiv_TFs": round(dense_flops / ms / 1e9, 1)}), flush=True)
+    # decode: B sequences of L cached keys, one query token each (the same pattern at qpos = L - 1)
+    B = a.decode_batch
+    kc = torch.randn(B * (L // P) + 2, Hkv, P, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(B * (L // P) + 2, Hkv, D, P, device=dev, dtype=torch.bfloat16)
+    bt = (torch.arange(B * (L // P), device=dev, dtype=torch.int32) + 1).view(B, -1)
+    qd = torch.randn(B, Hq, D, device=dev, dtype=torch.bfloat16)
+    sl = torch.full((B,), L, dtype=torch.int32, device=dev)
+    ws = ops.DecodeWorkspace(B, Hq, D, L, 512, dev)
+    od = ops.paged_decode(qd, kc, vc, bt, sl, scale, ws, blocksparse=bs)
+    for _ in range(3):
+        ops.paged_decode(qd, kc, vc, bt, sl, scale, ws, out=od, blocksparse=bs)
+    torch.cuda.synchronize()
+    e[0].record()
+    for _ in range(a.iters):
+        ops.paged_decode(qd, kc, vc, bt, sl, scale, ws, out=od, blocksparse=bs)
+    e[1].record()
+    torch.cuda.synchronize()
+    us = e[0].elapsed_time(e[1]) * 1e3 / a.iters
+    kv_bytes = B * L * Hkv * D * 2 * 2
+    print(json.dumps({"op": "decode", "mode": mode, "batch": B, "len": L, "us": round(us, 1),
+                      "dense_equiv_TBs": round(kv_bytes / us / 1e6, 2)}), flush=True)
 
 
 if __name__ == "__main__":

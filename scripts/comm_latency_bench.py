@@ -27,7 +27,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 REPS = 20
 
 
-def _graph_time(fn, dist):
+def _graph_time(fn, dist, align=None):
+    """us per call of ``fn`` over REPS graph-captured calls, max over ranks.  ``align``: a device-side
+    rendezvous (one custom all-reduce) enqueued right before the start event, so every rank's timer
+    starts at the same device moment.  Without it the host-side gloo barrier leaves the ranks'
+    replays up to ~1 ms apart and the early rank's first collective absorbs that skew (the round
+    3-5 "32 KiB outlier", see OME_AR_ORDER_PROBE)."""
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -44,6 +49,8 @@ def _graph_time(fn, dist):
     torch.cuda.synchronize()
     dist.barrier()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if align is not None:
+        align()
     a.record()
     for _ in range(3):
         g.replay()
@@ -67,11 +74,25 @@ def _worker(rank, world, port, q):
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         dev = torch.device("cuda", 0)
         ar = CustomAllReduce(None, max_bytes=32 << 20)
+        tiny = torch.zeros(64, device=dev, dtype=torch.bfloat16)
+        align = None if os.environ.get("OME_AR_ALIGN", "1") == "0" else (lambda: ar.all_reduce(tiny))
         rows = []
+        if os.environ.get("OME_AR_ORDER_PROBE") == "1":
+            # the same sizes at several table positions, with the host-barrier-only start (as rounds
+            # 3-5 measured) and with the device-aligned start
+            import time as _t
+            for mode, al in (("host-barrier start", None), ("device-aligned start", align)):
+                for pos, kib in enumerate((8, 32, 128, 32, 8, 32, 2048, 32)):
+                    n = kib * 1024 // 2
+                    x = torch.randn(n, device=dev).to(torch.bfloat16)
+                    t0 = _t.perf_counter()
+                    t = _graph_time(lambda: ar.all_reduce(x), dist, al)
+                    rows.append(f"order-probe {mode:22s} pos {pos} {kib:6d} KiB  {t:8.1f} us  "
+                                f"(rank{rank} host {1e3 * (_t.perf_counter() - t0):.1f} ms)")
         for kib in (8, 32, 128, 512, 2048, 8192, 16384):
             n = kib * 1024 // 2
             x = torch.randn(n, device=dev).to(torch.bfloat16)
-            t = _graph_time(lambda: ar.all_reduce(x), dist)
+            t = _graph_time(lambda: ar.all_reduce(x), dist, align)
             rows.append(f"all_reduce        {kib:6d} KiB  {t:8.1f} us  {2 * (world - 1) / world * kib / 1024 / t * 1e6 / 1024:6.2f} GB/s busbw")
         if os.environ.get("OME_AR_GRID_SWEEP") == "1":   # one-shot grid sizing: vectors per lane
             for vpt in (1, 2, 4):
@@ -79,7 +100,7 @@ def _worker(rank, world, port, q):
                 for kib in (8, 16, 24, 32, 48, 64, 96, 128, 256, 512):
                     n = kib * 1024 // 2
                     x = torch.randn(n, device=dev).to(torch.bfloat16)
-                    t = _graph_time(lambda: ar.all_reduce(x), dist)
+                    t = _graph_time(lambda: ar.all_reduce(x), dist, align)
                     rows.append(f"one-shot vpt={vpt} grid={ar._grid(n, False):3d} {kib:5d} KiB  {t:8.1f} us")
             ar.vpt = 0
         for r in (1, 16, 32, 64):
@@ -88,7 +109,7 @@ def _worker(rank, world, port, q):
             st.copy_(torch.randn(r, H, device=dev).to(torch.bfloat16))
             res = torch.randn(r, H, device=dev).to(torch.bfloat16)
             w = torch.ones(H, device=dev, dtype=torch.bfloat16)
-            t = _graph_time(lambda: ar.all_reduce_add_rmsnorm(st, res, w, 1e-5), dist)
+            t = _graph_time(lambda: ar.all_reduce_add_rmsnorm(st, res, w, 1e-5), dist, align)
             rows.append(f"ar+add+rmsnorm    {r:4d} x {H}  {t:8.1f} us  ({r * H * 2 // 1024} KiB)")
         E, H, I, K = 32, 2048, 512, 8
         el = E // world
@@ -100,13 +121,13 @@ def _worker(rank, world, port, q):
             x = torch.randn(T, H, device=dev).to(torch.bfloat16)
             logits = torch.randn(T, E, device=dev)
             tw, tid = ops.moe_route(logits, K)
-            t = _graph_time(lambda: ep.forward(x, tw, tid, w13, w2, 0, 1.0, el), dist)
+            t = _graph_time(lambda: ep.forward(x, tw, tid, w13, w2, 0, 1.0, el), dist, align)
             rows.append(f"ep_ll layer       T={T:4d} top{K}/{E} H{H}  {t:8.1f} us (dispatch + experts + combine)")
-            t = _graph_time(lambda: ep.forward(x, tw, tid, None, None, 0, 1.0, el), dist)
+            t = _graph_time(lambda: ep.forward(x, tw, tid, None, None, 0, 1.0, el), dist, align)
             rows.append(f"ep_ll exchange    T={T:4d} top{K}/{E} H{H}  {t:8.1f} us (dispatch + combine, no experts)")
             rt = torch.randn(T * K, H, device=dev).to(torch.bfloat16)
             rid = torch.randint(0, el, (T * K,), device=dev, dtype=torch.int32)
-            t = _graph_time(lambda: ops.moe_experts_sorted(rt, rid, w13, w2, 0, el), dist)
+            t = _graph_time(lambda: ops.moe_experts_sorted(rt, rid, w13, w2, 0, el), dist, align)
             rows.append(f"experts only      T={T:4d} top{K}/{E} H{H}  {t:8.1f} us (align + 2 grouped GEMMs + act)")
             dist.barrier()
             ep.close()
@@ -136,7 +157,8 @@ def main():
         print(f"rank {rank} failed:\n{tb}")
     if bad:
         sys.exit(1)
-    print(f"# world={world} ranks on one MI355X (hipIpc peers), HIP-graph replay of {REPS} calls, max over ranks")
+    print(f"# world={world} ranks on one MI355X (hipIpc peers), HIP-graph replay of {REPS} calls, max over ranks, "
+          f"timers started {'after a device-side rendezvous' if os.environ.get('OME_AR_ALIGN', '1') != '0' else 'after a host barrier only'}")
     for line in res[0][1] if res[0][0] == 0 else sorted(res)[0][1]:
         print(line)
 

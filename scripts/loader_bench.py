@@ -31,11 +31,20 @@ def evict(path):
         os.close(fd)
 
 
-def _rank_load(r, tp, d, cfg_hf, start, q, ready):
-    """One TP rank in its own process: wait for the common start, load its shard onto cuda:0."""
+def _rank_load(r, tp, d, cfg_hf, start, q, ready, port=0):
+    """One TP rank in its own process: wait for the common start, load its shard onto cuda:0.
+    ``port``: join a gloo group of the tp ranks, so the loader's cooperative exchange
+    (OME_LOAD_EXCHANGE, ome_amd.io.native.ShardExchange) can run over it."""
     try:
         cfg = ModelConfig.from_hf(cfg_hf)
-        pstate.set_state(pstate.ParallelState(tp_size=tp, tp_rank=r, world_size=tp, rank=r))
+        grp = None
+        if port:
+            import torch.distributed as dist
+
+            dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=r, world_size=tp)
+            grp = dist.group.WORLD
+        pstate.set_state(pstate.ParallelState(tp_size=tp, tp_rank=r, world_size=tp, rank=r, backend="gloo",
+                                              tp_cpu_group=grp))
         torch.cuda.init()
         torch.empty(1, device="cuda")
         ready.put(r)
@@ -50,16 +59,24 @@ def _rank_load(r, tp, d, cfg_hf, start, q, ready):
         q.put((r, 0.0, 0, repr(e)))
 
 
-def concurrent(tp, d, hf, shards, total):
+def concurrent(tp, d, hf, shards, total, exchange=False):
     """All tp ranks loading their slices at once (one process each, all on GPU 0 here; one per
-    GPU on a node) from a cold page cache: per-rank and aggregate GB/s."""
+    GPU on a node) from a cold page cache: per-rank and aggregate GB/s.  ``exchange``: the ranks
+    form a gloo group and read column shards / replicated tensors cooperatively."""
     import multiprocessing as mp
+    import socket
 
     for f in shards:
         evict(f)
+    port = 0
+    if exchange:
+        with socket.socket() as s_:
+            s_.bind(("127.0.0.1", 0))
+            port = s_.getsockname()[1]
+    os.environ["OME_LOAD_EXCHANGE"] = "1" if exchange else "0"
     ctx = mp.get_context("spawn")
     start, q, ready = ctx.Event(), ctx.Queue(), ctx.Queue()
-    ps = [ctx.Process(target=_rank_load, args=(r, tp, d, hf, start, q, ready)) for r in range(tp)]
+    ps = [ctx.Process(target=_rank_load, args=(r, tp, d, hf, start, q, ready, port)) for r in range(tp)]
     for p in ps:
         p.start()
     for _ in ps:   # every process imported torch and initialised the GPU before the common start
@@ -75,7 +92,8 @@ def concurrent(tp, d, hf, shards, total):
         raise RuntimeError(errs)
     nb = sum(g[2] for g in got)
     per = [g[2] / g[1] / 1e9 for g in got]
-    print(f"concurrent tp={tp}: {nb / 1e9:.2f} GB read by {tp} ranks in {wall:.2f}s wall = {nb / wall / 1e9:.2f} GB/s "
+    print(f"concurrent tp={tp}{' +exchange' if exchange else ''}: {nb / 1e9:.2f} GB read by {tp} ranks in {wall:.2f}s "
+          f"wall = {nb / wall / 1e9:.2f} GB/s "
           f"aggregate; per rank {min(per):.2f}-{max(per):.2f} GB/s (mean {sum(per) / len(per):.2f})", flush=True)
     return {"ranks": tp, "wall_s": round(wall, 3), "aggregate_GBps": round(nb / wall / 1e9, 2),
             "per_rank_GBps": [round(x, 2) for x in per], "bytes_total": int(nb), "checkpoint_bytes": int(total)}
@@ -145,6 +163,7 @@ def main():
     pstate.set_state(pstate.ParallelState())
     if a.concurrent:
         res[f"concurrent_tp{a.tp}"] = concurrent(a.tp, d, hf, shards, total)
+        res[f"concurrent_tp{a.tp}_exchange"] = concurrent(a.tp, d, hf, shards, total, exchange=True)
     print(json.dumps(res))
     if not a.dir:
         for f in shards:

@@ -84,8 +84,9 @@ def main():
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--prompts", type=int, default=64)
     ap.add_argument("--new", type=int, default=64)
+    ap.add_argument("--modes", default="off,on,off,on", help="comma list of off / on (one engine pair per entry)")
     a = ap.parse_args()
-    for tbo in (False, True, False, True):
+    for tbo in [m.strip() == "on" for m in a.modes.split(",")]:
         r = run(a, tbo)
         r.update(model=a.model, layers=a.layers, prompts=a.prompts, new_tokens=a.new,
                  setup="2 ranks sharing GPU 0, DP attention + EP over the IPC low-latency exchange, HIP graphs")
