@@ -331,6 +331,17 @@ class LlamaForCausalLM:
         return ops.paged_prefill(q, k_cache, v_cache, meta.block_tables, meta.cu_q, meta.kv_lens, meta.items,
                                  self.scale, self.window, k_scale=ks, v_scale=vs, softcap=cap)
 
+    def gemm_probe(self, i: int, x: torch.Tensor, a: torch.Tensor) -> None:
+        """Layer i's projection GEMMs exactly as the forward routes them (QKV, O, gate_up with its
+        SiLU epilogue, down), without the TP all-reduce: the row-count cost probe of
+        ``runtime/step_cost.py``.  ``x`` [M, hidden], ``a`` [M, O-projection input width]."""
+        linear(x, self.w_qkv[i], self.b_qkv[i])
+        self._row_parallel(a, self.w_o[i])
+        self._mlp_partial(i, x)
+
+    def gemm_probe_widths(self) -> tuple[int, int]:
+        return self.cfg.hidden_size, self.tp.hq * self.D
+
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
         return pstate.tp_all_reduce(self._mlp_partial(i, x))
 

@@ -178,7 +178,8 @@ def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None, out: torch.Tens
     (``ops.gemm_sk_plan``) -> ``ops.gemm_sk``; single-row decode -> the GEMV stream kernel
     (``ops.gemv``, ``OME_GEMV_ROWS``); the weight-streaming MFMA GEMM for decode shapes where it
     was measured faster (``ops.decode_gemm_plan``, opt-in); other plain tensors -> hipBLASLt;
-    Fp8Weight -> W8A8 MFMA path.  ``out``: write the result there (e.g. the TP all-reduce's IPC
+    Fp8Weight -> W8A16 (fp8 weight, bf16 activation) at the decode rows where ``ops.w8a16_plan``
+    measured it faster, else the W8A8 MFMA path.  ``out``: write the result there (e.g. the TP all-reduce's IPC
     staging buffer)."""
     if (x.dim() == 2 and x.is_cuda and x.shape[0] > _GEMV_ROWS and type(w) is torch.Tensor
             and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16):
@@ -195,8 +196,17 @@ def linear(x: torch.Tensor, w, bias: torch.Tensor | None = None, out: torch.Tens
         out.copy_(linear(x, w, bias))
         return out
     if isinstance(w, Fp8Weight):
-        if w.bf16 is not None and x.dim() == 2 and x.shape[0] <= w.bf16_max_m and x.dtype == torch.bfloat16:
-            return linear(x, w.bf16, bias)
+        if x.dim() == 2 and x.dtype == torch.bfloat16:
+            M = x.shape[0]
+            copy = w.bf16 is not None and M <= w.bf16_max_m
+            if x.is_cuda and not (copy and M > 8):
+                # decode rows: fp8 weight streamed + widened in registers, bf16 activation
+                # (csrc/kernels/w8a16.hip) where measured faster than W8A8
+                sp = ops.w8a16_plan(M, w.q.shape[0], w.q.shape[1], w.block)
+                if sp is not None and ops.w8a16_ok(x, w.q, w.scale, w.block):
+                    return ops.w8a16_gemm(x, w.q, w.scale, w.block, bias, splits=sp)
+            if copy:
+                return linear(x, w.bf16, bias)
         return ops.fp8_linear(x, w.q, w.scale, w.block, bias)
     if x.dim() == 2 and x.shape[0] <= 256 and x.is_cuda:
         if x.shape[0] <= _GEMV_ROWS and ops.gemv_ok(x, w, bias):

@@ -339,6 +339,90 @@ FP8_MX_MIN_ROWS = int(os.environ.get("OME_FP8_MX_MIN_ROWS", "65"))
 FP8_MX_MIN_TILES = int(os.environ.get("OME_FP8_MX_MIN_TILES", "112"))
 
 
+_w8_ws: dict = {}   # W8A16 split-K partial tiles + tile counters per (device, stream)
+
+
+def w8a16_ok(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0) -> bool:
+    """Shape / operand conditions of ``ome_w8a16_gemm`` (csrc/kernels/w8a16.hip)."""
+    if x.dim() != 2 or x.dtype != torch.bfloat16 or qw.dtype != torch.float8_e4m3fn:
+        return False
+    M, K = x.shape
+    N = qw.shape[0]
+    if not 0 < M <= 256 or block not in (0, 128) or (block and K % 128) or qw.shape[1] != K:
+        return False
+    if x.stride(1) != 1 or x.stride(0) % 8 or x.data_ptr() % 16 or qw.stride(1) != 1 or qw.stride(0) % 16 or \
+            qw.data_ptr() % 16 or sw.dtype != torch.float32 or not sw.is_contiguous():
+        return False
+    return K % 16 == 0 if M <= 8 else (N % 64 == 0 and K % 64 == 0)
+
+
+_W8_TABLE: dict | None = None
+_W8_TABLE_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_tuned",
+                              "w8a16_gfx950.json")
+# rows up to which W8A16 serves fp8 projections of unmeasured shapes (every measured shape wins at
+# M <= 2: the GEMV streams the fp8 weight at 2.5-4.2 TB/s, W8A8 pays an activation-quant launch)
+W8A16_DEFAULT_ROWS = int(os.environ.get("OME_W8A16_ROWS", "2"))
+
+
+def _w8_table() -> dict:
+    global _W8_TABLE
+    if _W8_TABLE is None:
+        import json
+
+        try:
+            with open(os.environ.get("OME_W8A16_TABLE", _W8_TABLE_PATH)) as f:
+                raw = json.load(f)
+            _W8_TABLE = {k: sorted((int(m), v) for m, v in d.items()) for k, d in raw.get("shapes", {}).items()}
+        except (OSError, ValueError):
+            _W8_TABLE = {}
+    return _W8_TABLE
+
+
+def w8a16_plan(M: int, N: int, K: int, block: int) -> int | None:
+    """Split-K factor when the W8A16 kernel was measured faster than W8A8 for this fp8 weight
+    shape at the nearest measured row count (``ome_amd/_tuned/w8a16_gfx950.json``, written from
+    ``scripts/w8a16_bench.py``), else None.  Unmeasured shapes: W8A16 at M <= W8A16_DEFAULT_ROWS."""
+    if os.environ.get("OME_W8A16", "1") == "0" or M > 256:
+        return None
+    rows = _w8_table().get(f"{N},{K},{block}")
+    if not rows:
+        return 1 if M <= W8A16_DEFAULT_ROWS else None
+    m_near, e = min(rows, key=lambda r: abs(r[0] - M) / max(r[0], M))
+    if max(m_near, M) > 1.34 * min(m_near, M) or (m_near <= 8) != (M <= 8):
+        return None
+    return int(e["splits"]) if e["us"] < 0.97 * e["w8a8_us"] else None
+
+
+def w8a16_gemm(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0, bias=None,
+               out: torch.Tensor | None = None, splits: int | None = None) -> torch.Tensor:
+    """out[M, N] bf16 = x[M, K] bf16 . dequant(qw)^T (+ bias) for decode rows (M <= 256): the fp8
+    weight is streamed and widened in registers, the activation stays bf16 (no quant pass).
+    qw [N, K] e4m3; sw [N] per channel (block 0) or [ceil(N/128), K/128] (block 128)."""
+    M, K = x.shape
+    N = qw.shape[0]
+    if not _gpu(x):
+        w = ref.fp8_dequant_weight(qw, sw, block).float()
+        r = torch.nn.functional.linear(x.float(), w, None if bias is None else bias.float()).to(torch.bfloat16)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    assert w8a16_ok(x, qw, sw, block), "w8a16_gemm: unsupported operands"
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if out is None else out
+    s = 1 if M <= 8 else (splits or skinny_splits(M, N, K))
+    ws = cnt = None
+    if s > 1:
+        key = _ws_key(x.device)
+        st = _w8_ws.get(key)
+        if st is None:
+            st = _w8_ws[key] = _SkinnyWorkspace(x.device)
+        ws, cnt = st.get((N // 64) * s * 256 * 64), st.cnt   # sized for Mp = 256: never regrown per M
+        assert N // 64 <= cnt.numel()
+    call("ome_w8a16_gemm", x.data_ptr(), x.stride(0), qw.data_ptr(), qw.stride(0), sw.data_ptr(), block, ptr(bias),
+         out.data_ptr(), out.stride(0), M, N, K, s, ptr(ws), ptr(cnt), stream_ptr())
+    return out
+
+
 def fp8_linear(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0, bias=None) -> torch.Tensor:
     """W8A8 linear: dynamic per-token (or per-1x128-group) activation quant + FP8 MFMA GEMM."""
     shape = x.shape

@@ -163,6 +163,8 @@ class Engine:
                                    args.chunked_prefill_size, self.max_context, args.enable_mixed_chunk, prefix)
         # TP / PP ranks schedule in lockstep on broadcast requests: no wall-clock decisions
         self.scheduler.lockstep = self.pstate.world_size > 1 and not self.dp
+        if args.enable_mixed_chunk and os.environ.get("OME_STEP_COST", "1") == "1":
+            self._init_step_cost(args)
         self.tokenizer = get_tokenizer(args.tokenizer_path or args.model_path, self.cfg.vocab_size)
         eos = getattr(self.tokenizer, "eos_token_id", None)
         self.eos_ids = {eos} if eos is not None else set()
@@ -366,6 +368,35 @@ class Engine:
         if self.pstate.world_size > 1 and self.pstate.rank == 0:
             self._broadcast_control([], [], stop=True)
         self._stop = True
+
+    def _init_step_cost(self, args) -> None:
+        """Measure this model's GEMM staircase (runtime/step_cost.py) and give it to the
+        scheduler.  Lockstep ranks (TP / PP) all measure, then take rank 0's table, so every rank
+        cuts its mixed steps identically."""
+        max_rows = min(args.chunked_prefill_size + args.max_running_requests,
+                       int(os.environ.get("OME_STEP_COST_MAX_ROWS", "4096")))
+        cost = self.runner.measure_step_cost(max_rows)
+        if self.scheduler.lockstep:
+            import torch.distributed as dist
+
+            from ome_amd.runtime.step_cost import StepCost
+
+            n = -(-max_rows // StepCost.G)
+            ok = torch.tensor([1 if cost is not None else 0], dtype=torch.int64)
+            dist.broadcast(ok, src=self.pstate.to_global(0), group=self._cpu_group())
+            if not int(ok[0]):
+                cost = None
+            else:
+                buf = torch.tensor(cost.to_list() if cost is not None else [0.0] * n, dtype=torch.float64)
+                dist.broadcast(buf, src=self.pstate.to_global(0), group=self._cpu_group())
+                cost = StepCost(buf.tolist())
+        dump = os.environ.get("OME_STEP_COST_DUMP")
+        if dump and cost is not None and self.pstate.rank == 0:
+            import json
+
+            with open(dump, "w") as f:
+                json.dump({"grid": cost.G, "us_per_layer": [round(v, 2) for v in cost.to_list()]}, f)
+        self.scheduler.cost = cost
 
     def _cpu_group(self):
         import torch.distributed as dist

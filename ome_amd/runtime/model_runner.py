@@ -278,6 +278,43 @@ class ModelRunner:
         if self.use_graph:
             self.capture_graphs()
 
+    # ------------------------------------------------------------------ step-cost table
+    def measure_step_cost(self, max_rows: int, grid: int = 16, reps: int = 3):
+        """GEMM time of one decoder layer at M = grid, 2 grid, ... max_rows rows, routed exactly as
+        the forward routes it (``model.gemm_probe``), alternating two layers so the weights come
+        from HBM as in a layer stack.  Returns a :class:`~ome_amd.runtime.step_cost.StepCost`, or
+        None when the model has no probe or this is not a GPU run."""
+        from ome_amd.runtime.step_cost import StepCost
+
+        m = self.model
+        probe = getattr(m, "gemm_probe", None)
+        layers = [i for i in getattr(m, "layers", range(getattr(self.cfg, "num_layers", 0)))][:2]
+        if probe is None or not self.is_cuda or not layers:
+            return None
+        h, wo = m.gemm_probe_widths()
+        x = torch.randn(max_rows, h, device=self.device, dtype=self.dtype) * 0.5
+        a = torch.randn(max_rows, wo, device=self.device, dtype=self.dtype) * 0.5
+        rows, us = [], []
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            for M in range(grid, max_rows + 1, grid):
+                for i in layers:   # warm-up: routing plans, hipBLASLt heuristics
+                    probe(i, x[:M], a[:M])
+                best = float("inf")
+                for _ in range(reps):
+                    s.record()
+                    for i in layers:
+                        probe(i, x[:M], a[:M])
+                    e.record()
+                    e.synchronize()
+                    best = min(best, s.elapsed_time(e) * 1000.0 / len(layers))
+                rows.append(M)
+                us.append(best)
+        log.info("step-cost table: %d row counts up to %d measured in %.1fs (t(256) %.0f us, t(%d) %.0f us per layer)",
+                 len(rows), max_rows, time.perf_counter() - t0, us[min(len(us), 256 // grid) - 1], rows[-1], us[-1])
+        return StepCost.from_measurements(rows, us, max_rows)
+
     # ------------------------------------------------------------------ helpers
     def decode_ws(self, bs: int, half: int = 0) -> ops.DecodeWorkspace | None:
         """Split-K partitioning chosen so a decode launch has >= ~1024 active workgroups.

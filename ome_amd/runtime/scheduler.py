@@ -87,6 +87,10 @@ class Scheduler:
         self.n_sched = 0
         self.sjf_age_steps = int(os.environ.get("OME_SJF_AGE_STEPS", "32"))
         self.prefill_max_wait_steps = int(os.environ.get("OME_PREFILL_MAX_WAIT_STEPS", "3"))
+        # row-count-aware chunk sizing of mixed steps (runtime/step_cost.py): set by the engine
+        # when the model runner measured its GEMM staircase; None = plain chunked_prefill_size
+        self.cost = None
+        self._pf_deferred = 0
 
     # ------------------------------------------------------------------ queue ops
     def add(self, req: Request) -> None:
@@ -217,8 +221,40 @@ class Scheduler:
             return head
         return min(self.waiting, key=lambda r: (not r.preempted, r.seq_len - r.num_cached))
 
+    def _decode_rows(self) -> int:
+        """Running requests that will ride the next mixed step as 1-token decode rows."""
+        return sum(1 for r in self.running if r.prefill_done and not self._exhausted(r))
+
+    def _prefill_avail(self) -> int:
+        """Prompt tokens a prefill step could take now: the rest of every partially prefilled
+        running request plus the prompts of as many waiting requests as there are free slots."""
+        n = sum(r.seq_len - r.num_cached for r in self.running if r.num_cached < r.seq_len - 1)
+        free = self.max_running - len(self.running)
+        if free > 0 and self.waiting:
+            rest = [r.seq_len - r.num_cached for r in self.waiting]
+            if len(rest) > free:
+                rest = sorted(rest)[:free] if self.policy == "sjf" else rest[:free]
+            n += sum(rest)
+        return n
+
+    def _sized_budget(self) -> int:
+        """The chunked-prefill budget of this step: ``chunk``, or (with a step-cost table and
+        decodes riding along) the chunk that lands M on the cheap side of the GEMM staircase;
+        0 = defer the prefill one step."""
+        if self.cost is None or not self.mixed:
+            return self.chunk
+        d = self._decode_rows()
+        avail = self._prefill_avail() if d else 0
+        if avail == 0:
+            return self.chunk
+        p = self.cost.choose(d, avail, self.chunk, self._pf_deferred)
+        self._pf_deferred = self._pf_deferred + 1 if p == 0 else 0
+        return p
+
     def _schedule_prefill(self) -> StepBatch | None:
-        budget = self.chunk
+        budget = self._sized_budget()
+        if budget <= 0:
+            return None
         chunks: list[ScheduledChunk] = []
         # 1) continue partially prefilled running requests
         for r in self.running:

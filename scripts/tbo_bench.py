@@ -85,7 +85,21 @@ def main():
     ap.add_argument("--prompts", type=int, default=64)
     ap.add_argument("--new", type=int, default=64)
     ap.add_argument("--modes", default="off,on,off,on", help="comma list of off / on (one engine pair per entry)")
+    ap.add_argument("--rank", type=int, default=-1,
+                    help="run ONE rank in this process (MASTER_PORT from the env; the first --modes entry): "
+                         "scripts/tbo_trace.sh starts each rank under its own rocprofv3")
     a = ap.parse_args()
+    if a.rank >= 0:
+        import queue
+
+        q = queue.Queue()
+        _worker(a.rank, 2, int(os.environ["MASTER_PORT"]), a, a.modes.split(",")[0].strip() == "on", q)
+        rank, out, tb = q.get()
+        if tb:
+            sys.exit(f"rank {rank}:\n{tb}")
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        return
     for tbo in [m.strip() == "on" for m in a.modes.split(",")]:
         r = run(a, tbo)
         r.update(model=a.model, layers=a.layers, prompts=a.prompts, new_tokens=a.new,

@@ -64,3 +64,41 @@ def test_fp8_engine_decode_graphs():
     eng.flush()
     assert all(len(r.output_ids) == 12 for r in reqs)
     assert reqs[0].output_ids == reqs[2].output_ids  # same prompt, greedy
+
+
+@pytest.mark.parametrize("block", [0, 128])
+@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (3, 1536, 7168), (8, 576, 7168), (5, 64, 128),
+                                   (9, 4096, 14336), (32, 6144, 4096), (64, 128, 256), (100, 1536, 7168),
+                                   (128, 4096, 4096), (200, 576, 7168), (256, 6144, 4096)])
+@pytest.mark.parametrize("splits", [None, 1])
+def test_w8a16_gemm(block, M, N, K, splits):
+    """fp8 weight x bf16 activation (csrc/kernels/w8a16.hip) vs the fp32 reference on the
+    dequantised weight: GEMV rows (M <= 8) and the skinny MFMA tile with and without split-K."""
+    if (M <= 8 and splits == 1) or (block and K % 128):
+        pytest.skip("GEMV has no split-K / block 128 needs K % 128 == 0")
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    qw = quantize_weight(w, block)
+    bias = torch.randn(N, device=DEV).to(torch.bfloat16)
+    got = ops.w8a16_gemm(x, qw.q, qw.scale, block, bias, splits=splits)
+    wd = ref.fp8_dequant_weight(qw.q.cpu(), qw.scale.cpu(), block).float()
+    want = F.linear(x.float().cpu(), wd, bias.float().cpu())
+    err = (got.float().cpu() - want).abs().max().item()
+    assert err <= 1e-2 * want.abs().max().item() + 1e-2, err
+    # graph replay of the split-K path re-arms its tile counters
+    if M > 8:
+        out = torch.empty_like(got)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            ops.w8a16_gemm(x, qw.q, qw.scale, block, bias, out=out, splits=splits)
+            with torch.cuda.graph(g, stream=s):
+                ops.w8a16_gemm(x, qw.q, qw.scale, block, bias, out=out, splits=splits)
+        torch.cuda.current_stream().wait_stream(s)
+        for _ in range(3):
+            out.zero_()
+            g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, got)
