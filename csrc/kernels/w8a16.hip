@@ -16,7 +16,9 @@
 //   * w8_skinny_kernel, 8 < M <= 256: the skinny MFMA tile (csrc/kernels/skinny_gemm.hip: one
 //     workgroup = all M rows x 64 weight rows, split-K when the weight has few row tiles) with
 //     the W step (64 rows x 64 k) loaded as 4 KiB of e4m3 -- one 16-byte load per thread -- and
-//     widened to bf16 on its way into LDS.  Per-channel scales multiply the fp32 accumulators in
+//     widened to bf16 on its way into LDS.  3-4 K steps of both operands ride a register ring
+//     (the first version waited one global round trip per 64-deep step: 0.4-0.8 TB/s) and the
+//     LDS tiles are double-buffered, one barrier per step.  Per-channel scales multiply the fp32 accumulators in
 //     the epilogue (exact widening, one rounding); block scales are folded into the widening of
 //     each 64-deep K step (bf16(q * s), the same values the old dequantised bf16 copy held).
 // Both end in the skinny kernel's deterministic split-K reduction (fixed split order, last
@@ -137,6 +139,14 @@ __global__ __launch_bounds__(256) void w8_gemv_kernel(const bf16* __restrict__ X
 constexpr int NT = 64;   // weight rows per workgroup
 constexpr int KB = 64;   // K per step
 
+// workgroup barrier ordering LDS only: wait for this wave's LDS traffic, then s_barrier (global
+// loads in flight stay in flight)
+__device__ __forceinline__ void w8_lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ int w8_sw(int row, int chunk) { return row * 8 + (chunk ^ (row & 7)); }
 
 template <int MB, int BLK>   // 16-row activation blocks per wave: Mp = 64 * MB
@@ -146,8 +156,11 @@ __global__ __launch_bounds__(256) void w8_skinny_kernel(const bf16* __restrict__
                                                         bf16* __restrict__ out, int64_t ldo, int M, int N, int K,
                                                         int splits, float* __restrict__ ws, int* __restrict__ cnt) {
   constexpr int MP = 64 * MB, XL = MP * 8 / 256;   // 16-byte X chunks per thread per step
-  __shared__ __attribute__((aligned(16))) bf16 sX[MP * KB];
-  __shared__ __attribute__((aligned(16))) bf16 sW[NT * KB];
+  // PD K steps of operands in flight per thread (a register ring: one global round trip per PD
+  // steps, not per step) and two LDS buffers (one barrier per step)
+  constexpr int PD = MB == 4 ? 3 : 4;
+  __shared__ __attribute__((aligned(16))) bf16 sX[2][MP * KB];
+  __shared__ __attribute__((aligned(16))) bf16 sW[2][NT * KB];
   __shared__ int s_last;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int tile = blockIdx.x / splits, split = blockIdx.x - tile * splits;
@@ -160,16 +173,16 @@ __global__ __launch_bounds__(256) void w8_skinny_kernel(const bf16* __restrict__
   const uint8_t* wp = W + (int64_t)wn * ldw + 16 * wc;
   const float* wsc = BLK ? sw + (int64_t)(wn >> 7) * kb : sw;
 
-  bf16x8 rx[XL];
-  w8_u32x4 rw;
-  auto load = [&](int s) {
+  bf16x8 rx[PD][XL];
+  w8_u32x4 rw[PD];
+  auto load = [&](int j, int s) {   // j: compile-time ring slot after unrolling
     const int k0 = s * KB;
 #pragma unroll
     for (int i = 0; i < XL; ++i) {
       const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
-      rx[i] = row < M ? ld8(X + (int64_t)row * ldx + k0 + 8 * ch) : bf16x8{};
+      rx[j][i] = row < M ? ld8(X + (int64_t)row * ldx + k0 + 8 * ch) : bf16x8{};
     }
-    rw = *reinterpret_cast<const w8_u32x4*>(wp + k0);
+    rw[j] = *reinterpret_cast<const w8_u32x4*>(wp + k0);
   };
 
   f32x4 acc[4][MB];
@@ -179,40 +192,52 @@ __global__ __launch_bounds__(256) void w8_skinny_kernel(const bf16* __restrict__
     for (int mb = 0; mb < MB; ++mb) acc[nb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int r0 = wave * 16 * MB, lr = lane & 15, lg = lane >> 4;
-  if (s0 < s1) load(s0);
-  for (int s = s0; s < s1; ++s) {
-    __syncthreads();   // the previous step's LDS reads are done
 #pragma unroll
-    for (int i = 0; i < XL; ++i) {
-      const int c = tid + 256 * i;
-      *reinterpret_cast<bf16x8*>(&sX[w8_sw(c >> 3, c & 7) * 8]) = rx[i];
-    }
-    bf16x8 w0, w1;
-    if constexpr (BLK) {
-      const float sc = wsc[(s * KB) >> 7];
-      w0 = w8_cvt8_scaled(rw[0], rw[1], sc);
-      w1 = w8_cvt8_scaled(rw[2], rw[3], sc);
-    } else {
-      w0 = w8_cvt8(rw[0], rw[1]);
-      w1 = w8_cvt8(rw[2], rw[3]);
-    }
-    *reinterpret_cast<bf16x8*>(&sW[w8_sw(wrow, 2 * wc) * 8]) = w0;
-    *reinterpret_cast<bf16x8*>(&sW[w8_sw(wrow, 2 * wc + 1) * 8]) = w1;
-    __syncthreads();
-    if (s + 1 < s1) load(s + 1);
+  for (int j = 0; j < PD; ++j)
+    if (s0 + j < s1) load(j, s0 + j);
+  for (int sb = s0; sb < s1; sb += PD) {
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ch = 4 * kk + lg;
-      bf16x8 a[4], b[MB];
+    for (int j = 0; j < PD; ++j) {
+      const int s = sb + j;
+      if (s >= s1) break;
+      bf16* bx = sX[(s - s0) & 1];
+      bf16* bw = sW[(s - s0) & 1];
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) a[nb] = *reinterpret_cast<const bf16x8*>(&sW[w8_sw(nb * 16 + lr, ch) * 8]);
+      for (int i = 0; i < XL; ++i) {
+        const int c = tid + 256 * i;
+        *reinterpret_cast<bf16x8*>(&bx[w8_sw(c >> 3, c & 7) * 8]) = rx[j][i];
+      }
+      bf16x8 w0, w1;
+      if constexpr (BLK) {
+        const float sc = wsc[(s * KB) >> 7];
+        w0 = w8_cvt8_scaled(rw[j][0], rw[j][1], sc);
+        w1 = w8_cvt8_scaled(rw[j][2], rw[j][3], sc);
+      } else {
+        w0 = w8_cvt8(rw[j][0], rw[j][1]);
+        w1 = w8_cvt8(rw[j][2], rw[j][3]);
+      }
+      *reinterpret_cast<bf16x8*>(&bw[w8_sw(wrow, 2 * wc) * 8]) = w0;
+      *reinterpret_cast<bf16x8*>(&bw[w8_sw(wrow, 2 * wc + 1) * 8]) = w1;
+      // this step's tile is visible; the buffer written here was last read two steps ago,
+      // before the previous step's barrier.  LDS-only barrier: __syncthreads() would also drain
+      // the register ring's global loads (vmcnt(0)) and serialise every step on a round trip
+      w8_lds_barrier();
+      if (s + PD < s1) load(j, s + PD);
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) b[mb] = *reinterpret_cast<const bf16x8*>(&sX[w8_sw(r0 + mb * 16 + lr, ch) * 8]);
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = 4 * kk + lg;
+        bf16x8 a[4], b[MB];
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
+        for (int nb = 0; nb < 4; ++nb) a[nb] = *reinterpret_cast<const bf16x8*>(&bw[w8_sw(nb * 16 + lr, ch) * 8]);
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)
-          acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nb], b[mb], acc[nb][mb], 0, 0, 0);
+          b[mb] = *reinterpret_cast<const bf16x8*>(&bx[w8_sw(r0 + mb * 16 + lr, ch) * 8]);
+#pragma unroll
+        for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb)
+            acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nb], b[mb], acc[nb][mb], 0, 0, 0);
+      }
     }
   }
 

@@ -339,7 +339,13 @@ class LlamaForCausalLM:
         self._row_parallel(a, self.w_o[i])
         self._mlp_partial(i, x)
 
-    def gemm_probe_widths(self) -> tuple[int, int]:
+    def gemm_probe_widths(self) -> tuple[int, int] | None:
+        """(hidden, O-projection input width) when this model's layers run exactly the dense
+        QKV / O / gate_up / down projections :meth:`gemm_probe` times, else None (MoE, MLA and
+        other subclasses that reuse the class with a different layer)."""
+        i = self.layers[0] if self.layers else None
+        if i is None or not self._plain() or any(lst[i] is None for lst in (self.w_qkv, self.w_o, self.w_gu, self.w_d)):
+            return None
         return self.cfg.hidden_size, self.tp.hq * self.D
 
     def mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:

@@ -1330,10 +1330,13 @@ def prefill_rows(Hq: int, Hkv: int, D: int, page: int = 16) -> int:
     """Rows per classic prefill work item for this attention shape (see PREFILL_ROWS)."""
     ok = D == 128 and page == 16 and Hq == 4 * Hkv and os.environ.get("OME_PREFILL_ATTN", "2") == "2"
     return PREFILL_ROWS if ok and PREFILL_ROWS in (32, 64) else 32
-# an item must span more than this many keys before a small grid is split.  2048 since the causal
-# fast body (profiles/r03_prefill_split_bench_fast.txt): classic now wins at 700 and 2000 keys
-# (27 vs 34 us, 85 vs 93 us) and split still wins 256 new rows over a 4096-key prefix (53 vs 132 us)
-PREFILL_SPLIT_MIN_KEYS = int(os.environ.get("OME_PREFILL_SPLIT_MIN_KEYS", "2048"))
+# an item must span more than this many keys before a small grid (< 256 workgroups) is split.
+# r03 (profiles/r03_prefill_split_bench_fast.txt) set 2048: at ~900 rows classic won at 700 and
+# 2000 keys (27 vs 34 us, 85 vs 93 us).  r06: with row-count-aware chunk sizing the mixed steps
+# carry 250-770 prompt rows, a 64-workgroup grid walking ~15 serial key tiles (27 us per layer);
+# splitting from 256 keys measured best of 2048 / 512 / 256 on the headline (16.30k / 16.35k /
+# 16.39k tok/s, one box)
+PREFILL_SPLIT_MIN_KEYS = int(os.environ.get("OME_PREFILL_SPLIT_MIN_KEYS", "256"))
 
 
 def prefill_plan(q_lens: list[int], kv_lens: list[int], tile: int = 32, target: int | None = None,

@@ -284,14 +284,22 @@ class ModelRunner:
         the forward routes it (``model.gemm_probe``), alternating two layers so the weights come
         from HBM as in a layer stack.  Returns a :class:`~ome_amd.runtime.step_cost.StepCost`, or
         None when the model has no probe or this is not a GPU run."""
-        from ome_amd.runtime.step_cost import StepCost
-
         m = self.model
         probe = getattr(m, "gemm_probe", None)
         layers = [i for i in getattr(m, "layers", range(getattr(self.cfg, "num_layers", 0)))][:2]
-        if probe is None or not self.is_cuda or not layers:
+        widths = m.gemm_probe_widths() if probe is not None and self.is_cuda and layers else None
+        if widths is None:
             return None
-        h, wo = m.gemm_probe_widths()
+        try:
+            return self._measure_step_cost(probe, layers, widths, max_rows, grid, reps)
+        except Exception as e:  # noqa: BLE001 -- a failed probe must not take serving down
+            log.warning("step-cost probe failed (%s); mixed steps use the fixed chunk size", e)
+            return None
+
+    def _measure_step_cost(self, probe, layers, widths, max_rows: int, grid: int, reps: int):
+        from ome_amd.runtime.step_cost import StepCost
+
+        h, wo = widths
         x = torch.randn(max_rows, h, device=self.device, dtype=self.dtype) * 0.5
         a = torch.randn(max_rows, wo, device=self.device, dtype=self.dtype) * 0.5
         rows, us = [], []

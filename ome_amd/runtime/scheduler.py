@@ -225,17 +225,23 @@ class Scheduler:
         """Running requests that will ride the next mixed step as 1-token decode rows."""
         return sum(1 for r in self.running if r.prefill_done and not self._exhausted(r))
 
-    def _prefill_avail(self) -> int:
-        """Prompt tokens a prefill step could take now: the rest of every partially prefilled
-        running request plus the prompts of as many waiting requests as there are free slots."""
-        n = sum(r.seq_len - r.num_cached for r in self.running if r.num_cached < r.seq_len - 1)
+    def _prefill_avail(self) -> tuple[int, list[int]]:
+        """Prompt tokens a prefill step could take now -- the rest of every partially prefilled
+        running request plus the prompts of as many waiting requests as there are free slots --
+        and the cumulative counts at which each of those prompts ends, in admission order."""
+        rest = [r.seq_len - r.num_cached for r in self.running if r.num_cached < r.seq_len - 1]
         free = self.max_running - len(self.running)
         if free > 0 and self.waiting:
-            rest = [r.seq_len - r.num_cached for r in self.waiting]
-            if len(rest) > free:
-                rest = sorted(rest)[:free] if self.policy == "sjf" else rest[:free]
-            n += sum(rest)
-        return n
+            w = [r.seq_len - r.num_cached for r in self.waiting]
+            if self.policy == "sjf":
+                w = [w[0]] + sorted(w[1:]) if self._waited(self.waiting[0], self.sjf_age_s, self.sjf_age_steps) \
+                    else sorted(w)
+            rest += w[:free]
+        bounds, n = [], 0
+        for k in rest:
+            n += k
+            bounds.append(n)
+        return n, bounds
 
     def _sized_budget(self) -> int:
         """The chunked-prefill budget of this step: ``chunk``, or (with a step-cost table and
@@ -244,10 +250,10 @@ class Scheduler:
         if self.cost is None or not self.mixed:
             return self.chunk
         d = self._decode_rows()
-        avail = self._prefill_avail() if d else 0
+        avail, bounds = self._prefill_avail() if d else (0, [])
         if avail == 0:
             return self.chunk
-        p = self.cost.choose(d, avail, self.chunk, self._pf_deferred)
+        p = self.cost.choose(d, avail, self.chunk, self._pf_deferred, bounds)
         self._pf_deferred = self._pf_deferred + 1 if p == 0 else 0
         return p
 

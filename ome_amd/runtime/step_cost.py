@@ -40,6 +40,8 @@ class StepCost:
         self.defer_ratio = float(os.environ.get("OME_STEP_COST_DEFER", "1.3")) if defer_ratio is None else defer_ratio
         self.max_defer = int(os.environ.get("OME_STEP_COST_MAX_DEFER", "1")) if max_defer is None else max_defer
         self.tie = tie
+        # relative cost slack for preferring a cut on a prompt boundary (TTFT)
+        self.ttft_tol = float(os.environ.get("OME_STEP_COST_TTFT_TOL", "0.05"))
 
     @property
     def max_rows(self) -> int:
@@ -74,20 +76,25 @@ class StepCost:
         lo = min(cap, max(1, 2 * self.slack))
         return min(self.marginal(d, p) for p in self._cands(d, lo, cap))
 
-    def choose(self, d: int, avail: int, cap: int, deferred: int = 0) -> int:
+    def choose(self, d: int, avail: int, cap: int, deferred: int = 0, bounds: list[int] | None = None) -> int:
         """Prompt tokens to prefill this step (0 = defer).  ``d``: decode rows riding the step,
         ``avail``: prompt tokens ready, ``cap``: the chunked-prefill cap, ``deferred``: how many
         consecutive steps this prefill has been deferred.
 
         Minimises this step's added GEMM time plus the leftover priced at :meth:`reference`:
         cost(p) = t(d + p) - t(d) + (hi - p) * ref over p in [hi - slack, hi] (and p = 0 when the
-        whole remainder is small and the deferral budget allows)."""
+        whole remainder is small and the deferral budget allows).  ``bounds``: cumulative token
+        counts at which a prompt ends in admission order; a cut there within ``ttft_tol`` of the
+        best cost is preferred (a prompt cut mid-way waits a whole extra step for its first token)."""
         hi = min(avail, cap)
         if hi <= 0:
             return 0
         ref = self.reference(d, cap)
         base = self.at(d)
-        cands = self._cands(d, max(1, hi - self.slack), hi)
+        lo = max(1, hi - self.slack)
+        cands = self._cands(d, lo, hi)
+        ends = sorted({b for b in (bounds or ()) if lo <= b <= hi})
+        cands = sorted(set(cands) | set(ends))
         if deferred < self.max_defer and hi <= self.slack < cap:
             cands = [0] + cands
         best_p, best_c = hi, None
@@ -97,6 +104,12 @@ class StepCost:
             if best_c is None or c < best_c - self.tie * ref * self.G or (c <= best_c + self.tie * ref * self.G
                                                                           and p > best_p):
                 best_p, best_c = p, c
+        if ends and best_p not in ends and best_p != hi:
+            # the largest prompt-boundary cut whose cost is within ttft_tol of the best
+            slack_us = self.ttft_tol * (self.at(d + max(best_p, 1)) - base + (hi - best_p) * ref)
+            for p in reversed(ends):
+                if self.at(d + p) - base + (hi - p) * ref <= best_c + slack_us:
+                    return p
         return best_p
 
     # ------------------------------------------------------------------ (de)serialisation

@@ -43,6 +43,28 @@ def main(d):
                   f"kernel time {busy / 1e6:.1f} ms, exchange wait / signal kernels {wait / 1e6:.1f} ms "
                   f"({100 * wait / max(busy, 1):.0f} %)")
             print("queues/streams:", dict(queues))
+            # intra-process overlap: time covered by >= 2 of this process's kernels at once
+            ev = []
+            for r in rs:
+                ev.append((int(r["Start_Timestamp"]), 1))
+                ev.append((int(r["End_Timestamp"]), -1))
+            ev.sort()
+            depth, last, cover, multi = 0, None, 0, 0
+            for t, dv in ev:
+                if last is not None and depth > 0:
+                    cover += t - last
+                    if depth > 1:
+                        multi += t - last
+                depth += dv
+                last = t
+            print(f"kernel-covered time {cover / 1e6:.1f} ms, of which >= 2 kernels in flight {multi / 1e6:.1f} ms "
+                  f"({100 * multi / max(cover, 1):.0f} %)")
+            # the exchange kernels' longest instances: a wait that lasts milliseconds is a rank
+            # waiting on a peer whose matching kernel is queued behind other work
+            ex = sorted(((int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), r["Kernel_Name"]) for r in rs
+                        if "ep_" in r["Kernel_Name"] or "wait" in r["Kernel_Name"]), reverse=True)[:8]
+            if ex:
+                print("longest exchange kernels (us):", ", ".join(f"{d / 1e3:.0f} {short(n, 40)}" for d, n in ex))
             print("| total ms | calls | avg us | max us | kernel |\n|---:|---:|---:|---:|---|")
             for n, v in tot.most_common(15):
                 print(f"| {v / 1e6:.2f} | {cnt[n]} | {v / cnt[n] / 1e3:.1f} | {mx[n] / 1e3:.1f} | `{short(n)}` |")

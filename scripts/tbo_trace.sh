@@ -20,7 +20,7 @@ for m in ${TBO_MODES:-off on}; do
   done
   rc=0
   for p in "${pids[@]}"; do wait $p || rc=$?; done
-  [ $rc -eq 0 ] || { echo "mode $m failed rc=$rc"; tail -5 $O/$m.r*.log; exit $rc; }
+  [ $rc -eq 0 ] || { echo "mode $m failed rc=$rc"; tail -n 5 $O/$m.r0.log $O/$m.r1.log; exit $rc; }
   echo "TBO $m: $(grep -h '"tok_s"' $O/$m.r0.log)"
   python3 $R/scripts/tbo_trace.py $O/$m > $O/summary_$m.md || exit 1
   find $O/$m -name "*kernel_trace.csv" -size +20M -delete

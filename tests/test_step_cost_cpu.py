@@ -99,3 +99,14 @@ def test_scheduler_without_decodes_uses_full_chunk():
     s.add(Request(prompt_ids=[3] * 100, params=SamplingParams(max_new_tokens=4), rid="p"))
     b = s.schedule()
     assert b.num_tokens == 100
+
+
+def test_prefers_prompt_boundary_within_tolerance():
+    sc = _stairs()
+    sc.ttft_tol = 0.05
+    # best grid cut is 256 (M = 512); a prompt ends at 250: nearly the same cost, no prompt split
+    assert sc.choose(256, 300, 2048, bounds=[250, 300]) == 250
+    # a boundary that would open a new tile is not worth it
+    assert sc.choose(256, 300, 2048, bounds=[280, 300]) == 256
+    sc.ttft_tol = 0.0
+    assert sc.choose(256, 300, 2048, bounds=[250, 300]) == 256
