@@ -268,6 +268,9 @@ __global__ __launch_bounds__(256) void ep_comb_pull_kernel(EpPeers P, int me, in
 // owner-writes / peers-read protocol of the unfused kernels above.
 // ------------------------------------------------------------------------------------------
 constexpr int kRecvBlocks = 32;
+// largest grid whose every workgroup may spin on the peer flags itself (decode-sized token
+// counts: saves the separate wait launch); larger grids wait in one 64-thread ep_wait_kernel
+constexpr int kSpinMaxBlocks = 64;
 
 __device__ __forceinline__ bool last_block(uint32_t* done) {
   __shared__ int last;
@@ -415,13 +418,17 @@ __global__ __launch_bounds__(256) void ep_comb_send_kernel(EpPeers P, int me, in
 }
 
 // grid = tokens: wait for every owner's combine flag, then the weighted sum of ep_comb_pull_kernel
+// spin = 0: the flags were already waited for by ep_wait_kernel on the same stream (grids larger
+// than kSpinMaxBlocks: thousands of resident spinning workgroups -- one per token of a prefill
+// chunk -- would hold the CUs that the co-scheduled work, e.g. the other two-batch-overlap half or
+// a peer process sharing the GPU, needs to make progress; profiles/r06_tbo_trace.md)
 __global__ __launch_bounds__(256) void ep_comb_recv_kernel(EpPeers P, int me, int W, int H, int k, int cap, Layout L,
                                                            EpSig* self, const float* __restrict__ topk_w,
                                                            const int* __restrict__ a_dst,
                                                            const int* __restrict__ a_slot, float scale,
-                                                           bf16* __restrict__ out, int64_t ldo) {
+                                                           bf16* __restrict__ out, int64_t ldo, int spin) {
   const uint32_t cur = self->epoch;
-  if ((int)threadIdx.x < W) spin_flag(P, self, 1, threadIdx.x, cur);
+  if (spin && (int)threadIdx.x < W) spin_flag(P, self, 1, threadIdx.x, cur);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const int t = blockIdx.x;
@@ -567,9 +574,12 @@ OME_API int ome_ep_combine(void* ctx, const void* y_sorted, const int* inv, cons
   if (fused()) {
     ep_comb_send_kernel<<<dim3(kRecvBlocks, c->world), 256, 0, stream>>>(
         c->peers, c->rank, c->world, (const bf16*)y_sorted, inv, rcount, c->H, c->cap, c->L, c->sig, c->buf);
-    if (T > 0)
+    if (T > 0) {
+      const int spin = T <= kSpinMaxBlocks;
+      if (!spin) ep_wait_kernel<<<1, 64, 0, stream>>>(c->peers, c->sig, c->world, 1);
       ep_comb_recv_kernel<<<T, 256, 0, stream>>>(c->peers, c->rank, c->world, c->H, k, c->cap, c->L, c->sig, topk_w,
-                                                 a_dst, a_slot, scale, (bf16*)out, ldo);
+                                                 a_dst, a_slot, scale, (bf16*)out, ldo, spin);
+    }
     return (int)hipGetLastError();
   }
   ep_comb_pack_kernel<<<dim3(c->cap, c->world), 256, 0, stream>>>((const bf16*)y_sorted, inv, rcount, c->H, c->cap,

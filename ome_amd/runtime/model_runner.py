@@ -8,6 +8,7 @@ sampled ids.  Prefill / mixed steps run eagerly (their GPU time dwarfs launch ov
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 
 import logging
@@ -169,6 +170,7 @@ class ModelRunner:
         self.tbo = bool(self.ep_ll and pstate.get().tbo and pstate.get().ep_ll_b is not None)
         self._tbo_stream = torch.cuda.Stream(self.device) if self.tbo else None
         self._tbo_keep: dict = {}
+        self.launch_stats = collections.Counter()
         self.stateful = bool(getattr(self.model, "stateful", False))
         if self.stateful:  # recurrent (SSM) state per request slot, the padding slot included; before
             # the KV sizing below so the page budget sees it
@@ -507,10 +509,13 @@ class ModelRunner:
         if batch.mode == "decode" and (not self.pp or self.use_graph) and all(c.length == 1 for c in batch.chunks):
             bs = next((b for b in self.buckets if b >= len(batch.chunks)), None)
             if bs is not None:
+                self.launch_stats["decode-graph" if allow_graph and self.use_graph else "decode-eager"] += 1
                 return self._launch_decode(batch, bs, prev, graph=allow_graph)
+        self.launch_stats[f"{batch.mode}-eager"] += 1
         return self._launch_eager(batch, prev)
 
     probe_log: list | None = None   # (mode, host ms from launch start to the input copy, prev step done?)
+    launch_stats: "collections.Counter"   # steps launched per path (decode-graph / decode-eager / <mode>-eager)
 
     def _probe_mark(self, mode: str) -> None:
         if self.probe is not None:

@@ -45,9 +45,10 @@ def _worker(rank, world, port, a, tbo, q):
             n = sum(len(r.output_ids) for r in reqs)
             eng.stop_group()
             q.put((rank, {"tbo": tbo, "tok_s": round(n / dt, 1), "seconds": round(dt, 3), "tokens": n,
-                          "runner_tbo": eng.runner.tbo}, None))
+                          "runner_tbo": eng.runner.tbo, "launches": dict(eng.runner.launch_stats)}, None))
         else:
             eng.run_forever()
+            print(json.dumps({"rank": rank, "launches": dict(eng.runner.launch_stats)}), flush=True)
             q.put((rank, None, None))
     except Exception:  # noqa: BLE001
         q.put((rank, None, traceback.format_exc()))
