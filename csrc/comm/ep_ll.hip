@@ -366,10 +366,10 @@ __global__ __launch_bounds__(256) void ep_send_kernel(EpPeers P, int me, int W, 
 // grid (kRecvBlocks, W): rows source `src` sent me, R [W][cap][H]; rids past the count = e_local
 __global__ __launch_bounds__(256) void ep_recv_kernel(EpPeers P, int me, int H, int cap, int e_local, Layout L,
                                                       EpSig* self, bf16* __restrict__ R, int* __restrict__ rids,
-                                                      int* __restrict__ rcount) {
+                                                      int* __restrict__ rcount, int spin) {
   const int g = blockIdx.x, src = blockIdx.y;
   const uint32_t cur = self->epoch;
-  if (threadIdx.x == 0) spin_flag(P, self, 0, src, cur);
+  if (spin && threadIdx.x == 0) spin_flag(P, self, 0, src, cur);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const int par = cur & 1;
@@ -452,6 +452,16 @@ __global__ __launch_bounds__(256) void ep_comb_recv_kernel(EpPeers P, int me, in
 }
 
 // OME_EP_LL_FUSED=0 selects the 10-launch kernels (A/B timing)
+// OME_EP_WAIT_KERNEL=1: every receive waits in one 64-thread kernel (no spinning workgroups in
+// the copy kernels; one extra launch per exchange) -- the two-batch-overlap experiment
+static bool wait_kernel() {
+  static const bool w = [] {
+    const char* e = getenv("OME_EP_WAIT_KERNEL");
+    return e && atoi(e) == 1;
+  }();
+  return w;
+}
+
 static bool fused() {
   static const bool f = !getenv("OME_EP_LL_FUSED") || atoi(getenv("OME_EP_LL_FUSED")) != 0;
   return f;
@@ -547,8 +557,10 @@ OME_API int ome_ep_dispatch(void* ctx, const void* x, int64_t ldx, const int* to
     ep_send_kernel<<<n > 0 ? n : 1, 256, 0, stream>>>(c->peers, c->rank, c->world, (const bf16*)x, ldx, c->H, k,
                                                       topk_ids, n, e_local, n_experts, c->cap, a_dst, a_slot, a_local,
                                                       rep_rank, rep_slot, n_rep, rmax, c->sig, c->buf, c->L);
+    const int spin = !wait_kernel();
+    if (!spin) ep_wait_kernel<<<1, 64, 0, stream>>>(c->peers, c->sig, c->world, 0);
     ep_recv_kernel<<<dim3(kRecvBlocks, c->world), 256, 0, stream>>>(c->peers, c->rank, c->H, c->cap, e_local, c->L,
-                                                                   c->sig, (bf16*)R, rids, rcount);
+                                                                   c->sig, (bf16*)R, rids, rcount, spin);
     return (int)hipGetLastError();
   }
   ep_begin_kernel<<<1, 64, 0, stream>>>(c->sig);
@@ -575,7 +587,7 @@ OME_API int ome_ep_combine(void* ctx, const void* y_sorted, const int* inv, cons
     ep_comb_send_kernel<<<dim3(kRecvBlocks, c->world), 256, 0, stream>>>(
         c->peers, c->rank, c->world, (const bf16*)y_sorted, inv, rcount, c->H, c->cap, c->L, c->sig, c->buf);
     if (T > 0) {
-      const int spin = T <= kSpinMaxBlocks;
+      const int spin = T <= kSpinMaxBlocks && !wait_kernel();
       if (!spin) ep_wait_kernel<<<1, 64, 0, stream>>>(c->peers, c->sig, c->world, 1);
       ep_comb_recv_kernel<<<T, 256, 0, stream>>>(c->peers, c->rank, c->world, c->H, k, c->cap, c->L, c->sig, topk_w,
                                                  a_dst, a_slot, scale, (bf16*)out, ldo, spin);
