@@ -1332,11 +1332,9 @@ def prefill_rows(Hq: int, Hkv: int, D: int, page: int = 16) -> int:
     return PREFILL_ROWS if ok and PREFILL_ROWS in (32, 64) else 32
 # an item must span more than this many keys before a small grid (< 256 workgroups) is split.
 # r03 (profiles/r03_prefill_split_bench_fast.txt) set 2048: at ~900 rows classic won at 700 and
-# 2000 keys (27 vs 34 us, 85 vs 93 us).  r06: with row-count-aware chunk sizing the mixed steps
-# carry 250-770 prompt rows, a 64-workgroup grid walking ~15 serial key tiles (27 us per layer);
-# splitting from 256 keys measured best of 2048 / 512 / 256 on the headline (16.30k / 16.35k /
-# 16.39k tok/s, one box)
-PREFILL_SPLIT_MIN_KEYS = int(os.environ.get("OME_PREFILL_SPLIT_MIN_KEYS", "256"))
+# 2000 keys (27 vs 34 us, 85 vs 93 us).  r06 tried 256: +0.5 % in-process (16.30k -> 16.39k,
+# within box noise) but -7 % over HTTP (15.05k -> 14.01k, profiles/r06_step_cost_ab.txt), so 2048 stays
+PREFILL_SPLIT_MIN_KEYS = int(os.environ.get("OME_PREFILL_SPLIT_MIN_KEYS", "2048"))
 
 
 def prefill_plan(q_lens: list[int], kv_lens: list[int], tile: int = 32, target: int | None = None,

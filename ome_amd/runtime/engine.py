@@ -163,7 +163,7 @@ class Engine:
                                    args.chunked_prefill_size, self.max_context, args.enable_mixed_chunk, prefix)
         # TP / PP ranks schedule in lockstep on broadcast requests: no wall-clock decisions
         self.scheduler.lockstep = self.pstate.world_size > 1 and not self.dp
-        if args.enable_mixed_chunk and os.environ.get("OME_STEP_COST", "1") == "1":
+        if args.enable_mixed_chunk and os.environ.get("OME_STEP_COST", "0") == "1":
             self._init_step_cost(args)
         self.tokenizer = get_tokenizer(args.tokenizer_path or args.model_path, self.cfg.vocab_size)
         eos = getattr(self.tokenizer, "eos_token_id", None)

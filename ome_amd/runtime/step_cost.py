@@ -16,7 +16,12 @@ the leftover is bounded), the leftover priced at what a full-size chunk costs pe
 is far above a good chunk's, the prefill is deferred one step (bounded by ``max_defer`` steps,
 counted in schedule() calls so TP / PP ranks stay in lockstep) to merge with the next arrivals.
 
-This is the MI355X-side replacement for the reference runtimes' fixed ``--chunked-prefill-size``
+Status (profiles/r06_step_cost_ab.txt): opt-in (``OME_STEP_COST=1``).  In-process the aggressive
+form measured +1-2 % tokens/s at +6-12 ms p50 TTFT; over HTTP it cost 2-12 % (more, smaller eager
+mixed steps compete with the server threads for the host), so the engine default stays the plain
+chunk cap.
+
+This is the MI355X-side complement to the reference runtimes' fixed ``--chunked-prefill-size``
 (``config/runtimes/srt/meta/llama-3-8b-instruct-rt.yaml``): the flag still caps the chunk; the
 cost table decides where below the cap to cut.  The table is measured by the model runner at
 start-up on the model's own layer-0/1 projection weights (``ModelRunner.measure_step_cost``) and,
@@ -42,6 +47,10 @@ class StepCost:
         self.tie = tie
         # relative cost slack for preferring a cut on a prompt boundary (TTFT)
         self.ttft_tol = float(os.environ.get("OME_STEP_COST_TTFT_TOL", "0.05"))
+        # below this many ready prompt tokens a step takes them all (no cut, no deferral): cutting
+        # small prefills makes more, smaller mixed steps -- eager launches whose host cost the HTTP
+        # server's threads compete for (profiles/r06_step_cost_ab.txt, HTTP block)
+        self.min_avail = int(os.environ.get("OME_STEP_COST_MIN_AVAIL", "768"))
 
     @property
     def max_rows(self) -> int:
@@ -89,6 +98,8 @@ class StepCost:
         hi = min(avail, cap)
         if hi <= 0:
             return 0
+        if hi < self.min_avail:
+            return hi
         ref = self.reference(d, cap)
         base = self.at(d)
         lo = max(1, hi - self.slack)

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--parts", default="4096,1024,512,256")
     ap.add_argument("--ctx", type=int, default=0, help="fixed context (0 = bench distribution)")
     ap.add_argument("--pool-pages", type=int, default=0, help="scatter pages over a pool this large (TLB test)")
+    ap.add_argument("--dyn-parts", default="", help="also per-sequence partitions: comma list of part counts "
+                                                   "(the runtime's OME_DECODE_DYN_PARTS layout; 1 = what bs 256 runs)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     rng = random.Random(0)
@@ -49,8 +51,10 @@ def main():
     kv_bytes = sum(lens) * Hkv * D * 2 * 2
     print(f"B={B} mean ctx={sum(lens) / B:.0f} max={max(lens)} KV bytes/call={kv_bytes / 1e6:.1f} MB")
     ref = None
-    for part in [int(x) for x in a.parts.split(",")]:
-        ws = ops.DecodeWorkspace(B, Hq, D, max(lens) + P, part, dev)
+    cfgs = [(int(x), None) for x in a.parts.split(",") if x] + [(0, int(x)) for x in a.dyn_parts.split(",") if x]
+    for part, dyn in cfgs:
+        ws = ops.DecodeWorkspace(B, Hq, D, max(lens) + P, part, dev, parts=dyn) if dyn else \
+            ops.DecodeWorkspace(B, Hq, D, max(lens) + P, part, dev)
         for v in a.variants.split(","):
             os.environ["OME_DECODE_ATTN"] = v
             out = ops.paged_decode(q, kc, vc, bt, sl, D ** -0.5, ws)
@@ -67,7 +71,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             us = s.elapsed_time(e) * 1000 / a.iters
-            print(f"variant {v} part {part:5d}: {us:8.1f} us  {kv_bytes / us / 1e6:6.2f} TB/s  maxerr {err:.2e}",
+            print(f"variant {v} part {part if not dyn else f'dyn{dyn}':>5}: {us:8.1f} us  {kv_bytes / us / 1e6:6.2f} TB/s  maxerr {err:.2e}",
                   flush=True)
 
 

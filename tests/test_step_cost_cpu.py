@@ -11,8 +11,10 @@ from ome_amd.runtime.step_cost import StepCost
 def _stairs(max_rows=4096, tile=256, per_tile=100.0, base=50.0):
     """t(M) = base + per_tile * ceil(M / tile): a pure tile-quantisation staircase."""
     rows = list(range(16, max_rows + 1, 16))
-    return StepCost.from_measurements(rows, [base + per_tile * -(-m // tile) for m in rows], max_rows,
-                                      slack=256, defer_ratio=1.3, max_defer=1)
+    sc = StepCost.from_measurements(rows, [base + per_tile * -(-m // tile) for m in rows], max_rows,
+                                    slack=256, defer_ratio=1.3, max_defer=1)
+    sc.min_avail = 0   # the unit tests exercise the cut itself
+    return sc
 
 
 def test_table_lookup_rounds_up_to_grid():
@@ -110,3 +112,11 @@ def test_prefers_prompt_boundary_within_tolerance():
     assert sc.choose(256, 300, 2048, bounds=[280, 300]) == 256
     sc.ttft_tol = 0.0
     assert sc.choose(256, 300, 2048, bounds=[250, 300]) == 256
+
+
+def test_small_prefills_are_not_cut():
+    sc = _stairs()
+    sc.min_avail = 768
+    assert sc.choose(256, 300, 2048) == 300      # below min_avail: everything, no cut
+    assert sc.choose(256, 20, 2048) == 20        # ... and no deferral
+    assert sc.choose(256, 1300, 2048) == 1280    # large: cut at the tile boundary (M = 1536)
