@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void w8_skinny_kernel(const bf16* __restrict__
       // before the previous step's barrier.  LDS-only barrier: __syncthreads() would also drain
       // the register ring's global loads (vmcnt(0)) and serialise every step on a round trip
       w8_lds_barrier();
-      if (s + PD < s1) load(j, s + PD);
+      load(j, min(s + PD, s1 - 1));   // unconditional (past the end: a re-read, never used) -- see w8_mgemv
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int ch = 4 * kk + lg;
@@ -260,16 +260,24 @@ __global__ __launch_bounds__(256) void w8_skinny_kernel(const bf16* __restrict__
     }
     __syncthreads();
     if (!s_last) return;
+    // fixed split order (deterministic); one split's fragments loaded together (see w8_mgemv)
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb)
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        f32x4 sum = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int p = 0; p < splits; ++p)   // fixed order: deterministic
-          sum += *reinterpret_cast<const f32x4*>(ws + ((int64_t)tile * splits + p) * MP * NT +
-                                                 (r0 + 16 * mb + lr) * NT + 16 * nb + 4 * lg);
-        acc[nb][mb] = sum;
-      }
+      for (int mb = 0; mb < MB; ++mb) acc[nb][mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < splits; ++p) {
+      const float* slab = ws + ((int64_t)tile * splits + p) * MP * NT;
+      f32x4 v[4][MB];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          v[nb][mb] = *reinterpret_cast<const f32x4*>(slab + (r0 + 16 * mb + lr) * NT + 16 * nb + 4 * lg);
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) acc[nb][mb] += v[nb][mb];
+    }
     if (tid == 0) cnt[tile] = 0;   // re-arm for the next launch / graph replay
   }
 #pragma unroll
@@ -288,6 +296,165 @@ __global__ __launch_bounds__(256) void w8_skinny_kernel(const bf16* __restrict__
         bf16x4 v;
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (bf16)(acc[nb][mb][r] * sv[r] + bv[r]);
+        *reinterpret_cast<bf16x4*>(out + (int64_t)m * ldo + n) = v;
+      }
+    }
+  }
+}
+
+
+// ------------------------------------------------------------------------------------ MFMA GEMV
+// 8 < M <= 64: the skinny tile's per-step LDS round trip of the weight (global -> VGPR -> LDS ->
+// VGPR, two barriers) is what capped it at 0.5-1 TB/s.  Here the weight never touches LDS: lane l
+// of a wave loads 16 e4m3 of weight row (l & 15) at k = kb + 16 (l >> 4) -- one 16-byte load per
+// 16-row block and 64-deep K step -- and those 16 values are the A operands of TWO
+// v_mfma_f32_16x16x32_bf16 (k permuted identically in A and B, so the sum is exact).  Only the
+// activation slice (M x kslice bf16, <= 64 KiB, rows padded by 16 B so the 16 row reads of a lane
+// group hit distinct banks) is staged in LDS, once per workgroup, and every wave reuses each X
+// fragment for its 4 weight blocks.  A wave owns 64 weight rows; a workgroup 256 rows x one K
+// slice; the K slices of a row tile meet in the skinny kernel's fixed-order slab reduction.
+// Weight loads run 4 K steps ahead (16 x 16 B per lane in flight) with no barrier in the K loop.
+constexpr int MG_NB = 4;                    // 16-row weight blocks per wave
+constexpr int MG_ROWS = 4 * MG_NB * 16;     // weight rows per workgroup
+constexpr int MG_U = 4;                     // K steps (64 deep) in flight per wave
+
+template <int MT, int BLK>   // MT: 16-row activation tiles (M <= 16 MT)
+__global__ __launch_bounds__(256) void w8_mgemv_kernel(const bf16* __restrict__ X, int64_t ldx,
+                                                       const uint8_t* __restrict__ W, int64_t ldw,
+                                                       const float* __restrict__ sw, const bf16* __restrict__ bias,
+                                                       bf16* __restrict__ out, int64_t ldo, int M, int N, int K,
+                                                       int kslice, int splits, float* __restrict__ ws,
+                                                       int* __restrict__ cnt) {
+  constexpr int MP = 16 * MT;
+  extern __shared__ __attribute__((aligned(16))) char mg_smem[];
+  __shared__ int s_last;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tile = blockIdx.x / splits, split = blockIdx.x - tile * splits;
+  const int k0 = split * kslice;
+  const int xs = kslice * 2 + 16;   // LDS row stride in bytes (padded)
+  // ---- this wave's weight rows: issue the first MG_U steps before staging X
+  const int lr = lane & 15, g = lane >> 4;
+  const int nb0 = tile * MG_ROWS + wave * MG_NB * 16;
+  const uint8_t* wp[MG_NB];
+  const float* sc[MG_NB];
+#pragma unroll
+  for (int b = 0; b < MG_NB; ++b) {
+    const int n = min(nb0 + 16 * b + lr, N - 1);   // rows past N are computed, never stored
+    wp[b] = W + (int64_t)n * ldw + k0 + 16 * g;
+    sc[b] = BLK ? sw + (int64_t)(n >> 7) * (K >> 7) + (k0 >> 7) : sw;
+  }
+  const int steps = kslice / 64;   // multiple of MG_U (host)
+  w8_u32x4 w[MG_U][MG_NB];
+#pragma unroll
+  for (int u = 0; u < MG_U; ++u)
+#pragma unroll
+    for (int b = 0; b < MG_NB; ++b) w[u][b] = *reinterpret_cast<const w8_u32x4*>(wp[b] + 64 * u);
+  // ---- stage X[0:MP][k0:k0+kslice] (rows >= M zero)
+  const int cpr = kslice / 8;   // 16-byte chunks per row
+  for (int c = tid; c < MP * cpr; c += 256) {
+    const int r = c / cpr, ch = c - r * cpr;
+    *reinterpret_cast<bf16x8*>(mg_smem + r * xs + ch * 16) =
+        r < M ? ld8(X + (int64_t)r * ldx + k0 + 8 * ch) : bf16x8{};
+  }
+  __syncthreads();
+
+  f32x4 acc[MG_NB][MT];
+#pragma unroll
+  for (int b = 0; b < MG_NB; ++b)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[b][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < steps; s += MG_U) {
+#pragma unroll
+    for (int u = 0; u < MG_U; ++u) {
+      const int ks = 64 * (s + u);
+      bf16x8 xa[MT], xb[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const char* p = mg_smem + (mt * 16 + lr) * xs + (ks + 16 * g) * 2;
+        xa[mt] = *reinterpret_cast<const bf16x8*>(p);
+        xb[mt] = *reinterpret_cast<const bf16x8*>(p + 16);
+      }
+#pragma unroll
+      for (int b = 0; b < MG_NB; ++b) {
+        bf16x8 wa, wb;
+        if constexpr (BLK) {
+          const float f = sc[b][ks >> 7];
+          wa = w8_cvt8_scaled(w[u][b][0], w[u][b][1], f);
+          wb = w8_cvt8_scaled(w[u][b][2], w[u][b][3], f);
+        } else {
+          wa = w8_cvt8(w[u][b][0], w[u][b][1]);
+          wb = w8_cvt8(w[u][b][2], w[u][b][3]);
+        }
+        // refill this ring slot with the step MG_U ahead (its registers are free now).  Issued
+        // unconditionally -- past the slice it re-reads the last step (a cache hit, never used):
+        // a branch around the load would make hipcc's vmcnt counting drain the ring every step
+        w[u][b] = *reinterpret_cast<const w8_u32x4*>(wp[b] + min(ks + 64 * MG_U, kslice - 64));
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xa[mt], acc[b][mt], 0, 0, 0);
+          acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, xb[mt], acc[b][mt], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // acc[b][mt][r] = C[m = 16 mt + lr][n = nb0 + 16 b + 4 g + r]
+  if (splits > 1) {
+    constexpr int TILE_F = MG_ROWS * MP;   // floats per (tile, split) slab
+    float* part = ws + ((int64_t)tile * splits + split) * TILE_F;
+#pragma unroll
+    for (int b = 0; b < MG_NB; ++b)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        *reinterpret_cast<f32x4*>(part + (((wave * MG_NB + b) * MT + mt) * 64 + lane) * 4) = acc[b][mt];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      s_last = __hip_atomic_fetch_add(&cnt[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == splits - 1;
+      if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // fixed split order (deterministic); each split's MG_NB x MT fragments are loaded together,
+    // so the reduction costs `splits` memory round trips, not splits x MG_NB x MT dependent ones
+#pragma unroll
+    for (int b = 0; b < MG_NB; ++b)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[b][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int p = 0; p < splits; ++p) {
+      const float* slab = ws + ((int64_t)tile * splits + p) * TILE_F;
+      f32x4 v[MG_NB][MT];
+#pragma unroll
+      for (int b = 0; b < MG_NB; ++b)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          v[b][mt] = *reinterpret_cast<const f32x4*>(slab + (((wave * MG_NB + b) * MT + mt) * 64 + lane) * 4);
+#pragma unroll
+      for (int b = 0; b < MG_NB; ++b)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[b][mt] += v[b][mt];
+    }
+    if (tid == 0) cnt[tile] = 0;   // re-arm for the next launch / graph replay
+  }
+#pragma unroll
+  for (int b = 0; b < MG_NB; ++b) {
+    const int n = nb0 + 16 * b + 4 * g;
+    if (n >= N) continue;   // N % 16 == 0 (host): a lane's 4 columns are all in or all out
+    float bv[4] = {0.f, 0.f, 0.f, 0.f}, sv[4] = {1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (bias) bv[r] = (float)bias[n + r];
+      if constexpr (!BLK) sv[r] = sw[n + r];
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int m = 16 * mt + lr;
+      if (m < M) {
+        bf16x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (bf16)(acc[b][mt][r] * sv[r] + bv[r]);
         *reinterpret_cast<bf16x4*>(out + (int64_t)m * ldo + n) = v;
       }
     }
@@ -341,6 +508,35 @@ OME_API int ome_w8a16_gemm(const void* X, int64_t ldx, const void* W, int64_t ld
   else if (M <= 128) { if (blk) W8SK(2, 1); else W8SK(2, 0); }
   else { if (blk) W8SK(4, 1); else W8SK(4, 0); }
 #undef W8SK
+  OME_CHECK_LAUNCH();
+  return 0;
+}
+
+// 8 < M <= 64 on the MFMA GEMV (w8_mgemv_kernel): K % 256 == 0, N % 16 == 0, kslice a multiple of
+// 256 dividing K with MP x (2 kslice + 16) <= 64 KiB (MP = 16 / 32 / 64 by M); splits = K / kslice > 1
+// needs ws (>= ceil(N / 256) * splits * 256 * MP floats) and cnt (>= ceil(N / 256) ints, zero on
+// first use; re-armed by the kernel).  ldo % 4 == 0.
+OME_API int ome_w8a16_mgemv(const void* X, int64_t ldx, const void* W, int64_t ldw, const float* sw, int block,
+                            const void* bias, void* out, int64_t ldo, int M, int N, int K, int kslice, float* ws,
+                            int* cnt, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 64 || K % 256 || N % 16 || ldx % 8 || ldw % 16 || ldo % 4 || (block != 0 && block != 128)) return -2;
+  if (kslice <= 0 || kslice % 256 || K % kslice) return -2;
+  const int MT = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  const size_t lds = (size_t)16 * MT * (2 * kslice + 16);
+  if (lds > 65536) return -2;
+  const int splits = K / kslice, tiles = (N + MG_ROWS - 1) / MG_ROWS;
+  if (splits > 1 && (!ws || !cnt)) return -3;
+  dim3 grid(tiles * splits);
+#define W8MG(MTV, BV)                                                                                        \
+  w8_mgemv_kernel<MTV, BV><<<grid, 256, lds, stream>>>((const bf16*)X, ldx, (const uint8_t*)W, ldw, sw,        \
+                                                       (const bf16*)bias, (bf16*)out, ldo, M, N, K, kslice,      \
+                                                       splits, ws, cnt)
+  const bool blk = block == 128;
+  if (MT == 1) { if (blk) W8MG(1, 1); else W8MG(1, 0); }
+  else if (MT == 2) { if (blk) W8MG(2, 1); else W8MG(2, 0); }
+  else { if (blk) W8MG(4, 1); else W8MG(4, 0); }
+#undef W8MG
   OME_CHECK_LAUNCH();
   return 0;
 }

@@ -393,6 +393,22 @@ def w8a16_plan(M: int, N: int, K: int, block: int) -> int | None:
     return int(e["splits"]) if e["us"] < 0.97 * e["w8a8_us"] else None
 
 
+def w8a16_mgemv_splits(M: int, N: int, K: int, target_wg: int | None = None) -> list[int]:
+    """Valid K-split counts of the MFMA GEMV (``ome_w8a16_mgemv``) for this shape, the default
+    (about ``target_wg`` workgroups, 2 per CU) first: each split is a multiple of 256 deep and its
+    activation slice fits 64 KiB of LDS.  [] when the shape is not supported."""
+    # M <= 32 only: at 64 rows the activation slice limits a split to 256 deep and the slab
+    # reduction outgrows the weight stream (profiles/r06_w8a16_bench.txt, v5) -- the skinny tile wins
+    if not 8 < M <= 32 or K % 256 or N % 16:
+        return []
+    mp = 16 if M <= 16 else 32 if M <= 32 else 64
+    kmax = ((65536 // mp - 16) // 2) // 256 * 256
+    tiles = -(-N // 256)
+    ok = [d for d in range(1, K // 256 + 1) if (K // 256) % d == 0 and K // d <= kmax]
+    tgt = target_wg or int(os.environ.get("OME_W8_MGEMV_WG", "512"))
+    return sorted(ok, key=lambda d: (abs(tiles * d - tgt), d))
+
+
 def w8a16_gemm(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int = 0, bias=None,
                out: torch.Tensor | None = None, splits: int | None = None) -> torch.Tensor:
     """out[M, N] bf16 = x[M, K] bf16 . dequant(qw)^T (+ bias) for decode rows (M <= 256): the fp8
@@ -409,6 +425,22 @@ def w8a16_gemm(x: torch.Tensor, qw: torch.Tensor, sw: torch.Tensor, block: int =
         return r
     assert w8a16_ok(x, qw, sw, block), "w8a16_gemm: unsupported operands"
     out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device) if out is None else out
+    mg = w8a16_mgemv_splits(M, N, K)
+    if mg and out.stride(1) == 1 and out.stride(0) % 4 == 0 and os.environ.get("OME_W8_MGEMV", "1") == "1":
+        # 8 < M <= 64: the MFMA GEMV (weight straight to registers, activation slice in LDS)
+        s = splits if splits in mg else mg[0]
+        ws = cnt = None
+        mp = 16 if M <= 16 else 32 if M <= 32 else 64
+        if s > 1:
+            key = _ws_key(x.device)
+            st = _w8_ws.get(key)
+            if st is None:
+                st = _w8_ws[key] = _SkinnyWorkspace(x.device)
+            ws, cnt = st.get(-(-N // 256) * s * 256 * 64), st.cnt   # sized for MP = 64: never regrown per M
+            assert -(-N // 256) <= cnt.numel()
+        call("ome_w8a16_mgemv", x.data_ptr(), x.stride(0), qw.data_ptr(), qw.stride(0), sw.data_ptr(), block,
+             ptr(bias), out.data_ptr(), out.stride(0), M, N, K, K // s, ptr(ws), ptr(cnt), stream_ptr())
+        return out
     s = 1 if M <= 8 else (splits or skinny_splits(M, N, K))
     ws = cnt = None
     if s > 1:

@@ -66,6 +66,7 @@ _SIGNATURES = {
         "ome_varlen_attention": [vp, i64, vp, i64, vp, i64, vp, vp, vp, i32, vp, i64, i32, i32, i32, f32, i32, vp],
         "ome_skinny_gemm": [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, vp, vp, vp],
         "ome_w8a16_gemm": [vp, i64, vp, i64, vp, i32, vp, vp, i64, i32, i32, i32, i32, vp, vp, vp],
+        "ome_w8a16_mgemv": [vp, i64, vp, i64, vp, i32, vp, vp, i64, i32, i32, i32, i32, vp, vp, vp],
         "ome_stream_gemm": [vp, i64, vp, vp, vp, i64, i32, i32, i32, i32, i32, vp, vp, vp],
         "ome_gemv": [vp, i64, vp, vp, vp, i64, i32, i32, i32, vp],
         "ome_gemv_act": [vp, i64, vp, vp, vp, i64, i32, i32, i32, vp],

@@ -76,7 +76,8 @@ def main():
                     assert err < 1e-2, (name, M, block, err)
                     t_b = timed(lambda i: linear(x, wb[i % len(wb)]))
                     t_88 = timed(lambda i: ops.fp8_linear(x, qs[i % copies].q, qs[i % copies].scale, block))
-                    cands = [None] if M <= 8 else [None, 1, 2, 3, 4, 6, 8]
+                    mg = ops.w8a16_mgemv_splits(M, N, K)
+                    cands = [None] if M <= 8 else ([None] + mg[:4] if mg else [None, 1, 2, 3, 4, 6, 8])
                     best, bs = 1e30, None
                     for sp in cands:
                         if sp is not None and sp > K // 64:
@@ -85,7 +86,7 @@ def main():
                                                            splits=sp))
                         if t < best:
                             best, bs = t, sp
-                    sp_used = bs if bs is not None else (1 if M <= 8 else ops.skinny_splits(M, N, K))
+                    sp_used = bs if bs is not None else (1 if M <= 8 else mg[0] if mg else ops.skinny_splits(M, N, K))
                     res[key][M] = {"w8a16_us": round(best, 2), "splits": sp_used, "w8a8_us": round(t_88, 2),
                                    "bf16_us": round(t_b, 2)}
                     print(f"{model:8s} {name:9s} blk{block:<3d} M={M:4d}  bf16 {t_b:7.1f}  w8a8 {t_88:7.1f}  "

@@ -158,3 +158,19 @@ def test_fp8_moe_experts_quantized_and_reference_path():
     tw, tid = ops.moe_route(torch.randn(5, 8), 2)
     y = ops.fused_moe(x, tw, tid, m.w13[i], m.w2[i], 0, 1.0)
     assert y.shape == (5, 256) and torch.isfinite(y).all()
+
+
+def test_w8a16_mgemv_split_choice():
+    """The MFMA GEMV's K splits: 256-deep multiples that divide K, the activation slice within
+    64 KiB of LDS, the split count nearest ~512 workgroups first (csrc/kernels/w8a16.hip)."""
+    from ome_amd import ops
+
+    assert ops.w8a16_mgemv_splits(8, 4096, 4096) == []       # GEMV rows
+    assert ops.w8a16_mgemv_splits(33, 4096, 4096) == []      # skinny tile rows
+    assert ops.w8a16_mgemv_splits(16, 4096, 4000) == []      # K not a multiple of 256
+    for M, N, K in [(16, 6144, 4096), (32, 4096, 14336), (32, 28672, 4096), (20, 576, 7168)]:
+        sp = ops.w8a16_mgemv_splits(M, N, K)
+        mp = 16 if M <= 16 else 32 if M <= 32 else 64
+        assert sp and all((K // 256) % d == 0 and mp * (2 * (K // d) + 16) <= 65536 for d in sp)
+        tiles = -(-N // 256)
+        assert abs(tiles * sp[0] - 512) == min(abs(tiles * d - 512) for d in sp)
