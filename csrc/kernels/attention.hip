@@ -302,12 +302,9 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
 // Split-K partition span of a sequence: a fixed ``part_size`` (multiple of 128), or with
 // part_size == 0 the sequence's own length spread over ``max_parts`` partitions (128-key granules),
 // so short contexts still fill every partition instead of leaving all but the first idle.
-// part_size > 0: fixed spans; 0: every sequence split into max_parts spans of its own length;
-// < 0: length-aware -- spans of at least -part_size keys, so only sequences longer than that are
-// split (the long tail of a mixed-length batch) and short ones finish in one workgroup
 __device__ __forceinline__ int decode_part_span(int part_size, int seq_len, int max_parts) {
   if (part_size > 0) return part_size;
-  return max(max(128, -part_size), (((seq_len + max_parts - 1) / max_parts) + 127) & ~127);
+  return max(128, (((seq_len + max_parts - 1) / max_parts) + 127) & ~127);
 }
 
 template <int D>
@@ -673,7 +670,7 @@ OME_API int ome_paged_decode(const void* q, int64_t q_stride, const void* k_cach
   if (B <= 0) return 0;
   if ((D != 64 && D != 128 && D != 256) || P != 16) return -2;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -3;
-  if (part_size % 128 != 0 || max_parts <= 0) return -4;   // 0: per-sequence span, < 0: min span
+  if (part_size < 0 || part_size % 128 != 0 || max_parts <= 0) return -4;   // 0: per-sequence span
   if (kv_fmt < 0 || kv_fmt > 2) return -5;
   Scaler scl = make_scaler(scale * k_scale, softcap, alibi, bsparse);
   scl.row_lo = row_lo;

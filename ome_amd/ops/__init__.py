@@ -642,15 +642,11 @@ class DecodeWorkspace:
 
     def __init__(self, max_batch: int, Hq: int, D: int, max_context: int, part_size: int = 512, device="cuda",
                  parts: int | None = None):
-        """``part_size`` > 0: fixed 128-multiple key spans; ``part_size`` < 0: spans of at least
-        ``-part_size`` keys, at most ``parts`` (only long sequences split); ``part_size`` == 0: every sequence is split
+        """``part_size`` > 0: fixed 128-multiple key spans; ``part_size`` == 0: every sequence is split
         into ``parts`` spans of its own length (128-key granules), so short contexts use every
         partition."""
         self.part_size = part_size
-        if part_size < 0:   # length-aware: spans of >= -part_size keys, at most ``parts`` of them
-            assert parts and parts >= 1 and part_size % 128 == 0
-            self.max_parts = parts
-        elif part_size == 0:
+        if part_size == 0:
             assert parts and parts >= 1
             self.max_parts = parts
         else:

@@ -337,12 +337,7 @@ class ModelRunner:
             hkv = self.model.tp.hkv
             parts = max(1, math.ceil(1024 / max(1, bs * hkv)))
             span = self.max_context + self.P  # seq_lens never exceed this: one part covers it all
-            min_span = int(os.environ.get("OME_DECODE_MIN_SPAN", "0"))
-            if parts == 1 and min_span > 0 and span > min_span:
-                # length-aware: only sequences longer than min_span keys split (the long tail)
-                ws = ops.DecodeWorkspace(bs, self.model.tp.hq, self.cfg.head_dim, span, -(-min_span // 128) * -128,
-                                         self.device, parts=min(4, -(-span // min_span)))
-            elif parts > 1 and os.environ.get("OME_DECODE_DYN_PARTS", "1") == "1":
+            if parts > 1 and os.environ.get("OME_DECODE_DYN_PARTS", "1") == "1":
                 # split each sequence by its own length (short contexts fill every partition)
                 ws = ops.DecodeWorkspace(bs, self.model.tp.hq, self.cfg.head_dim, span, 0, self.device, parts=parts)
             else:

@@ -20,8 +20,6 @@ def main():
     ap.add_argument("--parts", default="4096,1024,512,256")
     ap.add_argument("--ctx", type=int, default=0, help="fixed context (0 = bench distribution)")
     ap.add_argument("--pool-pages", type=int, default=0, help="scatter pages over a pool this large (TLB test)")
-    ap.add_argument("--min-span", default="", help="also length-aware partitions: comma list of minimum spans "
-                                                   "(only sequences longer than the span split; up to 4 parts)")
     ap.add_argument("--dyn-parts", default="", help="also per-sequence partitions: comma list of part counts "
                                                    "(the runtime's OME_DECODE_DYN_PARTS layout; 1 = what bs 256 runs)")
     a = ap.parse_args()
@@ -53,8 +51,7 @@ def main():
     kv_bytes = sum(lens) * Hkv * D * 2 * 2
     print(f"B={B} mean ctx={sum(lens) / B:.0f} max={max(lens)} KV bytes/call={kv_bytes / 1e6:.1f} MB")
     ref = None
-    cfgs = [(int(x), None) for x in a.parts.split(",") if x] + [(0, int(x)) for x in a.dyn_parts.split(",") if x] \
-        + [(-int(x), 4) for x in a.min_span.split(",") if x]
+    cfgs = [(int(x), None) for x in a.parts.split(",") if x] + [(0, int(x)) for x in a.dyn_parts.split(",") if x]
     for part, dyn in cfgs:
         ws = ops.DecodeWorkspace(B, Hq, D, max(lens) + P, part, dev, parts=dyn) if dyn else \
             ops.DecodeWorkspace(B, Hq, D, max(lens) + P, part, dev)
@@ -74,8 +71,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             us = s.elapsed_time(e) * 1000 / a.iters
-            lbl = f"min{-part}" if part < 0 else f"dyn{dyn}" if dyn else str(part)
-            print(f"variant {v} part {lbl:>7}: {us:8.1f} us  {kv_bytes / us / 1e6:6.2f} TB/s  maxerr {err:.2e}",
+            print(f"variant {v} part {part if not dyn else f'dyn{dyn}':>5}: {us:8.1f} us  {kv_bytes / us / 1e6:6.2f} TB/s  maxerr {err:.2e}",
                   flush=True)
 
 
