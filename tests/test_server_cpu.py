@@ -60,7 +60,8 @@ def test_sglang_style_flags_parse():
     ns, unknown = build_parser().parse_known_args(
         ["--model-path", "/raid/models/x", "--tp-size", "4", "--mem-frac", "0.9", "--enable-metrics",
          "--trust-remote-code", "--port", "8080", "--log-requests"])
-    assert ns.tp_size == 4 and ns.mem_frac == 0.9 and "--trust-remote-code" in unknown
+    # --trust-remote-code is on the reference-flag no-op list (runtime/flags.py): accepted, not unknown
+    assert ns.tp_size == 4 and ns.mem_frac == 0.9 and "--trust-remote-code" not in unknown
     ea = engine_args_from(ns)
     assert ea.tp_size == 4 and ea.model == "llama-3-8b"  # no config.json -> random-init preset
 

@@ -139,4 +139,5 @@ def test_lockstep_step_failure_on_comm_error_exits(monkeypatch):
     t.start()
     t.join(timeout=60)
     eng._stop = True
+    W.unregister_all()
     assert fatal == [1] and not t.is_alive()
