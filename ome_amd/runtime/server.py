@@ -538,6 +538,10 @@ def create_app(engine, ns=None):
             return {"prompt_tokens": len(ids), "completion_tokens": len(req.output_ids),
                     "total_tokens": len(ids) + len(req.output_ids)}
 
+        # streamed text-completion chunk template: {"id","object","created","model","choices"[,"usage"]}
+        text_pre = f'data: {{"id":{json.dumps(rid)},"object":"text_completion","created":'
+        text_mid = f',"model":{json.dumps(model_name)},"choices":[{{"index":0,"text":'
+
         use_tools = bool(chat and tool_kind and body.get("tools") and body.get("tool_choice", "auto") != "none")
         use_reason = bool(chat and reason_kind and body.get("separate_reasoning", True))
         # parsers look for special-token markers (harmony <|channel|>/<|call|>, [TOOL_CALLS]):
@@ -629,8 +633,22 @@ def create_app(engine, ns=None):
                         if finish:
                             choice["_finish"] = finish
                     else:
-                        choice = {"index": 0, "text": strip_special(delta, specials), "finish_reason": None}
-                        chunk_obj = "text_completion"
+                        # text completion: the chunk is formatted from a template -- one small
+                        # json.dumps of the text instead of the whole nested dict (~1.5 vs ~7.7 us per
+                        # chunk; 256 streams x one chunk per engine step run on the server's event-loop
+                        # thread, which shares the GIL with the engine loop)
+                        first = False
+                        fr = ("stop" if stopped else _finish(req)) if fin else None
+                        chunk = (f'{text_pre}{int(time.time())}{text_mid}{json.dumps(strip_special(delta, specials))}'
+                                 f',"finish_reason":{"null" if fr is None else json.dumps(fr)}}}]')
+                        if every_usage or (fin and (body.get("stream_options") or {}).get("include_usage", True)):
+                            n_out = len(req.output_ids)
+                            chunk += (f',"usage":{{"prompt_tokens":{len(ids)},"completion_tokens":{n_out},'
+                                      f'"total_tokens":{len(ids) + n_out}}}')
+                        yield f"{chunk}}}\n\n"
+                        if fin:
+                            break
+                        continue
                     first = False
                     forced = choice.pop("_finish", None)
                     if fin:

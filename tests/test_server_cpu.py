@@ -44,6 +44,28 @@ def test_chat_stream(client):
     assert chunks[-1]["usage"]["completion_tokens"] == 4
 
 
+def test_completion_stream_chunks(client):
+    """Streamed text completions are formatted from a template (server fast path): every chunk
+    must still be the OpenAI text_completion object, texts concatenating to the non-streamed
+    completion, usage on every chunk with continuous_usage_stats and on the last one otherwise."""
+    body = {"model": "tiny", "prompt": "hello there", "max_tokens": 5, "temperature": 0, "ignore_eos": True}
+    full = client.post("/v1/completions", json=body).json()
+    for cont in (True, False):
+        with client.stream("POST", "/v1/completions", json={**body, "stream": True, "stream_options": {
+                "include_usage": True, "continuous_usage_stats": cont}}) as r:
+            lines = [ln for ln in r.iter_lines() if ln.startswith("data: ")]
+        assert lines[-1] == "data: [DONE]"
+        chunks = [json.loads(ln[6:]) for ln in lines[:-1]]
+        assert all(c["object"] == "text_completion" and c["id"].startswith("cmpl-") and c["model"]
+                   and isinstance(c["created"], int) for c in chunks)
+        assert "".join(c["choices"][0]["text"] for c in chunks) == full["choices"][0]["text"]
+        assert [c["choices"][0]["finish_reason"] for c in chunks][-1] == "length"
+        assert all(c["choices"][0]["finish_reason"] is None for c in chunks[:-1])
+        assert chunks[-1]["usage"] == {"prompt_tokens": full["usage"]["prompt_tokens"], "completion_tokens": 5,
+                                       "total_tokens": full["usage"]["prompt_tokens"] + 5}
+        assert all(("usage" in c) == (cont or c is chunks[-1]) for c in chunks)
+
+
 def test_metrics_names(client):
     txt = client.get("/metrics").text
     for name in ("vllm:request_success_total", "vllm:avg_generation_throughput_toks_per_s",
