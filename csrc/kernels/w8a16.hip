@@ -318,7 +318,10 @@ constexpr int MG_NB = 4;                    // 16-row weight blocks per wave
 constexpr int MG_ROWS = 4 * MG_NB * 16;     // weight rows per workgroup
 constexpr int MG_U = 4;                     // K steps (64 deep) in flight per wave
 
-template <int MT, int BLK>   // MT: 16-row activation tiles (M <= 16 MT)
+// STEPS = kslice / 64, a template constant: the K loop is straight-line code, so the ring slot of
+// every step and the refill distance are compile-time and hipcc's vmcnt counting stays exact
+// (with a runtime trip count it drained the ring at every loop back-edge: 1-2 TB/s)
+template <int MT, int BLK, int STEPS>   // MT: 16-row activation tiles (M <= 16 MT)
 __global__ __launch_bounds__(256) void w8_mgemv_kernel(const bf16* __restrict__ X, int64_t ldx,
                                                        const uint8_t* __restrict__ W, int64_t ldw,
                                                        const float* __restrict__ sw, const bf16* __restrict__ bias,
@@ -343,18 +346,20 @@ __global__ __launch_bounds__(256) void w8_mgemv_kernel(const bf16* __restrict__ 
     wp[b] = W + (int64_t)n * ldw + k0 + 16 * g;
     sc[b] = BLK ? sw + (int64_t)(n >> 7) * (K >> 7) + (k0 >> 7) : sw;
   }
-  const int steps = kslice / 64;   // multiple of MG_U (host)
-  w8_u32x4 w[MG_U][MG_NB];
+  constexpr int R = STEPS < MG_U ? STEPS : MG_U;   // ring depth (K steps in flight)
+  w8_u32x4 w[R][MG_NB];
 #pragma unroll
-  for (int u = 0; u < MG_U; ++u)
+  for (int u = 0; u < R; ++u)
 #pragma unroll
     for (int b = 0; b < MG_NB; ++b) w[u][b] = *reinterpret_cast<const w8_u32x4*>(wp[b] + 64 * u);
   // ---- stage X[0:MP][k0:k0+kslice] (rows >= M zero)
-  const int cpr = kslice / 8;   // 16-byte chunks per row
-  for (int c = tid; c < MP * cpr; c += 256) {
-    const int r = c / cpr, ch = c - r * cpr;
-    *reinterpret_cast<bf16x8*>(mg_smem + r * xs + ch * 16) =
-        r < M ? ld8(X + (int64_t)r * ldx + k0 + 8 * ch) : bf16x8{};
+  constexpr int CPR = STEPS * 8;   // 16-byte chunks per row
+#pragma unroll
+  for (int c0 = 0; c0 < MP * CPR; c0 += 256) {
+    const int c = c0 + tid, r = c / CPR, ch = c - r * CPR;
+    if (c < MP * CPR)
+      *reinterpret_cast<bf16x8*>(mg_smem + r * xs + ch * 16) =
+          r < M ? ld8(X + (int64_t)r * ldx + k0 + 8 * ch) : bf16x8{};
   }
   __syncthreads();
 
@@ -363,37 +368,32 @@ __global__ __launch_bounds__(256) void w8_mgemv_kernel(const bf16* __restrict__ 
   for (int b = 0; b < MG_NB; ++b)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[b][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s = 0; s < steps; s += MG_U) {
 #pragma unroll
-    for (int u = 0; u < MG_U; ++u) {
-      const int ks = 64 * (s + u);
-      bf16x8 xa[MT], xb[MT];
+  for (int j = 0; j < STEPS; ++j) {
+    const int u = j % R, ks = 64 * j;
+    bf16x8 xa[MT], xb[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const char* p = mg_smem + (mt * 16 + lr) * xs + (ks + 16 * g) * 2;
+      xa[mt] = *reinterpret_cast<const bf16x8*>(p);
+      xb[mt] = *reinterpret_cast<const bf16x8*>(p + 16);
+    }
+#pragma unroll
+    for (int b = 0; b < MG_NB; ++b) {
+      bf16x8 wa, wb;
+      if constexpr (BLK) {
+        const float f = sc[b][ks >> 7];
+        wa = w8_cvt8_scaled(w[u][b][0], w[u][b][1], f);
+        wb = w8_cvt8_scaled(w[u][b][2], w[u][b][3], f);
+      } else {
+        wa = w8_cvt8(w[u][b][0], w[u][b][1]);
+        wb = w8_cvt8(w[u][b][2], w[u][b][3]);
+      }
+      if (j + R < STEPS) w[u][b] = *reinterpret_cast<const w8_u32x4*>(wp[b] + ks + 64 * R);   // compile-time guard
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const char* p = mg_smem + (mt * 16 + lr) * xs + (ks + 16 * g) * 2;
-        xa[mt] = *reinterpret_cast<const bf16x8*>(p);
-        xb[mt] = *reinterpret_cast<const bf16x8*>(p + 16);
-      }
-#pragma unroll
-      for (int b = 0; b < MG_NB; ++b) {
-        bf16x8 wa, wb;
-        if constexpr (BLK) {
-          const float f = sc[b][ks >> 7];
-          wa = w8_cvt8_scaled(w[u][b][0], w[u][b][1], f);
-          wb = w8_cvt8_scaled(w[u][b][2], w[u][b][3], f);
-        } else {
-          wa = w8_cvt8(w[u][b][0], w[u][b][1]);
-          wb = w8_cvt8(w[u][b][2], w[u][b][3]);
-        }
-        // refill this ring slot with the step MG_U ahead (its registers are free now).  Issued
-        // unconditionally -- past the slice it re-reads the last step (a cache hit, never used):
-        // a branch around the load would make hipcc's vmcnt counting drain the ring every step
-        w[u][b] = *reinterpret_cast<const w8_u32x4*>(wp[b] + min(ks + 64 * MG_U, kslice - 64));
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xa[mt], acc[b][mt], 0, 0, 0);
-          acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, xb[mt], acc[b][mt], 0, 0, 0);
-        }
+        acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xa[mt], acc[b][mt], 0, 0, 0);
+        acc[b][mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, xb[mt], acc[b][mt], 0, 0, 0);
       }
     }
   }
@@ -512,8 +512,8 @@ OME_API int ome_w8a16_gemm(const void* X, int64_t ldx, const void* W, int64_t ld
   return 0;
 }
 
-// 8 < M <= 64 on the MFMA GEMV (w8_mgemv_kernel): K % 256 == 0, N % 16 == 0, kslice a multiple of
-// 256 dividing K with MP x (2 kslice + 16) <= 64 KiB (MP = 16 / 32 / 64 by M); splits = K / kslice > 1
+// 8 < M <= 32 on the MFMA GEMV (w8_mgemv_kernel): K % 256 == 0, N % 16 == 0, kslice 256 / 512 / 1024
+// dividing K with MP x (2 kslice + 16) <= 64 KiB (MP = 16 / 32 by M); splits = K / kslice > 1
 // needs ws (>= ceil(N / 256) * splits * 256 * MP floats) and cnt (>= ceil(N / 256) ints, zero on
 // first use; re-armed by the kernel).  ldo % 4 == 0.
 OME_API int ome_w8a16_mgemv(const void* X, int64_t ldx, const void* W, int64_t ldw, const float* sw, int block,
@@ -522,20 +522,24 @@ OME_API int ome_w8a16_mgemv(const void* X, int64_t ldx, const void* W, int64_t l
   if (M <= 0 || N <= 0) return 0;
   if (M > 64 || K % 256 || N % 16 || ldx % 8 || ldw % 16 || ldo % 4 || (block != 0 && block != 128)) return -2;
   if (kslice <= 0 || kslice % 256 || K % kslice) return -2;
-  const int MT = M <= 16 ? 1 : M <= 32 ? 2 : 4;
+  const int MT = M <= 16 ? 1 : 2;
   const size_t lds = (size_t)16 * MT * (2 * kslice + 16);
-  if (lds > 65536) return -2;
+  if (M > 32 || lds > 65536 || (kslice != 256 && kslice != 512 && kslice != 1024)) return -2;
   const int splits = K / kslice, tiles = (N + MG_ROWS - 1) / MG_ROWS;
   if (splits > 1 && (!ws || !cnt)) return -3;
   dim3 grid(tiles * splits);
-#define W8MG(MTV, BV)                                                                                        \
-  w8_mgemv_kernel<MTV, BV><<<grid, 256, lds, stream>>>((const bf16*)X, ldx, (const uint8_t*)W, ldw, sw,        \
-                                                       (const bf16*)bias, (bf16*)out, ldo, M, N, K, kslice,      \
-                                                       splits, ws, cnt)
+#define W8MG(MTV, BV, SV)                                                                                    \
+  w8_mgemv_kernel<MTV, BV, SV><<<grid, 256, lds, stream>>>((const bf16*)X, ldx, (const uint8_t*)W, ldw, sw,    \
+                                                           (const bf16*)bias, (bf16*)out, ldo, M, N, K, kslice,  \
+                                                           splits, ws, cnt)
+#define W8MG_S(MTV, BV)                                                                                      \
+  if (kslice == 256) W8MG(MTV, BV, 4);                                                                       \
+  else if (kslice == 512) W8MG(MTV, BV, 8);                                                                  \
+  else W8MG(MTV, BV, 16)
   const bool blk = block == 128;
-  if (MT == 1) { if (blk) W8MG(1, 1); else W8MG(1, 0); }
-  else if (MT == 2) { if (blk) W8MG(2, 1); else W8MG(2, 0); }
-  else { if (blk) W8MG(4, 1); else W8MG(4, 0); }
+  if (MT == 1) { if (blk) { W8MG_S(1, 1); } else { W8MG_S(1, 0); } }
+  else { if (blk) { W8MG_S(2, 1); } else { W8MG_S(2, 0); } }
+#undef W8MG_S
 #undef W8MG
   OME_CHECK_LAUNCH();
   return 0;

@@ -395,16 +395,16 @@ def w8a16_plan(M: int, N: int, K: int, block: int) -> int | None:
 
 def w8a16_mgemv_splits(M: int, N: int, K: int, target_wg: int | None = None) -> list[int]:
     """Valid K-split counts of the MFMA GEMV (``ome_w8a16_mgemv``) for this shape, the default
-    (about ``target_wg`` workgroups, 2 per CU) first: each split is a multiple of 256 deep and its
+    (about ``target_wg`` workgroups, 2 per CU) first: each split is 256 / 512 / 1024 deep and its
     activation slice fits 64 KiB of LDS.  [] when the shape is not supported."""
     # M <= 32 only: at 64 rows the activation slice limits a split to 256 deep and the slab
     # reduction outgrows the weight stream (profiles/r06_w8a16_bench.txt, v5) -- the skinny tile wins
     if not 8 < M <= 32 or K % 256 or N % 16:
         return []
-    mp = 16 if M <= 16 else 32 if M <= 32 else 64
-    kmax = ((65536 // mp - 16) // 2) // 256 * 256
+    mp = 16 if M <= 16 else 32
     tiles = -(-N // 256)
-    ok = [d for d in range(1, K // 256 + 1) if (K // 256) % d == 0 and K // d <= kmax]
+    # the kernel is instantiated for K slices of 256 / 512 / 1024 (a compile-time K loop)
+    ok = [K // ks for ks in (256, 512, 1024) if K % ks == 0 and mp * (2 * ks + 16) <= 65536]
     tgt = target_wg or int(os.environ.get("OME_W8_MGEMV_WG", "512"))
     return sorted(ok, key=lambda d: (abs(tiles * d - tgt), d))
 

@@ -171,6 +171,7 @@ def test_w8a16_mgemv_split_choice():
     for M, N, K in [(16, 6144, 4096), (32, 4096, 14336), (32, 28672, 4096), (20, 576, 7168)]:
         sp = ops.w8a16_mgemv_splits(M, N, K)
         mp = 16 if M <= 16 else 32 if M <= 32 else 64
-        assert sp and all((K // 256) % d == 0 and mp * (2 * (K // d) + 16) <= 65536 for d in sp)
+        assert sp and all(K % d == 0 and K // d in (256, 512, 1024) and mp * (2 * (K // d) + 16) <= 65536
+                          for d in sp)
         tiles = -(-N // 256)
         assert abs(tiles * sp[0] - 512) == min(abs(tiles * d - 512) for d in sp)
