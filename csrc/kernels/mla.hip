@@ -41,19 +41,6 @@ constexpr int lds_chunks() { return ((DK / 8) + 7) / 8 * 8; }
 template <int DK>
 __device__ __forceinline__ int swz(int row, int chunk) { return row * lds_chunks<DK>() + (chunk ^ (row & 7)); }
 
-// The same transposed read issued from inline asm: the all-heads kernel keeps LDS DMA of later
-// tiles in flight across its reads, and hipcc's wait-count pass, which cannot tell the DMA's
-// destination image from the one being read, otherwise puts an s_waitcnt vmcnt(0) before every
-// builtin transposed read (draining the DMA ring each tile).  hipcc emits no wait for an asm
-// load: the caller waits lgkmcnt(0) before using the result.
-__device__ __forceinline__ bf16x4 tr_read_asm(const bf16* lds_base, int byte_off) {
-  s16x4 v;
-  const uint32_t addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char*)(
-                            (__attribute__((address_space(3))) bf16*)lds_base) + byte_off);
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr));
-  return __builtin_bit_cast(bf16x4, v);
-}
-
 __device__ __forceinline__ bf16x4 tr_read(const bf16* lds_base, int byte_off) {
   const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (s16x4 __attribute__((address_space(3)))*)((__attribute__((address_space(3))) char*)(
@@ -216,18 +203,6 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
 // ------------------------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void mla_lds_t;
 
-// s_waitcnt vmcnt(n) for a run-time (wave-uniform) n: the immediate must be a constant, so branch
-// to it (n <= 2 tiles x 9 pieces in this kernel)
-__device__ __forceinline__ void mla_wait_dma(int n) {
-  switch (n) {
-#define MLA_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    MLA_W(1) MLA_W(2) MLA_W(3) MLA_W(4) MLA_W(5) MLA_W(6) MLA_W(7) MLA_W(8) MLA_W(9) MLA_W(10)
-    MLA_W(11) MLA_W(12) MLA_W(13) MLA_W(14) MLA_W(15) MLA_W(16) MLA_W(17) MLA_W(18)
-#undef MLA_W
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
 template <int DK, int DV, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
     const bf16* __restrict__ q, int64_t q_stride_t, const bf16* __restrict__ cache,
@@ -237,12 +212,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
   static_assert(DK == 576 && lds_chunks<DK>() == DK / 8, "LDS DMA image assumes unpadded 72-chunk rows");
   constexpr int CH = DK / 8, NI = KT * CH / 64, NB = DV / 16;
   constexpr int IMG = KT * CH * 8;   // bf16 elements per K-tile image
-  // NBUF K-tile images (3 x 36 KiB): the DMA runs NBUF - 1 tiles ahead of the MFMAs.  With two
-  // images each 32-key tile paid a full DMA round trip (~2 us) against ~0.25 us of MFMA work.
-  // Four images (144 KiB) returned wrong tiles from the fourth: LDS-DMA destinations above 128 KiB
-  // are not usable here, so the ring stays below it
-  constexpr int NBUF = 3;
-  __shared__ __attribute__((aligned(16))) bf16 sK[NBUF * IMG];
+  __shared__ __attribute__((aligned(16))) bf16 sK[2 * IMG];
   const int t = blockIdx.x, part = blockIdx.z;
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int col = lane & 15, g = lane >> 4;
@@ -271,11 +241,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
                                                (uint32_t)(((row & 15) * CH + (xl ^ (row & 7))) * 16), 0, 0, 0);
     }
   };
-  // DMA instructions this wave issues per tile (the tile's NI pieces dealt round-robin over waves)
-  const int cw = (NI - wave + NW - 1) / NW;
-#pragma unroll
-  for (int k = 0; k < NBUF - 1; ++k)
-    if (pair_begin + k < pair_end) dma_pair(pair_begin + k, sK + k * IMG);
+  if (pair_begin < pair_end) dma_pair(pair_begin, sK);
 
   bf16x8 qf[DK / 32];
   const bf16* qp = q + (int64_t)t * q_stride_t + (int64_t)head * DK + 8 * g;
@@ -286,6 +252,8 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
 #pragma unroll
   for (int i = 0; i < NB; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = OME_NEG_INF, lsum = 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   // The XOR swizzle makes every LDS offset lane-dependent; split it so the compiler sees a lane
   // base plus an immediate: (8k + c) ^ z = 8k + (c ^ z) for c, z < 8.  S^T reads chunk 4 s + g of
@@ -301,17 +269,8 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
   int buf = 0;
   for (int pr = pair_begin; pr < pair_end; ++pr) {
     const bf16* img = sK + buf * IMG;
-    // retire tile pr's DMA pieces: tiles pr + 1 .. pr + NBUF - 2 may stay in flight (counted
-    // vmcnt, cw pieces per tile for this wave; the Q loads retired with the first wait), then a
-    // raw barrier -- __syncthreads() would drain every DMA in flight (cdna_hip_programming.md
-    // "Pipelining across barriers")
-    const int ahead = min(NBUF - 2, pair_end - 1 - pr);
-    mla_wait_dma(ahead * cw);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // refill the image read in the previous iteration (every wave is past its reads: barrier)
-    if (pr + NBUF - 1 < pair_end) dma_pair(pr + NBUF - 1, sK + ((buf + NBUF - 1) % NBUF) * IMG);
+    // the other image's last readers passed the barrier that ended the previous tile
+    if (pr + 1 < pair_end) dma_pair(pr + 1, sK + (buf ^ 1) * IMG);
     // ---- S^T [32 keys x 16 heads] ----
     const char* ib = reinterpret_cast<const char*>(img);
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
@@ -353,17 +312,17 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const int off = vofs[nb & 3] + (nb >> 2) * 128;   // swz(4g + qrow, 2 nb + pcol/2) + 8 (pcol & 1)
-      bf16x4 va = tr_read_asm(img, off);
-      bf16x4 vb = tr_read_asm(img, off + 16 * CH * 16);
-      // the asm outputs pass through the wait, so no use of them is scheduled above it
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(va), "+v"(vb) :: "memory");
+      const bf16x4 va = tr_read(img, off);
+      const bf16x4 vb = tr_read(img, off + 16 * CH * 16);
       bf16x8 a;
       a[0] = va[0]; a[1] = va[1]; a[2] = va[2]; a[3] = va[3];
       a[4] = vb[0]; a[5] = vb[1]; a[6] = vb[2]; a[7] = vb[3];
       o[nb] *= alpha;
       o[nb] = mfma16x32(a, pb, o[nb]);
     }
-    buf = (buf + 1) % NBUF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's DMA has landed
+    __syncthreads();
+    buf ^= 1;
   }
 
   // ---- epilogue: O^T lane map dim = 16 nb + 4 g + i, head = col ----
