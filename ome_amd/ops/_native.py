@@ -15,7 +15,11 @@ import os
 import threading
 from pathlib import Path
 
+# OME_LIB_DIR: load the native libraries from another in-tree directory (compiler-flag A/B runs,
+# scripts/build_variant.py); default ome_amd/_lib
+# (a library missing there comes from the default directory)
 _LIB_DIR = Path(__file__).resolve().parent.parent / "_lib"
+_LIB_OVERRIDE = Path(os.environ["OME_LIB_DIR"]).resolve() if os.environ.get("OME_LIB_DIR") else None
 _lock = threading.Lock()
 _libs: dict[str, C.CDLL] = {}
 
@@ -117,6 +121,8 @@ class NativeError(RuntimeError):
 
 
 def lib_path(name: str = "ome_kernels") -> Path:
+    if _LIB_OVERRIDE is not None and (_LIB_OVERRIDE / f"lib{name}.so").exists():
+        return _LIB_OVERRIDE / f"lib{name}.so"
     return _LIB_DIR / f"lib{name}.so"
 
 

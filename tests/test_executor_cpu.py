@@ -133,5 +133,5 @@ def test_lws_group_restart_when_a_rank_watchdog_exits(cluster, tmp_path):
     # the worker exited 75 (its container restart is recorded) and the group was recreated
     assert _wait(cluster, lambda: len(pods()) == 2 and all(p["metadata"]["uid"] != first.get(n)
                                                              for n, p in pods().items())
-                 and all(_ready(p) for p in pods().values()), timeout=60)
+                 and all(_ready(p) for p in pods().values()), timeout=150)
     assert EXIT_COLLECTIVE == 75
