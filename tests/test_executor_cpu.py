@@ -117,7 +117,9 @@ def test_lws_group_restart_when_a_rank_watchdog_exits(cluster, tmp_path):
             "if os.environ.get('LWS_WORKER_INDEX', '0') != '0' and not os.path.exists(m):\n"
             "    open(m, 'w').close()\n"
             "    from ome_amd.runtime import watchdog as W\n"
-            "    W.register_comm('allreduce(rank 1/2)', lambda: 1)\n"
+            "    t0 = time.time()\n"
+            # the collective error surfaces 5 s in, after the test has recorded the first pod uids
+            "    W.register_comm('allreduce(rank 1/2)', lambda: 1 if time.time() > t0 + 5 else 0)\n"
             "    W.Watchdog(60.0, rank=1, poll_s=0.05)\n"
             "time.sleep(600)\n")
     c = {"name": "c", "image": "busybox", "command": [PY, "-c", code]}
