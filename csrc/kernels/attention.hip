@@ -232,8 +232,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
       s1[i] = (k1 < p_end && k1 >= lo) ? s1[i] * scale_log2 : OME_NEG_INF;
       mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 16));
-    mt = fmaxf(mt, __shfl_xor(mt, 32));
+    mt = group4_max(mt);
     const float m_new = fmaxf(m_i, mt);
     const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
     const float alpha = fast_exp2(m_i - m_use);
@@ -246,8 +245,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
       pb[4 + i] = (bf16)p1;
       rs += p0 + p1;
     }
-    rs += __shfl_xor(rs, 16);
-    rs += __shfl_xor(rs, 32);
+    rs = group4_sum(rs);
     l_i = l_i * alpha + rs;
     m_i = m_new;
     const bf16* vA = v_cache + pA * kpage + (int64_t)kvh * D * P;
@@ -393,8 +391,7 @@ __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf1
     s1[i] = v1 ? (AL ? scl(s1[i]) + al * (float)(k1 - qpos) : scl(s1[i])) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
-  mt = fmaxf(mt, __shfl_xor(mt, 16));
-  mt = fmaxf(mt, __shfl_xor(mt, 32));
+  mt = group4_max(mt);
   const float m_new = fmaxf(m_i, mt);
   const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
   const float alpha = fast_exp2(m_i - m_use);
@@ -407,8 +404,7 @@ __device__ __forceinline__ void kv_tile_compute(const KVTile<D, F>& t, const bf1
     pb[4 + i] = (bf16)p1;
     rs += p0 + p1;
   }
-  rs += __shfl_xor(rs, 16);
-  rs += __shfl_xor(rs, 32);
+  rs = group4_sum(rs);
   l_i = l_i * alpha + rs;
   m_i = m_new;
 #pragma unroll
@@ -470,8 +466,7 @@ __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const b
     s1[i] = v1 ? (AL ? scl(s1[i]) + al * (float)(k1 - qpos) : scl(s1[i])) : OME_NEG_INF;
     mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
   }
-  mt = fmaxf(mt, __shfl_xor(mt, 16));
-  mt = fmaxf(mt, __shfl_xor(mt, 32));
+  mt = group4_max(mt);
   const float m_new = fmaxf(m_i, mt);
   const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
   const float alpha = fast_exp2(m_i - m_use);
@@ -484,8 +479,7 @@ __device__ __forceinline__ void kv_tilep_compute(const KVTileP<D, F>& t, const b
     pb[4 + i] = (bf16)p1;
     rs += p0 + p1;
   }
-  rs += __shfl_xor(rs, 16);
-  rs += __shfl_xor(rs, 32);
+  rs = group4_sum(rs);
   l_i = l_i * alpha + rs;
   m_i = m_new;
 #pragma unroll
@@ -801,8 +795,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
             sc[rb][X][i] = v;
             mt = fmaxf(mt, v);
           }
-        mt = fmaxf(mt, __shfl_xor(mt, 16));
-        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        mt = group4_max(mt);
         const float m_new = fmaxf(m_i[rb], mt);
         const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
         alpha[rb] = fast_exp2(m_i[rb] - m_use);
@@ -814,8 +807,7 @@ __global__ __launch_bounds__(512) void paged_prefill_kernel(
           pb[rb][4 + i] = (bf16)p1;
           rs += p0 + p1;
         }
-        rs += __shfl_xor(rs, 16);
-        rs += __shfl_xor(rs, 32);
+        rs = group4_sum(rs);
         l_i[rb] = l_i[rb] * alpha[rb] + rs;
         m_i[rb] = m_new;
       }
@@ -1048,8 +1040,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
               sc[rb][X][i] = v;
               mt = fmaxf(mt, v);
             }
-          mt = fmaxf(mt, __shfl_xor(mt, 16));
-          mt = fmaxf(mt, __shfl_xor(mt, 32));
+          mt = group4_max(mt);
           const float m_new = fmaxf(m_i[rb], mt);
           const float m_use = (m_new == OME_NEG_INF) ? 0.f : m_new;
           alpha[rb] = fast_exp2(m_i[rb] - m_use);
@@ -1061,8 +1052,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
             pb[rb][4 + i] = (bf16)p1;
             rs += p0 + p1;
           }
-          rs += __shfl_xor(rs, 16);
-          rs += __shfl_xor(rs, 32);
+          rs = group4_sum(rs);
           l_i[rb] = l_i[rb] * alpha[rb] + rs;
           m_i[rb] = m_new;
         }
@@ -1153,8 +1143,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
         for (int X = 0; X < 2; ++X)
 #pragma unroll
           for (int i = 0; i < 4; ++i) v = fmaxf(v, sc[u][rb][X][i]);
-      v = fmaxf(v, __shfl_xor(v, 16));
-      mt[rb] = fmaxf(v, __shfl_xor(v, 32)) * scl.mul;   // log2 domain
+      mt[rb] = group4_max(v) * scl.mul;   // log2 domain
     }
     // lazy rescale (FA-3 style): keep the running max while no row of the wave grew it by more
     // than 8 (p <= 2^8 then, exact in fp32 and bf16's range); O and l are rescaled only on the
@@ -1251,8 +1240,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void paged_prefill_v2_kernel(
   if constexpr (FAST) {   // per-lane partial row sums -> the row's total (its 4 lane groups)
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
-      l_i[rb] += __shfl_xor(l_i[rb], 16);
-      l_i[rb] += __shfl_xor(l_i[rb], 32);
+      l_i[rb] = group4_sum(l_i[rb]);
     }
   }
   if (SPLIT && part >= 0) {   // unnormalised partial: O^T rows of this wave + (m, l) per row

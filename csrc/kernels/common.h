@@ -35,6 +35,30 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Reductions over the 4 lane groups of 16 (lanes l, l^16, l^32, l^48: an MFMA 16x16 tile's
+// row spread) on the gfx950 permlane swaps: v_permlane16_swap / v_permlane32_swap(x, x) leave
+// x[l] in one result and x[l^16] (x[l^32]) in the other in EVERY lane, so max / sum of the pair
+// is the xor-shuffle result bit for bit -- two VALU ops per level instead of a ds_bpermute round
+// trip whose lgkmcnt wait also drains the wave's in-flight LDS reads.  v_max_f32 by asm: fmaxf
+// on the swap results adds two canonicalising v_max per level.
+__device__ __forceinline__ float vmax_f32(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float group4_max(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = vmax_f32(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return vmax_f32(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float group4_sum(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
 template <int NT>
 __device__ __forceinline__ float block_sum(float v, float* red) {

@@ -127,8 +127,7 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
       s1[i] = (kbase + 16 + 4 * g + i < L) ? s1[i] * scale_log2 : OME_NEG_INF;
       mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = group4_max(mx);
     const float m_new = fmaxf(m, mx);
     const float alpha = (m_new == OME_NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - m_new);
     bf16x8 pb;
@@ -141,8 +140,7 @@ __global__ __launch_bounds__(256) void mla_attn_kernel(
       pb[i] = (bf16)p0;
       pb[4 + i] = (bf16)p1;
     }
-    ps += __shfl_xor(ps, 16);
-    ps += __shfl_xor(ps, 32);
+    ps = group4_sum(ps);
     lsum = lsum * alpha + ps;
     m = m_new;
     // ---- O^T [this wave's DV / 4 dims x 16 heads] += V^T . P^T ----
@@ -290,8 +288,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
       s1[i] = (kbase + 16 + 4 * g + i < L) ? s1[i] * scale_log2 : OME_NEG_INF;
       mx = fmaxf(mx, fmaxf(s0[i], s1[i]));
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = group4_max(mx);
     const float m_new = fmaxf(m, mx);
     const float alpha = (m_new == OME_NEG_INF) ? 1.f : __builtin_amdgcn_exp2f(m - m_new);
     bf16x8 pb;
@@ -304,8 +301,7 @@ __global__ __launch_bounds__(64 * NW, 1) void mla_attn_all_kernel(
       pb[i] = (bf16)p0;
       pb[4 + i] = (bf16)p1;
     }
-    ps += __shfl_xor(ps, 16);
-    ps += __shfl_xor(ps, 32);
+    ps = group4_sum(ps);
     lsum = lsum * alpha + ps;
     m = m_new;
     // ---- O^T [DV x 16 heads] += V^T . P^T (keys permuted as in pb: 4g + i, 16 + 4g + i) ----

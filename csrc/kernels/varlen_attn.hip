@@ -215,8 +215,7 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
           for (int X = 0; X < 2; ++X)
 #pragma unroll
             for (int i = 0; i < 4; ++i) v = fmaxf(v, sc[rb][X][i]);
-          v = fmaxf(v, __shfl_xor(v, 16));
-          mt[rb] = fmaxf(v, __shfl_xor(v, 32)) * scale_log2;
+          mt[rb] = group4_max(v) * scale_log2;
         }
         if (__ballot(mt[0] > m_i[0] + 8.f || mt[1] > m_i[1] + 8.f) != 0) {
           asm volatile("" ::: "memory");
@@ -272,8 +271,7 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
             sc[rb][X][i] = val;
             mt = fmaxf(mt, val);
           }
-        mt = fmaxf(mt, __shfl_xor(mt, 16));
-        mt = fmaxf(mt, __shfl_xor(mt, 32));
+        mt = group4_max(mt);
         const float m_new = fmaxf(m_i[rb], mt);
         const float m_use = (m_new == VA_NEG_INF) ? 0.f : m_new;
         alpha[rb] = va_exp2(m_i[rb] - m_use);
@@ -285,8 +283,7 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
           pb[rb][4 + i] = (bf16)p1;
           rs += p0 + p1;
         }
-        rs += __shfl_xor(rs, 16);
-        rs += __shfl_xor(rs, 32);
+        rs = group4_sum(rs);
         l_i[rb] = l_i[rb] * alpha[rb] + rs;
         m_i[rb] = m_new;
       }
@@ -344,8 +341,7 @@ __global__ __launch_bounds__(256, 2) void varlen_attn_kernel(
   if constexpr (FAST) {   // the row's 4 lanes' partial sums
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
-      l_i[rb] += __shfl_xor(l_i[rb], 16);
-      l_i[rb] += __shfl_xor(l_i[rb], 32);
+      l_i[rb] = group4_sum(l_i[rb]);
     }
   }
   // ---- epilogue: O^T accumulators hold O[row n][dims 16nb + 4g .. +3] ----
